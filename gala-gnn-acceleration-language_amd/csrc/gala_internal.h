@@ -1,0 +1,54 @@
+// Internal helpers shared by the gfx950 kernels of libgala_hip.so.
+//
+// Numerics contract: the library is compiled with -ffp-contract=off and every rounding
+// step is written out (fmaf where nvcc contracts the reference's `a + b*c`, __fmul_rn /
+// __fadd_rn elsewhere), so that a kernel that keeps the reference's per-row edge order
+// is bit-identical to the reference kernel (src/codegen/cuda.h:286-436).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gala_hip.h"
+
+namespace gala {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kMaxSegPerLaunch = 64;
+
+// Segment table passed by value (kernel arguments live in the scalar cache).
+struct SegTable {
+    int32_t n;                         // segments in this launch
+    int32_t base[kMaxSegPerLaunch];    // first edge of each segment (seg_bounds[2s])
+    int32_t rp[kMaxSegPerLaunch];      // index of the segment's rowptr block (s)
+};
+
+// Thread-local last HIP error (the only mutable state of the library).
+void set_last_hip_error(int e);
+
+int check_csr(const gala_csr_t *A);
+int fill_segments(const gala_csr_t *A, int32_t first, SegTable *t);
+int launch_status();  // hipGetLastError -> gala_status
+
+__device__ __forceinline__ float ld_nt(const float *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ int32_t ld_nt(const int32_t *p) { return __builtin_nontemporal_load(p); }
+
+// Wave-uniform value broadcast (keeps the row bounds in SGPRs).
+__device__ __forceinline__ int32_t uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+    // xor-butterfly inside aligned groups of W lanes (W power of two <= 64)
+#pragma unroll
+    for (int o = W / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+    for (int o = W / 2; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+}  // namespace gala

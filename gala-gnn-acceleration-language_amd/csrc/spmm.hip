@@ -1,0 +1,404 @@
+// SpMM neighbour aggregation for gfx950 (CDNA4, wave64).
+//
+// Replaces the emitted `aggregate_node_mul_sum[_direct]_coarse{C}_kernel{k}[_offset]`
+// family (src/codegen/cuda.h:286-436) and its launch tree (coarsenedKernelCall,
+// cuda.h:58-168), the cuSPARSE "gather_forward" path (cuda.h:211-279) and the
+// kernel-sampled variants (cuda.h:313-321,389-397).
+//
+// Layout of one launch: a "row group" of G lanes (G a power of two) owns one CSR row;
+// lane g of the group owns VEC contiguous fp32 features at column (ch*G + g)*VEC for
+// ch < CH, so the group reads whole X rows with VEC*4-byte coalesced loads
+// (F = 32 -> float4 x 8 lanes = one 128-B line per neighbour).  A wave holds 64/G rows.
+// Inside a row, edges are accumulated sequentially in CSR order (segment 0 first),
+// with the neighbour loads of U edges issued before the first add, so the result is
+// bit-identical to the reference kernel while each lane keeps U*CH vector loads in
+// flight.  All address arithmetic is 64-bit.
+#include "gala_internal.h"
+
+namespace gala {
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<1> {
+    typedef float T;
+};
+template <>
+struct VecT<2> {
+    typedef float T __attribute__((ext_vector_type(2)));
+};
+template <>
+struct VecT<4> {
+    typedef float T __attribute__((ext_vector_type(4)));
+};
+
+struct SpmmParams {
+    const int32_t *rowptr;
+    const int32_t *col;
+    const float *val;
+    const float *X;
+    float *Y;
+    const float *src_scale;
+    const float *dst_scale;
+    int64_t n_rows;
+    int64_t ldx;
+    int64_t ldy;
+    int32_t F;
+    int32_t val_heads;
+    int32_t head_dim;   // F / val_heads
+    int32_t accum;      // 1: Y += ..., 0: Y = ...
+    int32_t nsamp, ra, rb;
+    SegTable seg;
+};
+
+template <int VEC>
+__device__ __forceinline__ typename VecT<VEC>::T ldv(const float *p) {
+    return *reinterpret_cast<const typename VecT<VEC>::T *>(p);
+}
+template <int VEC>
+__device__ __forceinline__ void stv(float *p, typename VecT<VEC>::T v) {
+    *reinterpret_cast<typename VecT<VEC>::T *>(p) = v;
+}
+
+// element access helpers for ext_vector / scalar
+template <int VEC>
+__device__ __forceinline__ float &el(typename VecT<VEC>::T &v, int i) {
+    return reinterpret_cast<float *>(&v)[i];
+}
+
+// acc (+)= w * (s * x), reference rounding:  s*x is the torch `norm * res` product
+// (rounded), `local + A*B` is contracted to fma by nvcc (cuda.h:335-342).
+template <int VEC, bool W, bool SRCS>
+__device__ __forceinline__ void accumulate(typename VecT<VEC>::T &acc,
+                                           const typename VecT<VEC>::T &x, float w, float s) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+        float v = reinterpret_cast<const float *>(&x)[i];
+        if (SRCS) v = __fmul_rn(s, v);
+        float &a = el<VEC>(acc, i);
+        if (W)
+            a = fmaf(w, v, a);
+        else
+            a = __fadd_rn(a, v);
+    }
+}
+
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+__global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
+    typedef typename VecT<VEC>::T V;
+    constexpr int RPW = kWave / G;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int grp = lane / G;
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
+    const int64_t row = wave * RPW + grp;
+    if (row >= p.n_rows) return;
+
+    // columns owned by this lane
+    bool cvalid[CH];
+    int64_t coff[CH];
+    int head[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const int f = (ch * G + gl) * VEC;
+        cvalid[ch] = f < p.F;
+        coff[ch] = f;
+        head[ch] = W ? (cvalid[ch] ? f / p.head_dim : 0) : 0;
+    }
+
+    V acc[CH];
+    const bool start_from_y = p.accum && p.dst_scale == nullptr;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        if (start_from_y && cvalid[ch])
+            acc[ch] = ldv<VEC>(p.Y + row * p.ldy + coff[ch]);
+        else
+            acc[ch] = V(0.0f);
+    }
+
+    const int64_t rp_stride = p.n_rows + 1;
+    for (int s = 0; s < p.seg.n; ++s) {
+        const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * rp_stride;
+        const int64_t base = p.seg.base[s];
+        const int64_t e0 = base + rp[row];
+        const int64_t e1 = base + rp[row + 1];
+        if (SAMP) {
+            const int32_t deg = (int32_t)(e1 - e0);
+            if (deg > 0) {
+                for (int ji = 0; ji < p.nsamp; ji += U) {
+                    int32_t c[U];
+                    float w[U][CH];
+                    V x[U][CH];
+#pragma unroll
+                    for (int k = 0; k < U; ++k) {
+                        if (ji + k < p.nsamp) {
+                            const int32_t j = (p.ra * (ji + k) + p.rb) % deg;
+                            c[k] = p.col[e0 + j];
+#pragma unroll
+                            for (int ch = 0; ch < CH; ++ch) {
+                                w[k][ch] = W ? p.val[(e0 + j) * p.val_heads + head[ch]] : 1.0f;
+                                if (cvalid[ch]) x[k][ch] = ldv<VEC>(p.X + (int64_t)c[k] * p.ldx + coff[ch]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < U; ++k) {
+                        if (ji + k < p.nsamp) {
+                            const float sc = SRCS ? p.src_scale[c[k]] : 1.0f;
+#pragma unroll
+                            for (int ch = 0; ch < CH; ++ch)
+                                if (cvalid[ch]) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc);
+                        }
+                    }
+                }
+            }
+        } else {
+            for (int64_t e = e0; e < e1; e += U) {
+                int32_t c[U];
+                float w[U][CH];
+                V x[U][CH];
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    if (e + k < e1) {
+                        c[k] = p.col[e + k];
+#pragma unroll
+                        for (int ch = 0; ch < CH; ++ch) {
+                            w[k][ch] = W ? p.val[(e + k) * p.val_heads + head[ch]] : 1.0f;
+                            if (cvalid[ch]) x[k][ch] = ldv<VEC>(p.X + (int64_t)c[k] * p.ldx + coff[ch]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    if (e + k < e1) {
+                        const float sc = SRCS ? p.src_scale[c[k]] : 1.0f;
+#pragma unroll
+                        for (int ch = 0; ch < CH; ++ch)
+                            if (cvalid[ch]) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc);
+                    }
+                }
+            }
+        }
+    }
+
+    const float ds = p.dst_scale ? p.dst_scale[row] : 1.0f;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        if (!cvalid[ch]) continue;
+        float *yp = p.Y + row * p.ldy + coff[ch];
+        V out = acc[ch];
+        if (p.dst_scale) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fmul_rn(ds, el<VEC>(out, i));
+            if (p.accum) {
+                V y = ldv<VEC>(yp);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fadd_rn(el<VEC>(y, i), el<VEC>(out, i));
+            }
+        }
+        stv<VEC>(yp, out);
+    }
+}
+
+// ---- degree: deg[r] = sum_e (val_e | 1), optionally ^power --------------------------
+struct DegParams {
+    const int32_t *rowptr;
+    const float *val;
+    float *deg;
+    int64_t n_rows;
+    float power;
+    int32_t sample;
+    int32_t nsamp;
+    SegTable seg;
+};
+
+__global__ __launch_bounds__(kBlock) void k_degree_count(DegParams p) {
+    const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (row >= p.n_rows) return;
+    float d;
+    if (p.sample) {
+        d = (float)p.nsamp * (float)p.seg.n;  // FULL_OP: n * global_segments[0] (common.h:1358-1359)
+    } else {
+        int64_t cnt = 0;
+        for (int s = 0; s < p.seg.n; ++s) {
+            const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * (p.n_rows + 1);
+            cnt += rp[row + 1] - rp[row];
+        }
+        d = (float)cnt;  // exact: sequential sum of 1.0f is exact below 2^24
+    }
+    if (p.power != 1.0f) d = (p.power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, p.power);
+    p.deg[row] = d;
+}
+
+// weighted degree: one row per 16-lane group, sequential per row to keep the order
+__global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
+    const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (row >= p.n_rows) return;
+    float d = 0.0f;
+    for (int s = 0; s < p.seg.n; ++s) {
+        const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * (p.n_rows + 1);
+        const int64_t e0 = p.seg.base[s] + (int64_t)rp[row], e1 = p.seg.base[s] + (int64_t)rp[row + 1];
+        for (int64_t e = e0; e < e1; ++e) d = __fadd_rn(d, p.val[e]);
+    }
+    if (p.power != 1.0f) d = (p.power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, p.power);
+    p.deg[row] = d;
+}
+
+// ---- dispatch ---------------------------------------------------------------------------
+template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
+static void launch_rg(const SpmmParams &p, hipStream_t st) {
+    // U: edges whose loads are in flight before the first add (per lane: U*CH vectors)
+    constexpr int U = (CH * VEC >= 16) ? 2 : ((CH * VEC >= 8) ? 4 : 8);
+    constexpr int rows_per_block = (kBlock / kWave) * (kWave / G);
+    const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
+    hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
+                       dim3(kBlock), 0, st, p);
+}
+
+template <int VEC, int G, int CH>
+static void launch_flags(const SpmmParams &p, bool w, bool samp, bool srcs, hipStream_t st) {
+    if (w) {
+        if (samp) {
+            if (srcs) launch_rg<VEC, G, CH, true, true, true>(p, st);
+            else launch_rg<VEC, G, CH, true, true, false>(p, st);
+        } else {
+            if (srcs) launch_rg<VEC, G, CH, true, false, true>(p, st);
+            else launch_rg<VEC, G, CH, true, false, false>(p, st);
+        }
+    } else {
+        if (samp) {
+            if (srcs) launch_rg<VEC, G, CH, false, true, true>(p, st);
+            else launch_rg<VEC, G, CH, false, true, false>(p, st);
+        } else {
+            if (srcs) launch_rg<VEC, G, CH, false, false, true>(p, st);
+            else launch_rg<VEC, G, CH, false, false, false>(p, st);
+        }
+    }
+}
+
+template <int VEC>
+static int launch_vec(const SpmmParams &p, int L, bool w, bool samp, bool srcs, hipStream_t st) {
+    // L = vector elements per row (ceil(F/VEC))
+    if (L <= 1) launch_flags<VEC, 1, 1>(p, w, samp, srcs, st);
+    else if (L <= 2) launch_flags<VEC, 2, 1>(p, w, samp, srcs, st);
+    else if (L <= 4) launch_flags<VEC, 4, 1>(p, w, samp, srcs, st);
+    else if (L <= 8) launch_flags<VEC, 8, 1>(p, w, samp, srcs, st);
+    else if (L <= 16) launch_flags<VEC, 16, 1>(p, w, samp, srcs, st);
+    else if (L <= 32) launch_flags<VEC, 32, 1>(p, w, samp, srcs, st);
+    else if (L <= 64) launch_flags<VEC, 64, 1>(p, w, samp, srcs, st);
+    else if (L <= 128) launch_flags<VEC, 64, 2>(p, w, samp, srcs, st);
+    else if (L <= 192) launch_flags<VEC, 64, 3>(p, w, samp, srcs, st);
+    else if (L <= 256) launch_flags<VEC, 64, 4>(p, w, samp, srcs, st);
+    else if (L <= 384) launch_flags<VEC, 64, 6>(p, w, samp, srcs, st);
+    else if (L <= 512) launch_flags<VEC, 64, 8>(p, w, samp, srcs, st);
+    else return GALA_ERR_UNSUPPORTED;
+    return GALA_OK;
+}
+
+}  // namespace gala
+
+using namespace gala;
+
+extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
+                             int64_t ldy, int32_t F, const float *src_scale,
+                             const float *dst_scale, int32_t flags, int32_t nsamp, int32_t ra,
+                             int32_t rb, void *stream) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 0 || ldx < F || ldy < F || (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE)))
+        return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || F == 0) return GALA_OK;
+    if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    const bool samp = (flags & GALA_SPMM_SAMPLE) != 0;
+    if (samp && nsamp < 0) return GALA_ERR_INVALID_ARG;
+    const bool w = A->val != nullptr;
+    if (w && (A->val_heads < 1 || F % A->val_heads != 0)) return GALA_ERR_INVALID_ARG;
+    const int32_t head_dim = w ? F / A->val_heads : F;
+
+    // widest vector that divides F, the head width and both strides with aligned bases
+    int vec = 4;
+    auto ok = [&](int v) {
+        return F % v == 0 && head_dim % v == 0 && ldx % v == 0 && ldy % v == 0 &&
+               ((uintptr_t)X % (4 * v)) == 0 && ((uintptr_t)Y % (4 * v)) == 0;
+    };
+    while (vec > 1 && !ok(vec)) vec >>= 1;
+
+    SpmmParams p;
+    p.rowptr = A->rowptr;
+    p.col = A->col;
+    p.val = A->val;
+    p.X = X;
+    p.Y = Y;
+    p.src_scale = src_scale;
+    p.dst_scale = dst_scale;
+    p.n_rows = A->n_rows;
+    p.ldx = ldx;
+    p.ldy = ldy;
+    p.F = F;
+    p.val_heads = w ? A->val_heads : 1;
+    p.head_dim = head_dim;
+    p.nsamp = nsamp;
+    p.ra = ra;
+    p.rb = rb;
+    hipStream_t hs = (hipStream_t)stream;
+
+    // feature chunks wider than 512 vectors per lane-group are split over launches
+    const int64_t max_cols = 512LL * vec;
+    for (int32_t seg0 = 0; seg0 < A->n_seg; seg0 += kMaxSegPerLaunch) {
+        st = fill_segments(A, seg0, &p.seg);
+        if (st) return st;
+        // segments after the first launch always accumulate onto the previous ones
+        const bool accum = (flags & GALA_SPMM_ACCUM) || seg0 > 0;
+        for (int64_t c0 = 0; c0 < F; c0 += max_cols) {
+            const int32_t Fc = (int32_t)((F - c0) < max_cols ? (F - c0) : max_cols);
+            SpmmParams q = p;
+            q.X = X ? X + c0 : nullptr;
+            q.Y = Y + c0;
+            q.F = Fc;
+            q.accum = accum;
+            if (w) {
+                // a column chunk must stay head-aligned for the per-head weight lookup
+                if (c0 % head_dim != 0 && p.val_heads > 1) return GALA_ERR_UNSUPPORTED;
+                q.val = A->val;  // head index computed from chunk-local column: shift heads
+            }
+            if (w && p.val_heads > 1 && c0 > 0) return GALA_ERR_UNSUPPORTED;
+            if (seg0 > 0 && dst_scale) return GALA_ERR_UNSUPPORTED;
+            const int L = (int)((Fc + vec - 1) / vec);
+            int r;
+            if (vec == 4) r = launch_vec<4>(q, L, w, samp, src_scale != nullptr, hs);
+            else if (vec == 2) r = launch_vec<2>(q, L, w, samp, src_scale != nullptr, hs);
+            else r = launch_vec<1>(q, L, w, samp, src_scale != nullptr, hs);
+            if (r) return r;
+            r = launch_status();
+            if (r) return r;
+        }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags,
+                               int32_t nsamp, void *stream) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (!deg || (flags & ~(GALA_SPMM_SAMPLE))) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (A->n_seg > kMaxSegPerLaunch) return GALA_ERR_UNSUPPORTED;
+    DegParams p;
+    p.rowptr = A->rowptr;
+    p.val = A->val;
+    p.deg = deg;
+    p.n_rows = A->n_rows;
+    p.power = power;
+    p.sample = (flags & GALA_SPMM_SAMPLE) ? 1 : 0;
+    p.nsamp = nsamp;
+    st = fill_segments(A, 0, &p.seg);
+    if (st) return st;
+    const int64_t blocks = (A->n_rows + kBlock - 1) / kBlock;
+    if (A->val && !p.sample)
+        hipLaunchKernelGGL(k_degree_weighted, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(k_degree_count, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)stream, p);
+    return launch_status();
+}

@@ -1,0 +1,113 @@
+"""ctypes binding of libgala_hip.so — a line-for-line mirror of include/gala_hip.h.
+
+This is the Python-side stub of the C ABI (the reference-side binding for C++ callers is
+`#include "gala_hip.h"`).  Loading fails loudly when the library is
+missing: there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgala_hip.so")
+
+GALA_OK = 0
+GALA_ERR_INVALID_ARG = -1
+GALA_ERR_UNSUPPORTED = -2
+GALA_ERR_HIP = -3
+GALA_ERR_GRAPH = -4
+
+GALA_SPMM_ACCUM = 0x1
+GALA_SPMM_SAMPLE = 0x2
+GALA_SDDVV_ADD = 0
+GALA_SDDVV_MUL = 1
+GALA_SDDVV_ADD_LRELU = 2
+GALA_SOFTMAX_REF = 0
+GALA_SOFTMAX_FIXED = 1
+
+
+class gala_csr_t(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", ctypes.c_int64),
+        ("n_cols", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("rowptr", ctypes.c_void_p),
+        ("col", ctypes.c_void_p),
+        ("val", ctypes.c_void_p),
+        ("val_heads", ctypes.c_int32),
+        ("n_seg", ctypes.c_int32),
+        ("seg_bounds", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_F = ctypes.c_float
+_CSR = ctypes.POINTER(gala_csr_t)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "gala_abi_version": (ctypes.c_int, []),
+    "gala_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gala_last_hip_error": (ctypes.c_int, []),
+    "gala_spmm_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _P]),
+    "gala_degree_f32": (ctypes.c_int, [_CSR, _P, _F, _I32, _I32, _P]),
+    "gala_sddvv_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _F, _P, _P]),
+    "gala_row_sum_f32": (ctypes.c_int, [_CSR, _P, _I32, _F, _P, _I32, _P]),
+    "gala_row_scale_f32": (ctypes.c_int, [_CSR, _P, _I32, _P, _P]),
+    "gala_sddmm_dot_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _I32, _P, _P]),
+    "gala_edge_softmax_fwd_f32": (ctypes.c_int, [_CSR, _P, _I32, _I32, _P, _P]),
+    "gala_edge_softmax_bwd_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _P, _P]),
+    "gala_gat_fwd_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _I32, _I32, _F, _I32, _P, _I64, _P, _P]),
+    "gala_edge_permute_f32": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
+    "gala_host_csr_build": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P]),
+    "gala_host_col_breakpoints": (ctypes.c_int64, [_I64, _I64, _P, _I64]),
+    "gala_host_col_tile": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _P, _P, _P, _P, _P]),
+    "gala_host_sample_ab": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    "gala_host_csr_transpose": (ctypes.c_int, [_I64, _I64, _P, _P, _P, _P, _P]),
+    "gala_host_gen_graph": (ctypes.c_int, [_I32, _I64, _I64, ctypes.c_uint64, _P, _P]),
+}
+
+
+class GalaError(RuntimeError):
+    def __init__(self, fn: str, status: int, hip_error: int = 0):
+        name = {0: "GALA_OK", -1: "GALA_ERR_INVALID_ARG", -2: "GALA_ERR_UNSUPPORTED",
+                -3: "GALA_ERR_HIP", -4: "GALA_ERR_GRAPH"}.get(status, str(status))
+        msg = f"{fn} failed: {name}"
+        if status == GALA_ERR_HIP:
+            msg += f" (hipError {hip_error})"
+        super().__init__(msg)
+        self.status = status
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgala_hip.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C gala-gnn-acceleration-language_amd`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(fn: str, status: int) -> None:
+    if status != GALA_OK:
+        raise GalaError(fn, status, lib().gala_last_hip_error() if status == GALA_ERR_HIP else 0)
+
+
+def call(fn: str, *args) -> int:
+    status = getattr(lib(), fn)(*args)
+    check(fn, status)
+    return status

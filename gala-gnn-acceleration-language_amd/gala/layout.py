@@ -1,0 +1,114 @@
+"""Host-side graph layout (numpy in, numpy out) through the C ABI's OpenMP builders.
+
+Mirrors what the generated program does on the CPU before its H2D copies:
+readSM_npy32 -> CSRCMatrix::build (tests/common.h:331-366, src/formats/csrc_matrix.h:148-376),
+static_ord_col_breakpoints + ord_col_tiling_torch (src/ops/tiling.h:1594-1608, 222-283),
+inplace_sample_graph_ab (src/ops/tiling.h:454-508).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+@dataclass
+class HostGraph:
+    n_rows: int
+    n_cols: int
+    rowptr: np.ndarray           # int32 [(n_rows+1)*n_seg]
+    col: np.ndarray              # int32 [nnz]
+    val: np.ndarray | None = None
+    n_seg: int = 1
+    bounds: np.ndarray | None = None  # int32 [2*n_seg] (host, like the reference)
+    val_heads: int = 1
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+    def degrees(self) -> np.ndarray:
+        rp = self.rowptr.reshape(self.n_seg, self.n_rows + 1).astype(np.int64)
+        return (rp[:, 1:] - rp[:, :-1]).sum(0)
+
+
+def csr_build(n_rows: int, n_cols: int, src, dst, return_perm: bool = False):
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    nnz = src.shape[0]
+    rowptr = np.empty(n_rows + 1, np.int32)
+    col = np.empty(nnz, np.int32)
+    perm = np.empty(nnz, np.int32) if return_perm else None
+    _abi.call("gala_host_csr_build", n_rows, n_cols, nnz, _p(src), _p(dst), _p(rowptr), _p(col),
+              _p(perm))
+    g = HostGraph(n_rows, n_cols, rowptr, col)
+    return (g, perm) if return_perm else g
+
+
+def col_breakpoints(n_cols: int, cols_per_partition: int) -> np.ndarray:
+    cap = n_cols // max(cols_per_partition, 1) + 2
+    out = np.empty(cap, np.int32)
+    n = _abi.lib().gala_host_col_breakpoints(n_cols, cols_per_partition, _p(out), cap)
+    _abi.check("gala_host_col_breakpoints", 0 if n > 0 else int(n))
+    return out[:n].copy()
+
+
+def col_tile(g: HostGraph, cols_per_partition: int) -> HostGraph:
+    assert g.n_seg == 1
+    bp = col_breakpoints(g.n_cols, cols_per_partition)
+    S = bp.shape[0] - 1
+    rp = np.empty((g.n_rows + 1) * S, np.int32)
+    col = np.empty(g.nnz, np.int32)
+    val = np.empty(g.nnz, np.float32) if g.val is not None else None
+    bounds = np.empty(2 * S, np.int32)
+    _abi.call("gala_host_col_tile", g.n_rows, _p(g.rowptr), _p(g.col), _p(g.val), S, _p(bp),
+              _p(rp), _p(col), _p(val), _p(bounds))
+    return HostGraph(g.n_rows, g.n_cols, rp, col, val, S, bounds, g.val_heads)
+
+
+def sample_ab(g: HostGraph, nsamp: int, ra: int = 5, rb: int = 7) -> HostGraph:
+    assert g.n_seg == 1
+    rp = np.empty(g.n_rows + 1, np.int32)
+    col = np.empty(g.n_rows * nsamp, np.int32)
+    val = np.empty(g.n_rows * nsamp, np.float32) if g.val is not None else None
+    _abi.call("gala_host_sample_ab", g.n_rows, _p(g.rowptr), _p(g.col), _p(g.val), nsamp, ra, rb,
+              _p(rp), _p(col), _p(val))
+    return HostGraph(g.n_rows, g.n_cols, rp, col, val)
+
+
+def transpose(g: HostGraph):
+    """CSR of A^T and perm (edge k of A^T is edge perm[k] of A)."""
+    assert g.n_seg == 1
+    rp = np.empty(g.n_cols + 1, np.int32)
+    col = np.empty(g.nnz, np.int32)
+    perm = np.empty(g.nnz, np.int32)
+    _abi.call("gala_host_csr_transpose", g.n_rows, g.n_cols, _p(g.rowptr), _p(g.col), _p(rp),
+              _p(col), _p(perm))
+    val = g.val[perm] if g.val is not None else None
+    return HostGraph(g.n_cols, g.n_rows, rp, col, val), perm
+
+
+def gen_graph(kind: str, n: int, n_undirected: int, seed: int = 42) -> HostGraph:
+    """Deterministic synthetic graph: 'uniform' (random symmetric + self loops) or 'rmat'."""
+    k = {"uniform": 0, "rmat": 1}[kind]
+    m = 2 * n_undirected + n
+    src = np.empty(m, np.int32)
+    dst = np.empty(m, np.int32)
+    _abi.call("gala_host_gen_graph", k, n, n_undirected, seed, _p(src), _p(dst))
+    return csr_build(n, n, src, dst)
+
+
+def load_npy_dataset(path: str) -> HostGraph:
+    """The reference's on-disk format (scripts/Data/gala_export_npy.py:104-171):
+    Adj_src.npy = uint32 [nrows, ncols, src...], Adj_dst.npy = uint32 [dst...]."""
+    src = np.load(os.path.join(path, "Adj_src.npy"))
+    dst = np.load(os.path.join(path, "Adj_dst.npy"))
+    n_rows, n_cols = int(src[0]), int(src[1])
+    return csr_build(n_rows, n_cols, src[2:].astype(np.int32), dst.astype(np.int32))

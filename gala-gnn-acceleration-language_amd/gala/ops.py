@@ -1,0 +1,142 @@
+"""torch-facing functional ops over the C ABI (device tensors, current HIP stream).
+
+Each op allocates its output with the torch caching allocator and launches the HIP
+kernel on torch's current stream.  There is no CPU fallback: CPU tensors raise.
+The C++/libtorch mirror of the reference's emitted operator API (the `*_call`
+wrappers and autograd Functions of codegen/gala.cu) lives in host/gala_torch.cpp.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi
+from .layout import HostGraph
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dp(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("gala ops take device tensors (no CPU fallback)")
+    return t.data_ptr()
+
+
+class DeviceGraph:
+    """Device-resident graph (the generated code's global_*_graph slots, gala.cu:32-43)."""
+
+    def __init__(self, n_rows, n_cols, rowptr, col, val=None, n_seg=1, bounds=None, val_heads=1):
+        self.n_rows, self.n_cols = int(n_rows), int(n_cols)
+        self.rowptr, self.col, self.val = rowptr, col, val
+        self.n_seg = int(n_seg)
+        self.val_heads = int(val_heads)
+        self.bounds = None if bounds is None else np.ascontiguousarray(bounds, np.int32)
+        self._csr = None
+
+    @classmethod
+    def from_host(cls, g: HostGraph, device="cuda"):
+        rp = torch.from_numpy(np.ascontiguousarray(g.rowptr)).to(device)
+        col = torch.from_numpy(np.ascontiguousarray(g.col)).to(device)
+        val = None if g.val is None else torch.from_numpy(np.ascontiguousarray(g.val, np.float32)).to(device)
+        return cls(g.n_rows, g.n_cols, rp, col, val, g.n_seg, g.bounds, g.val_heads)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+    def with_values(self, val, val_heads=1) -> "DeviceGraph":
+        return DeviceGraph(self.n_rows, self.n_cols, self.rowptr, self.col, val, self.n_seg,
+                           self.bounds, val_heads)
+
+    def csr(self):
+        if self._csr is None:
+            c = _abi.gala_csr_t()
+            c.n_rows, c.n_cols, c.nnz = self.n_rows, self.n_cols, self.nnz
+            c.rowptr = _dp(self.rowptr)
+            c.col = _dp(self.col)
+            c.val = _dp(self.val)
+            c.val_heads = self.val_heads
+            c.n_seg = self.n_seg
+            c.seg_bounds = None if self.bounds is None else self.bounds.ctypes.data
+            self._csr = c
+        return ctypes.byref(self._csr)
+
+
+def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=None,
+         accum=False, nsamp=None, ra=5, rb=7) -> torch.Tensor:
+    F = X.shape[1]
+    if out is None:
+        out = (torch.zeros if accum else torch.empty)((g.n_rows, F), device=X.device, dtype=torch.float32)
+    flags = (_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
+    _abi.call("gala_spmm_f32", g.csr(), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
+              _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, _stream())
+    return out
+
+
+def degree(g: DeviceGraph, power=1.0, nsamp=None) -> torch.Tensor:
+    out = torch.empty(g.n_rows, device=g.col.device, dtype=torch.float32)
+    flags = _abi.GALA_SPMM_SAMPLE if nsamp is not None else 0
+    _abi.call("gala_degree_f32", g.csr(), _dp(out), power, flags, nsamp or 0, _stream())
+    return out
+
+
+def sddvv(g: DeviceGraph, a, b, op=_abi.GALA_SDDVV_ADD, heads=1, slope=0.2) -> torch.Tensor:
+    out = torch.empty(g.nnz * heads, device=a.device, dtype=torch.float32)
+    _abi.call("gala_sddvv_f32", g.csr(), _dp(a), _dp(b), heads, op, slope, _dp(out), _stream())
+    return out
+
+
+def row_sum(g: DeviceGraph, v, heads=1, eps=1e-12, out=None, accum=False) -> torch.Tensor:
+    if out is None:
+        out = torch.zeros(g.n_rows * heads, device=v.device, dtype=torch.float32)
+    _abi.call("gala_row_sum_f32", g.csr(), _dp(v), heads, eps, _dp(out),
+              _abi.GALA_SPMM_ACCUM if accum else 0, _stream())
+    return out
+
+
+def row_scale_(g: DeviceGraph, q, v, heads=1) -> torch.Tensor:
+    _abi.call("gala_row_scale_f32", g.csr(), _dp(q), heads, _dp(v), _stream())
+    return v
+
+
+def sddmm(g: DeviceGraph, A, B, heads=1) -> torch.Tensor:
+    out = torch.empty(g.nnz * heads, device=A.device, dtype=torch.float32)
+    _abi.call("gala_sddmm_dot_f32", g.csr(), _dp(A), A.stride(0), _dp(B), B.stride(0),
+              A.shape[1], heads, _dp(out), _stream())
+    return out
+
+
+def edge_softmax(g: DeviceGraph, logits, heads=1, mode=_abi.GALA_SOFTMAX_REF) -> torch.Tensor:
+    out = torch.empty_like(logits)
+    _abi.call("gala_edge_softmax_fwd_f32", g.csr(), _dp(logits), heads, mode, _dp(out), _stream())
+    return out
+
+
+def edge_softmax_bwd(g: DeviceGraph, alpha, d_alpha, heads=1, mode=_abi.GALA_SOFTMAX_REF):
+    out = torch.empty_like(alpha)
+    _abi.call("gala_edge_softmax_bwd_f32", g.csr(), _dp(alpha), _dp(d_alpha), heads, mode,
+              _dp(out), _stream())
+    return out
+
+
+def gat_fwd(g: DeviceGraph, aL, aR, X, heads=1, slope=0.2, mode=_abi.GALA_SOFTMAX_REF,
+            want_alpha=False):
+    F = X.shape[1]
+    Y = torch.empty((g.n_rows, F), device=X.device, dtype=torch.float32)
+    alpha = torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32) if want_alpha else None
+    _abi.call("gala_gat_fwd_f32", g.csr(), _dp(aL), _dp(aR), _dp(X), X.stride(0), F, heads, slope,
+              mode, _dp(Y), Y.stride(0), _dp(alpha), _stream())
+    return (Y, alpha) if want_alpha else Y
+
+
+def edge_permute(perm, src, heads=1):
+    n = perm.numel()
+    dst = torch.empty(n * heads, device=src.device, dtype=torch.float32)
+    _abi.call("gala_edge_permute_f32", _dp(perm), _dp(src), n, heads, _dp(dst), _stream())
+    return dst

@@ -1,0 +1,254 @@
+/*
+ * gala_hip.h — C ABI of libgala_hip.so, the MI355X (gfx950) hot path of GALA's
+ * generated GNN programs: SpMM neighbour aggregation, SDDVV/SDDMM, edge-softmax and
+ * the per-edge / per-row scalings around them, plus the host-side graph-layout
+ * builders those kernels consume.
+ *
+ * Every entry point replaces one free function that GALA's CUDA code generator emits
+ * into gala.cu (src/codegen/cuda.h) or one host routine that gala.cu includes
+ * textually (src/formats, src/ops).  The reference interface each one replaces is
+ * cited as path:line relative to the GALA repository root.
+ *
+ * Conventions (all entry points):
+ *   - Plain C types only.  No torch/HIP types in the signatures; `stream` is a
+ *     hipStream_t passed as void* (NULL = the legacy null stream).
+ *   - Device pointers unless a parameter is documented HOST.  All memory is owned by
+ *     the caller; the library never allocates device memory and never synchronises
+ *     the device, so every call is capturable into a hipGraph.
+ *   - Return 0 (GALA_OK) or a negative gala_status.  The library never exits
+ *     (the reference prints and exit()s from CUDA_CHECK, codegen/gala.cu:46-64).
+ *   - Reentrant: no process globals except a thread-local last-HIP-error code.
+ *   - Indices are int32 (as in the reference, cuda.h:286-358); all address
+ *     arithmetic inside the kernels is 64-bit, so N*F >= 2^31 is supported
+ *     (the reference's `row*dcols` overflows there, SURVEY §7 hard part 3).
+ */
+#ifndef GALA_HIP_H
+#define GALA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GALA_ABI_VERSION 1
+
+typedef enum gala_status {
+    GALA_OK = 0,
+    GALA_ERR_INVALID_ARG = -1, /* null pointer, negative size, bad flag/mode, misaligned ld  */
+    GALA_ERR_UNSUPPORTED = -2, /* shape the library does not implement (reported, not UB)    */
+    GALA_ERR_HIP = -3,         /* a HIP runtime call failed; see gala_last_hip_error()         */
+    GALA_ERR_GRAPH = -4        /* malformed graph (rowptr not monotone, col out of range, ...) */
+} gala_status;
+
+/* ------------------------------------------------------------------------------------
+ * Graph descriptor.
+ *
+ * Mirrors the device-side graph the generated code keeps in the global slots
+ * global_offset_graph / global_columns_graph / global_value_graph / global_bounds /
+ * global_segments (codegen/gala.cu:32-43, emitted by src/codegen/common.h:1694-1705).
+ *
+ * n_seg == 1: plain CSR, rowptr[n_rows+1], rows sorted, cols ascending inside a row,
+ *             duplicates kept (CSRCMatrix::build, src/formats/csrc_matrix.h:148-376).
+ * n_seg  > 1: the column-tiled layout produced by ord_col_tiling_torch
+ *             (src/ops/tiling.h:222-283): rowptr holds n_seg blocks of n_rows+1
+ *             RELATIVE offsets, segment s's edges start at col[seg_bounds[2s]].
+ *             Aggregation over a tiled graph is defined as the ordered sum over the
+ *             segments (the reference launches segments on racing streams,
+ *             cuda.h:472-499; here segment 0 is accumulated first, then 1, ...).
+ * ---------------------------------------------------------------------------------- */
+typedef struct gala_csr {
+    int64_t n_rows;            /* rows of A (destination vertices of the aggregation)     */
+    int64_t n_cols;            /* columns of A (source vertices); X has n_cols rows      */
+    int64_t nnz;               /* stored edges over all segments                          */
+    const int32_t *rowptr;     /* device [(n_rows+1)*n_seg]                               */
+    const int32_t *col;        /* device [nnz]                                            */
+    const float *val;          /* device [nnz*val_heads] or NULL = unweighted (A_e = 1)   */
+    int32_t val_heads;         /* edge values per edge (1 = reference; H for multi-head) */
+    int32_t n_seg;             /* >= 1                                                    */
+    const int32_t *seg_bounds; /* HOST [2*n_seg] {start,end} edge of each segment, or
+                                  NULL when n_seg == 1 (reference keeps `bounds` on the
+                                  host: cuda.h:472-475 reads bounds_ptr on the CPU)        */
+} gala_csr_t;
+
+/* ---- library information ------------------------------------------------------------ */
+int gala_abi_version(void);
+const char *gala_status_string(int status);
+int gala_last_hip_error(void);                 /* hipError_t of the last GALA_ERR_HIP    */
+
+/* ---- SpMM neighbour aggregation ----------------------------------------------------- */
+#define GALA_SPMM_ACCUM 0x1   /* Y += result (reference: wrapper zero-fills Y, kernel adds,
+                                 cuda.h:463 + 309-310); without it Y is overwritten       */
+#define GALA_SPMM_SAMPLE 0x2  /* kernel sampling: per row with deg>0, nsamp edges
+                                 j = (ra*ji + rb) mod deg (cuda.h:313-321)                */
+
+/*
+ * Y[r, 0:F] (+)= dst_scale[r] * sum_{e in row r} w_e * (src_scale[col_e] * X[col_e, 0:F])
+ *
+ * w_e = val[e*val_heads + h] for the head h = f / (F/val_heads) of feature f
+ * (= 1 when val == NULL).  src_scale/dst_scale may be NULL (= 1); they fuse the GCN
+ * `norm * res` row broadcasts the generated forward wraps around every aggregation
+ * (codegen/gala.cu:442-456) with the reference's rounding (product rounded before
+ * the sum).  Edges are accumulated sequentially in CSR order per row, in fp32, with
+ * the same fma contraction nvcc applies to the emitted kernel, so results are
+ * bit-identical to the reference kernel for every input.
+ *
+ * Replaces: <aggregate_node_mul_sum[_direct]_coarse{C}>_call (cuda.h:441-502,
+ *           emitted codegen/gala.cu:227-390) and its kernels _kernel{k}/_offset
+ *           (cuda.h:286-436), the cuSPARSE "gather_forward" path (cuda.h:211-279),
+ *           and the kernel-sampled variants (cuda.h:313-321,389-397).
+ * ldx/ldy are row strides in elements (>= F).
+ */
+int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                  int32_t F, const float *src_scale, const float *dst_scale, int32_t flags,
+                  int32_t nsamp, int32_t ra, int32_t rb, void *stream);
+
+/*
+ * deg[r] = sum_{e in row r} (val ? val[e] : 1)  (exact integer counts for unweighted
+ * graphs), then deg[r] = deg[r]^power when power != 1 (fuses torch::pow(degrees,-0.5),
+ * codegen/gala.cu:437-440).  With GALA_SPMM_SAMPLE the degree of the kernel-sampled
+ * graph is used (nsamp for rows with deg>0), as FULL_OP does (common.h:1342-1374).
+ * Replaces: aggregate_node_mul_sum_direct_coarse{C}_call(ones, ...) (codegen/gala.cu:227-308).
+ */
+int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags, int32_t nsamp,
+                    void *stream);
+
+/* ---- edge (SDDVV / SDDMM) ops -------------------------------------------------------- */
+#define GALA_SDDVV_ADD 0        /* out[e,h] = a[row,h] + b[col_e,h]   (cuda.h:679-698)     */
+#define GALA_SDDVV_MUL 1        /* out[e,h] = a[row,h] * b[col_e,h]   (cuda.h:848-867)     */
+#define GALA_SDDVV_ADD_LRELU 2  /* ADD followed by LeakyReLU(slope) (common.h:1175-1184)   */
+
+/*
+ * Replaces: edge_sddvv (cuda.h:773-807), aggregate_edge_mul / aggregate_edge_mul_dir
+ *           (cuda.h:870-952).  a_row/b_col are [n_rows,heads] / [n_cols,heads].
+ */
+int gala_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col, int32_t heads,
+                   int32_t op, float slope, float *out_e, void *stream);
+
+/*
+ * out[r,h] (+)= sum_s ( eps + sum_{e in row r, segment s} v[e,h] )
+ * Replaces: node_spmv_backward_of_sddmm_{nln,eaggr} (cuda.h:565-600, 737-772; kernels
+ *           505-524, 659-678 start each segment's per-row sum at 1e-12).
+ * flags: GALA_SPMM_ACCUM adds into out_row, otherwise out_row is overwritten.
+ */
+int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t heads, float eps,
+                     float *out_row, int32_t flags, void *stream);
+
+/*
+ * v[e,h] *= q[row,h] in place.
+ * Replaces: inplace_softmax_sddvv / inplace_softmax_sddvv_mult (cuda.h:601-656,
+ *           kernels 525-562).
+ */
+int gala_row_scale_f32(const gala_csr_t *A, const float *q_row, int32_t heads, float *v_inout,
+                       void *stream);
+
+/*
+ * out[e,h] = sum_{k in head h} Ad[row,k] * Bd[col_e,k]   (F = heads*D features)
+ * Replaces: edge_sddmm (cuda.h:808-845, kernel 699-734; the reference stages Ad's row in
+ *           a block-shared LDS buffer that all 8 rows of a block overwrite — a race,
+ *           SURVEY §5 — here every row owns its slab).
+ */
+int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t lda, const float *Bd,
+                       int64_t ldb, int32_t F, int32_t heads, float *out_e, void *stream);
+
+/* ---- edge softmax ------------------------------------------------------------------- */
+#define GALA_SOFTMAX_REF 0    /* reference: p=min(exp(s),1e12), alpha = p*(1/(S*1e-12+sum p)),
+                                 no max subtraction (common.h:760-773)                    */
+#define GALA_SOFTMAX_FIXED 1  /* numerically stable: alpha = exp(s-max)/sum exp(s-max)    */
+
+/*
+ * alpha[e,h] = softmax over the edges of row(e) of logits[.,h].
+ * Replaces: non_lnr_op_softmax_AutoGrad::forward (common.h:760-773: torch::exp,
+ *           torch::clamp, K7 row-sum, torch::reciprocal, K8 row-scale).
+ */
+int gala_edge_softmax_fwd_f32(const gala_csr_t *A, const float *logits, int32_t heads,
+                              int32_t mode, float *alpha, void *stream);
+
+/*
+ * d_logits[e] = alpha[e]*d_alpha[e] - alpha[e]*(S*eps + sum_{row} alpha*d_alpha)
+ * (eps = 1e-12 in REF mode, 0 in FIXED mode).
+ * Replaces: non_lnr_op_softmax_AutoGrad::backward (common.h:791-799), without the
+ *           reference's in-place overwrite of the saved alpha.
+ */
+int gala_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha, const float *d_alpha,
+                              int32_t heads, int32_t mode, float *d_logits, void *stream);
+
+/*
+ * Fused GAT aggregation (one pass over the edges):
+ *   s = LeakyReLU_slope(aL[row,h] + aR[col,h]);  alpha = edge-softmax(s) (mode);
+ *   Y[row, h*D:(h+1)*D] = sum_e alpha[e,h] * X[col, h*D:(h+1)*D],  F = heads*D.
+ * alpha_out (nullable) receives alpha for the backward pass.
+ * Replaces the forward chain edge_sddvv -> LeakyReLU -> softmax autograd -> weighted
+ * aggregate_node_mul_sum_call (common.h:622-894).
+ */
+int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *X,
+                     int64_t ldx, int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
+                     int64_t ldy, float *alpha_out, void *stream);
+
+/* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
+int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
+                          float *dst, void *stream);
+
+/* ---- host-side graph layout (HOST pointers, OpenMP) --------------------------------- */
+
+/*
+ * COO -> CSR: counting sort by src, then cols ascending inside each row, duplicates
+ * kept (CSRCMatrix::build, csrc_matrix.h:148-376; count_atomic / count_sort_place_*,
+ * sort_range*arr, src/utils/mtx_sort.h:52-174,683-761).  perm_out (nullable) receives the
+ * input index of every CSR edge (stable: ties keep input order).
+ */
+int gala_host_csr_build(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *src,
+                        const int32_t *dst, int32_t *rowptr_out, int32_t *col_out,
+                        int32_t *perm_out);
+
+/*
+ * Column breakpoints {0, c, 2c, ..., n_cols} (static_ord_col_breakpoints,
+ * tiling.h:1594-1608).  Writes at most max_out entries; returns the count (>=2) or <0.
+ */
+int64_t gala_host_col_breakpoints(int64_t n_cols, int64_t cols_per_partition,
+                                  int32_t *out, int64_t max_out);
+
+/*
+ * Column tiling into the relative-offset segment layout (ord_col_tiling_torch,
+ * tiling.h:222-283).  breakpoints has n_seg+1 entries; out_rowptr [(n_rows+1)*n_seg],
+ * out_col/out_val [nnz], out_bounds [2*n_seg].  val / out_val may be NULL.
+ */
+int gala_host_col_tile(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
+                       const float *val, int32_t n_seg, const int32_t *breakpoints,
+                       int32_t *out_rowptr, int32_t *out_col, float *out_val,
+                       int32_t *out_bounds);
+
+/*
+ * Deterministic data sampling: every row keeps nsamp edges j = (ra*ji+rb) mod deg,
+ * sorted (inplace_sample_graph_ab, tiling.h:454-508).  out_rowptr [n_rows+1],
+ * out_col/out_val [n_rows*nsamp].  A row with deg 0 is GALA_ERR_GRAPH (the reference
+ * divides by zero there).
+ */
+int gala_host_sample_ab(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
+                        const float *val, int32_t nsamp, int32_t ra, int32_t rb,
+                        int32_t *out_rowptr, int32_t *out_col, float *out_val);
+
+/*
+ * Transpose a CSR (n_seg == 1): out_rowptr [n_cols+1], out_col [nnz], perm [nnz] with
+ * out edge k == in edge perm[k] (used by the FIXED-mode backward; the reference reuses
+ * the forward graph, cuda.h:1253-1257).
+ */
+int gala_host_csr_transpose(int64_t n_rows, int64_t n_cols, const int32_t *rowptr,
+                            const int32_t *col, int32_t *out_rowptr, int32_t *out_col,
+                            int32_t *perm);
+
+/*
+ * Deterministic synthetic graphs (counter-based hash RNG, thread-count independent):
+ *   kind 0: uniform random symmetric edges + one self loop per vertex;
+ *   kind 1: R-MAT (a=0.57,b=0.19,c=0.19; src/utils/generator.h:37-118) symmetrised
+ *           + self loops.
+ * n_undirected undirected edges -> 2*n_undirected + n vertices directed COO entries
+ * written to src/dst (capacity 2*n_undirected + n).
+ */
+int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected, uint64_t seed,
+                        int32_t *src, int32_t *dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GALA_HIP_H */

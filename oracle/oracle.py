@@ -1,0 +1,255 @@
+"""TEST INFRASTRUCTURE ONLY — numpy/ctypes front of the C oracle (oracle/gala_oracle.c)
+and of the reference harness (oracle/_ref/libgala_ref.so, built from /root/reference).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as
+the checker / CPU baseline.  Nothing in the product package imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(HERE, "_build", "liboracle.so")
+_REF = os.path.join(HERE, "_ref", "libgala_ref.so")
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def build() -> None:
+    """Compile the oracle (and the reference harness when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE, "_build/liboracle.so"], check=True)
+    subprocess.run([os.path.join(HERE, "build_ref.sh")], check=True)
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            subprocess.run(["make", "-s", "-C", HERE, "_build/liboracle.so"], check=True)
+        _lib = ctypes.CDLL(_LIB)
+    return _lib
+
+
+def ref_available() -> bool:
+    return os.path.exists(_REF)
+
+
+def ref():
+    """The reference's own CPU code (compiled from /root/reference)."""
+    global _ref
+    if _ref is None:
+        _ref = ctypes.CDLL(_REF)
+    return _ref
+
+
+@dataclass
+class Graph:
+    """CSR (n_seg == 1) or column-tiled (n_seg > 1) graph on the host."""
+
+    n_rows: int
+    n_cols: int
+    rowptr: np.ndarray  # int32 [(n_rows+1)*n_seg]
+    col: np.ndarray  # int32 [nnz]
+    val: np.ndarray | None = None  # float32 [nnz*val_heads]
+    n_seg: int = 1
+    bounds: np.ndarray | None = None  # int32 [2*n_seg]
+    val_heads: int = 1
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+    @property
+    def seg_base(self):
+        return None if self.n_seg == 1 else np.ascontiguousarray(self.bounds[0::2], dtype=np.int32)
+
+
+def _g(g: Graph):
+    return (_i64(g.n_rows), _i32(g.n_seg), _ptr(g.rowptr), _ptr(g.seg_base))
+
+
+def spmm(g: Graph, X, F=None, src_scale=None, dst_scale=None, Y=None, accum=False,
+         sample=False, nsamp=0, ra=5, rb=7):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    F = X.shape[1] if F is None else F
+    if Y is None:
+        Y = np.zeros((g.n_rows, F), dtype=np.float32)
+    L = lib()
+    L.orc_spmm(*_g(g), _ptr(g.col), _ptr(g.val), _i32(g.val_heads), _ptr(X), _i64(X.shape[1]),
+               _i32(F), _ptr(src_scale), _ptr(dst_scale), ctypes.c_int(int(accum)),
+               ctypes.c_int(int(sample)), _i32(nsamp), _i32(ra), _i32(rb), _ptr(Y),
+               _i64(Y.shape[1]))
+    return Y
+
+
+def gspmm(g: Graph, X):
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    Y = np.zeros((g.n_rows, X.shape[1]), dtype=np.float32)
+    lib().orc_gspmm(_i64(g.n_rows), _ptr(g.rowptr), _ptr(g.col), _ptr(g.val), _ptr(X),
+                    _i32(X.shape[1]), _ptr(Y))
+    return Y
+
+
+def degree(g: Graph, power=1.0, sample=False, nsamp=0):
+    out = np.zeros(g.n_rows, dtype=np.float32)
+    lib().orc_degree(*_g(g), _ptr(g.val), ctypes.c_float(power), ctypes.c_int(int(sample)),
+                     _i32(nsamp), _ptr(out))
+    return out
+
+
+def sddvv(g: Graph, a, b, heads=1, op=0, slope=0.2):
+    out = np.zeros(g.nnz * heads, dtype=np.float32)
+    lib().orc_sddvv(*_g(g), _ptr(g.col), _ptr(np.ascontiguousarray(a, np.float32)),
+                    _ptr(np.ascontiguousarray(b, np.float32)), _i32(heads), _i32(op),
+                    ctypes.c_float(slope), _ptr(out))
+    return out
+
+
+def row_sum(g: Graph, v, heads=1, eps=1e-12, out=None, accum=False):
+    if out is None:
+        out = np.zeros(g.n_rows * heads, dtype=np.float32)
+    lib().orc_row_sum(*_g(g), _ptr(np.ascontiguousarray(v, np.float32)), _i32(heads),
+                      ctypes.c_float(eps), ctypes.c_int(int(accum)), _ptr(out))
+    return out
+
+
+def row_scale(g: Graph, q, v, heads=1):
+    v = np.array(v, dtype=np.float32, copy=True)
+    lib().orc_row_scale(*_g(g), _ptr(np.ascontiguousarray(q, np.float32)), _i32(heads), _ptr(v))
+    return v
+
+
+def sddmm(g: Graph, A, B, heads=1):
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    out = np.zeros(g.nnz * heads, dtype=np.float32)
+    lib().orc_sddmm(*_g(g), _ptr(g.col), _ptr(A), _i64(A.shape[1]), _ptr(B), _i64(B.shape[1]),
+                    _i32(A.shape[1]), _i32(heads), _ptr(out))
+    return out
+
+
+def softmax_fwd(g: Graph, logit, heads=1, mode=0):
+    out = np.zeros(g.nnz * heads, dtype=np.float32)
+    lib().orc_softmax_fwd(*_g(g), _ptr(np.ascontiguousarray(logit, np.float32)), _i32(heads),
+                          ctypes.c_int(mode), _ptr(out))
+    return out
+
+
+def softmax_bwd(g: Graph, alpha, dalpha, heads=1, mode=0):
+    out = np.zeros(g.nnz * heads, dtype=np.float32)
+    lib().orc_softmax_bwd(*_g(g), _ptr(np.ascontiguousarray(alpha, np.float32)),
+                          _ptr(np.ascontiguousarray(dalpha, np.float32)), _i32(heads),
+                          ctypes.c_int(mode), _ptr(out))
+    return out
+
+
+def gat_fwd(g: Graph, aL, aR, X, heads=1, slope=0.2, mode=0):
+    """Reference GAT layer forward: edge_sddvv -> LeakyReLU -> softmax ->
+    weighted aggregation, composed from the restated kernels."""
+    s = sddvv(g, aL, aR, heads=heads, op=2, slope=slope)
+    alpha = softmax_fwd(g, s, heads=heads, mode=mode)
+    gw = Graph(g.n_rows, g.n_cols, g.rowptr, g.col, alpha, g.n_seg, g.bounds, heads)
+    return spmm(gw, X), alpha
+
+
+def csr_build(n_rows, src, dst):
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    rowptr = np.zeros(n_rows + 1, np.int32)
+    col = np.zeros(src.shape[0], np.int32)
+    rc = lib().orc_csr_build(_i64(n_rows), _i64(src.shape[0]), _ptr(src), _ptr(dst), _ptr(rowptr),
+                             _ptr(col))
+    assert rc == 0
+    return rowptr, col
+
+
+def col_tile(g: Graph, cols_per_partition):
+    S = (g.n_cols + cols_per_partition - 1) // cols_per_partition
+    rp = np.zeros((g.n_rows + 1) * max(S, 1), np.int32)
+    col = np.zeros(g.nnz, np.int32)
+    val = np.zeros(g.nnz, np.float32)
+    bounds = np.zeros(2 * max(S, 1), np.int32)
+    n = lib().orc_col_tile(_i64(g.n_rows), _i64(g.n_cols), _ptr(g.rowptr), _ptr(g.col),
+                           _ptr(g.val), _i32(cols_per_partition), _ptr(rp), _ptr(col), _ptr(val),
+                           _ptr(bounds))
+    assert n == S
+    return Graph(g.n_rows, g.n_cols, rp, col, val, S, bounds)
+
+
+def sample_ab(g: Graph, nsamp, ra=5, rb=7):
+    rp = np.zeros(g.n_rows + 1, np.int32)
+    col = np.zeros(g.n_rows * nsamp, np.int32)
+    val = np.zeros(g.n_rows * nsamp, np.float32)
+    rc = lib().orc_sample_ab(_i64(g.n_rows), _ptr(g.rowptr), _ptr(g.col), _ptr(g.val), _i32(nsamp),
+                             _i32(ra), _i32(rb), _ptr(rp), _ptr(col), _ptr(val))
+    assert rc == 0
+    return Graph(g.n_rows, g.n_cols, rp, col, val)
+
+
+# ---- reference (compiled from /root/reference) ----------------------------------------
+def ref_csr_build(n_rows, n_cols, src, dst):
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    rp = np.zeros(n_rows + 1, np.int32)
+    col = np.zeros(src.shape[0], np.int32)
+    val = np.zeros(src.shape[0], np.float32)
+    ref().ref_csr_build(ctypes.c_int(n_rows), ctypes.c_int(n_cols), ctypes.c_int(src.shape[0]),
+                        _ptr(src), _ptr(dst), _ptr(rp), _ptr(col), _ptr(val))
+    return rp, col, val
+
+
+def ref_gspmm(g: Graph, X, Y=None):
+    X = np.ascontiguousarray(X, np.float32)
+    val = g.val if g.val is not None else np.ones(g.nnz, np.float32)
+    if Y is None:
+        Y = np.zeros((g.n_rows, X.shape[1]), np.float32)
+    ref().ref_gspmm(ctypes.c_int(g.n_rows), ctypes.c_int(g.n_cols), ctypes.c_int(g.nnz),
+                    _ptr(g.rowptr), _ptr(g.col), _ptr(val), _ptr(X), ctypes.c_int(X.shape[1]),
+                    _ptr(Y))
+    return Y
+
+
+def ref_col_tile(g: Graph, cols_per_partition, max_seg=4096):
+    S = (g.n_cols + cols_per_partition - 1) // cols_per_partition
+    val = g.val if g.val is not None else np.ones(g.nnz, np.float32)
+    rp = np.zeros((g.n_rows + 1) * max(S, 1), np.int32)
+    col = np.zeros(g.nnz, np.int32)
+    oval = np.zeros(g.nnz, np.float32)
+    bounds = np.zeros(2 * max(S, 1), np.int32)
+    n = ref().ref_col_tile(ctypes.c_int(g.n_rows), ctypes.c_int(g.n_cols), ctypes.c_int(g.nnz),
+                           _ptr(g.rowptr), _ptr(g.col), _ptr(val), ctypes.c_int(cols_per_partition),
+                           ctypes.c_int(max_seg), _ptr(rp), _ptr(col), _ptr(oval), _ptr(bounds))
+    assert n == S, (n, S)
+    return Graph(g.n_rows, g.n_cols, rp, col, oval, S, bounds)
+
+
+def ref_sample_ab(g: Graph, nsamp, ra=5, rb=7):
+    val = g.val if g.val is not None else np.ones(g.nnz, np.float32)
+    rp = np.zeros(g.n_rows + 1, np.int32)
+    col = np.zeros(g.n_rows * nsamp, np.int32)
+    oval = np.zeros(g.n_rows * nsamp, np.float32)
+    ref().ref_sample_ab(ctypes.c_int(g.n_rows), ctypes.c_int(g.n_cols), ctypes.c_int(g.nnz),
+                        _ptr(g.rowptr), _ptr(g.col), _ptr(val), ctypes.c_int(nsamp),
+                        ctypes.c_int(ra), ctypes.c_int(rb), _ptr(rp), _ptr(col), _ptr(oval))
+    return Graph(g.n_rows, g.n_cols, rp, col, oval)
+
+
+def ref_threads() -> int:
+    return int(ref().ref_omp_threads())

@@ -1,0 +1,131 @@
+// TEST INFRASTRUCTURE ONLY — never linked into the product library.
+//
+// extern "C" shims over the reference's own CPU code, compiled by oracle/build_ref.sh
+// directly from the headers where they lie under /root/reference (nothing is copied
+// into this repository).  The output library oracle/_ref/libgala_ref.so is used by
+// tests/golden/make_golden.py to generate the golden fixtures and, when present, by
+// bench.py's cpu_baseline leg (kind "reference").
+//
+// Reference code exercised (paths relative to the reference root):
+//   readSM_npy32 build path  tests/common.h:331-366 -> CSRCMatrix::build
+//                             src/formats/csrc_matrix.h:148-376, set_all 413-421
+//   gSpMM + wsumAgg           src/ops/aggregators.h:12-31, 55-127
+//   static_ord_col_breakpoints + ord_col_tiling_torch  src/ops/tiling.h:1594-1608, 222-283
+//   inplace_sample_graph_ab   src/ops/tiling.h:454-508
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "src/formats/csrc_matrix.h"
+#include "src/formats/dense_matrix.h"
+#include "src/ops/aggregators.h"
+#include "src/ops/tiling.h"
+
+typedef CSRCMatrix<int, int, float> SM;
+typedef DenseMatrix<int, int, float> DM;
+
+template <typename T>
+static T *aligned_copy(const T *src, int64_t n) {
+    T *p = (T *)aligned_alloc(64, ((n * sizeof(T) + 63) / 64) * 64 + 64);
+    if (n) memcpy(p, src, n * sizeof(T));
+    return p;
+}
+
+extern "C" int ref_csr_build(int nrows, int ncols, int nnz, const int *src, const int *dst,
+                             int *rowptr_out, int *col_out, float *val_out) {
+    // exactly the readSM_npy32 sequence: aligned row/col id arrays, a value buffer,
+    // build(..., CSRC_TYPE::CSR), set_all(1)  (tests/common.h:354-363)
+    int *row_ids = aligned_copy(src, nnz);
+    int *col_ids = aligned_copy(dst, nnz);
+    float *vals = (float *)aligned_alloc(64, ((int64_t)nnz * 4 + 63) / 64 * 64 + 64);
+    SM adj;
+    adj.build(nrows, ncols, nnz, row_ids, col_ids, vals, CSRC_TYPE::CSR);
+    adj.set_all(1);
+    memcpy(rowptr_out, adj.offset_ptr(), (int64_t)(nrows + 1) * sizeof(int));
+    memcpy(col_out, adj.ids_ptr(), (int64_t)nnz * sizeof(int));
+    if (val_out) memcpy(val_out, adj.vals_ptr(), (int64_t)nnz * sizeof(float));
+    free(row_ids);
+    free(col_ids);
+    free(vals);
+    return 0;
+}
+
+static void import_graph(SM &A, int nrows, int ncols, int nnz, const int *rowptr, const int *col,
+                         const float *val) {
+    A.import_csr(nrows, ncols, nnz, const_cast<int *>(col), const_cast<float *>(val),
+                 const_cast<int *>(rowptr));
+}
+static void release_graph(SM &A) {  // imported arrays are not owned: detach before ~CSRCMatrix
+    A.import_csr(0, 0, 0, nullptr, nullptr, nullptr);
+}
+
+extern "C" int ref_gspmm(int nrows, int ncols, int nnz, const int *rowptr, const int *col,
+                         const float *val, const float *X, int F, float *Y) {
+    // out row r += sum_e val_e * X[col_e]  in CSR order (gSpMM + wsumAgg); Y is the
+    // accumulator (caller zero-fills it, as the generated code does)
+    SM A;
+    import_graph(A, nrows, ncols, nnz, rowptr, col, val);
+    DM B, out;
+    B.import_mtx(ncols, F, (int64_t)ncols * F, const_cast<float *>(X));
+    out.import_mtx(nrows, F, (int64_t)nrows * F, Y);
+    gSpMM<DM, SM>(&A, &B, &out, wsumAgg<float, float, int>);
+    B.import_mtx(nullptr);
+    out.import_mtx(nullptr);
+    release_graph(A);
+    return 0;
+}
+
+extern "C" int ref_col_tile(int nrows, int ncols, int nnz, const int *rowptr, const int *col,
+                            const float *val, int cols_per_partition, int max_seg,
+                            int *out_rowptr, int *out_col, float *out_val, int *out_bounds) {
+    // the emitted COL_TILE transformation (src/codegen/common.h:417-436)
+    SM A;
+    import_graph(A, nrows, ncols, nnz, rowptr, col, val);
+    std::vector<int> bp = static_ord_col_breakpoints<SM>(&A, cols_per_partition);
+    const int segments = (int)bp.size() - 1;
+    if (segments > max_seg) {
+        release_graph(A);
+        return -segments;
+    }
+    auto oi = torch::TensorOptions().dtype(torch::kInt).requires_grad(false);
+    auto of = torch::TensorOptions().dtype(torch::kFloat).requires_grad(false);
+    torch::Tensor offsets = torch::zeros({(int64_t)(nrows + 1) * segments}, oi);
+    torch::Tensor cols = torch::zeros({nnz}, oi);
+    torch::Tensor vals = torch::zeros({nnz}, of);
+    torch::Tensor bounds = torch::zeros({2 * segments}, oi);
+    ord_col_tiling_torch<SM>(bp, offsets, cols, vals, bounds, &A);
+    memcpy(out_rowptr, offsets.data_ptr<int>(), (int64_t)(nrows + 1) * segments * sizeof(int));
+    memcpy(out_col, cols.data_ptr<int>(), (int64_t)nnz * sizeof(int));
+    memcpy(out_val, vals.data_ptr<float>(), (int64_t)nnz * sizeof(float));
+    memcpy(out_bounds, bounds.data_ptr<int>(), 2 * segments * sizeof(int));
+    release_graph(A);
+    return segments;
+}
+
+extern "C" int ref_sample_ab(int nrows, int ncols, int nnz, const int *rowptr, const int *col,
+                             const float *val, int nsamp, int ra, int rb, int *out_rowptr,
+                             int *out_col, float *out_val) {
+    SM A;
+    // inplace_sample_graph_ab replaces the graph's arrays; hand it private copies
+    import_graph(A, nrows, ncols, nnz, aligned_copy(rowptr, nrows + 1), aligned_copy(col, nnz),
+                 aligned_copy(val, nnz));
+    int *o0 = A.offset_ptr();
+    int *c0 = A.ids_ptr();
+    float *v0 = A.vals_ptr();
+    inplace_sample_graph_ab<SM>(&A, nsamp, ra, rb);
+    memcpy(out_rowptr, A.offset_ptr(), (int64_t)(nrows + 1) * sizeof(int));
+    memcpy(out_col, A.ids_ptr(), (int64_t)nrows * nsamp * sizeof(int));
+    memcpy(out_val, A.vals_ptr(), (int64_t)nrows * nsamp * sizeof(float));
+    free(A.offset_ptr());
+    free(A.ids_ptr());
+    free(A.vals_ptr());
+    free(o0);
+    free(c0);
+    free(v0);
+    release_graph(A);
+    return 0;
+}
+
+extern "C" int ref_omp_threads(void) { return omp_get_max_threads(); }

@@ -1,0 +1,44 @@
+"""Shared test graphs (seeded, small enough for the oracle to finish in seconds)."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle as orc
+from gala import layout
+
+
+def to_oracle(g: layout.HostGraph, val=None, heads=1) -> orc.Graph:
+    v = g.val if val is None else val
+    return orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col, v, g.n_seg, g.bounds, heads)
+
+
+def cora_like(seed=42) -> layout.HostGraph:
+    # N=2708, 5278 undirected edges + N self loops = 13264 stored edges
+    return layout.gen_graph("uniform", 2708, 5278, seed)
+
+
+def powerlaw(n=4096, m=30000, seed=7) -> layout.HostGraph:
+    return layout.gen_graph("rmat", n, m, seed)
+
+
+def with_empty_rows(n=700, m=3000, seed=3) -> layout.HostGraph:
+    """Directed random graph (no self loops) with a block of empty rows + one heavy row."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n // 2, m).astype(np.int32)       # rows >= n/2 empty
+    dst = rng.integers(0, n, m).astype(np.int32)
+    heavy = np.full(900, 5, np.int32)                        # row 5: >= 900 edges
+    src = np.concatenate([src, heavy])
+    dst = np.concatenate([dst, rng.integers(0, n, 900).astype(np.int32)])
+    return layout.csr_build(n, n, src, dst)
+
+
+def features(n, F, seed=1234, integer=False):
+    rng = np.random.default_rng(seed)
+    if integer:
+        return rng.integers(-8, 9, (n, F)).astype(np.float32)
+    return rng.uniform(-1, 1, (n, F)).astype(np.float32)
+
+
+def edge_values(nnz, heads=1, seed=99, lo=0.0, hi=1.0):
+    rng = np.random.default_rng(seed)
+    return rng.uniform(lo, hi, nnz * heads).astype(np.float32)

@@ -1,0 +1,234 @@
+"""GPU parity: libgala_hip.so (through the C ABI) vs the oracle on the same seeded inputs.
+
+Bar: bit-exact for SpMM/degree/SDDVV/row-scale (same per-row CSR order and the same
+rounding steps as the reference kernels), |err| <= 1e-4 (abs) + 1e-4 (rel) for the
+reductions whose order the GPU changes (row-sum, SDDMM dot, softmax, fused GAT).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as orc
+from gala import _abi, layout, ops
+from _graphs import cora_like, edge_values, features, powerlaw, to_oracle, with_empty_rows
+
+pytestmark = pytest.mark.gpu
+TOL = dict(atol=1e-4, rtol=1e-4)
+DEV = "cuda"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+GRAPHS = {"cora": cora_like, "powerlaw": powerlaw, "empty_rows": with_empty_rows}
+
+
+@pytest.fixture(scope="module", params=list(GRAPHS))
+def graph(request):
+    return GRAPHS[request.param]()
+
+
+@pytest.mark.parametrize("F", [1, 2, 7, 16, 32, 40, 47, 64, 100, 128, 256, 602])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_bitexact(graph, F, weighted):
+    val = edge_values(graph.nnz) if weighted else None
+    X = features(graph.n_cols, F)
+    ref = orc.spmm(to_oracle(graph, val), X)
+    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val))
+    Y = host(ops.spmm(dg, dev(X)))
+    np.testing.assert_array_equal(Y, ref)
+
+
+@pytest.mark.parametrize("F", [16, 47])
+def test_spmm_reference_gspmm(F):
+    """Same numbers as the reference's own CPU gSpMM (pinned by the golden fixtures)."""
+    g = cora_like()
+    X = features(g.n_cols, F, integer=False)
+    dg = ops.DeviceGraph.from_host(g)
+    Y = host(ops.spmm(dg, dev(X)))
+    np.testing.assert_array_equal(Y, orc.gspmm(to_oracle(g), X))
+
+
+def test_spmm_strided_and_accum():
+    g = cora_like()
+    Xf = features(g.n_cols, 40)
+    X = dev(Xf)[:, 4:36]           # ldx = 40, F = 32, 16-B aligned
+    Y0 = features(g.n_rows, 48, seed=5)
+    Yt = dev(Y0)
+    out = Yt[:, 8:40]
+    ops.spmm(ops.DeviceGraph.from_host(g), X, out=out, accum=True)
+    ref = orc.spmm(to_oracle(g), Xf[:, 4:36].copy(), Y=Y0[:, 8:40].copy(), accum=True)
+    got = host(Yt)
+    np.testing.assert_array_equal(got[:, 8:40], ref)
+    np.testing.assert_array_equal(got[:, :8], Y0[:, :8])
+    np.testing.assert_array_equal(got[:, 40:], Y0[:, 40:])
+
+
+@pytest.mark.parametrize("F", [32, 47])
+def test_spmm_gcn_norm_fused(F):
+    g = powerlaw()
+    norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
+    X = features(g.n_cols, F)
+    ref = orc.spmm(to_oracle(g), X, src_scale=norm, dst_scale=norm)
+    dg = ops.DeviceGraph.from_host(g)
+    Y = host(ops.spmm(dg, dev(X), src_scale=dev(norm), dst_scale=dev(norm)))
+    np.testing.assert_array_equal(Y, ref)
+
+
+@pytest.mark.parametrize("cpp", [900, 1000, 2708])
+@pytest.mark.parametrize("F", [1, 32, 100])
+def test_spmm_col_tiled(cpp, F):
+    g = cora_like()
+    t = layout.col_tile(g, cpp)
+    X = features(g.n_cols, F)
+    ref = orc.spmm(to_oracle(t), X)
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(t), dev(X)))
+    np.testing.assert_array_equal(Y, ref)
+    # tiled == untiled: segments partition each row's ascending columns in order
+    np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g), X))
+
+
+def test_spmm_many_segments():
+    g = cora_like()
+    t = layout.col_tile(g, 20)   # 136 segments > 64 per launch
+    X = features(g.n_cols, 32)
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(t), dev(X)))
+    np.testing.assert_array_equal(Y, orc.spmm(to_oracle(t), X))
+
+
+@pytest.mark.parametrize("F", [32, 256])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_spmm_kernel_sampled(F, tiled):
+    g = with_empty_rows()
+    if tiled:
+        g = layout.col_tile(g, 300)
+    X = features(g.n_cols, F)
+    ref = orc.spmm(to_oracle(g), X, sample=True, nsamp=20, ra=5, rb=7)
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(g), dev(X), nsamp=20, ra=5, rb=7))
+    np.testing.assert_array_equal(Y, ref)
+
+
+def test_spmm_multihead_weights():
+    g = cora_like()
+    H, D = 4, 8
+    val = edge_values(g.nnz, heads=H)
+    X = features(g.n_cols, H * D)
+    ref = orc.spmm(to_oracle(g, val, heads=H), X)
+    dg = ops.DeviceGraph.from_host(g).with_values(dev(val), val_heads=H)
+    np.testing.assert_array_equal(host(ops.spmm(dg, dev(X))), ref)
+
+
+@pytest.mark.parametrize("power", [1.0, -0.5])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_degree(graph, power, weighted):
+    val = edge_values(graph.nnz) if weighted else None
+    ref = orc.degree(to_oracle(graph, val), power=power)
+    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val))
+    got = host(ops.degree(dg, power=power))
+    if power == 1.0:
+        np.testing.assert_array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, **TOL)
+
+
+def test_degree_sampled_full_op():
+    g = layout.col_tile(cora_like(), 1000)
+    got = host(ops.degree(ops.DeviceGraph.from_host(g), nsamp=20))
+    np.testing.assert_array_equal(got, np.full(g.n_rows, 20.0 * g.n_seg, np.float32))
+
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+@pytest.mark.parametrize("heads", [1, 4])
+def test_sddvv(graph, op, heads):
+    a = features(graph.n_rows, heads, seed=11)
+    b = features(graph.n_cols, heads, seed=12)
+    ref = orc.sddvv(to_oracle(graph), a, b, heads=heads, op=op, slope=0.2)
+    got = host(ops.sddvv(ops.DeviceGraph.from_host(graph), dev(a), dev(b), op=op, heads=heads, slope=0.2))
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_row_sum_and_scale(graph, tiled):
+    g = layout.col_tile(graph, 1000) if tiled else graph
+    v = edge_values(g.nnz, seed=5)
+    dg = ops.DeviceGraph.from_host(g)
+    got = host(ops.row_sum(dg, dev(v), eps=1e-12))
+    np.testing.assert_allclose(got, orc.row_sum(to_oracle(g), v, eps=1e-12), **TOL)
+    q = features(g.n_rows, 1, seed=6).ravel()
+    vv = dev(v)
+    ops.row_scale_(dg, dev(q), vv)
+    np.testing.assert_array_equal(host(vv), orc.row_scale(to_oracle(g), q, v))
+
+
+@pytest.mark.parametrize("F,heads", [(1, 1), (16, 1), (32, 1), (47, 1), (100, 1), (256, 8), (64, 2)])
+def test_sddmm(graph, F, heads):
+    A = features(graph.n_rows, F, seed=21)
+    B = features(graph.n_cols, F, seed=22)
+    got = host(ops.sddmm(ops.DeviceGraph.from_host(graph), dev(A), dev(B), heads=heads))
+    np.testing.assert_allclose(got, orc.sddmm(to_oracle(graph), A, B, heads=heads), **TOL)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("heads", [1, 3])
+def test_edge_softmax(graph, mode, heads):
+    s = edge_values(graph.nnz, heads=heads, lo=-3, hi=3, seed=8)
+    d = edge_values(graph.nnz, heads=heads, lo=-1, hi=1, seed=9)
+    dg = ops.DeviceGraph.from_host(graph)
+    a = host(ops.edge_softmax(dg, dev(s), heads=heads, mode=mode))
+    a_ref = orc.softmax_fwd(to_oracle(graph), s, heads=heads, mode=mode)
+    np.testing.assert_allclose(a, a_ref, **TOL)
+    ds = host(ops.edge_softmax_bwd(dg, dev(a_ref), dev(d), heads=heads, mode=mode))
+    np.testing.assert_allclose(ds, orc.softmax_bwd(to_oracle(graph), a_ref, d, heads=heads, mode=mode), **TOL)
+
+
+def test_edge_softmax_overflow_clamp():
+    """REF mode clamps exp at 1e12 and has no max subtraction (common.h:760-761)."""
+    g = cora_like()
+    s = edge_values(g.nnz, lo=20, hi=40, seed=8)
+    got = host(ops.edge_softmax(ops.DeviceGraph.from_host(g), dev(s)))
+    np.testing.assert_allclose(got, orc.softmax_fwd(to_oracle(g), s), **TOL)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8)])
+def test_gat_fused(graph, mode, F, heads):
+    aL = features(graph.n_rows, heads, seed=31)
+    aR = features(graph.n_cols, heads, seed=32)
+    X = features(graph.n_cols, F, seed=33)
+    Y_ref, al_ref = orc.gat_fwd(to_oracle(graph), aL, aR, X, heads=heads, slope=0.2, mode=mode)
+    Y, al = ops.gat_fwd(ops.DeviceGraph.from_host(graph), dev(aL), dev(aR), dev(X), heads=heads,
+                        slope=0.2, mode=mode, want_alpha=True)
+    np.testing.assert_allclose(host(al), al_ref, **TOL)
+    np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+
+
+def test_edge_permute():
+    g = powerlaw()
+    t, perm = layout.transpose(g)
+    v = edge_values(g.nnz, heads=2)
+    got = host(ops.edge_permute(dev(perm), dev(v), heads=2))
+    np.testing.assert_array_equal(got, v.reshape(-1, 2)[perm].ravel())
+
+
+def test_empty_graph_and_zero_features():
+    g = layout.HostGraph(5, 5, np.zeros(6, np.int32), np.zeros(0, np.int32))
+    dg = ops.DeviceGraph.from_host(g)
+    Y = host(ops.spmm(dg, torch.ones(5, 8, device=DEV)))
+    np.testing.assert_array_equal(Y, np.zeros((5, 8), np.float32))
+    np.testing.assert_array_equal(host(ops.degree(dg)), np.zeros(5, np.float32))
+
+
+def test_invalid_args_fail_loudly():
+    g = cora_like()
+    dg = ops.DeviceGraph.from_host(g)
+    X = torch.ones(g.n_cols, 8, device=DEV)
+    with pytest.raises(_abi.GalaError):
+        _abi.call("gala_spmm_f32", dg.csr(), X.data_ptr(), 4, X.data_ptr(), 8, 8, None, None, 0, 0, 0, 0, None)
+    with pytest.raises(ValueError):
+        ops.spmm(dg, torch.ones(g.n_cols, 8))
