@@ -6,7 +6,8 @@ ogbn-products-shaped graph (BASELINE.json: "aggregated edges/sec, GCN-2 ogbn-pro
 One step = the hot-path work of one GCN-2 training epoch of the generated program
 (codegen/gala.cu:423-459 + the autograd backward, gala.cu:391-414):
     norm = degree(A)^-1/2                       (gala_degree_f32, fused pow)
-    layer-1 forward  H1 = norm * A (norm * X)   (gala_spmm_f32, F=32, fused norms)
+    layer-1 forward  H1 = norm * A (norm * X)   (gala_row_broadcast_f32 + gala_spmm_f32
+                                                 with the dst norm fused, F=32)
     layer-2 forward  H2 = norm * A (norm * H1)
     layer-2 backward dH1 = norm * A (norm * dH2)   (undirected: same CSR, gala.cu:403-413)
     layer-1 backward dX  = norm * A (norm * dH1)
@@ -42,12 +43,12 @@ def log(*a):
 
 
 def spmm_alg_bytes(n_rows, n_cols, nnz, F, weighted=False, scaled=True):
-    """4(N+1) + 4E [+4E] + 4*N*F (X once) + 4*N*F (Y write) [+ 8N norms]."""
+    """4(N+1) + 4E [+4E] + 4*N*F (X once) + 4*N*F (Y write) [+ 4N dst norm]."""
     b = 4 * (n_rows + 1) + 4 * nnz + 4 * n_cols * F + 4 * n_rows * F
     if weighted:
         b += 4 * nnz
     if scaled:
-        b += 4 * n_cols + 4 * n_rows
+        b += 4 * n_rows
     return b
 
 
@@ -117,6 +118,7 @@ def main():
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     X = torch.rand((N, F), device="cuda", generator=gen) * 2 - 1
     dY = torch.rand((N, F), device="cuda", generator=gen) * 2 - 1
+    Xs = torch.empty_like(X)   # norm-prescaled input of the current aggregation
     H1 = torch.empty_like(X)
     H2 = torch.empty_like(X)
     G1 = torch.empty_like(X)
@@ -128,11 +130,12 @@ def main():
     def step(record=False):
         norm = ops.degree(dg, power=-0.5)
         for src, dst in ((X, H1), (H1, H2), (dY, G1), (G1, G0)):
+            ops.row_broadcast(norm, src, out=Xs)           # `norm * res` (ROW_BROADCAST)
             if record:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            ops.spmm(dg, src, src_scale=norm, dst_scale=norm, out=dst)
+            ops.spmm(dg, Xs, dst_scale=norm, out=dst)        # norm * A (.)
             if record:
                 e1.record(stream)
                 spmm_ev.append((e0, e1))
@@ -187,7 +190,7 @@ def main():
                    "n_rows": hg.n_rows, "nnz": hg.nnz, "F": F, "parallelism": f"replica{world}" if world > 1 else "1gpu"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "k_spmm_rowgroup<4,8,1,8,unweighted,src/dst-scaled> (gala_spmm_f32 F=32)",
+                     "kernel": "k_spmm_rowgroup<4,8,1,8,unweighted,dst-scaled> (gala_spmm_f32 F=32)",
                      "kernel_ms": t_spmm * 1e3, "alg_bytes_per_launch": alg,
                      "gather_GBps": (4 * (hg.n_rows + 1) + hg.nnz * (4 + 4 * F + 4) + 4 * hg.n_rows * F) / t_spmm / 1e9},
         "event_ms_per_step": elapsed * 1e3 / args.steps,

@@ -9,6 +9,8 @@
 //
 // Row-segment ops ("RS" kernels): a group of G lanes owns one row and strides over its
 // edges (coalesced edge arrays), reductions use xor butterflies inside the group.
+#include <stddef.h>
+
 #include "gala_internal.h"
 
 namespace gala {
@@ -23,9 +25,11 @@ struct EdgeParams {
 
 __device__ __forceinline__ void row_range(const EdgeParams &p, int s, int64_t row, int64_t &e0,
                                           int64_t &e1) {
-    const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * (p.n_rows + 1);
-    e0 = (int64_t)p.seg.base[s] + rp[row];
-    e1 = (int64_t)p.seg.base[s] + rp[row + 1];
+    // EdgeParams is every edge kernel's first argument: read the table from kernarg
+    KernargSegPtr seg = kernarg_segtable(offsetof(EdgeParams, seg));
+    const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * (p.n_rows + 1);
+    e0 = (int64_t)seg->base[s] + rp[row];
+    e1 = (int64_t)seg->base[s] + rp[row + 1];
 }
 
 #define GALA_ROW_PROLOGUE(G)                                                          \
@@ -194,124 +198,174 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
 }
 
 // ---- SDDMM dot (K9) -----------------------------------------------------------------
-// Row group of G lanes over the features (VEC per lane), heads reduce over HW lanes.
-template <int G, int VEC, int HW>
+// Row group of G lanes over the features (VEC per lane); U edges per batch have all
+// their loads in flight before the dot products.  For one head (HW == G) the U partial
+// dots are reduced with a reduce-scatter butterfly (U-1 + log2(G/U) shuffles per batch,
+// lane k*(G/U) ends with edge k); with heads each head reduces over its HW lanes.
+template <int G, int U>
+__device__ __forceinline__ float reduce_scatter(float (&v)[U], int gl) {
+#pragma unroll
+    for (int m = U, o = G / 2; m > 1; m >>= 1, o >>= 1) {
+        const bool up = (gl & o) != 0;
+#pragma unroll
+        for (int i = 0; i < m / 2; ++i) {
+            const float send = up ? v[i] : v[i + m / 2];
+            const float keep = up ? v[i + m / 2] : v[i];
+            v[i] = keep + __shfl_xor(send, o, 64);
+        }
+    }
+    float r = v[0];
+#pragma unroll
+    for (int o = G / (2 * U); o >= 1; o >>= 1) r += __shfl_xor(r, o, 64);
+    return r;
+}
+
+template <int G, int VEC, int HW, int U>
 __global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad, int64_t lda,
                                                   const float *Bd, int64_t ldb, int32_t F,
                                                   float *out) {
     GALA_ROW_PROLOGUE(G);
     const int f = gl * VEC;
     const bool cv = row_ok && f < F;
+    const int64_t fo = (f < F) ? f : 0;
     float a[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) a[i] = cv ? Ad[row * lda + f + i] : 0.0f;
     const int H = p.heads;
     const int D = F / H;
     const int h = cv ? f / D : 0;
-    // wave-uniform loop bound: groups of one wave own different rows
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0 = 0, e1 = 0;
         if (row_ok) row_range(p, s, row, e0, e1);
-        const int64_t n = e1 - e0;
-        int64_t nmax = n;
+        const int32_t n = (int32_t)(e1 - e0);
+        for (int32_t j0 = 0; j0 < n; j0 += U) {
+            float part[U];
 #pragma unroll
-        for (int o = 32; o >= G; o >>= 1) {
-            const int64_t other = __shfl_xor((long long)nmax, o, 64);
-            nmax = other > nmax ? other : nmax;
-        }
-        for (int64_t j = 0; j < nmax; ++j) {
-            float part = 0.0f;
-            if (j < n && cv) {
+            for (int k = 0; k < U; ++k) {
+                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
                 const int64_t c = p.col[e0 + j];
-                const float *bp = Bd + c * ldb + f;
+                const float *bp = Bd + c * ldb + fo;
+                float acc = 0.0f;
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) part = fmaf(a[i], bp[i], part);
+                for (int i = 0; i < VEC; ++i) acc = fmaf(a[i], bp[i], acc);
+                part[k] = acc;
             }
-            part = group_sum<HW>(part);
-            if (j < n && cv && (gl % HW) == 0) out[(e0 + j) * H + h] = part;
+            if (HW == G) {
+                const float r = reduce_scatter<G, U>(part, gl);
+                const int k = gl / (G / U);
+                if ((gl & (G / U - 1)) == 0 && j0 + k < n) out[e0 + j0 + k] = r;
+            } else {
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const float r = group_sum<HW>(part[k]);
+                    if (cv && (gl % HW) == 0 && j0 + k < n) out[(e0 + j0 + k) * H + h] = r;
+                }
+            }
         }
     }
 }
 
 // ---- fused GAT aggregation -----------------------------------------------------------
-// Row group of G lanes over the F = heads*D features (one feature per lane per chunk).
-template <int G, int CH, int MODE>
+// Row group of G lanes, lane g owns VEC features at g*VEC (G*VEC >= F); U edges per
+// batch: cols, aR[col] and the X row slices are all loaded before the softmax updates.
+template <int VEC>
+struct GVec;
+template <>
+struct GVec<1> { typedef float T; };
+template <>
+struct GVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
+template <>
+struct GVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
+
+template <int G, int VEC, int U, int MODE>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *aL, const float *aR,
                                                     const float *X, int64_t ldx, int32_t F,
                                                     float slope, float *Y, int64_t ldy,
                                                     float *alpha_out) {
+    typedef typename GVec<VEC>::T V;
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
     const int H = p.heads;
     const int D = F / H;
-    float acc[CH], m[CH], sum[CH], al[CH];
-    int hh[CH];
-    bool cv[CH];
+    const int f = gl * VEC;
+    const bool cv = f < F;
+    const int64_t fo = cv ? f : 0;
+    const int hh = (int)(fo / D);
+    const float al = aL[row * H + hh];
+    float acc[VEC];
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const int f = ch * G + gl;
-        cv[ch] = f < F;
-        hh[ch] = cv[ch] ? f / D : 0;
-        acc[ch] = 0.0f;
-        m[ch] = -INFINITY;
-        sum[ch] = 0.0f;
-        al[ch] = aL[row * H + hh[ch]];
-    }
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.0f;
+    float m = -INFINITY, sum = 0.0f;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        for (int64_t e = e0; e < e1; ++e) {
-            const int64_t c = p.col[e];
+        const int32_t n = (int32_t)(e1 - e0);
+        for (int32_t j0 = 0; j0 < n; j0 += U) {
+            int64_t c[U];
+            float ar[U];
+            V x[U];
 #pragma unroll
-            for (int ch = 0; ch < CH; ++ch) {
-                if (!cv[ch]) continue;
-                float z = __fadd_rn(al[ch], aR[c * H + hh[ch]]);
+            for (int k = 0; k < U; ++k) {
+                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+                c[k] = p.col[e0 + j];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                ar[k] = aR[c[k] * H + hh];
+                x[k] = *reinterpret_cast<const V *>(X + c[k] * ldx + fo);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                if (j0 + k >= n) continue;
+                float z = __fadd_rn(al, ar[k]);
                 z = z > 0.0f ? z : __fmul_rn(z, slope);
-                const float x = X[c * ldx + ch * G + gl];
+                const float *xv = reinterpret_cast<const float *>(&x[k]);
                 if (MODE == GALA_SOFTMAX_REF) {
                     const float pe = ref_exp(z);
-                    sum[ch] = __fadd_rn(sum[ch], pe);
-                    acc[ch] = fmaf(pe, x, acc[ch]);
+                    sum = __fadd_rn(sum, pe);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(pe, xv[i], acc[i]);
+                } else if (z > m) {
+                    const float r = expf(m - z);
+                    sum = fmaf(sum, r, 1.0f);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], r, xv[i]);
+                    m = z;
                 } else {
-                    if (z > m[ch]) {
-                        const float r = expf(m[ch] - z);
-                        sum[ch] = fmaf(sum[ch], r, 1.0f);
-                        acc[ch] = fmaf(acc[ch], r, x);
-                        m[ch] = z;
-                    } else {
-                        const float pe = expf(z - m[ch]);
-                        sum[ch] = __fadd_rn(sum[ch], pe);
-                        acc[ch] = fmaf(pe, x, acc[ch]);
-                    }
+                    const float pe = expf(z - m);
+                    sum = __fadd_rn(sum, pe);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(pe, xv[i], acc[i]);
                 }
             }
         }
     }
-    float q[CH];
+    const float den = (MODE == GALA_SOFTMAX_REF) ? sum + (float)p.seg.n * 1e-12f : sum;
+    const float q = 1.0f / den;
+    if (cv) {
+        V out;
+        float *ov = reinterpret_cast<float *>(&out);
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        if (!cv[ch]) continue;
-        const float den = (MODE == GALA_SOFTMAX_REF) ? sum[ch] + (float)p.seg.n * 1e-12f : sum[ch];
-        q[ch] = 1.0f / den;
-        Y[row * ldy + ch * G + gl] = (sum[ch] == 0.0f && MODE != GALA_SOFTMAX_REF)
-                                         ? 0.0f
-                                         : __fmul_rn(acc[ch], q[ch]);
+        for (int i = 0; i < VEC; ++i)
+            ov[i] = (MODE != GALA_SOFTMAX_REF && sum == 0.0f) ? 0.0f : __fmul_rn(acc[i], q);
+        *reinterpret_cast<V *>(Y + row * ldy + fo) = out;
     }
     if (alpha_out) {
-        // one lane per head writes alpha (lane holding the head's first feature)
+        // lanes stride over the row's edges; head h's (m, q) live in lane h*D/VEC of the group
+        const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
-            for (int64_t e = e0; e < e1; ++e) {
-                const int64_t c = p.col[e];
-#pragma unroll
-                for (int ch = 0; ch < CH; ++ch) {
-                    const int f = ch * G + gl;
-                    if (!cv[ch] || (f % D) != 0) continue;
-                    float z = __fadd_rn(al[ch], aR[c * H + hh[ch]]);
+            for (int hd = 0; hd < H; ++hd) {
+                const int src = gbase + (hd * D) / VEC;
+                const float mh = __shfl(m, src, 64);
+                const float qh = __shfl(q, src, 64);
+                const float alh = aL[row * H + hd];
+                for (int64_t e = e0 + gl; e < e1; e += G) {
+                    float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + hd]);
                     z = z > 0.0f ? z : __fmul_rn(z, slope);
-                    const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - m[ch]);
-                    alpha_out[e * H + hh[ch]] = __fmul_rn(pe, q[ch]);
+                    const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
+                    alpha_out[e * H + hd] = __fmul_rn(pe, qh);
                 }
             }
         }
@@ -330,9 +384,10 @@ __global__ __launch_bounds__(kBlock) void k_permute(const int32_t *perm, const f
 // ---- host side ------------------------------------------------------------------------
 static int pick_group(const gala_csr_t *A, int heads) {
     // lanes per row from the mean row length (edges*heads)
+    // ~2-4 edges per lane: several rows per wave amortise the per-row bookkeeping
     const double avg = A->n_rows ? (double)A->nnz * heads / (double)A->n_rows : 1.0;
     int g = 4;
-    while (g < 64 && g < avg) g <<= 1;
+    while (g < 64 && 2 * g * 2 <= avg) g <<= 1;
     return g;
 }
 
@@ -474,14 +529,15 @@ template <int G, int VEC>
 static void launch_sddmm(const EdgeParams &p, int hw, const float *Ad, int64_t lda,
                          const float *Bd, int64_t ldb, int32_t F, float *out, hipStream_t hs) {
     const dim3 grid(blocks_for(p.n_rows, G));
+    constexpr int U = (G >= 8) ? 8 : G;  // U <= G for the reduce-scatter
     switch (hw) {
-        case 1: hipLaunchKernelGGL((k_sddmm<G, VEC, 1>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 2: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 2 ? G : 2)>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 4: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 4 ? G : 4)>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 8: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 8 ? G : 8)>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 16: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 16 ? G : 16)>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 32: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 32 ? G : 32)>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        default: hipLaunchKernelGGL((k_sddmm<G, VEC, G>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 1: hipLaunchKernelGGL((k_sddmm<G, VEC, 1, U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 2: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 2 ? G : 2), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 4: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 4 ? G : 4), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 8: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 8 ? G : 8), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 16: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 16 ? G : 16), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 32: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 32 ? G : 32), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        default: hipLaunchKernelGGL((k_sddmm<G, VEC, G, U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
     }
 }
 
@@ -526,17 +582,33 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     return launch_status();
 }
 
-template <int G, int CH>
+template <int G, int VEC>
 static void launch_gat(const EdgeParams &p, int mode, const float *aL, const float *aR,
                        const float *X, int64_t ldx, int32_t F, float slope, float *Y,
                        int64_t ldy, float *alpha_out, hipStream_t hs) {
     const dim3 grid(blocks_for(p.n_rows, G));
+    constexpr int U = 8;
     if (mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_fwd<G, CH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, aL,
-                           aR, X, ldx, F, slope, Y, ldy, alpha_out);
-    else
-        hipLaunchKernelGGL((k_gat_fwd<G, CH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p,
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p,
                            aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
+    else
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs,
+                           p, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
+}
+
+template <int VEC>
+static int gat_vec(const EdgeParams &p, int L, int mode, const float *aL, const float *aR,
+                   const float *X, int64_t ldx, int32_t F, float slope, float *Y, int64_t ldy,
+                   float *alpha_out, hipStream_t hs) {
+    if (L <= 1) launch_gat<1, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 2) launch_gat<2, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 4) launch_gat<4, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 8) launch_gat<8, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 16) launch_gat<16, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 32) launch_gat<32, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (L <= 64) launch_gat<64, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else return GALA_ERR_UNSUPPORTED;
+    return GALA_OK;
 }
 
 extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
@@ -550,18 +622,18 @@ extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const floa
     if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || !aR || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    const int D = F / heads;
+    int vec = 4;
+    while (vec > 1 && (D % vec || ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) ||
+                       ((uintptr_t)Y % (4 * vec))))
+        vec >>= 1;
+    const int L = (F + vec - 1) / vec;
     hipStream_t hs = (hipStream_t)stream;
-    if (F <= 1) launch_gat<1, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 2) launch_gat<2, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 4) launch_gat<4, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 8) launch_gat<8, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 16) launch_gat<16, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 32) launch_gat<32, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 64) launch_gat<64, 1>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 128) launch_gat<64, 2>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 256) launch_gat<64, 4>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (F <= 512) launch_gat<64, 8>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else return GALA_ERR_UNSUPPORTED;
+    int r;
+    if (vec == 4) r = gat_vec<4>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else if (vec == 2) r = gat_vec<2>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    else r = gat_vec<1>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    if (r) return r;
     return launch_status();
 }
 

@@ -24,6 +24,21 @@ struct SegTable {
     int32_t rp[kMaxSegPerLaunch];      // index of the segment's rowptr block (s)
 };
 
+// Kernel-argument structs keep the segment table by value; indexing it with a runtime
+// segment id must not copy the array into VGPRs, so kernels read it through the kernarg
+// segment pointer (scalar loads).  `off` = offsetof(<params struct>, seg); the params
+// struct is the kernel's first argument (kernarg offset 0).
+typedef const SegTable __attribute__((address_space(4))) *KernargSegPtr;
+__device__ __forceinline__ KernargSegPtr kernarg_segtable(size_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const char __attribute__((address_space(4))) *KernargBytes;
+    return (KernargSegPtr)((KernargBytes)__builtin_amdgcn_kernarg_segment_ptr() + off);
+#else
+    (void)off;
+    return nullptr;
+#endif
+}
+
 // Thread-local last HIP error (the only mutable state of the library).
 void set_last_hip_error(int e);
 

@@ -13,6 +13,8 @@
 // with the neighbour loads of U edges issued before the first add, so the result is
 // bit-identical to the reference kernel while each lane keeps U*CH vector loads in
 // flight.  All address arithmetic is 64-bit.
+#include <stddef.h>
+
 #include "gala_internal.h"
 
 namespace gala {
@@ -93,8 +95,9 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
     const int64_t row = wave * RPW + grp;
     if (row >= p.n_rows) return;
+    KernargSegPtr seg = kernarg_segtable(offsetof(SpmmParams, seg));
 
-    // columns owned by this lane
+    // columns owned by this lane; lanes past F load a valid column and never store
     bool cvalid[CH];
     int64_t coff[CH];
     int head[CH];
@@ -102,80 +105,54 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
     for (int ch = 0; ch < CH; ++ch) {
         const int f = (ch * G + gl) * VEC;
         cvalid[ch] = f < p.F;
-        coff[ch] = f;
-        head[ch] = W ? (cvalid[ch] ? f / p.head_dim : 0) : 0;
+        coff[ch] = cvalid[ch] ? f : 0;
+        head[ch] = W ? (int)(coff[ch] / p.head_dim) : 0;
     }
 
     V acc[CH];
     const bool start_from_y = p.accum && p.dst_scale == nullptr;
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        if (start_from_y && cvalid[ch])
-            acc[ch] = ldv<VEC>(p.Y + row * p.ldy + coff[ch]);
-        else
-            acc[ch] = V(0.0f);
-    }
+    for (int ch = 0; ch < CH; ++ch)
+        acc[ch] = (start_from_y && cvalid[ch]) ? ldv<VEC>(p.Y + row * p.ldy + coff[ch]) : V(0.0f);
 
     const int64_t rp_stride = p.n_rows + 1;
-    for (int s = 0; s < p.seg.n; ++s) {
-        const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * rp_stride;
-        const int64_t base = p.seg.base[s];
+    const int nseg = p.seg.n;
+    for (int s = 0; s < nseg; ++s) {
+        const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
+        const int64_t base = seg->base[s];
         const int64_t e0 = base + rp[row];
         const int64_t e1 = base + rp[row + 1];
-        if (SAMP) {
-            const int32_t deg = (int32_t)(e1 - e0);
-            if (deg > 0) {
-                for (int ji = 0; ji < p.nsamp; ji += U) {
-                    int32_t c[U];
-                    float w[U][CH];
-                    V x[U][CH];
+        const int32_t deg = (int32_t)(e1 - e0);
+        // n edges visited: all of them, or nsamp samples when the row is not empty
+        const int32_t n = SAMP ? (deg > 0 ? p.nsamp : 0) : deg;
+        for (int32_t j0 = 0; j0 < n; j0 += U) {
+            int32_t c[U];
+            V x[U][CH];
+            float w[U][CH];
+            float sc[U];
+            // issue every load of the batch before the first add: clamped indices keep
+            // the addresses valid, the tail is masked in the accumulation
 #pragma unroll
-                    for (int k = 0; k < U; ++k) {
-                        if (ji + k < p.nsamp) {
-                            const int32_t j = (p.ra * (ji + k) + p.rb) % deg;
-                            c[k] = p.col[e0 + j];
+            for (int k = 0; k < U; ++k) {
+                const int32_t jj = (j0 + k < n) ? j0 + k : n - 1;
+                const int32_t j = SAMP ? (p.ra * jj + p.rb) % deg : jj;
+                const int64_t e = e0 + j;
+                c[k] = p.col[e];
 #pragma unroll
-                            for (int ch = 0; ch < CH; ++ch) {
-                                w[k][ch] = W ? p.val[(e0 + j) * p.val_heads + head[ch]] : 1.0f;
-                                if (cvalid[ch]) x[k][ch] = ldv<VEC>(p.X + (int64_t)c[k] * p.ldx + coff[ch]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < U; ++k) {
-                        if (ji + k < p.nsamp) {
-                            const float sc = SRCS ? p.src_scale[c[k]] : 1.0f;
-#pragma unroll
-                            for (int ch = 0; ch < CH; ++ch)
-                                if (cvalid[ch]) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc);
-                        }
-                    }
-                }
+                for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + head[ch]] : 1.0f;
             }
-        } else {
-            for (int64_t e = e0; e < e1; e += U) {
-                int32_t c[U];
-                float w[U][CH];
-                V x[U][CH];
 #pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    if (e + k < e1) {
-                        c[k] = p.col[e + k];
+            for (int k = 0; k < U; ++k) {
+                const float *xr = p.X + (int64_t)c[k] * p.ldx;
 #pragma unroll
-                        for (int ch = 0; ch < CH; ++ch) {
-                            w[k][ch] = W ? p.val[(e + k) * p.val_heads + head[ch]] : 1.0f;
-                            if (cvalid[ch]) x[k][ch] = ldv<VEC>(p.X + (int64_t)c[k] * p.ldx + coff[ch]);
-                        }
-                    }
-                }
+                for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + coff[ch]);
+                sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
+            }
 #pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    if (e + k < e1) {
-                        const float sc = SRCS ? p.src_scale[c[k]] : 1.0f;
+            for (int k = 0; k < U; ++k) {
+                if (j0 + k < n) {
 #pragma unroll
-                        for (int ch = 0; ch < CH; ++ch)
-                            if (cvalid[ch]) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc);
-                    }
+                    for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
                 }
             }
         }
@@ -220,8 +197,9 @@ __global__ __launch_bounds__(kBlock) void k_degree_count(DegParams p) {
         d = (float)p.nsamp * (float)p.seg.n;  // FULL_OP: n * global_segments[0] (common.h:1358-1359)
     } else {
         int64_t cnt = 0;
+        KernargSegPtr seg = kernarg_segtable(offsetof(DegParams, seg));
         for (int s = 0; s < p.seg.n; ++s) {
-            const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * (p.n_rows + 1);
+            const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * (p.n_rows + 1);
             cnt += rp[row + 1] - rp[row];
         }
         d = (float)cnt;  // exact: sequential sum of 1.0f is exact below 2^24
@@ -235,9 +213,10 @@ __global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
     const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (row >= p.n_rows) return;
     float d = 0.0f;
+    KernargSegPtr seg = kernarg_segtable(offsetof(DegParams, seg));
     for (int s = 0; s < p.seg.n; ++s) {
-        const int32_t *rp = p.rowptr + (int64_t)p.seg.rp[s] * (p.n_rows + 1);
-        const int64_t e0 = p.seg.base[s] + (int64_t)rp[row], e1 = p.seg.base[s] + (int64_t)rp[row + 1];
+        const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * (p.n_rows + 1);
+        const int64_t e0 = seg->base[s] + (int64_t)rp[row], e1 = seg->base[s] + (int64_t)rp[row + 1];
         for (int64_t e = e0; e < e1; ++e) d = __fadd_rn(d, p.val[e]);
     }
     if (p.power != 1.0f) d = (p.power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, p.power);
@@ -400,5 +379,48 @@ extern "C" int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int
     else
         hipLaunchKernelGGL(k_degree_count, dim3((unsigned)blocks), dim3(kBlock), 0,
                            (hipStream_t)stream, p);
+    return launch_status();
+}
+
+// ---- ROW_BROADCAST: Y[r,:] = scale[r] * X[r,:] ----------------------------------------
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void k_row_broadcast(int64_t n_rows, int32_t L,
+                                                          const float *scale, const float *X,
+                                                          int64_t ldx, float *Y, int64_t ldy) {
+    typedef typename VecT<VEC>::T V;
+    const int64_t total = n_rows * L;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = t / L;
+        const int64_t c = (t - r * L) * VEC;
+        const float s = scale[r];
+        V v = ldv<VEC>(X + r * ldx + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) el<VEC>(v, i) = __fmul_rn(s, el<VEC>(v, i));
+        stv<VEC>(Y + r * ldy + c, v);
+    }
+}
+
+extern "C" int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale,
+                                      const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                      void *stream) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!scale || !X || !Y) return GALA_ERR_INVALID_ARG;
+    int vec = 4;
+    while (vec > 1 && (F % vec || ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) ||
+                       ((uintptr_t)Y % (4 * vec))))
+        vec >>= 1;
+    const int32_t L = F / vec;
+    const int64_t total = n_rows * L;
+    int64_t blocks = (total + kBlock - 1) / kBlock;
+    if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride: 16 workgroups per CU
+    hipStream_t hs = (hipStream_t)stream;
+    if (vec == 4)
+        hipLaunchKernelGGL(k_row_broadcast<4>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
+    else if (vec == 2)
+        hipLaunchKernelGGL(k_row_broadcast<2>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
+    else
+        hipLaunchKernelGGL(k_row_broadcast<1>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
     return launch_status();
 }

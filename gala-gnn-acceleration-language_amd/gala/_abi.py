@@ -54,6 +54,7 @@ SIGNATURES = {
     "gala_last_hip_error": (ctypes.c_int, []),
     "gala_spmm_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _P]),
     "gala_degree_f32": (ctypes.c_int, [_CSR, _P, _F, _I32, _I32, _P]),
+    "gala_row_broadcast_f32": (ctypes.c_int, [_I64, _I32, _P, _P, _I64, _P, _I64, _P]),
     "gala_sddvv_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _F, _P, _P]),
     "gala_row_sum_f32": (ctypes.c_int, [_CSR, _P, _I32, _F, _P, _I32, _P]),
     "gala_row_scale_f32": (ctypes.c_int, [_CSR, _P, _I32, _P, _P]),

@@ -86,6 +86,15 @@ def degree(g: DeviceGraph, power=1.0, nsamp=None) -> torch.Tensor:
     return out
 
 
+def row_broadcast(scale, X, out=None) -> torch.Tensor:
+    """out[r, :] = scale[r] * X[r, :] (ROW_BROADCAST_OP, `norm * res`)."""
+    if out is None:
+        out = torch.empty_like(X)
+    _abi.call("gala_row_broadcast_f32", X.shape[0], X.shape[1], _dp(scale), _dp(X), X.stride(0),
+              _dp(out), out.stride(0), _stream())
+    return out
+
+
 def sddvv(g: DeviceGraph, a, b, op=_abi.GALA_SDDVV_ADD, heads=1, slope=0.2) -> torch.Tensor:
     out = torch.empty(g.nnz * heads, device=a.device, dtype=torch.float32)
     _abi.call("gala_sddvv_f32", g.csr(), _dp(a), _dp(b), heads, op, slope, _dp(out), _stream())

@@ -107,11 +107,20 @@ int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, in
  * deg[r] = sum_{e in row r} (val ? val[e] : 1)  (exact integer counts for unweighted
  * graphs), then deg[r] = deg[r]^power when power != 1 (fuses torch::pow(degrees,-0.5),
  * codegen/gala.cu:437-440).  With GALA_SPMM_SAMPLE the degree of the kernel-sampled
- * graph is used (nsamp for rows with deg>0), as FULL_OP does (common.h:1342-1374).
+ * graph is used: nsamp * n_seg for every row, as FULL_OP does (common.h:1342-1374).
  * Replaces: aggregate_node_mul_sum_direct_coarse{C}_call(ones, ...) (codegen/gala.cu:227-308).
  */
 int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags, int32_t nsamp,
                     void *stream);
+
+/*
+ * Y[r, 0:F] = scale[r] * X[r, 0:F]  (rounded product, torch `norm * res`).
+ * Replaces: the ROW_BROADCAST_OP the generated forward applies around every GCN
+ * aggregation (src/codegen/common.h:1150-1169, emitted codegen/gala.cu:442-456).
+ * Y may alias X (in place) when ldy == ldx.
+ */
+int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale, const float *X,
+                           int64_t ldx, float *Y, int64_t ldy, void *stream);
 
 /* ---- edge (SDDVV / SDDMM) ops -------------------------------------------------------- */
 #define GALA_SDDVV_ADD 0        /* out[e,h] = a[row,h] + b[col_e,h]   (cuda.h:679-698)     */

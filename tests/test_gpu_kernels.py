@@ -81,6 +81,19 @@ def test_spmm_gcn_norm_fused(F):
     np.testing.assert_array_equal(Y, ref)
 
 
+@pytest.mark.parametrize("F", [1, 3, 32, 47, 100])
+def test_row_broadcast_then_spmm_matches_fused(F):
+    """norm * A (norm * X) as two kernels == the fused src/dst-scaled SpMM, bit for bit."""
+    g = powerlaw()
+    norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
+    X = features(g.n_cols, F)
+    dg = ops.DeviceGraph.from_host(g)
+    Xs = ops.row_broadcast(dev(norm), dev(X))
+    np.testing.assert_array_equal(host(Xs), norm[:, None] * X)
+    Y = host(ops.spmm(dg, Xs, dst_scale=dev(norm)))
+    np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g), X, src_scale=norm, dst_scale=norm))
+
+
 @pytest.mark.parametrize("cpp", [900, 1000, 2708])
 @pytest.mark.parametrize("F", [1, 32, 100])
 def test_spmm_col_tiled(cpp, F):
