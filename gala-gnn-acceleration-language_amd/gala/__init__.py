@@ -7,4 +7,11 @@
 """
 from . import _abi, layout  # noqa: F401
 
-__all__ = ["_abi", "layout"]
+__all__ = ["_abi", "layout", "torch_ext"]
+
+
+def torch_ext():
+    """The C++/libtorch operator mirror (host/gala_torch.cpp) as a Python module."""
+    import torch  # noqa: F401  (loads libtorch before the extension)
+    from . import _gala_torch
+    return _gala_torch

@@ -1,0 +1,517 @@
+// C++/libtorch mirror of GALA's emitted operator API over the C ABI (see gala_torch.h).
+#include "gala_torch.h"
+
+#include <c10/hip/HIPStream.h>
+
+namespace gala {
+
+namespace {
+
+void *stream() { return (void *)c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int status, const char *fn) {
+    TORCH_CHECK(status == GALA_OK, "gala: ", fn, " failed: ", gala_status_string(status),
+                status == GALA_ERR_HIP ? " (hipError " + std::to_string(gala_last_hip_error()) + ")"
+                                       : std::string());
+}
+
+void check_dev(const torch::Tensor &t, torch::ScalarType ty, const char *name) {
+    TORCH_CHECK(t.defined(), "gala: ", name, " is undefined");
+    TORCH_CHECK(t.is_cuda(), "gala: ", name, " must be a device tensor (no CPU fallback)");
+    TORCH_CHECK(t.scalar_type() == ty, "gala: ", name, " has dtype ", t.scalar_type());
+    TORCH_CHECK(t.is_contiguous(), "gala: ", name, " must be contiguous");
+}
+
+// A gala_csr_t view of the generated program's (offset, columns, value, bounds) tensors.
+struct CsrView {
+    gala_csr_t c{};
+    torch::Tensor bounds_host;  // keeps the host bounds alive
+};
+
+CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torch::Tensor *vals,
+             const torch::Tensor &bounds, int64_t segments, int val_heads = 1) {
+    check_dev(offsets, torch::kInt, "offset_graph");
+    check_dev(cols, torch::kInt, "columns_graph");
+    TORCH_CHECK(segments >= 1, "gala: segments must be >= 1");
+    TORCH_CHECK(offsets.numel() % segments == 0, "gala: offset_graph size is not (nrows+1)*segments");
+    CsrView v;
+    v.c.n_rows = offsets.numel() / segments - 1;
+    v.c.n_cols = v.c.n_rows;
+    v.c.nnz = cols.numel();
+    v.c.rowptr = offsets.data_ptr<int32_t>();
+    v.c.col = cols.data_ptr<int32_t>();
+    v.c.val = nullptr;
+    v.c.val_heads = val_heads;
+    if (vals) {
+        check_dev(*vals, torch::kFloat, "value_graph");
+        v.c.val = vals->data_ptr<float>();
+    }
+    v.c.n_seg = (int32_t)segments;
+    v.c.seg_bounds = nullptr;
+    if (segments > 1) {
+        TORCH_CHECK(bounds.defined() && bounds.numel() >= 2 * segments, "gala: bounds missing");
+        v.bounds_host = bounds.to(torch::kCPU, torch::kInt).contiguous();
+        v.c.seg_bounds = v.bounds_host.data_ptr<int32_t>();
+    }
+    return v;
+}
+
+torch::TensorOptions fopts(const torch::Tensor &like) {
+    return torch::TensorOptions().dtype(torch::kFloat).device(like.device());
+}
+
+torch::Tensor row_sum_impl(const torch::Tensor &offsets, const torch::Tensor &cols,
+                           const torch::Tensor &v, const torch::Tensor &bounds, int64_t nrows,
+                           int64_t segments, float eps) {
+    auto vv = v.contiguous();
+    CsrView cv = view(offsets, cols, nullptr, bounds, segments);
+    TORCH_CHECK(cv.c.n_rows == nrows, "gala: nrows does not match offset_graph");
+    check_dev(vv, torch::kFloat, "value_graph");
+    const int heads = (int)(vv.numel() / std::max<int64_t>(cols.numel(), 1));
+    auto out = torch::empty({nrows, std::max(heads, 1)}, fopts(v));
+    check(gala_row_sum_f32(&cv.c, vv.data_ptr<float>(), std::max(heads, 1), eps,
+                           out.data_ptr<float>(), 0, stream()),
+          "gala_row_sum_f32");
+    return out;
+}
+
+torch::Tensor row_scale_impl(const torch::Tensor &row_val, const torch::Tensor &offsets,
+                             const torch::Tensor &cols, torch::Tensor value_graph,
+                             const torch::Tensor &bounds, int64_t nrows, int64_t segments) {
+    CsrView cv = view(offsets, cols, nullptr, bounds, segments);
+    TORCH_CHECK(cv.c.n_rows == nrows, "gala: nrows does not match offset_graph");
+    auto q = row_val.contiguous();
+    check_dev(q, torch::kFloat, "row_val");
+    check_dev(value_graph, torch::kFloat, "value_graph");
+    const int heads = (int)(q.numel() / std::max<int64_t>(nrows, 1));
+    check(gala_row_scale_f32(&cv.c, q.data_ptr<float>(), std::max(heads, 1),
+                             value_graph.data_ptr<float>(), stream()),
+          "gala_row_scale_f32");
+    return value_graph;
+}
+
+torch::Tensor sddvv_impl(const torch::Tensor &a, const torch::Tensor &b,
+                         const torch::Tensor &offsets, const torch::Tensor &cols,
+                         const torch::Tensor &bounds, int64_t segments, int op, float slope) {
+    CsrView cv = view(offsets, cols, nullptr, bounds, segments);
+    auto ac = a.contiguous(), bc = b.contiguous();
+    check_dev(ac, torch::kFloat, "input_dense1");
+    check_dev(bc, torch::kFloat, "input_dense2");
+    const int64_t nrows = cv.c.n_rows;
+    const int heads = (int)std::max<int64_t>(ac.numel() / std::max<int64_t>(nrows, 1), 1);
+    cv.c.n_cols = bc.numel() / heads;
+    auto out = heads == 1 ? torch::empty({cols.numel()}, fopts(a))
+                          : torch::empty({cols.numel(), heads}, fopts(a));
+    check(gala_sddvv_f32(&cv.c, ac.data_ptr<float>(), bc.data_ptr<float>(), heads, op, slope,
+                         out.data_ptr<float>(), stream()),
+          "gala_sddvv_f32");
+    return out;
+}
+
+torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
+                        const torch::Tensor &cols, const torch::Tensor *vals,
+                        const torch::Tensor &bounds, int64_t segments, int val_heads,
+                        const torch::Tensor *src_scale, const torch::Tensor *dst_scale,
+                        int64_t nsamples, int64_t ra, int64_t rb) {
+    CsrView cv = view(offsets, cols, vals, bounds, segments, val_heads);
+    auto x = X.contiguous();
+    check_dev(x, torch::kFloat, "input_dense");
+    const int64_t nrows = cv.c.n_rows;
+    // reference: dcols = input_dense.numel() / nrows (cuda.h:453-454)
+    const int64_t dcols = x.dim() == 2 ? x.size(1) : x.numel() / std::max<int64_t>(nrows, 1);
+    cv.c.n_cols = dcols ? x.numel() / dcols : 0;
+    auto out = torch::empty({nrows, dcols}, fopts(X));
+    const float *ss = nullptr, *ds = nullptr;
+    torch::Tensor ssc, dsc;
+    if (src_scale) {
+        ssc = src_scale->contiguous();
+        check_dev(ssc, torch::kFloat, "src_scale");
+        ss = ssc.data_ptr<float>();
+    }
+    if (dst_scale) {
+        dsc = dst_scale->contiguous();
+        check_dev(dsc, torch::kFloat, "dst_scale");
+        ds = dsc.data_ptr<float>();
+    }
+    const int32_t flags = nsamples > 0 ? GALA_SPMM_SAMPLE : 0;
+    check(gala_spmm_f32(&cv.c, x.data_ptr<float>(), dcols, out.data_ptr<float>(), dcols,
+                        (int32_t)dcols, ss, ds, flags, (int32_t)nsamples, (int32_t)ra,
+                        (int32_t)rb, stream()),
+          "gala_spmm_f32");
+    return out;
+}
+
+}  // namespace
+
+// ---- slots ----------------------------------------------------------------------------
+int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor vals,
+                     torch::Tensor b, int segs, bool w) {
+    offset_graph.push_back(offsets);
+    columns_graph.push_back(cols);
+    value_graph.push_back(vals);
+    bounds.push_back(b.defined() ? b.to(torch::kCPU, torch::kInt).contiguous() : b);
+    segments.push_back(segs);
+    weighted.push_back(w);
+    transpose_perm.push_back(torch::Tensor());
+    if (offset_graph.size() == 1) nrows = offsets.numel() / segs - 1;
+    return (int)offset_graph.size() - 1;
+}
+
+void GraphSlots::clear() { *this = GraphSlots(); }
+
+GraphSlots &global_slots() {
+    static GraphSlots s;
+    return s;
+}
+
+// ---- emitted free functions ---------------------------------------------------------------
+torch::Tensor aggregate_node_mul_sum_call(torch::Tensor input_dense, torch::Tensor offset_graph,
+                                          torch::Tensor columns_graph, torch::Tensor value_graph,
+                                          torch::Tensor bounds, int64_t segments, bool weighted,
+                                          int64_t nsamples, int64_t ra, int64_t rb) {
+    return spmm_impl(input_dense, offset_graph, columns_graph, weighted ? &value_graph : nullptr,
+                     bounds, segments, 1, nullptr, nullptr, nsamples, ra, rb);
+}
+
+torch::Tensor aggregate_node_mul_sum_direct_call(torch::Tensor input_dense,
+                                                 torch::Tensor offset_graph,
+                                                 torch::Tensor columns_graph,
+                                                 torch::Tensor value_graph, torch::Tensor bounds,
+                                                 int64_t segments, bool weighted) {
+    return aggregate_node_mul_sum_call(input_dense, offset_graph, columns_graph, value_graph,
+                                       bounds, segments, weighted);
+}
+
+torch::Tensor gather_forward(torch::Tensor input_dense, torch::Tensor offset_graph,
+                             torch::Tensor columns_graph, torch::Tensor value_graph) {
+    // cuSPARSE CSR_ALG2 path, alpha = beta = 1 onto a zero output (cuda.h:211-279)
+    return aggregate_node_mul_sum_call(input_dense, offset_graph, columns_graph, value_graph, {},
+                                       1, true);
+}
+
+torch::Tensor node_spmv_backward_of_sddmm_nln(torch::Tensor offset_graph,
+                                              torch::Tensor columns_graph,
+                                              torch::Tensor value_graph, torch::Tensor bounds,
+                                              int64_t nrows, int64_t segments) {
+    return row_sum_impl(offset_graph, columns_graph, value_graph, bounds, nrows, segments, 1e-12f);
+}
+
+torch::Tensor node_spmv_backward_of_sddmm_eaggr(torch::Tensor offset_graph,
+                                                torch::Tensor columns_graph,
+                                                torch::Tensor value_graph, torch::Tensor bounds,
+                                                int64_t nrows, int64_t segments) {
+    return row_sum_impl(offset_graph, columns_graph, value_graph, bounds, nrows, segments, 1e-12f);
+}
+
+torch::Tensor inplace_softmax_sddvv(torch::Tensor row_val, torch::Tensor offset_graph,
+                                    torch::Tensor columns_graph, torch::Tensor value_graph,
+                                    torch::Tensor bounds, int64_t nrows, int64_t segments) {
+    return row_scale_impl(row_val, offset_graph, columns_graph, value_graph, bounds, nrows,
+                          segments);
+}
+
+torch::Tensor inplace_softmax_sddvv_mult(torch::Tensor row_val, torch::Tensor offset_graph,
+                                         torch::Tensor columns_graph, torch::Tensor value_graph,
+                                         torch::Tensor bounds, int64_t nrows, int64_t segments) {
+    return row_scale_impl(row_val, offset_graph, columns_graph, value_graph, bounds, nrows,
+                          segments);
+}
+
+torch::Tensor edge_sddvv(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                         torch::Tensor offset_graph, torch::Tensor columns_graph,
+                         torch::Tensor value_graph, torch::Tensor bounds, int64_t nrows,
+                         int64_t segments) {
+    (void)value_graph;
+    (void)nrows;
+    return sddvv_impl(input_dense1, input_dense2, offset_graph, columns_graph, bounds, segments,
+                      GALA_SDDVV_ADD, 0.0f);
+}
+
+torch::Tensor edge_sddmm(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                         torch::Tensor offset_graph, torch::Tensor columns_graph,
+                         torch::Tensor value_graph, torch::Tensor bounds, int64_t nrows,
+                         int64_t segments) {
+    (void)value_graph;
+    CsrView cv = view(offset_graph, columns_graph, nullptr, bounds, segments);
+    TORCH_CHECK(cv.c.n_rows == nrows, "gala: nrows does not match offset_graph");
+    auto a = input_dense1.contiguous(), b = input_dense2.contiguous();
+    check_dev(a, torch::kFloat, "input_dense1");
+    check_dev(b, torch::kFloat, "input_dense2");
+    const int64_t dcols = a.numel() / std::max<int64_t>(nrows, 1);  // cuda.h:813-814
+    cv.c.n_cols = b.numel() / std::max<int64_t>(dcols, 1);
+    auto out = torch::empty({columns_graph.numel()}, fopts(a));
+    check(gala_sddmm_dot_f32(&cv.c, a.data_ptr<float>(), dcols, b.data_ptr<float>(), dcols,
+                             (int32_t)dcols, 1, out.data_ptr<float>(), stream()),
+          "gala_sddmm_dot_f32");
+    return out;
+}
+
+torch::Tensor aggregate_edge_mul(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                 torch::Tensor offset_graph, torch::Tensor columns_graph,
+                                 torch::Tensor value_graph, torch::Tensor bounds,
+                                 int64_t segments) {
+    (void)value_graph;
+    return sddvv_impl(input_dense1, input_dense2, offset_graph, columns_graph, bounds, segments,
+                      GALA_SDDVV_MUL, 0.0f);
+}
+
+torch::Tensor aggregate_edge_mul_dir(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                     torch::Tensor offset_graph, torch::Tensor columns_graph,
+                                     torch::Tensor value_graph) {
+    return aggregate_edge_mul(input_dense1, input_dense2, offset_graph, columns_graph,
+                              value_graph, {}, 1);
+}
+
+torch::Tensor row_broadcast(torch::Tensor scale, torch::Tensor X) {
+    auto s = scale.contiguous(), x = X.contiguous();
+    check_dev(s, torch::kFloat, "scale");
+    check_dev(x, torch::kFloat, "X");
+    const int64_t n = x.size(0), F = x.numel() / std::max<int64_t>(n, 1);
+    auto out = torch::empty_like(x);
+    check(gala_row_broadcast_f32(n, (int32_t)F, s.data_ptr<float>(), x.data_ptr<float>(), F,
+                                 out.data_ptr<float>(), F, stream()),
+          "gala_row_broadcast_f32");
+    return out;
+}
+
+torch::Tensor degree_norm(torch::Tensor offset_graph, torch::Tensor bounds, int64_t segments,
+                          double power) {
+    auto cols = torch::empty({0}, offset_graph.options());
+    CsrView cv = view(offset_graph, cols, nullptr, bounds, segments);
+    auto out = torch::empty({cv.c.n_rows, 1}, fopts(offset_graph));
+    check(gala_degree_f32(&cv.c, out.data_ptr<float>(), (float)power, 0, 0, stream()),
+          "gala_degree_f32");
+    return out;
+}
+
+torch::Tensor gcn_aggregate(torch::Tensor X, torch::Tensor norm, torch::Tensor offset_graph,
+                            torch::Tensor columns_graph, torch::Tensor bounds, int64_t segments) {
+    // norm * A (norm * X): prescale pass (streaming) + SpMM with the dst norm fused; the
+    // src norm is not fused into the SpMM because a per-edge norm[col] gather costs as much
+    // as the feature row itself at F <= 32
+    auto xs = row_broadcast(norm, X);
+    return spmm_impl(xs, offset_graph, columns_graph, nullptr, bounds, segments, 1, nullptr,
+                     &norm, 0, 5, 7);
+}
+
+// ---- autograd Functions ------------------------------------------------------------------
+using torch::autograd::AutogradContext;
+using torch::autograd::tensor_list;
+
+namespace {
+
+struct Slot {
+    torch::Tensor off, cols, vals, bounds, perm;
+    int segs;
+    bool weighted;
+};
+
+Slot slot(int64_t idx) {
+    auto &S = global_slots();
+    TORCH_CHECK(idx >= 0 && idx < (int64_t)S.offset_graph.size(), "gala: graph slot ", idx,
+                " not registered");
+    return {S.offset_graph[idx], S.columns_graph[idx], S.value_graph[idx], S.bounds[idx],
+            S.transpose_perm[idx], S.segments[idx], S.weighted[idx]};
+}
+
+// aggregate_node_mul_sum_coarse{C}_AutoGrad (common.h:928-978; gala.cu:391-414)
+struct AggregateNodeMulSum : public torch::autograd::Function<AggregateNodeMulSum> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor input_dense, int64_t li) {
+        ctx->saved_data["li"] = li;
+        Slot s = slot(2 * li);
+        auto &S = global_slots();
+        return aggregate_node_mul_sum_call(input_dense, s.off, s.cols, s.vals, s.bounds, s.segs,
+                                           s.weighted, S.nsamples, S.ra, S.rb);
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        const int64_t li = ctx->saved_data["li"].toInt();
+        Slot s = slot(2 * li + 1);
+        auto &S = global_slots();
+        return {aggregate_node_mul_sum_call(grad_outputs[0], s.off, s.cols, s.vals, s.bounds,
+                                            s.segs, s.weighted, S.nsamples, S.ra, S.rb),
+                torch::Tensor()};
+    }
+};
+
+// attention-weighted variant (hasFFNEdgeUpdate, common.h:835-894)
+struct AggregateNodeMulSumAttn : public torch::autograd::Function<AggregateNodeMulSumAttn> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor input_dense,
+                                 torch::Tensor value_graph, int64_t li) {
+        ctx->saved_data["li"] = li;
+        ctx->save_for_backward({value_graph, input_dense});
+        Slot s = slot(2 * li);
+        return aggregate_node_mul_sum_call(input_dense, s.off, s.cols, value_graph.contiguous(),
+                                           s.bounds, s.segs, true);
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto saved = ctx->get_saved_variables();
+        torch::Tensor value_graph = saved[0], X = saved[1];
+        torch::Tensor dZ = grad_outputs[0].contiguous();
+        const int64_t li = ctx->saved_data["li"].toInt();
+        Slot s = slot(2 * li + 1);
+        const int64_t nrows = s.off.numel() / s.segs - 1;
+        return {aggregate_node_mul_sum_call(dZ, s.off, s.cols, value_graph, s.bounds, s.segs, true),
+                edge_sddmm(dZ, X, s.off, s.cols, value_graph, s.bounds, nrows, s.segs),
+                torch::Tensor()};
+    }
+};
+
+// aggregate_edge_sum_AutoGrad (common.h:622-675)
+struct AggregateEdgeSum : public torch::autograd::Function<AggregateEdgeSum> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor in1, torch::Tensor in2,
+                                 int64_t li) {
+        ctx->saved_data["li"] = li;
+        Slot s = slot(2 * li);
+        const int64_t nrows = s.off.numel() / s.segs - 1;
+        return edge_sddvv(in1, in2, s.off, s.cols, s.vals, s.bounds, nrows, s.segs);
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        const int64_t li = ctx->saved_data["li"].toInt();
+        Slot s = slot(2 * li + 1);
+        const int64_t nrows = s.off.numel() / s.segs - 1;
+        auto back_res = node_spmv_backward_of_sddmm_eaggr(s.off, s.cols, grad_outputs[0], s.bounds,
+                                                          nrows, s.segs);
+        return {back_res, back_res, torch::Tensor()};
+    }
+};
+
+// non_lnr_op_softmax_AutoGrad (common.h:735-810), fused: one kernel per direction
+struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor value_graph, int64_t li) {
+        ctx->saved_data["li"] = li;
+        Slot s = slot(2 * li);
+        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        auto v = value_graph.contiguous();
+        check_dev(v, torch::kFloat, "value_graph");
+        auto alpha = torch::empty_like(v);
+        check(gala_edge_softmax_fwd_f32(&cv.c, v.data_ptr<float>(), 1, GALA_SOFTMAX_REF,
+                                        alpha.data_ptr<float>(), stream()),
+              "gala_edge_softmax_fwd_f32");
+        ctx->save_for_backward({alpha});
+        return alpha;
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        const int64_t li = ctx->saved_data["li"].toInt();
+        Slot s = slot(2 * li + 1);
+        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        auto alpha = ctx->get_saved_variables()[0];
+        auto d = grad_outputs[0].contiguous();
+        auto ds = torch::empty_like(alpha);
+        check(gala_edge_softmax_bwd_f32(&cv.c, alpha.data_ptr<float>(), d.data_ptr<float>(), 1,
+                                        GALA_SOFTMAX_REF, ds.data_ptr<float>(), stream()),
+              "gala_edge_softmax_bwd_f32");
+        return {ds, torch::Tensor()};
+    }
+};
+
+torch::Tensor permute_edges(const torch::Tensor &perm, const torch::Tensor &v, int heads) {
+    auto out = torch::empty_like(v);
+    check(gala_edge_permute_f32(perm.data_ptr<int32_t>(), v.data_ptr<float>(), perm.numel(), heads,
+                                out.data_ptr<float>(), stream()),
+          "gala_edge_permute_f32");
+    return out;
+}
+
+// fused GAT layer: sddvv + LeakyReLU + edge softmax + weighted aggregation in one pass
+struct GatAggregate : public torch::autograd::Function<GatAggregate> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor aL, torch::Tensor aR,
+                                 torch::Tensor X, int64_t li, double slope, int64_t mode) {
+        Slot s = slot(2 * li);
+        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        auto l = aL.contiguous(), r = aR.contiguous(), x = X.contiguous();
+        check_dev(l, torch::kFloat, "attn_l");
+        check_dev(r, torch::kFloat, "attn_r");
+        check_dev(x, torch::kFloat, "X");
+        const int64_t nrows = cv.c.n_rows, F = x.size(1);
+        const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
+        cv.c.n_cols = x.size(0);
+        auto Y = torch::empty({nrows, F}, fopts(x));
+        auto alpha = torch::empty({s.cols.numel() * heads}, fopts(x));
+        check(gala_gat_fwd_f32(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
+                               F, (int32_t)F, heads, (float)slope, (int32_t)mode,
+                               Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream()),
+              "gala_gat_fwd_f32");
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["slope"] = slope;
+        ctx->saved_data["mode"] = mode;
+        ctx->saved_data["heads"] = (int64_t)heads;
+        ctx->save_for_backward({l, r, x, alpha});
+        return Y;
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto sv = ctx->get_saved_variables();
+        auto l = sv[0], r = sv[1], x = sv[2], alpha = sv[3];
+        auto dY = grad_outputs[0].contiguous();
+        const int64_t li = ctx->saved_data["li"].toInt();
+        const double slope = ctx->saved_data["slope"].toDouble();
+        const int64_t mode = ctx->saved_data["mode"].toInt();
+        const int heads = (int)ctx->saved_data["heads"].toInt();
+        Slot fw = slot(2 * li), bw = slot(2 * li + 1);
+        const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
+        CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
+        cf.c.n_cols = x.size(0);
+        const bool fixed = mode == GALA_SOFTMAX_FIXED;
+        TORCH_CHECK(!fixed || bw.perm.defined(),
+                    "gala: FIXED-mode GAT backward needs the transposed graph and its edge "
+                    "permutation in slot 2*li+1 (transpose_perm)");
+        // dX: reference multiplies by alpha on slot 2li+1's pattern (common.h:876);
+        // FIXED: A^T with the transposed alpha
+        torch::Tensor alpha_b = fixed ? permute_edges(bw.perm, alpha, heads) : alpha;
+        torch::Tensor dX = spmm_impl(dY, bw.off, bw.cols, &alpha_b, bw.bounds, bw.segs, heads,
+                                     nullptr, nullptr, 0, 5, 7);
+        // d alpha_e = <dY_row, X_col> per head (edge_sddmm, cuda.h:808-845)
+        const Slot &ps = fixed ? fw : bw;
+        CsrView cp = view(ps.off, ps.cols, nullptr, ps.bounds, ps.segs);
+        cp.c.n_cols = x.size(0);
+        auto dalpha = torch::empty_like(alpha);
+        check(gala_sddmm_dot_f32(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
+                                 (int32_t)F, heads, dalpha.data_ptr<float>(), stream()),
+              "gala_sddmm_dot_f32");
+        auto ds = torch::empty_like(alpha);
+        check(gala_edge_softmax_bwd_f32(&cp.c, alpha.data_ptr<float>(), dalpha.data_ptr<float>(),
+                                        heads, (int32_t)mode, ds.data_ptr<float>(), stream()),
+              "gala_edge_softmax_bwd_f32");
+        // LeakyReLU backward on the recomputed logits z = aL[row] + aR[col]
+        auto z = torch::empty_like(alpha);
+        check(gala_sddvv_f32(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(), heads,
+                             GALA_SDDVV_ADD, 0.0f, z.data_ptr<float>(), stream()),
+              "gala_sddvv_f32");
+        auto dz = torch::where(z > 0, ds, ds * slope).contiguous();
+        torch::Tensor daL, daR;
+        if (!fixed) {
+            // reference: d aL = d aR = K7(ds) on slot 2li+1 (common.h:662-667)
+            daL = row_sum_impl(bw.off, bw.cols, dz, bw.bounds, nrows, bw.segs, 1e-12f);
+            daR = daL;
+        } else {
+            daL = row_sum_impl(fw.off, fw.cols, dz, fw.bounds, nrows, fw.segs, 0.0f);
+            auto dzT = permute_edges(bw.perm, dz, heads);
+            daR = row_sum_impl(bw.off, bw.cols, dzT, bw.bounds, bw.off.numel() / bw.segs - 1,
+                               bw.segs, 0.0f);
+        }
+        return {daL.view_as(l), daR.view_as(r), dX, torch::Tensor(), torch::Tensor(),
+                torch::Tensor()};
+    }
+};
+
+}  // namespace
+
+torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li) {
+    return AggregateNodeMulSum::apply(input_dense, li);
+}
+torch::Tensor aggregate_node_mul_sum_attn_apply(torch::Tensor input_dense,
+                                                torch::Tensor value_graph, int64_t li) {
+    return AggregateNodeMulSumAttn::apply(input_dense, value_graph, li);
+}
+torch::Tensor aggregate_edge_sum_apply(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                       int64_t li) {
+    return AggregateEdgeSum::apply(input_dense1, input_dense2, li);
+}
+torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li) {
+    return NonLnrOpSoftmax::apply(value_graph, li);
+}
+torch::Tensor gat_aggregate_apply(torch::Tensor attn_l, torch::Tensor attn_r, torch::Tensor X,
+                                  int64_t li, double slope, int64_t mode) {
+    return GatAggregate::apply(attn_l, attn_r, X, li, slope, mode);
+}
+
+}  // namespace gala

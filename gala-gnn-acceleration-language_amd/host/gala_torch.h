@@ -1,0 +1,116 @@
+// gala_torch.h — C++/libtorch mirror of the operator API GALA's code generator emits
+// into gala.cu, implemented over the C ABI of libgala_hip.so (include/gala_hip.h).
+//
+// A generated program (or the HIP emitter that replaces src/codegen/cuda.h) calls these
+// with exactly the names, argument order and argument meaning of the emitted functions:
+//   <aggregate_node_mul_sum[_direct]>_call     src/codegen/cuda.h:441-502 (gala.cu:227-390)
+//   gather_forward (cuSPARSE weighted path)      src/codegen/cuda.h:211-279
+//   node_spmv_backward_of_sddmm_{nln,eaggr}      src/codegen/cuda.h:565-600, 737-772
+//   inplace_softmax_sddvv[_mult]                 src/codegen/cuda.h:601-656
+//   edge_sddvv / edge_sddmm                      src/codegen/cuda.h:773-845
+//   aggregate_edge_mul / aggregate_edge_mul_dir  src/codegen/cuda.h:870-952
+// and the emitted autograd Functions (src/codegen/common.h:622-1084, gala.cu:391-414).
+// The `_coarse{C}` suffixes of the emitted names select CUDA launch geometry only; the
+// gfx950 kernels pick their own geometry, so every suffix maps to the same function.
+//
+// Differences from the reference, all deliberate:
+//   - errors throw c10::Error (TORCH_CHECK) instead of exit(EXIT_FAILURE);
+//   - every kernel runs on the caller's current HIP stream (no leaked per-launch streams);
+//   - column-tiled segments are summed in order (no inter-stream race on the output);
+//   - the softmax backward does not overwrite the saved forward alpha in place.
+#pragma once
+
+#include <torch/torch.h>
+
+#include <string>
+#include <vector>
+
+#include "gala_hip.h"
+
+namespace gala {
+
+// The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's
+// forward graph, slot 2*li+1 its backward graph (the same tensors for undirected graphs,
+// cuda.h:1253-1257).  `bounds` stay on the host like the reference's total_bounds.
+struct GraphSlots {
+    std::vector<torch::Tensor> offset_graph, columns_graph, value_graph, bounds;
+    std::vector<int> segments;
+    std::vector<bool> weighted;
+    std::vector<torch::Tensor> transpose_perm;  // optional: edge k of slot == edge perm[k] of forward
+    int64_t nrows = 0;
+    int ra = 5, rb = 7;    // kernel-sampling coefficients (common.h:813-833)
+    int nsamples = 0;      // 0 = no kernel sampling
+
+    int push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor vals, torch::Tensor bounds,
+             int segments, bool weighted);
+    void clear();
+};
+GraphSlots &global_slots();
+
+// ---- emitted free functions ------------------------------------------------------------
+torch::Tensor aggregate_node_mul_sum_call(torch::Tensor input_dense, torch::Tensor offset_graph,
+                                          torch::Tensor columns_graph, torch::Tensor value_graph,
+                                          torch::Tensor bounds = {}, int64_t segments = 1,
+                                          bool weighted = false, int64_t nsamples = 0,
+                                          int64_t ra = 5, int64_t rb = 7);
+torch::Tensor aggregate_node_mul_sum_direct_call(torch::Tensor input_dense,
+                                                 torch::Tensor offset_graph,
+                                                 torch::Tensor columns_graph,
+                                                 torch::Tensor value_graph,
+                                                 torch::Tensor bounds = {}, int64_t segments = 1,
+                                                 bool weighted = false);
+torch::Tensor gather_forward(torch::Tensor input_dense, torch::Tensor offset_graph,
+                             torch::Tensor columns_graph, torch::Tensor value_graph);
+torch::Tensor node_spmv_backward_of_sddmm_nln(torch::Tensor offset_graph,
+                                              torch::Tensor columns_graph,
+                                              torch::Tensor value_graph, torch::Tensor bounds,
+                                              int64_t nrows, int64_t segments);
+torch::Tensor node_spmv_backward_of_sddmm_eaggr(torch::Tensor offset_graph,
+                                                torch::Tensor columns_graph,
+                                                torch::Tensor value_graph, torch::Tensor bounds,
+                                                int64_t nrows, int64_t segments);
+torch::Tensor inplace_softmax_sddvv(torch::Tensor row_val, torch::Tensor offset_graph,
+                                    torch::Tensor columns_graph, torch::Tensor value_graph,
+                                    torch::Tensor bounds, int64_t nrows, int64_t segments);
+torch::Tensor inplace_softmax_sddvv_mult(torch::Tensor row_val, torch::Tensor offset_graph,
+                                         torch::Tensor columns_graph, torch::Tensor value_graph,
+                                         torch::Tensor bounds, int64_t nrows, int64_t segments);
+torch::Tensor edge_sddvv(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                         torch::Tensor offset_graph, torch::Tensor columns_graph,
+                         torch::Tensor value_graph, torch::Tensor bounds, int64_t nrows,
+                         int64_t segments);
+torch::Tensor edge_sddmm(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                         torch::Tensor offset_graph, torch::Tensor columns_graph,
+                         torch::Tensor value_graph, torch::Tensor bounds, int64_t nrows,
+                         int64_t segments);
+torch::Tensor aggregate_edge_mul(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                 torch::Tensor offset_graph, torch::Tensor columns_graph,
+                                 torch::Tensor value_graph, torch::Tensor bounds,
+                                 int64_t segments);
+torch::Tensor aggregate_edge_mul_dir(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                     torch::Tensor offset_graph, torch::Tensor columns_graph,
+                                     torch::Tensor value_graph);
+
+// ---- fused ops (no reference counterpart: one kernel for a reference op chain) ---------
+// norm * A (norm * X): the GCN aggregation with both ROW_BROADCASTs (gala.cu:442-456)
+torch::Tensor gcn_aggregate(torch::Tensor X, torch::Tensor norm, torch::Tensor offset_graph,
+                            torch::Tensor columns_graph, torch::Tensor bounds = {},
+                            int64_t segments = 1);
+torch::Tensor row_broadcast(torch::Tensor scale, torch::Tensor X);
+torch::Tensor degree_norm(torch::Tensor offset_graph, torch::Tensor bounds, int64_t segments,
+                          double power);
+
+// ---- emitted autograd Functions (apply() wrappers; li = layer index into the slots) ---
+torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li);
+torch::Tensor aggregate_node_mul_sum_attn_apply(torch::Tensor input_dense,
+                                                torch::Tensor value_graph, int64_t li);
+torch::Tensor aggregate_edge_sum_apply(torch::Tensor input_dense1, torch::Tensor input_dense2,
+                                       int64_t li);
+torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li);
+// Fused GAT aggregation with autograd (mode GALA_SOFTMAX_REF reproduces the reference's
+// forward and backward chain, GALA_SOFTMAX_FIXED the mathematically correct gradients,
+// using the slot's transposed graph).
+torch::Tensor gat_aggregate_apply(torch::Tensor attn_l, torch::Tensor attn_r, torch::Tensor X,
+                                  int64_t li, double slope, int64_t mode);
+
+}  // namespace gala

@@ -245,3 +245,31 @@ def test_invalid_args_fail_loudly():
         _abi.call("gala_spmm_f32", dg.csr(), X.data_ptr(), 4, X.data_ptr(), 8, 8, None, None, 0, 0, 0, 0, None)
     with pytest.raises(ValueError):
         ops.spmm(dg, torch.ones(g.n_cols, 8))
+
+
+# ---- against the reference's own outputs (tests/golden, generated from /root/reference)
+import glob as _glob  # noqa: E402
+import os as _os  # noqa: E402
+
+_GOLDEN = sorted(_glob.glob(_os.path.join(_os.path.dirname(__file__), "golden", "*.npz")))
+
+
+@pytest.mark.parametrize("path", _GOLDEN, ids=[_os.path.basename(p)[:-4] for p in _GOLDEN])
+def test_spmm_matches_reference_gspmm_fixtures(path):
+    fx = dict(np.load(path, allow_pickle=False))
+    n = int(fx["n"])
+    g = layout.HostGraph(n, n, fx["rowptr"], fx["col"])
+    dg = ops.DeviceGraph.from_host(g)
+    for k in [k for k in fx if k.startswith("Y_F") or k.startswith("Yw_F")]:
+        F = int(k.split("_F")[1])
+        X = dev(np.ascontiguousarray(fx["X"][:, :F]))
+        gg = dg if k.startswith("Y_") else dg.with_values(dev(fx["w"]))
+        np.testing.assert_array_equal(host(ops.spmm(gg, X)), fx[k], err_msg=k)
+    # tiled layouts from ord_col_tiling_torch give the same aggregation
+    for k in [k for k in fx if k.startswith("tile") and k.endswith("_rowptr")]:
+        cpp = k[4:-len("_rowptr")]
+        bounds = fx[f"tile{cpp}_bounds"]
+        t = layout.HostGraph(n, n, fx[k], fx[f"tile{cpp}_col"], None, len(bounds) // 2, bounds)
+        F = min(int(k2[3:]) for k2 in fx if k2.startswith("Y_F"))
+        X = dev(np.ascontiguousarray(fx["X"][:, :F]))
+        np.testing.assert_array_equal(host(ops.spmm(ops.DeviceGraph.from_host(t), X)), fx[f"Y_F{F}"])

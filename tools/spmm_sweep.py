@@ -67,6 +67,16 @@ def main():
         if "sddmm" in todo:
             ms = timeit(lambda: ops.sddmm(dg, X, X))
             print(json.dumps({"op": "sddmm", "F": F, "ms": ms, "edges_per_s": E / ms * 1e3, "alg_GBps": (4 * (N + 1) + 8 * E + 8 * N * F) / ms / 1e6}), flush=True)
+    if "rocsparse" in todo:
+        # vendor reference point: torch.sparse CSR matmul -> hipSPARSE/rocSPARSE SpMM
+        A = torch.sparse_csr_tensor(dg.rowptr, dg.col, torch.ones(E, device="cuda"), size=(N, N))
+        for F in [int(f) for f in args.F.split(",")]:
+            X = torch.rand((N, F), device="cuda")
+            try:
+                ms = timeit(lambda: torch.sparse.mm(A, X), reps=5)
+                print(json.dumps({"op": "rocsparse_spmm", "F": F, "ms": ms, "edges_per_s": E / ms * 1e3}), flush=True)
+            except Exception as e:
+                print(json.dumps({"op": "rocsparse_spmm", "F": F, "error": repr(e)[:200]}), flush=True)
     if "degree" in todo:
         ms = timeit(lambda: ops.degree(dg, power=-0.5))
         print(json.dumps({"op": "degree", "ms": ms, "alg_GBps": (4 * (N + 1) + 4 * N) / ms / 1e6}), flush=True)
