@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Per-config hot-path timings for BASELINE.json's other configs (not the headline line).
+
+  arxiv   ogbn-arxiv-shaped GCN-2, hidden 128: N=169,343, E=1,335,586 stored edges,
+          4 norm-scaled F=128 aggregations per step (same step definition as bench.py)
+  gat     ogbn-products-shaped GAT layer, 8 heads x D=32 (F=256) and 1 head x D=47:
+          fused forward (logits + LeakyReLU + edge softmax + aggregation) and the
+          autograd backward (REF chain and FIXED exact gradients)
+  reddit  Reddit-shaped GraphSAGE aggregation with kernel sampling sample(20):
+          N=232,965, E=114,615,892 (R-MAT power law), F=256, nsamp=20, ra=5, rb=7
+Prints one JSON line per measurement (median of HIP-event timed reps).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gala-gnn-acceleration-language_amd"))
+import gala  # noqa: E402
+from gala import layout, ops  # noqa: E402
+
+
+def timeit(fn, reps=10, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts)) / 1e3
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def gcn_step(name, hg, F):
+    dg = ops.DeviceGraph.from_host(hg)
+    N, E = hg.n_rows, hg.nnz
+    X = torch.rand((N, F), device="cuda") * 2 - 1
+    bufs = [torch.empty_like(X) for _ in range(5)]
+
+    def step():
+        norm = ops.degree(dg, power=-0.5)
+        src = X
+        for dst in bufs[1:]:
+            ops.row_broadcast(norm, src, out=bufs[0])
+            ops.spmm(dg, bufs[0], dst_scale=norm, out=dst)
+            src = dst
+    t = timeit(step)
+    norm = ops.degree(dg, power=-0.5)
+    tk = timeit(lambda: ops.spmm(dg, bufs[0], dst_scale=norm, out=bufs[1]), reps=20)
+    alg = 4 * (N + 1) + 4 * E + 8 * N * F + 4 * N
+    emit(config=name, op="gcn2_step", ms=t * 1e3, edges_per_s=4 * E / t, N=N, E=E, F=F)
+    emit(config=name, op="spmm_kernel", ms=tk * 1e3, edges_per_s=E / tk, alg_GBps=alg / tk / 1e9,
+         roofline_frac=alg / tk / 8e12)
+
+
+def gat(hg):
+    E_ = gala.torch_ext()
+    N, E = hg.n_rows, hg.nnz
+    off = torch.from_numpy(hg.rowptr).cuda()
+    cols = torch.from_numpy(hg.col).cuda()
+    t0 = time.time()
+    tg, perm = layout.transpose(hg)
+    print(f"transpose {time.time()-t0:.1f}s", file=sys.stderr, flush=True)
+    E_.slots_clear()
+    E_.slots_push(off, cols, None, None, 1, False)
+    E_.slots_push(torch.from_numpy(tg.rowptr).cuda(), torch.from_numpy(tg.col).cuda(), None, None, 1, False)
+    E_.slots_set_transpose_perm(1, torch.from_numpy(perm).cuda())
+    dg = ops.DeviceGraph.from_host(hg)
+    for heads, D in ((8, 32), (1, 47), (1, 32)):
+        F = heads * D
+        aL = torch.rand((N, heads), device="cuda")
+        aR = torch.rand((N, heads), device="cuda")
+        X = torch.rand((N, F), device="cuda")
+        tf = timeit(lambda: ops.gat_fwd(dg, aL, aR, X, heads=heads, want_alpha=True), reps=5)
+        emit(config="products_gat", op="gat_fwd_fused", heads=heads, D=D, ms=tf * 1e3, edges_per_s=E / tf)
+        for mode in (0, 1):
+            l = aL.clone().requires_grad_()
+            r = aR.clone().requires_grad_()
+            x = X.clone().requires_grad_()
+
+            def fb():
+                Y = E_.gat_aggregate_apply(l, r, x, 0, 0.2, mode)
+                Y.backward(torch.ones_like(Y))
+            t = timeit(fb, reps=5, warm=2)
+            emit(config="products_gat", op="gat_layer_fwd_bwd", mode=["REF", "FIXED"][mode], heads=heads,
+                 D=D, ms=t * 1e3, edges_per_s=E / t)
+        s = torch.rand(E * heads, device="cuda")
+        emit(config="products_gat", op="sddvv_lrelu", heads=heads,
+             ms=timeit(lambda: ops.sddvv(dg, aL, aR, op=2, heads=heads)) * 1e3)
+        emit(config="products_gat", op="edge_softmax_fwd", heads=heads,
+             ms=timeit(lambda: ops.edge_softmax(dg, s, heads=heads)) * 1e3)
+        emit(config="products_gat", op="sddmm", heads=heads, F=F,
+             ms=timeit(lambda: ops.sddmm(dg, X, X, heads=heads)) * 1e3)
+        gw = dg.with_values(s, val_heads=heads)
+        emit(config="products_gat", op="weighted_spmm", heads=heads, F=F,
+             ms=timeit(lambda: ops.spmm(gw, X)) * 1e3)
+
+
+def reddit(hg):
+    dg = ops.DeviceGraph.from_host(hg)
+    N, E = hg.n_rows, hg.nnz
+    deg = hg.degrees()
+    F = 256
+    X = torch.rand((N, F), device="cuda")
+    t = timeit(lambda: ops.spmm(dg, X, nsamp=20, ra=5, rb=7))
+    alg = 4 * (N + 1) + 4 * N * 20 + 8 * N * F
+    emit(config="reddit_sage", op="spmm_kernel_sampled_n20", ms=t * 1e3, sampled_edges_per_s=N * 20 / t,
+         alg_GBps=alg / t / 1e9, roofline_frac=alg / t / 8e12, deg_max=int(deg.max()), deg_mean=float(deg.mean()))
+    t = timeit(lambda: ops.spmm(dg, X), reps=3, warm=1)
+    emit(config="reddit_sage", op="spmm_full_F256", ms=t * 1e3, edges_per_s=E / t)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="arxiv,gat,reddit")
+    a = ap.parse_args()
+    w = a.which.split(",")
+    if "arxiv" in w:
+        gcn_step("arxiv_gcn", layout.gen_graph("uniform", 169_343, (1_335_586 - 169_343) // 2, seed=42), 128)
+    if "gat" in w:
+        gat(layout.gen_graph("uniform", 2_449_029, 61_859_140, seed=42))
+    if "reddit" in w:
+        reddit(layout.gen_graph("rmat", 232_965, (114_615_892 - 232_965) // 2, seed=42))
+
+
+if __name__ == "__main__":
+    main()
