@@ -11,6 +11,8 @@
 // edges (coalesced edge arrays), reductions use xor butterflies inside the group.
 #include <stddef.h>
 
+#include <algorithm>
+
 #include "gala_internal.h"
 
 namespace gala {
@@ -39,9 +41,182 @@ __device__ __forceinline__ void row_range(const EdgeParams &p, int s, int64_t ro
                             * (kWave / (G)) + lane / (G);                             \
     const bool row_ok = row < p.n_rows;
 
+// ---- row-segment edge ops over flattened (edge, head) elements ----------------------
+// With HP heads (a power of two dividing G) the row's HP*deg edge values are contiguous,
+// lane g always handles head g % HP, and per-head reductions run over the xor offsets
+// G/2 .. HP.  Non-power-of-two head counts use the *_generic kernels further down.
+template <int G, int HP>
+__device__ __forceinline__ float head_sum(float v) {
+#pragma unroll
+    for (int o = G / 2; o >= HP; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+template <int G, int HP>
+__device__ __forceinline__ float head_max(float v) {
+#pragma unroll
+    for (int o = G / 2; o >= HP; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+template <int G, int HP, int OP>
+__global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, const float *b,
+                                                  float slope, float *out) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    constexpr int LH = __builtin_ctz(HP);
+    const int h = gl & (HP - 1);
+    const float av = a[row * HP + h];
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int64_t n = (e1 - e0) << LH;
+        for (int64_t t = gl; t < n; t += G) {
+            const int64_t e = e0 + (t >> LH);
+            const float bv = b[((int64_t)p.col[e] << LH) + h];
+            float r;
+            if (OP == GALA_SDDVV_MUL) {
+                r = __fmul_rn(av, bv);
+            } else {
+                r = __fadd_rn(av, bv);
+                if (OP == GALA_SDDVV_ADD_LRELU) r = r > 0.0f ? r : __fmul_rn(r, slope);
+            }
+            out[(e0 << LH) + t] = r;
+        }
+    }
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
+                                                    int accum, float *out) {
+    GALA_ROW_PROLOGUE(G);
+    constexpr int LH = __builtin_ctz(HP);
+    float part = 0.0f;
+    if (row_ok) {
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            const int64_t n = (e1 - e0) << LH;
+            const float *vr = v + (e0 << LH);
+            for (int64_t t = gl; t < n; t += G) part += vr[t];
+        }
+    }
+    part = head_sum<G, HP>(part);
+    if (row_ok && gl < HP) {
+        // reference: each segment's sum starts at 1e-12 (cuda.h:512,666)
+        float r = part + (float)p.seg.n * eps;
+        if (accum) r = out[row * HP + gl] + r;
+        out[row * HP + gl] = r;
+    }
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float *q, float *v) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    constexpr int LH = __builtin_ctz(HP);
+    const float qv = q[row * HP + (gl & (HP - 1))];
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int64_t n = (e1 - e0) << LH;
+        float *vr = v + (e0 << LH);
+        for (int64_t t = gl; t < n; t += G) vr[t] = __fmul_rn(vr[t], qv);
+    }
+}
+
+__device__ __forceinline__ float ref_exp(float s) {
+    // torch::exp then torch::clamp(0, 1e12) (common.h:760-761); NaN propagates like clamp
+    const float p = expf(s);
+    return p > 1e12f ? 1e12f : p;
+}
+
+template <int G, int HP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const float *logit,
+                                                        float *alpha) {
+    GALA_ROW_PROLOGUE(G);
+    constexpr int LH = __builtin_ctz(HP);
+    float m = -INFINITY, sum = 0.0f;
+    if (row_ok) {
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            const int64_t n = (e1 - e0) << LH;
+            const float *lr = logit + (e0 << LH);
+            for (int64_t t = gl; t < n; t += G) {
+                const float x = lr[t];
+                if (MODE == GALA_SOFTMAX_REF) {
+                    sum += ref_exp(x);
+                } else if (x > m) {  // online max / sum
+                    sum = sum * expf(m - x) + 1.0f;
+                    m = x;
+                } else {
+                    sum += expf(x - m);
+                }
+            }
+        }
+    }
+    float q;
+    if (MODE == GALA_SOFTMAX_REF) {
+        sum = head_sum<G, HP>(sum);
+        q = 1.0f / (sum + (float)p.seg.n * 1e-12f);  // torch::reciprocal(row_sum)
+    } else {
+        const float gm = head_max<G, HP>(m);
+        sum = (m == -INFINITY) ? 0.0f : sum * expf(m - gm);
+        sum = head_sum<G, HP>(sum);
+        m = gm;
+        q = 1.0f / sum;
+    }
+    if (!row_ok) return;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int64_t n = (e1 - e0) << LH;
+        const float *lr = logit + (e0 << LH);
+        float *ar = alpha + (e0 << LH);
+        for (int64_t t = gl; t < n; t += G) {
+            const float x = lr[t];
+            const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x) : expf(x - m);
+            ar[t] = __fmul_rn(pe, q);
+        }
+    }
+}
+
+template <int G, int HP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const float *alpha,
+                                                        const float *dalpha, float *dlogit) {
+    GALA_ROW_PROLOGUE(G);
+    constexpr int LH = __builtin_ctz(HP);
+    const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
+    float part = 0.0f;
+    if (row_ok) {
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            const int64_t n = (e1 - e0) << LH;
+            const int64_t o = e0 << LH;
+            for (int64_t t = gl; t < n; t += G) part += __fmul_rn(alpha[o + t], dalpha[o + t]);
+        }
+    }
+    part = head_sum<G, HP>(part);
+    const float acc = part + (float)p.seg.n * eps;  // K7 on sds (common.h:793-794)
+    if (!row_ok) return;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int64_t n = (e1 - e0) << LH;
+        const int64_t o = e0 << LH;
+        for (int64_t t = gl; t < n; t += G) {
+            const float a = alpha[o + t];
+            const float sds = __fmul_rn(a, dalpha[o + t]);
+            dlogit[o + t] = __fsub_rn(sds, __fmul_rn(a, acc));  // sds - K8(acc)
+        }
+    }
+}
+
+// ---- generic-heads variants (runtime head count, per-head passes) ---------------------
 // ---- SDDVV --------------------------------------------------------------------------
 template <int G, int OP>
-__global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, const float *b,
+__global__ __launch_bounds__(kBlock) void k_sddvv_generic(EdgeParams p, const float *a, const float *b,
                                                   float slope, float *out) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
@@ -69,7 +244,7 @@ __global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, 
 
 // ---- edge -> row sum (K7) ----------------------------------------------------------
 template <int G>
-__global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
+__global__ __launch_bounds__(kBlock) void k_row_sum_generic(EdgeParams p, const float *v, float eps,
                                                     int accum, float *out) {
     GALA_ROW_PROLOGUE(G);
     const int H = p.heads;
@@ -94,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
 
 // ---- row -> edge scale (K8) --------------------------------------------------------
 template <int G>
-__global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float *q, float *v) {
+__global__ __launch_bounds__(kBlock) void k_row_scale_generic(EdgeParams p, const float *q, float *v) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
     const int H = p.heads;
@@ -110,14 +285,9 @@ __global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float 
 }
 
 // ---- edge softmax -------------------------------------------------------------------
-__device__ __forceinline__ float ref_exp(float s) {
-    // torch::exp then torch::clamp(0, 1e12) (common.h:760-761); NaN propagates like clamp
-    const float p = expf(s);
-    return p > 1e12f ? 1e12f : p;
-}
 
 template <int G, int MODE>
-__global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const float *logit,
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd_generic(EdgeParams p, const float *logit,
                                                         float *alpha) {
     GALA_ROW_PROLOGUE(G);
     const int H = p.heads;
@@ -167,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
 }
 
 template <int G, int MODE>
-__global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const float *alpha,
+__global__ __launch_bounds__(kBlock) void k_softmax_bwd_generic(EdgeParams p, const float *alpha,
                                                         const float *dalpha, float *dlogit) {
     GALA_ROW_PROLOGUE(G);
     const int H = p.heads;
@@ -351,21 +521,42 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
         *reinterpret_cast<V *>(Y + row * ldy + fo) = out;
     }
     if (alpha_out) {
-        // lanes stride over the row's edges; head h's (m, q) live in lane h*D/VEC of the group
+        // alpha pass: lanes stride the row's contiguous (edge, head) values.  When H divides
+        // G every lane keeps one head (g % H) whose (m, q) live in lane (h*D)/VEC of the group.
         const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
-        for (int s = 0; s < p.seg.n; ++s) {
-            int64_t e0, e1;
-            row_range(p, s, row, e0, e1);
-            for (int hd = 0; hd < H; ++hd) {
-                const int src = gbase + (hd * D) / VEC;
-                const float mh = __shfl(m, src, 64);
-                const float qh = __shfl(q, src, 64);
-                const float alh = aL[row * H + hd];
-                for (int64_t e = e0 + gl; e < e1; e += G) {
-                    float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + hd]);
+        if (G % H == 0) {
+            const int h = gl % H;
+            const int src = gbase + (h * D) / VEC;
+            const float mh = __shfl(m, src, 64);
+            const float qh = __shfl(q, src, 64);
+            const float alh = aL[row * H + h];
+            for (int s = 0; s < p.seg.n; ++s) {
+                int64_t e0, e1;
+                row_range(p, s, row, e0, e1);
+                const int64_t n = (e1 - e0) * H;
+                for (int64_t t = gl; t < n; t += G) {
+                    const int64_t e = e0 + t / H;
+                    float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + h]);
                     z = z > 0.0f ? z : __fmul_rn(z, slope);
                     const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
-                    alpha_out[e * H + hd] = __fmul_rn(pe, qh);
+                    alpha_out[e0 * H + t] = __fmul_rn(pe, qh);
+                }
+            }
+        } else {
+            for (int s = 0; s < p.seg.n; ++s) {
+                int64_t e0, e1;
+                row_range(p, s, row, e0, e1);
+                for (int hd = 0; hd < H; ++hd) {
+                    const int src = gbase + (hd * D) / VEC;
+                    const float mh = __shfl(m, src, 64);
+                    const float qh = __shfl(q, src, 64);
+                    const float alh = aL[row * H + hd];
+                    for (int64_t e = e0 + gl; e < e1; e += G) {
+                        float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + hd]);
+                        z = z > 0.0f ? z : __fmul_rn(z, slope);
+                        const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
+                        alpha_out[e * H + hd] = __fmul_rn(pe, qh);
+                    }
                 }
             }
         }
@@ -417,6 +608,28 @@ static unsigned blocks_for(int64_t n_rows, int G) {
         default: { constexpr int GG = 64; __VA_ARGS__; } break; \
     }
 
+// heads as a compile-time power of two (0 = not supported by the flattened kernels)
+static int pow2_heads(int heads) {
+    return (heads == 1 || heads == 2 || heads == 4 || heads == 8 || heads == 16) ? heads : 0;
+}
+
+#define GALA_CASE_HP(GV, ...)                                                              \
+    switch (hp) {                                                                          \
+        case 1: { constexpr int GG = GV, HH = 1; __VA_ARGS__; } break;                     \
+        case 2: { constexpr int GG = GV, HH = (2 <= GV ? 2 : GV); __VA_ARGS__; } break;    \
+        case 4: { constexpr int GG = GV, HH = (4 <= GV ? 4 : GV); __VA_ARGS__; } break;    \
+        case 8: { constexpr int GG = GV, HH = (8 <= GV ? 8 : GV); __VA_ARGS__; } break;    \
+        default: { constexpr int GG = GV, HH = (16 <= GV ? 16 : GV); __VA_ARGS__; } break; \
+    }
+#define GALA_DISPATCH_GH(G, ...)                           \
+    switch (G) {                                           \
+        case 4: GALA_CASE_HP(4, __VA_ARGS__) break;        \
+        case 8: GALA_CASE_HP(8, __VA_ARGS__) break;        \
+        case 16: GALA_CASE_HP(16, __VA_ARGS__) break;      \
+        case 32: GALA_CASE_HP(32, __VA_ARGS__) break;      \
+        default: GALA_CASE_HP(64, __VA_ARGS__) break;      \
+    }
+
 }  // namespace gala
 
 using namespace gala;
@@ -430,19 +643,30 @@ extern "C" int gala_sddvv_f32(const gala_csr_t *A, const float *a_row, const flo
     if (op < GALA_SDDVV_ADD || op > GALA_SDDVV_ADD_LRELU) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
     if (!a_row || !b_col || !out_e) return GALA_ERR_INVALID_ARG;
-    const int G = pick_group(A, heads);
     hipStream_t hs = (hipStream_t)stream;
+    const int hp = pow2_heads(heads);
+    if (hp) {
+        const int G = std::max(pick_group(A, heads), hp);
+        const dim3 grid(blocks_for(A->n_rows, G));
+        GALA_DISPATCH_GH(G, {
+            if (op == GALA_SDDVV_ADD)
+                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_ADD>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+            else if (op == GALA_SDDVV_MUL)
+                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_MUL>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+            else
+                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_ADD_LRELU>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+        });
+        return launch_status();
+    }
+    const int G = pick_group(A, heads);
     GALA_DISPATCH_G(G, {
+        const dim3 grid(blocks_for(A->n_rows, GG));
         if (op == GALA_SDDVV_ADD)
-            hipLaunchKernelGGL((k_sddvv<GG, GALA_SDDVV_ADD>), dim3(blocks_for(A->n_rows, GG)),
-                               dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+            hipLaunchKernelGGL((k_sddvv_generic<GG, GALA_SDDVV_ADD>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
         else if (op == GALA_SDDVV_MUL)
-            hipLaunchKernelGGL((k_sddvv<GG, GALA_SDDVV_MUL>), dim3(blocks_for(A->n_rows, GG)),
-                               dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+            hipLaunchKernelGGL((k_sddvv_generic<GG, GALA_SDDVV_MUL>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
         else
-            hipLaunchKernelGGL((k_sddvv<GG, GALA_SDDVV_ADD_LRELU>),
-                               dim3(blocks_for(A->n_rows, GG)), dim3(kBlock), 0, hs, p, a_row,
-                               b_col, slope, out_e);
+            hipLaunchKernelGGL((k_sddvv_generic<GG, GALA_SDDVV_ADD_LRELU>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
     });
     return launch_status();
 }
@@ -455,11 +679,18 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
     if (flags & ~GALA_SPMM_ACCUM) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!out_row || (!v_e && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
-    const int G = pick_group(A, 1);
     const int accum = (flags & GALA_SPMM_ACCUM) ? 1 : 0;
-    GALA_DISPATCH_G(G, hipLaunchKernelGGL((k_row_sum<GG>), dim3(blocks_for(A->n_rows, GG)),
-                                          dim3(kBlock), 0, (hipStream_t)stream, p, v_e, eps,
-                                          accum, out_row));
+    hipStream_t hs = (hipStream_t)stream;
+    const int hp = pow2_heads(heads);
+    if (hp) {
+        const int G = std::max(pick_group(A, heads), hp);
+        const dim3 grid(blocks_for(A->n_rows, G));
+        GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row));
+        return launch_status();
+    }
+    const int G = pick_group(A, 1);
+    GALA_DISPATCH_G(G, hipLaunchKernelGGL((k_row_sum_generic<GG>), dim3(blocks_for(A->n_rows, GG)),
+                                          dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row));
     return launch_status();
 }
 
@@ -470,10 +701,17 @@ extern "C" int gala_row_scale_f32(const gala_csr_t *A, const float *q_row, int32
     if (st) return st;
     if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
     if (!q_row || !v_inout) return GALA_ERR_INVALID_ARG;
+    hipStream_t hs = (hipStream_t)stream;
+    const int hp = pow2_heads(heads);
+    if (hp) {
+        const int G = std::max(pick_group(A, heads), hp);
+        const dim3 grid(blocks_for(A->n_rows, G));
+        GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_scale<GG, HH>), grid, dim3(kBlock), 0, hs, p, q_row, v_inout));
+        return launch_status();
+    }
     const int G = pick_group(A, heads);
-    GALA_DISPATCH_G(G, hipLaunchKernelGGL((k_row_scale<GG>), dim3(blocks_for(A->n_rows, GG)),
-                                          dim3(kBlock), 0, (hipStream_t)stream, p, q_row,
-                                          v_inout));
+    GALA_DISPATCH_G(G, hipLaunchKernelGGL((k_row_scale_generic<GG>), dim3(blocks_for(A->n_rows, GG)),
+                                          dim3(kBlock), 0, hs, p, q_row, v_inout));
     return launch_status();
 }
 
@@ -486,17 +724,26 @@ extern "C" int gala_edge_softmax_fwd_f32(const gala_csr_t *A, const float *logit
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
     if (!logits || !alpha) return GALA_ERR_INVALID_ARG;
-    const int G = pick_group(A, 1);
     hipStream_t hs = (hipStream_t)stream;
+    const int hp = pow2_heads(heads);
+    if (hp) {
+        const int G = std::max(pick_group(A, heads), hp);
+        const dim3 grid(blocks_for(A->n_rows, G));
+        GALA_DISPATCH_GH(G, {
+            if (mode == GALA_SOFTMAX_REF)
+                hipLaunchKernelGGL((k_softmax_fwd<GG, HH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
+            else
+                hipLaunchKernelGGL((k_softmax_fwd<GG, HH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
+        });
+        return launch_status();
+    }
+    const int G = pick_group(A, 1);
     GALA_DISPATCH_G(G, {
+        const dim3 grid(blocks_for(A->n_rows, GG));
         if (mode == GALA_SOFTMAX_REF)
-            hipLaunchKernelGGL((k_softmax_fwd<GG, GALA_SOFTMAX_REF>),
-                               dim3(blocks_for(A->n_rows, GG)), dim3(kBlock), 0, hs, p, logits,
-                               alpha);
+            hipLaunchKernelGGL((k_softmax_fwd_generic<GG, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
         else
-            hipLaunchKernelGGL((k_softmax_fwd<GG, GALA_SOFTMAX_FIXED>),
-                               dim3(blocks_for(A->n_rows, GG)), dim3(kBlock), 0, hs, p, logits,
-                               alpha);
+            hipLaunchKernelGGL((k_softmax_fwd_generic<GG, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
     });
     return launch_status();
 }
@@ -510,17 +757,26 @@ extern "C" int gala_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
     if (!alpha || !d_alpha || !d_logits) return GALA_ERR_INVALID_ARG;
-    const int G = pick_group(A, 1);
     hipStream_t hs = (hipStream_t)stream;
+    const int hp = pow2_heads(heads);
+    if (hp) {
+        const int G = std::max(pick_group(A, heads), hp);
+        const dim3 grid(blocks_for(A->n_rows, G));
+        GALA_DISPATCH_GH(G, {
+            if (mode == GALA_SOFTMAX_REF)
+                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
+            else
+                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
+        });
+        return launch_status();
+    }
+    const int G = pick_group(A, 1);
     GALA_DISPATCH_G(G, {
+        const dim3 grid(blocks_for(A->n_rows, GG));
         if (mode == GALA_SOFTMAX_REF)
-            hipLaunchKernelGGL((k_softmax_bwd<GG, GALA_SOFTMAX_REF>),
-                               dim3(blocks_for(A->n_rows, GG)), dim3(kBlock), 0, hs, p, alpha,
-                               d_alpha, d_logits);
+            hipLaunchKernelGGL((k_softmax_bwd_generic<GG, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
         else
-            hipLaunchKernelGGL((k_softmax_bwd<GG, GALA_SOFTMAX_FIXED>),
-                               dim3(blocks_for(A->n_rows, GG)), dim3(kBlock), 0, hs, p, alpha,
-                               d_alpha, d_logits);
+            hipLaunchKernelGGL((k_softmax_bwd_generic<GG, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
     });
     return launch_status();
 }

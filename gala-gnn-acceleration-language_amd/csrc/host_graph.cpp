@@ -231,3 +231,32 @@ extern "C" int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected
     }
     return GALA_OK;
 }
+
+extern "C" int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshold,
+                                    int32_t chunk, int32_t *rows, int32_t *row_chunk0,
+                                    int32_t *chunk_row, int64_t *n_rows_split,
+                                    int64_t *n_chunks) {
+    if (n_rows < 0 || !rowptr || threshold < 1 || chunk < 1 || !n_rows_split || !n_chunks)
+        return GALA_ERR_INVALID_ARG;
+    const bool fill = rows != nullptr;
+    if (fill && (!row_chunk0 || !chunk_row)) return GALA_ERR_INVALID_ARG;
+    int64_t cnt = 0, chunks = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t deg = (int64_t)rowptr[r + 1] - rowptr[r];
+        if (deg < 0) return GALA_ERR_GRAPH;
+        if (deg <= threshold) continue;
+        const int64_t nc = (deg + chunk - 1) / chunk;
+        if (fill) {
+            rows[cnt] = (int32_t)r;
+            row_chunk0[cnt] = (int32_t)chunks;
+            for (int64_t k = 0; k < nc; ++k) chunk_row[chunks + k] = (int32_t)cnt;
+        }
+        ++cnt;
+        chunks += nc;
+    }
+    if (chunks > INT32_MAX) return GALA_ERR_UNSUPPORTED;
+    if (fill) row_chunk0[cnt] = (int32_t)chunks;
+    *n_rows_split = cnt;
+    *n_chunks = chunks;
+    return GALA_OK;
+}

@@ -50,6 +50,7 @@ struct SpmmParams {
     int32_t head_dim;   // F / val_heads
     int32_t accum;      // 1: Y += ..., 0: Y = ...
     int32_t nsamp, ra, rb;
+    int32_t split_threshold;  // > 0: rows longer than this are left to the split kernels
     SegTable seg;
 };
 
@@ -85,84 +86,82 @@ __device__ __forceinline__ void accumulate(typename VecT<VEC>::T &acc,
     }
 }
 
-template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
-__global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
-    typedef typename VecT<VEC>::T V;
-    constexpr int RPW = kWave / G;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int gl = lane & (G - 1);
-    const int grp = lane / G;
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
-    const int64_t row = wave * RPW + grp;
-    if (row >= p.n_rows) return;
-    KernargSegPtr seg = kernarg_segtable(offsetof(SpmmParams, seg));
-
-    // columns owned by this lane; lanes past F load a valid column and never store
-    bool cvalid[CH];
-    int64_t coff[CH];
+// Per-lane column ownership of a row group.
+template <int VEC, int G, int CH, bool W>
+struct Cols {
+    bool valid[CH];
+    int64_t off[CH];
     int head[CH];
+    __device__ __forceinline__ Cols(const SpmmParams &p, int gl) {
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const int f = (ch * G + gl) * VEC;
-        cvalid[ch] = f < p.F;
-        coff[ch] = cvalid[ch] ? f : 0;
-        head[ch] = W ? (int)(coff[ch] / p.head_dim) : 0;
+        for (int ch = 0; ch < CH; ++ch) {
+            const int f = (ch * G + gl) * VEC;
+            valid[ch] = f < p.F;  // lanes past F load a valid column and never store
+            off[ch] = valid[ch] ? f : 0;
+            head[ch] = W ? (int)(off[ch] / p.head_dim) : 0;
+        }
     }
+};
 
-    V acc[CH];
-    const bool start_from_y = p.accum && p.dst_scale == nullptr;
+// acc += the edges [e0, e1) of one row (or nsamp kernel samples), sequentially in CSR
+// order; the loads of U edges are issued before the first add of the batch.
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+__device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
+                                                 int64_t e0, int64_t e1,
+                                                 typename VecT<VEC>::T (&acc)[CH]) {
+    typedef typename VecT<VEC>::T V;
+    const int32_t deg = (int32_t)(e1 - e0);
+    const int32_t n = SAMP ? (deg > 0 ? p.nsamp : 0) : deg;
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        int32_t c[U];
+        V x[U][CH];
+        float w[U][CH];
+        float sc[U];
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch)
-        acc[ch] = (start_from_y && cvalid[ch]) ? ldv<VEC>(p.Y + row * p.ldy + coff[ch]) : V(0.0f);
-
-    const int64_t rp_stride = p.n_rows + 1;
-    const int nseg = p.seg.n;
-    for (int s = 0; s < nseg; ++s) {
-        const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
-        const int64_t base = seg->base[s];
-        const int64_t e0 = base + rp[row];
-        const int64_t e1 = base + rp[row + 1];
-        const int32_t deg = (int32_t)(e1 - e0);
-        // n edges visited: all of them, or nsamp samples when the row is not empty
-        const int32_t n = SAMP ? (deg > 0 ? p.nsamp : 0) : deg;
-        for (int32_t j0 = 0; j0 < n; j0 += U) {
-            int32_t c[U];
-            V x[U][CH];
-            float w[U][CH];
-            float sc[U];
-            // issue every load of the batch before the first add: clamped indices keep
-            // the addresses valid, the tail is masked in the accumulation
+        for (int k = 0; k < U; ++k) {
+            const int32_t jj = (j0 + k < n) ? j0 + k : n - 1;  // clamped: valid address
+            const int32_t j = SAMP ? (p.ra * jj + p.rb) % deg : jj;
+            const int64_t e = e0 + j;
+            c[k] = p.col[e];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int32_t jj = (j0 + k < n) ? j0 + k : n - 1;
-                const int32_t j = SAMP ? (p.ra * jj + p.rb) % deg : jj;
-                const int64_t e = e0 + j;
-                c[k] = p.col[e];
+            for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + cl.head[ch]] : 1.0f;
+        }
 #pragma unroll
-                for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + head[ch]] : 1.0f;
-            }
+        for (int k = 0; k < U; ++k) {
+            const float *xr = p.X + (int64_t)c[k] * p.ldx;
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const float *xr = p.X + (int64_t)c[k] * p.ldx;
+            for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + cl.off[ch]);
+            sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
+        }
 #pragma unroll
-                for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + coff[ch]);
-                sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
-            }
+        for (int k = 0; k < U; ++k) {
+            if (j0 + k < n) {
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (j0 + k < n) {
-#pragma unroll
-                    for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
-                }
+                for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
             }
         }
     }
+}
 
+template <int VEC, int G, int CH, bool W>
+__device__ __forceinline__ void init_acc(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
+                                         int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
+    typedef typename VecT<VEC>::T V;
+    const bool start_from_y = p.accum && p.dst_scale == nullptr;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+        acc[ch] = (start_from_y && cl.valid[ch]) ? ldv<VEC>(p.Y + row * p.ldy + cl.off[ch]) : V(0.0f);
+}
+
+template <int VEC, int G, int CH, bool W>
+__device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
+                                          int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
+    typedef typename VecT<VEC>::T V;
     const float ds = p.dst_scale ? p.dst_scale[row] : 1.0f;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
-        if (!cvalid[ch]) continue;
-        float *yp = p.Y + row * p.ldy + coff[ch];
+        if (!cl.valid[ch]) continue;
+        float *yp = p.Y + row * p.ldy + cl.off[ch];
         V out = acc[ch];
         if (p.dst_scale) {
 #pragma unroll
@@ -175,6 +174,102 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
         }
         stv<VEC>(yp, out);
     }
+}
+
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+__global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
+    typedef typename VecT<VEC>::T V;
+    constexpr int RPW = kWave / G;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
+    const int64_t row = wave * RPW + lane / G;
+    if (row >= p.n_rows) return;
+    KernargSegPtr seg = kernarg_segtable(offsetof(SpmmParams, seg));
+    if (p.split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > p.split_threshold)
+        return;  // hub row: done by k_spmm_chunk + k_spmm_fixup
+    const Cols<VEC, G, CH, W> cl(p, gl);
+    V acc[CH];
+    init_acc<VEC, G, CH, W>(p, cl, row, acc);
+    const int64_t rp_stride = p.n_rows + 1;
+    const int nseg = p.seg.n;
+    for (int s = 0; s < nseg; ++s) {
+        const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
+        const int64_t base = seg->base[s];
+        accumulate_range<VEC, G, CH, U, W, SAMP, SRCS>(p, cl, base + rp[row], base + rp[row + 1], acc);
+    }
+    store_row<VEC, G, CH, W>(p, cl, row, acc);
+}
+
+// ---- split rows: chunk partials + ordered fix-up ---------------------------------------
+struct SplitParams {
+    const int32_t *rows;
+    const int32_t *row_chunk0;
+    const int32_t *chunk_row;
+    float *ws;
+    int64_t ws_cols;
+    int64_t n_chunks;
+    int64_t n_rows_split;
+    int32_t chunk;
+};
+
+template <int VEC, int G, int CH, int U, bool W, bool SRCS>
+__global__ __launch_bounds__(kBlock) void k_spmm_chunk(SpmmParams p, SplitParams sp) {
+    typedef typename VecT<VEC>::T V;
+    constexpr int RPW = kWave / G;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * RPW + lane / G;
+    if (c >= sp.n_chunks) return;
+    const int32_t ri = sp.chunk_row[c];
+    const int64_t row = sp.rows[ri];
+    const int64_t k = c - sp.row_chunk0[ri];
+    const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];
+    const int64_t e0 = r0 + k * sp.chunk;
+    const int64_t e1 = (e0 + sp.chunk < r1) ? e0 + sp.chunk : r1;
+    const Cols<VEC, G, CH, W> cl(p, gl);
+    V acc[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) acc[ch] = V(0.0f);
+    accumulate_range<VEC, G, CH, U, W, false, SRCS>(p, cl, e0, e1, acc);
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+        if (cl.valid[ch]) stv<VEC>(sp.ws + c * sp.ws_cols + cl.off[ch], acc[ch]);
+}
+
+template <int VEC, int G, int CH, bool W>
+__global__ __launch_bounds__(kBlock) void k_spmm_fixup(SpmmParams p, SplitParams sp) {
+    typedef typename VecT<VEC>::T V;
+    constexpr int RPW = kWave / G;
+    constexpr int U = 8;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t ri = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * RPW + lane / G;
+    if (ri >= sp.n_rows_split) return;
+    const int64_t row = sp.rows[ri];
+    const Cols<VEC, G, CH, W> cl(p, gl);
+    V acc[CH];
+    init_acc<VEC, G, CH, W>(p, cl, row, acc);
+    const int64_t c0 = sp.row_chunk0[ri], c1 = sp.row_chunk0[ri + 1];
+    for (int64_t c = c0; c < c1; c += U) {
+        V part[U][CH];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t cc = (c + k < c1) ? c + k : c1 - 1;
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) part[k][ch] = ldv<VEC>(sp.ws + cc * sp.ws_cols + cl.off[ch]);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (c + k >= c1) continue;
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    el<VEC>(acc[ch], i) = __fadd_rn(el<VEC>(acc[ch], i), el<VEC>(part[k][ch], i));
+        }
+    }
+    store_row<VEC, G, CH, W>(p, cl, row, acc);
 }
 
 // ---- degree: deg[r] = sum_e (val_e | 1), optionally ^power --------------------------
@@ -225,51 +320,61 @@ __global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
 
 // ---- dispatch ---------------------------------------------------------------------------
 template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
-static void launch_rg(const SpmmParams &p, hipStream_t st) {
+static void launch_rg(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
     // U: edges whose loads are in flight before the first add (per lane: U*CH vectors)
     constexpr int U = (CH * VEC >= 16) ? 2 : ((CH * VEC >= 8) ? 4 : 8);
     constexpr int rows_per_block = (kBlock / kWave) * (kWave / G);
     const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
                        dim3(kBlock), 0, st, p);
+    if (!SAMP && sp && sp->n_chunks > 0) {
+        const int64_t cb = (sp->n_chunks + rows_per_block - 1) / rows_per_block;
+        hipLaunchKernelGGL((k_spmm_chunk<VEC, G, CH, U, W, SRCS>), dim3((unsigned)cb), dim3(kBlock), 0,
+                           st, p, *sp);
+        const int64_t fb = (sp->n_rows_split + rows_per_block - 1) / rows_per_block;
+        hipLaunchKernelGGL((k_spmm_fixup<VEC, G, CH, W>), dim3((unsigned)fb), dim3(kBlock), 0, st, p,
+                           *sp);
+    }
 }
 
 template <int VEC, int G, int CH>
-static void launch_flags(const SpmmParams &p, bool w, bool samp, bool srcs, hipStream_t st) {
+static void launch_flags(const SpmmParams &p, const SplitParams *sp, bool w, bool samp, bool srcs,
+                         hipStream_t st) {
     if (w) {
         if (samp) {
-            if (srcs) launch_rg<VEC, G, CH, true, true, true>(p, st);
-            else launch_rg<VEC, G, CH, true, true, false>(p, st);
+            if (srcs) launch_rg<VEC, G, CH, true, true, true>(p, sp, st);
+            else launch_rg<VEC, G, CH, true, true, false>(p, sp, st);
         } else {
-            if (srcs) launch_rg<VEC, G, CH, true, false, true>(p, st);
-            else launch_rg<VEC, G, CH, true, false, false>(p, st);
+            if (srcs) launch_rg<VEC, G, CH, true, false, true>(p, sp, st);
+            else launch_rg<VEC, G, CH, true, false, false>(p, sp, st);
         }
     } else {
         if (samp) {
-            if (srcs) launch_rg<VEC, G, CH, false, true, true>(p, st);
-            else launch_rg<VEC, G, CH, false, true, false>(p, st);
+            if (srcs) launch_rg<VEC, G, CH, false, true, true>(p, sp, st);
+            else launch_rg<VEC, G, CH, false, true, false>(p, sp, st);
         } else {
-            if (srcs) launch_rg<VEC, G, CH, false, false, true>(p, st);
-            else launch_rg<VEC, G, CH, false, false, false>(p, st);
+            if (srcs) launch_rg<VEC, G, CH, false, false, true>(p, sp, st);
+            else launch_rg<VEC, G, CH, false, false, false>(p, sp, st);
         }
     }
 }
 
 template <int VEC>
-static int launch_vec(const SpmmParams &p, int L, bool w, bool samp, bool srcs, hipStream_t st) {
+static int launch_vec(const SpmmParams &p, const SplitParams *sp, int L, bool w, bool samp,
+                      bool srcs, hipStream_t st) {
     // L = vector elements per row (ceil(F/VEC))
-    if (L <= 1) launch_flags<VEC, 1, 1>(p, w, samp, srcs, st);
-    else if (L <= 2) launch_flags<VEC, 2, 1>(p, w, samp, srcs, st);
-    else if (L <= 4) launch_flags<VEC, 4, 1>(p, w, samp, srcs, st);
-    else if (L <= 8) launch_flags<VEC, 8, 1>(p, w, samp, srcs, st);
-    else if (L <= 16) launch_flags<VEC, 16, 1>(p, w, samp, srcs, st);
-    else if (L <= 32) launch_flags<VEC, 32, 1>(p, w, samp, srcs, st);
-    else if (L <= 64) launch_flags<VEC, 64, 1>(p, w, samp, srcs, st);
-    else if (L <= 128) launch_flags<VEC, 64, 2>(p, w, samp, srcs, st);
-    else if (L <= 192) launch_flags<VEC, 64, 3>(p, w, samp, srcs, st);
-    else if (L <= 256) launch_flags<VEC, 64, 4>(p, w, samp, srcs, st);
-    else if (L <= 384) launch_flags<VEC, 64, 6>(p, w, samp, srcs, st);
-    else if (L <= 512) launch_flags<VEC, 64, 8>(p, w, samp, srcs, st);
+    if (L <= 1) launch_flags<VEC, 1, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 2) launch_flags<VEC, 2, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 4) launch_flags<VEC, 4, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 8) launch_flags<VEC, 8, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 16) launch_flags<VEC, 16, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 32) launch_flags<VEC, 32, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 64) launch_flags<VEC, 64, 1>(p, sp, w, samp, srcs, st);
+    else if (L <= 128) launch_flags<VEC, 64, 2>(p, sp, w, samp, srcs, st);
+    else if (L <= 192) launch_flags<VEC, 64, 3>(p, sp, w, samp, srcs, st);
+    else if (L <= 256) launch_flags<VEC, 64, 4>(p, sp, w, samp, srcs, st);
+    else if (L <= 384) launch_flags<VEC, 64, 6>(p, sp, w, samp, srcs, st);
+    else if (L <= 512) launch_flags<VEC, 64, 8>(p, sp, w, samp, srcs, st);
     else return GALA_ERR_UNSUPPORTED;
     return GALA_OK;
 }
@@ -284,7 +389,8 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
                              int32_t rb, void *stream) {
     int st = check_csr(A);
     if (st) return st;
-    if (F < 0 || ldx < F || ldy < F || (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE)))
+    if (F < 0 || ldx < F || ldy < F ||
+        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT)))
         return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
@@ -319,15 +425,39 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     p.nsamp = nsamp;
     p.ra = ra;
     p.rb = rb;
+    p.split_threshold = 0;
     hipStream_t hs = (hipStream_t)stream;
+
+    // hub rows: chunk partials + ordered fix-up (plan built once per graph on the host)
+    SplitParams spl{};
+    const SplitParams *sp = nullptr;
+    const gala_split_plan_t *plan = A->split;
+    if (plan && plan->n_chunks > 0 && A->n_seg == 1 && !samp && !(flags & GALA_SPMM_EXACT)) {
+        if (plan->threshold < 1 || plan->chunk < 1 || !plan->rows || !plan->row_chunk0 ||
+            !plan->chunk_row || !plan->workspace)
+            return GALA_ERR_INVALID_ARG;
+        spl.rows = plan->rows;
+        spl.row_chunk0 = plan->row_chunk0;
+        spl.chunk_row = plan->chunk_row;
+        spl.ws = plan->workspace;
+        spl.ws_cols = plan->ws_cols;
+        spl.n_chunks = plan->n_chunks;
+        spl.n_rows_split = plan->n_rows_split;
+        spl.chunk = plan->chunk;
+        p.split_threshold = plan->threshold;
+        sp = &spl;
+    }
 
     // feature chunks wider than 512 vectors per lane-group are split over launches
     const int64_t max_cols = 512LL * vec;
+    if (sp && plan->ws_cols < (F < max_cols ? F : max_cols)) return GALA_ERR_INVALID_ARG;
+    if (w && p.val_heads > 1 && F > max_cols) return GALA_ERR_UNSUPPORTED;
     for (int32_t seg0 = 0; seg0 < A->n_seg; seg0 += kMaxSegPerLaunch) {
         st = fill_segments(A, seg0, &p.seg);
         if (st) return st;
         // segments after the first launch always accumulate onto the previous ones
         const bool accum = (flags & GALA_SPMM_ACCUM) || seg0 > 0;
+        if (seg0 > 0 && dst_scale) return GALA_ERR_UNSUPPORTED;
         for (int64_t c0 = 0; c0 < F; c0 += max_cols) {
             const int32_t Fc = (int32_t)((F - c0) < max_cols ? (F - c0) : max_cols);
             SpmmParams q = p;
@@ -335,18 +465,11 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
             q.Y = Y + c0;
             q.F = Fc;
             q.accum = accum;
-            if (w) {
-                // a column chunk must stay head-aligned for the per-head weight lookup
-                if (c0 % head_dim != 0 && p.val_heads > 1) return GALA_ERR_UNSUPPORTED;
-                q.val = A->val;  // head index computed from chunk-local column: shift heads
-            }
-            if (w && p.val_heads > 1 && c0 > 0) return GALA_ERR_UNSUPPORTED;
-            if (seg0 > 0 && dst_scale) return GALA_ERR_UNSUPPORTED;
             const int L = (int)((Fc + vec - 1) / vec);
             int r;
-            if (vec == 4) r = launch_vec<4>(q, L, w, samp, src_scale != nullptr, hs);
-            else if (vec == 2) r = launch_vec<2>(q, L, w, samp, src_scale != nullptr, hs);
-            else r = launch_vec<1>(q, L, w, samp, src_scale != nullptr, hs);
+            if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs);
+            else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
+            else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
             if (r) return r;
             r = launch_status();
             if (r) return r;

@@ -20,11 +20,26 @@ GALA_ERR_GRAPH = -4
 
 GALA_SPMM_ACCUM = 0x1
 GALA_SPMM_SAMPLE = 0x2
+GALA_SPMM_EXACT = 0x4
 GALA_SDDVV_ADD = 0
 GALA_SDDVV_MUL = 1
 GALA_SDDVV_ADD_LRELU = 2
 GALA_SOFTMAX_REF = 0
 GALA_SOFTMAX_FIXED = 1
+
+
+class gala_split_plan_t(ctypes.Structure):
+    _fields_ = [
+        ("threshold", ctypes.c_int32),
+        ("chunk", ctypes.c_int32),
+        ("n_rows_split", ctypes.c_int64),
+        ("n_chunks", ctypes.c_int64),
+        ("rows", ctypes.c_void_p),
+        ("row_chunk0", ctypes.c_void_p),
+        ("chunk_row", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p),
+        ("ws_cols", ctypes.c_int64),
+    ]
 
 
 class gala_csr_t(ctypes.Structure):
@@ -38,6 +53,7 @@ class gala_csr_t(ctypes.Structure):
         ("val_heads", ctypes.c_int32),
         ("n_seg", ctypes.c_int32),
         ("seg_bounds", ctypes.c_void_p),
+        ("split", ctypes.c_void_p),
     ]
 
 
@@ -67,6 +83,7 @@ SIGNATURES = {
     "gala_host_col_breakpoints": (ctypes.c_int64, [_I64, _I64, _P, _I64]),
     "gala_host_col_tile": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _P, _P, _P, _P, _P]),
     "gala_host_sample_ab": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    "gala_host_split_plan": (ctypes.c_int, [_I64, _P, _I32, _I32, _P, _P, _P, _P, _P]),
     "gala_host_csr_transpose": (ctypes.c_int, [_I64, _I64, _P, _P, _P, _P, _P]),
     "gala_host_gen_graph": (ctypes.c_int, [_I32, _I64, _I64, ctypes.c_uint64, _P, _P]),
 }

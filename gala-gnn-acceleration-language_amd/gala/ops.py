@@ -38,23 +38,69 @@ class DeviceGraph:
         self.val_heads = int(val_heads)
         self.bounds = None if bounds is None else np.ascontiguousarray(bounds, np.int32)
         self._csr = None
+        # hub-row split plan, shared with with_values() views:
+        # {"plan": gala_split_plan_t, "arrays": device index arrays, "ws": workspace tensor}
+        self._split = None
 
     @classmethod
-    def from_host(cls, g: HostGraph, device="cuda"):
+    def from_host(cls, g: HostGraph, device="cuda", split="auto"):
         rp = torch.from_numpy(np.ascontiguousarray(g.rowptr)).to(device)
         col = torch.from_numpy(np.ascontiguousarray(g.col)).to(device)
         val = None if g.val is None else torch.from_numpy(np.ascontiguousarray(g.val, np.float32)).to(device)
-        return cls(g.n_rows, g.n_cols, rp, col, val, g.n_seg, g.bounds, g.val_heads)
+        dg = cls(g.n_rows, g.n_cols, rp, col, val, g.n_seg, g.bounds, g.val_heads)
+        if split and g.n_seg == 1 and g.n_rows > 0:
+            deg = np.diff(g.rowptr)
+            thr = max(1024, 8 * int(np.ceil(g.nnz / max(g.n_rows, 1))))
+            if split != "auto":
+                thr = int(split)
+            if deg.max(initial=0) > thr:
+                dg.set_split_plan(g.rowptr, thr, chunk=512)
+        return dg
+
+    def set_split_plan(self, host_rowptr, threshold: int, chunk: int = 512):
+        """Hub-row splitting (gala_split_plan_t), built from the host rowptr."""
+        rp = np.ascontiguousarray(host_rowptr, np.int32)
+        nr = ctypes.c_int64()
+        nc = ctypes.c_int64()
+        _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk, None, None,
+                  None, ctypes.byref(nr), ctypes.byref(nc))
+        rows = np.empty(max(nr.value, 1), np.int32)
+        rc0 = np.empty(nr.value + 1, np.int32)
+        crow = np.empty(max(nc.value, 1), np.int32)
+        _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk,
+                  rows.ctypes.data, rc0.ctypes.data, crow.ctypes.data, ctypes.byref(nr), ctypes.byref(nc))
+        dev = self.col.device
+        arrays = tuple(torch.from_numpy(a).to(dev) for a in (rows, rc0, crow))
+        plan = _abi.gala_split_plan_t()
+        plan.threshold, plan.chunk = threshold, chunk
+        plan.n_rows_split, plan.n_chunks = nr.value, nc.value
+        plan.rows, plan.row_chunk0, plan.chunk_row = (a.data_ptr() for a in arrays)
+        plan.workspace, plan.ws_cols = None, 0
+        self._split = {"plan": plan, "arrays": arrays, "ws": None}
+        self._csr = None
+
+    @property
+    def split_rows(self) -> int:
+        return 0 if self._split is None else int(self._split["plan"].n_rows_split)
 
     @property
     def nnz(self) -> int:
         return int(self.col.numel())
 
     def with_values(self, val, val_heads=1) -> "DeviceGraph":
-        return DeviceGraph(self.n_rows, self.n_cols, self.rowptr, self.col, val, self.n_seg,
-                           self.bounds, val_heads)
+        g = DeviceGraph(self.n_rows, self.n_cols, self.rowptr, self.col, val, self.n_seg,
+                        self.bounds, val_heads)
+        g._split = self._split
+        return g
 
-    def csr(self):
+    def csr(self, F: int = 0):
+        if self._split is not None and F > 0:
+            plan = self._split["plan"]
+            if plan.ws_cols < F:  # workspace for the chunk partials, grown on demand
+                ws = torch.empty(max(int(plan.n_chunks), 1) * F, device=self.col.device)
+                self._split["ws"] = ws
+                plan.workspace, plan.ws_cols = ws.data_ptr(), F
+            self._csr = None
         if self._csr is None:
             c = _abi.gala_csr_t()
             c.n_rows, c.n_cols, c.nnz = self.n_rows, self.n_cols, self.nnz
@@ -64,17 +110,21 @@ class DeviceGraph:
             c.val_heads = self.val_heads
             c.n_seg = self.n_seg
             c.seg_bounds = None if self.bounds is None else self.bounds.ctypes.data
+            c.split = None
+            if self._split is not None and self._split["plan"].ws_cols > 0:
+                c.split = ctypes.addressof(self._split["plan"])
             self._csr = c
         return ctypes.byref(self._csr)
 
 
 def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=None,
-         accum=False, nsamp=None, ra=5, rb=7) -> torch.Tensor:
+         accum=False, nsamp=None, ra=5, rb=7, exact=False) -> torch.Tensor:
     F = X.shape[1]
     if out is None:
         out = (torch.zeros if accum else torch.empty)((g.n_rows, F), device=X.device, dtype=torch.float32)
-    flags = (_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
-    _abi.call("gala_spmm_f32", g.csr(), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
+    flags = ((_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
+             | (_abi.GALA_SPMM_EXACT if exact else 0))
+    _abi.call("gala_spmm_f32", g.csr(F), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
               _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, _stream())
     return out
 

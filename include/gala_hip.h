@@ -57,6 +57,26 @@ typedef enum gala_status {
  *             segments (the reference launches segments on racing streams,
  *             cuda.h:472-499; here segment 0 is accumulated first, then 1, ...).
  * ---------------------------------------------------------------------------------- */
+/*
+ * Optional split plan for power-law graphs: rows longer than `threshold` edges are cut
+ * into chunks of `chunk` edges that run in parallel; each chunk writes a partial sum to
+ * `workspace` and a fix-up pass adds the partials of a row in chunk order.  Built once per
+ * graph on the host with gala_host_split_plan; only used for n_seg == 1.  Rows that are
+ * split are summed per chunk (not in one sequential pass), so their results match the
+ * reference within fp32 rounding instead of bit for bit; GALA_SPMM_EXACT disables it.
+ */
+typedef struct gala_split_plan {
+    int32_t threshold;         /* rows with deg > threshold are split                    */
+    int32_t chunk;             /* edges per chunk                                        */
+    int64_t n_rows_split;
+    int64_t n_chunks;
+    const int32_t *rows;       /* device [n_rows_split]: split row ids (ascending)       */
+    const int32_t *row_chunk0; /* device [n_rows_split+1]: first chunk of each split row  */
+    const int32_t *chunk_row;  /* device [n_chunks]: index into rows[] of every chunk    */
+    float *workspace;          /* device [n_chunks * ws_cols] partial results            */
+    int64_t ws_cols;           /* floats per chunk (>= F for SpMM, >= F + 2*heads GAT)    */
+} gala_split_plan_t;
+
 typedef struct gala_csr {
     int64_t n_rows;            /* rows of A (destination vertices of the aggregation)     */
     int64_t n_cols;            /* columns of A (source vertices); X has n_cols rows      */
@@ -69,6 +89,7 @@ typedef struct gala_csr {
     const int32_t *seg_bounds; /* HOST [2*n_seg] {start,end} edge of each segment, or
                                   NULL when n_seg == 1 (reference keeps `bounds` on the
                                   host: cuda.h:472-475 reads bounds_ptr on the CPU)        */
+    const gala_split_plan_t *split; /* HOST pointer, NULL = no row splitting              */
 } gala_csr_t;
 
 /* ---- library information ------------------------------------------------------------ */
@@ -81,6 +102,7 @@ int gala_last_hip_error(void);                 /* hipError_t of the last GALA_ER
                                  cuda.h:463 + 309-310); without it Y is overwritten       */
 #define GALA_SPMM_SAMPLE 0x2  /* kernel sampling: per row with deg>0, nsamp edges
                                  j = (ra*ji + rb) mod deg (cuda.h:313-321)                */
+#define GALA_SPMM_EXACT 0x4   /* ignore A->split: every row in one sequential pass       */
 
 /*
  * Y[r, 0:F] (+)= dst_scale[r] * sum_{e in row r} w_e * (src_scale[col_e] * X[col_e, 0:F])
@@ -236,6 +258,16 @@ int gala_host_col_tile(int64_t n_rows, const int32_t *rowptr, const int32_t *col
 int gala_host_sample_ab(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
                         const float *val, int32_t nsamp, int32_t ra, int32_t rb,
                         int32_t *out_rowptr, int32_t *out_col, float *out_val);
+
+/*
+ * Split plan of a CSR (gala_split_plan_t): rows with deg > threshold, chunks of `chunk`
+ * edges.  Two-call pattern: with rows/row_chunk0/chunk_row NULL it only writes the counts
+ * (*n_rows_split, *n_chunks); then call again with arrays of those sizes (+1 for
+ * row_chunk0).
+ */
+int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshold, int32_t chunk,
+                         int32_t *rows, int32_t *row_chunk0, int32_t *chunk_row,
+                         int64_t *n_rows_split, int64_t *n_chunks);
 
 /*
  * Transpose a CSR (n_seg == 1): out_rowptr [n_cols+1], out_col [nnz], perm [nnz] with

@@ -273,3 +273,45 @@ def test_spmm_matches_reference_gspmm_fixtures(path):
         F = min(int(k2[3:]) for k2 in fx if k2.startswith("Y_F"))
         X = dev(np.ascontiguousarray(fx["X"][:, :F]))
         np.testing.assert_array_equal(host(ops.spmm(ops.DeviceGraph.from_host(t), X)), fx[f"Y_F{F}"])
+
+
+# ---- hub rows (power-law): split plan ----------------------------------------------------
+def hub_graph():
+    """R-MAT graph plus a star row of 20k edges and a few mid-size rows."""
+    rng = np.random.default_rng(11)
+    base = powerlaw(n=6000, m=40000, seed=5)
+    rows = np.repeat(np.arange(base.n_rows), np.diff(base.rowptr)).astype(np.int32)
+    src = np.concatenate([rows, np.full(20000, 17, np.int32), np.full(3000, 4000, np.int32)])
+    dst = np.concatenate([base.col, rng.integers(0, 6000, 23000).astype(np.int32)])
+    return layout.csr_build(6000, 6000, src, dst)
+
+
+@pytest.mark.parametrize("F", [1, 32, 47, 256])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_split_hub_rows(F, weighted):
+    g = hub_graph()
+    val = edge_values(g.nnz) if weighted else None
+    hg = layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, g.col, val)
+    dg = ops.DeviceGraph.from_host(hg)
+    assert dg.split_rows >= 2
+    X = features(g.n_cols, F)
+    ref = orc.spmm(to_oracle(hg), X)
+    Y = host(ops.spmm(dg, dev(X)))
+    np.testing.assert_allclose(Y, ref, **TOL)                  # split rows: chunked order
+    deg = np.diff(g.rowptr)
+    light = deg <= 1024
+    np.testing.assert_array_equal(Y[light], ref[light])       # other rows: still bit-exact
+    Ye = host(ops.spmm(dg, dev(X), exact=True))                # GALA_SPMM_EXACT: no split
+    np.testing.assert_array_equal(Ye, ref)
+
+
+def test_spmm_split_with_norms_and_accum():
+    g = hub_graph()
+    dg = ops.DeviceGraph.from_host(g)
+    norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
+    X = features(g.n_cols, 32)
+    Y0 = features(g.n_rows, 32, seed=3)
+    Yt = dev(Y0)
+    ops.spmm(dg, dev(X), dst_scale=dev(norm), out=Yt, accum=True)
+    ref = orc.spmm(to_oracle(g), X, dst_scale=norm, Y=Y0.copy(), accum=True)
+    np.testing.assert_allclose(host(Yt), ref, **TOL)
