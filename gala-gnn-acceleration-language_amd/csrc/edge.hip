@@ -70,6 +70,7 @@ __global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, 
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
+        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const int64_t e = e0 + (t >> LH);
             const float bv = b[((int64_t)p.col[e] << LH) + h];
@@ -97,6 +98,7 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const float *vr = v + (e0 << LH);
+            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) part += vr[t];
         }
     }
@@ -120,6 +122,7 @@ __global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float 
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         float *vr = v + (e0 << LH);
+        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) vr[t] = __fmul_rn(vr[t], qv);
     }
 }
@@ -142,6 +145,7 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const float *lr = logit + (e0 << LH);
+            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) {
                 const float x = lr[t];
                 if (MODE == GALA_SOFTMAX_REF) {
@@ -173,6 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
         const int64_t n = (e1 - e0) << LH;
         const float *lr = logit + (e0 << LH);
         float *ar = alpha + (e0 << LH);
+        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const float x = lr[t];
             const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x) : expf(x - m);
@@ -194,6 +199,7 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const int64_t o = e0 << LH;
+            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) part += __fmul_rn(alpha[o + t], dalpha[o + t]);
         }
     }
@@ -205,6 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         const int64_t o = e0 << LH;
+        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const float a = alpha[o + t];
             const float sds = __fmul_rn(a, dalpha[o + t]);
@@ -390,11 +397,12 @@ __device__ __forceinline__ float reduce_scatter(float (&v)[U], int gl) {
     return r;
 }
 
+// Edges [e0, e1) of `row` (one row group): out[e] = <Ad[row], Bd[col_e]> per head.
 template <int G, int VEC, int HW, int U>
-__global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad, int64_t lda,
-                                                  const float *Bd, int64_t ldb, int32_t F,
-                                                  float *out) {
-    GALA_ROW_PROLOGUE(G);
+__device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool row_ok, int64_t row,
+                                            const float *Ad, int64_t lda, const float *Bd,
+                                            int64_t ldb, int32_t F, float *out, int64_t e0,
+                                            int64_t e1) {
     const int f = gl * VEC;
     const bool cv = row_ok && f < F;
     const int64_t fo = (f < F) ? f : 0;
@@ -404,34 +412,66 @@ __global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad,
     const int H = p.heads;
     const int D = F / H;
     const int h = cv ? f / D : 0;
+    const int32_t n = (int32_t)(e1 - e0);
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        float part[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+            const int64_t c = p.col[e0 + j];
+            const float *bp = Bd + c * ldb + fo;
+            float acc = 0.0f;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc = fmaf(a[i], bp[i], acc);
+            part[k] = acc;
+        }
+        if (HW == G) {
+            const float r = reduce_scatter<G, U>(part, gl);
+            const int k = gl / (G / U);
+            if ((gl & (G / U - 1)) == 0 && j0 + k < n) out[e0 + j0 + k] = r;
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const float r = group_sum<HW>(part[k]);
+                if (cv && (gl % HW) == 0 && j0 + k < n) out[(e0 + j0 + k) * H + h] = r;
+            }
+        }
+    }
+}
+
+// hub rows (A->split): one row group per chunk of a split row; no fix-up needed
+template <int G, int VEC, int HW, int U>
+__global__ __launch_bounds__(kBlock) void k_sddmm_chunk(EdgeParams p, const float *Ad, int64_t lda,
+                                                        const float *Bd, int64_t ldb, int32_t F,
+                                                        float *out, const int32_t *rows,
+                                                        const int32_t *row_chunk0,
+                                                        const int32_t *chunk_row, int64_t n_chunks,
+                                                        int32_t chunk) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / G) + lane / G;
+    if (c >= n_chunks) return;  // whole groups exit together
+    const int32_t ri = chunk_row[c];
+    const int64_t row = rows[ri];
+    const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];
+    const int64_t e0 = r0 + (c - row_chunk0[ri]) * (int64_t)chunk;
+    const int64_t e1 = (e0 + chunk < r1) ? e0 + chunk : r1;
+    sddmm_range<G, VEC, HW, U>(p, gl, true, row, Ad, lda, Bd, ldb, F, out, e0, e1);
+}
+
+template <int G, int VEC, int HW, int U>
+__global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad, int64_t lda,
+                                                  const float *Bd, int64_t ldb, int32_t F,
+                                                  float *out, int32_t split_threshold) {
+    GALA_ROW_PROLOGUE(G);
+    if (split_threshold > 0) {
+        // rows of one group share the row: the skip is uniform inside every group
+        if (row_ok && p.rowptr[row + 1] - p.rowptr[row] > split_threshold) return;
+    }
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0 = 0, e1 = 0;
         if (row_ok) row_range(p, s, row, e0, e1);
-        const int32_t n = (int32_t)(e1 - e0);
-        for (int32_t j0 = 0; j0 < n; j0 += U) {
-            float part[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
-                const int64_t c = p.col[e0 + j];
-                const float *bp = Bd + c * ldb + fo;
-                float acc = 0.0f;
-#pragma unroll
-                for (int i = 0; i < VEC; ++i) acc = fmaf(a[i], bp[i], acc);
-                part[k] = acc;
-            }
-            if (HW == G) {
-                const float r = reduce_scatter<G, U>(part, gl);
-                const int k = gl / (G / U);
-                if ((gl & (G / U - 1)) == 0 && j0 + k < n) out[e0 + j0 + k] = r;
-            } else {
-#pragma unroll
-                for (int k = 0; k < U; ++k) {
-                    const float r = group_sum<HW>(part[k]);
-                    if (cv && (gl % HW) == 0 && j0 + k < n) out[(e0 + j0 + k) * H + h] = r;
-                }
-            }
-        }
+        sddmm_range<G, VEC, HW, U>(p, gl, row_ok, row, Ad, lda, Bd, ldb, F, out, e0, e1);
     }
 }
 
@@ -781,32 +821,52 @@ extern "C" int gala_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha
     return launch_status();
 }
 
-template <int G, int VEC>
-static void launch_sddmm(const EdgeParams &p, int hw, const float *Ad, int64_t lda,
-                         const float *Bd, int64_t ldb, int32_t F, float *out, hipStream_t hs) {
-    const dim3 grid(blocks_for(p.n_rows, G));
+struct SddmmSplit {
+    const int32_t *rows = nullptr, *row_chunk0 = nullptr, *chunk_row = nullptr;
+    int64_t n_chunks = 0;
+    int32_t chunk = 0, threshold = 0;
+};
+
+template <int G, int VEC, int HWV>
+static void launch_sddmm_hw(const EdgeParams &p, const SddmmSplit &sp, const float *Ad, int64_t lda,
+                            const float *Bd, int64_t ldb, int32_t F, float *out, hipStream_t hs) {
     constexpr int U = (G >= 8) ? 8 : G;  // U <= G for the reduce-scatter
+    constexpr int HW = (HWV < G) ? HWV : G;
+    hipLaunchKernelGGL((k_sddmm<G, VEC, HW, U>), dim3(blocks_for(p.n_rows, G)), dim3(kBlock), 0, hs,
+                       p, Ad, lda, Bd, ldb, F, out, sp.threshold);
+    if (sp.n_chunks > 0) {
+        const int64_t per_block = (kBlock / kWave) * (kWave / G);
+        hipLaunchKernelGGL((k_sddmm_chunk<G, VEC, HW, U>), dim3((unsigned)((sp.n_chunks + per_block - 1) / per_block)),
+                           dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out, sp.rows, sp.row_chunk0,
+                           sp.chunk_row, sp.n_chunks, sp.chunk);
+    }
+}
+
+template <int G, int VEC>
+static void launch_sddmm(const EdgeParams &p, const SddmmSplit &sp, int hw, const float *Ad,
+                         int64_t lda, const float *Bd, int64_t ldb, int32_t F, float *out,
+                         hipStream_t hs) {
     switch (hw) {
-        case 1: hipLaunchKernelGGL((k_sddmm<G, VEC, 1, U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 2: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 2 ? G : 2), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 4: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 4 ? G : 4), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 8: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 8 ? G : 8), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 16: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 16 ? G : 16), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        case 32: hipLaunchKernelGGL((k_sddmm<G, VEC, (G < 32 ? G : 32), U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
-        default: hipLaunchKernelGGL((k_sddmm<G, VEC, G, U>), grid, dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out); break;
+        case 1: launch_sddmm_hw<G, VEC, 1>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        case 2: launch_sddmm_hw<G, VEC, 2>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        case 4: launch_sddmm_hw<G, VEC, 4>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        case 8: launch_sddmm_hw<G, VEC, 8>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        case 16: launch_sddmm_hw<G, VEC, 16>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        case 32: launch_sddmm_hw<G, VEC, 32>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
+        default: launch_sddmm_hw<G, VEC, G>(p, sp, Ad, lda, Bd, ldb, F, out, hs); break;
     }
 }
 
 template <int VEC>
-static int sddmm_vec(const EdgeParams &p, int L, int hw, const float *Ad, int64_t lda,
+static int sddmm_vec(const EdgeParams &p, const SddmmSplit &sp, int L, int hw, const float *Ad, int64_t lda,
                      const float *Bd, int64_t ldb, int32_t F, float *out, hipStream_t hs) {
-    if (L <= 1) launch_sddmm<1, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 2) launch_sddmm<2, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 4) launch_sddmm<4, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 8) launch_sddmm<8, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 16) launch_sddmm<16, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 32) launch_sddmm<32, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
-    else if (L <= 64) launch_sddmm<64, VEC>(p, hw, Ad, lda, Bd, ldb, F, out, hs);
+    if (L <= 1) launch_sddmm<1, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 2) launch_sddmm<2, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 4) launch_sddmm<4, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 8) launch_sddmm<8, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 16) launch_sddmm<16, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 32) launch_sddmm<32, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
+    else if (L <= 64) launch_sddmm<64, VEC>(p, sp, hw, Ad, lda, Bd, ldb, F, out, hs);
     else return GALA_ERR_UNSUPPORTED;
     return GALA_OK;
 }
@@ -830,10 +890,22 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     while (Gp < L) Gp <<= 1;
     if (heads > 1 && (hw_l & (hw_l - 1))) return GALA_ERR_UNSUPPORTED;
     const int hw = heads > 1 ? hw_l : Gp;
+    SddmmSplit sp;
+    const gala_split_plan_t *plan = A->split;
+    if (plan && plan->n_chunks > 0 && A->n_seg == 1) {
+        if (!plan->rows || !plan->row_chunk0 || !plan->chunk_row || plan->chunk < 1)
+            return GALA_ERR_INVALID_ARG;
+        sp.rows = plan->rows;
+        sp.row_chunk0 = plan->row_chunk0;
+        sp.chunk_row = plan->chunk_row;
+        sp.n_chunks = plan->n_chunks;
+        sp.chunk = plan->chunk;
+        sp.threshold = plan->threshold;
+    }
     int r;
-    if (vec == 4) r = sddmm_vec<4>(p, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
-    else if (vec == 2) r = sddmm_vec<2>(p, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
-    else r = sddmm_vec<1>(p, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
+    if (vec == 4) r = sddmm_vec<4>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
+    else if (vec == 2) r = sddmm_vec<2>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
+    else r = sddmm_vec<1>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
     if (r) return r;
     return launch_status();
 }

@@ -111,7 +111,7 @@ class DeviceGraph:
             c.n_seg = self.n_seg
             c.seg_bounds = None if self.bounds is None else self.bounds.ctypes.data
             c.split = None
-            if self._split is not None and self._split["plan"].ws_cols > 0:
+            if self._split is not None:
                 c.split = ctypes.addressof(self._split["plan"])
             self._csr = c
         return ctypes.byref(self._csr)

@@ -28,6 +28,15 @@ struct CsrView {
     torch::Tensor bounds_host;  // keeps the host bounds alive
 };
 
+// the split plan registered for this offsets tensor (same TensorImpl as a slot's)
+SplitState *find_split(const torch::Tensor &offsets) {
+    auto &S = global_slots();
+    for (size_t i = 0; i < S.offset_graph.size(); ++i)
+        if (S.split[i] && S.offset_graph[i].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
+            return S.split[i].get();
+    return nullptr;
+}
+
 CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torch::Tensor *vals,
              const torch::Tensor &bounds, int64_t segments, int val_heads = 1) {
     check_dev(offsets, torch::kInt, "offset_graph");
@@ -48,6 +57,10 @@ CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torc
     }
     v.c.n_seg = (int32_t)segments;
     v.c.seg_bounds = nullptr;
+    v.c.split = nullptr;
+    if (segments == 1) {
+        if (SplitState *sp = find_split(offsets)) v.c.split = &sp->plan;
+    }
     if (segments > 1) {
         TORCH_CHECK(bounds.defined() && bounds.numel() >= 2 * segments, "gala: bounds missing");
         v.bounds_host = bounds.to(torch::kCPU, torch::kInt).contiguous();
@@ -119,6 +132,11 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
     const int64_t nrows = cv.c.n_rows;
     // reference: dcols = input_dense.numel() / nrows (cuda.h:453-454)
     const int64_t dcols = x.dim() == 2 ? x.size(1) : x.numel() / std::max<int64_t>(nrows, 1);
+    if (cv.c.split) {
+        SplitState *sp = find_split(offsets);
+        sp->ensure_workspace(std::min<int64_t>(dcols, 2048));
+        cv.c.split = &sp->plan;
+    }
     cv.c.n_cols = dcols ? x.numel() / dcols : 0;
     auto out = torch::empty({nrows, dcols}, fopts(X));
     const float *ss = nullptr, *ds = nullptr;
@@ -143,6 +161,48 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
 
 }  // namespace
 
+// ---- split plans ----------------------------------------------------------------------
+void SplitState::ensure_workspace(int64_t F) {
+    if (plan.ws_cols >= F) return;
+    ws = torch::empty({std::max<int64_t>(plan.n_chunks, 1) * F},
+                      torch::TensorOptions().dtype(torch::kFloat).device(rows.device()));
+    plan.workspace = ws.data_ptr<float>();
+    plan.ws_cols = F;
+}
+
+std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int segments) {
+    if (segments != 1 || !offsets.defined() || offsets.numel() < 2) return nullptr;
+    auto rp = offsets.to(torch::kCPU, torch::kInt).contiguous();
+    const int64_t n = rp.numel() - 1;
+    const int32_t *r = rp.data_ptr<int32_t>();
+    const int64_t nnz = r[n];
+    const int32_t thr = (int32_t)std::max<int64_t>(1024, 8 * ((nnz + n - 1) / std::max<int64_t>(n, 1)));
+    const int32_t chunk = 512;
+    int64_t nr = 0, nc = 0;
+    check(gala_host_split_plan(n, r, thr, chunk, nullptr, nullptr, nullptr, &nr, &nc),
+          "gala_host_split_plan");
+    if (nr == 0) return nullptr;
+    auto io = torch::TensorOptions().dtype(torch::kInt);
+    auto rows = torch::empty({nr}, io), rc0 = torch::empty({nr + 1}, io), crow = torch::empty({nc}, io);
+    check(gala_host_split_plan(n, r, thr, chunk, rows.data_ptr<int32_t>(), rc0.data_ptr<int32_t>(),
+                               crow.data_ptr<int32_t>(), &nr, &nc),
+          "gala_host_split_plan");
+    auto st = std::make_shared<SplitState>();
+    st->rows = rows.to(offsets.device());
+    st->row_chunk0 = rc0.to(offsets.device());
+    st->chunk_row = crow.to(offsets.device());
+    st->plan.threshold = thr;
+    st->plan.chunk = chunk;
+    st->plan.n_rows_split = nr;
+    st->plan.n_chunks = nc;
+    st->plan.rows = st->rows.data_ptr<int32_t>();
+    st->plan.row_chunk0 = st->row_chunk0.data_ptr<int32_t>();
+    st->plan.chunk_row = st->chunk_row.data_ptr<int32_t>();
+    st->plan.workspace = nullptr;
+    st->plan.ws_cols = 0;
+    return st;
+}
+
 // ---- slots ----------------------------------------------------------------------------
 int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor vals,
                      torch::Tensor b, int segs, bool w) {
@@ -153,6 +213,14 @@ int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor va
     segments.push_back(segs);
     weighted.push_back(w);
     transpose_perm.push_back(torch::Tensor());
+    // a slot sharing the previous slot's tensors (undirected backward) shares its plan
+    std::shared_ptr<SplitState> sp;
+    if (!split.empty() && offset_graph.size() >= 2 &&
+        offset_graph[offset_graph.size() - 2].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
+        sp = split.back();
+    else
+        sp = make_split_plan(offsets, segs);
+    split.push_back(sp);
     if (offset_graph.size() == 1) nrows = offsets.numel() / segs - 1;
     return (int)offset_graph.size() - 1;
 }

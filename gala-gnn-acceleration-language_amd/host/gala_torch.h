@@ -22,12 +22,23 @@
 
 #include <torch/torch.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "gala_hip.h"
 
 namespace gala {
+
+// Hub-row split plan of one graph (gala_split_plan_t + the device arrays it points to).
+struct SplitState {
+    gala_split_plan_t plan{};
+    torch::Tensor rows, row_chunk0, chunk_row, ws;
+    void ensure_workspace(int64_t F);
+};
+// Builds the plan from the device rowptr (one D2H copy) when some row is longer than
+// max(1024, 8 * mean degree); returns nullptr otherwise or for tiled graphs.
+std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int segments);
 
 // The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's
 // forward graph, slot 2*li+1 its backward graph (the same tensors for undirected graphs,
@@ -37,6 +48,7 @@ struct GraphSlots {
     std::vector<int> segments;
     std::vector<bool> weighted;
     std::vector<torch::Tensor> transpose_perm;  // optional: edge k of slot == edge perm[k] of forward
+    std::vector<std::shared_ptr<SplitState>> split;  // hub-row plans (nullptr: none)
     int64_t nrows = 0;
     int ra = 5, rb = 7;    // kernel-sampling coefficients (common.h:813-833)
     int nsamples = 0;      // 0 = no kernel sampling

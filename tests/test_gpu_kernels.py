@@ -40,7 +40,7 @@ def test_spmm_bitexact(graph, F, weighted):
     val = edge_values(graph.nnz) if weighted else None
     X = features(graph.n_cols, F)
     ref = orc.spmm(to_oracle(graph, val), X)
-    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val))
+    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val), split=False)
     Y = host(ops.spmm(dg, dev(X)))
     np.testing.assert_array_equal(Y, ref)
 
@@ -50,7 +50,7 @@ def test_spmm_reference_gspmm(F):
     """Same numbers as the reference's own CPU gSpMM (pinned by the golden fixtures)."""
     g = cora_like()
     X = features(g.n_cols, F, integer=False)
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     Y = host(ops.spmm(dg, dev(X)))
     np.testing.assert_array_equal(Y, orc.gspmm(to_oracle(g), X))
 
@@ -62,7 +62,7 @@ def test_spmm_strided_and_accum():
     Y0 = features(g.n_rows, 48, seed=5)
     Yt = dev(Y0)
     out = Yt[:, 8:40]
-    ops.spmm(ops.DeviceGraph.from_host(g), X, out=out, accum=True)
+    ops.spmm(ops.DeviceGraph.from_host(g, split=False), X, out=out, accum=True)
     ref = orc.spmm(to_oracle(g), Xf[:, 4:36].copy(), Y=Y0[:, 8:40].copy(), accum=True)
     got = host(Yt)
     np.testing.assert_array_equal(got[:, 8:40], ref)
@@ -76,7 +76,7 @@ def test_spmm_gcn_norm_fused(F):
     norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
     X = features(g.n_cols, F)
     ref = orc.spmm(to_oracle(g), X, src_scale=norm, dst_scale=norm)
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     Y = host(ops.spmm(dg, dev(X), src_scale=dev(norm), dst_scale=dev(norm)))
     np.testing.assert_array_equal(Y, ref)
 
@@ -87,7 +87,7 @@ def test_row_broadcast_then_spmm_matches_fused(F):
     g = powerlaw()
     norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
     X = features(g.n_cols, F)
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     Xs = ops.row_broadcast(dev(norm), dev(X))
     np.testing.assert_array_equal(host(Xs), norm[:, None] * X)
     Y = host(ops.spmm(dg, Xs, dst_scale=dev(norm)))
@@ -101,7 +101,7 @@ def test_spmm_col_tiled(cpp, F):
     t = layout.col_tile(g, cpp)
     X = features(g.n_cols, F)
     ref = orc.spmm(to_oracle(t), X)
-    Y = host(ops.spmm(ops.DeviceGraph.from_host(t), dev(X)))
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(t, split=False), dev(X)))
     np.testing.assert_array_equal(Y, ref)
     # tiled == untiled: segments partition each row's ascending columns in order
     np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g), X))
@@ -111,7 +111,7 @@ def test_spmm_many_segments():
     g = cora_like()
     t = layout.col_tile(g, 20)   # 136 segments > 64 per launch
     X = features(g.n_cols, 32)
-    Y = host(ops.spmm(ops.DeviceGraph.from_host(t), dev(X)))
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(t, split=False), dev(X)))
     np.testing.assert_array_equal(Y, orc.spmm(to_oracle(t), X))
 
 
@@ -123,7 +123,7 @@ def test_spmm_kernel_sampled(F, tiled):
         g = layout.col_tile(g, 300)
     X = features(g.n_cols, F)
     ref = orc.spmm(to_oracle(g), X, sample=True, nsamp=20, ra=5, rb=7)
-    Y = host(ops.spmm(ops.DeviceGraph.from_host(g), dev(X), nsamp=20, ra=5, rb=7))
+    Y = host(ops.spmm(ops.DeviceGraph.from_host(g, split=False), dev(X), nsamp=20, ra=5, rb=7))
     np.testing.assert_array_equal(Y, ref)
 
 
@@ -133,7 +133,7 @@ def test_spmm_multihead_weights():
     val = edge_values(g.nnz, heads=H)
     X = features(g.n_cols, H * D)
     ref = orc.spmm(to_oracle(g, val, heads=H), X)
-    dg = ops.DeviceGraph.from_host(g).with_values(dev(val), val_heads=H)
+    dg = ops.DeviceGraph.from_host(g, split=False).with_values(dev(val), val_heads=H)
     np.testing.assert_array_equal(host(ops.spmm(dg, dev(X))), ref)
 
 
@@ -142,7 +142,7 @@ def test_spmm_multihead_weights():
 def test_degree(graph, power, weighted):
     val = edge_values(graph.nnz) if weighted else None
     ref = orc.degree(to_oracle(graph, val), power=power)
-    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val))
+    dg = ops.DeviceGraph.from_host(layout.HostGraph(graph.n_rows, graph.n_cols, graph.rowptr, graph.col, val), split=False)
     got = host(ops.degree(dg, power=power))
     if power == 1.0:
         np.testing.assert_array_equal(got, ref)
@@ -152,7 +152,7 @@ def test_degree(graph, power, weighted):
 
 def test_degree_sampled_full_op():
     g = layout.col_tile(cora_like(), 1000)
-    got = host(ops.degree(ops.DeviceGraph.from_host(g), nsamp=20))
+    got = host(ops.degree(ops.DeviceGraph.from_host(g, split=False), nsamp=20))
     np.testing.assert_array_equal(got, np.full(g.n_rows, 20.0 * g.n_seg, np.float32))
 
 
@@ -162,7 +162,7 @@ def test_sddvv(graph, op, heads):
     a = features(graph.n_rows, heads, seed=11)
     b = features(graph.n_cols, heads, seed=12)
     ref = orc.sddvv(to_oracle(graph), a, b, heads=heads, op=op, slope=0.2)
-    got = host(ops.sddvv(ops.DeviceGraph.from_host(graph), dev(a), dev(b), op=op, heads=heads, slope=0.2))
+    got = host(ops.sddvv(ops.DeviceGraph.from_host(graph, split=False), dev(a), dev(b), op=op, heads=heads, slope=0.2))
     np.testing.assert_array_equal(got, ref)
 
 
@@ -170,7 +170,7 @@ def test_sddvv(graph, op, heads):
 def test_row_sum_and_scale(graph, tiled):
     g = layout.col_tile(graph, 1000) if tiled else graph
     v = edge_values(g.nnz, seed=5)
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     got = host(ops.row_sum(dg, dev(v), eps=1e-12))
     np.testing.assert_allclose(got, orc.row_sum(to_oracle(g), v, eps=1e-12), **TOL)
     q = features(g.n_rows, 1, seed=6).ravel()
@@ -183,7 +183,7 @@ def test_row_sum_and_scale(graph, tiled):
 def test_sddmm(graph, F, heads):
     A = features(graph.n_rows, F, seed=21)
     B = features(graph.n_cols, F, seed=22)
-    got = host(ops.sddmm(ops.DeviceGraph.from_host(graph), dev(A), dev(B), heads=heads))
+    got = host(ops.sddmm(ops.DeviceGraph.from_host(graph, split=False), dev(A), dev(B), heads=heads))
     np.testing.assert_allclose(got, orc.sddmm(to_oracle(graph), A, B, heads=heads), **TOL)
 
 
@@ -192,7 +192,7 @@ def test_sddmm(graph, F, heads):
 def test_edge_softmax(graph, mode, heads):
     s = edge_values(graph.nnz, heads=heads, lo=-3, hi=3, seed=8)
     d = edge_values(graph.nnz, heads=heads, lo=-1, hi=1, seed=9)
-    dg = ops.DeviceGraph.from_host(graph)
+    dg = ops.DeviceGraph.from_host(graph, split=False)
     a = host(ops.edge_softmax(dg, dev(s), heads=heads, mode=mode))
     a_ref = orc.softmax_fwd(to_oracle(graph), s, heads=heads, mode=mode)
     np.testing.assert_allclose(a, a_ref, **TOL)
@@ -204,7 +204,7 @@ def test_edge_softmax_overflow_clamp():
     """REF mode clamps exp at 1e12 and has no max subtraction (common.h:760-761)."""
     g = cora_like()
     s = edge_values(g.nnz, lo=20, hi=40, seed=8)
-    got = host(ops.edge_softmax(ops.DeviceGraph.from_host(g), dev(s)))
+    got = host(ops.edge_softmax(ops.DeviceGraph.from_host(g, split=False), dev(s)))
     np.testing.assert_allclose(got, orc.softmax_fwd(to_oracle(g), s), **TOL)
 
 
@@ -215,7 +215,7 @@ def test_gat_fused(graph, mode, F, heads):
     aR = features(graph.n_cols, heads, seed=32)
     X = features(graph.n_cols, F, seed=33)
     Y_ref, al_ref = orc.gat_fwd(to_oracle(graph), aL, aR, X, heads=heads, slope=0.2, mode=mode)
-    Y, al = ops.gat_fwd(ops.DeviceGraph.from_host(graph), dev(aL), dev(aR), dev(X), heads=heads,
+    Y, al = ops.gat_fwd(ops.DeviceGraph.from_host(graph, split=False), dev(aL), dev(aR), dev(X), heads=heads,
                         slope=0.2, mode=mode, want_alpha=True)
     np.testing.assert_allclose(host(al), al_ref, **TOL)
     np.testing.assert_allclose(host(Y), Y_ref, **TOL)
@@ -231,7 +231,7 @@ def test_edge_permute():
 
 def test_empty_graph_and_zero_features():
     g = layout.HostGraph(5, 5, np.zeros(6, np.int32), np.zeros(0, np.int32))
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     Y = host(ops.spmm(dg, torch.ones(5, 8, device=DEV)))
     np.testing.assert_array_equal(Y, np.zeros((5, 8), np.float32))
     np.testing.assert_array_equal(host(ops.degree(dg)), np.zeros(5, np.float32))
@@ -239,7 +239,7 @@ def test_empty_graph_and_zero_features():
 
 def test_invalid_args_fail_loudly():
     g = cora_like()
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     X = torch.ones(g.n_cols, 8, device=DEV)
     with pytest.raises(_abi.GalaError):
         _abi.call("gala_spmm_f32", dg.csr(), X.data_ptr(), 4, X.data_ptr(), 8, 8, None, None, 0, 0, 0, 0, None)
@@ -259,7 +259,7 @@ def test_spmm_matches_reference_gspmm_fixtures(path):
     fx = dict(np.load(path, allow_pickle=False))
     n = int(fx["n"])
     g = layout.HostGraph(n, n, fx["rowptr"], fx["col"])
-    dg = ops.DeviceGraph.from_host(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     for k in [k for k in fx if k.startswith("Y_F") or k.startswith("Yw_F")]:
         F = int(k.split("_F")[1])
         X = dev(np.ascontiguousarray(fx["X"][:, :F]))
@@ -272,7 +272,7 @@ def test_spmm_matches_reference_gspmm_fixtures(path):
         t = layout.HostGraph(n, n, fx[k], fx[f"tile{cpp}_col"], None, len(bounds) // 2, bounds)
         F = min(int(k2[3:]) for k2 in fx if k2.startswith("Y_F"))
         X = dev(np.ascontiguousarray(fx["X"][:, :F]))
-        np.testing.assert_array_equal(host(ops.spmm(ops.DeviceGraph.from_host(t), X)), fx[f"Y_F{F}"])
+        np.testing.assert_array_equal(host(ops.spmm(ops.DeviceGraph.from_host(t, split=False), X)), fx[f"Y_F{F}"])
 
 
 # ---- hub rows (power-law): split plan ----------------------------------------------------
@@ -315,3 +315,14 @@ def test_spmm_split_with_norms_and_accum():
     ops.spmm(dg, dev(X), dst_scale=dev(norm), out=Yt, accum=True)
     ref = orc.spmm(to_oracle(g), X, dst_scale=norm, Y=Y0.copy(), accum=True)
     np.testing.assert_allclose(host(Yt), ref, **TOL)
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8)])
+def test_sddmm_split_hub_rows(F, heads):
+    g = hub_graph()
+    dg = ops.DeviceGraph.from_host(g)
+    assert dg.split_rows >= 2
+    A = features(g.n_rows, F, seed=21)
+    B = features(g.n_cols, F, seed=22)
+    got = host(ops.sddmm(dg, dev(A), dev(B), heads=heads))
+    np.testing.assert_allclose(got, orc.sddmm(to_oracle(g), A, B, heads=heads), **TOL)
