@@ -70,7 +70,6 @@ __global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, 
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
-        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const int64_t e = e0 + (t >> LH);
             const float bv = b[((int64_t)p.col[e] << LH) + h];
@@ -98,7 +97,6 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const float *vr = v + (e0 << LH);
-            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) part += vr[t];
         }
     }
@@ -122,7 +120,6 @@ __global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float 
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         float *vr = v + (e0 << LH);
-        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) vr[t] = __fmul_rn(vr[t], qv);
     }
 }
@@ -145,7 +142,6 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const float *lr = logit + (e0 << LH);
-            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) {
                 const float x = lr[t];
                 if (MODE == GALA_SOFTMAX_REF) {
@@ -177,7 +173,6 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
         const int64_t n = (e1 - e0) << LH;
         const float *lr = logit + (e0 << LH);
         float *ar = alpha + (e0 << LH);
-        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const float x = lr[t];
             const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x) : expf(x - m);
@@ -199,7 +194,6 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const int64_t o = e0 << LH;
-            #pragma unroll 4
             for (int64_t t = gl; t < n; t += G) part += __fmul_rn(alpha[o + t], dalpha[o + t]);
         }
     }
@@ -211,7 +205,6 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         const int64_t o = e0 << LH;
-        #pragma unroll 4
         for (int64_t t = gl; t < n; t += G) {
             const float a = alpha[o + t];
             const float sds = __fmul_rn(a, dalpha[o + t]);

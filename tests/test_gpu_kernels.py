@@ -286,6 +286,29 @@ def hub_graph():
     return layout.csr_build(6000, 6000, src, dst)
 
 
+def assert_reordered_sum(Y, g, X, val=None, dst_scale=None, Y0=None):
+    """Rows the split plan sums in chunks are compared with the exact (float64) sum.
+
+    A chunked fp32 sum of a 20k-edge row differs from the sequential one by rounding alone,
+    so the bound scales with the row's L1 mass: |Y - exact| <= 1e-6 * sum|A_e X_j| + 1e-6.
+    """
+    import scipy.sparse as sp
+    v = np.ones(g.nnz) if val is None else np.asarray(val, np.float64)
+    A = sp.csr_matrix((v, g.col, g.rowptr), shape=(g.n_rows, g.n_cols))
+    X64 = X.astype(np.float64)
+    exact = A @ X64
+    mass = abs(A) @ np.abs(X64)
+    if dst_scale is not None:
+        exact *= dst_scale[:, None]
+        mass *= np.abs(dst_scale)[:, None]
+    if Y0 is not None:
+        exact += Y0
+        mass += np.abs(Y0)
+    err = np.abs(Y.astype(np.float64) - exact)
+    bound = 1e-6 * mass + 1e-6
+    assert np.all(err <= bound), f"max err/bound {np.max(err / bound):.3f}"
+
+
 @pytest.mark.parametrize("F", [1, 32, 47, 256])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_split_hub_rows(F, weighted):
@@ -297,7 +320,7 @@ def test_spmm_split_hub_rows(F, weighted):
     X = features(g.n_cols, F)
     ref = orc.spmm(to_oracle(hg), X)
     Y = host(ops.spmm(dg, dev(X)))
-    np.testing.assert_allclose(Y, ref, **TOL)                  # split rows: chunked order
+    assert_reordered_sum(Y, g, X, val)                         # split rows: chunked order
     deg = np.diff(g.rowptr)
     light = deg <= 1024
     np.testing.assert_array_equal(Y[light], ref[light])       # other rows: still bit-exact
@@ -314,7 +337,9 @@ def test_spmm_split_with_norms_and_accum():
     Yt = dev(Y0)
     ops.spmm(dg, dev(X), dst_scale=dev(norm), out=Yt, accum=True)
     ref = orc.spmm(to_oracle(g), X, dst_scale=norm, Y=Y0.copy(), accum=True)
-    np.testing.assert_allclose(host(Yt), ref, **TOL)
+    light = np.diff(g.rowptr) <= 1024
+    np.testing.assert_allclose(host(Yt)[light], ref[light], **TOL)
+    assert_reordered_sum(host(Yt), g, X, dst_scale=norm.astype(np.float64), Y0=Y0)
 
 
 @pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8)])
