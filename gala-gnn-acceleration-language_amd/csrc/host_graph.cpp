@@ -260,3 +260,36 @@ extern "C" int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32
     *n_chunks = chunks;
     return GALA_OK;
 }
+
+extern "C" int gala_host_mask_subgraph(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
+                                       const int32_t *mask, int32_t *out_rowptr,
+                                       int32_t *out_col, int32_t *next_mask) {
+    // one level of getMaskSubgraphs (tests/common.h:21-110): keep the rows whose mask is
+    // set (every edge of such a row, in order), empty the rest; the next level's mask is
+    // maxAgg over the full graph, next[i] = max_{e in row i} mask[col_e] (gSpMM + maxAgg,
+    // tests/common.h:103-107), with an empty row giving 0 (maxAgg's initial value).
+    if (n_rows < 0 || !rowptr || !mask || !out_rowptr) return GALA_ERR_INVALID_ARG;
+    const int64_t nnz = rowptr[n_rows];
+    if (nnz > 0 && !col) return GALA_ERR_INVALID_ARG;
+    out_rowptr[0] = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t d = mask[r] > 0 ? rowptr[r + 1] - rowptr[r] : 0;
+        out_rowptr[r + 1] = (int32_t)(out_rowptr[r] + d);
+    }
+    if (out_col) {
+#pragma omp parallel for schedule(dynamic, 1024)
+        for (int64_t r = 0; r < n_rows; ++r) {
+            if (mask[r] <= 0) continue;
+            std::copy(col + rowptr[r], col + rowptr[r + 1], out_col + out_rowptr[r]);
+        }
+    }
+    if (next_mask) {
+#pragma omp parallel for schedule(dynamic, 1024)
+        for (int64_t r = 0; r < n_rows; ++r) {
+            int32_t m = 0;
+            for (int32_t e = rowptr[r]; e < rowptr[r + 1]; ++e) m = std::max(m, mask[col[e]]);
+            next_mask[r] = m;
+        }
+    }
+    return GALA_OK;
+}

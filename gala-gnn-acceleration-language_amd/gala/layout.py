@@ -95,6 +95,25 @@ def transpose(g: HostGraph):
     return HostGraph(g.n_cols, g.n_rows, rp, col, val), perm
 
 
+def mask_subgraphs(g: HostGraph, mask: np.ndarray, levels: int):
+    """getMaskSubgraphs (tests/common.h:21-110): level l keeps the rows within l hops
+    (through maxAgg over g) of the mask; returns [level 0, ..., level levels-1]."""
+    assert g.n_seg == 1
+    cur = np.ascontiguousarray(mask, dtype=np.int32)
+    out = []
+    for _ in range(levels):
+        rp = np.empty(g.n_rows + 1, np.int32)
+        _abi.call("gala_host_mask_subgraph", g.n_rows, _p(g.rowptr), _p(g.col), _p(cur), _p(rp),
+                  None, None)
+        col = np.empty(int(rp[-1]), np.int32)
+        nxt = np.empty(g.n_rows, np.int32)
+        _abi.call("gala_host_mask_subgraph", g.n_rows, _p(g.rowptr), _p(g.col), _p(cur), _p(rp),
+                  _p(col), _p(nxt))
+        out.append(HostGraph(g.n_rows, g.n_cols, rp, col))
+        cur = nxt
+    return out
+
+
 def gen_graph(kind: str, n: int, n_undirected: int, seed: int = 42) -> HostGraph:
     """Deterministic synthetic graph: 'uniform' (random symmetric + self loops) or 'rmat'."""
     k = {"uniform": 0, "rmat": 1}[kind]

@@ -289,6 +289,19 @@ int gala_host_csr_transpose(int64_t n_rows, int64_t n_cols, const int32_t *rowpt
 int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected, uint64_t seed,
                         int32_t *src, int32_t *dst);
 
+/*
+ * One level of the training-subgraph transformation (getMaskSubgraphs,
+ * tests/common.h:21-110; requested by middle-end.h:39-211 and emitted by
+ * codegen/common.h:480-492): out = the rows i with mask[i] > 0 (all their edges, in
+ * order), every other row empty; next_mask[i] = max over row i's edges of mask[col]
+ * (gSpMM with maxAgg) for the level below.  Two-call pattern: with out_col == NULL only
+ * out_rowptr [n_rows+1] is written (its last entry is the nnz to allocate).
+ * next_mask may be NULL.
+ */
+int gala_host_mask_subgraph(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
+                            const int32_t *mask, int32_t *out_rowptr, int32_t *out_col,
+                            int32_t *next_mask);
+
 #ifdef __cplusplus
 }
 #endif

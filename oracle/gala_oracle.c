@@ -329,3 +329,25 @@ int orc_sample_ab(int64_t n_rows, const int32_t *rowptr, const int32_t *col, con
     free(used);
     return 0;
 }
+
+/* getMaskSubgraphs, one level (tests/common.h:21-110): rows with mask > 0 keep all
+ * their edges in order, the others become empty; next[i] = max(0, max_{e in row i}
+ * mask[col_e]) (gSpMM with maxAgg into a zero-initialised vector, :103-107). */
+int orc_mask_subgraph(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
+                      const int32_t *mask, int32_t *out_rowptr, int32_t *out_col,
+                      int32_t *next) {
+    int64_t k = 0;
+    out_rowptr[0] = 0;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        if (mask[i] > 0)
+            for (int32_t e = rowptr[i]; e < rowptr[i + 1]; ++e) out_col[k++] = col[e];
+        out_rowptr[i + 1] = (int32_t)k;
+    }
+    for (int64_t i = 0; i < n_rows; ++i) {
+        int32_t m = 0;
+        for (int32_t e = rowptr[i]; e < rowptr[i + 1]; ++e)
+            if (mask[col[e]] > m) m = mask[col[e]];
+        next[i] = m;
+    }
+    return 0;
+}

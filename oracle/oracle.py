@@ -203,6 +203,22 @@ def sample_ab(g: Graph, nsamp, ra=5, rb=7):
     return Graph(g.n_rows, g.n_cols, rp, col, val)
 
 
+def mask_subgraphs(g: Graph, mask, levels):
+    """getMaskSubgraphs levels 0..levels-1 (tests/common.h:21-110)."""
+    cur = np.ascontiguousarray(mask, np.int32)
+    out = []
+    for _ in range(levels):
+        rp = np.zeros(g.n_rows + 1, np.int32)
+        col = np.zeros(max(g.nnz, 1), np.int32)
+        nxt = np.zeros(g.n_rows, np.int32)
+        rc = lib().orc_mask_subgraph(_i64(g.n_rows), _ptr(g.rowptr), _ptr(g.col), _ptr(cur),
+                                     _ptr(rp), _ptr(col), _ptr(nxt))
+        assert rc == 0
+        out.append(Graph(g.n_rows, g.n_cols, rp, col[: rp[-1]].copy(), None))
+        cur = nxt
+    return out
+
+
 # ---- reference (compiled from /root/reference) ----------------------------------------
 def ref_csr_build(n_rows, n_cols, src, dst):
     src = np.ascontiguousarray(src, np.int32)
@@ -249,6 +265,26 @@ def ref_sample_ab(g: Graph, nsamp, ra=5, rb=7):
                         _ptr(g.rowptr), _ptr(g.col), _ptr(val), ctypes.c_int(nsamp),
                         ctypes.c_int(ra), ctypes.c_int(rb), _ptr(rp), _ptr(col), _ptr(oval))
     return Graph(g.n_rows, g.n_cols, rp, col, oval)
+
+
+def ref_mask_subgraphs(g: Graph, mask, levels):
+    """Reference getMaskSubgraphs: [(fwd rowptr, fwd col, bwd rowptr, bwd col)] per level."""
+    n, nnz = g.n_rows, g.nnz
+    m = np.ascontiguousarray(mask, np.float32)
+    rp = np.zeros(levels * (n + 1), np.int32)
+    col = np.zeros(levels * max(nnz, 1), np.int32)
+    nv = np.zeros(levels, np.int32)
+    trp = np.zeros(levels * (n + 1), np.int32)
+    tcol = np.zeros(levels * max(nnz, 1), np.int32)
+    ref().ref_mask_subgraphs(ctypes.c_int(n), ctypes.c_int(nnz), _ptr(g.rowptr), _ptr(g.col),
+                             _ptr(m), ctypes.c_int(levels), _ptr(rp), _ptr(col), _ptr(nv),
+                             _ptr(trp), _ptr(tcol))
+    out = []
+    for l in range(levels):
+        k = int(nv[l])
+        out.append((rp[l * (n + 1):(l + 1) * (n + 1)].copy(), col[l * nnz:l * nnz + k].copy(),
+                    trp[l * (n + 1):(l + 1) * (n + 1)].copy(), tcol[l * nnz:l * nnz + k].copy()))
+    return out
 
 
 def ref_threads() -> int:

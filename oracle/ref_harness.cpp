@@ -12,6 +12,8 @@
 //   gSpMM + wsumAgg           src/ops/aggregators.h:12-31, 55-127
 //   static_ord_col_breakpoints + ord_col_tiling_torch  src/ops/tiling.h:1594-1608, 222-283
 //   inplace_sample_graph_ab   src/ops/tiling.h:454-508
+//   getMaskSubgraphs + buildTranspose  src/utils/common.h:26-129 (same as tests/common.h:21-124)
+#include <malloc.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,6 +24,7 @@
 #include "src/formats/dense_matrix.h"
 #include "src/ops/aggregators.h"
 #include "src/ops/tiling.h"
+#include "src/utils/common.h"
 
 typedef CSRCMatrix<int, int, float> SM;
 typedef DenseMatrix<int, int, float> DM;
@@ -124,6 +127,38 @@ extern "C" int ref_sample_ab(int nrows, int ncols, int nnz, const int *rowptr, c
     free(o0);
     free(c0);
     free(v0);
+    release_graph(A);
+    return 0;
+}
+
+extern "C" int ref_mask_subgraphs(int nrows, int nnz, const int *rowptr, const int *col,
+                                  const float *mask, int levels, int *out_rowptr, int *out_col,
+                                  int *out_nnz, int *t_rowptr, int *t_col) {
+    // the emitted SUBGRAPH_DOPT sequence (src/codegen/common.h:480-492): level l of
+    // forward_adj / backward_adj; level l's arrays start at l*(nrows+1) and l*nnz
+    SM A;
+    std::vector<float> ones(nnz, 1.0f);
+    import_graph(A, nrows, nrows, nnz, rowptr, col, ones.data());
+    DM m;
+    m.build(nrows, 1, DM::DENSE_MTX_TYPE::RM, 0);
+    memcpy(m.vals_ptr(), mask, (int64_t)nrows * sizeof(float));
+    std::vector<SM *> fwd, bwd;
+    // getMaskSubgraphs accumulates maxAgg into new_mask->build(nrows, 1, type, 0), which
+    // is an uninitialised aligned_alloc (dense_matrix.h:128-141): its result depends on
+    // what the heap hands back.  Large graphs get fresh (zero) mmap pages; here glibc's
+    // M_PERTURB fills every new allocation with perturb^0xff = 0, so the fixture records
+    // the zero-initialised accumulator the code intends.
+    mallopt(M_PERTURB, 0xff);
+    getMaskSubgraphs<SM, DM>(&A, &m, levels, fwd, bwd);
+    mallopt(M_PERTURB, 0);
+    for (int l = 0; l < levels; ++l) {
+        const int64_t nv = fwd[l]->nvals();
+        out_nnz[l] = (int)nv;
+        memcpy(out_rowptr + (int64_t)l * (nrows + 1), fwd[l]->offset_ptr(), (int64_t)(nrows + 1) * sizeof(int));
+        memcpy(out_col + (int64_t)l * nnz, fwd[l]->ids_ptr(), nv * sizeof(int));
+        memcpy(t_rowptr + (int64_t)l * (nrows + 1), bwd[l]->offset_ptr(), (int64_t)(nrows + 1) * sizeof(int));
+        memcpy(t_col + (int64_t)l * nnz, bwd[l]->ids_ptr(), nv * sizeof(int));
+    }
     release_graph(A);
     return 0;
 }

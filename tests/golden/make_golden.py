@@ -13,6 +13,7 @@ Every expected output below is produced by the reference implementation itself:
                  (src/ops/tiling.h:1594-1608, 222-283)
   sampling       inplace_sample_graph_ab(n, 5, 7) (src/ops/tiling.h:454-508)
   SpMM           gSpMM + wsumAgg (src/ops/aggregators.h:12-31,55-127)
+  subgraphs      getMaskSubgraphs + buildTranspose (src/utils/common.h:26-129)
 Inputs are seeded numpy draws, stored in the fixture next to the outputs.
 """
 import os
@@ -86,6 +87,12 @@ def make(name, n, src, dst, F_list, weighted_F, integer_x, tiles, samples):
         s = orc.ref_sample_ab(g, ns, 5, 7)
         out[f"sample{ns}_rowptr"] = s.rowptr
         out[f"sample{ns}_col"] = s.col
+    # training-subgraph levels for a 30% train mask (codegen/common.h:480-492)
+    mask = (np.random.default_rng(5).uniform(0, 1, n) < 0.3).astype(np.float32)
+    out["train_mask"] = mask
+    for lvl, (frp, fcol, trp, tcol) in enumerate(orc.ref_mask_subgraphs(g, mask, 3)):
+        out[f"sub{lvl}_rowptr"], out[f"sub{lvl}_col"] = frp, fcol
+        out[f"subT{lvl}_rowptr"], out[f"subT{lvl}_col"] = trp, tcol
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **out)
     print(f"{path}: N={n} E={col.shape[0]} keys={len(out)} {os.path.getsize(path)/1024:.0f} KiB")
