@@ -82,6 +82,13 @@ PYBIND11_MODULE(_gala_torch, m) {
     m.def("aggregate_node_mul_sum_attn_apply", &aggregate_node_mul_sum_attn_apply);
     m.def("aggregate_edge_sum_apply", &aggregate_edge_sum_apply);
     m.def("non_lnr_op_softmax_apply", &non_lnr_op_softmax_apply);
+    m.def("gcn_aggregate_apply",
+          [opt](torch::Tensor x, std::optional<torch::Tensor> pre,
+                std::optional<torch::Tensor> post, int64_t li) {
+              return gcn_aggregate_apply(x, opt(pre), opt(post), li);
+          },
+          py::arg("X"), py::arg("pre") = py::none(), py::arg("post") = py::none(),
+          py::arg("li") = 0);
     m.def("gat_aggregate_apply", &gat_aggregate_apply, py::arg("attn_l"), py::arg("attn_r"),
           py::arg("X"), py::arg("li"), py::arg("slope") = 0.2, py::arg("mode") = 0);
 }

@@ -418,9 +418,12 @@ struct AggregateNodeMulSumAttn : public torch::autograd::Function<AggregateNodeM
         const int64_t li = ctx->saved_data["li"].toInt();
         Slot s = slot(2 * li + 1);
         const int64_t nrows = s.off.numel() / s.segs - 1;
+        // fixed weights (the sparse rewrite's norm_i * norm_j) need no d alpha
+        torch::Tensor dalpha = ctx->needs_input_grad(1)
+                                   ? edge_sddmm(dZ, X, s.off, s.cols, value_graph, s.bounds, nrows, s.segs)
+                                   : torch::Tensor();
         return {aggregate_node_mul_sum_call(dZ, s.off, s.cols, value_graph, s.bounds, s.segs, true),
-                edge_sddmm(dZ, X, s.off, s.cols, value_graph, s.bounds, nrows, s.segs),
-                torch::Tensor()};
+                dalpha, torch::Tensor()};
     }
 };
 
@@ -561,7 +564,41 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
     }
 };
 
+// post * A (pre * X) with autograd: the ROW_BROADCAST / AGGREGATE / ROW_BROADCAST chain
+// of a GCN layer (or of SAGE's mean, pre undefined) as one op.  Backward is the same
+// chain on slot 2li+1: pre * A_b (post * dY), which is what autograd through the
+// reference's unfused ops computes (torch mul, <K>_AutoGrad::backward, torch mul), with
+// the same roundings.
+struct GcnAggregate : public torch::autograd::Function<GcnAggregate> {
+    static torch::Tensor run(const torch::Tensor &X, const torch::Tensor &pre,
+                             const torch::Tensor &post, const Slot &s) {
+        auto &S = global_slots();
+        torch::Tensor xs = pre.defined() ? row_broadcast(pre, X) : X.contiguous();
+        return spmm_impl(xs, s.off, s.cols, s.weighted ? &s.vals : nullptr, s.bounds, s.segs, 1,
+                         nullptr, post.defined() ? &post : nullptr, S.nsamples, S.ra, S.rb);
+    }
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor pre,
+                                 torch::Tensor post, int64_t li) {
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["pre"] = pre.defined() ? pre.detach() : pre;
+        ctx->saved_data["post"] = post.defined() ? post.detach() : post;
+        return run(X, pre, post, slot(2 * li));
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        const int64_t li = ctx->saved_data["li"].toInt();
+        auto pre = ctx->saved_data["pre"].toTensor();
+        auto post = ctx->saved_data["post"].toTensor();
+        return {run(grad_outputs[0], post, pre, slot(2 * li + 1)), torch::Tensor(),
+                torch::Tensor(), torch::Tensor()};
+    }
+};
+
 }  // namespace
+
+torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
+                                  int64_t li) {
+    return GcnAggregate::apply(X, pre, post, li);
+}
 
 torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li) {
     return AggregateNodeMulSum::apply(input_dense, li);

@@ -119,6 +119,10 @@ torch::Tensor aggregate_node_mul_sum_attn_apply(torch::Tensor input_dense,
 torch::Tensor aggregate_edge_sum_apply(torch::Tensor input_dense1, torch::Tensor input_dense2,
                                        int64_t li);
 torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li);
+// post * A (pre * X) with autograd on slot 2li (backward: pre * A_b (post * dY) on slot
+// 2li+1); pre / post may be undefined.  Honours the slot's weights and kernel sampling.
+torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
+                                  int64_t li);
 // Fused GAT aggregation with autograd (mode GALA_SOFTMAX_REF reproduces the reference's
 // forward and backward chain, GALA_SOFTMAX_FIXED the mathematically correct gradients,
 // using the slot's transposed graph).

@@ -1,0 +1,249 @@
+"""TEST INFRASTRUCTURE: a float64 torch-CPU executor for galac's IR (galac --ir-json).
+
+It gives the IR its mathematical meaning, independently of the generated C++ and of the
+HIP operators, so that
+  * CPU tests can check that the middle-end passes keep a program's meaning
+    (pre-pass vs post-pass IR on the same weights), and
+  * GPU tests can check a generated program end to end (its --dump of the first
+    forward/backward against this executor on the dumped weights and data).
+Op semantics follow the reference: AGGREGATE_MUL_SUM = A x in CSR order,
+edge softmax p = min(e^s, 1e12), alpha = p / (1e-12 + sum_row p), LeakyReLU(0.2) on the
+attention logits, (1 + eps) x for GIN's scalar, degrees = row edge counts of graph 0,
+kernel sampling = the (ra*j + rb) mod deg edge of each row (cuda.h:313-321).
+"""
+import json
+import struct
+
+import numpy as np
+import torch
+
+from gala import layout
+
+
+def read_dump(path):
+    """Reads a gala_prog --dump file (gala_runtime.cpp rt::dump)."""
+    out = {}
+    with open(path, "rb") as f:
+        assert f.read(8) == b"GALADMP1"
+        (n,) = struct.unpack("<I", f.read(4))
+        for _ in range(n):
+            (nl,) = struct.unpack("<I", f.read(4))
+            name = f.read(nl).decode()
+            code = f.read(1)[0]
+            (nd,) = struct.unpack("<I", f.read(4))
+            shape = struct.unpack("<" + "q" * nd, f.read(8 * nd)) if nd else ()
+            dt = {0: np.float32, 1: np.int64, 2: np.int32, 3: np.bool_}[code]
+            cnt = int(np.prod(shape)) if nd else 1
+            out[name] = np.frombuffer(f.read(cnt * np.dtype(dt).itemsize), dt).reshape(shape).copy()
+    return out
+
+
+def load_ir(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+def _csr(rowptr, col, n_cols, val=None):
+    rowptr = torch.as_tensor(np.asarray(rowptr, np.int64))
+    col = torch.as_tensor(np.asarray(col, np.int64))
+    v = torch.ones(col.shape[0], dtype=torch.float64) if val is None else val
+    return torch.sparse_csr_tensor(rowptr, col, v, (rowptr.shape[0] - 1, n_cols))
+
+
+def _rows(rowptr):
+    return torch.as_tensor(np.repeat(np.arange(len(rowptr) - 1), np.diff(rowptr)))
+
+
+def sampled_graph(rowptr, col, nsamp, ra, rb):
+    """The edges a kernel-sampled aggregation visits (cuda.h:313-321), in visit order."""
+    n = len(rowptr) - 1
+    deg = np.diff(rowptr)
+    rp = np.zeros(n + 1, np.int64)
+    cols = []
+    for i in range(n):
+        if deg[i] > 0:
+            j = np.arange(nsamp)
+            cols.append(col[rowptr[i] + (ra * j + rb) % deg[i]])
+            rp[i + 1] = rp[i] + nsamp
+        else:
+            rp[i + 1] = rp[i]
+    return rp, (np.concatenate(cols) if cols else np.zeros(0, np.int32))
+
+
+class Graphs:
+    """Graph g of a program: 0 = the whole graph, 1 + c = the c-th aggregation's mask
+    subgraph (level L-1-c of getMaskSubgraphs).  The backward of an aggregation on graph g
+    reads slot 2g+1 (common.h:928-978): the same matrix for graph 0 of an undirected
+    program (cuda.h:1253-1257), the transpose otherwise (buildTranspose)."""
+
+    def __init__(self, ir, rowptr, col, train_mask, ra=5, rb=7):
+        s = ir["sched"]
+        n = len(rowptr) - 1
+        self.n = n
+        self.undirected = bool(s["undirected"])
+        g = layout.HostGraph(n, n, np.asarray(rowptr, np.int32), np.asarray(col, np.int32))
+        if s["data_sample"] > 0:
+            g = layout.sample_ab(g, s["data_sample"], 5, 7)
+        graphs = [g]
+        L = ir["num_graphs"] - 1
+        if L > 0:
+            levels = layout.mask_subgraphs(g, np.asarray(train_mask, np.int32), L)
+            graphs += [levels[L - 1 - c] for c in range(L)]
+        self.host = graphs
+        self.ks = s["kernel_sample"]
+        self.ra, self.rb = ra, rb
+        self.deg0 = torch.as_tensor(np.diff(graphs[0].rowptr).astype(np.float64)).view(-1, 1)
+
+    def edges(self, gi):
+        g = self.host[gi]
+        if self.ks > 0:
+            return sampled_graph(g.rowptr, g.col, self.ks, self.ra, self.rb)
+        return g.rowptr, g.col
+
+    def matrix(self, gi, val=None):
+        rp, col = self.edges(gi)
+        return _csr(rp, col, self.n, val)
+
+    def backward_matrix(self, gi):
+        if gi == 0 and self.undirected:
+            return self.matrix(gi)
+        g = self.host[gi]
+        t, _ = layout.transpose(layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, g.col))
+        if self.ks > 0:
+            rp, col = sampled_graph(t.rowptr, t.col, self.ks, self.ra, self.rb)
+            return _csr(rp, col, self.n)
+        return _csr(t.rowptr, t.col, self.n)
+
+
+class _SlotSpmm(torch.autograd.Function):
+    """A x forward, B dY backward: the emitted <K>_AutoGrad pair (B = slot 2g+1)."""
+
+    @staticmethod
+    def forward(ctx, x, A, B):
+        ctx.B = B
+        return A @ x
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ctx.B @ dy, None, None
+
+
+class _GatRef(torch.autograd.Function):
+    """GAT aggregation with the reference's backward chain (`ref` mode):
+    dX = A_alpha dY on slot 2g+1's pattern, d alpha_e = <dY_row, X_col>,
+    ds = alpha*dalpha - alpha*(1e-12 + sum_row alpha*dalpha), dz = LeakyReLU'(z) ds,
+    daL = daR = 1e-12 + sum_row dz."""
+
+    @staticmethod
+    def forward(ctx, aL, aR, x, rp, col, n, slope):
+        rows = _rows(rp)
+        colt = torch.as_tensor(col, dtype=torch.long)
+        z = aL.view(-1)[rows] + aR.view(-1)[colt]
+        alpha = _softmax(rp, _lrelu(z, slope))
+        ctx.save_for_backward(x, alpha, z)
+        ctx.rp, ctx.col, ctx.n, ctx.slope = rp, colt, n, slope
+        return _csr(rp, col, n, alpha) @ x
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, alpha, z = ctx.saved_tensors
+        rp, col, n = ctx.rp, ctx.col, ctx.n
+        rows = _rows(rp)
+        dx = _csr(rp, col.numpy(), n, alpha) @ dy
+        dalpha = (dy[rows] * x[col]).sum(1)
+        sds = alpha * dalpha
+        acc = torch.zeros(n, dtype=dy.dtype).index_add(0, rows, sds) + 1e-12
+        ds = sds - alpha * acc[rows]
+        dz = torch.where(z > 0, ds, ds * ctx.slope)
+        da = (torch.zeros(n, dtype=dy.dtype).index_add(0, rows, dz) + 1e-12).view(-1, 1)
+        return da, da.clone(), dx, None, None, None, None
+
+
+def run(ir, graphs: Graphs, X, params, segments=1):
+    """Forward of one IR ({"pre"|"post"} part of galac --ir-json) in float64.
+    params: name -> float64 tensor (fc0.weight, fc0.bias, eps0, ...)."""
+    vals = {}
+    for nd in ir["nodes"]:
+        op, ins = nd["op"], nd["in"]
+        a = [vals[i] if i >= 0 else None for i in ins]
+        gi = nd["graph"]
+        if op == "INPUT":
+            y = X
+        elif op == "DEGREES":
+            y = graphs.deg0.clone()
+        elif op == "FULL":
+            y = torch.full((graphs.n, 1), float(nd["param"]) * segments, dtype=torch.float64)
+        elif op == "POWER":
+            y = torch.pow(a[0], nd["param"])
+        elif op == "ROW_BROADCAST":
+            y = a[0] * a[1]
+        elif op == "AGGREGATE_MUL_SUM":
+            if len(a) > 1:
+                y = graphs.matrix(gi, a[1]) @ a[0]
+            else:
+                y = _SlotSpmm.apply(a[0], graphs.matrix(gi), graphs.backward_matrix(gi))
+        elif op == "GCN_AGGREGATE":
+            x = a[0] if a[1] is None else a[1] * a[0]
+            y = _SlotSpmm.apply(x, graphs.matrix(gi), graphs.backward_matrix(gi))
+            if a[2] is not None:
+                y = a[2] * y
+        elif op == "GAT_AGGREGATE":
+            rp, col = graphs.edges(gi)
+            if ir["sched"]["gat_mode"] == 0:
+                y = _GatRef.apply(a[0], a[1], a[2], rp, col, graphs.n, nd["param"])
+            else:
+                alpha = _softmax(rp, _lrelu(a[0].view(-1)[_rows(rp)] +
+                                            a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)],
+                                            nd["param"]))
+                y = _csr(rp, col, graphs.n, alpha) @ a[2]
+        elif op == "FFN":
+            w = nd["weight"]
+            y = a[0] @ params[w + ".weight"].T + params[w + ".bias"]
+        elif op == "RELU":
+            y = torch.relu(a[0])
+        elif op == "LEAKY_RELU":
+            y = _lrelu(a[0], nd["param"])
+        elif op == "AGGREGATE_EDGE_SUM":
+            rp, col = graphs.edges(gi)
+            y = a[0].view(-1)[_rows(rp)] + a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)]
+        elif op == "AGGREGATE_EDGE_MUL":
+            rp, col = graphs.edges(gi)
+            y = a[0].view(-1)[_rows(rp)] * a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)]
+        elif op == "SOFTMAX":
+            rp, _ = graphs.edges(gi)
+            y = _softmax(rp, a[0])
+        elif op == "SCALAR_ADD_EPS_MULTIPLY":
+            y = (1 + params[nd["weight"]]) * a[0]
+        elif op == "ADD":
+            y = a[0] + a[1]
+        else:
+            raise NotImplementedError(op)
+        vals[nd["out"]] = y
+    return vals[ir["output"]]
+
+
+def _lrelu(x, slope):
+    return torch.where(x > 0, x, x * slope)
+
+
+def _softmax(rowptr, s):
+    p = torch.clamp(torch.exp(s), max=1e12)
+    rows = _rows(rowptr)
+    r = torch.zeros(len(rowptr) - 1, dtype=s.dtype).index_add(0, rows, p) + 1e-12
+    return p * (1.0 / r)[rows]
+
+
+def init_params(ir, seed=0, zero_bias=False):
+    """Random float64 weights for every weight the IR names (requires_grad)."""
+    g = torch.Generator().manual_seed(seed)
+    p = {}
+    for w in ir["weights"]:
+        if w["type"] == "linear":
+            p[w["name"] + ".weight"] = (torch.rand(w["out"], w["in"], generator=g, dtype=torch.float64) - 0.5) / np.sqrt(w["in"])
+            b = (torch.rand(w["out"], generator=g, dtype=torch.float64) - 0.5) / np.sqrt(w["in"])
+            p[w["name"] + ".bias"] = torch.zeros_like(b) if zero_bias else b
+        else:
+            p[w["name"]] = torch.tensor([float(w["init"])], dtype=torch.float64)
+    for t in p.values():
+        t.requires_grad_(True)
+    return p
