@@ -228,8 +228,10 @@ int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor va
 void GraphSlots::clear() { *this = GraphSlots(); }
 
 GraphSlots &global_slots() {
-    static GraphSlots s;
-    return s;
+    // never destroyed: device tensors must not be freed from a static destructor, after
+    // the HIP caching allocator may already be gone (process exit)
+    static GraphSlots *s = new GraphSlots();
+    return *s;
 }
 
 // ---- emitted free functions ---------------------------------------------------------------
@@ -573,15 +575,16 @@ struct GcnAggregate : public torch::autograd::Function<GcnAggregate> {
     static torch::Tensor run(const torch::Tensor &X, const torch::Tensor &pre,
                              const torch::Tensor &post, const Slot &s) {
         auto &S = global_slots();
-        torch::Tensor xs = pre.defined() ? row_broadcast(pre, X) : X.contiguous();
+        const bool has_pre = pre.numel() > 0, has_post = post.numel() > 0;
+        torch::Tensor xs = has_pre ? row_broadcast(pre, X) : X.contiguous();
         return spmm_impl(xs, s.off, s.cols, s.weighted ? &s.vals : nullptr, s.bounds, s.segs, 1,
-                         nullptr, post.defined() ? &post : nullptr, S.nsamples, S.ra, S.rb);
+                         nullptr, has_post ? &post : nullptr, S.nsamples, S.ra, S.rb);
     }
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor pre,
                                  torch::Tensor post, int64_t li) {
         ctx->saved_data["li"] = li;
-        ctx->saved_data["pre"] = pre.defined() ? pre.detach() : pre;
-        ctx->saved_data["post"] = post.defined() ? post.detach() : post;
+        ctx->saved_data["pre"] = pre.detach();
+        ctx->saved_data["post"] = post.detach();
         return run(X, pre, post, slot(2 * li));
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
@@ -597,7 +600,12 @@ struct GcnAggregate : public torch::autograd::Function<GcnAggregate> {
 
 torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
                                   int64_t li) {
-    return GcnAggregate::apply(X, pre, post, li);
+    // autograd::Function::apply needs defined tensors: an absent scale travels as a
+    // zero-element tensor
+    auto absent = [&](const torch::Tensor &t) {
+        return t.defined() ? t : torch::empty({0}, X.options().requires_grad(false));
+    };
+    return GcnAggregate::apply(X, absent(pre), absent(post), li);
 }
 
 torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li) {

@@ -50,6 +50,15 @@ def _csr(rowptr, col, n_cols, val=None):
     return torch.sparse_csr_tensor(rowptr, col, v, (rowptr.shape[0] - 1, n_cols))
 
 
+def _spmm(rowptr, col, x, w=None):
+    """sum_e w_e x[col_e] per row, differentiable in x and w (duplicate edges kept)."""
+    rows = _rows(rowptr)
+    g = x[torch.as_tensor(np.asarray(col, np.int64))]
+    if w is not None:
+        g = g * w.view(-1, 1)
+    return torch.zeros(len(rowptr) - 1, x.shape[1], dtype=x.dtype).index_add(0, rows, g)
+
+
 def _rows(rowptr):
     return torch.as_tensor(np.repeat(np.arange(len(rowptr) - 1), np.diff(rowptr)))
 
@@ -179,7 +188,8 @@ def run(ir, graphs: Graphs, X, params, segments=1):
             y = a[0] * a[1]
         elif op == "AGGREGATE_MUL_SUM":
             if len(a) > 1:
-                y = graphs.matrix(gi, a[1]) @ a[0]
+                rp, col = graphs.edges(gi)
+                y = _spmm(rp, col, a[0], a[1])
             else:
                 y = _SlotSpmm.apply(a[0], graphs.matrix(gi), graphs.backward_matrix(gi))
         elif op == "GCN_AGGREGATE":
@@ -195,7 +205,7 @@ def run(ir, graphs: Graphs, X, params, segments=1):
                 alpha = _softmax(rp, _lrelu(a[0].view(-1)[_rows(rp)] +
                                             a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)],
                                             nd["param"]))
-                y = _csr(rp, col, graphs.n, alpha) @ a[2]
+                y = _spmm(rp, col, a[2], alpha)
         elif op == "FFN":
             w = nd["weight"]
             y = a[0] @ params[w + ".weight"].T + params[w + ".bias"]

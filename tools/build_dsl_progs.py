@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Compiles every tests/dsl/*.txt program with galac and builds it (g++ over libtorch +
+"""Compiles every tests/dsl/*.txt and bench/dsl/*.txt program with galac and builds it (g++ over libtorch +
 libgala_torch.so) into gala-gnn-acceleration-language_amd/progs/<name>/gala_prog, with the
 IR next to it (ir.json) for the GPU parity tests.  Unchanged programs are not rebuilt.
 
@@ -53,7 +53,8 @@ def main(argv=None) -> int:
     ap.add_argument("-j", type=int, default=4)
     ap.add_argument("programs", nargs="*")
     a = ap.parse_args(argv)
-    srcs = a.programs or sorted(glob.glob(os.path.join(ROOT, "tests", "dsl", "*.txt")))
+    srcs = a.programs or sorted(glob.glob(os.path.join(ROOT, "tests", "dsl", "*.txt")) +
+                                glob.glob(os.path.join(ROOT, "bench", "dsl", "*.txt")))
     with cf.ThreadPoolExecutor(max_workers=a.j) as ex:
         for msg in ex.map(build_one, srcs):
             print(msg)
