@@ -67,9 +67,11 @@ PYBIND11_MODULE(_gala_torch, m) {
     m.def("row_broadcast", &row_broadcast);
     m.def("degree_norm",
           [opt](torch::Tensor off, std::optional<torch::Tensor> bounds, int64_t segments,
-                double power) { return degree_norm(off, opt(bounds), segments, power); },
+                double power, std::optional<torch::Tensor> cols) {
+              return degree_norm(off, opt(bounds), segments, power, opt(cols));
+          },
           py::arg("offset_graph"), py::arg("bounds") = py::none(), py::arg("segments") = 1,
-          py::arg("power") = -0.5);
+          py::arg("power") = -0.5, py::arg("columns_graph") = py::none());
     m.def("gcn_aggregate",
           [opt](torch::Tensor x, torch::Tensor norm, torch::Tensor off, torch::Tensor cols,
                 std::optional<torch::Tensor> bounds, int64_t segments) {

@@ -422,7 +422,7 @@ torch::Tensor sampled_degrees(int64_t nsamples) {
 torch::Tensor degrees() {
     auto &S = global_slots();
     TORCH_CHECK(!S.offset_graph.empty(), "gala: no graph registered");
-    return degree_norm(S.offset_graph[0], S.bounds[0], S.segments[0], 1.0);
+    return degree_norm(S.offset_graph[0], S.bounds[0], S.segments[0], 1.0, S.columns_graph[0]);
 }
 
 double get_time() { return omp_get_wtime(); }

@@ -345,8 +345,11 @@ torch::Tensor row_broadcast(torch::Tensor scale, torch::Tensor X) {
 }
 
 torch::Tensor degree_norm(torch::Tensor offset_graph, torch::Tensor bounds, int64_t segments,
-                          double power) {
-    auto cols = torch::empty({0}, offset_graph.options());
+                          double power, torch::Tensor columns_graph) {
+    TORCH_CHECK(segments == 1 || columns_graph.defined(),
+                "gala: degree_norm of a column-tiled graph needs its columns_graph");
+    // the degree kernel reads rowptr only; the columns give the segment bounds their range
+    auto cols = columns_graph.defined() ? columns_graph : torch::empty({0}, offset_graph.options());
     CsrView cv = view(offset_graph, cols, nullptr, bounds, segments);
     auto out = torch::empty({cv.c.n_rows, 1}, fopts(offset_graph));
     check(gala_degree_f32(&cv.c, out.data_ptr<float>(), (float)power, 0, 0, stream()),

@@ -110,7 +110,7 @@ torch::Tensor gcn_aggregate(torch::Tensor X, torch::Tensor norm, torch::Tensor o
                             int64_t segments = 1);
 torch::Tensor row_broadcast(torch::Tensor scale, torch::Tensor X);
 torch::Tensor degree_norm(torch::Tensor offset_graph, torch::Tensor bounds, int64_t segments,
-                          double power);
+                          double power, torch::Tensor columns_graph = {});
 
 // ---- emitted autograd Functions (apply() wrappers; li = layer index into the slots) ---
 torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li);
