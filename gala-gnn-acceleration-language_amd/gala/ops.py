@@ -199,3 +199,20 @@ def edge_permute(perm, src, heads=1):
     dst = torch.empty(n * heads, device=src.device, dtype=torch.float32)
     _abi.call("gala_edge_permute_f32", _dp(perm), _dp(src), n, heads, _dp(dst), _stream())
     return dst
+
+
+def dense_grad(X, dY, bias=True, dW=None, db=None, accumulate=False):
+    """FFN weight / bias gradients dW = dY^T X [M, K], db = dY.sum(0) (gala_dense_grad_f32)."""
+    X = X.contiguous()
+    dY = dY.contiguous()
+    N, K = X.shape
+    M = dY.shape[1]
+    if dW is None:
+        dW = torch.empty(M, K, device=X.device, dtype=torch.float32)
+    if bias and db is None:
+        db = torch.empty(M, device=X.device, dtype=torch.float32)
+    wsb = _abi.lib().gala_dense_grad_workspace(N, K, M)
+    ws = torch.empty(max(wsb // 4, 1), device=X.device, dtype=torch.float32)
+    _abi.call("gala_dense_grad_f32", N, K, M, _dp(X), K, _dp(dY), M, _dp(dW),
+              _dp(db) if bias else None, int(accumulate), _dp(ws), wsb, _stream())
+    return (dW, db) if bias else dW

@@ -91,6 +91,11 @@ PYBIND11_MODULE(_gala_torch, m) {
           },
           py::arg("X"), py::arg("pre") = py::none(), py::arg("post") = py::none(),
           py::arg("li") = 0);
+    m.def("ffn_apply",
+          [opt](torch::Tensor x, torch::Tensor w, std::optional<torch::Tensor> b) {
+              return ffn_apply(x, w, opt(b));
+          },
+          py::arg("X"), py::arg("weight"), py::arg("bias") = py::none());
     m.def("gat_aggregate_apply", &gat_aggregate_apply, py::arg("attn_l"), py::arg("attn_r"),
           py::arg("X"), py::arg("li"), py::arg("slope") = 0.2, py::arg("mode") = 0);
 }

@@ -599,7 +599,44 @@ struct GcnAggregate : public torch::autograd::Function<GcnAggregate> {
     }
 };
 
+// FFN_OP with the weight / bias gradients on gala_dense_grad_f32 (split over rows) and dX
+// on the library GEMM; the forward is at::linear's addmm, bit for bit.
+struct Ffn : public torch::autograd::Function<Ffn> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor weight,
+                                 torch::Tensor bias) {
+        ctx->save_for_backward({X, weight});
+        ctx->saved_data["has_bias"] = bias.defined() && bias.numel() > 0;
+        return bias.defined() && bias.numel() > 0 ? torch::addmm(bias, X, weight.t())
+                                                  : X.mm(weight.t());
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto sv = ctx->get_saved_variables();
+        torch::Tensor X = sv[0].contiguous(), W = sv[1];
+        torch::Tensor dY = grad_outputs[0].contiguous();
+        const bool has_bias = ctx->saved_data["has_bias"].toBool();
+        torch::Tensor dX = ctx->needs_input_grad(0) ? dY.mm(W) : torch::Tensor();
+        check_dev(X, torch::kFloat, "X");
+        check_dev(dY, torch::kFloat, "dY");
+        const int64_t N = X.size(0);
+        const int32_t K = (int32_t)X.size(1), M = (int32_t)dY.size(1);
+        auto dW = torch::empty({M, K}, fopts(X));
+        torch::Tensor db = has_bias ? torch::empty({M}, fopts(X)) : torch::Tensor();
+        const int64_t wsb = gala_dense_grad_workspace(N, K, M);
+        TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
+        auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(X));
+        check(gala_dense_grad_f32(N, K, M, X.data_ptr<float>(), K, dY.data_ptr<float>(), M,
+                                  dW.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, 0,
+                                  ws.data_ptr<float>(), wsb, stream()),
+              "gala_dense_grad_f32");
+        return {dX, dW, db};
+    }
+};
+
 }  // namespace
+
+torch::Tensor ffn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias) {
+    return Ffn::apply(X, weight, bias.defined() ? bias : torch::empty({0}, weight.options()));
+}
 
 torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
                                   int64_t li) {

@@ -123,6 +123,9 @@ torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li);
 // 2li+1); pre / post may be undefined.  Honours the slot's weights and kernel sampling.
 torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
                                   int64_t li);
+// FFN_OP: X W^T + b (at::linear's forward) whose weight / bias gradients run on
+// gala_dense_grad_f32; bias may be undefined.
+torch::Tensor ffn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias);
 // Fused GAT aggregation with autograd (mode GALA_SOFTMAX_REF reproduces the reference's
 // forward and backward chain, GALA_SOFTMAX_FIXED the mathematically correct gradients,
 // using the slot's transposed graph).

@@ -290,6 +290,20 @@ int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected, uint64_t 
                         int32_t *src, int32_t *dst);
 
 /*
+ * FFN (torch Linear) gradients of a tall-skinny node matrix: dW[m,k] = sum_n dY[n,m]
+ * X[n,k] ([M,K] row-major, the Linear weight layout) and, if db != NULL, db[m] =
+ * sum_n dY[n,m].  accumulate != 0 adds into dW / db.  The rows are split into chunks
+ * whose partial tiles go to `workspace` (gala_dense_grad_workspace bytes), then summed
+ * in chunk order: deterministic for given shapes.  Replaces the weight / bias part of
+ * the backward of the generated programs' FFN_OP (common.h:1188-1242; torch's generic
+ * kernels serve that backward in the reference).
+ */
+int64_t gala_dense_grad_workspace(int64_t n_rows, int32_t K, int32_t M);
+int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,
+                        const float *dY, int64_t ldy, float *dW, float *db, int32_t accumulate,
+                        void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
  * One level of the training-subgraph transformation (getMaskSubgraphs,
  * tests/common.h:21-110; requested by middle-end.h:39-211 and emitted by
  * codegen/common.h:480-492): out = the rows i with mask[i] > 0 (all their edges, in

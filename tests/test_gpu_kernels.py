@@ -351,3 +351,33 @@ def test_sddmm_split_hub_rows(F, heads):
     B = features(g.n_cols, F, seed=22)
     got = host(ops.sddmm(dg, dev(A), dev(B), heads=heads))
     np.testing.assert_allclose(got, orc.sddmm(to_oracle(g), A, B, heads=heads), **TOL)
+
+
+# ---- FFN gradients (gala_dense_grad_f32) ---------------------------------------------------
+@pytest.mark.parametrize("N,K,M", [(2708, 64, 32), (100000, 100, 32), (50000, 32, 47),
+                                   (20000, 602, 256), (33, 7, 1), (1, 1, 1), (0, 16, 8)])
+def test_dense_grad_matches_float64(N, K, M):
+    """dW = dY^T X, db = sum_n dY: |err| <= 1e-5 * sum_n |dY||X| (fp32 accumulation bound)."""
+    rng = np.random.default_rng(N + K + M)
+    X = rng.uniform(-1, 1, (N, K)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (N, M)).astype(np.float32)
+    dW, db = ops.dense_grad(dev(X), dev(dY))
+    X64, Y64 = X.astype(np.float64), dY.astype(np.float64)
+    want = Y64.T @ X64
+    mass = np.abs(Y64).T @ np.abs(X64)
+    assert np.all(np.abs(host(dW) - want) <= 1e-5 * mass + 1e-6)
+    np.testing.assert_allclose(host(db), Y64.sum(0), atol=1e-5 * max(N, 1), rtol=1e-5)
+    # deterministic: the same shapes give the same bits
+    dW2, db2 = ops.dense_grad(dev(X), dev(dY))
+    np.testing.assert_array_equal(host(dW2), host(dW))
+    np.testing.assert_array_equal(host(db2), host(db))
+
+
+def test_dense_grad_strided_accumulate_and_no_bias():
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-1, 1, (4000, 40)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (4000, 12)).astype(np.float32)
+    W0 = rng.uniform(-1, 1, (12, 40)).astype(np.float32)
+    dW = dev(W0)
+    ops.dense_grad(dev(X), dev(dY), bias=False, dW=dW, accumulate=True)
+    np.testing.assert_allclose(host(dW), W0 + dY.astype(np.float64).T @ X, atol=2e-4, rtol=1e-5)

@@ -195,3 +195,23 @@ def test_errors_are_exceptions_not_exit(E):
         E.aggregate_node_mul_sum_call(torch.ones(g.n_rows, 4), off, cols, vals)
     with pytest.raises(RuntimeError, match="slot"):
         E.aggregate_node_mul_sum_apply(torch.ones(g.n_rows, 4, device="cuda"), 7)
+
+
+def test_ffn_apply_matches_linear(E):
+    """ffn_apply: at::linear's forward bit for bit; gradients vs float64 autograd."""
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(100, 32).cuda()
+    X = torch.rand(50000, 100, device="cuda") - 0.5
+    X.requires_grad_(True)
+    Y = E.ffn_apply(X, lin.weight, lin.bias)
+    assert torch.equal(Y, lin(X))
+    g = torch.rand_like(Y) - 0.5
+    Y.backward(g)
+    X64, W64 = X.detach().double().cpu(), lin.weight.detach().double().cpu()
+    g64 = g.double().cpu()
+    np.testing.assert_allclose(lin.weight.grad.cpu().numpy(), (g64.T @ X64).numpy(), atol=1e-3, rtol=1e-4)
+    np.testing.assert_allclose(lin.bias.grad.cpu().numpy(), g64.sum(0).numpy(), atol=1e-3, rtol=1e-4)
+    np.testing.assert_allclose(X.grad.cpu().numpy(), (g64 @ W64).numpy(), atol=1e-4, rtol=1e-4)
+    # no bias
+    Z = E.ffn_apply(X.detach(), lin.weight, None)
+    assert torch.equal(Z, torch.nn.functional.linear(X.detach(), lin.weight))
