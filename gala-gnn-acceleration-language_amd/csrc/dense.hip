@@ -6,47 +6,71 @@
 // contraction runs over the N rows.  Measured on the Products GCN program, torch's bias
 // reduction over dim 0 takes 18.6 ms and the weight GEMM 3.3 ms (profiles/r01_e2e_*), for
 // 1.3 GB of input that HBM streams in ~0.2 ms.  Here the rows are split into P chunks
-// (split-K): every workgroup accumulates one 64x64 (m, k) tile of one chunk in registers
-// (4x4 per lane, both operands staged through LDS 32 rows at a time), writes the partial
-// tile, and a second kernel sums the P partials in chunk order.  Deterministic: the same
+// (split-K): every workgroup accumulates one (m, k) tile (64x64, or 32x128 for narrow M)
+// of one chunk in registers (4x4 per lane, both operands staged through LDS 32 rows at a
+// time, the next step prefetched into registers), writes the partial tile, and a second
+// kernel sums the P partials in a fixed order.  Deterministic: the same
 // shapes always use the same chunking and summation order.
 #include "gala_internal.h"
 
 namespace gala {
 namespace {
 
-constexpr int kTile = 64;    // output tile (m and k)
 constexpr int kRows = 32;    // rows staged in LDS per step
 constexpr int kPad = 4;
+constexpr int kRedLanes = 4; // lanes per output in the partial-sum reduction
 
+// One TK x TM (k, m) tile of one row chunk.  Lane layout: (TK/4) x (TM/4) = 256 lanes,
+// each owning a 4x4 register block; the next 32-row step is loaded into registers while
+// the current one is consumed from LDS.
+template <int TK, int TM>
 __global__ __launch_bounds__(kBlock) void k_tn_partial(int64_t N, int32_t K, int32_t M,
                                                        const float *__restrict__ X, int64_t ldx,
                                                        const float *__restrict__ dY, int64_t ldy,
                                                        int64_t rows_per_chunk,
                                                        float *__restrict__ part,
                                                        float *__restrict__ bpart) {
-    __shared__ float sx[kRows][kTile + kPad];
-    __shared__ float sy[kRows][kTile + kPad];
+    static_assert((TK / 4) * (TM / 4) == kBlock, "one 4x4 block per lane");
+    constexpr int LX = kRows * TK / kBlock, LY = kRows * TM / kBlock;  // staged values per lane
+    __shared__ float sx[kRows][TK + kPad];
+    __shared__ float sy[kRows][TM + kPad];
     const int t = threadIdx.x;
-    const int tk = (t & 15) * 4, tm = (t >> 4) * 4;
-    const int k0 = blockIdx.x * kTile, m0 = blockIdx.y * kTile;
+    const int tk = (t % (TK / 4)) * 4, tm = (t / (TK / 4)) * 4;
+    const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TM;
     const int64_t p = blockIdx.z;
     const int64_t r0 = p * rows_per_chunk;
     const int64_t r1 = r0 + rows_per_chunk < N ? r0 + rows_per_chunk : N;
     float acc[4][4] = {};
     float bacc[4] = {};
-    for (int64_t rb = r0; rb < r1; rb += kRows) {
-        // stage kRows x 64 of X and of dY (coalesced along the columns; zero outside)
+    float rx[LX], ry[LY];
+    auto fetch = [&](int64_t rb) {
 #pragma unroll
-        for (int i = 0; i < (kRows * kTile) / kBlock; ++i) {
-            const int e = t + i * kBlock;
-            const int r = e / kTile, c = e % kTile;
+        for (int i = 0; i < LX; ++i) {
+            const int e = t + i * kBlock, r = e / TK, c = e % TK;
             const int64_t row = rb + r;
-            const bool in_rows = row < r1;
-            sx[r][c] = (in_rows && k0 + c < K) ? X[row * ldx + k0 + c] : 0.0f;
-            sy[r][c] = (in_rows && m0 + c < M) ? dY[row * ldy + m0 + c] : 0.0f;
+            rx[i] = (row < r1 && k0 + c < K) ? X[row * ldx + k0 + c] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < LY; ++i) {
+            const int e = t + i * kBlock, r = e / TM, c = e % TM;
+            const int64_t row = rb + r;
+            ry[i] = (row < r1 && m0 + c < M) ? dY[row * ldy + m0 + c] : 0.0f;
+        }
+    };
+    if (r0 < r1) fetch(r0);
+    for (int64_t rb = r0; rb < r1; rb += kRows) {
+#pragma unroll
+        for (int i = 0; i < LX; ++i) {
+            const int e = t + i * kBlock;
+            sx[e / TK][e % TK] = rx[i];
+        }
+#pragma unroll
+        for (int i = 0; i < LY; ++i) {
+            const int e = t + i * kBlock;
+            sy[e / TM][e % TM] = ry[i];
         }
         __syncthreads();
+        if (rb + kRows < r1) fetch(rb + kRows);  // in flight during the FMAs below
 #pragma unroll 8
         for (int r = 0; r < kRows; ++r) {
             const float4 xv = *reinterpret_cast<const float4 *>(&sx[r][tk]);
@@ -81,28 +105,44 @@ __global__ __launch_bounds__(kBlock) void k_tn_partial(int64_t N, int32_t K, int
     }
 }
 
+// out[i] (+)= sum_p part[p][i]: kRedLanes lanes per output each sum a fixed residue class
+// of p in order, then lane 0 adds the kRedLanes sums in lane order (deterministic).
 __global__ __launch_bounds__(kBlock) void k_tn_reduce(int64_t count, int64_t P,
                                                       const float *__restrict__ part,
                                                       float *__restrict__ out, int accum) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= count) return;
+    constexpr int kOut = kBlock / kRedLanes;
+    __shared__ float red[kRedLanes][kOut];
+    const int o = threadIdx.x % kOut, g = threadIdx.x / kOut;
+    const int64_t i = (int64_t)blockIdx.x * kOut + o;
     float s = 0.0f;
-    for (int64_t p = 0; p < P; ++p) s += part[p * count + i];
-    out[i] = accum ? out[i] + s : s;
+    if (i < count)
+        for (int64_t p = g; p < P; p += kRedLanes) s += part[p * count + i];
+    red[g][o] = s;
+    __syncthreads();
+    if (g == 0 && i < count) {
+        float tot = red[0][o];
+#pragma unroll
+        for (int q = 1; q < kRedLanes; ++q) tot += red[q][o];
+        out[i] = accum ? out[i] + tot : tot;
+    }
 }
 
 struct Plan {
+    int tk, tm;  // tile shape
     int tiles_k, tiles_m;
     int64_t P, rows_per_chunk;
 };
 
 Plan plan_for(int64_t N, int32_t K, int32_t M) {
     Plan pl;
-    pl.tiles_k = (K + kTile - 1) / kTile;
-    pl.tiles_m = (M + kTile - 1) / kTile;
+    // narrow outputs (M <= 32, e.g. hidden 32 or 16) take a 128 x 32 tile: no idle lanes
+    pl.tm = M <= 32 ? 32 : 64;
+    pl.tk = M <= 32 ? 128 : 64;
+    pl.tiles_k = (K + pl.tk - 1) / pl.tk;
+    pl.tiles_m = (M + pl.tm - 1) / pl.tm;
     const int64_t tiles = (int64_t)pl.tiles_k * pl.tiles_m;
-    // ~8 workgroups per CU in total, each chunk a multiple of the LDS step
-    int64_t P = (2048 + tiles - 1) / tiles;
+    // ~4 workgroups per CU in total, each chunk a multiple of the LDS step
+    int64_t P = (1024 + tiles - 1) / tiles;
     const int64_t max_p = (N + kRows - 1) / kRows;
     if (P > max_p) P = max_p;
     if (P < 1) P = 1;
@@ -149,17 +189,22 @@ extern "C" int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const f
         return GALA_ERR_INVALID_ARG;
     float *part = (float *)workspace;
     float *bpart = part + pl.P * (int64_t)M * K;
-    hipLaunchKernelGGL(k_tn_partial, dim3(pl.tiles_k, pl.tiles_m, (unsigned)pl.P), dim3(kBlock), 0,
-                       hs, n_rows, K, M, X, ldx, dY, ldy, pl.rows_per_chunk, part,
-                       db ? bpart : nullptr);
+    const dim3 grid(pl.tiles_k, pl.tiles_m, (unsigned)pl.P);
+    if (pl.tm == 32)
+        hipLaunchKernelGGL((k_tn_partial<128, 32>), grid, dim3(kBlock), 0, hs, n_rows, K, M, X, ldx,
+                           dY, ldy, pl.rows_per_chunk, part, db ? bpart : nullptr);
+    else
+        hipLaunchKernelGGL((k_tn_partial<64, 64>), grid, dim3(kBlock), 0, hs, n_rows, K, M, X, ldx,
+                           dY, ldy, pl.rows_per_chunk, part, db ? bpart : nullptr);
     int st = launch_status();
     if (st) return st;
     const int64_t cw = (int64_t)M * K;
-    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((cw + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+    constexpr int kOut = kBlock / kRedLanes;
+    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((cw + kOut - 1) / kOut)), dim3(kBlock), 0,
                        hs, cw, pl.P, part, dW, accumulate);
     st = launch_status();
     if (st || !db) return st;
-    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((M + kOut - 1) / kOut)), dim3(kBlock), 0,
                        hs, (int64_t)M, pl.P, bpart, db, accumulate);
     return launch_status();
 }
