@@ -45,6 +45,13 @@ __device__ __forceinline__ void row_range(const EdgeParams &p, int s, int64_t ro
 // With HP heads (a power of two dividing G) the row's HP*deg edge values are contiguous,
 // lane g always handles head g % HP, and per-head reductions run over the xor offsets
 // G/2 .. HP.  Non-power-of-two head counts use the *_generic kernels further down.
+//
+// Register tiles: a row slice is walked in tiles of G*K values; lane g holds the values
+// t0 + g + k*G (k < K), so every lane has K coalesced loads in flight before it uses any
+// (one load per lane at a time left these kernels latency-bound: 0.5 TB/s at 8 heads).
+// When a row fits one tile, the second pass of softmax fwd/bwd runs from the registers.
+constexpr int kTileK = 8;
+
 template <int G, int HP>
 __device__ __forceinline__ float head_sum(float v) {
 #pragma unroll
@@ -58,29 +65,53 @@ __device__ __forceinline__ float head_max(float v) {
     return v;
 }
 
+// v[k] = base[t0 + gl + k*G] for indices < n, `fill` elsewhere
+template <int G, int K>
+__device__ __forceinline__ void load_tile(const float *base, int64_t n, int64_t t0, int gl,
+                                          float fill, float (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t t = t0 + gl + (int64_t)k * G;
+        v[k] = t < n ? base[t] : fill;
+    }
+}
+
 template <int G, int HP, int OP>
 __global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, const float *b,
                                                   float slope, float *out) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
     constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
     const int h = gl & (HP - 1);
     const float av = a[row * HP + h];
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
-        for (int64_t t = gl; t < n; t += G) {
-            const int64_t e = e0 + (t >> LH);
-            const float bv = b[((int64_t)p.col[e] << LH) + h];
-            float r;
-            if (OP == GALA_SDDVV_MUL) {
-                r = __fmul_rn(av, bv);
-            } else {
-                r = __fadd_rn(av, bv);
-                if (OP == GALA_SDDVV_ADD_LRELU) r = r > 0.0f ? r : __fmul_rn(r, slope);
+        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+            int32_t c[K];
+            float bv[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                c[k] = p.col[e0 + ((t < n ? t : 0) >> LH)];
             }
-            out[(e0 << LH) + t] = r;
+#pragma unroll
+            for (int k = 0; k < K; ++k) bv[k] = b[((int64_t)c[k] << LH) + h];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                if (t >= n) continue;
+                float r;
+                if (OP == GALA_SDDVV_MUL) {
+                    r = __fmul_rn(av, bv[k]);
+                } else {
+                    r = __fadd_rn(av, bv[k]);
+                    if (OP == GALA_SDDVV_ADD_LRELU) r = r > 0.0f ? r : __fmul_rn(r, slope);
+                }
+                out[(e0 << LH) + t] = r;
+            }
         }
     }
 }
@@ -90,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
                                                     int accum, float *out) {
     GALA_ROW_PROLOGUE(G);
     constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
     float part = 0.0f;
     if (row_ok) {
         for (int s = 0; s < p.seg.n; ++s) {
@@ -97,7 +129,12 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
             const float *vr = v + (e0 << LH);
-            for (int64_t t = gl; t < n; t += G) part += vr[t];
+            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+                float x[K];
+                load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
+#pragma unroll
+                for (int k = 0; k < K; ++k) part += x[k];
+            }
         }
     }
     part = head_sum<G, HP>(part);
@@ -114,13 +151,22 @@ __global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float 
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
     constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
     const float qv = q[row * HP + (gl & (HP - 1))];
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         float *vr = v + (e0 << LH);
-        for (int64_t t = gl; t < n; t += G) vr[t] = __fmul_rn(vr[t], qv);
+        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+            float x[K];
+            load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                if (t < n) vr[t] = __fmul_rn(x[k], qv);
+            }
+        }
     }
 }
 
@@ -135,22 +181,34 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
                                                         float *alpha) {
     GALA_ROW_PROLOGUE(G);
     constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
     float m = -INFINITY, sum = 0.0f;
+    float x[K];
+    bool in_regs = false;  // the whole row is in x[] (one segment, one tile)
     if (row_ok) {
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
+            in_regs = p.seg.n == 1 && n <= G * K;
             const float *lr = logit + (e0 << LH);
-            for (int64_t t = gl; t < n; t += G) {
-                const float x = lr[t];
+            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+                load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);  // exp(-inf) = 0: fill is inert
                 if (MODE == GALA_SOFTMAX_REF) {
-                    sum += ref_exp(x);
-                } else if (x > m) {  // online max / sum
-                    sum = sum * expf(m - x) + 1.0f;
-                    m = x;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) sum += ref_exp(x[k]);
                 } else {
-                    sum += expf(x - m);
+                    float mt = x[0];
+#pragma unroll
+                    for (int k = 1; k < K; ++k) mt = fmaxf(mt, x[k]);
+                    if (mt > m) {  // online max / sum
+                        sum = (m == -INFINITY) ? 0.0f : sum * expf(m - mt);
+                        m = mt;
+                    }
+                    if (m != -INFINITY) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k) sum += expf(x[k] - m);
+                    }
                 }
             }
         }
@@ -167,16 +225,33 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
         q = 1.0f / sum;
     }
     if (!row_ok) return;
+    if (in_regs) {
+        int64_t e0, e1;
+        row_range(p, 0, row, e0, e1);
+        const int64_t n = (e1 - e0) << LH;
+        float *ar = alpha + (e0 << LH);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = gl + (int64_t)k * G;
+            const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x[k]) : expf(x[k] - m);
+            if (t < n) ar[t] = __fmul_rn(pe, q);
+        }
+        return;
+    }
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         const float *lr = logit + (e0 << LH);
         float *ar = alpha + (e0 << LH);
-        for (int64_t t = gl; t < n; t += G) {
-            const float x = lr[t];
-            const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x) : expf(x - m);
-            ar[t] = __fmul_rn(pe, q);
+        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+            load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x[k]) : expf(x[k] - m);
+                if (t < n) ar[t] = __fmul_rn(pe, q);
+            }
         }
     }
 }
@@ -186,15 +261,24 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
                                                         const float *dalpha, float *dlogit) {
     GALA_ROW_PROLOGUE(G);
     constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
     const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
     float part = 0.0f;
+    float a[K], d[K];
+    bool in_regs = false;
     if (row_ok) {
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
             const int64_t n = (e1 - e0) << LH;
+            in_regs = p.seg.n == 1 && n <= G * K;
             const int64_t o = e0 << LH;
-            for (int64_t t = gl; t < n; t += G) part += __fmul_rn(alpha[o + t], dalpha[o + t]);
+            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+                load_tile<G, K>(alpha + o, n, t0, gl, 0.0f, a);
+                load_tile<G, K>(dalpha + o, n, t0, gl, 0.0f, d);
+#pragma unroll
+                for (int k = 0; k < K; ++k) part += __fmul_rn(a[k], d[k]);
+            }
         }
     }
     part = head_sum<G, HP>(part);
@@ -205,10 +289,17 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const floa
         row_range(p, s, row, e0, e1);
         const int64_t n = (e1 - e0) << LH;
         const int64_t o = e0 << LH;
-        for (int64_t t = gl; t < n; t += G) {
-            const float a = alpha[o + t];
-            const float sds = __fmul_rn(a, dalpha[o + t]);
-            dlogit[o + t] = __fsub_rn(sds, __fmul_rn(a, acc));  // sds - K8(acc)
+        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+            if (!in_regs) {
+                load_tile<G, K>(alpha + o, n, t0, gl, 0.0f, a);
+                load_tile<G, K>(dalpha + o, n, t0, gl, 0.0f, d);
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                const float sds = __fmul_rn(a[k], d[k]);
+                if (t < n) dlogit[o + t] = __fsub_rn(sds, __fmul_rn(a[k], acc));  // sds - K8(acc)
+            }
         }
     }
 }
@@ -499,6 +590,11 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[i] = 0.0f;
     float m = -INFINITY, sum = 0.0f;
+    // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
+    // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
+    // place: a contiguous re-read of the row instead of a second col -> aR gather.
+    const bool park = alpha_out != nullptr && (G % H) == 0;
+    const bool leader = park && cv && (fo % D) == 0;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
@@ -525,10 +621,14 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
                 const float *xv = reinterpret_cast<const float *>(&x[k]);
                 if (MODE == GALA_SOFTMAX_REF) {
                     const float pe = ref_exp(z);
+                    if (leader) alpha_out[(e0 + j0 + k) * H + hh] = pe;
                     sum = __fadd_rn(sum, pe);
 #pragma unroll
                     for (int i = 0; i < VEC; ++i) acc[i] = fmaf(pe, xv[i], acc[i]);
-                } else if (z > m) {
+                    continue;
+                }
+                if (leader) alpha_out[(e0 + j0 + k) * H + hh] = z;
+                if (z > m) {
                     const float r = expf(m - z);
                     sum = fmaf(sum, r, 1.0f);
 #pragma unroll
@@ -557,22 +657,28 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
         // alpha pass: lanes stride the row's contiguous (edge, head) values.  When H divides
         // G every lane keeps one head (g % H) whose (m, q) live in lane (h*D)/VEC of the group.
         const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
-        if (G % H == 0) {
+        if (park) {
             const int h = gl % H;
             const int src = gbase + (h * D) / VEC;
             const float mh = __shfl(m, src, 64);
             const float qh = __shfl(q, src, 64);
-            const float alh = aL[row * H + h];
+            // the parked values were stored by other lanes of this wave
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            constexpr int K = kTileK;
             for (int s = 0; s < p.seg.n; ++s) {
                 int64_t e0, e1;
                 row_range(p, s, row, e0, e1);
                 const int64_t n = (e1 - e0) * H;
-                for (int64_t t = gl; t < n; t += G) {
-                    const int64_t e = e0 + t / H;
-                    float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + h]);
-                    z = z > 0.0f ? z : __fmul_rn(z, slope);
-                    const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
-                    alpha_out[e0 * H + t] = __fmul_rn(pe, qh);
+                float *ar = alpha_out + e0 * H;
+                for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+                    float v[K];
+                    load_tile<G, K>(ar, n, t0, gl, 0.0f, v);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int64_t t = t0 + gl + (int64_t)k * G;
+                        const float pe = (MODE == GALA_SOFTMAX_REF) ? v[k] : expf(v[k] - mh);
+                        if (t < n) ar[t] = __fmul_rn(pe, qh);
+                    }
                 }
             }
         } else {
@@ -596,6 +702,128 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
     }
 }
 
+// ---- fused GAT backward -------------------------------------------------------------
+// Row group of G lanes over the features (VEC per lane), HW lanes per head.  Pass 1:
+// U edges per batch load col, X row slice, aR[col,h] and alpha before the head-wise dot
+// reductions; every lane of a head then holds d_alpha and accumulates the head's
+// sum(sds) (and, in REF mode, sum(m*sds) and sum(m*alpha)).  FIXED mode parks sds in
+// d_logit (head leader lane) and a second, contiguous (edge, head) pass forms dz.
+template <int G, int VEC, int U, int HW, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *aL, const float *aR,
+                                                    const float *X, int64_t ldx, const float *dY,
+                                                    int64_t lddy, int32_t F, float slope,
+                                                    const float *alpha, float *d_logit,
+                                                    float *d_aL) {
+    typedef typename GVec<VEC>::T V;
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    const int H = p.heads;
+    const int D = F / H;
+    const int f = gl * VEC;
+    const bool cv = f < F;
+    const int64_t fo = cv ? f : 0;
+    const int hh = (int)(fo / D);
+    const bool leader = cv && (fo % D) == 0;
+    const float al = aL[row * H + hh];
+    float dy[VEC];
+    {
+        const V t = *reinterpret_cast<const V *>(dY + row * lddy + fo);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dy[i] = cv ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+    }
+    const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
+    float acc = 0.0f, s_msds = 0.0f, s_ma = 0.0f;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int32_t n = (int32_t)(e1 - e0);
+        for (int32_t j0 = 0; j0 < n; j0 += U) {
+            int64_t c[U];
+            float ar[U], a[U], part[U];
+            V x[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+                c[k] = p.col[e0 + j];
+                a[k] = alpha[(e0 + j) * H + hh];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                ar[k] = aR[c[k] * H + hh];
+                x[k] = *reinterpret_cast<const V *>(X + c[k] * ldx + fo);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const float *xv = reinterpret_cast<const float *>(&x[k]);
+                float d = 0.0f;
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) d = fmaf(dy[i], xv[i], d);
+                part[k] = d;
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) part[k] = group_sum<HW>(part[k]);
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                if (j0 + k >= n) continue;
+                const float sds = __fmul_rn(a[k], part[k]);
+                acc += sds;
+                if (MODE == GALA_SOFTMAX_REF) {
+                    const bool pos = __fadd_rn(al, ar[k]) > 0.0f;
+                    s_msds += pos ? sds : __fmul_rn(sds, slope);
+                    s_ma += pos ? a[k] : __fmul_rn(a[k], slope);
+                } else if (leader) {
+                    d_logit[(e0 + j0 + k) * H + hh] = sds;
+                }
+            }
+        }
+    }
+    acc += (float)p.seg.n * eps;  // K7 on sds (common.h:793-794)
+    if (MODE == GALA_SOFTMAX_REF) {
+        // sum_row m*(sds - alpha*acc), then K7's 1e-12 per segment (common.h:662-667)
+        if (leader) d_aL[row * H + hh] = (s_msds - acc * s_ma) + (float)p.seg.n * eps;
+        return;
+    }
+    // FIXED: dz per (edge, head) from the parked sds; lane g keeps head g % H (H | G)
+    const int gbase = lane & ~(G - 1);
+    const int h = gl % H;
+    const float acch = __shfl(acc, gbase + (h * D) / VEC, 64);
+    const float alh = aL[row * H + h];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // parked by other lanes
+    constexpr int K = kTileK;
+    float rs = 0.0f;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        const int64_t n = (e1 - e0) * H;
+        float *dl = d_logit + e0 * H;
+        const float *ap = alpha + e0 * H;
+        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+            float sv[K], av[K], rv[K];
+            int32_t cc[K];
+            load_tile<G, K>(dl, n, t0, gl, 0.0f, sv);
+            load_tile<G, K>(ap, n, t0, gl, 0.0f, av);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                cc[k] = p.col[e0 + (t < n ? t : 0) / H];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) rv[k] = aR[(int64_t)cc[k] * H + h];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int64_t t = t0 + gl + (int64_t)k * G;
+                if (t >= n) continue;
+                const float ds = __fsub_rn(sv[k], __fmul_rn(av[k], acch));
+                const float dz = __fadd_rn(alh, rv[k]) > 0.0f ? ds : __fmul_rn(ds, slope);
+                dl[t] = dz;
+                rs += dz;
+            }
+        }
+    }
+    for (int o = G / 2; o >= H; o >>= 1) rs += __shfl_xor(rs, o, 64);  // lanes of head h
+    if (gl < H) d_aL[row * H + gl] = rs;
+}
+
 __global__ __launch_bounds__(kBlock) void k_permute(const int32_t *perm, const float *src,
                                                     int64_t n, int32_t H, float *dst) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -612,6 +840,15 @@ static int pick_group(const gala_csr_t *A, int heads) {
     const double avg = A->n_rows ? (double)A->nnz * heads / (double)A->n_rows : 1.0;
     int g = 4;
     while (g < 64 && 2 * g * 2 <= avg) g <<= 1;
+    return g;
+}
+
+// lanes per row for the register-tiled kernels: the smallest group whose tile (G*K
+// values) holds a mean row with 15 % slack, so most rows take one tile
+static int pick_group_tiled(const gala_csr_t *A, int heads) {
+    const double avg = A->n_rows ? (double)A->nnz * heads / (double)A->n_rows : 1.0;
+    int g = 4;
+    while (g < 64 && (double)g * kTileK < 1.15 * avg) g <<= 1;
     return g;
 }
 
@@ -679,7 +916,7 @@ extern "C" int gala_sddvv_f32(const gala_csr_t *A, const float *a_row, const flo
     hipStream_t hs = (hipStream_t)stream;
     const int hp = pow2_heads(heads);
     if (hp) {
-        const int G = std::max(pick_group(A, heads), hp);
+        const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         GALA_DISPATCH_GH(G, {
             if (op == GALA_SDDVV_ADD)
@@ -716,7 +953,7 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
     hipStream_t hs = (hipStream_t)stream;
     const int hp = pow2_heads(heads);
     if (hp) {
-        const int G = std::max(pick_group(A, heads), hp);
+        const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row));
         return launch_status();
@@ -737,7 +974,7 @@ extern "C" int gala_row_scale_f32(const gala_csr_t *A, const float *q_row, int32
     hipStream_t hs = (hipStream_t)stream;
     const int hp = pow2_heads(heads);
     if (hp) {
-        const int G = std::max(pick_group(A, heads), hp);
+        const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_scale<GG, HH>), grid, dim3(kBlock), 0, hs, p, q_row, v_inout));
         return launch_status();
@@ -760,7 +997,7 @@ extern "C" int gala_edge_softmax_fwd_f32(const gala_csr_t *A, const float *logit
     hipStream_t hs = (hipStream_t)stream;
     const int hp = pow2_heads(heads);
     if (hp) {
-        const int G = std::max(pick_group(A, heads), hp);
+        const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         GALA_DISPATCH_GH(G, {
             if (mode == GALA_SOFTMAX_REF)
@@ -793,7 +1030,7 @@ extern "C" int gala_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha
     hipStream_t hs = (hipStream_t)stream;
     const int hp = pow2_heads(heads);
     if (hp) {
-        const int G = std::max(pick_group(A, heads), hp);
+        const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         GALA_DISPATCH_GH(G, {
             if (mode == GALA_SOFTMAX_REF)
@@ -954,6 +1191,90 @@ extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const floa
     if (vec == 4) r = gat_vec<4>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
     else if (vec == 2) r = gat_vec<2>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
     else r = gat_vec<1>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    if (r) return r;
+    return launch_status();
+}
+
+template <int G, int VEC, int HW>
+static void launch_gat_bwd(const EdgeParams &p, int mode, const float *aL, const float *aR,
+                           const float *X, int64_t ldx, const float *dY, int64_t lddy, int32_t F,
+                           float slope, const float *alpha, float *d_logit, float *d_aL,
+                           hipStream_t hs) {
+    const dim3 grid(blocks_for(p.n_rows, G));
+    constexpr int U = 8;
+    constexpr int HWc = (HW < G) ? HW : G;
+    if (mode == GALA_SOFTMAX_REF)
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p,
+                           aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
+    else
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p,
+                           aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
+}
+
+template <int G, int VEC>
+static void gat_bwd_hw(const EdgeParams &p, int hw, int mode, const float *aL, const float *aR,
+                       const float *X, int64_t ldx, const float *dY, int64_t lddy, int32_t F,
+                       float slope, const float *alpha, float *d_logit, float *d_aL, hipStream_t hs) {
+#define GALA_GB(HWV) launch_gat_bwd<G, VEC, HWV>(p, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
+    switch (hw) {
+        case 1: GALA_GB(1); break;
+        case 2: GALA_GB(2); break;
+        case 4: GALA_GB(4); break;
+        case 8: GALA_GB(8); break;
+        case 16: GALA_GB(16); break;
+        case 32: GALA_GB(32); break;
+        default: GALA_GB(G); break;
+    }
+#undef GALA_GB
+}
+
+template <int VEC>
+static int gat_bwd_vec(const EdgeParams &p, int L, int hw, int mode, const float *aL,
+                       const float *aR, const float *X, int64_t ldx, const float *dY, int64_t lddy,
+                       int32_t F, float slope, const float *alpha, float *d_logit, float *d_aL,
+                       hipStream_t hs) {
+#define GALA_GBV(GV) gat_bwd_hw<GV, VEC>(p, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
+    if (L <= 1) GALA_GBV(1);
+    else if (L <= 2) GALA_GBV(2);
+    else if (L <= 4) GALA_GBV(4);
+    else if (L <= 8) GALA_GBV(8);
+    else if (L <= 16) GALA_GBV(16);
+    else if (L <= 32) GALA_GBV(32);
+    else if (L <= 64) GALA_GBV(64);
+    else return GALA_ERR_UNSUPPORTED;
+#undef GALA_GBV
+    return GALA_OK;
+}
+
+extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                const float *X, int64_t ldx, const float *dY, int64_t lddy,
+                                int32_t F, int32_t heads, float slope, int32_t mode,
+                                const float *alpha, float *d_logit, float *d_aL, void *stream) {
+    EdgeParams p;
+    int st = edge_setup(A, heads, &p);
+    if (st) return st;
+    if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
+    if (F < 1 || F % heads != 0 || ldx < F || lddy < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || !aR || !dY || !d_aL || (A->nnz > 0 && (!X || !alpha))) return GALA_ERR_INVALID_ARG;
+    if (mode == GALA_SOFTMAX_FIXED && !d_logit && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    const int D = F / heads;
+    int vec = 4;
+    while (vec > 1 && (D % vec || ldx % vec || lddy % vec || ((uintptr_t)X % (4 * vec)) ||
+                       ((uintptr_t)dY % (4 * vec))))
+        vec >>= 1;
+    const int L = (F + vec - 1) / vec;
+    int G = 1;
+    while (G < L) G <<= 1;
+    const int hw_l = D / vec;
+    if (heads > 1 && ((hw_l & (hw_l - 1)) || G % heads)) return GALA_ERR_UNSUPPORTED;
+    if (mode == GALA_SOFTMAX_FIXED && G % heads) return GALA_ERR_UNSUPPORTED;
+    const int hw = heads > 1 ? hw_l : G;
+    hipStream_t hs = (hipStream_t)stream;
+    int r;
+    if (vec == 4) r = gat_bwd_vec<4>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
+    else if (vec == 2) r = gat_bwd_vec<2>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
+    else r = gat_bwd_vec<1>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
     if (r) return r;
     return launch_status();
 }

@@ -78,6 +78,7 @@ SIGNATURES = {
     "gala_edge_softmax_fwd_f32": (ctypes.c_int, [_CSR, _P, _I32, _I32, _P, _P]),
     "gala_edge_softmax_bwd_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _P, _P]),
     "gala_gat_fwd_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _I32, _I32, _F, _I32, _P, _I64, _P, _P]),
+    "gala_gat_bwd_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _P, _I64, _I32, _I32, _F, _I32, _P, _P, _P, _P]),
     "gala_edge_permute_f32": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
     "gala_host_csr_build": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "gala_host_col_breakpoints": (ctypes.c_int64, [_I64, _I64, _P, _I64]),

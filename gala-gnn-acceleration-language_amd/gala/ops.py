@@ -194,6 +194,17 @@ def gat_fwd(g: DeviceGraph, aL, aR, X, heads=1, slope=0.2, mode=_abi.GALA_SOFTMA
     return (Y, alpha) if want_alpha else Y
 
 
+def gat_bwd(g: DeviceGraph, aL, aR, X, dY, alpha, heads=1, slope=0.2, mode=_abi.GALA_SOFTMAX_REF,
+            want_dz=False):
+    """Fused GAT edge backward (gala_gat_bwd_f32): returns (d_aL, dz or None)."""
+    F = X.shape[1]
+    d_aL = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    dz = (torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32)
+          if (want_dz or mode == _abi.GALA_SOFTMAX_FIXED) else None)
+    _abi.call("gala_gat_bwd_f32", g.csr(), _dp(aL), _dp(aR), _dp(X), X.stride(0), _dp(dY),
+              dY.stride(0), F, heads, slope, mode, _dp(alpha), _dp(dz), _dp(d_aL), _stream())
+    return d_aL, dz
+
 def edge_permute(perm, src, heads=1):
     n = perm.numel()
     dst = torch.empty(n * heads, device=src.device, dtype=torch.float32)

@@ -216,6 +216,24 @@ int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR, cons
                      int64_t ldx, int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
                      int64_t ldy, float *alpha_out, void *stream);
 
+/*
+ * Fused GAT backward over the edges of A (the forward pattern), per head h:
+ *   d_alpha[e] = <dY[row, hD:(h+1)D], X[col, hD:(h+1)D]>;  sds = alpha*d_alpha;
+ *   acc = S*eps + sum_row sds;  ds = sds - alpha*acc;
+ *   dz = ds if aL[row,h]+aR[col,h] > 0 else ds*slope       (LeakyReLU backward);
+ *   d_aL[row,h] = S*eps + sum_row dz                         (eps = 1e-12 REF, 0 FIXED).
+ * d_logit (nullable in REF mode, required in FIXED mode) receives dz per (edge, head);
+ * REF mode computes the row sum of dz as sum(m*sds) - acc*sum(m*alpha), m the LeakyReLU
+ * slope factor, in the same single pass.  Replaces the backward chain edge_sddmm ->
+ * softmax backward -> LeakyReLU backward -> node_spmv_backward_of_sddmm
+ * (cuda.h:505-524,808-845; common.h:622-675,791-799,835-894) in one kernel.  Requires
+ * heads | 64 and D/VEC a power of two when heads > 1 (else GALA_ERR_UNSUPPORTED).
+ */
+int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *X,
+                     int64_t ldx, const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                     float slope, int32_t mode, const float *alpha, float *d_logit, float *d_aL,
+                     void *stream);
+
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                           float *dst, void *stream);

@@ -169,6 +169,20 @@ def gat_fwd(g: Graph, aL, aR, X, heads=1, slope=0.2, mode=0):
     return spmm(gw, X), alpha
 
 
+def gat_bwd(g: Graph, aL, aR, X, dY, alpha, heads=1, slope=0.2, mode=0):
+    """Reference GAT edge backward on one pattern, composed from the restated kernels:
+    edge_sddmm (cuda.h:808-845) -> softmax backward (common.h:791-799) -> LeakyReLU
+    backward (torch where(z > 0, ds, ds*slope) on z = aL[row]+aR[col], common.h:1175-1184)
+    -> node_spmv_backward_of_sddmm row sum (cuda.h:505-524; eps 1e-12 in REF mode).
+    Returns (dz per (edge, head), d_aL [n_rows*heads])."""
+    dalpha = sddmm(g, dY, X, heads=heads)
+    ds = softmax_bwd(g, alpha, dalpha, heads=heads, mode=mode)
+    z = sddvv(g, aL, aR, heads=heads, op=0)
+    dz = np.where(z > 0, ds, (ds * np.float32(slope)).astype(np.float32)).astype(np.float32)
+    daL = row_sum(g, dz, heads=heads, eps=1e-12 if mode == 0 else 0.0)
+    return dz, daL
+
+
 def csr_build(n_rows, src, dst):
     src = np.ascontiguousarray(src, np.int32)
     dst = np.ascontiguousarray(dst, np.int32)

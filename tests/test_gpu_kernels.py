@@ -157,7 +157,7 @@ def test_degree_sampled_full_op():
 
 
 @pytest.mark.parametrize("op", [0, 1, 2])
-@pytest.mark.parametrize("heads", [1, 4])
+@pytest.mark.parametrize("heads", [1, 3, 4, 8])
 def test_sddvv(graph, op, heads):
     a = features(graph.n_rows, heads, seed=11)
     b = features(graph.n_cols, heads, seed=12)
@@ -167,16 +167,17 @@ def test_sddvv(graph, op, heads):
 
 
 @pytest.mark.parametrize("tiled", [False, True])
-def test_row_sum_and_scale(graph, tiled):
+@pytest.mark.parametrize("heads", [1, 3, 8])
+def test_row_sum_and_scale(graph, tiled, heads):
     g = layout.col_tile(graph, 1000) if tiled else graph
-    v = edge_values(g.nnz, seed=5)
+    v = edge_values(g.nnz, heads=heads, seed=5)
     dg = ops.DeviceGraph.from_host(g, split=False)
-    got = host(ops.row_sum(dg, dev(v), eps=1e-12))
-    np.testing.assert_allclose(got, orc.row_sum(to_oracle(g), v, eps=1e-12), **TOL)
-    q = features(g.n_rows, 1, seed=6).ravel()
+    got = host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12))
+    np.testing.assert_allclose(got, orc.row_sum(to_oracle(g), v, heads=heads, eps=1e-12), **TOL)
+    q = features(g.n_rows, heads, seed=6).ravel()
     vv = dev(v)
-    ops.row_scale_(dg, dev(q), vv)
-    np.testing.assert_array_equal(host(vv), orc.row_scale(to_oracle(g), q, v))
+    ops.row_scale_(dg, dev(q), vv, heads=heads)
+    np.testing.assert_array_equal(host(vv), orc.row_scale(to_oracle(g), q, v, heads=heads))
 
 
 @pytest.mark.parametrize("F,heads", [(1, 1), (16, 1), (32, 1), (47, 1), (100, 1), (256, 8), (64, 2)])
@@ -188,16 +189,18 @@ def test_sddmm(graph, F, heads):
 
 
 @pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
-@pytest.mark.parametrize("heads", [1, 3])
-def test_edge_softmax(graph, mode, heads):
-    s = edge_values(graph.nnz, heads=heads, lo=-3, hi=3, seed=8)
-    d = edge_values(graph.nnz, heads=heads, lo=-1, hi=1, seed=9)
-    dg = ops.DeviceGraph.from_host(graph, split=False)
+@pytest.mark.parametrize("heads", [1, 3, 8])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_edge_softmax(graph, mode, heads, tiled):
+    g = layout.col_tile(graph, 1000) if tiled else graph
+    s = edge_values(g.nnz, heads=heads, lo=-3, hi=3, seed=8)
+    d = edge_values(g.nnz, heads=heads, lo=-1, hi=1, seed=9)
+    dg = ops.DeviceGraph.from_host(g, split=False)
     a = host(ops.edge_softmax(dg, dev(s), heads=heads, mode=mode))
-    a_ref = orc.softmax_fwd(to_oracle(graph), s, heads=heads, mode=mode)
+    a_ref = orc.softmax_fwd(to_oracle(g), s, heads=heads, mode=mode)
     np.testing.assert_allclose(a, a_ref, **TOL)
     ds = host(ops.edge_softmax_bwd(dg, dev(a_ref), dev(d), heads=heads, mode=mode))
-    np.testing.assert_allclose(ds, orc.softmax_bwd(to_oracle(graph), a_ref, d, heads=heads, mode=mode), **TOL)
+    np.testing.assert_allclose(ds, orc.softmax_bwd(to_oracle(g), a_ref, d, heads=heads, mode=mode), **TOL)
 
 
 def test_edge_softmax_overflow_clamp():
@@ -219,6 +222,26 @@ def test_gat_fused(graph, mode, F, heads):
                         slope=0.2, mode=mode, want_alpha=True)
     np.testing.assert_allclose(host(al), al_ref, **TOL)
     np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4)])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_gat_bwd_fused(graph, mode, F, heads, tiled):
+    """Fused d alpha -> softmax bwd -> LeakyReLU bwd -> row sum vs the oracle chain."""
+    g = layout.col_tile(graph, 1000) if tiled else graph
+    aL = features(g.n_rows, heads, seed=41)
+    aR = features(g.n_cols, heads, seed=42)
+    X = features(g.n_cols, F, seed=43)
+    dY = features(g.n_rows, F, seed=44)
+    og = to_oracle(g)
+    _, alpha = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=mode)
+    dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, alpha, heads=heads, slope=0.2, mode=mode)
+    daL, dz = ops.gat_bwd(ops.DeviceGraph.from_host(g, split=False), dev(aL), dev(aR), dev(X), dev(dY),
+                          dev(alpha), heads=heads, slope=0.2, mode=mode)
+    np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+    if mode == _abi.GALA_SOFTMAX_FIXED:
+        np.testing.assert_allclose(host(dz), dz_ref, **TOL)
 
 
 def test_edge_permute():

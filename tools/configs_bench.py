@@ -75,10 +75,14 @@ def gat(hg):
     t0 = time.time()
     tg, perm = layout.transpose(hg)
     print(f"transpose {time.time()-t0:.1f}s", file=sys.stderr, flush=True)
+    # layer slot 0 (REF): backward slot = the forward graph (undirected, as gala.cu registers
+    # it); layer slot 1 (FIXED): backward slot = the transpose + its edge permutation
     E_.slots_clear()
     E_.slots_push(off, cols, None, None, 1, False)
+    E_.slots_push(off, cols, None, None, 1, False)
+    E_.slots_push(off, cols, None, None, 1, False)
     E_.slots_push(torch.from_numpy(tg.rowptr).cuda(), torch.from_numpy(tg.col).cuda(), None, None, 1, False)
-    E_.slots_set_transpose_perm(1, torch.from_numpy(perm).cuda())
+    E_.slots_set_transpose_perm(3, torch.from_numpy(perm).cuda())
     dg = ops.DeviceGraph.from_host(hg)
     for heads, D in ((8, 32), (1, 47), (1, 32)):
         F = heads * D
@@ -93,7 +97,7 @@ def gat(hg):
             x = X.clone().requires_grad_()
 
             def fb():
-                Y = E_.gat_aggregate_apply(l, r, x, 0, 0.2, mode)
+                Y = E_.gat_aggregate_apply(l, r, x, mode, 0.2, mode)
                 Y.backward(torch.ones_like(Y))
             t = timeit(fb, reps=5, warm=2)
             emit(config="products_gat", op="gat_layer_fwd_bwd", mode=["REF", "FIXED"][mode], heads=heads,
@@ -103,6 +107,11 @@ def gat(hg):
              ms=timeit(lambda: ops.sddvv(dg, aL, aR, op=2, heads=heads)) * 1e3)
         emit(config="products_gat", op="edge_softmax_fwd", heads=heads,
              ms=timeit(lambda: ops.edge_softmax(dg, s, heads=heads)) * 1e3)
+        emit(config="products_gat", op="edge_softmax_bwd", heads=heads,
+             ms=timeit(lambda: ops.edge_softmax_bwd(dg, s, s, heads=heads)) * 1e3)
+        for mode in (0, 1):
+            emit(config="products_gat", op="gat_bwd_fused", mode=["REF", "FIXED"][mode], heads=heads, F=F,
+                 ms=timeit(lambda: ops.gat_bwd(dg, aL, aR, X, X, s, heads=heads, mode=mode)) * 1e3)
         emit(config="products_gat", op="sddmm", heads=heads, F=F,
              ms=timeit(lambda: ops.sddmm(dg, X, X, heads=heads)) * 1e3)
         gw = dg.with_values(s, val_heads=heads)

@@ -3,7 +3,7 @@
 # kernel-trace of one of them ($PROF_PROG, default gcn_products).
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo pytest=$rc
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo pytest=$rc
 case $rc in 0|1) ;; *) exit $rc;; esac
 bash tools/gpu_dsl_bench.sh || exit $?
 P=${PROF_PROG:-gcn_products}
