@@ -1,0 +1,559 @@
+// libgala_cpu.so — host-CPU backend of the operator set (include/gala_cpu.h).
+//
+// The reference has no CPU code generator (src/codegen/cpu.h:1-7); its only CPU
+// aggregation is the gSpMM/wsumAgg pair used by its host-side tiling code
+// (src/ops/aggregators.h:12-127).  This file gives every entry point of gala_hip.h a CPU
+// counterpart with the same signature, validation and status codes, so a generated
+// program runs unchanged on the host cores when it places its tensors there (config 1 of
+// BASELINE.json: Cora GCN on CPU).  Rows are distributed over OpenMP threads; inside a
+// row the edges are accumulated in CSR order with the reference's rounding steps
+// (compiled with -ffp-contract=off; fmaf exactly where nvcc contracts the emitted
+// kernels' `a + b*c`), which makes SpMM, degree, SDDVV, row-scale and row-broadcast
+// bit-identical to libgala_hip.so.
+#include <math.h>
+#include <omp.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/gala_cpu.h"
+
+namespace {
+
+int check_csr(const gala_csr_t *A) {
+    if (!A) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows < 0 || A->n_cols < 0 || A->nnz < 0 || A->n_seg < 1) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows > 0 && !A->rowptr) return GALA_ERR_INVALID_ARG;
+    if (A->nnz > 0 && !A->col) return GALA_ERR_INVALID_ARG;
+    if (A->n_seg > 1 && !A->seg_bounds) return GALA_ERR_INVALID_ARG;
+    if (A->val && A->val_heads < 1) return GALA_ERR_INVALID_ARG;
+    if (A->nnz > INT32_MAX || A->n_rows >= INT32_MAX || A->n_cols > INT32_MAX)
+        return GALA_ERR_UNSUPPORTED;
+    for (int32_t s = 0; A->n_seg > 1 && s < A->n_seg; ++s) {
+        const int32_t b0 = A->seg_bounds[2 * s], b1 = A->seg_bounds[2 * s + 1];
+        if (b0 < 0 || b1 < b0 || b1 > A->nnz) return GALA_ERR_GRAPH;
+    }
+    return GALA_OK;
+}
+
+// edges [e0, e1) of row r in segment s (relative offsets + segment base, tiling.h:222-283)
+inline void row_range(const gala_csr_t *A, int32_t s, int64_t r, int64_t &e0, int64_t &e1) {
+    const int32_t *rp = A->rowptr + (int64_t)s * (A->n_rows + 1);
+    const int64_t base = A->n_seg == 1 ? 0 : A->seg_bounds[2 * s];
+    e0 = base + rp[r];
+    e1 = base + rp[r + 1];
+}
+
+inline float ref_exp(float s) {
+    const float p = expf(s);  // torch::exp then clamp(0, 1e12) (common.h:760-761)
+    return p > 1e12f ? 1e12f : p;
+}
+
+constexpr int64_t kRowChunk = 256;  // rows per OpenMP work item
+
+}  // namespace
+
+extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
+                                 int64_t ldy, int32_t F, const float *src_scale,
+                                 const float *dst_scale, int32_t flags, int32_t nsamp,
+                                 int32_t ra, int32_t rb, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 0 || ldx < F || ldy < F ||
+        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT)))
+        return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || F == 0) return GALA_OK;
+    if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    const bool samp = (flags & GALA_SPMM_SAMPLE) != 0;
+    if (samp && nsamp < 0) return GALA_ERR_INVALID_ARG;
+    const bool w = A->val != nullptr;
+    if (w && (A->val_heads < 1 || F % A->val_heads != 0)) return GALA_ERR_INVALID_ARG;
+    const int32_t H = w ? A->val_heads : 1, D = F / H;
+    const bool accum = (flags & GALA_SPMM_ACCUM) != 0;
+#pragma omp parallel
+    {
+        std::vector<float> acc((size_t)F);
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t r = 0; r < A->n_rows; ++r) {
+            float *a = acc.data();
+            float *yr = Y + r * ldy;
+            if (accum && !dst_scale)
+                memcpy(a, yr, sizeof(float) * (size_t)F);
+            else
+                std::fill(a, a + F, 0.0f);
+            for (int32_t s = 0; s < A->n_seg; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                const int32_t deg = (int32_t)(e1 - e0);
+                const int32_t n = samp ? (deg > 0 ? nsamp : 0) : deg;
+                for (int32_t ji = 0; ji < n; ++ji) {
+                    const int32_t j = samp ? (ra * ji + rb) % deg : ji;  // cuda.h:313-321
+                    const int64_t e = e0 + j;
+                    const int64_t c = A->col[e];
+                    const float *xr = X + c * ldx;
+                    const float sc = src_scale ? src_scale[c] : 1.0f;
+                    if (w) {
+                        for (int32_t h = 0; h < H; ++h) {
+                            const float wv = A->val[e * H + h];
+                            if (src_scale)
+                                for (int32_t f = h * D; f < (h + 1) * D; ++f) a[f] = fmaf(wv, sc * xr[f], a[f]);
+                            else
+                                for (int32_t f = h * D; f < (h + 1) * D; ++f) a[f] = fmaf(wv, xr[f], a[f]);
+                        }
+                    } else if (src_scale) {
+                        for (int32_t f = 0; f < F; ++f) a[f] = a[f] + sc * xr[f];
+                    } else {
+                        for (int32_t f = 0; f < F; ++f) a[f] = a[f] + xr[f];
+                    }
+                }
+            }
+            if (dst_scale) {
+                const float ds = dst_scale[r];
+                if (accum)
+                    for (int32_t f = 0; f < F; ++f) yr[f] = yr[f] + ds * a[f];
+                else
+                    for (int32_t f = 0; f < F; ++f) yr[f] = ds * a[f];
+            } else {
+                memcpy(yr, a, sizeof(float) * (size_t)F);
+            }
+        }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags,
+                                   int32_t nsamp, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (!deg || (flags & ~(GALA_SPMM_SAMPLE))) return GALA_ERR_INVALID_ARG;
+    const bool samp = (flags & GALA_SPMM_SAMPLE) != 0;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t r = 0; r < A->n_rows; ++r) {
+        float d;
+        if (samp) {
+            d = (float)nsamp * (float)A->n_seg;  // FULL_OP n * S (common.h:1358-1359)
+        } else if (A->val) {
+            d = 0.0f;
+            for (int32_t s = 0; s < A->n_seg; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                for (int64_t e = e0; e < e1; ++e) d = d + A->val[e];
+            }
+        } else {
+            int64_t cnt = 0;
+            for (int32_t s = 0; s < A->n_seg; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                cnt += e1 - e0;
+            }
+            d = (float)cnt;
+        }
+        if (power != 1.0f) d = (power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, power);
+        deg[r] = d;
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale,
+                                          const float *X, int64_t ldx, float *Y, int64_t ldy,
+                                          void *) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!scale || !X || !Y) return GALA_ERR_INVALID_ARG;
+#pragma omp parallel for schedule(static, 1024)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const float s = scale[r];
+        for (int32_t f = 0; f < F; ++f) Y[r * ldy + f] = s * X[r * ldx + f];
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col,
+                                  int32_t heads, int32_t op, float slope, float *out_e, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (op < GALA_SDDVV_ADD || op > GALA_SDDVV_ADD_LRELU) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
+    if (!a_row || !b_col || !out_e) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t s = 0; s < A->n_seg; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e) {
+                const int64_t c = A->col[e];
+                for (int32_t h = 0; h < H; ++h) {
+                    const float av = a_row[r * H + h], bv = b_col[c * H + h];
+                    float v;
+                    if (op == GALA_SDDVV_MUL) {
+                        v = av * bv;
+                    } else {
+                        v = av + bv;
+                        if (op == GALA_SDDVV_ADD_LRELU) v = v > 0.0f ? v : v * slope;
+                    }
+                    out_e[e * H + h] = v;
+                }
+            }
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t heads,
+                                    float eps, float *out_row, int32_t flags, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || (flags & ~GALA_SPMM_ACCUM)) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!out_row || (!v_e && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    const bool accum = (flags & GALA_SPMM_ACCUM) != 0;
+    const int32_t H = heads;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t h = 0; h < H; ++h) {
+            float c = accum ? out_row[r * H + h] : 0.0f;
+            for (int32_t s = 0; s < A->n_seg; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                float local = eps;  // each segment launch starts at 1e-12 (cuda.h:512,666)
+                for (int64_t e = e0; e < e1; ++e) local = local + v_e[e * H + h];
+                c = c + local;
+            }
+            out_row[r * H + h] = c;
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_row_scale_f32(const gala_csr_t *A, const float *q_row, int32_t heads,
+                                      float *v_inout, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
+    if (!q_row || !v_inout) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t s = 0; s < A->n_seg; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e)
+                for (int32_t h = 0; h < H; ++h) v_inout[e * H + h] = v_inout[e * H + h] * q_row[r * H + h];
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t lda,
+                                      const float *Bd, int64_t ldb, int32_t F, int32_t heads,
+                                      float *out_e, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (F < 1 || F % heads != 0 || lda < F || ldb < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
+    if (!Ad || !Bd || !out_e) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, D = F / H;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t s = 0; s < A->n_seg; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e) {
+                const float *br = Bd + (int64_t)A->col[e] * ldb;
+                for (int32_t h = 0; h < H; ++h) {
+                    float local = 0.0f;  // cuda.h:720-727, fma contracted
+                    for (int32_t k = h * D; k < (h + 1) * D; ++k) local = fmaf(Ad[r * lda + k], br[k], local);
+                    out_e[e * H + h] = local;
+                }
+            }
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_edge_softmax_fwd_f32(const gala_csr_t *A, const float *logits,
+                                             int32_t heads, int32_t mode, float *alpha, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
+    if (!logits || !alpha) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, S = A->n_seg;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t h = 0; h < H; ++h) {
+            float m = 0.0f, q;
+            if (mode == GALA_SOFTMAX_REF) {
+                // val_exp = clamp(exp(s)); row_sum = K7 (1e-12 per segment); reciprocal
+                float c = 0.0f;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    float local = 1e-12f;
+                    for (int64_t e = e0; e < e1; ++e) local = local + ref_exp(logits[e * H + h]);
+                    c = c + local;
+                }
+                q = 1.0f / c;
+            } else {
+                m = -INFINITY;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) m = fmaxf(m, logits[e * H + h]);
+                }
+                float sum = 0.0f;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) sum = sum + expf(logits[e * H + h] - m);
+                }
+                q = 1.0f / sum;
+            }
+            for (int32_t s = 0; s < S; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                for (int64_t e = e0; e < e1; ++e) {
+                    const float x = logits[e * H + h];
+                    const float pe = mode == GALA_SOFTMAX_REF ? ref_exp(x) : expf(x - m);
+                    alpha[e * H + h] = pe * q;
+                }
+            }
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha,
+                                             const float *d_alpha, int32_t heads, int32_t mode,
+                                             float *d_logits, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
+    if (!alpha || !d_alpha || !d_logits) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, S = A->n_seg;
+    const float eps = mode == GALA_SOFTMAX_REF ? 1e-12f : 0.0f;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t h = 0; h < H; ++h) {
+            float c = 0.0f;  // accum = K7(sds) (common.h:793-794)
+            for (int32_t s = 0; s < S; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                float local = eps;
+                for (int64_t e = e0; e < e1; ++e) local = local + alpha[e * H + h] * d_alpha[e * H + h];
+                c = c + local;
+            }
+            for (int32_t s = 0; s < S; ++s) {
+                int64_t e0, e1;
+                row_range(A, s, r, e0, e1);
+                for (int64_t e = e0; e < e1; ++e) {
+                    const float a = alpha[e * H + h];
+                    d_logits[e * H + h] = a * d_alpha[e * H + h] - a * c;  // sds - K8(accum)
+                }
+            }
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                    const float *X, int64_t ldx, int32_t F, int32_t heads,
+                                    float slope, int32_t mode, float *Y, int64_t ldy,
+                                    float *alpha_out, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
+    if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || !aR || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+#pragma omp parallel
+    {
+        std::vector<float> acc((size_t)D);
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t r = 0; r < A->n_rows; ++r)
+            for (int32_t h = 0; h < H; ++h) {
+                const float al = aL[r * H + h];
+                auto logit = [&](int64_t e) {
+                    float z = al + aR[(int64_t)A->col[e] * H + h];
+                    return z > 0.0f ? z : z * slope;  // LeakyReLU (common.h:1175-1184)
+                };
+                float m = 0.0f;
+                if (mode == GALA_SOFTMAX_FIXED) {
+                    m = -INFINITY;
+                    for (int32_t s = 0; s < S; ++s) {
+                        int64_t e0, e1;
+                        row_range(A, s, r, e0, e1);
+                        for (int64_t e = e0; e < e1; ++e) m = fmaxf(m, logit(e));
+                    }
+                }
+                std::fill(acc.begin(), acc.end(), 0.0f);
+                float sum = 0.0f;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) {
+                        const float z = logit(e);
+                        const float pe = mode == GALA_SOFTMAX_REF ? ref_exp(z) : expf(z - m);
+                        sum = sum + pe;
+                        const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
+                        for (int32_t f = 0; f < D; ++f) acc[f] = fmaf(pe, xr[f], acc[f]);
+                    }
+                }
+                const float den = mode == GALA_SOFTMAX_REF ? sum + (float)S * 1e-12f : sum;
+                const float q = 1.0f / den;
+                const bool empty = mode != GALA_SOFTMAX_REF && sum == 0.0f;
+                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = empty ? 0.0f : acc[f] * q;
+                if (!alpha_out) continue;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) {
+                        const float z = logit(e);
+                        const float pe = mode == GALA_SOFTMAX_REF ? ref_exp(z) : expf(z - m);
+                        alpha_out[e * H + h] = pe * q;
+                    }
+                }
+            }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                    const float *X, int64_t ldx, const float *dY, int64_t lddy,
+                                    int32_t F, int32_t heads, float slope, int32_t mode,
+                                    const float *alpha, float *d_logit, float *d_aL, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1) return GALA_ERR_INVALID_ARG;
+    if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
+    if (F < 1 || F % heads != 0 || ldx < F || lddy < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || !aR || !dY || !d_aL || (A->nnz > 0 && (!X || !alpha))) return GALA_ERR_INVALID_ARG;
+    if (mode == GALA_SOFTMAX_FIXED && !d_logit && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+    const float eps = mode == GALA_SOFTMAX_REF ? 1e-12f : 0.0f;
+#pragma omp parallel
+    {
+        std::vector<float> sds;
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t r = 0; r < A->n_rows; ++r)
+            for (int32_t h = 0; h < H; ++h) {
+                const float *dyr = dY + r * lddy + h * D;
+                // d alpha = edge_sddmm (cuda.h:808-845); sds = alpha*d alpha; acc = K7(sds)
+                float c = 0.0f;
+                sds.clear();
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    float local = eps;
+                    for (int64_t e = e0; e < e1; ++e) {
+                        const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
+                        float d = 0.0f;
+                        for (int32_t k = 0; k < D; ++k) d = fmaf(dyr[k], xr[k], d);
+                        const float v = alpha[e * H + h] * d;
+                        sds.push_back(v);
+                        local = local + v;
+                    }
+                    c = c + local;
+                }
+                // ds = sds - alpha*acc; LeakyReLU backward; K7 row sum of dz
+                float c2 = 0.0f;
+                size_t i = 0;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    float local = eps;
+                    for (int64_t e = e0; e < e1; ++e, ++i) {
+                        const float ds = sds[i] - alpha[e * H + h] * c;
+                        const float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                        const float dz = z > 0.0f ? ds : ds * slope;
+                        if (d_logit) d_logit[e * H + h] = dz;
+                        local = local + dz;
+                    }
+                    c2 = c2 + local;
+                }
+                d_aL[r * H + h] = c2;
+            }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,
+                                         int32_t heads, float *dst, void *) {
+    if (n < 0 || heads < 1) return GALA_ERR_INVALID_ARG;
+    if (n == 0) return GALA_OK;
+    if (!perm || !src || !dst) return GALA_ERR_INVALID_ARG;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t i = 0; i < n; ++i)
+        for (int32_t h = 0; h < heads; ++h) dst[i * heads + h] = src[(int64_t)perm[i] * heads + h];
+    return GALA_OK;
+}
+
+// FFN weight / bias gradients: fixed row chunks, per-chunk partial tiles, partials summed in
+// chunk order (deterministic for given shapes, like the GPU kernel pair in dense.hip)
+namespace {
+constexpr int64_t kDenseChunk = 8192;
+int64_t dense_chunks(int64_t n_rows) { return (n_rows + kDenseChunk - 1) / kDenseChunk; }
+}  // namespace
+
+extern "C" int64_t gala_cpu_dense_grad_workspace(int64_t n_rows, int32_t K, int32_t M) {
+    if (n_rows < 0 || K < 0 || M < 0) return -1;
+    if (n_rows == 0 || K == 0 || M == 0) return 0;
+    return (int64_t)sizeof(float) * dense_chunks(n_rows) * ((int64_t)M * K + M);
+}
+
+extern "C" int gala_cpu_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const float *X,
+                                       int64_t ldx, const float *dY, int64_t ldy, float *dW,
+                                       float *db, int32_t accumulate, void *workspace,
+                                       int64_t workspace_bytes, void *) {
+    if (n_rows < 0 || K < 0 || M < 0 || ldx < K || ldy < M) return GALA_ERR_INVALID_ARG;
+    if (K == 0 || M == 0) return GALA_OK;
+    if (!dW) return GALA_ERR_INVALID_ARG;
+    const int64_t MK = (int64_t)M * K;
+    if (n_rows == 0) {
+        if (!accumulate) {
+            std::fill(dW, dW + MK, 0.0f);
+            if (db) std::fill(db, db + M, 0.0f);
+        }
+        return GALA_OK;
+    }
+    if (!X || !dY || !workspace) return GALA_ERR_INVALID_ARG;
+    const int64_t P = dense_chunks(n_rows);
+    if (workspace_bytes < (int64_t)sizeof(float) * P * (MK + M)) return GALA_ERR_INVALID_ARG;
+    float *part = (float *)workspace;
+    float *bpart = part + P * MK;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t p = 0; p < P; ++p) {
+        float *w = part + p * MK;
+        float *b = bpart + p * M;
+        std::fill(w, w + MK, 0.0f);
+        std::fill(b, b + M, 0.0f);
+        const int64_t r1 = std::min(n_rows, (p + 1) * kDenseChunk);
+        for (int64_t n = p * kDenseChunk; n < r1; ++n) {
+            const float *xr = X + n * ldx;
+            for (int32_t m = 0; m < M; ++m) {
+                const float y = dY[n * ldy + m];
+                float *wm = w + (int64_t)m * K;
+                for (int32_t k = 0; k < K; ++k) wm[k] = fmaf(y, xr[k], wm[k]);
+                b[m] = b[m] + y;
+            }
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < MK; ++i) {
+        float s = 0.0f;
+        for (int64_t p = 0; p < P; ++p) s = s + part[p * MK + i];
+        dW[i] = accumulate ? dW[i] + s : s;
+    }
+    if (db)
+        for (int32_t m = 0; m < M; ++m) {
+            float s = 0.0f;
+            for (int64_t p = 0; p < P; ++p) s = s + bpart[p * M + m];
+            db[m] = accumulate ? db[m] + s : s;
+        }
+    return GALA_OK;
+}

@@ -4,6 +4,7 @@
 #include "gala_datasets.h"
 
 #include <hip/hip_runtime_api.h>
+#include <unistd.h>
 #include <omp.h>
 #include <sys/stat.h>
 
@@ -274,8 +275,9 @@ DevGraph upload(const HostCsr &g, int64_t col_tile, torch::Device dev) {
             return d;
         }
     }
-    d.off = torch::from_blob((void *)g.rowptr.data(), {g.n_rows + 1}, io).to(dev);
-    d.cols = torch::from_blob((void *)g.col.data(), {nnz}, io).to(dev);
+    // .to(dev, ..., copy=true): on the CPU device a plain .to() would alias the host vectors
+    d.off = torch::from_blob((void *)g.rowptr.data(), {g.n_rows + 1}, io).to(dev, torch::kInt, false, true);
+    d.cols = torch::from_blob((void *)g.col.data(), {nnz}, io).to(dev, torch::kInt, false, true);
     d.vals = torch::ones({nnz}, torch::TensorOptions().dtype(torch::kFloat).device(dev));
     return d;
 }
@@ -303,10 +305,23 @@ RunArgs parse_args(int argc, char **argv) {
         else if (k == "--seed") a.seed = std::stoull(val());
         else if (k == "--dump") a.dump_path = val();
         else if (k == "--quiet") a.quiet = true;
+        else if (k == "--device") a.device = val();
         else TORCH_CHECK(false, "gala: unknown option ", k);
     }
     TORCH_CHECK(a.scale > 0, "gala: --scale must be positive");
+    TORCH_CHECK(a.device == "gpu" || a.device == "cpu", "gala: --device must be gpu or cpu");
     return a;
+}
+
+torch::Device device(const RunArgs &args) {
+    if (args.device == "cpu") return torch::Device(torch::kCPU);
+    TORCH_CHECK(torch::cuda::is_available(), "gala: no GPU visible (run with --device cpu for "
+                "the host backend; there is no silent fallback)");
+    return torch::Device(torch::kCUDA, 0);
+}
+
+void sync(const torch::Device &dev) {
+    if (dev.is_cuda()) torch::cuda::synchronize();
 }
 
 Dataset load_dataset(const std::string &name, const RunArgs &args, int64_t feat_size,
@@ -384,7 +399,8 @@ int prepare_graphs(const Dataset &ds, const GraphPlan &plan, torch::Device dev) 
             if (plan.transpose_perm) {
                 TORCH_CHECK(bw.segs == 1, "gala: FIXED-mode GAT needs an untiled graph");
                 S.transpose_perm[idx] =
-                    torch::from_blob(perm.data(), {(int64_t)perm.size()}, torch::kInt).to(dev);
+                    torch::from_blob(perm.data(), {(int64_t)perm.size()}, torch::kInt)
+                        .to(dev, torch::kInt, false, true);
             }
         }
     }
@@ -434,7 +450,13 @@ double calc_mean(const std::vector<double> &v) {
     return s / (double)v.size();
 }
 
-int64_t device_memory_mb() {
+int64_t device_memory_mb(const torch::Device &dev) {
+    if (!dev.is_cuda()) {
+        std::ifstream f("/proc/self/statm");
+        int64_t pages = 0, rss = 0;
+        if (!(f >> pages >> rss)) return -1;
+        return rss * (int64_t)sysconf(_SC_PAGESIZE) / (1024 * 1024);
+    }
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -1;
     return (int64_t)((total_b - free_b) / (1024 * 1024));

@@ -29,14 +29,18 @@ namespace rt {
 //   --seed N        weight init / synthetic data seed
 //   --dump FILE     write the first forward's inputs, weights and output (parity tests)
 //   --quiet         only the reference's result line
+//   --device D      gpu (default: cuda:0, libgala_hip.so) or cpu (host cores,
+//                   libgala_cpu.so; the reference has no CPU backend, src/codegen/cpu.h)
 struct RunArgs {
-    std::string data_dir, dump_path;
+    std::string data_dir, dump_path, device = "gpu";
     bool synthetic = false, quiet = false;
     double scale = 1.0;
     int64_t iters = -1;
     uint64_t seed = 1;
 };
 RunArgs parse_args(int argc, char **argv);
+torch::Device device(const RunArgs &args);  // --device: where every tensor of the run lives
+void sync(const torch::Device &dev);         // device barrier before a timestamp (no-op on CPU)
 
 // A dataset on the host (CPU tensors).
 struct Dataset {
@@ -80,7 +84,8 @@ torch::Tensor degrees();
 
 double get_time();
 double calc_mean(const std::vector<double> &v);
-int64_t device_memory_mb();  // printMemoryUsage (cuda.h:1000-1020): used device memory
+int64_t device_memory_mb(const torch::Device &dev);  // printMemoryUsage (cuda.h:1000-1020):
+                                                     // used device memory (CPU: resident MB)
 
 // --dump: named tensors to a flat little-endian file (name, dtype, shape, bytes)
 void dump(const std::string &path,

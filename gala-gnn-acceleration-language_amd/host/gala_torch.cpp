@@ -1,6 +1,8 @@
 // C++/libtorch mirror of GALA's emitted operator API over the C ABI (see gala_torch.h).
 #include "gala_torch.h"
 
+#include "gala_cpu.h"
+
 
 #include <c10/hip/HIPStream.h>
 
@@ -10,6 +12,45 @@ namespace {
 
 void *stream() { return (void *)c10::hip::getCurrentHIPStream().stream(); }
 
+// The operator set of one device: libgala_hip.so (include/gala_hip.h) for GPU tensors,
+// libgala_cpu.so (include/gala_cpu.h) for tensors a program placed on the host
+// (--device cpu).  The graph's device selects the table; every other operand must be on
+// that device (check_on), so nothing moves between devices behind the caller's back and a
+// GPU call never runs on the CPU.
+struct Backend {
+    decltype(&gala_spmm_f32) spmm;
+    decltype(&gala_degree_f32) degree;
+    decltype(&gala_row_broadcast_f32) row_broadcast;
+    decltype(&gala_sddvv_f32) sddvv;
+    decltype(&gala_row_sum_f32) row_sum;
+    decltype(&gala_row_scale_f32) row_scale;
+    decltype(&gala_sddmm_dot_f32) sddmm;
+    decltype(&gala_edge_softmax_fwd_f32) softmax_fwd;
+    decltype(&gala_edge_softmax_bwd_f32) softmax_bwd;
+    decltype(&gala_gat_fwd_f32) gat_fwd;
+    decltype(&gala_gat_bwd_f32) gat_bwd;
+    decltype(&gala_edge_permute_f32) permute;
+    decltype(&gala_dense_grad_workspace) dense_ws;
+    decltype(&gala_dense_grad_f32) dense_grad;
+};
+const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32, gala_sddvv_f32,
+                   gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
+                   gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
+                   gala_gat_bwd_f32, gala_edge_permute_f32, gala_dense_grad_workspace,
+                   gala_dense_grad_f32};
+const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
+                   gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
+                   gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
+                   gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
+                   gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
+                   gala_cpu_dense_grad_f32};
+
+const Backend &be(const torch::Tensor &t) {
+    TORCH_CHECK(t.is_cuda() || t.is_cpu(), "gala: unsupported device ", t.device());
+    return t.is_cuda() ? kHip : kCpu;
+}
+void *stream_of(const torch::Tensor &t) { return t.is_cuda() ? stream() : nullptr; }
+
 void check(int status, const char *fn) {
     TORCH_CHECK(status == GALA_OK, "gala: ", fn, " failed: ", gala_status_string(status),
                 status == GALA_ERR_HIP ? " (hipError " + std::to_string(gala_last_hip_error()) + ")"
@@ -18,9 +59,15 @@ void check(int status, const char *fn) {
 
 void check_dev(const torch::Tensor &t, torch::ScalarType ty, const char *name) {
     TORCH_CHECK(t.defined(), "gala: ", name, " is undefined");
-    TORCH_CHECK(t.is_cuda(), "gala: ", name, " must be a device tensor (no CPU fallback)");
+    TORCH_CHECK(t.is_cuda() || t.is_cpu(), "gala: ", name, " is on unsupported device ", t.device());
     TORCH_CHECK(t.scalar_type() == ty, "gala: ", name, " has dtype ", t.scalar_type());
     TORCH_CHECK(t.is_contiguous(), "gala: ", name, " must be contiguous");
+}
+
+// operand `t` must live on the graph's device (no implicit copies, no CPU fallback)
+void check_on(const torch::Tensor &t, const torch::Tensor &graph, const char *name) {
+    TORCH_CHECK(t.device() == graph.device(), "gala: ", name, " is on ", t.device(),
+                " but the graph is on ", graph.device());
 }
 
 // A gala_csr_t view of the generated program's (offset, columns, value, bounds) tensors.
@@ -83,8 +130,9 @@ torch::Tensor row_sum_impl(const torch::Tensor &offsets, const torch::Tensor &co
     check_dev(vv, torch::kFloat, "value_graph");
     const int heads = (int)(vv.numel() / std::max<int64_t>(cols.numel(), 1));
     auto out = torch::empty({nrows, std::max(heads, 1)}, fopts(v));
-    check(gala_row_sum_f32(&cv.c, vv.data_ptr<float>(), std::max(heads, 1), eps,
-                           out.data_ptr<float>(), 0, stream()),
+    check_on(vv, offsets, "value_graph");
+    check(be(offsets).row_sum(&cv.c, vv.data_ptr<float>(), std::max(heads, 1), eps,
+                              out.data_ptr<float>(), 0, stream_of(offsets)),
           "gala_row_sum_f32");
     return out;
 }
@@ -98,8 +146,10 @@ torch::Tensor row_scale_impl(const torch::Tensor &row_val, const torch::Tensor &
     check_dev(q, torch::kFloat, "row_val");
     check_dev(value_graph, torch::kFloat, "value_graph");
     const int heads = (int)(q.numel() / std::max<int64_t>(nrows, 1));
-    check(gala_row_scale_f32(&cv.c, q.data_ptr<float>(), std::max(heads, 1),
-                             value_graph.data_ptr<float>(), stream()),
+    check_on(q, offsets, "row_val");
+    check_on(value_graph, offsets, "value_graph");
+    check(be(offsets).row_scale(&cv.c, q.data_ptr<float>(), std::max(heads, 1),
+                                value_graph.data_ptr<float>(), stream_of(offsets)),
           "gala_row_scale_f32");
     return value_graph;
 }
@@ -116,8 +166,10 @@ torch::Tensor sddvv_impl(const torch::Tensor &a, const torch::Tensor &b,
     cv.c.n_cols = bc.numel() / heads;
     auto out = heads == 1 ? torch::empty({cols.numel()}, fopts(a))
                           : torch::empty({cols.numel(), heads}, fopts(a));
-    check(gala_sddvv_f32(&cv.c, ac.data_ptr<float>(), bc.data_ptr<float>(), heads, op, slope,
-                         out.data_ptr<float>(), stream()),
+    check_on(ac, offsets, "input_dense1");
+    check_on(bc, offsets, "input_dense2");
+    check(be(offsets).sddvv(&cv.c, ac.data_ptr<float>(), bc.data_ptr<float>(), heads, op, slope,
+                            out.data_ptr<float>(), stream_of(offsets)),
           "gala_sddvv_f32");
     return out;
 }
@@ -153,9 +205,12 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
         ds = dsc.data_ptr<float>();
     }
     const int32_t flags = nsamples > 0 ? GALA_SPMM_SAMPLE : 0;
-    check(gala_spmm_f32(&cv.c, x.data_ptr<float>(), dcols, out.data_ptr<float>(), dcols,
-                        (int32_t)dcols, ss, ds, flags, (int32_t)nsamples, (int32_t)ra,
-                        (int32_t)rb, stream()),
+    check_on(x, offsets, "input_dense");
+    if (ss) check_on(ssc, offsets, "src_scale");
+    if (ds) check_on(dsc, offsets, "dst_scale");
+    check(be(offsets).spmm(&cv.c, x.data_ptr<float>(), dcols, out.data_ptr<float>(), dcols,
+                           (int32_t)dcols, ss, ds, flags, (int32_t)nsamples, (int32_t)ra,
+                           (int32_t)rb, stream_of(offsets)),
           "gala_spmm_f32");
     return out;
 }
@@ -219,7 +274,7 @@ int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor va
     if (!split.empty() && offset_graph.size() >= 2 &&
         offset_graph[offset_graph.size() - 2].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
         sp = split.back();
-    else
+    else if (offsets.is_cuda())  // the CPU backend runs every row in one sequential pass
         sp = make_split_plan(offsets, segs);
     split.push_back(sp);
     if (offset_graph.size() == 1) nrows = offsets.numel() / segs - 1;
@@ -311,8 +366,10 @@ torch::Tensor edge_sddmm(torch::Tensor input_dense1, torch::Tensor input_dense2,
     const int64_t dcols = a.numel() / std::max<int64_t>(nrows, 1);  // cuda.h:813-814
     cv.c.n_cols = b.numel() / std::max<int64_t>(dcols, 1);
     auto out = torch::empty({columns_graph.numel()}, fopts(a));
-    check(gala_sddmm_dot_f32(&cv.c, a.data_ptr<float>(), dcols, b.data_ptr<float>(), dcols,
-                             (int32_t)dcols, 1, out.data_ptr<float>(), stream()),
+    check_on(a, offset_graph, "input_dense1");
+    check_on(b, offset_graph, "input_dense2");
+    check(be(offset_graph).sddmm(&cv.c, a.data_ptr<float>(), dcols, b.data_ptr<float>(), dcols,
+                                 (int32_t)dcols, 1, out.data_ptr<float>(), stream_of(offset_graph)),
           "gala_sddmm_dot_f32");
     return out;
 }
@@ -339,8 +396,9 @@ torch::Tensor row_broadcast(torch::Tensor scale, torch::Tensor X) {
     check_dev(x, torch::kFloat, "X");
     const int64_t n = x.size(0), F = x.numel() / std::max<int64_t>(n, 1);
     auto out = torch::empty_like(x);
-    check(gala_row_broadcast_f32(n, (int32_t)F, s.data_ptr<float>(), x.data_ptr<float>(), F,
-                                 out.data_ptr<float>(), F, stream()),
+    check_on(s, x, "scale");
+    check(be(x).row_broadcast(n, (int32_t)F, s.data_ptr<float>(), x.data_ptr<float>(), F,
+                              out.data_ptr<float>(), F, stream_of(x)),
           "gala_row_broadcast_f32");
     return out;
 }
@@ -353,7 +411,8 @@ torch::Tensor degree_norm(torch::Tensor offset_graph, torch::Tensor bounds, int6
     auto cols = columns_graph.defined() ? columns_graph : torch::empty({0}, offset_graph.options());
     CsrView cv = view(offset_graph, cols, nullptr, bounds, segments);
     auto out = torch::empty({cv.c.n_rows, 1}, fopts(offset_graph));
-    check(gala_degree_f32(&cv.c, out.data_ptr<float>(), (float)power, 0, 0, stream()),
+    check(be(offset_graph).degree(&cv.c, out.data_ptr<float>(), (float)power, 0, 0,
+                                  stream_of(offset_graph)),
           "gala_degree_f32");
     return out;
 }
@@ -461,8 +520,9 @@ struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
         auto v = value_graph.contiguous();
         check_dev(v, torch::kFloat, "value_graph");
         auto alpha = torch::empty_like(v);
-        check(gala_edge_softmax_fwd_f32(&cv.c, v.data_ptr<float>(), 1, GALA_SOFTMAX_REF,
-                                        alpha.data_ptr<float>(), stream()),
+        check_on(v, s.off, "value_graph");
+        check(be(s.off).softmax_fwd(&cv.c, v.data_ptr<float>(), 1, GALA_SOFTMAX_REF,
+                                    alpha.data_ptr<float>(), stream_of(s.off)),
               "gala_edge_softmax_fwd_f32");
         ctx->save_for_backward({alpha});
         return alpha;
@@ -474,8 +534,9 @@ struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
         auto alpha = ctx->get_saved_variables()[0];
         auto d = grad_outputs[0].contiguous();
         auto ds = torch::empty_like(alpha);
-        check(gala_edge_softmax_bwd_f32(&cv.c, alpha.data_ptr<float>(), d.data_ptr<float>(), 1,
-                                        GALA_SOFTMAX_REF, ds.data_ptr<float>(), stream()),
+        check_on(d, s.off, "grad");
+        check(be(s.off).softmax_bwd(&cv.c, alpha.data_ptr<float>(), d.data_ptr<float>(), 1,
+                                    GALA_SOFTMAX_REF, ds.data_ptr<float>(), stream_of(s.off)),
               "gala_edge_softmax_bwd_f32");
         return {ds, torch::Tensor()};
     }
@@ -483,8 +544,9 @@ struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
 
 torch::Tensor permute_edges(const torch::Tensor &perm, const torch::Tensor &v, int heads) {
     auto out = torch::empty_like(v);
-    check(gala_edge_permute_f32(perm.data_ptr<int32_t>(), v.data_ptr<float>(), perm.numel(), heads,
-                                out.data_ptr<float>(), stream()),
+    check_on(v, perm, "edge values");
+    check(be(perm).permute(perm.data_ptr<int32_t>(), v.data_ptr<float>(), perm.numel(), heads,
+                           out.data_ptr<float>(), stream_of(perm)),
           "gala_edge_permute_f32");
     return out;
 }
@@ -511,9 +573,12 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         cv.c.n_cols = x.size(0);
         auto Y = torch::empty({nrows, F}, fopts(x));
         auto alpha = torch::empty({s.cols.numel() * heads}, fopts(x));
-        check(gala_gat_fwd_f32(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
+        check_on(l, s.off, "attn_l");
+        check_on(r, s.off, "attn_r");
+        check_on(x, s.off, "X");
+        check(be(s.off).gat_fwd(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
                                F, (int32_t)F, heads, (float)slope, (int32_t)mode,
-                               Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream()),
+                               Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream_of(s.off)),
               "gala_gat_fwd_f32");
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
@@ -534,6 +599,7 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
         CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
         cf.c.n_cols = x.size(0);
+        check_on(dY, fw.off, "grad");
         const bool fixed = mode == GALA_SOFTMAX_FIXED;
         TORCH_CHECK(!fixed || bw.perm.defined(),
                     "gala: FIXED-mode GAT backward needs the transposed graph and its edge "
@@ -550,12 +616,12 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         if (fixed || same) {
             auto daL = torch::empty_like(l);
             torch::Tensor dz = fixed ? torch::empty_like(alpha) : torch::Tensor();
-            const int st = gala_gat_bwd_f32(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(),
+            const int st = be(fw.off).gat_bwd(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(),
                                             x.data_ptr<float>(), F, dY.data_ptr<float>(), F,
                                             (int32_t)F, heads, (float)slope, (int32_t)mode,
                                             alpha.data_ptr<float>(),
                                             fixed ? dz.data_ptr<float>() : nullptr,
-                                            daL.data_ptr<float>(), stream());
+                                            daL.data_ptr<float>(), stream_of(fw.off));
             if (st != GALA_ERR_UNSUPPORTED) {
                 check(st, "gala_gat_bwd_f32");
                 torch::Tensor daR = daL;
@@ -573,17 +639,17 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         CsrView cp = view(ps.off, ps.cols, nullptr, ps.bounds, ps.segs);
         cp.c.n_cols = x.size(0);
         auto dalpha = torch::empty_like(alpha);
-        check(gala_sddmm_dot_f32(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
-                                 (int32_t)F, heads, dalpha.data_ptr<float>(), stream()),
+        check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
+                                 (int32_t)F, heads, dalpha.data_ptr<float>(), stream_of(ps.off)),
               "gala_sddmm_dot_f32");
         auto ds = torch::empty_like(alpha);
-        check(gala_edge_softmax_bwd_f32(&cp.c, alpha.data_ptr<float>(), dalpha.data_ptr<float>(),
-                                        heads, (int32_t)mode, ds.data_ptr<float>(), stream()),
+        check(be(ps.off).softmax_bwd(&cp.c, alpha.data_ptr<float>(), dalpha.data_ptr<float>(),
+                                        heads, (int32_t)mode, ds.data_ptr<float>(), stream_of(ps.off)),
               "gala_edge_softmax_bwd_f32");
         // LeakyReLU backward on the recomputed logits z = aL[row] + aR[col]
         auto z = torch::empty_like(alpha);
-        check(gala_sddvv_f32(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(), heads,
-                             GALA_SDDVV_ADD, 0.0f, z.data_ptr<float>(), stream()),
+        check(be(fw.off).sddvv(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(), heads,
+                             GALA_SDDVV_ADD, 0.0f, z.data_ptr<float>(), stream_of(fw.off)),
               "gala_sddvv_f32");
         auto dz = torch::where(z > 0, ds, ds * slope).contiguous();
         torch::Tensor daL, daR;
@@ -654,12 +720,14 @@ struct Ffn : public torch::autograd::Function<Ffn> {
         const int32_t K = (int32_t)X.size(1), M = (int32_t)dY.size(1);
         auto dW = torch::empty({M, K}, fopts(X));
         torch::Tensor db = has_bias ? torch::empty({M}, fopts(X)) : torch::Tensor();
-        const int64_t wsb = gala_dense_grad_workspace(N, K, M);
+        check_on(dY, X, "dY");
+        const Backend &B = be(X);
+        const int64_t wsb = B.dense_ws(N, K, M);
         TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
         auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(X));
-        check(gala_dense_grad_f32(N, K, M, X.data_ptr<float>(), K, dY.data_ptr<float>(), M,
-                                  dW.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, 0,
-                                  ws.data_ptr<float>(), wsb, stream()),
+        check(B.dense_grad(N, K, M, X.data_ptr<float>(), K, dY.data_ptr<float>(), M,
+                           dW.data_ptr<float>(), has_bias ? db.data_ptr<float>() : nullptr, 0,
+                           ws.data_ptr<float>(), wsb, stream_of(X)),
               "gala_dense_grad_f32");
         return {dX, dW, db};
     }

@@ -1,0 +1,64 @@
+"""Shared driver for the galac-generated test programs (tests/dsl/*.txt, built by
+tools/build_dsl_progs.py): run one with --dump and check its first epoch against
+tests/_ir_ref.py executing the program's post-pass IR in float64 on the same weights,
+with the backward semantics of the reference's emitted autograd classes (slot 2g+1; GAT
+`ref` chain).  Tolerance (fp32 vs float64): |got - want| <= 1e-4 + 1e-4 |want| for
+predictions and the loss, <= 1e-4 * max|want| + 1e-6 * (largest gradient of the model)
+for each gradient.  Rows outside the training subgraph are not compared (the reference
+computes them on purpose-incomplete graphs)."""
+import glob
+import os
+import re
+import subprocess
+
+import numpy as np
+import torch
+
+import _ir_ref as ref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "gala-gnn-acceleration-language_amd")
+# the tests/dsl programs only (bench/dsl programs are full-size configs)
+PROGS = sorted(os.path.splitext(os.path.basename(p))[0]
+               for p in glob.glob(os.path.join(HERE, "dsl", "*.txt"))
+               if os.path.exists(os.path.join(PKG, "progs", os.path.splitext(os.path.basename(p))[0],
+                                              "gala_prog")))
+RESULT = re.compile(r"^-?[0-9.e+-]+,-?[0-9.e+-]+$")
+
+
+def run_prog(name, tmp_path, *extra, timeout=300):
+    exe = os.path.join(PKG, "progs", name, "gala_prog")
+    dump = tmp_path / f"{name}.dump"
+    r = subprocess.run([exe, "--synthetic", "--seed", "3", "--dump", str(dump), *extra],
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    last = r.stdout.strip().splitlines()[-1]
+    assert RESULT.match(last), r.stdout
+    return r.stdout, ref.read_dump(str(dump))
+
+
+def check_against_ir(name, d):
+    ir = ref.load_ir(os.path.join(PKG, "progs", name, "ir.json"))["post"]
+    if ir["sched"]["dynamic_sample"]:
+        assert np.isfinite(d["loss"]).all()
+        return
+    graphs = ref.Graphs(ir, d["rowptr"], d["col"], d["train_mask"].astype(np.int32))
+    X = torch.as_tensor(d["t_iden"], dtype=torch.float64)
+    params = {k[6:]: torch.tensor(v, dtype=torch.float64, requires_grad=True)
+              for k, v in d.items() if k.startswith("param:")}
+    pred = ref.run(ir, graphs, X, params)
+    train = torch.as_tensor(d["train_mask"])
+    np.testing.assert_allclose(d["prediction"][d["train_mask"]], pred[train].detach().numpy(),
+                               rtol=1e-4, atol=1e-4)
+    loss = torch.nn.functional.cross_entropy(pred[train], torch.as_tensor(d["labels"])[train])
+    np.testing.assert_allclose(float(d["loss"]), loss.item(), rtol=1e-4, atol=1e-5)
+    loss.backward()
+    # noise floor: 1e-6 of the largest gradient of the model (the reference's `ref` GAT
+    # backward makes the attention gradients 1e-12 + a row sum that cancels to ~0, so
+    # their fp32 values are rounding noise at that level)
+    top = max(np.abs(p.grad.numpy()).max() for p in params.values())
+    for k, p in params.items():
+        want = p.grad.numpy()
+        got = d["grad:" + k]
+        tol = 1e-4 * np.abs(want).max() + 1e-6 * top
+        assert np.abs(got - want).max() <= tol, (k, np.abs(got - want).max(), tol)

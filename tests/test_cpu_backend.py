@@ -1,0 +1,209 @@
+"""CPU: the host-CPU backend libgala_cpu.so (include/gala_cpu.h)
+against the oracle, through its C ABI (host pointers).
+
+Bar, as for the HIP library: bit-exact for SpMM / degree / SDDVV / row-scale /
+row-broadcast / edge permutation (same per-row CSR order and rounding steps as the
+reference kernels), |err| <= 1e-4 (abs) + 1e-4 (rel) for the reductions (row-sum, SDDMM,
+softmax, fused GAT forward / backward, dense gradients).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from gala import _abi, layout
+from _graphs import cora_like, edge_values, features, powerlaw, to_oracle, with_empty_rows
+
+TOL = dict(atol=1e-4, rtol=1e-4)
+GRAPHS = {"cora": cora_like, "powerlaw": powerlaw, "empty_rows": with_empty_rows}
+
+
+@pytest.fixture(scope="module", params=list(GRAPHS))
+def graph(request):
+    return GRAPHS[request.param]()
+
+
+def P(a):
+    return None if a is None else a.ctypes.data
+
+
+class HostCsr:
+    """gala_csr_t over numpy arrays (kept alive with the struct)."""
+
+    def __init__(self, g: layout.HostGraph, val=None, heads=1):
+        self.g, self.val = g, (None if val is None else np.ascontiguousarray(val, np.float32))
+        c = _abi.gala_csr_t()
+        c.n_rows, c.n_cols, c.nnz = g.n_rows, g.n_cols, g.nnz
+        c.rowptr, c.col, c.val = P(g.rowptr), P(g.col), P(self.val)
+        c.val_heads, c.n_seg = heads, g.n_seg
+        c.seg_bounds = None if g.bounds is None else g.bounds.ctypes.data
+        c.split = None
+        self.c = c
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.c)
+
+
+def spmm_cpu(g, X, val=None, heads=1, src=None, dst=None, Y=None, accum=False, nsamp=None):
+    F = X.shape[1]
+    Y = np.zeros((g.n_rows, F), np.float32) if Y is None else Y
+    flags = (_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
+    A = HostCsr(g, val, heads)
+    _abi.call_cpu("gala_spmm_f32", A.ref, P(X), F, P(Y), F, F, P(src), P(dst), flags, nsamp or 0, 5, 7, None)
+    return Y
+
+
+def test_exports_every_operator():
+    L = _abi.cpu_lib()
+    for fn in _abi.CPU_OPS:
+        assert hasattr(L, _abi.cpu_name(fn)), fn
+    hdr = open(_abi.os.path.join(_abi._HERE, "..", "..", "include", "gala_cpu.h")).read()
+    for fn in _abi.CPU_OPS:
+        assert _abi.cpu_name(fn) + "(" in hdr, fn
+
+
+@pytest.mark.parametrize("F", [1, 7, 32, 47, 100])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_bitexact(graph, F, weighted):
+    val = edge_values(graph.nnz) if weighted else None
+    X = features(graph.n_cols, F)
+    np.testing.assert_array_equal(spmm_cpu(graph, X, val), orc.spmm(to_oracle(graph, val), X))
+
+
+def test_spmm_scales_accum_tiled_sampled():
+    g = cora_like()
+    X = features(g.n_cols, 32)
+    n = features(g.n_rows, 1, seed=3).ravel() + 2.0
+    Y0 = features(g.n_rows, 32, seed=4)
+    got = spmm_cpu(g, X, src=n, dst=n, Y=Y0.copy(), accum=True)
+    np.testing.assert_array_equal(got, orc.spmm(to_oracle(g), X, src_scale=n, dst_scale=n, Y=Y0.copy(), accum=True))
+    t = layout.col_tile(g, 1000)
+    np.testing.assert_array_equal(spmm_cpu(t, X), orc.spmm(to_oracle(t), X))
+    np.testing.assert_array_equal(spmm_cpu(t, X, nsamp=20), orc.spmm(to_oracle(t), X, sample=True, nsamp=20))
+
+
+def test_spmm_multihead_weights():
+    g = powerlaw()
+    val = edge_values(g.nnz, heads=4)
+    X = features(g.n_cols, 64)
+    np.testing.assert_array_equal(spmm_cpu(g, X, val, heads=4), orc.spmm(to_oracle(g, val, heads=4), X))
+
+
+@pytest.mark.parametrize("power", [1.0, -0.5])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_degree(graph, power, weighted):
+    val = edge_values(graph.nnz) if weighted else None
+    out = np.empty(graph.n_rows, np.float32)
+    _abi.call_cpu("gala_degree_f32", HostCsr(graph, val).ref, P(out), power, 0, 0, None)
+    np.testing.assert_array_equal(out, orc.degree(to_oracle(graph, val), power=power))
+
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+@pytest.mark.parametrize("heads", [1, 3, 8])
+def test_sddvv(graph, op, heads):
+    a = features(graph.n_rows, heads, seed=11)
+    b = features(graph.n_cols, heads, seed=12)
+    out = np.empty(graph.nnz * heads, np.float32)
+    _abi.call_cpu("gala_sddvv_f32", HostCsr(graph).ref, P(a), P(b), heads, op, 0.2, P(out), None)
+    np.testing.assert_array_equal(out, orc.sddvv(to_oracle(graph), a, b, heads=heads, op=op, slope=0.2))
+
+
+@pytest.mark.parametrize("heads", [1, 8])
+def test_row_sum_scale_broadcast(graph, heads):
+    t = layout.col_tile(graph, 1000)
+    v = edge_values(t.nnz, heads=heads, seed=5)
+    out = np.empty(t.n_rows * heads, np.float32)
+    _abi.call_cpu("gala_row_sum_f32", HostCsr(t).ref, P(v), heads, 1e-12, P(out), 0, None)
+    np.testing.assert_allclose(out, orc.row_sum(to_oracle(t), v, heads=heads, eps=1e-12), **TOL)
+    q = features(t.n_rows, heads, seed=6).ravel()
+    vv = v.copy()
+    _abi.call_cpu("gala_row_scale_f32", HostCsr(t).ref, P(q), heads, P(vv), None)
+    np.testing.assert_array_equal(vv, orc.row_scale(to_oracle(t), q, v, heads=heads))
+    X = features(graph.n_rows, 13)
+    s = features(graph.n_rows, 1).ravel()
+    Y = np.empty_like(X)
+    _abi.call_cpu("gala_row_broadcast_f32", graph.n_rows, 13, P(s), P(X), 13, P(Y), 13, None)
+    np.testing.assert_array_equal(Y, (s[:, None] * X).astype(np.float32))
+
+
+@pytest.mark.parametrize("F,heads", [(1, 1), (32, 1), (47, 1), (256, 8), (12, 3)])
+def test_sddmm(graph, F, heads):
+    A = features(graph.n_rows, F, seed=21)
+    B = features(graph.n_cols, F, seed=22)
+    out = np.empty(graph.nnz * heads, np.float32)
+    _abi.call_cpu("gala_sddmm_dot_f32", HostCsr(graph).ref, P(A), F, P(B), F, F, heads, P(out), None)
+    np.testing.assert_allclose(out, orc.sddmm(to_oracle(graph), A, B, heads=heads), **TOL)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("heads", [1, 3])
+def test_edge_softmax(graph, mode, heads):
+    g = layout.col_tile(graph, 1000)
+    s = edge_values(g.nnz, heads=heads, lo=-3, hi=3, seed=8)
+    d = edge_values(g.nnz, heads=heads, lo=-1, hi=1, seed=9)
+    a = np.empty_like(s)
+    _abi.call_cpu("gala_edge_softmax_fwd_f32", HostCsr(g).ref, P(s), heads, mode, P(a), None)
+    a_ref = orc.softmax_fwd(to_oracle(g), s, heads=heads, mode=mode)
+    np.testing.assert_allclose(a, a_ref, **TOL)
+    ds = np.empty_like(s)
+    _abi.call_cpu("gala_edge_softmax_bwd_f32", HostCsr(g).ref, P(a_ref), P(d), heads, mode, P(ds), None)
+    np.testing.assert_allclose(ds, orc.softmax_bwd(to_oracle(g), a_ref, d, heads=heads, mode=mode), **TOL)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (64, 4)])
+def test_gat_fwd_bwd(graph, mode, F, heads):
+    aL = features(graph.n_rows, heads, seed=31)
+    aR = features(graph.n_cols, heads, seed=32)
+    X = features(graph.n_cols, F, seed=33)
+    dY = features(graph.n_rows, F, seed=34)
+    og = to_oracle(graph)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=mode)
+    Y = np.empty((graph.n_rows, F), np.float32)
+    al = np.empty(graph.nnz * heads, np.float32)
+    _abi.call_cpu("gala_gat_fwd_f32", HostCsr(graph).ref, P(aL), P(aR), P(X), F, F, heads, 0.2, mode,
+                  P(Y), F, P(al), None)
+    np.testing.assert_allclose(al, al_ref, **TOL)
+    np.testing.assert_allclose(Y, Y_ref, **TOL)
+    dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=mode)
+    dz = np.empty(graph.nnz * heads, np.float32)
+    daL = np.empty(graph.n_rows * heads, np.float32)
+    _abi.call_cpu("gala_gat_bwd_f32", HostCsr(graph).ref, P(aL), P(aR), P(X), F, P(dY), F, F, heads, 0.2,
+                  mode, P(al_ref), P(dz), P(daL), None)
+    np.testing.assert_allclose(daL, daL_ref, **TOL)
+    np.testing.assert_allclose(dz, dz_ref, **TOL)
+
+
+def test_edge_permute_and_dense_grad():
+    g = powerlaw()
+    t, perm = layout.transpose(g)
+    v = edge_values(g.nnz, heads=2)
+    out = np.empty_like(v)
+    _abi.call_cpu("gala_edge_permute_f32", P(perm), P(v), g.nnz, 2, P(out), None)
+    np.testing.assert_array_equal(out, v.reshape(-1, 2)[perm].ravel())
+    N, K, M = 20000, 33, 17
+    X = features(N, K, seed=1)
+    dY = features(N, M, seed=2)
+    ws_b = _abi.cpu_lib().gala_cpu_dense_grad_workspace(N, K, M)
+    ws = np.empty(max(ws_b // 4, 1), np.float32)
+    dW = np.empty((M, K), np.float32)
+    db = np.empty(M, np.float32)
+    _abi.call_cpu("gala_dense_grad_f32", N, K, M, P(X), K, P(dY), M, P(dW), P(db), 0, P(ws), ws_b, None)
+    np.testing.assert_allclose(dW, dY.astype(np.float64).T @ X.astype(np.float64), atol=1e-3, rtol=1e-4)
+    np.testing.assert_allclose(db, dY.astype(np.float64).sum(0), atol=1e-3, rtol=1e-4)
+
+
+def test_status_codes_match_the_hip_abi():
+    g = cora_like()
+    A = HostCsr(g)
+    X = features(g.n_cols, 4)
+    Y = np.empty((g.n_rows, 4), np.float32)
+    L = _abi.cpu_lib()
+    assert L.gala_cpu_spmm_f32(A.ref, P(X), 4, P(Y), 4, -1, None, None, 0, 0, 5, 7, None) == _abi.GALA_ERR_INVALID_ARG
+    assert L.gala_cpu_spmm_f32(A.ref, P(X), 4, P(Y), 4, 4, None, None, 0x80, 0, 5, 7, None) == _abi.GALA_ERR_INVALID_ARG
+    assert L.gala_cpu_edge_softmax_fwd_f32(A.ref, P(X), 1, 7, P(Y), None) == _abi.GALA_ERR_INVALID_ARG
+    bad = HostCsr(layout.col_tile(g, 1000))
+    bad.g.bounds[1] = g.nnz + 5
+    assert L.gala_cpu_spmm_f32(bad.ref, P(X), 4, P(Y), 4, 4, None, None, 0, 0, 5, 7, None) == _abi.GALA_ERR_GRAPH
