@@ -191,7 +191,8 @@ def test_gat_fused_fixed_mode_true_gradients(E, heads, D):
 def test_errors_are_exceptions_not_exit(E):
     g = cora_like()
     off, cols, vals, _ = push_graph(E, g)
-    with pytest.raises(RuntimeError, match="device tensor"):
+    # a host tensor against a device graph: an error, never a silent copy or CPU fallback
+    with pytest.raises(RuntimeError, match="is on cpu but the graph is on cuda"):
         E.aggregate_node_mul_sum_call(torch.ones(g.n_rows, 4), off, cols, vals)
     with pytest.raises(RuntimeError, match="slot"):
         E.aggregate_node_mul_sum_apply(torch.ones(g.n_rows, 4, device="cuda"), 7)
