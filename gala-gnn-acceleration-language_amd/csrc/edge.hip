@@ -481,21 +481,39 @@ __device__ __forceinline__ float reduce_scatter(float (&v)[U], int gl) {
     return r;
 }
 
+// Feature ownership of one lane inside a row group: CH chunks of VEC floats at
+// (ch*G + gl)*VEC.  CH > 1 is used for one head whose row is not a multiple of 4 floats
+// (F = 47, the Products class count: VEC = 1), so that 16 lanes, not 64, share a row.
+template <int G, int VEC, int CH>
+struct Lanes {
+    bool valid[CH];
+    int64_t off[CH];
+    __device__ __forceinline__ Lanes(int gl, int32_t F) {
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch) {
+            const int f = (ch * G + gl) * VEC;
+            valid[ch] = f < F;
+            off[ch] = valid[ch] ? f : 0;  // lanes past F read a valid column, never store
+        }
+    }
+};
+
 // Edges [e0, e1) of `row` (one row group): out[e] = <Ad[row], Bd[col_e]> per head.
-template <int G, int VEC, int HW, int U>
+template <int G, int VEC, int HW, int U, int CH = 1>
 __device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool row_ok, int64_t row,
                                             const float *Ad, int64_t lda, const float *Bd,
                                             int64_t ldb, int32_t F, float *out, int64_t e0,
                                             int64_t e1) {
-    const int f = gl * VEC;
-    const bool cv = row_ok && f < F;
-    const int64_t fo = (f < F) ? f : 0;
-    float a[VEC];
+    const Lanes<G, VEC, CH> ln(gl, F);
+    const bool cv = row_ok && ln.valid[0];
+    float a[CH][VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) a[i] = cv ? Ad[row * lda + f + i] : 0.0f;
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) a[ch][i] = (row_ok && ln.valid[ch]) ? Ad[row * lda + ln.off[ch] + i] : 0.0f;
     const int H = p.heads;
     const int D = F / H;
-    const int h = cv ? f / D : 0;
+    const int h = cv ? (int)(ln.off[0] / D) : 0;
     const int32_t n = (int32_t)(e1 - e0);
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         float part[U];
@@ -503,10 +521,12 @@ __device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool ro
         for (int k = 0; k < U; ++k) {
             const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
             const int64_t c = p.col[e0 + j];
-            const float *bp = Bd + c * ldb + fo;
+            const float *bp = Bd + c * ldb;
             float acc = 0.0f;
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) acc = fmaf(a[i], bp[i], acc);
+            for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) acc = fmaf(a[ch][i], bp[ln.off[ch] + i], acc);
             part[k] = acc;
         }
         if (HW == G) {
@@ -524,7 +544,7 @@ __device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool ro
 }
 
 // hub rows (A->split): one row group per chunk of a split row; no fix-up needed
-template <int G, int VEC, int HW, int U>
+template <int G, int VEC, int HW, int U, int CH>
 __global__ __launch_bounds__(kBlock) void k_sddmm_chunk(EdgeParams p, const float *Ad, int64_t lda,
                                                         const float *Bd, int64_t ldb, int32_t F,
                                                         float *out, const int32_t *rows,
@@ -540,10 +560,10 @@ __global__ __launch_bounds__(kBlock) void k_sddmm_chunk(EdgeParams p, const floa
     const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];
     const int64_t e0 = r0 + (c - row_chunk0[ri]) * (int64_t)chunk;
     const int64_t e1 = (e0 + chunk < r1) ? e0 + chunk : r1;
-    sddmm_range<G, VEC, HW, U>(p, gl, true, row, Ad, lda, Bd, ldb, F, out, e0, e1);
+    sddmm_range<G, VEC, HW, U, CH>(p, gl, true, row, Ad, lda, Bd, ldb, F, out, e0, e1);
 }
 
-template <int G, int VEC, int HW, int U>
+template <int G, int VEC, int HW, int U, int CH>
 __global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad, int64_t lda,
                                                   const float *Bd, int64_t ldb, int32_t F,
                                                   float *out, int32_t split_threshold) {
@@ -555,13 +575,13 @@ __global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad,
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0 = 0, e1 = 0;
         if (row_ok) row_range(p, s, row, e0, e1);
-        sddmm_range<G, VEC, HW, U>(p, gl, row_ok, row, Ad, lda, Bd, ldb, F, out, e0, e1);
+        sddmm_range<G, VEC, HW, U, CH>(p, gl, row_ok, row, Ad, lda, Bd, ldb, F, out, e0, e1);
     }
 }
 
 // ---- fused GAT aggregation -----------------------------------------------------------
-// Row group of G lanes, lane g owns VEC features at g*VEC (G*VEC >= F); U edges per
-// batch: cols, aR[col] and the X row slices are all loaded before the softmax updates.
+// Row group of G lanes, lane g owns CH x VEC features (Lanes); U edges per batch: cols,
+// aR[col] and the X row slices are all loaded before the softmax updates.
 template <int VEC>
 struct GVec;
 template <>
@@ -571,7 +591,7 @@ struct GVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
 template <>
 struct GVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
 
-template <int G, int VEC, int U, int MODE>
+template <int G, int VEC, int U, int MODE, int CH>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *aL, const float *aR,
                                                     const float *X, int64_t ldx, int32_t F,
                                                     float slope, float *Y, int64_t ldy,
@@ -579,16 +599,18 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
     typedef typename GVec<VEC>::T V;
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
-    const int H = p.heads;
+    const int H = p.heads;  // CH > 1 only with H == 1
     const int D = F / H;
-    const int f = gl * VEC;
-    const bool cv = f < F;
-    const int64_t fo = cv ? f : 0;
+    const Lanes<G, VEC, CH> ln(gl, F);
+    const bool cv = ln.valid[0];
+    const int64_t fo = ln.off[0];
     const int hh = (int)(fo / D);
     const float al = aL[row * H + hh];
-    float acc[VEC];
+    float acc[CH][VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[i] = 0.0f;
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[ch][i] = 0.0f;
     float m = -INFINITY, sum = 0.0f;
     // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
     // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
@@ -602,7 +624,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
         for (int32_t j0 = 0; j0 < n; j0 += U) {
             int64_t c[U];
             float ar[U];
-            V x[U];
+            V x[U][CH];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
@@ -611,20 +633,25 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 ar[k] = aR[c[k] * H + hh];
-                x[k] = *reinterpret_cast<const V *>(X + c[k] * ldx + fo);
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch)
+                    x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 if (j0 + k >= n) continue;
                 float z = __fadd_rn(al, ar[k]);
                 z = z > 0.0f ? z : __fmul_rn(z, slope);
-                const float *xv = reinterpret_cast<const float *>(&x[k]);
                 if (MODE == GALA_SOFTMAX_REF) {
                     const float pe = ref_exp(z);
                     if (leader) alpha_out[(e0 + j0 + k) * H + hh] = pe;
                     sum = __fadd_rn(sum, pe);
 #pragma unroll
-                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(pe, xv[i], acc[i]);
+                    for (int ch = 0; ch < CH; ++ch) {
+                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(pe, xv[i], acc[ch][i]);
+                    }
                     continue;
                 }
                 if (leader) alpha_out[(e0 + j0 + k) * H + hh] = z;
@@ -632,26 +659,36 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
                     const float r = expf(m - z);
                     sum = fmaf(sum, r, 1.0f);
 #pragma unroll
-                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], r, xv[i]);
+                    for (int ch = 0; ch < CH; ++ch) {
+                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(acc[ch][i], r, xv[i]);
+                    }
                     m = z;
                 } else {
                     const float pe = expf(z - m);
                     sum = __fadd_rn(sum, pe);
 #pragma unroll
-                    for (int i = 0; i < VEC; ++i) acc[i] = fmaf(pe, xv[i], acc[i]);
+                    for (int ch = 0; ch < CH; ++ch) {
+                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(pe, xv[i], acc[ch][i]);
+                    }
                 }
             }
         }
     }
     const float den = (MODE == GALA_SOFTMAX_REF) ? sum + (float)p.seg.n * 1e-12f : sum;
     const float q = 1.0f / den;
-    if (cv) {
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        if (!ln.valid[ch]) continue;
         V out;
         float *ov = reinterpret_cast<float *>(&out);
 #pragma unroll
         for (int i = 0; i < VEC; ++i)
-            ov[i] = (MODE != GALA_SOFTMAX_REF && sum == 0.0f) ? 0.0f : __fmul_rn(acc[i], q);
-        *reinterpret_cast<V *>(Y + row * ldy + fo) = out;
+            ov[i] = (MODE != GALA_SOFTMAX_REF && sum == 0.0f) ? 0.0f : __fmul_rn(acc[ch][i], q);
+        *reinterpret_cast<V *>(Y + row * ldy + ln.off[ch]) = out;
     }
     if (alpha_out) {
         // alpha pass: lanes stride the row's contiguous (edge, head) values.  When H divides
@@ -703,12 +740,12 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
 }
 
 // ---- fused GAT backward -------------------------------------------------------------
-// Row group of G lanes over the features (VEC per lane), HW lanes per head.  Pass 1:
-// U edges per batch load col, X row slice, aR[col,h] and alpha before the head-wise dot
-// reductions; every lane of a head then holds d_alpha and accumulates the head's
-// sum(sds) (and, in REF mode, sum(m*sds) and sum(m*alpha)).  FIXED mode parks sds in
-// d_logit (head leader lane) and a second, contiguous (edge, head) pass forms dz.
-template <int G, int VEC, int U, int HW, int MODE>
+// Row group of G lanes over the features (Lanes: CH x VEC per lane), HW lanes per head.
+// Pass 1: U edges per batch load col, X row slice, aR[col,h] and alpha before the
+// head-wise dot reductions; every lane of a head then holds d_alpha and accumulates the
+// head's sum(sds) (and, in REF mode, sum(m*sds) and sum(m*alpha)).  FIXED mode parks sds
+// in d_logit (head leader lane) and a second, contiguous (edge, head) pass forms dz.
+template <int G, int VEC, int U, int HW, int MODE, int CH>
 __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *aL, const float *aR,
                                                     const float *X, int64_t ldx, const float *dY,
                                                     int64_t lddy, int32_t F, float slope,
@@ -717,19 +754,20 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *a
     typedef typename GVec<VEC>::T V;
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
-    const int H = p.heads;
+    const int H = p.heads;  // CH > 1 only with H == 1
     const int D = F / H;
-    const int f = gl * VEC;
-    const bool cv = f < F;
-    const int64_t fo = cv ? f : 0;
+    const Lanes<G, VEC, CH> ln(gl, F);
+    const bool cv = ln.valid[0];
+    const int64_t fo = ln.off[0];
     const int hh = (int)(fo / D);
     const bool leader = cv && (fo % D) == 0;
     const float al = aL[row * H + hh];
-    float dy[VEC];
-    {
-        const V t = *reinterpret_cast<const V *>(dY + row * lddy + fo);
+    float dy[CH][VEC];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) dy[i] = cv ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+    for (int ch = 0; ch < CH; ++ch) {
+        const V t = *reinterpret_cast<const V *>(dY + row * lddy + ln.off[ch]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dy[ch][i] = ln.valid[ch] ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
     }
     const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
     float acc = 0.0f, s_msds = 0.0f, s_ma = 0.0f;
@@ -740,7 +778,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *a
         for (int32_t j0 = 0; j0 < n; j0 += U) {
             int64_t c[U];
             float ar[U], a[U], part[U];
-            V x[U];
+            V x[U][CH];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
@@ -750,14 +788,19 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *a
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 ar[k] = aR[c[k] * H + hh];
-                x[k] = *reinterpret_cast<const V *>(X + c[k] * ldx + fo);
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch)
+                    x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                const float *xv = reinterpret_cast<const float *>(&x[k]);
                 float d = 0.0f;
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) d = fmaf(dy[i], xv[i], d);
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) d = fmaf(dy[ch][i], xv[i], d);
+                }
                 part[k] = d;
             }
 #pragma unroll
@@ -850,6 +893,14 @@ static int pick_group_tiled(const gala_csr_t *A, int heads) {
     int g = 4;
     while (g < 64 && (double)g * kTileK < 1.15 * avg) g <<= 1;
     return g;
+}
+
+// One head whose row is not a multiple of 4 floats (VEC < 4) and spans 17..64 vectors:
+// 16 lanes own ceil(L/16) chunks each (Lanes), instead of 64 lanes one vector each, so 4
+// rows share a wave and the per-edge softmax / reduction work is not repeated 64-fold.
+// Returns the chunk count (1 = the one-vector-per-lane layout).
+static int narrow_chunks(int heads, int vec, int L) {
+    return (heads == 1 && vec < 4 && L > 16 && L <= 64) ? (L + 15) / 16 : 1;
 }
 
 static int edge_setup(const gala_csr_t *A, int32_t heads, EdgeParams *p) {
@@ -1057,16 +1108,16 @@ struct SddmmSplit {
     int32_t chunk = 0, threshold = 0;
 };
 
-template <int G, int VEC, int HWV>
+template <int G, int VEC, int HWV, int CH = 1>
 static void launch_sddmm_hw(const EdgeParams &p, const SddmmSplit &sp, const float *Ad, int64_t lda,
                             const float *Bd, int64_t ldb, int32_t F, float *out, hipStream_t hs) {
     constexpr int U = (G >= 8) ? 8 : G;  // U <= G for the reduce-scatter
     constexpr int HW = (HWV < G) ? HWV : G;
-    hipLaunchKernelGGL((k_sddmm<G, VEC, HW, U>), dim3(blocks_for(p.n_rows, G)), dim3(kBlock), 0, hs,
+    hipLaunchKernelGGL((k_sddmm<G, VEC, HW, U, CH>), dim3(blocks_for(p.n_rows, G)), dim3(kBlock), 0, hs,
                        p, Ad, lda, Bd, ldb, F, out, sp.threshold);
     if (sp.n_chunks > 0) {
         const int64_t per_block = (kBlock / kWave) * (kWave / G);
-        hipLaunchKernelGGL((k_sddmm_chunk<G, VEC, HW, U>), dim3((unsigned)((sp.n_chunks + per_block - 1) / per_block)),
+        hipLaunchKernelGGL((k_sddmm_chunk<G, VEC, HW, U, CH>), dim3((unsigned)((sp.n_chunks + per_block - 1) / per_block)),
                            dim3(kBlock), 0, hs, p, Ad, lda, Bd, ldb, F, out, sp.rows, sp.row_chunk0,
                            sp.chunk_row, sp.n_chunks, sp.chunk);
     }
@@ -1133,6 +1184,18 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
         sp.threshold = plan->threshold;
     }
     int r;
+    const int ch = narrow_chunks(heads, vec, L);
+    if (ch > 1) {
+        hipStream_t hs = (hipStream_t)stream;
+#define GALA_SD(V, C) launch_sddmm_hw<16, V, 16, C>(p, sp, Ad, lda, Bd, ldb, F, out_e, hs)
+        if (vec == 2) {
+            if (ch == 2) GALA_SD(2, 2); else if (ch == 3) GALA_SD(2, 3); else GALA_SD(2, 4);
+        } else {
+            if (ch == 2) GALA_SD(1, 2); else if (ch == 3) GALA_SD(1, 3); else GALA_SD(1, 4);
+        }
+#undef GALA_SD
+        return launch_status();
+    }
     if (vec == 4) r = sddmm_vec<4>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
     else if (vec == 2) r = sddmm_vec<2>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
     else r = sddmm_vec<1>(p, sp, L, hw, Ad, lda, Bd, ldb, F, out_e, (hipStream_t)stream);
@@ -1140,17 +1203,17 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     return launch_status();
 }
 
-template <int G, int VEC>
+template <int G, int VEC, int CH = 1>
 static void launch_gat(const EdgeParams &p, int mode, const float *aL, const float *aR,
                        const float *X, int64_t ldx, int32_t F, float slope, float *Y,
                        int64_t ldy, float *alpha_out, hipStream_t hs) {
     const dim3 grid(blocks_for(p.n_rows, G));
     constexpr int U = 8;
     if (mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p,
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF, CH>), grid, dim3(kBlock), 0, hs, p,
                            aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
     else
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs,
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED, CH>), grid, dim3(kBlock), 0, hs,
                            p, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
 }
 
@@ -1188,6 +1251,17 @@ extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const floa
     const int L = (F + vec - 1) / vec;
     hipStream_t hs = (hipStream_t)stream;
     int r;
+    const int ch = narrow_chunks(heads, vec, L);
+    if (ch > 1) {
+#define GALA_GF(V, C) launch_gat<16, V, C>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs)
+        if (vec == 2) {
+            if (ch == 2) GALA_GF(2, 2); else if (ch == 3) GALA_GF(2, 3); else GALA_GF(2, 4);
+        } else {
+            if (ch == 2) GALA_GF(1, 2); else if (ch == 3) GALA_GF(1, 3); else GALA_GF(1, 4);
+        }
+#undef GALA_GF
+        return launch_status();
+    }
     if (vec == 4) r = gat_vec<4>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
     else if (vec == 2) r = gat_vec<2>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
     else r = gat_vec<1>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
@@ -1195,7 +1269,7 @@ extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const floa
     return launch_status();
 }
 
-template <int G, int VEC, int HW>
+template <int G, int VEC, int HW, int CH = 1>
 static void launch_gat_bwd(const EdgeParams &p, int mode, const float *aL, const float *aR,
                            const float *X, int64_t ldx, const float *dY, int64_t lddy, int32_t F,
                            float slope, const float *alpha, float *d_logit, float *d_aL,
@@ -1204,10 +1278,10 @@ static void launch_gat_bwd(const EdgeParams &p, int mode, const float *aL, const
     constexpr int U = 8;
     constexpr int HWc = (HW < G) ? HW : G;
     if (mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p,
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF, CH>), grid, dim3(kBlock), 0, hs, p,
                            aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
     else
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p,
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED, CH>), grid, dim3(kBlock), 0, hs, p,
                            aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
 }
 
@@ -1272,6 +1346,17 @@ extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const floa
     const int hw = heads > 1 ? hw_l : G;
     hipStream_t hs = (hipStream_t)stream;
     int r;
+    const int ch = narrow_chunks(heads, vec, L);
+    if (ch > 1) {
+#define GALA_GBC(V, C) launch_gat_bwd<16, V, 16, C>(p, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
+        if (vec == 2) {
+            if (ch == 2) GALA_GBC(2, 2); else if (ch == 3) GALA_GBC(2, 3); else GALA_GBC(2, 4);
+        } else {
+            if (ch == 2) GALA_GBC(1, 2); else if (ch == 3) GALA_GBC(1, 3); else GALA_GBC(1, 4);
+        }
+#undef GALA_GBC
+        return launch_status();
+    }
     if (vec == 4) r = gat_bwd_vec<4>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
     else if (vec == 2) r = gat_bwd_vec<2>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
     else r = gat_bwd_vec<1>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);

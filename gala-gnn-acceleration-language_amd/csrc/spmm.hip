@@ -362,7 +362,16 @@ static void launch_flags(const SpmmParams &p, const SplitParams *sp, bool w, boo
 template <int VEC>
 static int launch_vec(const SpmmParams &p, const SplitParams *sp, int L, bool w, bool samp,
                       bool srcs, hipStream_t st) {
-    // L = vector elements per row (ceil(F/VEC))
+    // L = vector elements per row (ceil(F/VEC)).  Rows that are not a multiple of 4 floats
+    // (VEC < 4) and span 17..64 vectors (F = 47, the Products class count) take 16 lanes
+    // with ceil(L/16) chunks each rather than 64 lanes with one: 4 rows per wave.
+    if (VEC < 4 && L > 16 && L <= 64) {
+        const int ch = (L + 15) / 16;
+        if (ch == 2) launch_flags<VEC, 16, 2>(p, sp, w, samp, srcs, st);
+        else if (ch == 3) launch_flags<VEC, 16, 3>(p, sp, w, samp, srcs, st);
+        else launch_flags<VEC, 16, 4>(p, sp, w, samp, srcs, st);
+        return GALA_OK;
+    }
     if (L <= 1) launch_flags<VEC, 1, 1>(p, sp, w, samp, srcs, st);
     else if (L <= 2) launch_flags<VEC, 2, 1>(p, sp, w, samp, srcs, st);
     else if (L <= 4) launch_flags<VEC, 4, 1>(p, sp, w, samp, srcs, st);

@@ -34,7 +34,7 @@ def graph(request):
     return GRAPHS[request.param]()
 
 
-@pytest.mark.parametrize("F", [1, 2, 7, 16, 32, 40, 47, 64, 100, 128, 256, 602])
+@pytest.mark.parametrize("F", [1, 2, 7, 16, 32, 33, 40, 47, 62, 64, 100, 128, 256, 602])
 @pytest.mark.parametrize("weighted", [False, True])
 def test_spmm_bitexact(graph, F, weighted):
     val = edge_values(graph.nnz) if weighted else None
@@ -180,7 +180,7 @@ def test_row_sum_and_scale(graph, tiled, heads):
     np.testing.assert_array_equal(host(vv), orc.row_scale(to_oracle(g), q, v, heads=heads))
 
 
-@pytest.mark.parametrize("F,heads", [(1, 1), (16, 1), (32, 1), (47, 1), (100, 1), (256, 8), (64, 2)])
+@pytest.mark.parametrize("F,heads", [(1, 1), (16, 1), (32, 1), (33, 1), (47, 1), (62, 1), (100, 1), (256, 8), (64, 2)])
 def test_sddmm(graph, F, heads):
     A = features(graph.n_rows, F, seed=21)
     B = features(graph.n_cols, F, seed=22)
@@ -212,7 +212,7 @@ def test_edge_softmax_overflow_clamp():
 
 
 @pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
-@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8)])
+@pytest.mark.parametrize("F,heads", [(32, 1), (33, 1), (47, 1), (62, 1), (256, 8)])
 def test_gat_fused(graph, mode, F, heads):
     aL = features(graph.n_rows, heads, seed=31)
     aR = features(graph.n_cols, heads, seed=32)
@@ -225,7 +225,7 @@ def test_gat_fused(graph, mode, F, heads):
 
 
 @pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
-@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4)])
+@pytest.mark.parametrize("F,heads", [(32, 1), (33, 1), (47, 1), (62, 1), (256, 8), (64, 4)])
 @pytest.mark.parametrize("tiled", [False, True])
 def test_gat_bwd_fused(graph, mode, F, heads, tiled):
     """Fused d alpha -> softmax bwd -> LeakyReLU bwd -> row sum vs the oracle chain."""
