@@ -257,6 +257,18 @@ void fuse(Module &m) {
         agg.in = {m.nodes[ei].in[0], m.nodes[ei].in[1], agg.in[0]};
         m.nodes[si].dead = m.nodes[li].dead = m.nodes[ei].dead = true;
         m.notes.push_back("fuse: edge add + leaky relu + softmax + aggregation -> gat_aggregate");
+        // attnR = ffn(res, out=1) of the aggregated res itself: the kernels recompute the
+        // source logit from the X row they gather (gat_aggregate_ffn), no aR[col] reads
+        const int fi = m.producer(agg.in[1]);
+        if (fi >= 0 && m.nodes[fi].op == Op::Ffn && m.nodes[fi].weight >= 0 &&
+            m.nodes[fi].in[0] == agg.in[2] && m.weights[m.nodes[fi].weight].out == 1 &&
+            m.uses(agg.in[1]).size() == 1 && m.nodes[fi].hoisted == agg.hoisted) {
+            agg.weight = m.nodes[fi].weight;
+            agg.in[1] = -1;
+            m.nodes[fi].dead = true;
+            m.notes.push_back("fuse: attention linear of the aggregated rows recomputed in the "
+                              "GAT kernels -> gat_aggregate_ffn");
+        }
     }
     // GCN: [RowBroadcast(pre)] -> Aggregate (unweighted or fixed weights) -> [RowBroadcast(post)]
     for (int i = 0; i < (int)m.nodes.size(); ++i) {

@@ -482,6 +482,48 @@ extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const 
     return GALA_OK;
 }
 
+// aR[j] = <X[j, 0:F], wR> + bR: the attention Linear the *_attn entry points recompute
+static std::vector<float> attn_logits(const gala_csr_t *A, const float *wR, const float *bR,
+                                      const float *X, int64_t ldx, int32_t F) {
+    std::vector<float> aR((size_t)A->n_cols);
+    const float b = bR ? bR[0] : 0.0f;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t j = 0; j < A->n_cols; ++j) {
+        float d = 0.0f;
+        for (int32_t f = 0; f < F; ++f) d = fmaf(wR[f], X[j * ldx + f], d);
+        aR[(size_t)j] = d + b;
+    }
+    return aR;
+}
+
+extern "C" int gala_cpu_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                                         const float *bR, const float *X, int64_t ldx, int32_t F,
+                                         float slope, int32_t mode, float *Y, int64_t ldy,
+                                         float *alpha_out, void *stream) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 1 || ldx < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!wR || (!X && A->n_cols > 0)) return GALA_ERR_INVALID_ARG;
+    const std::vector<float> aR = attn_logits(A, wR, bR, X, ldx, F);
+    return gala_cpu_gat_fwd_f32(A, aL, aR.data(), X, ldx, F, 1, slope, mode, Y, ldy, alpha_out,
+                                stream);
+}
+
+extern "C" int gala_cpu_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                                         const float *bR, const float *X, int64_t ldx,
+                                         const float *dY, int64_t lddy, int32_t F, float slope,
+                                         const float *alpha, float *d_aL, void *stream) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 1 || ldx < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!wR || (!X && A->n_cols > 0)) return GALA_ERR_INVALID_ARG;
+    const std::vector<float> aR = attn_logits(A, wR, bR, X, ldx, F);
+    return gala_cpu_gat_bwd_f32(A, aL, aR.data(), X, ldx, dY, lddy, F, 1, slope, GALA_SOFTMAX_REF,
+                                alpha, nullptr, d_aL, stream);
+}
+
 extern "C" int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,
                                          int32_t heads, float *dst, void *) {
     if (n < 0 || heads < 1) return GALA_ERR_INVALID_ARG;

@@ -591,21 +591,53 @@ struct GVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
 template <>
 struct GVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
 
-template <int G, int VEC, int U, int MODE, int CH>
+// RC (one head): the source logit aR[col] = <X[col,:], wR> + bR is recomputed from the X
+// row the aggregation gathers anyway (the DSL's attnR = dsl.nn.ffn(res, out=1) of the
+// aggregated `res`, tests/GALA-DSL/gat/*), instead of a separate random aR[col] read.
+template <int G, int VEC, int CH>
+__device__ __forceinline__ float attn_dot(const float (&w)[CH][VEC],
+                                          const typename GVec<VEC>::T (&x)[CH]) {
+    float d = 0.0f;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const float *xv = reinterpret_cast<const float *>(&x[ch]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) d = fmaf(w[ch][i], xv[i], d);
+    }
+    return group_sum<G>(d);
+}
+
+template <int G, int VEC, int CH>
+__device__ __forceinline__ void load_attn(const Lanes<G, VEC, CH> &ln, const float *wR,
+                                          float (&w)[CH][VEC]) {
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) w[ch][i] = ln.valid[ch] ? wR[ln.off[ch] + i] : 0.0f;
+}
+
+template <int G, int VEC, int U, int MODE, int CH, bool RC>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *aL, const float *aR,
                                                     const float *X, int64_t ldx, int32_t F,
                                                     float slope, float *Y, int64_t ldy,
-                                                    float *alpha_out) {
+                                                    float *alpha_out, const float *wR,
+                                                    const float *bR) {
     typedef typename GVec<VEC>::T V;
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
-    const int H = p.heads;  // CH > 1 only with H == 1
+    const int H = p.heads;  // CH > 1 and RC only with H == 1
     const int D = F / H;
     const Lanes<G, VEC, CH> ln(gl, F);
     const bool cv = ln.valid[0];
     const int64_t fo = ln.off[0];
     const int hh = (int)(fo / D);
     const float al = aL[row * H + hh];
+    float w[CH][VEC];
+    float wb = 0.0f;
+    if (RC) {
+        load_attn<G, VEC, CH>(ln, wR, w);
+        wb = bR ? bR[0] : 0.0f;
+    }
     float acc[CH][VEC];
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
@@ -632,10 +664,14 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                ar[k] = aR[c[k] * H + hh];
+                if (!RC) ar[k] = aR[c[k] * H + hh];
 #pragma unroll
                 for (int ch = 0; ch < CH; ++ch)
                     x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
+            }
+            if (RC) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(w, x[k]), wb);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
@@ -745,12 +781,12 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
 // head-wise dot reductions; every lane of a head then holds d_alpha and accumulates the
 // head's sum(sds) (and, in REF mode, sum(m*sds) and sum(m*alpha)).  FIXED mode parks sds
 // in d_logit (head leader lane) and a second, contiguous (edge, head) pass forms dz.
-template <int G, int VEC, int U, int HW, int MODE, int CH>
+template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
 __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *aL, const float *aR,
                                                     const float *X, int64_t ldx, const float *dY,
                                                     int64_t lddy, int32_t F, float slope,
                                                     const float *alpha, float *d_logit,
-                                                    float *d_aL) {
+                                                    float *d_aL, const float *wR, const float *bR) {
     typedef typename GVec<VEC>::T V;
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
@@ -768,6 +804,12 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *a
         const V t = *reinterpret_cast<const V *>(dY + row * lddy + ln.off[ch]);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dy[ch][i] = ln.valid[ch] ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+    }
+    float w[CH][VEC];
+    float wb = 0.0f;
+    if (RC) {  // REF mode, one head (see k_gat_fwd)
+        load_attn<G, VEC, CH>(ln, wR, w);
+        wb = bR ? bR[0] : 0.0f;
     }
     const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
     float acc = 0.0f, s_msds = 0.0f, s_ma = 0.0f;
@@ -787,10 +829,14 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *a
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
-                ar[k] = aR[c[k] * H + hh];
+                if (!RC) ar[k] = aR[c[k] * H + hh];
 #pragma unroll
                 for (int ch = 0; ch < CH; ++ch)
                     x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
+            }
+            if (RC) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(w, x[k]), wb);
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
@@ -1203,135 +1249,159 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     return launch_status();
 }
 
-template <int G, int VEC, int CH = 1>
-static void launch_gat(const EdgeParams &p, int mode, const float *aL, const float *aR,
-                       const float *X, int64_t ldx, int32_t F, float slope, float *Y,
-                       int64_t ldy, float *alpha_out, hipStream_t hs) {
-    const dim3 grid(blocks_for(p.n_rows, G));
+// Host-side argument bundle of the fused GAT kernels (forward and backward).
+struct GatArgs {
+    EdgeParams p;
+    int mode;
+    const float *aL, *aR, *wR, *bR;  // aR == nullptr: recompute from X with wR / bR (RC)
+    const float *X;
+    int64_t ldx;
+    int32_t F;
+    float slope;
+    float *Y;                        // forward
+    int64_t ldy;
+    float *alpha_out;
+    const float *dY;                 // backward
+    int64_t lddy;
+    const float *alpha;
+    float *d_logit, *d_aL;
+    hipStream_t hs;
+};
+
+template <int G, int VEC, int CH, bool RC>
+static void launch_gat(const GatArgs &a) {
+    const dim3 grid(blocks_for(a.p.n_rows, G));
     constexpr int U = 8;
-    if (mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF, CH>), grid, dim3(kBlock), 0, hs, p,
-                           aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
+    if (a.mode == GALA_SOFTMAX_REF)
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF, CH, RC>), grid, dim3(kBlock), 0, a.hs,
+                           a.p, a.aL, a.aR, a.X, a.ldx, a.F, a.slope, a.Y, a.ldy, a.alpha_out, a.wR, a.bR);
     else
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED, CH>), grid, dim3(kBlock), 0, hs,
-                           p, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out);
+        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED, CH, RC>), grid, dim3(kBlock), 0, a.hs,
+                           a.p, a.aL, a.aR, a.X, a.ldx, a.F, a.slope, a.Y, a.ldy, a.alpha_out, a.wR, a.bR);
 }
 
-template <int VEC>
-static int gat_vec(const EdgeParams &p, int L, int mode, const float *aL, const float *aR,
-                   const float *X, int64_t ldx, int32_t F, float slope, float *Y, int64_t ldy,
-                   float *alpha_out, hipStream_t hs) {
-    if (L <= 1) launch_gat<1, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 2) launch_gat<2, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 4) launch_gat<4, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 8) launch_gat<8, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 16) launch_gat<16, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 32) launch_gat<32, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (L <= 64) launch_gat<64, VEC>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+template <int VEC, bool RC>
+static int gat_vec(const GatArgs &a, int L, int ch) {
+    if (ch == 2) launch_gat<16, VEC, 2, RC>(a);
+    else if (ch == 3) launch_gat<16, VEC, 3, RC>(a);
+    else if (ch == 4) launch_gat<16, VEC, 4, RC>(a);
+    else if (L <= 1) launch_gat<1, VEC, 1, RC>(a);
+    else if (L <= 2) launch_gat<2, VEC, 1, RC>(a);
+    else if (L <= 4) launch_gat<4, VEC, 1, RC>(a);
+    else if (L <= 8) launch_gat<8, VEC, 1, RC>(a);
+    else if (L <= 16) launch_gat<16, VEC, 1, RC>(a);
+    else if (L <= 32) launch_gat<32, VEC, 1, RC>(a);
+    else if (L <= 64) launch_gat<64, VEC, 1, RC>(a);
     else return GALA_ERR_UNSUPPORTED;
     return GALA_OK;
 }
 
-extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                const float *X, int64_t ldx, int32_t F, int32_t heads,
-                                float slope, int32_t mode, float *Y, int64_t ldy,
-                                float *alpha_out, void *stream) {
-    EdgeParams p;
-    int st = edge_setup(A, heads, &p);
+static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                        const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                        float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
+                        void *stream) {
+    GatArgs a{};
+    int st = edge_setup(A, heads, &a.p);
     if (st) return st;
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
     if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
-    if (!aL || !aR || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     int vec = 4;
     while (vec > 1 && (D % vec || ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) ||
                        ((uintptr_t)Y % (4 * vec))))
         vec >>= 1;
     const int L = (F + vec - 1) / vec;
-    hipStream_t hs = (hipStream_t)stream;
-    int r;
+    a.mode = mode;
+    a.aL = aL, a.aR = aR, a.wR = wR, a.bR = bR, a.X = X, a.ldx = ldx, a.F = F, a.slope = slope;
+    a.Y = Y, a.ldy = ldy, a.alpha_out = alpha_out, a.hs = (hipStream_t)stream;
     const int ch = narrow_chunks(heads, vec, L);
-    if (ch > 1) {
-#define GALA_GF(V, C) launch_gat<16, V, C>(p, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs)
-        if (vec == 2) {
-            if (ch == 2) GALA_GF(2, 2); else if (ch == 3) GALA_GF(2, 3); else GALA_GF(2, 4);
-        } else {
-            if (ch == 2) GALA_GF(1, 2); else if (ch == 3) GALA_GF(1, 3); else GALA_GF(1, 4);
-        }
-#undef GALA_GF
-        return launch_status();
-    }
-    if (vec == 4) r = gat_vec<4>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else if (vec == 2) r = gat_vec<2>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
-    else r = gat_vec<1>(p, L, mode, aL, aR, X, ldx, F, slope, Y, ldy, alpha_out, hs);
+    const bool rc = aR == nullptr;
+    int r;
+    if (vec == 4) r = rc ? gat_vec<4, true>(a, L, ch) : gat_vec<4, false>(a, L, ch);
+    else if (vec == 2) r = rc ? gat_vec<2, true>(a, L, ch) : gat_vec<2, false>(a, L, ch);
+    else r = rc ? gat_vec<1, true>(a, L, ch) : gat_vec<1, false>(a, L, ch);
     if (r) return r;
     return launch_status();
 }
 
-template <int G, int VEC, int HW, int CH = 1>
-static void launch_gat_bwd(const EdgeParams &p, int mode, const float *aL, const float *aR,
-                           const float *X, int64_t ldx, const float *dY, int64_t lddy, int32_t F,
-                           float slope, const float *alpha, float *d_logit, float *d_aL,
-                           hipStream_t hs) {
-    const dim3 grid(blocks_for(p.n_rows, G));
+extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                const float *X, int64_t ldx, int32_t F, int32_t heads,
+                                float slope, int32_t mode, float *Y, int64_t ldy,
+                                float *alpha_out, void *stream) {
+    if (!aR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, nullptr, nullptr, X, ldx, F, heads, slope, mode, Y, ldy,
+                        alpha_out, stream);
+}
+
+extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                                     const float *bR, const float *X, int64_t ldx, int32_t F,
+                                     float slope, int32_t mode, float *Y, int64_t ldy,
+                                     float *alpha_out, void *stream) {
+    if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, nullptr, wR, bR, X, ldx, F, 1, slope, mode, Y, ldy, alpha_out,
+                        stream);
+}
+
+template <int G, int VEC, int HW, int CH, bool RC>
+static void launch_gat_bwd(const GatArgs &a) {
+    const dim3 grid(blocks_for(a.p.n_rows, G));
     constexpr int U = 8;
     constexpr int HWc = (HW < G) ? HW : G;
-    if (mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF, CH>), grid, dim3(kBlock), 0, hs, p,
-                           aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
-    else
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED, CH>), grid, dim3(kBlock), 0, hs, p,
-                           aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL);
+    if (a.mode == GALA_SOFTMAX_REF)
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF, CH, RC>), grid, dim3(kBlock), 0, a.hs,
+                           a.p, a.aL, a.aR, a.X, a.ldx, a.dY, a.lddy, a.F, a.slope, a.alpha, a.d_logit,
+                           a.d_aL, a.wR, a.bR);
+    else if (!RC)  // FIXED recomputes the LeakyReLU mask from aR in its second pass
+        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED, CH, false>), grid, dim3(kBlock), 0,
+                           a.hs, a.p, a.aL, a.aR, a.X, a.ldx, a.dY, a.lddy, a.F, a.slope, a.alpha,
+                           a.d_logit, a.d_aL, a.wR, a.bR);
 }
 
-template <int G, int VEC>
-static void gat_bwd_hw(const EdgeParams &p, int hw, int mode, const float *aL, const float *aR,
-                       const float *X, int64_t ldx, const float *dY, int64_t lddy, int32_t F,
-                       float slope, const float *alpha, float *d_logit, float *d_aL, hipStream_t hs) {
-#define GALA_GB(HWV) launch_gat_bwd<G, VEC, HWV>(p, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
+template <int G, int VEC, bool RC>
+static void gat_bwd_hw(const GatArgs &a, int hw) {
     switch (hw) {
-        case 1: GALA_GB(1); break;
-        case 2: GALA_GB(2); break;
-        case 4: GALA_GB(4); break;
-        case 8: GALA_GB(8); break;
-        case 16: GALA_GB(16); break;
-        case 32: GALA_GB(32); break;
-        default: GALA_GB(G); break;
+        case 1: launch_gat_bwd<G, VEC, 1, 1, RC>(a); break;
+        case 2: launch_gat_bwd<G, VEC, 2, 1, RC>(a); break;
+        case 4: launch_gat_bwd<G, VEC, 4, 1, RC>(a); break;
+        case 8: launch_gat_bwd<G, VEC, 8, 1, RC>(a); break;
+        case 16: launch_gat_bwd<G, VEC, 16, 1, RC>(a); break;
+        case 32: launch_gat_bwd<G, VEC, 32, 1, RC>(a); break;
+        default: launch_gat_bwd<G, VEC, G, 1, RC>(a); break;
     }
-#undef GALA_GB
 }
 
-template <int VEC>
-static int gat_bwd_vec(const EdgeParams &p, int L, int hw, int mode, const float *aL,
-                       const float *aR, const float *X, int64_t ldx, const float *dY, int64_t lddy,
-                       int32_t F, float slope, const float *alpha, float *d_logit, float *d_aL,
-                       hipStream_t hs) {
-#define GALA_GBV(GV) gat_bwd_hw<GV, VEC>(p, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
-    if (L <= 1) GALA_GBV(1);
-    else if (L <= 2) GALA_GBV(2);
-    else if (L <= 4) GALA_GBV(4);
-    else if (L <= 8) GALA_GBV(8);
-    else if (L <= 16) GALA_GBV(16);
-    else if (L <= 32) GALA_GBV(32);
-    else if (L <= 64) GALA_GBV(64);
+template <int VEC, bool RC>
+static int gat_bwd_vec(const GatArgs &a, int L, int hw, int ch) {
+    if (ch == 2) launch_gat_bwd<16, VEC, 16, 2, RC>(a);
+    else if (ch == 3) launch_gat_bwd<16, VEC, 16, 3, RC>(a);
+    else if (ch == 4) launch_gat_bwd<16, VEC, 16, 4, RC>(a);
+    else if (L <= 1) gat_bwd_hw<1, VEC, RC>(a, hw);
+    else if (L <= 2) gat_bwd_hw<2, VEC, RC>(a, hw);
+    else if (L <= 4) gat_bwd_hw<4, VEC, RC>(a, hw);
+    else if (L <= 8) gat_bwd_hw<8, VEC, RC>(a, hw);
+    else if (L <= 16) gat_bwd_hw<16, VEC, RC>(a, hw);
+    else if (L <= 32) gat_bwd_hw<32, VEC, RC>(a, hw);
+    else if (L <= 64) gat_bwd_hw<64, VEC, RC>(a, hw);
     else return GALA_ERR_UNSUPPORTED;
-#undef GALA_GBV
     return GALA_OK;
 }
 
-extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                const float *X, int64_t ldx, const float *dY, int64_t lddy,
-                                int32_t F, int32_t heads, float slope, int32_t mode,
-                                const float *alpha, float *d_logit, float *d_aL, void *stream) {
-    EdgeParams p;
-    int st = edge_setup(A, heads, &p);
+static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                        const float *bR, const float *X, int64_t ldx, const float *dY,
+                        int64_t lddy, int32_t F, int32_t heads, float slope, int32_t mode,
+                        const float *alpha, float *d_logit, float *d_aL, void *stream) {
+    GatArgs a{};
+    int st = edge_setup(A, heads, &a.p);
     if (st) return st;
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
     if (F < 1 || F % heads != 0 || ldx < F || lddy < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
-    if (!aL || !aR || !dY || !d_aL || (A->nnz > 0 && (!X || !alpha))) return GALA_ERR_INVALID_ARG;
+    if (!aL || (!aR && !wR) || !dY || !d_aL || (A->nnz > 0 && (!X || !alpha)))
+        return GALA_ERR_INVALID_ARG;
     if (mode == GALA_SOFTMAX_FIXED && !d_logit && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (!aR && (mode != GALA_SOFTMAX_REF || heads != 1)) return GALA_ERR_UNSUPPORTED;
     const int D = F / heads;
     int vec = 4;
     while (vec > 1 && (D % vec || ldx % vec || lddy % vec || ((uintptr_t)X % (4 * vec)) ||
@@ -1344,24 +1414,36 @@ extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const floa
     if (heads > 1 && ((hw_l & (hw_l - 1)) || G % heads)) return GALA_ERR_UNSUPPORTED;
     if (mode == GALA_SOFTMAX_FIXED && G % heads) return GALA_ERR_UNSUPPORTED;
     const int hw = heads > 1 ? hw_l : G;
-    hipStream_t hs = (hipStream_t)stream;
-    int r;
+    a.mode = mode;
+    a.aL = aL, a.aR = aR, a.wR = wR, a.bR = bR, a.X = X, a.ldx = ldx, a.F = F, a.slope = slope;
+    a.dY = dY, a.lddy = lddy, a.alpha = alpha, a.d_logit = d_logit, a.d_aL = d_aL;
+    a.hs = (hipStream_t)stream;
     const int ch = narrow_chunks(heads, vec, L);
-    if (ch > 1) {
-#define GALA_GBC(V, C) launch_gat_bwd<16, V, 16, C>(p, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs)
-        if (vec == 2) {
-            if (ch == 2) GALA_GBC(2, 2); else if (ch == 3) GALA_GBC(2, 3); else GALA_GBC(2, 4);
-        } else {
-            if (ch == 2) GALA_GBC(1, 2); else if (ch == 3) GALA_GBC(1, 3); else GALA_GBC(1, 4);
-        }
-#undef GALA_GBC
-        return launch_status();
-    }
-    if (vec == 4) r = gat_bwd_vec<4>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
-    else if (vec == 2) r = gat_bwd_vec<2>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
-    else r = gat_bwd_vec<1>(p, L, hw, mode, aL, aR, X, ldx, dY, lddy, F, slope, alpha, d_logit, d_aL, hs);
+    const bool rc = aR == nullptr;
+    int r;
+    if (vec == 4) r = rc ? gat_bwd_vec<4, true>(a, L, hw, ch) : gat_bwd_vec<4, false>(a, L, hw, ch);
+    else if (vec == 2) r = rc ? gat_bwd_vec<2, true>(a, L, hw, ch) : gat_bwd_vec<2, false>(a, L, hw, ch);
+    else r = rc ? gat_bwd_vec<1, true>(a, L, hw, ch) : gat_bwd_vec<1, false>(a, L, hw, ch);
     if (r) return r;
     return launch_status();
+}
+
+extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                const float *X, int64_t ldx, const float *dY, int64_t lddy,
+                                int32_t F, int32_t heads, float slope, int32_t mode,
+                                const float *alpha, float *d_logit, float *d_aL, void *stream) {
+    if (!aR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_bwd_impl(A, aL, aR, nullptr, nullptr, X, ldx, dY, lddy, F, heads, slope, mode,
+                        alpha, d_logit, d_aL, stream);
+}
+
+extern "C" int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                                     const float *bR, const float *X, int64_t ldx,
+                                     const float *dY, int64_t lddy, int32_t F, float slope,
+                                     const float *alpha, float *d_aL, void *stream) {
+    if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_bwd_impl(A, aL, nullptr, wR, bR, X, ldx, dY, lddy, F, 1, slope, GALA_SOFTMAX_REF,
+                        alpha, nullptr, d_aL, stream);
 }
 
 extern "C" int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,

@@ -82,6 +82,8 @@ SIGNATURES = {
     "gala_edge_softmax_bwd_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _P, _P]),
     "gala_gat_fwd_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _I32, _I32, _F, _I32, _P, _I64, _P, _P]),
     "gala_gat_bwd_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _P, _I64, _I32, _I32, _F, _I32, _P, _P, _P, _P]),
+    "gala_gat_fwd_attn_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _I64, _I32, _F, _I32, _P, _I64, _P, _P]),
+    "gala_gat_bwd_attn_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _I64, _P, _I64, _I32, _F, _P, _P, _P]),
     "gala_edge_permute_f32": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),
     "gala_host_csr_build": (ctypes.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _P]),
     "gala_host_col_breakpoints": (ctypes.c_int64, [_I64, _I64, _P, _I64]),
@@ -142,7 +144,8 @@ def call(fn: str, *args) -> int:
 CPU_OPS = ("gala_spmm_f32", "gala_degree_f32", "gala_row_broadcast_f32", "gala_sddvv_f32",
            "gala_row_sum_f32", "gala_row_scale_f32", "gala_sddmm_dot_f32",
            "gala_edge_softmax_fwd_f32", "gala_edge_softmax_bwd_f32", "gala_gat_fwd_f32",
-           "gala_gat_bwd_f32", "gala_edge_permute_f32", "gala_dense_grad_workspace",
+           "gala_gat_bwd_f32", "gala_gat_fwd_attn_f32", "gala_gat_bwd_attn_f32",
+           "gala_edge_permute_f32", "gala_dense_grad_workspace",
            "gala_dense_grad_f32")
 
 

@@ -29,6 +29,8 @@ struct Backend {
     decltype(&gala_edge_softmax_bwd_f32) softmax_bwd;
     decltype(&gala_gat_fwd_f32) gat_fwd;
     decltype(&gala_gat_bwd_f32) gat_bwd;
+    decltype(&gala_gat_fwd_attn_f32) gat_fwd_attn;
+    decltype(&gala_gat_bwd_attn_f32) gat_bwd_attn;
     decltype(&gala_edge_permute_f32) permute;
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
@@ -36,12 +38,13 @@ struct Backend {
 const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32, gala_sddvv_f32,
                    gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
-                   gala_gat_bwd_f32, gala_edge_permute_f32, gala_dense_grad_workspace,
-                   gala_dense_grad_f32};
+                   gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
+                   gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
                    gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
+                   gala_cpu_gat_fwd_attn_f32, gala_cpu_gat_bwd_attn_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32};
 
@@ -558,6 +561,103 @@ bool same_pattern(const Slot &a, const Slot &b) {
            a.segs == b.segs;
 }
 
+struct GatGrads {
+    torch::Tensor daL, daR, dX;
+};
+
+// Backward of the fused GAT layer (both autograd Functions below).  r is the source logit
+// aR; with wR defined and r undefined, aR = X wR^T + bR was recomputed inside the forward
+// kernel, and is either recomputed again by the backward kernel (REF on one pattern) or
+// formed here for the other paths.
+GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tensor &x,
+                      const torch::Tensor &alpha, const torch::Tensor &dY, int64_t li,
+                      double slope, int64_t mode, int heads, const torch::Tensor &wR,
+                      const torch::Tensor &bR) {
+    Slot fw = slot(2 * li), bw = slot(2 * li + 1);
+    const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
+    CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
+    cf.c.n_cols = x.size(0);
+    check_on(dY, fw.off, "grad");
+    const bool fixed = mode == GALA_SOFTMAX_FIXED;
+    TORCH_CHECK(!fixed || bw.perm.defined(),
+                "gala: FIXED-mode GAT backward needs the transposed graph and its edge "
+                "permutation in slot 2*li+1 (transpose_perm)");
+    // dX: reference multiplies by alpha on slot 2li+1's pattern (common.h:876);
+    // FIXED: A^T with the transposed alpha
+    torch::Tensor alpha_b = fixed ? permute_edges(bw.perm, alpha, heads) : alpha;
+    torch::Tensor dX = spmm_impl(dY, bw.off, bw.cols, &alpha_b, bw.bounds, bw.segs, heads,
+                                 nullptr, nullptr, 0, 5, 7);
+    // one fused edge kernel for d alpha -> softmax bwd -> LeakyReLU bwd -> row sum when
+    // every step runs on one pattern: FIXED always (slot 2li), REF when slot 2li+1 is
+    // the forward graph itself (undirected graphs: cuda.h:1253-1257)
+    const bool same = same_pattern(fw, bw);
+    if (!r.defined() && !fixed && same) {
+        auto daL = torch::empty_like(l);
+        check(be(fw.off).gat_bwd_attn(&cf.c, l.data_ptr<float>(), wR.data_ptr<float>(),
+                                      bR.defined() ? bR.data_ptr<float>() : nullptr,
+                                      x.data_ptr<float>(), F, dY.data_ptr<float>(), F, (int32_t)F,
+                                      (float)slope, alpha.data_ptr<float>(), daL.data_ptr<float>(),
+                                      stream_of(fw.off)),
+              "gala_gat_bwd_attn_f32");
+        return {daL, daL, dX};
+    }
+    if (!r.defined()) {  // the explicit source logits for the other paths
+        r = x.mv(wR.reshape({-1}));
+        if (bR.defined()) r = r + bR.reshape({-1});
+        r = r.contiguous();
+    }
+    if (fixed || same) {
+        auto daL = torch::empty_like(l);
+        torch::Tensor dz = fixed ? torch::empty_like(alpha) : torch::Tensor();
+        const int st = be(fw.off).gat_bwd(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(),
+                                          x.data_ptr<float>(), F, dY.data_ptr<float>(), F,
+                                          (int32_t)F, heads, (float)slope, (int32_t)mode,
+                                          alpha.data_ptr<float>(),
+                                          fixed ? dz.data_ptr<float>() : nullptr,
+                                          daL.data_ptr<float>(), stream_of(fw.off));
+        if (st != GALA_ERR_UNSUPPORTED) {
+            check(st, "gala_gat_bwd_f32");
+            torch::Tensor daR = daL;
+            if (fixed) {
+                auto dzT = permute_edges(bw.perm, dz, heads);
+                daR = row_sum_impl(bw.off, bw.cols, dzT, bw.bounds,
+                                   bw.off.numel() / bw.segs - 1, bw.segs, 0.0f);
+            }
+            return {daL, daR, dX};
+        }
+    }
+    // d alpha_e = <dY_row, X_col> per head (edge_sddmm, cuda.h:808-845)
+    const Slot &ps = fixed ? fw : bw;
+    CsrView cp = view(ps.off, ps.cols, nullptr, ps.bounds, ps.segs);
+    cp.c.n_cols = x.size(0);
+    auto dalpha = torch::empty_like(alpha);
+    check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
+                           (int32_t)F, heads, dalpha.data_ptr<float>(), stream_of(ps.off)),
+          "gala_sddmm_dot_f32");
+    auto ds = torch::empty_like(alpha);
+    check(be(ps.off).softmax_bwd(&cp.c, alpha.data_ptr<float>(), dalpha.data_ptr<float>(),
+                                 heads, (int32_t)mode, ds.data_ptr<float>(), stream_of(ps.off)),
+          "gala_edge_softmax_bwd_f32");
+    // LeakyReLU backward on the recomputed logits z = aL[row] + aR[col]
+    auto z = torch::empty_like(alpha);
+    check(be(fw.off).sddvv(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(), heads,
+                           GALA_SDDVV_ADD, 0.0f, z.data_ptr<float>(), stream_of(fw.off)),
+          "gala_sddvv_f32");
+    auto dz = torch::where(z > 0, ds, ds * slope).contiguous();
+    torch::Tensor daL, daR;
+    if (!fixed) {
+        // reference: d aL = d aR = K7(ds) on slot 2li+1 (common.h:662-667)
+        daL = row_sum_impl(bw.off, bw.cols, dz, bw.bounds, nrows, bw.segs, 1e-12f);
+        daR = daL;
+    } else {
+        daL = row_sum_impl(fw.off, fw.cols, dz, fw.bounds, nrows, fw.segs, 0.0f);
+        auto dzT = permute_edges(bw.perm, dz, heads);
+        daR = row_sum_impl(bw.off, bw.cols, dzT, bw.bounds, bw.off.numel() / bw.segs - 1,
+                           bw.segs, 0.0f);
+    }
+    return {daL, daR, dX};
+}
+
 // fused GAT layer: sddvv + LeakyReLU + edge softmax + weighted aggregation in one pass
 struct GatAggregate : public torch::autograd::Function<GatAggregate> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor aL, torch::Tensor aR,
@@ -577,8 +677,8 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         check_on(r, s.off, "attn_r");
         check_on(x, s.off, "X");
         check(be(s.off).gat_fwd(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
-                               F, (int32_t)F, heads, (float)slope, (int32_t)mode,
-                               Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream_of(s.off)),
+                                F, (int32_t)F, heads, (float)slope, (int32_t)mode,
+                                Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream_of(s.off)),
               "gala_gat_fwd_f32");
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
@@ -590,81 +690,79 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         auto l = sv[0], r = sv[1], x = sv[2], alpha = sv[3];
-        auto dY = grad_outputs[0].contiguous();
-        const int64_t li = ctx->saved_data["li"].toInt();
-        const double slope = ctx->saved_data["slope"].toDouble();
-        const int64_t mode = ctx->saved_data["mode"].toInt();
-        const int heads = (int)ctx->saved_data["heads"].toInt();
-        Slot fw = slot(2 * li), bw = slot(2 * li + 1);
-        const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
-        CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
-        cf.c.n_cols = x.size(0);
-        check_on(dY, fw.off, "grad");
-        const bool fixed = mode == GALA_SOFTMAX_FIXED;
-        TORCH_CHECK(!fixed || bw.perm.defined(),
-                    "gala: FIXED-mode GAT backward needs the transposed graph and its edge "
-                    "permutation in slot 2*li+1 (transpose_perm)");
-        // dX: reference multiplies by alpha on slot 2li+1's pattern (common.h:876);
-        // FIXED: A^T with the transposed alpha
-        torch::Tensor alpha_b = fixed ? permute_edges(bw.perm, alpha, heads) : alpha;
-        torch::Tensor dX = spmm_impl(dY, bw.off, bw.cols, &alpha_b, bw.bounds, bw.segs, heads,
-                                     nullptr, nullptr, 0, 5, 7);
-        // one fused edge kernel for d alpha -> softmax bwd -> LeakyReLU bwd -> row sum when
-        // every step runs on one pattern: FIXED always (slot 2li), REF when slot 2li+1 is
-        // the forward graph itself (undirected graphs: cuda.h:1253-1257)
-        const bool same = same_pattern(fw, bw);
-        if (fixed || same) {
-            auto daL = torch::empty_like(l);
-            torch::Tensor dz = fixed ? torch::empty_like(alpha) : torch::Tensor();
-            const int st = be(fw.off).gat_bwd(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(),
-                                            x.data_ptr<float>(), F, dY.data_ptr<float>(), F,
-                                            (int32_t)F, heads, (float)slope, (int32_t)mode,
-                                            alpha.data_ptr<float>(),
-                                            fixed ? dz.data_ptr<float>() : nullptr,
-                                            daL.data_ptr<float>(), stream_of(fw.off));
-            if (st != GALA_ERR_UNSUPPORTED) {
-                check(st, "gala_gat_bwd_f32");
-                torch::Tensor daR = daL;
-                if (fixed) {
-                    auto dzT = permute_edges(bw.perm, dz, heads);
-                    daR = row_sum_impl(bw.off, bw.cols, dzT, bw.bounds,
-                                       bw.off.numel() / bw.segs - 1, bw.segs, 0.0f);
-                }
-                return {daL.view_as(l), daR.view_as(r), dX, torch::Tensor(), torch::Tensor(),
-                        torch::Tensor()};
-            }
-        }
-        // d alpha_e = <dY_row, X_col> per head (edge_sddmm, cuda.h:808-845)
-        const Slot &ps = fixed ? fw : bw;
-        CsrView cp = view(ps.off, ps.cols, nullptr, ps.bounds, ps.segs);
-        cp.c.n_cols = x.size(0);
-        auto dalpha = torch::empty_like(alpha);
-        check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
-                                 (int32_t)F, heads, dalpha.data_ptr<float>(), stream_of(ps.off)),
-              "gala_sddmm_dot_f32");
-        auto ds = torch::empty_like(alpha);
-        check(be(ps.off).softmax_bwd(&cp.c, alpha.data_ptr<float>(), dalpha.data_ptr<float>(),
-                                        heads, (int32_t)mode, ds.data_ptr<float>(), stream_of(ps.off)),
-              "gala_edge_softmax_bwd_f32");
-        // LeakyReLU backward on the recomputed logits z = aL[row] + aR[col]
-        auto z = torch::empty_like(alpha);
-        check(be(fw.off).sddvv(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(), heads,
-                             GALA_SDDVV_ADD, 0.0f, z.data_ptr<float>(), stream_of(fw.off)),
-              "gala_sddvv_f32");
-        auto dz = torch::where(z > 0, ds, ds * slope).contiguous();
-        torch::Tensor daL, daR;
-        if (!fixed) {
-            // reference: d aL = d aR = K7(ds) on slot 2li+1 (common.h:662-667)
-            daL = row_sum_impl(bw.off, bw.cols, dz, bw.bounds, nrows, bw.segs, 1e-12f);
-            daR = daL;
-        } else {
-            daL = row_sum_impl(fw.off, fw.cols, dz, fw.bounds, nrows, fw.segs, 0.0f);
-            auto dzT = permute_edges(bw.perm, dz, heads);
-            daR = row_sum_impl(bw.off, bw.cols, dzT, bw.bounds, bw.off.numel() / bw.segs - 1,
-                               bw.segs, 0.0f);
-        }
-        return {daL.view_as(l), daR.view_as(r), dX, torch::Tensor(), torch::Tensor(),
+        GatGrads g = gat_backward(l, r, x, alpha, grad_outputs[0].contiguous(),
+                                  ctx->saved_data["li"].toInt(),
+                                  ctx->saved_data["slope"].toDouble(),
+                                  ctx->saved_data["mode"].toInt(),
+                                  (int)ctx->saved_data["heads"].toInt(), {}, {});
+        return {g.daL.view_as(l), g.daR.view_as(r), g.dX, torch::Tensor(), torch::Tensor(),
                 torch::Tensor()};
+    }
+};
+
+// The DSL's GAT layer (tests/GALA-DSL/gat/*: attnR = dsl.nn.ffn(res, out=1); ...;
+// res = aggregate_fn(G.graphs, res)): the source logit is a Linear of the aggregated rows,
+// so the kernels recompute aR[col] = <X[col], wR> + bR from the X row they gather instead
+// of reading aR (gala_gat_{fwd,bwd}_attn_f32).  The Linear's gradients follow from d_aR:
+// d wR = d_aR^T X (gala_dense_grad_f32), d bR = sum d_aR, dX += d_aR wR.
+struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor aL, torch::Tensor X,
+                                 torch::Tensor wR, torch::Tensor bR, int64_t li, double slope,
+                                 int64_t mode) {
+        Slot s = slot(2 * li);
+        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        auto l = aL.contiguous(), x = X.contiguous(), w = wR.contiguous();
+        torch::Tensor b = bR.defined() && bR.numel() > 0 ? bR.contiguous() : torch::Tensor();
+        check_dev(l, torch::kFloat, "attn_l");
+        check_dev(x, torch::kFloat, "X");
+        check_dev(w, torch::kFloat, "attn_r weight");
+        const int64_t nrows = cv.c.n_rows, F = x.size(1);
+        TORCH_CHECK(l.numel() == nrows && w.numel() == F, "gala: gat_aggregate_ffn is one head");
+        check_on(l, s.off, "attn_l");
+        check_on(x, s.off, "X");
+        check_on(w, s.off, "attn_r weight");
+        if (b.defined()) check_on(b, s.off, "attn_r bias");
+        cv.c.n_cols = x.size(0);
+        auto Y = torch::empty({nrows, F}, fopts(x));
+        auto alpha = torch::empty({s.cols.numel()}, fopts(x));
+        check(be(s.off).gat_fwd_attn(&cv.c, l.data_ptr<float>(), w.data_ptr<float>(),
+                                     b.defined() ? b.data_ptr<float>() : nullptr,
+                                     x.data_ptr<float>(), F, (int32_t)F, (float)slope,
+                                     (int32_t)mode, Y.data_ptr<float>(), F,
+                                     alpha.data_ptr<float>(), stream_of(s.off)),
+              "gala_gat_fwd_attn_f32");
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["slope"] = slope;
+        ctx->saved_data["mode"] = mode;
+        ctx->saved_data["has_bias"] = b.defined();
+        ctx->save_for_backward({l, x, w, b.defined() ? b : torch::empty({0}, fopts(x)), alpha});
+        return Y;
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto sv = ctx->get_saved_variables();
+        auto l = sv[0], x = sv[1], w = sv[2], alpha = sv[4];
+        const bool has_bias = ctx->saved_data["has_bias"].toBool();
+        torch::Tensor b = has_bias ? sv[3] : torch::Tensor();
+        GatGrads g = gat_backward(l, {}, x, alpha, grad_outputs[0].contiguous(),
+                                  ctx->saved_data["li"].toInt(),
+                                  ctx->saved_data["slope"].toDouble(),
+                                  ctx->saved_data["mode"].toInt(), 1, w, b);
+        auto daR = g.daR.reshape({-1, 1}).contiguous();
+        const int64_t N = x.size(0);
+        const int32_t F = (int32_t)x.size(1);
+        auto dW = torch::empty({1, F}, fopts(x));
+        auto db = torch::empty({1}, fopts(x));
+        const Backend &B = be(x);
+        const int64_t wsb = B.dense_ws(N, F, 1);
+        TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
+        auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(x));
+        check(B.dense_grad(N, F, 1, x.data_ptr<float>(), F, daR.data_ptr<float>(), 1,
+                           dW.data_ptr<float>(), db.data_ptr<float>(), 0, ws.data_ptr<float>(),
+                           wsb, stream_of(x)),
+              "gala_dense_grad_f32");
+        g.dX.addr_(daR.reshape({-1}), w.reshape({-1}));  // through aR = X wR^T + bR
+        return {g.daL.view_as(l), g.dX, dW.view_as(w), has_bias ? db.view_as(b) : torch::Tensor(),
+                torch::Tensor(), torch::Tensor(), torch::Tensor()};
     }
 };
 
@@ -766,6 +864,12 @@ torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li) {
 torch::Tensor gat_aggregate_apply(torch::Tensor attn_l, torch::Tensor attn_r, torch::Tensor X,
                                   int64_t li, double slope, int64_t mode) {
     return GatAggregate::apply(attn_l, attn_r, X, li, slope, mode);
+}
+
+torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, torch::Tensor attn_r_weight,
+                                      torch::Tensor attn_r_bias, int64_t li, double slope,
+                                      int64_t mode) {
+    return GatAggregateFfn::apply(attn_l, X, attn_r_weight, attn_r_bias, li, slope, mode);
 }
 
 }  // namespace gala

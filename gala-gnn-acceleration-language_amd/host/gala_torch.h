@@ -131,5 +131,10 @@ torch::Tensor ffn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bia
 // using the slot's transposed graph).
 torch::Tensor gat_aggregate_apply(torch::Tensor attn_l, torch::Tensor attn_r, torch::Tensor X,
                                   int64_t li, double slope, int64_t mode);
+// the same layer with attn_r = X attn_r_weight^T + attn_r_bias recomputed inside the kernels
+// (the DSL's attnR = dsl.nn.ffn(res, out=1) of the aggregated res; one head)
+torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, torch::Tensor attn_r_weight,
+                                      torch::Tensor attn_r_bias, int64_t li, double slope,
+                                      int64_t mode);
 
 }  // namespace gala

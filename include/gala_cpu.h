@@ -53,6 +53,14 @@ int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR, 
                          int64_t ldx, const float *dY, int64_t lddy, int32_t F, int32_t heads,
                          float slope, int32_t mode, const float *alpha, float *d_logit,
                          float *d_aL, void *stream);
+int gala_cpu_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                              const float *bR, const float *X, int64_t ldx, int32_t F,
+                              float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
+                              void *stream);
+int gala_cpu_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                              const float *bR, const float *X, int64_t ldx, const float *dY,
+                              int64_t lddy, int32_t F, float slope, const float *alpha,
+                              float *d_aL, void *stream);
 int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                               float *dst, void *stream);
 int64_t gala_cpu_dense_grad_workspace(int64_t n_rows, int32_t K, int32_t M);

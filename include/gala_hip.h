@@ -234,6 +234,23 @@ int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR, cons
                      float slope, int32_t mode, const float *alpha, float *d_logit, float *d_aL,
                      void *stream);
 
+/*
+ * The same fused forward / backward with the source logit recomputed from the aggregated
+ * rows instead of read from aR: aR[j] = <X[j, 0:F], wR[0:F]> + bR[0] (bR nullable = 0).
+ * This is the DSL's GAT layer, where attnR = dsl.nn.ffn(res, out=1) is a Linear of the
+ * very `res` that the layer aggregates (tests/GALA-DSL/gat/Products/h100.txt:7-11): the
+ * kernels gather X[col] anyway, so the per-edge aR[col] read disappears.  One head.
+ * gala_gat_bwd_attn_f32 is REF mode (d_aL = d_aR, no per-edge output).  The gradients
+ * of wR / bR / X through aR follow from d_aR on the caller's side (dense, per row).
+ */
+int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                          const float *bR, const float *X, int64_t ldx, int32_t F, float slope,
+                          int32_t mode, float *Y, int64_t ldy, float *alpha_out, void *stream);
+int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
+                          const float *bR, const float *X, int64_t ldx, const float *dY,
+                          int64_t lddy, int32_t F, float slope, const float *alpha, float *d_aL,
+                          void *stream);
+
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                           float *dst, void *stream);

@@ -199,6 +199,9 @@ def run(ir, graphs: Graphs, X, params, segments=1):
                 y = a[2] * y
         elif op == "GAT_AGGREGATE":
             rp, col = graphs.edges(gi)
+            if nd["weight"]:  # gat_aggregate_ffn: attnR = Linear(X) of the aggregated rows
+                w = nd["weight"]
+                a[1] = a[2] @ params[w + ".weight"].T + params[w + ".bias"]
             if ir["sched"]["gat_mode"] == 0:
                 y = _GatRef.apply(a[0], a[1], a[2], rp, col, graphs.n, nd["param"])
             else:

@@ -176,6 +176,31 @@ def test_gat_fwd_bwd(graph, mode, F, heads):
     np.testing.assert_allclose(dz, dz_ref, **TOL)
 
 
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+def test_gat_attention_recompute(graph, mode):
+    F = 47
+    aL = features(graph.n_rows, 1, seed=51)
+    X = features(graph.n_cols, F, seed=53)
+    dY = features(graph.n_rows, F, seed=54)
+    wR = features(1, F, seed=55).ravel() * 0.5
+    bR = np.array([0.1], np.float32)
+    aR = (X.astype(np.float64) @ wR.astype(np.float64) + 0.1).astype(np.float32)
+    og = to_oracle(graph)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=1, slope=0.2, mode=mode)
+    Y = np.empty((graph.n_rows, F), np.float32)
+    al = np.empty(graph.nnz, np.float32)
+    _abi.call_cpu("gala_gat_fwd_attn_f32", HostCsr(graph).ref, P(aL), P(wR), P(bR), P(X), F, F, 0.2, mode,
+                  P(Y), F, P(al), None)
+    np.testing.assert_allclose(al, al_ref, **TOL)
+    np.testing.assert_allclose(Y, Y_ref, **TOL)
+    if mode == _abi.GALA_SOFTMAX_REF:
+        _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=1, slope=0.2, mode=mode)
+        daL = np.empty(graph.n_rows, np.float32)
+        _abi.call_cpu("gala_gat_bwd_attn_f32", HostCsr(graph).ref, P(aL), P(wR), P(bR), P(X), F, P(dY), F, F,
+                      0.2, P(al_ref), P(daL), None)
+        np.testing.assert_allclose(daL, daL_ref, **TOL)
+
+
 def test_edge_permute_and_dense_grad():
     g = powerlaw()
     t, perm = layout.transpose(g)

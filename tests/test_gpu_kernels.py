@@ -244,6 +244,31 @@ def test_gat_bwd_fused(graph, mode, F, heads, tiled):
         np.testing.assert_allclose(host(dz), dz_ref, **TOL)
 
 
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F", [32, 47, 64])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_gat_attention_recompute(graph, mode, F, tiled):
+    """gala_gat_{fwd,bwd}_attn_f32: aR = X wR + bR recomputed from the gathered rows,
+    against the oracle chain on that aR (computed here in float64, rounded to fp32)."""
+    g = layout.col_tile(graph, 1000) if tiled else graph
+    aL = features(g.n_rows, 1, seed=51)
+    X = features(g.n_cols, F, seed=53)
+    dY = features(g.n_rows, F, seed=54)
+    wR = features(1, F, seed=55).ravel() * 0.5
+    bR = np.array([0.1], np.float32)
+    aR = (X.astype(np.float64) @ wR.astype(np.float64) + 0.1).astype(np.float32)
+    og = to_oracle(g)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=1, slope=0.2, mode=mode)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    Y, al = ops.gat_fwd_attn(dg, dev(aL), dev(wR), dev(bR), dev(X), slope=0.2, mode=mode, want_alpha=True)
+    np.testing.assert_allclose(host(al), al_ref, **TOL)
+    np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+    if mode == _abi.GALA_SOFTMAX_REF:
+        _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=1, slope=0.2, mode=mode)
+        daL = ops.gat_bwd_attn(dg, dev(aL), dev(wR), dev(bR), dev(X), dev(dY), dev(al_ref), slope=0.2)
+        np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+
+
 def test_edge_permute():
     g = powerlaw()
     t, perm = layout.transpose(g)

@@ -188,6 +188,35 @@ def test_gat_fused_fixed_mode_true_gradients(E, heads, D):
     np.testing.assert_allclose(aR.grad.cpu().numpy(), r64.grad.numpy(), atol=1e-4, rtol=1e-3)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("F", [32, 47])
+def test_gat_ffn_recompute_matches_explicit_attention(E, mode, F):
+    """gat_aggregate_ffn_apply (aR = Linear(X) recomputed in the kernels) against
+    gat_aggregate_apply on aR = torch Linear(X): output and the gradients of aL, X and the
+    attention Linear (through aR), within fp32 tolerance."""
+    g = powerlaw(n=1500, m=9000)
+    push_graph(E, g, with_transpose=(mode == 1))
+    N = g.n_rows
+    aL0, X0 = features(N, 1, seed=1), features(N, F, seed=3)
+    lin0 = torch.nn.Linear(F, 1).cuda()
+    outs, grads = [], []
+    for ffn in (False, True):
+        aL = dev(aL0).requires_grad_()
+        X = dev(X0).requires_grad_()
+        lin = torch.nn.Linear(F, 1).cuda()
+        lin.load_state_dict(lin0.state_dict())
+        if ffn:
+            Y = E.gat_aggregate_ffn_apply(aL, X, lin.weight, lin.bias, 0, 0.2, mode)
+        else:
+            Y = E.gat_aggregate_apply(aL, lin(X), X, 0, 0.2, mode)
+        (Y * torch.linspace(-1, 1, F, device="cuda")).sum().backward()
+        outs.append(Y.detach().cpu().numpy())
+        grads.append([t.grad.cpu().numpy() for t in (aL, X, lin.weight, lin.bias)])
+    np.testing.assert_allclose(outs[1], outs[0], **TOL)
+    for a, b in zip(grads[1], grads[0]):
+        np.testing.assert_allclose(a, b, atol=1e-4, rtol=1e-3)
+
+
 def test_errors_are_exceptions_not_exit(E):
     g = cora_like()
     off, cols, vals, _ = push_graph(E, g)

@@ -102,6 +102,26 @@ def gat(hg):
             t = timeit(fb, reps=5, warm=2)
             emit(config="products_gat", op="gat_layer_fwd_bwd", mode=["REF", "FIXED"][mode], heads=heads,
                  D=D, ms=t * 1e3, edges_per_s=E / t)
+        if heads == 1:
+            # the DSL's layer: attnR = Linear(X) recomputed inside the kernels
+            wR = torch.rand(F, device="cuda") - 0.5
+            bR = torch.zeros(1, device="cuda")
+            emit(config="products_gat", op="gat_fwd_attn", heads=1, D=D,
+                 ms=timeit(lambda: ops.gat_fwd_attn(dg, aL, wR, bR, X, want_alpha=True), reps=5) * 1e3)
+            al1 = torch.rand(E, device="cuda")
+            emit(config="products_gat", op="gat_bwd_attn", heads=1, D=D,
+                 ms=timeit(lambda: ops.gat_bwd_attn(dg, aL, wR, bR, X, X, al1), reps=5) * 1e3)
+            for mode in (0, 1):
+                l = aL.clone().requires_grad_()
+                x = X.clone().requires_grad_()
+                lin = torch.nn.Linear(F, 1).cuda()
+
+                def fbf():
+                    Y = E_.gat_aggregate_ffn_apply(l, x, lin.weight, lin.bias, mode, 0.2, mode)
+                    Y.backward(torch.ones_like(Y))
+                t = timeit(fbf, reps=5, warm=2)
+                emit(config="products_gat", op="gat_layer_ffn_fwd_bwd", mode=["REF", "FIXED"][mode], heads=1,
+                     D=D, ms=t * 1e3, edges_per_s=E / t)
         s = torch.rand(E * heads, device="cuda")
         emit(config="products_gat", op="sddvv_lrelu", heads=heads,
              ms=timeit(lambda: ops.sddvv(dg, aL, aR, op=2, heads=heads)) * 1e3)
