@@ -90,6 +90,28 @@ def load_traffic(kernel_substr: str):
     return None
 
 
+def gather_ceiling(col, X, stream, reps=10):
+    """Time (HIP events, same stream) an unordered gather of the very rows the SpMM fetches:
+    X[col[e]] for every edge e, any order, no row bookkeeping, no output rows
+    (tools/gather_ceiling.hip -> tools/libgala_probe.so).  The floor for any kernel that
+    fetches one X row per edge.  None when the probe library was not built."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libgala_probe.so")
+    if not os.path.exists(path) or X.shape[1] not in (32, 128, 256):
+        return None
+    L = ctypes.CDLL(path)
+    fn = L.gala_probe_gather_f32
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                   ctypes.c_void_p]
+    E, F = col.numel(), X.shape[1]
+    out = torch.empty(((E + 63) // 64, F), device=X.device, dtype=torch.float32)
+    args = (col.data_ptr(), X.data_ptr(), E, F, out.data_ptr(), stream.cuda_stream)
+    if fn(*args) != 0:
+        return None
+    return event_time(lambda: fn(*args), reps, stream)
+
+
 def event_time(fn, reps, stream):
     ts = []
     for _ in range(reps):
@@ -213,6 +235,13 @@ def main():
                                      "uniform random columns: each edge's 128-B X row misses L2"},
         "event_ms_per_step": ev0.elapsed_time(ev1) / args.steps,
     }
+    t_ceil = gather_ceiling(seg0.col, agg.Xs, stream)
+    if t_ceil:
+        out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
+        out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_kernel
+        out["roofline"]["gather_ceiling_note"] = (
+            "same process and graph: X[col[e]] for every edge, unordered, no output rows "
+            "(tools/gather_ceiling.hip); the SpMM's floor on a graph without reuse")
     if world > 1:
         send = agg.Xs[:part.b]
         recv = agg.Xs[part.n:]

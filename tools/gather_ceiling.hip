@@ -7,6 +7,9 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/gather_ceiling tools/gather_ceiling.hip
 //   tools/gather_ceiling [N] [E] [F]
+// With -DGALA_PROBE_LIB -shared -fPIC it builds tools/libgala_probe.so instead, whose
+// gala_probe_gather_f32 bench.py times on the benchmark graph's own column array
+// (measurement code only; the product library never contains it).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -99,6 +102,25 @@ static float run(const int32_t *idx, const float *X, int64_t E, float *out, cons
     return ms;
 }
 
+// Unordered gather of X[idx[e], 0:F] for all e (chunks of 64 edges per row group, 4 rows
+// in flight per lane), summed per chunk into out[E/64, F].  F = 32, 128 or 256.
+extern "C" int gala_probe_gather_f32(const int32_t *idx, const float *X, int64_t E, int32_t F,
+                                     float *out, void *stream) {
+    constexpr int C = 64;
+    const int64_t groups = (E + C - 1) / C;
+    hipStream_t st = (hipStream_t)stream;
+    if (F == 32)
+        hipLaunchKernelGGL((k_gather<8, 4, C, false>), dim3((groups * 8 + 255) / 256), dim3(256), 0, st, idx, X, E, out);
+    else if (F == 128)
+        hipLaunchKernelGGL((k_gather<32, 8, C, false>), dim3((groups * 32 + 255) / 256), dim3(256), 0, st, idx, X, E, out);
+    else if (F == 256)
+        hipLaunchKernelGGL((k_gather<64, 4, C, false>), dim3((groups * 64 + 255) / 256), dim3(256), 0, st, idx, X, E, out);
+    else
+        return -2;
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+#ifndef GALA_PROBE_LIB
 int main(int argc, char **argv) {
     const int32_t N = argc > 1 ? atoi(argv[1]) : 2449029;
     const int64_t E = argc > 2 ? atoll(argv[2]) : 126167309LL;
@@ -127,3 +149,4 @@ int main(int argc, char **argv) {
     }
     return 0;
 }
+#endif
