@@ -261,6 +261,23 @@ extern "C" int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32
     return GALA_OK;
 }
 
+extern "C" int gala_host_row_order(int64_t n_rows, const int32_t *rowptr, int32_t *order) {
+    if (n_rows < 0 || (n_rows > 0 && (!rowptr || !order))) return GALA_ERR_INVALID_ARG;
+    constexpr int64_t kCap = 4096;
+    std::vector<int64_t> start(kCap + 2, 0);
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t deg = (int64_t)rowptr[r + 1] - rowptr[r];
+        if (deg < 0) return GALA_ERR_GRAPH;
+        start[kCap - std::min(deg, kCap) + 1]++;  // bucket 0 = the longest rows
+    }
+    for (int64_t b = 1; b <= kCap + 1; ++b) start[b] += start[b - 1];
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t deg = (int64_t)rowptr[r + 1] - rowptr[r];
+        order[start[kCap - std::min(deg, kCap)]++] = (int32_t)r;
+    }
+    return GALA_OK;
+}
+
 extern "C" int gala_host_mask_subgraph(int64_t n_rows, const int32_t *rowptr, const int32_t *col,
                                        const int32_t *mask, int32_t *out_rowptr,
                                        int32_t *out_col, int32_t *next_mask) {

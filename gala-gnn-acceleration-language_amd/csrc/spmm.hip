@@ -51,6 +51,7 @@ struct SpmmParams {
     int32_t accum;      // 1: Y += ..., 0: Y = ...
     int32_t nsamp, ra, rb;
     int32_t split_threshold;  // > 0: rows longer than this are left to the split kernels
+    const int32_t *row_order; // nullable: row group i handles row row_order[i]
     SegTable seg;
 };
 
@@ -183,8 +184,9 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
     const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
-    const int64_t row = wave * RPW + lane / G;
-    if (row >= p.n_rows) return;
+    const int64_t rid = wave * RPW + lane / G;
+    if (rid >= p.n_rows) return;
+    const int64_t row = p.row_order ? (int64_t)p.row_order[rid] : rid;
     KernargSegPtr seg = kernarg_segtable(offsetof(SpmmParams, seg));
     if (p.split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > p.split_threshold)
         return;  // hub row: done by k_spmm_chunk + k_spmm_fixup
@@ -319,10 +321,8 @@ __global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
 }
 
 // ---- dispatch ---------------------------------------------------------------------------
-template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
-static void launch_rg(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
-    // U: edges whose loads are in flight before the first add (per lane: U*CH vectors)
-    constexpr int U = (CH * VEC >= 16) ? 2 : ((CH * VEC >= 8) ? 4 : 8);
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
     constexpr int rows_per_block = (kBlock / kWave) * (kWave / G);
     const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
     hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
@@ -335,6 +335,16 @@ static void launch_rg(const SpmmParams &p, const SplitParams *sp, hipStream_t st
         hipLaunchKernelGGL((k_spmm_fixup<VEC, G, CH, W>), dim3((unsigned)fb), dim3(kBlock), 0, st, p,
                            *sp);
     }
+}
+
+template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
+static void launch_rg(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
+    // U: edges whose loads are in flight before the first add (per lane: U*CH vectors).
+    // Measured on the Products shape (tools/spmm_sweep.py, uniform and R-MAT graphs):
+    // 8 or 16 lanes per row (F = 32, 64) are fastest with 4 edges in flight (F = 32: 2.44
+    // vs 2.60 ms at 8); narrower and wider rows keep 8.
+    constexpr int U = (CH * VEC >= 16) ? 2 : (CH * VEC >= 8) ? 4 : (VEC == 4 && (G == 8 || G == 16)) ? 4 : 8;
+    launch_rg_u<VEC, G, CH, U, W, SAMP, SRCS>(p, sp, st);
 }
 
 template <int VEC, int G, int CH>
@@ -435,12 +445,14 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     p.ra = ra;
     p.rb = rb;
     p.split_threshold = 0;
+    p.row_order = nullptr;
     hipStream_t hs = (hipStream_t)stream;
 
     // hub rows: chunk partials + ordered fix-up (plan built once per graph on the host)
     SplitParams spl{};
     const SplitParams *sp = nullptr;
     const gala_split_plan_t *plan = A->split;
+    if (plan && plan->row_order && A->n_seg == 1) p.row_order = plan->row_order;
     if (plan && plan->n_chunks > 0 && A->n_seg == 1 && !samp && !(flags & GALA_SPMM_EXACT)) {
         if (plan->threshold < 1 || plan->chunk < 1 || !plan->rows || !plan->row_chunk0 ||
             !plan->chunk_row || !plan->workspace)

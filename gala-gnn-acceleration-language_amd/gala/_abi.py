@@ -42,6 +42,7 @@ class gala_split_plan_t(ctypes.Structure):
         ("chunk_row", ctypes.c_void_p),
         ("workspace", ctypes.c_void_p),
         ("ws_cols", ctypes.c_int64),
+        ("row_order", ctypes.c_void_p),
     ]
 
 
@@ -91,6 +92,7 @@ SIGNATURES = {
     "gala_host_sample_ab": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "gala_host_split_plan": (ctypes.c_int, [_I64, _P, _I32, _I32, _P, _P, _P, _P, _P]),
     "gala_host_csr_transpose": (ctypes.c_int, [_I64, _I64, _P, _P, _P, _P, _P]),
+    "gala_host_row_order": (ctypes.c_int, [_I64, _P, _P]),
     "gala_host_gen_graph": (ctypes.c_int, [_I32, _I64, _I64, ctypes.c_uint64, _P, _P]),
     "gala_host_mask_subgraph": (ctypes.c_int, [_I64, _P, _P, _P, _P, _P, _P]),
     "gala_dense_grad_workspace": (ctypes.c_int64, [_I64, _I32, _I32]),

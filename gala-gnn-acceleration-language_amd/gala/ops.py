@@ -50,33 +50,45 @@ class DeviceGraph:
         dg = cls(g.n_rows, g.n_cols, rp, col, val, g.n_seg, g.bounds, g.val_heads)
         if split and g.n_seg == 1 and g.n_rows > 0:
             deg = np.diff(g.rowptr)
-            thr = max(1024, 8 * int(np.ceil(g.nnz / max(g.n_rows, 1))))
+            mean = g.nnz / max(g.n_rows, 1)
+            thr = max(1024, 8 * int(np.ceil(mean)))
             if split != "auto":
                 thr = int(split)
-            if deg.max(initial=0) > thr:
-                dg.set_split_plan(g.rowptr, thr, chunk=512)
+            hubs = deg.max(initial=0) > thr
+            skewed = deg.max(initial=0) > 4 * max(mean, 1.0)
+            if hubs or skewed:
+                dg.set_split_plan(g.rowptr, thr if hubs else 0, chunk=512, row_order=skewed)
         return dg
 
-    def set_split_plan(self, host_rowptr, threshold: int, chunk: int = 512):
-        """Hub-row splitting (gala_split_plan_t), built from the host rowptr."""
+    def set_split_plan(self, host_rowptr, threshold: int, chunk: int = 512, row_order: bool = False):
+        """Hub-row splitting and / or a degree-ordered row schedule (gala_split_plan_t), built
+        from the host rowptr.  threshold 0: no hub rows, only the row order."""
         rp = np.ascontiguousarray(host_rowptr, np.int32)
-        nr = ctypes.c_int64()
-        nc = ctypes.c_int64()
-        _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk, None, None,
-                  None, ctypes.byref(nr), ctypes.byref(nc))
-        rows = np.empty(max(nr.value, 1), np.int32)
-        rc0 = np.empty(nr.value + 1, np.int32)
-        crow = np.empty(max(nc.value, 1), np.int32)
-        _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk,
-                  rows.ctypes.data, rc0.ctypes.data, crow.ctypes.data, ctypes.byref(nr), ctypes.byref(nc))
+        nr = ctypes.c_int64(0)
+        nc = ctypes.c_int64(0)
+        rows, rc0, crow = np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(1, np.int32)
+        if threshold > 0:
+            _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk, None, None,
+                      None, ctypes.byref(nr), ctypes.byref(nc))
+            rows = np.empty(max(nr.value, 1), np.int32)
+            rc0 = np.empty(nr.value + 1, np.int32)
+            crow = np.empty(max(nc.value, 1), np.int32)
+            _abi.call("gala_host_split_plan", self.n_rows, rp.ctypes.data, threshold, chunk,
+                      rows.ctypes.data, rc0.ctypes.data, crow.ctypes.data, ctypes.byref(nr), ctypes.byref(nc))
+        order = None
+        if row_order:
+            order = np.empty(max(self.n_rows, 1), np.int32)
+            _abi.call("gala_host_row_order", self.n_rows, rp.ctypes.data, order.ctypes.data)
         dev = self.col.device
         arrays = tuple(torch.from_numpy(a).to(dev) for a in (rows, rc0, crow))
+        order_t = None if order is None else torch.from_numpy(order).to(dev)
         plan = _abi.gala_split_plan_t()
-        plan.threshold, plan.chunk = threshold, chunk
+        plan.threshold, plan.chunk = max(threshold, 1), chunk
         plan.n_rows_split, plan.n_chunks = nr.value, nc.value
         plan.rows, plan.row_chunk0, plan.chunk_row = (a.data_ptr() for a in arrays)
         plan.workspace, plan.ws_cols = None, 0
-        self._split = {"plan": plan, "arrays": arrays, "ws": None}
+        plan.row_order = None if order_t is None else order_t.data_ptr()
+        self._split = {"plan": plan, "arrays": arrays + (order_t,), "ws": None}
         self._csr = None
 
     @property

@@ -229,27 +229,41 @@ void SplitState::ensure_workspace(int64_t F) {
     plan.ws_cols = F;
 }
 
+// Hub-row split plan and degree-ordered row schedule of a device graph (gala_split_plan_t),
+// built once per graph on the host: hub rows (deg > max(1024, 8 x mean)) are split into
+// chunks; a skewed graph (max deg > 4 x mean) also gets the descending-degree row order.
 std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int segments) {
     if (segments != 1 || !offsets.defined() || offsets.numel() < 2) return nullptr;
     auto rp = offsets.to(torch::kCPU, torch::kInt).contiguous();
     const int64_t n = rp.numel() - 1;
     const int32_t *r = rp.data_ptr<int32_t>();
     const int64_t nnz = r[n];
+    const double mean = (double)nnz / (double)std::max<int64_t>(n, 1);
+    int64_t max_deg = 0;
+    for (int64_t i = 0; i < n; ++i) max_deg = std::max<int64_t>(max_deg, r[i + 1] - r[i]);
     const int32_t thr = (int32_t)std::max<int64_t>(1024, 8 * ((nnz + n - 1) / std::max<int64_t>(n, 1)));
     const int32_t chunk = 512;
+    const bool skewed = (double)max_deg > 4.0 * std::max(mean, 1.0);
     int64_t nr = 0, nc = 0;
     check(gala_host_split_plan(n, r, thr, chunk, nullptr, nullptr, nullptr, &nr, &nc),
           "gala_host_split_plan");
-    if (nr == 0) return nullptr;
+    if (nr == 0 && !skewed) return nullptr;
     auto io = torch::TensorOptions().dtype(torch::kInt);
-    auto rows = torch::empty({nr}, io), rc0 = torch::empty({nr + 1}, io), crow = torch::empty({nc}, io);
-    check(gala_host_split_plan(n, r, thr, chunk, rows.data_ptr<int32_t>(), rc0.data_ptr<int32_t>(),
-                               crow.data_ptr<int32_t>(), &nr, &nc),
-          "gala_host_split_plan");
+    auto rows = torch::empty({std::max<int64_t>(nr, 1)}, io), rc0 = torch::zeros({nr + 1}, io),
+         crow = torch::empty({std::max<int64_t>(nc, 1)}, io);
+    if (nr > 0)
+        check(gala_host_split_plan(n, r, thr, chunk, rows.data_ptr<int32_t>(), rc0.data_ptr<int32_t>(),
+                                   crow.data_ptr<int32_t>(), &nr, &nc),
+              "gala_host_split_plan");
     auto st = std::make_shared<SplitState>();
     st->rows = rows.to(offsets.device());
     st->row_chunk0 = rc0.to(offsets.device());
     st->chunk_row = crow.to(offsets.device());
+    if (skewed) {
+        auto order = torch::empty({n}, io);
+        check(gala_host_row_order(n, r, order.data_ptr<int32_t>()), "gala_host_row_order");
+        st->row_order = order.to(offsets.device());
+    }
     st->plan.threshold = thr;
     st->plan.chunk = chunk;
     st->plan.n_rows_split = nr;
@@ -259,6 +273,7 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
     st->plan.chunk_row = st->chunk_row.data_ptr<int32_t>();
     st->plan.workspace = nullptr;
     st->plan.ws_cols = 0;
+    st->plan.row_order = st->row_order.defined() ? st->row_order.data_ptr<int32_t>() : nullptr;
     return st;
 }
 

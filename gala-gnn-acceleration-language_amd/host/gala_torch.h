@@ -33,11 +33,12 @@ namespace gala {
 // Hub-row split plan of one graph (gala_split_plan_t + the device arrays it points to).
 struct SplitState {
     gala_split_plan_t plan{};
-    torch::Tensor rows, row_chunk0, chunk_row, ws;
+    torch::Tensor rows, row_chunk0, chunk_row, row_order, ws;
     void ensure_workspace(int64_t F);
 };
 // Builds the plan from the device rowptr (one D2H copy) when some row is longer than
-// max(1024, 8 * mean degree); returns nullptr otherwise or for tiled graphs.
+// max(1024, 8 * mean degree) (hub-row split) or the graph is skewed (max degree > 4 x
+// mean: descending-degree row order); returns nullptr otherwise or for tiled graphs.
 std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int segments);
 
 // The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's

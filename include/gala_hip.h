@@ -75,6 +75,12 @@ typedef struct gala_split_plan {
     const int32_t *chunk_row;  /* device [n_chunks]: index into rows[] of every chunk    */
     float *workspace;          /* device [n_chunks * ws_cols] partial results            */
     int64_t ws_cols;           /* floats per chunk (>= F for SpMM, >= F + 2*heads GAT)    */
+    const int32_t *row_order;  /* device [n_rows] or NULL: the SpMM processes rows in this
+                                  order (gala_host_row_order: by descending degree), so the
+                                  rows sharing a wavefront have similar lengths on skewed
+                                  graphs; results are unchanged (every row is still one
+                                  sequential pass).  A plan may carry only a row order
+                                  (n_chunks == 0).                                       */
 } gala_split_plan_t;
 
 typedef struct gala_csr {
@@ -303,6 +309,13 @@ int gala_host_sample_ab(int64_t n_rows, const int32_t *rowptr, const int32_t *co
 int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshold, int32_t chunk,
                          int32_t *rows, int32_t *row_chunk0, int32_t *chunk_row,
                          int64_t *n_rows_split, int64_t *n_chunks);
+
+/*
+ * Row schedule for skewed graphs: order[] = the rows sorted by descending degree (stable
+ * counting sort; degrees above 4096 share one bucket).  Degree-aware row binning
+ * (SURVEY §7): rows that share a wavefront then have similar lengths.
+ */
+int gala_host_row_order(int64_t n_rows, const int32_t *rowptr, int32_t *order);
 
 /*
  * Transpose a CSR (n_seg == 1): out_rowptr [n_cols+1], out_col [nnz], perm [nnz] with

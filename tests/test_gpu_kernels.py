@@ -342,7 +342,8 @@ def assert_reordered_sum(Y, g, X, val=None, dst_scale=None, Y0=None):
     """
     import scipy.sparse as sp
     v = np.ones(g.nnz) if val is None else np.asarray(val, np.float64)
-    A = sp.csr_matrix((v, g.col, g.rowptr), shape=(g.n_rows, g.n_cols))
+    # copies: scipy canonicalises (sums duplicate edges) in place on the arrays it is given
+    A = sp.csr_matrix((v, g.col.copy(), g.rowptr.copy()), shape=(g.n_rows, g.n_cols))
     X64 = X.astype(np.float64)
     exact = A @ X64
     mass = abs(A) @ np.abs(X64)
@@ -374,6 +375,30 @@ def test_spmm_split_hub_rows(F, weighted):
     np.testing.assert_array_equal(Y[light], ref[light])       # other rows: still bit-exact
     Ye = host(ops.spmm(dg, dev(X), exact=True))                # GALA_SPMM_EXACT: no split
     np.testing.assert_array_equal(Ye, ref)
+
+
+@pytest.mark.parametrize("F", [1, 32, 47, 256])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("hubs", [False, True])
+def test_spmm_row_order_bitexact(F, weighted, hubs):
+    """Degree-ordered row schedule (gala_host_row_order), alone and with the hub-row split:
+    rows run in another order, each still one sequential pass -> bit-identical (without
+    hubs), and the sampled path too."""
+    g = powerlaw()
+    val = edge_values(g.nnz) if weighted else None
+    X = features(g.n_cols, F)
+    dg = ops.DeviceGraph.from_host(layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, g.col, val), split=False)
+    dg.set_split_plan(g.rowptr, 64 if hubs else 0, chunk=32, row_order=True)
+    ref = orc.spmm(to_oracle(g, val), X)
+    got = host(ops.spmm(dg, dev(X)))
+    if hubs:
+        assert_reordered_sum(got, g, X, val)                     # split rows: chunked order
+        light = np.diff(g.rowptr) <= 64
+        np.testing.assert_array_equal(got[light], ref[light])  # the others: bit-exact
+    else:
+        np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(host(ops.spmm(dg, dev(X), nsamp=20)),
+                                  orc.spmm(to_oracle(g, val), X, sample=True, nsamp=20))
 
 
 def test_spmm_split_with_norms_and_accum():

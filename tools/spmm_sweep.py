@@ -41,9 +41,18 @@ def main():
     ap.add_argument("--u", type=int, default=61_859_140)
     ap.add_argument("--F", default="8,16,32,64,128")
     ap.add_argument("--ops", default="spmm,spmm_scaled,degree,sddvv,softmax,sddmm,gat")
+    ap.add_argument("--sort-rows", action="store_true")
     args = ap.parse_args()
     t0 = time.time()
     hg = layout.gen_graph(args.graph, args.n, args.u, seed=42)
+    if args.sort_rows:  # experiment: rows relabelled by descending degree (stable)
+        deg = np.diff(hg.rowptr)
+        order = np.argsort(-deg, kind="stable")
+        rp = np.zeros(hg.n_rows + 1, np.int64)
+        rp[1:] = np.cumsum(deg[order])
+        starts = hg.rowptr[:-1][order].astype(np.int64)
+        idx = np.repeat(starts - rp[:-1], deg[order]) + np.arange(hg.nnz)
+        hg = layout.HostGraph(hg.n_rows, hg.n_cols, rp.astype(np.int32), hg.col[idx])
     print(f"graph built {time.time()-t0:.1f}s N={hg.n_rows} E={hg.nnz}", file=sys.stderr, flush=True)
     dg = ops.DeviceGraph.from_host(hg)
     N, E = hg.n_rows, hg.nnz
