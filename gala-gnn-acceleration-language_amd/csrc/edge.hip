@@ -616,163 +616,315 @@ __device__ __forceinline__ void load_attn(const Lanes<G, VEC, CH> &ln, const flo
         for (int i = 0; i < VEC; ++i) w[ch][i] = ln.valid[ch] ? wR[ln.off[ch] + i] : 0.0f;
 }
 
-template <int G, int VEC, int U, int MODE, int CH, bool RC>
-__global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *aL, const float *aR,
-                                                    const float *X, int64_t ldx, int32_t F,
-                                                    float slope, float *Y, int64_t ldy,
-                                                    float *alpha_out, const float *wR,
-                                                    const float *bR) {
-    typedef typename GVec<VEC>::T V;
-    GALA_ROW_PROLOGUE(G);
-    if (!row_ok) return;
-    const int H = p.heads;  // CH > 1 and RC only with H == 1
-    const int D = F / H;
-    const Lanes<G, VEC, CH> ln(gl, F);
-    const bool cv = ln.valid[0];
-    const int64_t fo = ln.off[0];
-    const int hh = (int)(fo / D);
-    const float al = aL[row * H + hh];
+// Operands of the fused GAT kernels (forward and backward).
+struct GatDev {
+    const float *aL, *aR, *wR, *bR;  // aR == nullptr: recompute aR from X, wR, bR (RC)
+    const float *X;
+    const float *dY, *alpha;         // backward
+    float *Y, *alpha_out;            // forward
+    float *d_logit, *d_aL;           // backward
+    int64_t ldx, ldy, lddy;
+    int32_t F;
+    float slope;
+};
+
+// Device view of the hub-row plan: rows longer than `threshold` are cut into chunks of
+// `chunk` edges that separate row groups run in parallel; their per-chunk partial state
+// goes to ws (ws_cols floats per chunk) and fix-up kernels combine it in chunk order.
+struct GatSplit {
+    const int32_t *rows, *row_chunk0, *chunk_row;
+    float *ws;
+    int64_t ws_cols, n_chunks, n_rows_split;
+    int32_t chunk, threshold;
+};
+
+// The lane's share of one row (or one chunk of a hub row) for the GAT kernels.
+template <int G, int VEC, int CH, bool RC>
+struct GatLane {
+    Lanes<G, VEC, CH> ln;
+    int H, D, hh;
+    bool cv, leader;
+    float al, wb;
     float w[CH][VEC];
-    float wb = 0.0f;
-    if (RC) {
-        load_attn<G, VEC, CH>(ln, wR, w);
-        wb = bR ? bR[0] : 0.0f;
+    __device__ __forceinline__ GatLane(const EdgeParams &p, const GatDev &d, int gl, int64_t row)
+        : ln(gl, d.F) {
+        H = p.heads;  // CH > 1 and RC only with H == 1
+        D = d.F / H;
+        cv = ln.valid[0];
+        hh = (int)(ln.off[0] / D);
+        leader = cv && (ln.off[0] % D) == 0;
+        al = d.aL[row * H + hh];
+        wb = 0.0f;
+        if (RC) {
+            load_attn<G, VEC, CH>(ln, d.wR, w);
+            wb = d.bR ? d.bR[0] : 0.0f;
+        }
     }
+};
+
+// Running state of the forward for one row / chunk: per lane CH x VEC accumulators and the
+// head's (max, sum) of the softmax (FIXED: online, relative to m; REF: plain sums).
+template <int VEC, int CH>
+struct FwdState {
     float acc[CH][VEC];
+    float m, sum;
+    __device__ __forceinline__ FwdState() : m(-INFINITY), sum(0.0f) {
 #pragma unroll
-    for (int ch = 0; ch < CH; ++ch)
+        for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[ch][i] = 0.0f;
-    float m = -INFINITY, sum = 0.0f;
-    // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
-    // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
-    // place: a contiguous re-read of the row instead of a second col -> aR gather.
-    const bool park = alpha_out != nullptr && (G % H) == 0;
-    const bool leader = park && cv && (fo % D) == 0;
-    for (int s = 0; s < p.seg.n; ++s) {
-        int64_t e0, e1;
-        row_range(p, s, row, e0, e1);
-        const int32_t n = (int32_t)(e1 - e0);
-        for (int32_t j0 = 0; j0 < n; j0 += U) {
-            int64_t c[U];
-            float ar[U];
-            V x[U][CH];
+            for (int i = 0; i < VEC; ++i) acc[ch][i] = 0.0f;
+    }
+};
+
+// Edges [e0, e1) of `row` into the forward state.  When `park`, the head leader lane parks
+// each edge's exp term (REF) or logit (FIXED) in alpha_out for the alpha pass.
+template <int G, int VEC, int U, int MODE, int CH, bool RC>
+__device__ __forceinline__ void gat_fwd_range(const EdgeParams &p, const GatDev &d,
+                                              const GatLane<G, VEC, CH, RC> &gl_, bool park,
+                                              int64_t e0, int64_t e1, FwdState<VEC, CH> &st) {
+    typedef typename GVec<VEC>::T V;
+    const int H = gl_.H, hh = gl_.hh;
+    const bool leader = park && gl_.leader;
+    const int32_t n = (int32_t)(e1 - e0);
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        int64_t c[U];
+        float ar[U];
+        V x[U][CH];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
-                c[k] = p.col[e0 + j];
-            }
+        for (int k = 0; k < U; ++k) {
+            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+            c[k] = p.col[e0 + j];
+        }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (!RC) ar[k] = aR[c[k] * H + hh];
+        for (int k = 0; k < U; ++k) {
+            if (!RC) ar[k] = d.aR[c[k] * H + hh];
 #pragma unroll
-                for (int ch = 0; ch < CH; ++ch)
-                    x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
-            }
-            if (RC) {
+            for (int ch = 0; ch < CH; ++ch)
+                x[k][ch] = *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]);
+        }
+        if (RC) {
 #pragma unroll
-                for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(w, x[k]), wb);
-            }
+            for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(gl_.w, x[k]), gl_.wb);
+        }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (j0 + k >= n) continue;
-                float z = __fadd_rn(al, ar[k]);
-                z = z > 0.0f ? z : __fmul_rn(z, slope);
-                if (MODE == GALA_SOFTMAX_REF) {
-                    const float pe = ref_exp(z);
-                    if (leader) alpha_out[(e0 + j0 + k) * H + hh] = pe;
-                    sum = __fadd_rn(sum, pe);
+        for (int k = 0; k < U; ++k) {
+            if (j0 + k >= n) continue;
+            float z = __fadd_rn(gl_.al, ar[k]);
+            z = z > 0.0f ? z : __fmul_rn(z, d.slope);
+            if (MODE == GALA_SOFTMAX_REF) {
+                const float pe = ref_exp(z);
+                if (leader) d.alpha_out[(e0 + j0 + k) * H + hh] = pe;
+                st.sum = __fadd_rn(st.sum, pe);
 #pragma unroll
-                    for (int ch = 0; ch < CH; ++ch) {
-                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
 #pragma unroll
-                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(pe, xv[i], acc[ch][i]);
-                    }
-                    continue;
+                    for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(pe, xv[i], st.acc[ch][i]);
                 }
-                if (leader) alpha_out[(e0 + j0 + k) * H + hh] = z;
-                if (z > m) {
-                    const float r = expf(m - z);
-                    sum = fmaf(sum, r, 1.0f);
+                continue;
+            }
+            if (leader) d.alpha_out[(e0 + j0 + k) * H + hh] = z;
+            if (z > st.m) {
+                const float r = expf(st.m - z);
+                st.sum = fmaf(st.sum, r, 1.0f);
 #pragma unroll
-                    for (int ch = 0; ch < CH; ++ch) {
-                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
 #pragma unroll
-                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(acc[ch][i], r, xv[i]);
-                    }
-                    m = z;
-                } else {
-                    const float pe = expf(z - m);
-                    sum = __fadd_rn(sum, pe);
+                    for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(st.acc[ch][i], r, xv[i]);
+                }
+                st.m = z;
+            } else {
+                const float pe = expf(z - st.m);
+                st.sum = __fadd_rn(st.sum, pe);
 #pragma unroll
-                    for (int ch = 0; ch < CH; ++ch) {
-                        const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
 #pragma unroll
-                        for (int i = 0; i < VEC; ++i) acc[ch][i] = fmaf(pe, xv[i], acc[ch][i]);
-                    }
+                    for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(pe, xv[i], st.acc[ch][i]);
                 }
             }
         }
     }
-    const float den = (MODE == GALA_SOFTMAX_REF) ? sum + (float)p.seg.n * 1e-12f : sum;
+}
+
+// Y[row] = acc * q with q = 1 / (sum [+ S * 1e-12 in REF mode]); returns q.
+template <int G, int VEC, int CH, bool RC, int MODE>
+__device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
+                                               int64_t row, int nseg, const FwdState<VEC, CH> &st) {
+    typedef typename GVec<VEC>::T V;
+    const float den = (MODE == GALA_SOFTMAX_REF) ? st.sum + (float)nseg * 1e-12f : st.sum;
     const float q = 1.0f / den;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
-        if (!ln.valid[ch]) continue;
+        if (!gl_.ln.valid[ch]) continue;
         V out;
         float *ov = reinterpret_cast<float *>(&out);
 #pragma unroll
         for (int i = 0; i < VEC; ++i)
-            ov[i] = (MODE != GALA_SOFTMAX_REF && sum == 0.0f) ? 0.0f : __fmul_rn(acc[ch][i], q);
-        *reinterpret_cast<V *>(Y + row * ldy + ln.off[ch]) = out;
+            ov[i] = (MODE != GALA_SOFTMAX_REF && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
+        *reinterpret_cast<V *>(d.Y + row * d.ldy + gl_.ln.off[ch]) = out;
     }
-    if (alpha_out) {
-        // alpha pass: lanes stride the row's contiguous (edge, head) values.  When H divides
-        // G every lane keeps one head (g % H) whose (m, q) live in lane (h*D)/VEC of the group.
-        const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
-        if (park) {
-            const int h = gl % H;
-            const int src = gbase + (h * D) / VEC;
-            const float mh = __shfl(m, src, 64);
-            const float qh = __shfl(q, src, 64);
-            // the parked values were stored by other lanes of this wave
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            constexpr int K = kTileK;
-            for (int s = 0; s < p.seg.n; ++s) {
-                int64_t e0, e1;
-                row_range(p, s, row, e0, e1);
-                const int64_t n = (e1 - e0) * H;
-                float *ar = alpha_out + e0 * H;
-                for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-                    float v[K];
-                    load_tile<G, K>(ar, n, t0, gl, 0.0f, v);
+    return q;
+}
+
+// alpha of the parked (edge, head) values [t0, t1) of one row: lane g handles head g % H
+// (H | G) with that head's (m, q)
+template <int G, int MODE>
+__device__ __forceinline__ void gat_alpha_rescale(float *ar, int64_t n, int gl, float mh, float qh) {
+    constexpr int K = kTileK;
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float v[K];
+        load_tile<G, K>(ar, n, t0, gl, 0.0f, v);
 #pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        const int64_t t = t0 + gl + (int64_t)k * G;
-                        const float pe = (MODE == GALA_SOFTMAX_REF) ? v[k] : expf(v[k] - mh);
-                        if (t < n) ar[t] = __fmul_rn(pe, qh);
-                    }
-                }
-            }
-        } else {
-            for (int s = 0; s < p.seg.n; ++s) {
-                int64_t e0, e1;
-                row_range(p, s, row, e0, e1);
-                for (int hd = 0; hd < H; ++hd) {
-                    const int src = gbase + (hd * D) / VEC;
-                    const float mh = __shfl(m, src, 64);
-                    const float qh = __shfl(q, src, 64);
-                    const float alh = aL[row * H + hd];
-                    for (int64_t e = e0 + gl; e < e1; e += G) {
-                        float z = __fadd_rn(alh, aR[(int64_t)p.col[e] * H + hd]);
-                        z = z > 0.0f ? z : __fmul_rn(z, slope);
-                        const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
-                        alpha_out[e * H + hd] = __fmul_rn(pe, qh);
-                    }
-                }
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            const float pe = (MODE == GALA_SOFTMAX_REF) ? v[k] : expf(v[k] - mh);
+            if (t < n) ar[t] = __fmul_rn(pe, qh);
+        }
+    }
+}
+
+// One pass per row: logits, LeakyReLU, softmax (REF exp-clamp / FIXED online max), the
+// alpha-weighted aggregation, then 1/sum; alpha (if requested) in a parked-value pass.
+template <int G, int VEC, int U, int MODE, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int32_t split_threshold) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
+        return;  // hub row: k_gat_fwd_chunk / _fixup / k_gat_alpha_chunk
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    const int H = gl_.H, D = gl_.D;
+    // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
+    // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
+    // place: a contiguous re-read of the row instead of a second col -> aR gather.
+    const bool park = d.alpha_out != nullptr && (G % H) == 0;
+    FwdState<VEC, CH> st;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, park, e0, e1, st);
+    }
+    const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, p.seg.n, st);
+    if (!d.alpha_out) return;
+    const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
+    if (park) {
+        const int h = gl % H;
+        const int src = gbase + (h * D) / VEC;
+        const float mh = __shfl(st.m, src, 64);
+        const float qh = __shfl(q, src, 64);
+        // the parked values were stored by other lanes of this wave
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            gat_alpha_rescale<G, MODE>(d.alpha_out + e0 * H, (e1 - e0) * H, gl, mh, qh);
+        }
+        return;
+    }
+    // heads that do not divide G: per head, lanes stride the row's edges (aR re-read)
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        for (int hd = 0; hd < H; ++hd) {
+            const int src = gbase + (hd * D) / VEC;
+            const float mh = __shfl(st.m, src, 64);
+            const float qh = __shfl(q, src, 64);
+            const float alh = d.aL[row * H + hd];
+            for (int64_t e = e0 + gl; e < e1; e += G) {
+                float z = __fadd_rn(alh, d.aR[(int64_t)p.col[e] * H + hd]);
+                z = z > 0.0f ? z : __fmul_rn(z, d.slope);
+                const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
+                d.alpha_out[e * H + hd] = __fmul_rn(pe, qh);
             }
         }
     }
+}
+
+// chunk c of a hub row -> its row group (n_seg == 1: plain CSR offsets)
+#define GALA_CHUNK_PROLOGUE(G)                                                                  \
+    const int lane = threadIdx.x & (kWave - 1);                                                 \
+    const int gl = lane & ((G)-1);                                                              \
+    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / (G)) \
+                      + lane / (G);                                                             \
+    if (c >= sp.n_chunks) return;                                                               \
+    const int32_t ri = sp.chunk_row[c];                                                         \
+    const int64_t row = sp.rows[ri];                                                            \
+    const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];                                   \
+    const int64_t e0 = r0 + (c - sp.row_chunk0[ri]) * (int64_t)sp.chunk;                       \
+    const int64_t e1 = (e0 + sp.chunk < r1) ? e0 + sp.chunk : r1;
+
+// hub rows, forward: chunk partial state -> ws[c] = {acc[F], m[H], sum[H]}
+template <int G, int VEC, int U, int MODE, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    FwdState<VEC, CH> st;
+    gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, d.alpha_out != nullptr, e0, e1, st);
+    float *w = sp.ws + c * sp.ws_cols;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+        if (gl_.ln.valid[ch])
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) w[gl_.ln.off[ch] + i] = st.acc[ch][i];
+    if (gl_.leader) {
+        w[d.F + gl_.hh] = st.m;
+        w[d.F + gl_.H + gl_.hh] = st.sum;
+    }
+}
+
+// hub rows, forward: combine the chunk partials in chunk order, store Y; (m, q) of every
+// head go to the row's first chunk slot for k_gat_alpha_chunk
+template <int G, int VEC, int MODE, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d, GatSplit sp) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t ri = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / G) + lane / G;
+    if (ri >= sp.n_rows_split) return;
+    const int64_t row = sp.rows[ri];
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    const int F = d.F, H = gl_.H, hh = gl_.hh;
+    FwdState<VEC, CH> st;
+    const int64_t c0 = sp.row_chunk0[ri], c1 = sp.row_chunk0[ri + 1];
+    for (int64_t cc = c0; cc < c1; ++cc) {
+        const float *w = sp.ws + cc * sp.ws_cols;
+        const float mc = w[F + hh], sc = w[F + H + hh];
+        float a = 1.0f, b = 1.0f;
+        if (MODE != GALA_SOFTMAX_REF) {
+            if (mc == -INFINITY) continue;  // no edges in this chunk's partial
+            const float mn = fmaxf(st.m, mc);
+            a = (st.m == -INFINITY) ? 0.0f : expf(st.m - mn);
+            b = expf(mc - mn);
+            st.m = mn;
+            st.sum = fmaf(st.sum, a, __fmul_rn(sc, b));
+        } else {
+            st.sum = __fadd_rn(st.sum, sc);
+        }
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+                const float v = gl_.ln.valid[ch] ? w[gl_.ln.off[ch] + i] : 0.0f;
+                st.acc[ch][i] = (MODE == GALA_SOFTMAX_REF) ? __fadd_rn(st.acc[ch][i], v)
+                                                           : fmaf(st.acc[ch][i], a, __fmul_rn(v, b));
+            }
+    }
+    const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, 1, st);
+    if (gl_.leader && d.alpha_out) {
+        float *w0 = sp.ws + c0 * sp.ws_cols;
+        w0[F + hh] = st.m;
+        w0[F + H + hh] = q;
+    }
+}
+
+// hub rows, forward: alpha of one chunk's parked values with its row's (m, q)
+template <int G, int VEC, int MODE>
+__global__ __launch_bounds__(kBlock) void k_gat_alpha_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const int H = p.heads;
+    const int h = gl % H;
+    const float *w0 = sp.ws + (int64_t)sp.row_chunk0[ri] * sp.ws_cols;
+    gat_alpha_rescale<G, MODE>(d.alpha_out + e0 * H, (e1 - e0) * H, gl, w0[d.F + h], w0[d.F + H + h]);
 }
 
 // ---- fused GAT backward -------------------------------------------------------------
@@ -781,136 +933,225 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, const float *a
 // head-wise dot reductions; every lane of a head then holds d_alpha and accumulates the
 // head's sum(sds) (and, in REF mode, sum(m*sds) and sum(m*alpha)).  FIXED mode parks sds
 // in d_logit (head leader lane) and a second, contiguous (edge, head) pass forms dz.
-template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
-__global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, const float *aL, const float *aR,
-                                                    const float *X, int64_t ldx, const float *dY,
-                                                    int64_t lddy, int32_t F, float slope,
-                                                    const float *alpha, float *d_logit,
-                                                    float *d_aL, const float *wR, const float *bR) {
-    typedef typename GVec<VEC>::T V;
-    GALA_ROW_PROLOGUE(G);
-    if (!row_ok) return;
-    const int H = p.heads;  // CH > 1 only with H == 1
-    const int D = F / H;
-    const Lanes<G, VEC, CH> ln(gl, F);
-    const bool cv = ln.valid[0];
-    const int64_t fo = ln.off[0];
-    const int hh = (int)(fo / D);
-    const bool leader = cv && (fo % D) == 0;
-    const float al = aL[row * H + hh];
-    float dy[CH][VEC];
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const V t = *reinterpret_cast<const V *>(dY + row * lddy + ln.off[ch]);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) dy[ch][i] = ln.valid[ch] ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
-    }
-    float w[CH][VEC];
-    float wb = 0.0f;
-    if (RC) {  // REF mode, one head (see k_gat_fwd)
-        load_attn<G, VEC, CH>(ln, wR, w);
-        wb = bR ? bR[0] : 0.0f;
-    }
-    const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
+struct BwdState {
     float acc = 0.0f, s_msds = 0.0f, s_ma = 0.0f;
-    for (int s = 0; s < p.seg.n; ++s) {
-        int64_t e0, e1;
-        row_range(p, s, row, e0, e1);
-        const int32_t n = (int32_t)(e1 - e0);
-        for (int32_t j0 = 0; j0 < n; j0 += U) {
-            int64_t c[U];
-            float ar[U], a[U], part[U];
-            V x[U][CH];
+};
+
+template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
+__device__ __forceinline__ void gat_bwd_range(const EdgeParams &p, const GatDev &d,
+                                              const GatLane<G, VEC, CH, RC> &gl_,
+                                              const float (&dy)[CH][VEC], int64_t e0, int64_t e1,
+                                              BwdState &st) {
+    typedef typename GVec<VEC>::T V;
+    const int H = gl_.H, hh = gl_.hh;
+    const int32_t n = (int32_t)(e1 - e0);
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        int64_t c[U];
+        float ar[U], a[U], part[U];
+        V x[U][CH];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
-                c[k] = p.col[e0 + j];
-                a[k] = alpha[(e0 + j) * H + hh];
+        for (int k = 0; k < U; ++k) {
+            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+            c[k] = p.col[e0 + j];
+            a[k] = d.alpha[(e0 + j) * H + hh];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (!RC) ar[k] = d.aR[c[k] * H + hh];
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch)
+                x[k][ch] = *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]);
+        }
+        if (RC) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(gl_.w, x[k]), gl_.wb);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            float dd = 0.0f;
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) {
+                const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) dd = fmaf(dy[ch][i], xv[i], dd);
             }
+            part[k] = dd;
+        }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (!RC) ar[k] = aR[c[k] * H + hh];
+        for (int k = 0; k < U; ++k) part[k] = group_sum<HW>(part[k]);
 #pragma unroll
-                for (int ch = 0; ch < CH; ++ch)
-                    x[k][ch] = *reinterpret_cast<const V *>(X + c[k] * ldx + ln.off[ch]);
-            }
-            if (RC) {
-#pragma unroll
-                for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(w, x[k]), wb);
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                float d = 0.0f;
-#pragma unroll
-                for (int ch = 0; ch < CH; ++ch) {
-                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
-#pragma unroll
-                    for (int i = 0; i < VEC; ++i) d = fmaf(dy[ch][i], xv[i], d);
-                }
-                part[k] = d;
-            }
-#pragma unroll
-            for (int k = 0; k < U; ++k) part[k] = group_sum<HW>(part[k]);
-#pragma unroll
-            for (int k = 0; k < U; ++k) {
-                if (j0 + k >= n) continue;
-                const float sds = __fmul_rn(a[k], part[k]);
-                acc += sds;
-                if (MODE == GALA_SOFTMAX_REF) {
-                    const bool pos = __fadd_rn(al, ar[k]) > 0.0f;
-                    s_msds += pos ? sds : __fmul_rn(sds, slope);
-                    s_ma += pos ? a[k] : __fmul_rn(a[k], slope);
-                } else if (leader) {
-                    d_logit[(e0 + j0 + k) * H + hh] = sds;
-                }
+        for (int k = 0; k < U; ++k) {
+            if (j0 + k >= n) continue;
+            const float sds = __fmul_rn(a[k], part[k]);
+            st.acc += sds;
+            if (MODE == GALA_SOFTMAX_REF) {
+                const bool pos = __fadd_rn(gl_.al, ar[k]) > 0.0f;
+                st.s_msds += pos ? sds : __fmul_rn(sds, d.slope);
+                st.s_ma += pos ? a[k] : __fmul_rn(a[k], d.slope);
+            } else if (gl_.leader) {
+                d.d_logit[(e0 + j0 + k) * H + hh] = sds;
             }
         }
     }
-    acc += (float)p.seg.n * eps;  // K7 on sds (common.h:793-794)
+}
+
+template <int G, int VEC, int CH, bool RC>
+__device__ __forceinline__ void load_dy(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_, int64_t row,
+                                        float (&dy)[CH][VEC]) {
+    typedef typename GVec<VEC>::T V;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const V t = *reinterpret_cast<const V *>(d.dY + row * d.lddy + gl_.ln.off[ch]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.valid[ch] ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+    }
+}
+
+// FIXED second pass over the parked sds of (edge, head) values [0, n) of one row slice:
+// dz = LeakyReLU'(z) * (sds - alpha * acc_h); returns the lane's partial sum of dz
+template <int G>
+__device__ __forceinline__ float gat_bwd_dz(const EdgeParams &p, const GatDev &d, int64_t row,
+                                            int64_t e0, int64_t n, int gl, int h, float acch) {
+    constexpr int K = kTileK;
+    const int H = p.heads;
+    const float alh = d.aL[row * H + h];
+    float *dl = d.d_logit + e0 * H;
+    const float *ap = d.alpha + e0 * H;
+    float rs = 0.0f;
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float sv[K], av[K], rv[K];
+        int32_t cc[K];
+        load_tile<G, K>(dl, n, t0, gl, 0.0f, sv);
+        load_tile<G, K>(ap, n, t0, gl, 0.0f, av);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            cc[k] = p.col[e0 + (t < n ? t : 0) / H];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) rv[k] = d.aR[(int64_t)cc[k] * H + h];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            if (t >= n) continue;
+            const float ds = __fsub_rn(sv[k], __fmul_rn(av[k], acch));
+            const float dz = __fadd_rn(alh, rv[k]) > 0.0f ? ds : __fmul_rn(ds, d.slope);
+            dl[t] = dz;
+            rs += dz;
+        }
+    }
+    return rs;
+}
+
+template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, GatDev d, int32_t split_threshold) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
+        return;  // hub row: k_gat_bwd_chunk / _fixup (/ _chunk2 / _fixup2)
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    const int H = gl_.H, D = gl_.D;
+    float dy[CH][VEC];
+    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+    const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
+    BwdState st;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        gat_bwd_range<G, VEC, U, HW, MODE, CH, RC>(p, d, gl_, dy, e0, e1, st);
+    }
+    const float acc = st.acc + (float)p.seg.n * eps;  // K7 on sds (common.h:793-794)
     if (MODE == GALA_SOFTMAX_REF) {
         // sum_row m*(sds - alpha*acc), then K7's 1e-12 per segment (common.h:662-667)
-        if (leader) d_aL[row * H + hh] = (s_msds - acc * s_ma) + (float)p.seg.n * eps;
+        if (gl_.leader) d.d_aL[row * H + gl_.hh] = (st.s_msds - acc * st.s_ma) + (float)p.seg.n * eps;
         return;
     }
     // FIXED: dz per (edge, head) from the parked sds; lane g keeps head g % H (H | G)
     const int gbase = lane & ~(G - 1);
     const int h = gl % H;
     const float acch = __shfl(acc, gbase + (h * D) / VEC, 64);
-    const float alh = aL[row * H + h];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // parked by other lanes
-    constexpr int K = kTileK;
     float rs = 0.0f;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        const int64_t n = (e1 - e0) * H;
-        float *dl = d_logit + e0 * H;
-        const float *ap = alpha + e0 * H;
-        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-            float sv[K], av[K], rv[K];
-            int32_t cc[K];
-            load_tile<G, K>(dl, n, t0, gl, 0.0f, sv);
-            load_tile<G, K>(ap, n, t0, gl, 0.0f, av);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                cc[k] = p.col[e0 + (t < n ? t : 0) / H];
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) rv[k] = aR[(int64_t)cc[k] * H + h];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                if (t >= n) continue;
-                const float ds = __fsub_rn(sv[k], __fmul_rn(av[k], acch));
-                const float dz = __fadd_rn(alh, rv[k]) > 0.0f ? ds : __fmul_rn(ds, slope);
-                dl[t] = dz;
-                rs += dz;
-            }
-        }
+        rs += gat_bwd_dz<G>(p, d, row, e0, (e1 - e0) * H, gl, h, acch);
     }
     for (int o = G / 2; o >= H; o >>= 1) rs += __shfl_xor(rs, o, 64);  // lanes of head h
-    if (gl < H) d_aL[row * H + gl] = rs;
+    if (gl < H) d.d_aL[row * H + gl] = rs;
+}
+
+// hub rows, backward pass 1: chunk partials -> ws[c] = {acc[H], s_msds[H], s_ma[H]}
+// (REF) or {acc[H]} with sds parked in d_logit (FIXED)
+template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    float dy[CH][VEC];
+    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+    BwdState st;
+    gat_bwd_range<G, VEC, U, HW, MODE, CH, RC>(p, d, gl_, dy, e0, e1, st);
+    if (!gl_.leader) return;
+    float *w = sp.ws + c * sp.ws_cols;
+    const int H = gl_.H, hh = gl_.hh;
+    w[hh] = st.acc;
+    if (MODE == GALA_SOFTMAX_REF) {
+        w[H + hh] = st.s_msds;
+        w[2 * H + hh] = st.s_ma;
+    }
+}
+
+// hub rows, backward: sum the chunk partials in chunk order.  REF: d_aL.  FIXED: the row's
+// acc per head -> ws[c0][H + h] for k_gat_bwd_chunk2.  One thread per (split row, head).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup(EdgeParams p, GatDev d, GatSplit sp) {
+    const int H = p.heads;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sp.n_rows_split * H) return;
+    const int64_t ri = t / H;
+    const int h = (int)(t % H);
+    const int64_t row = sp.rows[ri];
+    const int64_t c0 = sp.row_chunk0[ri], c1 = sp.row_chunk0[ri + 1];
+    float acc = 0.0f, s1 = 0.0f, s2 = 0.0f;
+    for (int64_t cc = c0; cc < c1; ++cc) {
+        const float *w = sp.ws + cc * sp.ws_cols;
+        acc = __fadd_rn(acc, w[h]);
+        if (MODE == GALA_SOFTMAX_REF) {
+            s1 = __fadd_rn(s1, w[H + h]);
+            s2 = __fadd_rn(s2, w[2 * H + h]);
+        }
+    }
+    if (MODE == GALA_SOFTMAX_REF) {
+        acc = __fadd_rn(acc, 1e-12f);
+        d.d_aL[row * H + h] = (s1 - acc * s2) + 1e-12f;
+    } else {
+        sp.ws[c0 * sp.ws_cols + H + h] = acc;
+    }
+}
+
+// hub rows, FIXED backward pass 2: dz of one chunk; partial row sums -> ws[c][2H + h]
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk2(EdgeParams p, GatDev d, GatSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const int H = p.heads;
+    const int h = gl % H;
+    const float acch = sp.ws[(int64_t)sp.row_chunk0[ri] * sp.ws_cols + H + h];
+    float rs = gat_bwd_dz<G>(p, d, row, e0, (e1 - e0) * H, gl, h, acch);
+    for (int o = G / 2; o >= H; o >>= 1) rs += __shfl_xor(rs, o, 64);
+    if (gl < H) sp.ws[c * sp.ws_cols + 2 * H + gl] = rs;
+}
+
+// hub rows, FIXED backward: d_aL = the chunks' dz sums in chunk order
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup2(EdgeParams p, GatDev d, GatSplit sp) {
+    const int H = p.heads;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sp.n_rows_split * H) return;
+    const int64_t ri = t / H;
+    const int h = (int)(t % H);
+    float rs = 0.0f;
+    for (int64_t cc = sp.row_chunk0[ri]; cc < sp.row_chunk0[ri + 1]; ++cc)
+        rs = __fadd_rn(rs, sp.ws[cc * sp.ws_cols + 2 * H + h]);
+    d.d_aL[(int64_t)sp.rows[ri] * H + h] = rs;
 }
 
 __global__ __launch_bounds__(kBlock) void k_permute(const int32_t *perm, const float *src,
@@ -1249,35 +1490,40 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     return launch_status();
 }
 
-// Host-side argument bundle of the fused GAT kernels (forward and backward).
+// Host-side launch description of the fused GAT kernels (forward and backward).
 struct GatArgs {
     EdgeParams p;
+    GatDev d;
+    GatSplit sp;
+    bool split;
     int mode;
-    const float *aL, *aR, *wR, *bR;  // aR == nullptr: recompute from X with wR / bR (RC)
-    const float *X;
-    int64_t ldx;
-    int32_t F;
-    float slope;
-    float *Y;                        // forward
-    int64_t ldy;
-    float *alpha_out;
-    const float *dY;                 // backward
-    int64_t lddy;
-    const float *alpha;
-    float *d_logit, *d_aL;
     hipStream_t hs;
 };
 
+static unsigned blocks_for_groups(int64_t n, int G) {
+    const int64_t per_block = (int64_t)(kBlock / kWave) * (kWave / G);
+    return (unsigned)((n + per_block - 1) / per_block);
+}
+
+template <int G, int VEC, int CH, bool RC, int MODE>
+static void launch_gat_mode(const GatArgs &a) {
+    constexpr int U = 8;
+    hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, MODE, CH, RC>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
+                       0, a.hs, a.p, a.d, a.split ? a.sp.threshold : 0);
+    if (!a.split) return;
+    hipLaunchKernelGGL((k_gat_fwd_chunk<G, VEC, U, MODE, CH, RC>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+    hipLaunchKernelGGL((k_gat_fwd_fixup<G, VEC, MODE, CH, RC>), dim3(blocks_for_groups(a.sp.n_rows_split, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+    if (a.d.alpha_out)
+        hipLaunchKernelGGL((k_gat_alpha_chunk<G, VEC, MODE>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+                           dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+}
+
 template <int G, int VEC, int CH, bool RC>
 static void launch_gat(const GatArgs &a) {
-    const dim3 grid(blocks_for(a.p.n_rows, G));
-    constexpr int U = 8;
-    if (a.mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_REF, CH, RC>), grid, dim3(kBlock), 0, a.hs,
-                           a.p, a.aL, a.aR, a.X, a.ldx, a.F, a.slope, a.Y, a.ldy, a.alpha_out, a.wR, a.bR);
-    else
-        hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, GALA_SOFTMAX_FIXED, CH, RC>), grid, dim3(kBlock), 0, a.hs,
-                           a.p, a.aL, a.aR, a.X, a.ldx, a.F, a.slope, a.Y, a.ldy, a.alpha_out, a.wR, a.bR);
+    if (a.mode == GALA_SOFTMAX_REF) launch_gat_mode<G, VEC, CH, RC, GALA_SOFTMAX_REF>(a);
+    else launch_gat_mode<G, VEC, CH, RC, GALA_SOFTMAX_FIXED>(a);
 }
 
 template <int VEC, bool RC>
@@ -1294,6 +1540,26 @@ static int gat_vec(const GatArgs &a, int L, int ch) {
     else if (L <= 64) launch_gat<64, VEC, 1, RC>(a);
     else return GALA_ERR_UNSUPPORTED;
     return GALA_OK;
+}
+
+// the hub-row plan of A, when it applies and its workspace holds `need` floats per chunk
+// (otherwise hub rows run in one pass, like every other row)
+static bool gat_split(const gala_csr_t *A, int64_t need, GatSplit *sp) {
+    const gala_split_plan_t *plan = A->split;
+    if (!plan || plan->n_chunks <= 0 || A->n_seg != 1 || !plan->rows || !plan->row_chunk0 ||
+        !plan->chunk_row || !plan->workspace || plan->ws_cols < need || plan->chunk < 1 ||
+        plan->threshold < 1)
+        return false;
+    sp->rows = plan->rows;
+    sp->row_chunk0 = plan->row_chunk0;
+    sp->chunk_row = plan->chunk_row;
+    sp->ws = plan->workspace;
+    sp->ws_cols = plan->ws_cols;
+    sp->n_chunks = plan->n_chunks;
+    sp->n_rows_split = plan->n_rows_split;
+    sp->chunk = plan->chunk;
+    sp->threshold = plan->threshold;
+    return true;
 }
 
 static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
@@ -1313,10 +1579,17 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
                        ((uintptr_t)Y % (4 * vec))))
         vec >>= 1;
     const int L = (F + vec - 1) / vec;
-    a.mode = mode;
-    a.aL = aL, a.aR = aR, a.wR = wR, a.bR = bR, a.X = X, a.ldx = ldx, a.F = F, a.slope = slope;
-    a.Y = Y, a.ldy = ldy, a.alpha_out = alpha_out, a.hs = (hipStream_t)stream;
     const int ch = narrow_chunks(heads, vec, L);
+    int G = 16;
+    if (ch == 1) {
+        G = 1;
+        while (G < L) G <<= 1;
+    }
+    a.mode = mode;
+    a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
+    a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out;
+    a.hs = (hipStream_t)stream;
+    a.split = (!alpha_out || G % heads == 0) && gat_split(A, (int64_t)F + 2 * heads, &a.sp);
     const bool rc = aR == nullptr;
     int r;
     if (vec == 4) r = rc ? gat_vec<4, true>(a, L, ch) : gat_vec<4, false>(a, L, ch);
@@ -1344,19 +1617,28 @@ extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const
                         stream);
 }
 
-template <int G, int VEC, int HW, int CH, bool RC>
-static void launch_gat_bwd(const GatArgs &a) {
-    const dim3 grid(blocks_for(a.p.n_rows, G));
+template <int G, int VEC, int HW, int CH, bool RC, int MODE>
+static void launch_gat_bwd_mode(const GatArgs &a) {
     constexpr int U = 8;
     constexpr int HWc = (HW < G) ? HW : G;
-    if (a.mode == GALA_SOFTMAX_REF)
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_REF, CH, RC>), grid, dim3(kBlock), 0, a.hs,
-                           a.p, a.aL, a.aR, a.X, a.ldx, a.dY, a.lddy, a.F, a.slope, a.alpha, a.d_logit,
-                           a.d_aL, a.wR, a.bR);
-    else if (!RC)  // FIXED recomputes the LeakyReLU mask from aR in its second pass
-        hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, GALA_SOFTMAX_FIXED, CH, false>), grid, dim3(kBlock), 0,
-                           a.hs, a.p, a.aL, a.aR, a.X, a.ldx, a.dY, a.lddy, a.F, a.slope, a.alpha,
-                           a.d_logit, a.d_aL, a.wR, a.bR);
+    hipLaunchKernelGGL((k_gat_bwd<G, VEC, U, HWc, MODE, CH, RC>), dim3(blocks_for(a.p.n_rows, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.split ? a.sp.threshold : 0);
+    if (!a.split) return;
+    const unsigned tb = (unsigned)((a.sp.n_rows_split * a.p.heads + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((k_gat_bwd_chunk<G, VEC, U, HWc, MODE, CH, RC>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+    hipLaunchKernelGGL((k_gat_bwd_fixup<MODE>), dim3(tb), dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+    if (MODE == GALA_SOFTMAX_REF) return;
+    hipLaunchKernelGGL((k_gat_bwd_chunk2<G>), dim3(blocks_for_groups(a.sp.n_chunks, G)), dim3(kBlock), 0,
+                       a.hs, a.p, a.d, a.sp);
+    hipLaunchKernelGGL(k_gat_bwd_fixup2, dim3(tb), dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+}
+
+template <int G, int VEC, int HW, int CH, bool RC>
+static void launch_gat_bwd(const GatArgs &a) {
+    if (a.mode == GALA_SOFTMAX_REF) launch_gat_bwd_mode<G, VEC, HW, CH, RC, GALA_SOFTMAX_REF>(a);
+    else if (!RC) launch_gat_bwd_mode<G, VEC, HW, CH, false, GALA_SOFTMAX_FIXED>(a);
+    // FIXED + RC is refused by gat_bwd_impl: its second pass needs aR
 }
 
 template <int G, int VEC, bool RC>
@@ -1414,11 +1696,13 @@ static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (heads > 1 && ((hw_l & (hw_l - 1)) || G % heads)) return GALA_ERR_UNSUPPORTED;
     if (mode == GALA_SOFTMAX_FIXED && G % heads) return GALA_ERR_UNSUPPORTED;
     const int hw = heads > 1 ? hw_l : G;
-    a.mode = mode;
-    a.aL = aL, a.aR = aR, a.wR = wR, a.bR = bR, a.X = X, a.ldx = ldx, a.F = F, a.slope = slope;
-    a.dY = dY, a.lddy = lddy, a.alpha = alpha, a.d_logit = d_logit, a.d_aL = d_aL;
-    a.hs = (hipStream_t)stream;
     const int ch = narrow_chunks(heads, vec, L);
+    a.mode = mode;
+    a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
+    a.d.slope = slope, a.d.dY = dY, a.d.lddy = lddy, a.d.alpha = alpha, a.d.d_logit = d_logit;
+    a.d.d_aL = d_aL;
+    a.hs = (hipStream_t)stream;
+    a.split = gat_split(A, 3 * (int64_t)heads, &a.sp);
     const bool rc = aR == nullptr;
     int r;
     if (vec == 4) r = rc ? gat_bwd_vec<4, true>(a, L, hw, ch) : gat_bwd_vec<4, false>(a, L, hw, ch);

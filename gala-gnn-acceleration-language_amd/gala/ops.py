@@ -201,7 +201,7 @@ def gat_fwd(g: DeviceGraph, aL, aR, X, heads=1, slope=0.2, mode=_abi.GALA_SOFTMA
     F = X.shape[1]
     Y = torch.empty((g.n_rows, F), device=X.device, dtype=torch.float32)
     alpha = torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32) if want_alpha else None
-    _abi.call("gala_gat_fwd_f32", g.csr(), _dp(aL), _dp(aR), _dp(X), X.stride(0), F, heads, slope,
+    _abi.call("gala_gat_fwd_f32", g.csr(F + 2 * heads), _dp(aL), _dp(aR), _dp(X), X.stride(0), F, heads, slope,
               mode, _dp(Y), Y.stride(0), _dp(alpha), _stream())
     return (Y, alpha) if want_alpha else Y
 
@@ -211,7 +211,7 @@ def gat_fwd_attn(g: DeviceGraph, aL, wR, bR, X, slope=0.2, mode=_abi.GALA_SOFTMA
     F = X.shape[1]
     Y = torch.empty((g.n_rows, F), device=X.device, dtype=torch.float32)
     alpha = torch.empty(g.nnz, device=X.device, dtype=torch.float32) if want_alpha else None
-    _abi.call("gala_gat_fwd_attn_f32", g.csr(), _dp(aL), _dp(wR), _dp(bR), _dp(X), X.stride(0), F, slope,
+    _abi.call("gala_gat_fwd_attn_f32", g.csr(F + 2), _dp(aL), _dp(wR), _dp(bR), _dp(X), X.stride(0), F, slope,
               mode, _dp(Y), Y.stride(0), _dp(alpha), _stream())
     return (Y, alpha) if want_alpha else Y
 
@@ -219,7 +219,7 @@ def gat_fwd_attn(g: DeviceGraph, aL, wR, bR, X, slope=0.2, mode=_abi.GALA_SOFTMA
 def gat_bwd_attn(g: DeviceGraph, aL, wR, bR, X, dY, alpha, slope=0.2):
     """gala_gat_bwd_attn_f32 (REF mode): d_aL (= d_aR)."""
     d_aL = torch.empty(g.n_rows, device=X.device, dtype=torch.float32)
-    _abi.call("gala_gat_bwd_attn_f32", g.csr(), _dp(aL), _dp(wR), _dp(bR), _dp(X), X.stride(0), _dp(dY),
+    _abi.call("gala_gat_bwd_attn_f32", g.csr(3), _dp(aL), _dp(wR), _dp(bR), _dp(X), X.stride(0), _dp(dY),
               dY.stride(0), X.shape[1], slope, _dp(alpha), _dp(d_aL), _stream())
     return d_aL
 
@@ -231,7 +231,7 @@ def gat_bwd(g: DeviceGraph, aL, aR, X, dY, alpha, heads=1, slope=0.2, mode=_abi.
     d_aL = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
     dz = (torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32)
           if (want_dz or mode == _abi.GALA_SOFTMAX_FIXED) else None)
-    _abi.call("gala_gat_bwd_f32", g.csr(), _dp(aL), _dp(aR), _dp(X), X.stride(0), _dp(dY),
+    _abi.call("gala_gat_bwd_f32", g.csr(3 * heads), _dp(aL), _dp(aR), _dp(X), X.stride(0), _dp(dY),
               dY.stride(0), F, heads, slope, mode, _dp(alpha), _dp(dz), _dp(d_aL), _stream())
     return d_aL, dz
 

@@ -120,6 +120,14 @@ CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torc
     return v;
 }
 
+// a graph view whose hub-row plan carries a workspace of at least `cols` floats per chunk
+void with_workspace(CsrView &cv, const torch::Tensor &offsets, int64_t cols) {
+    if (!cv.c.split) return;
+    SplitState *sp = find_split(offsets);
+    sp->ensure_workspace(cols);
+    cv.c.split = &sp->plan;
+}
+
 torch::TensorOptions fopts(const torch::Tensor &like) {
     return torch::TensorOptions().dtype(torch::kFloat).device(like.device());
 }
@@ -592,6 +600,7 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
     const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
     CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
     cf.c.n_cols = x.size(0);
+    with_workspace(cf, fw.off, 3 * heads);  // hub-row partials of the backward
     check_on(dY, fw.off, "grad");
     const bool fixed = mode == GALA_SOFTMAX_FIXED;
     TORCH_CHECK(!fixed || bw.perm.defined(),
@@ -686,6 +695,7 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         const int64_t nrows = cv.c.n_rows, F = x.size(1);
         const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
         cv.c.n_cols = x.size(0);
+        with_workspace(cv, s.off, F + 2 * heads);  // hub-row partials: acc[F], m[H], sum[H]
         auto Y = torch::empty({nrows, F}, fopts(x));
         auto alpha = torch::empty({s.cols.numel() * heads}, fopts(x));
         check_on(l, s.off, "attn_l");
@@ -738,6 +748,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         check_on(w, s.off, "attn_r weight");
         if (b.defined()) check_on(b, s.off, "attn_r bias");
         cv.c.n_cols = x.size(0);
+        with_workspace(cv, s.off, F + 2);
         auto Y = torch::empty({nrows, F}, fopts(x));
         auto alpha = torch::empty({s.cols.numel()}, fopts(x));
         check(be(s.off).gat_fwd_attn(&cv.c, l.data_ptr<float>(), w.data_ptr<float>(),

@@ -269,6 +269,43 @@ def test_gat_attention_recompute(graph, mode, F, tiled):
         np.testing.assert_allclose(host(daL), daL_ref, **TOL)
 
 
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4)])
+def test_gat_hub_rows_split(mode, F, heads):
+    """Hub rows cut into chunks (plan threshold 64, chunks of 32 edges): the fused GAT
+    forward / backward combine per-chunk partials (online-softmax merge, ordered sums)."""
+    g = powerlaw()
+    aL = features(g.n_rows, heads, seed=61)
+    aR = features(g.n_cols, heads, seed=62)
+    X = features(g.n_cols, F, seed=63)
+    dY = features(g.n_rows, F, seed=64)
+    og = to_oracle(g)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=mode)
+    dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=mode)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    assert dg.split_rows > 10
+    Y, al = ops.gat_fwd(dg, dev(aL), dev(aR), dev(X), heads=heads, slope=0.2, mode=mode, want_alpha=True)
+    np.testing.assert_allclose(host(al), al_ref, **TOL)
+    np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+    daL, dz = ops.gat_bwd(dg, dev(aL), dev(aR), dev(X), dev(dY), dev(al_ref), heads=heads, slope=0.2, mode=mode)
+    np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+    if mode == _abi.GALA_SOFTMAX_FIXED:
+        np.testing.assert_allclose(host(dz), dz_ref, **TOL)
+    if heads == 1:  # attention recompute on the same split plan
+        wR = features(1, F, seed=65).ravel() * 0.5
+        bR = np.array([0.1], np.float32)
+        aR2 = (X.astype(np.float64) @ wR.astype(np.float64) + 0.1).astype(np.float32)
+        Y2_ref, al2_ref = orc.gat_fwd(og, aL, aR2, X, heads=1, slope=0.2, mode=mode)
+        Y2, al2 = ops.gat_fwd_attn(dg, dev(aL), dev(wR), dev(bR), dev(X), slope=0.2, mode=mode, want_alpha=True)
+        np.testing.assert_allclose(host(al2), al2_ref, **TOL)
+        np.testing.assert_allclose(host(Y2), Y2_ref, **TOL)
+        if mode == _abi.GALA_SOFTMAX_REF:
+            _, daL2_ref = orc.gat_bwd(og, aL, aR2, X, dY, al2_ref, heads=1, slope=0.2, mode=mode)
+            daL2 = ops.gat_bwd_attn(dg, dev(aL), dev(wR), dev(bR), dev(X), dev(dY), dev(al2_ref), slope=0.2)
+            np.testing.assert_allclose(host(daL2), daL2_ref, **TOL)
+
+
 def test_edge_permute():
     g = powerlaw()
     t, perm = layout.transpose(g)
