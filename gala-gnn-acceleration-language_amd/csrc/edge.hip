@@ -41,6 +41,29 @@ __device__ __forceinline__ void row_range(const EdgeParams &p, int s, int64_t ro
                             * (kWave / (G)) + lane / (G);                             \
     const bool row_ok = row < p.n_rows;
 
+// Device view of the hub-row plan: rows longer than `threshold` are cut into chunks of
+// `chunk` edges that separate row groups run in parallel; their per-chunk partial state
+// goes to ws (ws_cols floats per chunk) and fix-up kernels combine it in chunk order.
+struct HubSplit {
+    const int32_t *rows, *row_chunk0, *chunk_row;
+    float *ws;
+    int64_t ws_cols, n_chunks, n_rows_split;
+    int32_t chunk, threshold;
+};
+
+// chunk c of a hub row -> its row group (n_seg == 1: plain CSR offsets)
+#define GALA_CHUNK_PROLOGUE(G)                                                                  \
+    const int lane = threadIdx.x & (kWave - 1);                                                 \
+    const int gl = lane & ((G)-1);                                                              \
+    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / (G)) \
+                      + lane / (G);                                                             \
+    if (c >= sp.n_chunks) return;                                                               \
+    const int32_t ri = sp.chunk_row[c];                                                         \
+    const int64_t row = sp.rows[ri];                                                            \
+    const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];                                   \
+    const int64_t e0 = r0 + (c - sp.row_chunk0[ri]) * (int64_t)sp.chunk;                       \
+    const int64_t e1 = (e0 + sp.chunk < r1) ? e0 + sp.chunk : r1;
+
 // ---- row-segment edge ops over flattened (edge, head) elements ----------------------
 // With HP heads (a power of two dividing G) the row's HP*deg edge values are contiguous,
 // lane g always handles head g % HP, and per-head reductions run over the xor offsets
@@ -76,69 +99,101 @@ __device__ __forceinline__ void load_tile(const float *base, int64_t n, int64_t 
     }
 }
 
+// Hub rows (skewed graphs, A->split): the main kernel skips rows longer than the plan's
+// threshold; *_chunk kernels run their 512-edge chunks in separate row groups, and
+// *_fixup kernels (one thread per (hub row, head)) combine the chunk partials in chunk
+// order.  The partials live in the plan's workspace (2*HP floats per chunk).
+__device__ __forceinline__ bool hub_row(const EdgeParams &p, int32_t thr, int64_t row) {
+    return thr > 0 && p.rowptr[row + 1] - p.rowptr[row] > thr;
+}
+
+// out[e, h] = a[row, h] op b[col_e, h] for the edges [e0, e1) of `row`
 template <int G, int HP, int OP>
-__global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, const float *b,
-                                                  float slope, float *out) {
-    GALA_ROW_PROLOGUE(G);
-    if (!row_ok) return;
+__device__ __forceinline__ void sddvv_range(const EdgeParams &p, const float *a, const float *b,
+                                            float slope, float *out, int64_t row, int64_t e0,
+                                            int64_t e1, int gl) {
     constexpr int LH = __builtin_ctz(HP);
     constexpr int K = kTileK;
     const int h = gl & (HP - 1);
     const float av = a[row * HP + h];
-    for (int s = 0; s < p.seg.n; ++s) {
-        int64_t e0, e1;
-        row_range(p, s, row, e0, e1);
-        const int64_t n = (e1 - e0) << LH;
-        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-            int32_t c[K];
-            float bv[K];
+    const int64_t n = (e1 - e0) << LH;
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        int32_t c[K];
+        float bv[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                c[k] = p.col[e0 + ((t < n ? t : 0) >> LH)];
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            c[k] = p.col[e0 + ((t < n ? t : 0) >> LH)];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) bv[k] = b[((int64_t)c[k] << LH) + h];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            if (t >= n) continue;
+            float r;
+            if (OP == GALA_SDDVV_MUL) {
+                r = __fmul_rn(av, bv[k]);
+            } else {
+                r = __fadd_rn(av, bv[k]);
+                if (OP == GALA_SDDVV_ADD_LRELU) r = r > 0.0f ? r : __fmul_rn(r, slope);
             }
-#pragma unroll
-            for (int k = 0; k < K; ++k) bv[k] = b[((int64_t)c[k] << LH) + h];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                if (t >= n) continue;
-                float r;
-                if (OP == GALA_SDDVV_MUL) {
-                    r = __fmul_rn(av, bv[k]);
-                } else {
-                    r = __fadd_rn(av, bv[k]);
-                    if (OP == GALA_SDDVV_ADD_LRELU) r = r > 0.0f ? r : __fmul_rn(r, slope);
-                }
-                out[(e0 << LH) + t] = r;
-            }
+            out[(e0 << LH) + t] = r;
         }
     }
 }
 
-template <int G, int HP>
-__global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
-                                                    int accum, float *out) {
+template <int G, int HP, int OP>
+__global__ __launch_bounds__(kBlock) void k_sddvv(EdgeParams p, const float *a, const float *b,
+                                                  float slope, float *out, int32_t thr) {
     GALA_ROW_PROLOGUE(G);
+    if (!row_ok || hub_row(p, thr, row)) return;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        sddvv_range<G, HP, OP>(p, a, b, slope, out, row, e0, e1, gl);
+    }
+}
+
+template <int G, int HP, int OP>
+__global__ __launch_bounds__(kBlock) void k_sddvv_chunk(EdgeParams p, const float *a, const float *b,
+                                                        float slope, float *out, HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    sddvv_range<G, HP, OP>(p, a, b, slope, out, row, e0, e1, gl);
+}
+
+// the lane's partial sum of the (edge, head) values [e0*HP, e1*HP)
+template <int G, int HP>
+__device__ __forceinline__ float sum_range(const float *v, int64_t e0, int64_t e1, int gl) {
     constexpr int LH = __builtin_ctz(HP);
     constexpr int K = kTileK;
+    const int64_t n = (e1 - e0) << LH;
+    const float *vr = v + (e0 << LH);
     float part = 0.0f;
-    if (row_ok) {
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float x[K];
+        load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
+#pragma unroll
+        for (int k = 0; k < K; ++k) part += x[k];
+    }
+    return part;
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
+                                                    int accum, float *out, int32_t thr) {
+    GALA_ROW_PROLOGUE(G);
+    const bool mine = row_ok && !hub_row(p, thr, row);
+    float part = 0.0f;
+    if (mine) {
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
-            const int64_t n = (e1 - e0) << LH;
-            const float *vr = v + (e0 << LH);
-            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-                float x[K];
-                load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
-#pragma unroll
-                for (int k = 0; k < K; ++k) part += x[k];
-            }
+            part += sum_range<G, HP>(v, e0, e1, gl);
         }
     }
     part = head_sum<G, HP>(part);
-    if (row_ok && gl < HP) {
+    if (mine && gl < HP) {
         // reference: each segment's sum starts at 1e-12 (cuda.h:512,666)
         float r = part + (float)p.seg.n * eps;
         if (accum) r = out[row * HP + gl] + r;
@@ -146,28 +201,64 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
     }
 }
 
+// hub rows: per-chunk head sums of v -> ws[c][h]
 template <int G, int HP>
-__global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float *q, float *v) {
-    GALA_ROW_PROLOGUE(G);
-    if (!row_ok) return;
+__global__ __launch_bounds__(kBlock) void k_row_sum_chunk(EdgeParams p, const float *v, HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const float part = head_sum<G, HP>(sum_range<G, HP>(v, e0, e1, gl));
+    if (gl < HP) sp.ws[c * sp.ws_cols + gl] = part;
+}
+
+// hub rows: out[row, h] (+)= eps + the chunk sums in chunk order
+__global__ __launch_bounds__(kBlock) void k_row_sum_fixup(EdgeParams p, float eps, int accum,
+                                                          float *out, HubSplit sp) {
+    const int H = p.heads;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sp.n_rows_split * H) return;
+    const int64_t ri = t / H;
+    const int h = (int)(t % H);
+    float r = 0.0f;
+    for (int64_t cc = sp.row_chunk0[ri]; cc < sp.row_chunk0[ri + 1]; ++cc) r += sp.ws[cc * sp.ws_cols + h];
+    r = r + eps;
+    const int64_t o = (int64_t)sp.rows[ri] * H + h;
+    if (accum) r = out[o] + r;
+    out[o] = r;
+}
+
+template <int G, int HP>
+__device__ __forceinline__ void scale_range(float *v, float qv, int64_t e0, int64_t e1, int gl) {
     constexpr int LH = __builtin_ctz(HP);
     constexpr int K = kTileK;
+    const int64_t n = (e1 - e0) << LH;
+    float *vr = v + (e0 << LH);
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float x[K];
+        load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            if (t < n) vr[t] = __fmul_rn(x[k], qv);
+        }
+    }
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_row_scale(EdgeParams p, const float *q, float *v, int32_t thr) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok || hub_row(p, thr, row)) return;
     const float qv = q[row * HP + (gl & (HP - 1))];
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        const int64_t n = (e1 - e0) << LH;
-        float *vr = v + (e0 << LH);
-        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-            float x[K];
-            load_tile<G, K>(vr, n, t0, gl, 0.0f, x);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                if (t < n) vr[t] = __fmul_rn(x[k], qv);
-            }
-        }
+        scale_range<G, HP>(v, qv, e0, e1, gl);
     }
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_row_scale_chunk(EdgeParams p, const float *q, float *v,
+                                                            HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    scale_range<G, HP>(v, q[row * HP + (gl & (HP - 1))], e0, e1, gl);
 }
 
 __device__ __forceinline__ float ref_exp(float s) {
@@ -176,55 +267,91 @@ __device__ __forceinline__ float ref_exp(float s) {
     return p > 1e12f ? 1e12f : p;
 }
 
+// softmax statistics of the logits [e0*HP, e1*HP): REF sum of clamped exp terms, FIXED an
+// online (max, sum); x keeps the last tile
 template <int G, int HP, int MODE>
-__global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const float *logit,
-                                                        float *alpha) {
-    GALA_ROW_PROLOGUE(G);
+__device__ __forceinline__ void softmax_stats(const float *logit, int64_t e0, int64_t e1, int gl,
+                                              float &m, float &sum, float (&x)[kTileK]) {
     constexpr int LH = __builtin_ctz(HP);
     constexpr int K = kTileK;
-    float m = -INFINITY, sum = 0.0f;
-    float x[K];
-    bool in_regs = false;  // the whole row is in x[] (one segment, one tile)
-    if (row_ok) {
-        for (int s = 0; s < p.seg.n; ++s) {
-            int64_t e0, e1;
-            row_range(p, s, row, e0, e1);
-            const int64_t n = (e1 - e0) << LH;
-            in_regs = p.seg.n == 1 && n <= G * K;
-            const float *lr = logit + (e0 << LH);
-            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-                load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);  // exp(-inf) = 0: fill is inert
-                if (MODE == GALA_SOFTMAX_REF) {
+    const int64_t n = (e1 - e0) << LH;
+    const float *lr = logit + (e0 << LH);
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);  // exp(-inf) = 0: fill is inert
+        if (MODE == GALA_SOFTMAX_REF) {
 #pragma unroll
-                    for (int k = 0; k < K; ++k) sum += ref_exp(x[k]);
-                } else {
-                    float mt = x[0];
+            for (int k = 0; k < K; ++k) sum += ref_exp(x[k]);
+        } else {
+            float mt = x[0];
 #pragma unroll
-                    for (int k = 1; k < K; ++k) mt = fmaxf(mt, x[k]);
-                    if (mt > m) {  // online max / sum
-                        sum = (m == -INFINITY) ? 0.0f : sum * expf(m - mt);
-                        m = mt;
-                    }
-                    if (m != -INFINITY) {
+            for (int k = 1; k < K; ++k) mt = fmaxf(mt, x[k]);
+            if (mt > m) {  // online max / sum
+                sum = (m == -INFINITY) ? 0.0f : sum * expf(m - mt);
+                m = mt;
+            }
+            if (m != -INFINITY) {
 #pragma unroll
-                        for (int k = 0; k < K; ++k) sum += expf(x[k] - m);
-                    }
-                }
+                for (int k = 0; k < K; ++k) sum += expf(x[k] - m);
             }
         }
     }
-    float q;
+}
+
+// the lanes' (m, sum) -> the head's (m, sum) (all lanes of the head get it)
+template <int G, int HP, int MODE>
+__device__ __forceinline__ void softmax_reduce(float &m, float &sum) {
     if (MODE == GALA_SOFTMAX_REF) {
         sum = head_sum<G, HP>(sum);
-        q = 1.0f / (sum + (float)p.seg.n * 1e-12f);  // torch::reciprocal(row_sum)
     } else {
         const float gm = head_max<G, HP>(m);
         sum = (m == -INFINITY) ? 0.0f : sum * expf(m - gm);
         sum = head_sum<G, HP>(sum);
         m = gm;
-        q = 1.0f / sum;
     }
-    if (!row_ok) return;
+}
+
+template <int G, int HP, int MODE>
+__device__ __forceinline__ void softmax_write(const float *logit, float *alpha, int64_t e0, int64_t e1,
+                                              int gl, float m, float q) {
+    constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
+    const int64_t n = (e1 - e0) << LH;
+    const float *lr = logit + (e0 << LH);
+    float *ar = alpha + (e0 << LH);
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float x[K];
+        load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x[k]) : expf(x[k] - m);
+            if (t < n) ar[t] = __fmul_rn(pe, q);
+        }
+    }
+}
+
+template <int G, int HP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const float *logit,
+                                                        float *alpha, int32_t thr) {
+    GALA_ROW_PROLOGUE(G);
+    constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
+    const bool mine = row_ok && !hub_row(p, thr, row);
+    float m = -INFINITY, sum = 0.0f;
+    float x[K];
+    bool in_regs = false;  // the whole row is in x[] (one segment, one tile)
+    if (mine) {
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            in_regs = p.seg.n == 1 && ((e1 - e0) << LH) <= G * K;
+            softmax_stats<G, HP, MODE>(logit, e0, e1, gl, m, sum, x);
+        }
+    }
+    softmax_reduce<G, HP, MODE>(m, sum);
+    const float q = (MODE == GALA_SOFTMAX_REF) ? 1.0f / (sum + (float)p.seg.n * 1e-12f)  // torch::reciprocal
+                                               : 1.0f / sum;
+    if (!mine) return;
     if (in_regs) {
         int64_t e0, e1;
         row_range(p, 0, row, e0, e1);
@@ -241,67 +368,157 @@ __global__ __launch_bounds__(kBlock) void k_softmax_fwd(EdgeParams p, const floa
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        const int64_t n = (e1 - e0) << LH;
-        const float *lr = logit + (e0 << LH);
-        float *ar = alpha + (e0 << LH);
-        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-            load_tile<G, K>(lr, n, t0, gl, -INFINITY, x);
+        softmax_write<G, HP, MODE>(logit, alpha, e0, e1, gl, m, q);
+    }
+}
+
+// hub rows: per-chunk head (m, sum) -> ws[c] = {m[HP], sum[HP]}
+template <int G, int HP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd_chunk(EdgeParams p, const float *logit, HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    float m = -INFINITY, sum = 0.0f, x[kTileK];
+    softmax_stats<G, HP, MODE>(logit, e0, e1, gl, m, sum, x);
+    softmax_reduce<G, HP, MODE>(m, sum);
+    if (gl < HP) {
+        sp.ws[c * sp.ws_cols + gl] = m;
+        sp.ws[c * sp.ws_cols + HP + gl] = sum;
+    }
+}
+
+// hub rows: merge the chunks' (m, sum) in chunk order -> the row's (m, q) in ws[c0]
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd_fixup(EdgeParams p, HubSplit sp) {
+    const int H = p.heads;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sp.n_rows_split * H) return;
+    const int64_t ri = t / H;
+    const int h = (int)(t % H);
+    const int64_t c0 = sp.row_chunk0[ri];
+    float m = -INFINITY, sum = 0.0f;
+    for (int64_t cc = c0; cc < sp.row_chunk0[ri + 1]; ++cc) {
+        const float mc = sp.ws[cc * sp.ws_cols + h], sc = sp.ws[cc * sp.ws_cols + H + h];
+        if (MODE == GALA_SOFTMAX_REF) {
+            sum += sc;
+        } else if (mc != -INFINITY) {
+            const float mn = fmaxf(m, mc);
+            sum = ((m == -INFINITY) ? 0.0f : sum * expf(m - mn)) + sc * expf(mc - mn);
+            m = mn;
+        }
+    }
+    const float q = (MODE == GALA_SOFTMAX_REF) ? 1.0f / (sum + 1e-12f) : 1.0f / sum;
+    sp.ws[c0 * sp.ws_cols + h] = m;
+    sp.ws[c0 * sp.ws_cols + H + h] = q;
+}
+
+// hub rows: alpha of one chunk with its row's (m, q)
+template <int G, int HP, int MODE>
+__global__ __launch_bounds__(kBlock) void k_softmax_fwd_chunk2(EdgeParams p, const float *logit, float *alpha,
+                                                               HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const int h = gl & (HP - 1);
+    const float *w0 = sp.ws + (int64_t)sp.row_chunk0[ri] * sp.ws_cols;
+    softmax_write<G, HP, MODE>(logit, alpha, e0, e1, gl, w0[h], w0[HP + h]);
+}
+
+template <int G, int HP>
+__device__ __forceinline__ float dot_range(const float *a, const float *b, int64_t e0, int64_t e1, int gl,
+                                           float (&av)[kTileK], float (&dv)[kTileK]) {
+    constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
+    const int64_t n = (e1 - e0) << LH;
+    const int64_t o = e0 << LH;
+    float part = 0.0f;
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        load_tile<G, K>(a + o, n, t0, gl, 0.0f, av);
+        load_tile<G, K>(b + o, n, t0, gl, 0.0f, dv);
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(x[k]) : expf(x[k] - m);
-                if (t < n) ar[t] = __fmul_rn(pe, q);
-            }
+        for (int k = 0; k < K; ++k) part += __fmul_rn(av[k], dv[k]);
+    }
+    return part;
+}
+
+template <int G, int HP>
+__device__ __forceinline__ void softmax_bwd_write(const float *alpha, const float *dalpha, float *dlogit,
+                                                  int64_t e0, int64_t e1, int gl, float acc,
+                                                  float (&a)[kTileK], float (&d)[kTileK], bool in_regs) {
+    constexpr int LH = __builtin_ctz(HP);
+    constexpr int K = kTileK;
+    const int64_t n = (e1 - e0) << LH;
+    const int64_t o = e0 << LH;
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        if (!in_regs) {
+            load_tile<G, K>(alpha + o, n, t0, gl, 0.0f, a);
+            load_tile<G, K>(dalpha + o, n, t0, gl, 0.0f, d);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            const float sds = __fmul_rn(a[k], d[k]);
+            if (t < n) dlogit[o + t] = __fsub_rn(sds, __fmul_rn(a[k], acc));  // sds - K8(acc)
         }
     }
 }
 
 template <int G, int HP, int MODE>
 __global__ __launch_bounds__(kBlock) void k_softmax_bwd(EdgeParams p, const float *alpha,
-                                                        const float *dalpha, float *dlogit) {
+                                                        const float *dalpha, float *dlogit, int32_t thr) {
     GALA_ROW_PROLOGUE(G);
     constexpr int LH = __builtin_ctz(HP);
     constexpr int K = kTileK;
+    const bool mine = row_ok && !hub_row(p, thr, row);
     const float eps = (MODE == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
     float part = 0.0f;
     float a[K], d[K];
     bool in_regs = false;
-    if (row_ok) {
+    if (mine) {
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
-            const int64_t n = (e1 - e0) << LH;
-            in_regs = p.seg.n == 1 && n <= G * K;
-            const int64_t o = e0 << LH;
-            for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-                load_tile<G, K>(alpha + o, n, t0, gl, 0.0f, a);
-                load_tile<G, K>(dalpha + o, n, t0, gl, 0.0f, d);
-#pragma unroll
-                for (int k = 0; k < K; ++k) part += __fmul_rn(a[k], d[k]);
-            }
+            in_regs = p.seg.n == 1 && ((e1 - e0) << LH) <= G * K;
+            part += dot_range<G, HP>(alpha, dalpha, e0, e1, gl, a, d);
         }
     }
     part = head_sum<G, HP>(part);
     const float acc = part + (float)p.seg.n * eps;  // K7 on sds (common.h:793-794)
-    if (!row_ok) return;
+    if (!mine) return;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        const int64_t n = (e1 - e0) << LH;
-        const int64_t o = e0 << LH;
-        for (int64_t t0 = 0; t0 < n; t0 += G * K) {
-            if (!in_regs) {
-                load_tile<G, K>(alpha + o, n, t0, gl, 0.0f, a);
-                load_tile<G, K>(dalpha + o, n, t0, gl, 0.0f, d);
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int64_t t = t0 + gl + (int64_t)k * G;
-                const float sds = __fmul_rn(a[k], d[k]);
-                if (t < n) dlogit[o + t] = __fsub_rn(sds, __fmul_rn(a[k], acc));  // sds - K8(acc)
-            }
-        }
+        softmax_bwd_write<G, HP>(alpha, dalpha, dlogit, e0, e1, gl, acc, a, d, in_regs);
     }
+}
+
+// hub rows: per-chunk head sums of alpha * d_alpha -> ws[c][h]
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_softmax_bwd_chunk(EdgeParams p, const float *alpha,
+                                                              const float *dalpha, HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    float a[kTileK], d[kTileK];
+    const float part = head_sum<G, HP>(dot_range<G, HP>(alpha, dalpha, e0, e1, gl, a, d));
+    if (gl < HP) sp.ws[c * sp.ws_cols + gl] = part;
+}
+
+// hub rows: acc = eps + the chunk sums in chunk order -> ws[c0][HP + h]
+__global__ __launch_bounds__(kBlock) void k_softmax_bwd_fixup(EdgeParams p, float eps, HubSplit sp) {
+    const int H = p.heads;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sp.n_rows_split * H) return;
+    const int64_t ri = t / H;
+    const int h = (int)(t % H);
+    const int64_t c0 = sp.row_chunk0[ri];
+    float r = 0.0f;
+    for (int64_t cc = c0; cc < sp.row_chunk0[ri + 1]; ++cc) r += sp.ws[cc * sp.ws_cols + h];
+    sp.ws[c0 * sp.ws_cols + H + h] = r + eps;
+}
+
+template <int G, int HP>
+__global__ __launch_bounds__(kBlock) void k_softmax_bwd_chunk2(EdgeParams p, const float *alpha,
+                                                               const float *dalpha, float *dlogit,
+                                                               HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const float acc = sp.ws[(int64_t)sp.row_chunk0[ri] * sp.ws_cols + HP + (gl & (HP - 1))];
+    float a[kTileK], d[kTileK];
+    softmax_bwd_write<G, HP>(alpha, dalpha, dlogit, e0, e1, gl, acc, a, d, false);
 }
 
 // ---- generic-heads variants (runtime head count, per-head passes) ---------------------
@@ -628,15 +845,6 @@ struct GatDev {
     float slope;
 };
 
-// Device view of the hub-row plan: rows longer than `threshold` are cut into chunks of
-// `chunk` edges that separate row groups run in parallel; their per-chunk partial state
-// goes to ws (ws_cols floats per chunk) and fix-up kernels combine it in chunk order.
-struct GatSplit {
-    const int32_t *rows, *row_chunk0, *chunk_row;
-    float *ws;
-    int64_t ws_cols, n_chunks, n_rows_split;
-    int32_t chunk, threshold;
-};
 
 // The lane's share of one row (or one chunk of a hub row) for the GAT kernels.
 template <int G, int VEC, int CH, bool RC>
@@ -841,22 +1049,10 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     }
 }
 
-// chunk c of a hub row -> its row group (n_seg == 1: plain CSR offsets)
-#define GALA_CHUNK_PROLOGUE(G)                                                                  \
-    const int lane = threadIdx.x & (kWave - 1);                                                 \
-    const int gl = lane & ((G)-1);                                                              \
-    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / (G)) \
-                      + lane / (G);                                                             \
-    if (c >= sp.n_chunks) return;                                                               \
-    const int32_t ri = sp.chunk_row[c];                                                         \
-    const int64_t row = sp.rows[ri];                                                            \
-    const int64_t r0 = p.rowptr[row], r1 = p.rowptr[row + 1];                                   \
-    const int64_t e0 = r0 + (c - sp.row_chunk0[ri]) * (int64_t)sp.chunk;                       \
-    const int64_t e1 = (e0 + sp.chunk < r1) ? e0 + sp.chunk : r1;
 
 // hub rows, forward: chunk partial state -> ws[c] = {acc[F], m[H], sum[H]}
 template <int G, int VEC, int U, int MODE, int CH, bool RC>
-__global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     FwdState<VEC, CH> st;
@@ -876,7 +1072,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d
 // hub rows, forward: combine the chunk partials in chunk order, store Y; (m, q) of every
 // head go to the row's first chunk slot for k_gat_alpha_chunk
 template <int G, int VEC, int MODE, int CH, bool RC>
-__global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d, HubSplit sp) {
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
     const int64_t ri = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / G) + lane / G;
@@ -919,7 +1115,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
 
 // hub rows, forward: alpha of one chunk's parked values with its row's (m, q)
 template <int G, int VEC, int MODE>
-__global__ __launch_bounds__(kBlock) void k_gat_alpha_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_alpha_chunk(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const int H = p.heads;
     const int h = gl % H;
@@ -1084,7 +1280,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd(EdgeParams p, GatDev d, int3
 // hub rows, backward pass 1: chunk partials -> ws[c] = {acc[H], s_msds[H], s_ma[H]}
 // (REF) or {acc[H]} with sds parked in d_logit (FIXED)
 template <int G, int VEC, int U, int HW, int MODE, int CH, bool RC>
-__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     float dy[CH][VEC];
@@ -1104,7 +1300,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk(EdgeParams p, GatDev d
 // hub rows, backward: sum the chunk partials in chunk order.  REF: d_aL.  FIXED: the row's
 // acc per head -> ws[c0][H + h] for k_gat_bwd_chunk2.  One thread per (split row, head).
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup(EdgeParams p, GatDev d, HubSplit sp) {
     const int H = p.heads;
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= sp.n_rows_split * H) return;
@@ -1131,7 +1327,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup(EdgeParams p, GatDev d
 
 // hub rows, FIXED backward pass 2: dz of one chunk; partial row sums -> ws[c][2H + h]
 template <int G>
-__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk2(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk2(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const int H = p.heads;
     const int h = gl % H;
@@ -1142,7 +1338,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_chunk2(EdgeParams p, GatDev 
 }
 
 // hub rows, FIXED backward: d_aL = the chunks' dz sums in chunk order
-__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup2(EdgeParams p, GatDev d, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fixup2(EdgeParams p, GatDev d, HubSplit sp) {
     const int H = p.heads;
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= sp.n_rows_split * H) return;
@@ -1242,6 +1438,31 @@ static int pow2_heads(int heads) {
 
 using namespace gala;
 
+static unsigned blocks_for_groups(int64_t n, int G) {
+    const int64_t per_block = (int64_t)(kBlock / kWave) * (kWave / G);
+    return (unsigned)((n + per_block - 1) / per_block);
+}
+
+// the hub-row plan of A, when it applies and its workspace holds `need` floats per chunk
+// (otherwise hub rows run in one pass, like every other row)
+static bool hub_split(const gala_csr_t *A, int64_t need, HubSplit *sp) {
+    const gala_split_plan_t *plan = A->split;
+    if (!plan || plan->n_chunks <= 0 || A->n_seg != 1 || !plan->rows || !plan->row_chunk0 ||
+        !plan->chunk_row || (need > 0 && (!plan->workspace || plan->ws_cols < need)) || plan->chunk < 1 ||
+        plan->threshold < 1)
+        return false;
+    sp->rows = plan->rows;
+    sp->row_chunk0 = plan->row_chunk0;
+    sp->chunk_row = plan->chunk_row;
+    sp->ws = plan->workspace;
+    sp->ws_cols = plan->ws_cols;
+    sp->n_chunks = plan->n_chunks;
+    sp->n_rows_split = plan->n_rows_split;
+    sp->chunk = plan->chunk;
+    sp->threshold = plan->threshold;
+    return true;
+}
+
 extern "C" int gala_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col,
                               int32_t heads, int32_t op, float slope, float *out_e,
                               void *stream) {
@@ -1256,14 +1477,22 @@ extern "C" int gala_sddvv_f32(const gala_csr_t *A, const float *a_row, const flo
     if (hp) {
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
+        HubSplit sp{};
+        const bool split = hub_split(A, 0, &sp);
+        const int32_t thr = split ? sp.threshold : 0;
+#define GALA_SDDVV_OP(OPV)                                                                          \
+    {                                                                                                \
+        hipLaunchKernelGGL((k_sddvv<GG, HH, OPV>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e, thr); \
+        if (split)                                                                                   \
+            hipLaunchKernelGGL((k_sddvv_chunk<GG, HH, OPV>), dim3(blocks_for_groups(sp.n_chunks, GG)), dim3(kBlock), \
+                               0, hs, p, a_row, b_col, slope, out_e, sp);                            \
+    }
         GALA_DISPATCH_GH(G, {
-            if (op == GALA_SDDVV_ADD)
-                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_ADD>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
-            else if (op == GALA_SDDVV_MUL)
-                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_MUL>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
-            else
-                hipLaunchKernelGGL((k_sddvv<GG, HH, GALA_SDDVV_ADD_LRELU>), grid, dim3(kBlock), 0, hs, p, a_row, b_col, slope, out_e);
+            if (op == GALA_SDDVV_ADD) GALA_SDDVV_OP(GALA_SDDVV_ADD)
+            else if (op == GALA_SDDVV_MUL) GALA_SDDVV_OP(GALA_SDDVV_MUL)
+            else GALA_SDDVV_OP(GALA_SDDVV_ADD_LRELU)
         });
+#undef GALA_SDDVV_OP
         return launch_status();
     }
     const int G = pick_group(A, heads);
@@ -1293,7 +1522,18 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
     if (hp) {
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
-        GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row));
+        HubSplit sp{};
+        const bool split = hub_split(A, 2 * (int64_t)hp, &sp);
+        const int32_t thr = split ? sp.threshold : 0;
+        GALA_DISPATCH_GH(G, {
+            hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row, thr);
+            if (split) {
+                hipLaunchKernelGGL((k_row_sum_chunk<GG, HH>), dim3(blocks_for_groups(sp.n_chunks, GG)), dim3(kBlock),
+                                   0, hs, p, v_e, sp);
+                hipLaunchKernelGGL(k_row_sum_fixup, dim3((unsigned)((sp.n_rows_split * hp + kBlock - 1) / kBlock)),
+                                   dim3(kBlock), 0, hs, p, eps, accum, out_row, sp);
+            }
+        });
         return launch_status();
     }
     const int G = pick_group(A, 1);
@@ -1314,7 +1554,15 @@ extern "C" int gala_row_scale_f32(const gala_csr_t *A, const float *q_row, int32
     if (hp) {
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
-        GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_scale<GG, HH>), grid, dim3(kBlock), 0, hs, p, q_row, v_inout));
+        HubSplit sp{};
+        const bool split = hub_split(A, 0, &sp);
+        const int32_t thr = split ? sp.threshold : 0;
+        GALA_DISPATCH_GH(G, {
+            hipLaunchKernelGGL((k_row_scale<GG, HH>), grid, dim3(kBlock), 0, hs, p, q_row, v_inout, thr);
+            if (split)
+                hipLaunchKernelGGL((k_row_scale_chunk<GG, HH>), dim3(blocks_for_groups(sp.n_chunks, GG)), dim3(kBlock),
+                                   0, hs, p, q_row, v_inout, sp);
+        });
         return launch_status();
     }
     const int G = pick_group(A, heads);
@@ -1337,12 +1585,26 @@ extern "C" int gala_edge_softmax_fwd_f32(const gala_csr_t *A, const float *logit
     if (hp) {
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
+        HubSplit sp{};
+        const bool split = hub_split(A, 2 * (int64_t)hp, &sp);
+        const int32_t thr = split ? sp.threshold : 0;
+        const unsigned cb = split ? blocks_for_groups(sp.n_chunks, G) : 0;
+        const unsigned tb = split ? (unsigned)((sp.n_rows_split * hp + kBlock - 1) / kBlock) : 0;
+#define GALA_SMF(MODEV)                                                                              \
+    {                                                                                                \
+        hipLaunchKernelGGL((k_softmax_fwd<GG, HH, MODEV>), grid, dim3(kBlock), 0, hs, p, logits, alpha, thr); \
+        if (split) {                                                                                 \
+            hipLaunchKernelGGL((k_softmax_fwd_chunk<GG, HH, MODEV>), dim3(cb), dim3(kBlock), 0, hs, p, logits, sp); \
+            hipLaunchKernelGGL((k_softmax_fwd_fixup<MODEV>), dim3(tb), dim3(kBlock), 0, hs, p, sp);  \
+            hipLaunchKernelGGL((k_softmax_fwd_chunk2<GG, HH, MODEV>), dim3(cb), dim3(kBlock), 0, hs, p, logits, \
+                               alpha, sp);                                                           \
+        }                                                                                            \
+    }
         GALA_DISPATCH_GH(G, {
-            if (mode == GALA_SOFTMAX_REF)
-                hipLaunchKernelGGL((k_softmax_fwd<GG, HH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
-            else
-                hipLaunchKernelGGL((k_softmax_fwd<GG, HH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, logits, alpha);
+            if (mode == GALA_SOFTMAX_REF) GALA_SMF(GALA_SOFTMAX_REF)
+            else GALA_SMF(GALA_SOFTMAX_FIXED)
         });
+#undef GALA_SMF
         return launch_status();
     }
     const int G = pick_group(A, 1);
@@ -1370,11 +1632,23 @@ extern "C" int gala_edge_softmax_bwd_f32(const gala_csr_t *A, const float *alpha
     if (hp) {
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
+        HubSplit sp{};
+        const bool split = hub_split(A, 2 * (int64_t)hp, &sp);
+        const int32_t thr = split ? sp.threshold : 0;
+        const unsigned cb = split ? blocks_for_groups(sp.n_chunks, G) : 0;
+        const unsigned tb = split ? (unsigned)((sp.n_rows_split * hp + kBlock - 1) / kBlock) : 0;
+        const float eps = (mode == GALA_SOFTMAX_REF) ? 1e-12f : 0.0f;
         GALA_DISPATCH_GH(G, {
             if (mode == GALA_SOFTMAX_REF)
-                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
+                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_REF>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits, thr);
             else
-                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits);
+                hipLaunchKernelGGL((k_softmax_bwd<GG, HH, GALA_SOFTMAX_FIXED>), grid, dim3(kBlock), 0, hs, p, alpha, d_alpha, d_logits, thr);
+            if (split) {
+                hipLaunchKernelGGL((k_softmax_bwd_chunk<GG, HH>), dim3(cb), dim3(kBlock), 0, hs, p, alpha, d_alpha, sp);
+                hipLaunchKernelGGL(k_softmax_bwd_fixup, dim3(tb), dim3(kBlock), 0, hs, p, eps, sp);
+                hipLaunchKernelGGL((k_softmax_bwd_chunk2<GG, HH>), dim3(cb), dim3(kBlock), 0, hs, p, alpha, d_alpha,
+                                   d_logits, sp);
+            }
         });
         return launch_status();
     }
@@ -1494,16 +1768,12 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
 struct GatArgs {
     EdgeParams p;
     GatDev d;
-    GatSplit sp;
+    HubSplit sp;
     bool split;
     int mode;
     hipStream_t hs;
 };
 
-static unsigned blocks_for_groups(int64_t n, int G) {
-    const int64_t per_block = (int64_t)(kBlock / kWave) * (kWave / G);
-    return (unsigned)((n + per_block - 1) / per_block);
-}
 
 template <int G, int VEC, int CH, bool RC, int MODE>
 static void launch_gat_mode(const GatArgs &a) {
@@ -1542,25 +1812,6 @@ static int gat_vec(const GatArgs &a, int L, int ch) {
     return GALA_OK;
 }
 
-// the hub-row plan of A, when it applies and its workspace holds `need` floats per chunk
-// (otherwise hub rows run in one pass, like every other row)
-static bool gat_split(const gala_csr_t *A, int64_t need, GatSplit *sp) {
-    const gala_split_plan_t *plan = A->split;
-    if (!plan || plan->n_chunks <= 0 || A->n_seg != 1 || !plan->rows || !plan->row_chunk0 ||
-        !plan->chunk_row || !plan->workspace || plan->ws_cols < need || plan->chunk < 1 ||
-        plan->threshold < 1)
-        return false;
-    sp->rows = plan->rows;
-    sp->row_chunk0 = plan->row_chunk0;
-    sp->chunk_row = plan->chunk_row;
-    sp->ws = plan->workspace;
-    sp->ws_cols = plan->ws_cols;
-    sp->n_chunks = plan->n_chunks;
-    sp->n_rows_split = plan->n_rows_split;
-    sp->chunk = plan->chunk;
-    sp->threshold = plan->threshold;
-    return true;
-}
 
 static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
@@ -1589,7 +1840,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
     a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out;
     a.hs = (hipStream_t)stream;
-    a.split = (!alpha_out || G % heads == 0) && gat_split(A, (int64_t)F + 2 * heads, &a.sp);
+    a.split = (!alpha_out || G % heads == 0) && hub_split(A, (int64_t)F + 2 * heads, &a.sp);
     const bool rc = aR == nullptr;
     int r;
     if (vec == 4) r = rc ? gat_vec<4, true>(a, L, ch) : gat_vec<4, false>(a, L, ch);
@@ -1702,7 +1953,7 @@ static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.d.slope = slope, a.d.dY = dY, a.d.lddy = lddy, a.d.alpha = alpha, a.d.d_logit = d_logit;
     a.d.d_aL = d_aL;
     a.hs = (hipStream_t)stream;
-    a.split = gat_split(A, 3 * (int64_t)heads, &a.sp);
+    a.split = hub_split(A, 3 * (int64_t)heads, &a.sp);
     const bool rc = aR == nullptr;
     int r;
     if (vec == 4) r = rc ? gat_bwd_vec<4, true>(a, L, hw, ch) : gat_bwd_vec<4, false>(a, L, hw, ch);

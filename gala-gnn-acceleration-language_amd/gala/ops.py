@@ -166,7 +166,7 @@ def sddvv(g: DeviceGraph, a, b, op=_abi.GALA_SDDVV_ADD, heads=1, slope=0.2) -> t
 def row_sum(g: DeviceGraph, v, heads=1, eps=1e-12, out=None, accum=False) -> torch.Tensor:
     if out is None:
         out = torch.zeros(g.n_rows * heads, device=v.device, dtype=torch.float32)
-    _abi.call("gala_row_sum_f32", g.csr(), _dp(v), heads, eps, _dp(out),
+    _abi.call("gala_row_sum_f32", g.csr(2 * heads), _dp(v), heads, eps, _dp(out),
               _abi.GALA_SPMM_ACCUM if accum else 0, _stream())
     return out
 
@@ -185,13 +185,13 @@ def sddmm(g: DeviceGraph, A, B, heads=1) -> torch.Tensor:
 
 def edge_softmax(g: DeviceGraph, logits, heads=1, mode=_abi.GALA_SOFTMAX_REF) -> torch.Tensor:
     out = torch.empty_like(logits)
-    _abi.call("gala_edge_softmax_fwd_f32", g.csr(), _dp(logits), heads, mode, _dp(out), _stream())
+    _abi.call("gala_edge_softmax_fwd_f32", g.csr(2 * heads), _dp(logits), heads, mode, _dp(out), _stream())
     return out
 
 
 def edge_softmax_bwd(g: DeviceGraph, alpha, d_alpha, heads=1, mode=_abi.GALA_SOFTMAX_REF):
     out = torch.empty_like(alpha)
-    _abi.call("gala_edge_softmax_bwd_f32", g.csr(), _dp(alpha), _dp(d_alpha), heads, mode,
+    _abi.call("gala_edge_softmax_bwd_f32", g.csr(2 * heads), _dp(alpha), _dp(d_alpha), heads, mode,
               _dp(out), _stream())
     return out
 

@@ -88,6 +88,14 @@ SplitState *find_split(const torch::Tensor &offsets) {
     return nullptr;
 }
 
+// a graph view whose hub-row plan carries a workspace of at least `cols` floats per chunk
+void with_workspace(CsrView &cv, const torch::Tensor &offsets, int64_t cols) {
+    if (!cv.c.split) return;
+    SplitState *sp = find_split(offsets);
+    sp->ensure_workspace(cols);
+    cv.c.split = &sp->plan;
+}
+
 CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torch::Tensor *vals,
              const torch::Tensor &bounds, int64_t segments, int val_heads = 1) {
     check_dev(offsets, torch::kInt, "offset_graph");
@@ -120,14 +128,6 @@ CsrView view(const torch::Tensor &offsets, const torch::Tensor &cols, const torc
     return v;
 }
 
-// a graph view whose hub-row plan carries a workspace of at least `cols` floats per chunk
-void with_workspace(CsrView &cv, const torch::Tensor &offsets, int64_t cols) {
-    if (!cv.c.split) return;
-    SplitState *sp = find_split(offsets);
-    sp->ensure_workspace(cols);
-    cv.c.split = &sp->plan;
-}
-
 torch::TensorOptions fopts(const torch::Tensor &like) {
     return torch::TensorOptions().dtype(torch::kFloat).device(like.device());
 }
@@ -140,6 +140,7 @@ torch::Tensor row_sum_impl(const torch::Tensor &offsets, const torch::Tensor &co
     TORCH_CHECK(cv.c.n_rows == nrows, "gala: nrows does not match offset_graph");
     check_dev(vv, torch::kFloat, "value_graph");
     const int heads = (int)(vv.numel() / std::max<int64_t>(cols.numel(), 1));
+    with_workspace(cv, offsets, 2 * std::max(heads, 1));  // hub-row partial sums
     auto out = torch::empty({nrows, std::max(heads, 1)}, fopts(v));
     check_on(vv, offsets, "value_graph");
     check(be(offsets).row_sum(&cv.c, vv.data_ptr<float>(), std::max(heads, 1), eps,
@@ -543,6 +544,7 @@ struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
         ctx->saved_data["li"] = li;
         Slot s = slot(2 * li);
         CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        with_workspace(cv, s.off, 2);
         auto v = value_graph.contiguous();
         check_dev(v, torch::kFloat, "value_graph");
         auto alpha = torch::empty_like(v);
@@ -557,6 +559,7 @@ struct NonLnrOpSoftmax : public torch::autograd::Function<NonLnrOpSoftmax> {
         const int64_t li = ctx->saved_data["li"].toInt();
         Slot s = slot(2 * li + 1);
         CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        with_workspace(cv, s.off, 2);
         auto alpha = ctx->get_saved_variables()[0];
         auto d = grad_outputs[0].contiguous();
         auto ds = torch::empty_like(alpha);
@@ -654,6 +657,7 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
     const Slot &ps = fixed ? fw : bw;
     CsrView cp = view(ps.off, ps.cols, nullptr, ps.bounds, ps.segs);
     cp.c.n_cols = x.size(0);
+    with_workspace(cp, ps.off, 2 * heads);
     auto dalpha = torch::empty_like(alpha);
     check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
                            (int32_t)F, heads, dalpha.data_ptr<float>(), stream_of(ps.off)),

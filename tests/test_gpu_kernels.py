@@ -306,6 +306,34 @@ def test_gat_hub_rows_split(mode, F, heads):
             np.testing.assert_allclose(host(daL2), daL2_ref, **TOL)
 
 
+@pytest.mark.parametrize("heads", [1, 8])
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+def test_edge_ops_hub_rows_split(heads, mode):
+    """Row-segment edge ops with hub rows cut into chunks (plan threshold 64, 32-edge
+    chunks): SDDVV / row-scale per chunk (bit-exact), row sum and softmax fwd/bwd from
+    chunk partials combined in order (tolerance)."""
+    g = powerlaw()
+    og = to_oracle(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    a = features(g.n_rows, heads, seed=71)
+    b = features(g.n_cols, heads, seed=72)
+    np.testing.assert_array_equal(host(ops.sddvv(dg, dev(a), dev(b), op=2, heads=heads, slope=0.2)),
+                                  orc.sddvv(og, a, b, heads=heads, op=2, slope=0.2))
+    v = edge_values(g.nnz, heads=heads, seed=73)
+    np.testing.assert_allclose(host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12)),
+                               orc.row_sum(og, v, heads=heads, eps=1e-12), **TOL)
+    vv = dev(v)
+    ops.row_scale_(dg, dev(a), vv, heads=heads)
+    np.testing.assert_array_equal(host(vv), orc.row_scale(og, a.ravel(), v, heads=heads))
+    s = edge_values(g.nnz, heads=heads, lo=-3, hi=3, seed=74)
+    d = edge_values(g.nnz, heads=heads, lo=-1, hi=1, seed=75)
+    a_ref = orc.softmax_fwd(og, s, heads=heads, mode=mode)
+    np.testing.assert_allclose(host(ops.edge_softmax(dg, dev(s), heads=heads, mode=mode)), a_ref, **TOL)
+    np.testing.assert_allclose(host(ops.edge_softmax_bwd(dg, dev(a_ref), dev(d), heads=heads, mode=mode)),
+                               orc.softmax_bwd(og, a_ref, d, heads=heads, mode=mode), **TOL)
+
+
 def test_edge_permute():
     g = powerlaw()
     t, perm = layout.transpose(g)
