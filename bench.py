@@ -206,7 +206,7 @@ def main():
     alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, seg0.nnz, F)
     achieved = alg / t_kernel
     gather_bytes = 4 * (hg.n_rows + 1) + seg0.nnz * (4 + 4 * F) + 4 * hg.n_rows * F
-    traffic = load_traffic("k_spmm_rowgroup<4, 8, 1, 8, false, false, false>") if world == 1 else None
+    traffic = load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>") if world == 1 else None
     out = {
         "metric": "aggregated edges/sec, GCN-2 ogbn-products (4 F=32 aggregations per step)",
         "value": value,
@@ -228,7 +228,7 @@ def main():
                    "parallelism": "1 GPU" if world == 1 else f"vertex partitions x{world}, RCCL all-gather halo"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK, "traffic": traffic,
-                     "kernel": "gala::k_spmm_rowgroup<VEC=4,G=8,CH=1,U=8,unweighted> (gala_spmm_f32, F=32, dst norm)",
+                     "kernel": "gala::k_spmm_rowgroup<VEC=4,G=8,CH=1,U=4,unweighted> (gala_spmm_f32, F=32, dst norm)",
                      "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg,
                      "gather_model_GBps": gather_bytes / t_kernel / 1e9,
                      "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json); "

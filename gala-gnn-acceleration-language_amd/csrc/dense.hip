@@ -18,7 +18,7 @@ namespace {
 
 constexpr int kRows = 32;    // rows staged in LDS per step
 constexpr int kPad = 4;
-constexpr int kRedLanes = 4; // lanes per output in the partial-sum reduction
+constexpr int kRedLanes = 64; // lanes (one wave) per output in the partial-sum reduction
 
 // One TK x TM (k, m) tile of one row chunk.  Lane layout: (TK/4) x (TM/4) = 256 lanes,
 // each owning a 4x4 register block; the next 32-row step is loaded into registers while
@@ -105,26 +105,30 @@ __global__ __launch_bounds__(kBlock) void k_tn_partial(int64_t N, int32_t K, int
     }
 }
 
-// out[i] (+)= sum_p part[p][i]: kRedLanes lanes per output each sum a fixed residue class
-// of p in order, then lane 0 adds the kRedLanes sums in lane order (deterministic).
+// out[i] (+)= sum_p part[p][i]: one wave per output; lane g sums the residue class
+// p = g mod 64 in order (8 loads in flight), then a fixed xor butterfly adds the 64 lane
+// sums (deterministic for given shapes).  One wave per output keeps the ~1000 partials
+// of a chunk-split contraction from serialising in a handful of lanes.
 __global__ __launch_bounds__(kBlock) void k_tn_reduce(int64_t count, int64_t P,
                                                       const float *__restrict__ part,
                                                       float *__restrict__ out, int accum) {
     constexpr int kOut = kBlock / kRedLanes;
-    __shared__ float red[kRedLanes][kOut];
-    const int o = threadIdx.x % kOut, g = threadIdx.x / kOut;
-    const int64_t i = (int64_t)blockIdx.x * kOut + o;
+    const int g = threadIdx.x % kRedLanes;
+    const int64_t i = (int64_t)blockIdx.x * kOut + threadIdx.x / kRedLanes;
+    if (i >= count) return;  // whole waves exit together
     float s = 0.0f;
-    if (i < count)
-        for (int64_t p = g; p < P; p += kRedLanes) s += part[p * count + i];
-    red[g][o] = s;
-    __syncthreads();
-    if (g == 0 && i < count) {
-        float tot = red[0][o];
+    int64_t p = g;
+    for (; p + 7 * kRedLanes < P; p += 8 * kRedLanes) {
+        float v[8];
 #pragma unroll
-        for (int q = 1; q < kRedLanes; ++q) tot += red[q][o];
-        out[i] = accum ? out[i] + tot : tot;
+        for (int k = 0; k < 8; ++k) v[k] = part[(p + k * kRedLanes) * count + i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[k];
     }
+    for (; p < P; p += kRedLanes) s += part[p * count + i];
+#pragma unroll
+    for (int o = kRedLanes / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (g == 0) out[i] = accum ? out[i] + s : s;
 }
 
 struct Plan {

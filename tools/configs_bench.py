@@ -8,6 +8,7 @@
           autograd backward (REF chain and FIXED exact gradients)
   reddit  Reddit-shaped GraphSAGE aggregation with kernel sampling sample(20):
           N=232,965, E=114,615,892 (R-MAT power law), F=256, nsamp=20, ra=5, rb=7
+  papers  one GPU's shard of the 8-way ogbn-papers100M partition, GCN-3 at F=128
 Prints one JSON line per measurement (median of HIP-event timed reps).
 """
 import argparse
@@ -45,11 +46,11 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def gcn_step(name, hg, F):
+def gcn_step(name, hg, F, aggs=4):
     dg = ops.DeviceGraph.from_host(hg)
     N, E = hg.n_rows, hg.nnz
     X = torch.rand((N, F), device="cuda") * 2 - 1
-    bufs = [torch.empty_like(X) for _ in range(5)]
+    bufs = [torch.empty_like(X) for _ in range(aggs + 1)]
 
     def step():
         norm = ops.degree(dg, power=-0.5)
@@ -62,7 +63,7 @@ def gcn_step(name, hg, F):
     norm = ops.degree(dg, power=-0.5)
     tk = timeit(lambda: ops.spmm(dg, bufs[0], dst_scale=norm, out=bufs[1]), reps=20)
     alg = 4 * (N + 1) + 4 * E + 8 * N * F + 4 * N
-    emit(config=name, op="gcn2_step", ms=t * 1e3, edges_per_s=4 * E / t, N=N, E=E, F=F)
+    emit(config=name, op=f"gcn_step_{aggs}_aggregations", ms=t * 1e3, edges_per_s=aggs * E / t, N=N, E=E, F=F)
     emit(config=name, op="spmm_kernel", ms=tk * 1e3, edges_per_s=E / tk, alg_GBps=alg / tk / 1e9,
          roofline_frac=alg / tk / 8e12)
 
@@ -155,7 +156,7 @@ def reddit(hg):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="arxiv,gat,reddit")
+    ap.add_argument("--which", default="arxiv,gat,reddit,papers")
     a = ap.parse_args()
     w = a.which.split(",")
     if "arxiv" in w:
@@ -164,6 +165,13 @@ def main():
         gat(layout.gen_graph("uniform", 2_449_029, 61_859_140, seed=42))
     if "reddit" in w:
         reddit(layout.gen_graph("rmat", 232_965, (114_615_892 - 232_965) // 2, seed=42))
+    if "papers" in w:
+        # config 5, one GPU's share of the 8-way vertex partition of ogbn-papers100M
+        # (N = 111,059,956 / 8, E = 1,726,745,828 / 8), GCN-3 at F = 128: 3 forward + 3
+        # backward aggregations per step (the cut-edge halo exchange needs the 8 ranks)
+        n = 111_059_956 // 8
+        gcn_step("papers100M_shard_of_8", layout.gen_graph("uniform", n, (1_726_745_828 // 8 - n) // 2, seed=42),
+                 128, aggs=6)
 
 
 if __name__ == "__main__":
