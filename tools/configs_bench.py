@@ -9,6 +9,7 @@
   reddit  Reddit-shaped GraphSAGE aggregation with kernel sampling sample(20):
           N=232,965, E=114,615,892 (R-MAT power law), F=256, nsamp=20, ra=5, rb=7
   papers  one GPU's shard of the 8-way ogbn-papers100M partition, GCN-3 at F=128
+  papers_full  (not in the default set) the whole Papers100M shape on one GPU, F=128
 Prints one JSON line per measurement (median of HIP-event timed reps).
 """
 import argparse
@@ -154,6 +155,33 @@ def reddit(hg):
     emit(config="reddit_sage", op="spmm_full_F256", ms=t * 1e3, edges_per_s=E / t)
 
 
+def papers_full():
+    """The whole ogbn-papers100M shape (111 M vertices, 1.73 B edges, F = 128) resident on ONE
+    MI355X: X and Y are 57 GB each.  Integer-valued features make the sum order-free, so
+    2000 sampled rows are checked exactly against a float64 gather of the same rows."""
+    n = 111_059_956
+    t0 = time.time()
+    hg = layout.gen_graph("uniform", n, (1_726_745_828 - n) // 2, seed=42)
+    print(f"graph built {time.time()-t0:.1f}s N={hg.n_rows} E={hg.nnz}", file=sys.stderr, flush=True)
+    dg = ops.DeviceGraph.from_host(hg)
+    N, E, F = hg.n_rows, hg.nnz, 128
+    X = torch.randint(-8, 9, (N, F), device="cuda", dtype=torch.float32)
+    Y = torch.empty_like(X)
+    t = timeit(lambda: ops.spmm(dg, X, out=Y), reps=5, warm=1)
+    print(f"spmm timed {time.time()-t0:.1f}s", file=sys.stderr, flush=True)
+    rng = np.random.default_rng(7)
+    rows = np.sort(rng.choice(N, 2000, replace=False))
+    worst = 0.0
+    for r in rows:
+        c = torch.from_numpy(hg.col[hg.rowptr[r]:hg.rowptr[r + 1]].astype(np.int64)).cuda()
+        ref = X.index_select(0, c).double().sum(0)
+        worst = max(worst, float((Y[r].double() - ref).abs().max()))
+    alg = 4 * (N + 1) + 4 * E + 8 * N * F
+    emit(config="papers100M_full_1gpu", op="spmm_kernel", ms=t * 1e3, edges_per_s=E / t, alg_GBps=alg / t / 1e9,
+         roofline_frac=alg / t / 8e12, gather_GB=E * F * 4 / 1e9, N=N, E=E, F=F,
+         max_mem_GB=torch.cuda.max_memory_allocated() / 1e9, sampled_rows_max_abs_err=worst)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="arxiv,gat,reddit,papers")
@@ -172,6 +200,8 @@ def main():
         n = 111_059_956 // 8
         gcn_step("papers100M_shard_of_8", layout.gen_graph("uniform", n, (1_726_745_828 // 8 - n) // 2, seed=42),
                  128, aggs=6)
+    if "papers_full" in w:
+        papers_full()
 
 
 if __name__ == "__main__":
