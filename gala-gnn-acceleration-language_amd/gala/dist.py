@@ -193,3 +193,205 @@ class DistGCNAggregator:
             self.dist.all_gather_into_tensor(recv, send, group=self.group)
             self._spmm(self.segs[0], self.Xs, out, self.norm, False)
         return self._spmm(self.segs[1], self.Xs, out, self.norm, True)  # cut edges, ACCUM
+
+
+# ---- partitioning a given graph ----------------------------------------------------------
+# SURVEY §8(e) for graphs that arrive whole (the reference's npy datasets, config 5): rank p
+# owns the contiguous vertex range [bounds[p], bounds[p+1)) -- cut where the stored-edge
+# count (plus one per row) crosses p/P of the total -- with all edges into those rows.
+# Each rank's feature buffer Xs holds, in GLOBAL id order,
+#     [ halo rows owned by ranks < p | own rows | halo rows owned by ranks > p ]
+# so the remap global id -> Xs row is monotone and a row's edges keep their CSR order:
+# one SpMM over `graph` sums every row in exactly the single-GPU (and reference) order,
+# which makes the distributed result bit-identical to the one-GPU result.  The halo rows
+# are fetched once per aggregation by point-to-point sends/receives straight into their
+# Xs slices (RCCL grouped send/recv: only the rows a peer actually needs cross xGMI).
+# Overlap mode instead runs the own-column edges (`own_graph`) while the halo is in
+# flight and accumulates the halo edges (`halo_graph`) afterwards: faster, but a row's
+# sum is then (own part) + (halo part), exact to fp32 rounding only.
+
+
+def row_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
+    """[world+1] vertex-range cuts balancing stored edges + rows per rank (deterministic:
+    every rank computes the same cuts from the same rowptr)."""
+    n = rowptr.shape[0] - 1
+    w = rowptr.astype(np.int64) + np.arange(n + 1, dtype=np.int64)
+    targets = (np.arange(1, world, dtype=np.int64) * int(w[-1])) // world
+    cuts = np.searchsorted(w, targets, side="left")
+    return np.concatenate([[0], cuts, [n]]).astype(np.int64)
+
+
+def _csr_select(rowptr: np.ndarray, col: np.ndarray, keep: np.ndarray, n_cols: int) -> layout.HostGraph:
+    """The rows' edges with keep[e] set, CSR order preserved."""
+    n = rowptr.shape[0] - 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
+    rp = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(rows[keep], minlength=n), out=rp[1:])
+    return layout.HostGraph(n, n_cols, rp.astype(np.int32), np.ascontiguousarray(col[keep], np.int32))
+
+
+@dataclass
+class GraphPartition:
+    rank: int
+    world: int
+    bounds: np.ndarray          # int64 [world+1] global vertex ranges
+    lo: int                     # halo rows owned by lower ranks: Xs[0:lo]
+    halo: np.ndarray            # int64 global ids of all halo rows, ascending
+    recv_counts: np.ndarray     # int64 [world] halo rows owned by each rank (0 for self)
+    graph: layout.HostGraph     # own rows over the Xs columns, global edge order (exact)
+    own_graph: layout.HostGraph   # the edges into own columns (overlap mode, first)
+    halo_graph: layout.HostGraph  # the edges into halo columns (overlap mode, second)
+    split_threshold: int = 0      # the WHOLE graph's hub-row threshold (ops.DeviceGraph.from_host):
+                                  # the same rows split into the same chunks as on one GPU
+
+    @property
+    def r0(self) -> int:
+        return int(self.bounds[self.rank])
+
+    @property
+    def n(self) -> int:
+        return int(self.bounds[self.rank + 1] - self.bounds[self.rank])
+
+    @property
+    def n_cols(self) -> int:
+        return self.n + int(self.halo.shape[0])
+
+    @property
+    def own_slice(self) -> slice:
+        return slice(self.lo, self.lo + self.n)
+
+    def recv_offsets(self) -> np.ndarray:
+        """Xs row where the block received from rank q starts ([world])."""
+        off = np.zeros(self.world, np.int64)
+        pos = 0
+        for q in range(self.world):
+            if q == self.rank:
+                pos = self.lo + self.n
+                continue
+            off[q] = pos
+            pos += int(self.recv_counts[q])
+        return off
+
+    def xs_to_global(self) -> np.ndarray:
+        """Global vertex id of every Xs row (int64 [n_cols])."""
+        own = np.arange(self.r0, self.r0 + self.n, dtype=np.int64)
+        return np.concatenate([self.halo[:self.lo], own, self.halo[self.lo:]])
+
+
+def partition_graph(g: layout.HostGraph, rank: int, world: int,
+                    bounds: np.ndarray | None = None) -> GraphPartition:
+    """Rank `rank`'s share of the square one-segment graph `g` (rows = destinations)."""
+    if g.n_rows != g.n_cols or g.n_seg != 1:
+        raise ValueError("partition_graph needs a square, one-segment CSR")
+    b = row_bounds(g.rowptr, world) if bounds is None else np.asarray(bounds, np.int64)
+    r0, r1 = int(b[rank]), int(b[rank + 1])
+    e0, e1 = int(g.rowptr[r0]), int(g.rowptr[r1])
+    rp = (g.rowptr[r0:r1 + 1].astype(np.int64) - e0)
+    cols = g.col[e0:e1].astype(np.int64)
+    own = (cols >= r0) & (cols < r1)
+    halo = np.unique(cols[~own])
+    lo = int(np.searchsorted(halo, r0))
+    n = r1 - r0
+    xs_col = np.where(own, lo + (cols - r0), 0)
+    hidx = np.searchsorted(halo, cols[~own])
+    xs_col[~own] = np.where(hidx < lo, hidx, hidx + n)
+    xs_col = xs_col.astype(np.int32)
+    n_cols = n + int(halo.shape[0])
+    owner = np.searchsorted(b, halo, side="right") - 1
+    recv_counts = np.bincount(owner, minlength=world).astype(np.int64)
+    graph = layout.HostGraph(n, n_cols, rp.astype(np.int32), xs_col)
+    thr = max(1024, 8 * int(np.ceil(g.nnz / max(g.n_rows, 1))))
+    return GraphPartition(rank, world, b, lo, halo, recv_counts, graph,
+                          _csr_select(rp, xs_col, own, n_cols), _csr_select(rp, xs_col, ~own, n_cols), thr)
+
+
+class HaloExchange:
+    """Per-aggregation halo fetch for a GraphPartition: rank p sends every peer exactly
+    the own rows that peer's edges read, received straight into the peer's Xs slices.
+
+    Setup exchanges the request lists once (counts by all_to_all_single, ids by grouped
+    send/recv); each call packs the rows to send with one index_select and issues one
+    grouped batch of sends/receives (RCCL on the GPU, gloo on the CPU tests)."""
+
+    def __init__(self, part: GraphPartition, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.part, self.group = torch, dist, part, group
+        self.device = torch.device(device)
+        P, p = part.world, part.rank
+        recv = torch.from_numpy(part.recv_counts.copy()).to(self.device)
+        send = torch.empty_like(recv)
+        dist.all_to_all_single(send, recv, group=group)
+        self.send_counts = send.cpu().numpy().astype(np.int64)
+        self.recv_counts = part.recv_counts
+        # my requests to q, as q-local row ids; q's requests to me -> my send rows
+        owner = np.searchsorted(part.bounds, part.halo, side="right") - 1
+        req = {q: torch.from_numpy((part.halo[owner == q] - part.bounds[q]).astype(np.int64)).to(self.device)
+               for q in range(P) if q != p and self.recv_counts[q] > 0}
+        got = {q: torch.empty(int(self.send_counts[q]), dtype=torch.int64, device=self.device)
+               for q in range(P) if q != p and self.send_counts[q] > 0}
+        ops = [dist.P2POp(dist.isend, req[q], q, group) for q in sorted(req)]
+        ops += [dist.P2POp(dist.irecv, got[q], q, group) for q in sorted(got)]
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        self.send_peers = sorted(got)
+        self.recv_peers = sorted(req)
+        self.send_idx = (torch.cat([got[q] for q in self.send_peers]) if got
+                         else torch.empty(0, dtype=torch.int64, device=self.device))
+        self.send_off = np.concatenate([[0], np.cumsum([self.send_counts[q] for q in self.send_peers])]).astype(np.int64)
+        self.recv_off = part.recv_offsets()
+        self.sendbuf = None
+
+    def start(self, Xs):
+        """Pack and post the exchange for Xs (own rows already written); returns works."""
+        torch, dist, part = self.torch, self.dist, self.part
+        F = Xs.shape[1]
+        if self.sendbuf is None or self.sendbuf.shape[1] != F:
+            self.sendbuf = torch.empty((self.send_idx.shape[0], F), dtype=Xs.dtype, device=Xs.device)
+        if self.send_idx.shape[0]:
+            torch.index_select(Xs[part.own_slice], 0, self.send_idx, out=self.sendbuf)
+        ops = [dist.P2POp(dist.isend, self.sendbuf[self.send_off[i]:self.send_off[i + 1]], q, self.group)
+               for i, q in enumerate(self.send_peers)]
+        ops += [dist.P2POp(dist.irecv, Xs[self.recv_off[q]:self.recv_off[q] + self.recv_counts[q]], q, self.group)
+                for q in self.recv_peers]
+        return dist.batch_isend_irecv(ops) if ops else []
+
+
+class DistAggregator:
+    """norm * A (norm * H) over a GraphPartition of a given graph (see the block comment
+    above partition_graph).  exact=True: one SpMM after the halo arrives, bit-identical
+    to the one-GPU aggregation; exact=False: own-column edges overlap the exchange.
+    spmm / row_broadcast / degree default to the HIP ops (injectable for CPU tests)."""
+
+    def __init__(self, part: GraphPartition, F: int, device, exact: bool = True, spmm=None,
+                 row_broadcast=None, degree=None, group=None):
+        import torch
+        self.torch, self.part, self.F, self.exact = torch, part, F, exact
+        if spmm is None:
+            from . import ops
+            spmm = lambda g, X, out, dst_scale, accum: ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)  # noqa: E731
+            row_broadcast = lambda s, X, out: ops.row_broadcast(s, X, out=out)  # noqa: E731
+            degree = lambda g: ops.degree(g, power=-0.5)  # noqa: E731
+            mk = lambda hg: ops.DeviceGraph.from_host(hg, device, split=part.split_threshold)  # noqa: E731
+        else:
+            mk = lambda hg: hg  # noqa: E731
+        self._spmm, self._rb = spmm, row_broadcast
+        self.graph = mk(part.graph)
+        self.own_graph = None if exact else mk(part.own_graph)
+        self.halo_graph = None if exact else mk(part.halo_graph)
+        self.norm = degree(self.graph)          # own rows' full degrees
+        self.Xs = torch.empty((part.n_cols, F), device=device, dtype=torch.float32)
+        self.exchange = HaloExchange(part, device, group) if part.world > 1 else None
+
+    def __call__(self, H, out):
+        p = self.part
+        self._rb(self.norm, H, self.Xs[p.own_slice])                 # own rows of Xs = norm * H
+        works = self.exchange.start(self.Xs) if self.exchange else []
+        if self.exact:
+            for w in works:
+                w.wait()
+            return self._spmm(self.graph, self.Xs, out, self.norm, False)
+        self._spmm(self.own_graph, self.Xs, out, self.norm, False)   # overlaps the exchange
+        for w in works:
+            w.wait()
+        return self._spmm(self.halo_graph, self.Xs, out, self.norm, True)
