@@ -705,15 +705,42 @@ template <int G, int VEC, int CH>
 struct Lanes {
     bool valid[CH];
     int64_t off[CH];
+    int nv[CH];  // real columns of the lane's vector: VEC, fewer in a padded row's last one
     __device__ __forceinline__ Lanes(int gl, int32_t F) {
 #pragma unroll
         for (int ch = 0; ch < CH; ++ch) {
             const int f = (ch * G + gl) * VEC;
             valid[ch] = f < F;
             off[ch] = valid[ch] ? f : 0;  // lanes past F read a valid column, never store
+            nv[ch] = valid[ch] ? (F - f < VEC ? F - f : VEC) : 0;
         }
     }
+    // element i of vector ch is a real column (padding columns are read but zeroed before
+    // any dot product, and never written)
+    __device__ __forceinline__ bool in(int ch, int i) const { return i < nv[ch]; }
 };
+
+// fp32 vectors of VEC lanes' worth of features
+template <int VEC>
+struct GVec;
+template <>
+struct GVec<1> { typedef float T; };
+template <>
+struct GVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
+template <>
+struct GVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
+
+// A gathered vector with its padding columns (element i >= nv) zeroed: padding may hold
+// anything, and 0 * Inf would reach a dot product.
+template <int VEC, typename V>
+__device__ __forceinline__ V mask_pad(int nv, V v) {
+    if (nv < VEC) {
+        float *e = reinterpret_cast<float *>(&v);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) e[i] = i < nv ? e[i] : 0.0f;
+    }
+    return v;
+}
 
 // Edges [e0, e1) of `row` (one row group): out[e] = <Ad[row], Bd[col_e]> per head.
 template <int G, int VEC, int HW, int U, int CH = 1>
@@ -727,7 +754,7 @@ __device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool ro
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) a[ch][i] = (row_ok && ln.valid[ch]) ? Ad[row * lda + ln.off[ch] + i] : 0.0f;
+        for (int i = 0; i < VEC; ++i) a[ch][i] = (row_ok && ln.in(ch, i)) ? Ad[row * lda + ln.off[ch] + i] : 0.0f;
     const int H = p.heads;
     const int D = F / H;
     const int h = cv ? (int)(ln.off[0] / D) : 0;
@@ -741,9 +768,12 @@ __device__ __forceinline__ void sddmm_range(const EdgeParams &p, int gl, bool ro
             const float *bp = Bd + c * ldb;
             float acc = 0.0f;
 #pragma unroll
-            for (int ch = 0; ch < CH; ++ch)
+            for (int ch = 0; ch < CH; ++ch) {
+                typedef typename GVec<VEC>::T V;
+                const V bv = mask_pad<VEC>(ln.nv[ch], *reinterpret_cast<const V *>(bp + ln.off[ch]));
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) acc = fmaf(a[ch][i], bp[ln.off[ch] + i], acc);
+                for (int i = 0; i < VEC; ++i) acc = fmaf(a[ch][i], reinterpret_cast<const float *>(&bv)[i], acc);
+            }
             part[k] = acc;
         }
         if (HW == G) {
@@ -799,14 +829,6 @@ __global__ __launch_bounds__(kBlock) void k_sddmm(EdgeParams p, const float *Ad,
 // ---- fused GAT aggregation -----------------------------------------------------------
 // Row group of G lanes, lane g owns CH x VEC features (Lanes); U edges per batch: cols,
 // aR[col] and the X row slices are all loaded before the softmax updates.
-template <int VEC>
-struct GVec;
-template <>
-struct GVec<1> { typedef float T; };
-template <>
-struct GVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
-template <>
-struct GVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
 
 // RC (one head): the source logit aR[col] = <X[col,:], wR> + bR is recomputed from the X
 // row the aggregation gathers anyway (the DSL's attnR = dsl.nn.ffn(res, out=1) of the
@@ -830,7 +852,7 @@ __device__ __forceinline__ void load_attn(const Lanes<G, VEC, CH> &ln, const flo
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) w[ch][i] = ln.valid[ch] ? wR[ln.off[ch] + i] : 0.0f;
+        for (int i = 0; i < VEC; ++i) w[ch][i] = ln.in(ch, i) ? wR[ln.off[ch] + i] : 0.0f;
 }
 
 // Operands of the fused GAT kernels (forward and backward).
@@ -908,7 +930,7 @@ __device__ __forceinline__ void gat_fwd_range(const EdgeParams &p, const GatDev 
             if (!RC) ar[k] = d.aR[c[k] * H + hh];
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch)
-                x[k][ch] = *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]);
+                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
         }
         if (RC) {
 #pragma unroll
@@ -971,7 +993,14 @@ __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G,
 #pragma unroll
         for (int i = 0; i < VEC; ++i)
             ov[i] = (MODE != GALA_SOFTMAX_REF && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
-        *reinterpret_cast<V *>(d.Y + row * d.ldy + gl_.ln.off[ch]) = out;
+        float *yp = d.Y + row * d.ldy + gl_.ln.off[ch];
+        if (gl_.ln.nv[ch] == VEC) {
+            *reinterpret_cast<V *>(yp) = out;
+        } else {  // a padded row's last vector: its real columns only
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                if (gl_.ln.in(ch, i)) yp[i] = ov[i];
+        }
     }
     return q;
 }
@@ -1060,9 +1089,9 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d
     float *w = sp.ws + c * sp.ws_cols;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
-        if (gl_.ln.valid[ch])
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) w[gl_.ln.off[ch] + i] = st.acc[ch][i];
+        for (int i = 0; i < VEC; ++i)
+            if (gl_.ln.in(ch, i)) w[gl_.ln.off[ch] + i] = st.acc[ch][i];
     if (gl_.leader) {
         w[d.F + gl_.hh] = st.m;
         w[d.F + gl_.H + gl_.hh] = st.sum;
@@ -1100,7 +1129,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
         for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
-                const float v = gl_.ln.valid[ch] ? w[gl_.ln.off[ch] + i] : 0.0f;
+                const float v = gl_.ln.in(ch, i) ? w[gl_.ln.off[ch] + i] : 0.0f;
                 st.acc[ch][i] = (MODE == GALA_SOFTMAX_REF) ? __fadd_rn(st.acc[ch][i], v)
                                                            : fmaf(st.acc[ch][i], a, __fmul_rn(v, b));
             }
@@ -1156,7 +1185,7 @@ __device__ __forceinline__ void gat_bwd_range(const EdgeParams &p, const GatDev 
             if (!RC) ar[k] = d.aR[c[k] * H + hh];
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch)
-                x[k][ch] = *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]);
+                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
         }
         if (RC) {
 #pragma unroll
@@ -1199,7 +1228,7 @@ __device__ __forceinline__ void load_dy(const GatDev &d, const GatLane<G, VEC, C
     for (int ch = 0; ch < CH; ++ch) {
         const V t = *reinterpret_cast<const V *>(d.dY + row * d.lddy + gl_.ln.off[ch]);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.valid[ch] ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+        for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.in(ch, i) ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
     }
 }
 
@@ -1382,6 +1411,9 @@ static int pick_group_tiled(const gala_csr_t *A, int heads) {
 // 16 lanes own ceil(L/16) chunks each (Lanes), instead of 64 lanes one vector each, so 4
 // rows share a wave and the per-edge softmax / reduction work is not repeated 64-fold.
 // Returns the chunk count (1 = the one-vector-per-lane layout).
+// F rounded up to a multiple of v (a padded row's width)
+static int64_t pad_to(int64_t F, int v) { return (F + v - 1) / v * v; }
+
 static int narrow_chunks(int heads, int vec, int L) {
     return (heads == 1 && vec < 4 && L > 16 && L <= 64) ? (L + 15) / 16 : 1;
 }
@@ -1723,9 +1755,12 @@ extern "C" int gala_sddmm_dot_f32(const gala_csr_t *A, const float *Ad, int64_t 
     if (A->n_rows == 0 || A->nnz == 0) return GALA_OK;
     if (!Ad || !Bd || !out_e) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
-    // VEC divides D, L = lanes per row, the per-head lane count D/VEC must be a power of 2
+    // VEC divides D (or, one head, fits padded rows: lda, ldb >= F rounded up to VEC), L =
+    // lanes per row, the per-head lane count D/VEC must be a power of 2
     int vec = 4;
-    while (vec > 1 && (D % vec || lda % vec || ldb % vec)) vec >>= 1;
+    while (vec > 1 && (!(D % vec == 0 || (heads == 1 && lda >= pad_to(F, vec) && ldb >= pad_to(F, vec))) ||
+                       lda % vec || ldb % vec || ((uintptr_t)Ad % (4 * vec)) || ((uintptr_t)Bd % (4 * vec))))
+        vec >>= 1;
     const int L = (F + vec - 1) / vec;
     const int hw_l = D / vec;
     int Gp = 1;
@@ -1825,9 +1860,10 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
+    // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
     int vec = 4;
-    while (vec > 1 && (D % vec || ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) ||
-                       ((uintptr_t)Y % (4 * vec))))
+    while (vec > 1 && (!(D % vec == 0 || (heads == 1 && ldx >= pad_to(F, vec) && ldy >= pad_to(F, vec))) ||
+                       ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) || ((uintptr_t)Y % (4 * vec))))
         vec >>= 1;
     const int L = (F + vec - 1) / vec;
     const int ch = narrow_chunks(heads, vec, L);
@@ -1937,8 +1973,8 @@ static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (!aR && (mode != GALA_SOFTMAX_REF || heads != 1)) return GALA_ERR_UNSUPPORTED;
     const int D = F / heads;
     int vec = 4;
-    while (vec > 1 && (D % vec || ldx % vec || lddy % vec || ((uintptr_t)X % (4 * vec)) ||
-                       ((uintptr_t)dY % (4 * vec))))
+    while (vec > 1 && (!(D % vec == 0 || (heads == 1 && ldx >= pad_to(F, vec) && lddy >= pad_to(F, vec))) ||
+                       ldx % vec || lddy % vec || ((uintptr_t)X % (4 * vec)) || ((uintptr_t)dY % (4 * vec))))
         vec >>= 1;
     const int L = (F + vec - 1) / vec;
     int G = 1;

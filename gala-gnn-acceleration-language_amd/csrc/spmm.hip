@@ -87,12 +87,15 @@ __device__ __forceinline__ void accumulate(typename VecT<VEC>::T &acc,
     }
 }
 
-// Per-lane column ownership of a row group.
+// Per-lane column ownership of a row group.  When F is not a multiple of VEC the rows are
+// padded (ldx, ldy >= F rounded up to VEC, checked on the host): the last vector of a row
+// loads the padding too (never used) and stores only its nv < VEC real columns.
 template <int VEC, int G, int CH, bool W>
 struct Cols {
     bool valid[CH];
     int64_t off[CH];
     int head[CH];
+    int nv[CH];
     __device__ __forceinline__ Cols(const SpmmParams &p, int gl) {
 #pragma unroll
         for (int ch = 0; ch < CH; ++ch) {
@@ -100,9 +103,22 @@ struct Cols {
             valid[ch] = f < p.F;  // lanes past F load a valid column and never store
             off[ch] = valid[ch] ? f : 0;
             head[ch] = W ? (int)(off[ch] / p.head_dim) : 0;
+            nv[ch] = valid[ch] ? (p.F - f < VEC ? p.F - f : VEC) : 0;
         }
     }
 };
+
+// Y row slice store of nv <= VEC columns (nv < VEC only for a padded row's last vector).
+template <int VEC>
+__device__ __forceinline__ void stv_n(float *p, const typename VecT<VEC>::T &v, int nv) {
+    if (nv == VEC) {
+        stv<VEC>(p, v);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+        if (i < nv) p[i] = reinterpret_cast<const float *>(&v)[i];
+}
 
 // acc += the edges [e0, e1) of one row (or nsamp kernel samples), sequentially in CSR
 // order; the loads of U edges are issued before the first add of the batch.
@@ -173,7 +189,7 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
                 for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fadd_rn(el<VEC>(y, i), el<VEC>(out, i));
             }
         }
-        stv<VEC>(yp, out);
+        stv_n<VEC>(yp, out, cl.nv[ch]);
     }
 }
 
@@ -419,11 +435,23 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     if (w && (A->val_heads < 1 || F % A->val_heads != 0)) return GALA_ERR_INVALID_ARG;
     const int32_t head_dim = w ? F / A->val_heads : F;
 
-    // widest vector that divides F, the head width and both strides with aligned bases
+    // widest vector that divides both strides with aligned bases and either divides F and
+    // the head width, or fits padded rows (one head, ldx and ldy >= F rounded up to it:
+    // the padding is read, never written)
+    // (a hub-row workspace row then holds whole vectors: ws_cols a multiple of VEC and at
+    // least the padded width)
     int vec = 4;
+    const bool one_head = !w || A->val_heads == 1;
+    const gala_split_plan_t *plan = A->split;
+    const bool use_split =
+        plan && plan->n_chunks > 0 && A->n_seg == 1 && !samp && !(flags & GALA_SPMM_EXACT);
     auto ok = [&](int v) {
-        return F % v == 0 && head_dim % v == 0 && ldx % v == 0 && ldy % v == 0 &&
-               ((uintptr_t)X % (4 * v)) == 0 && ((uintptr_t)Y % (4 * v)) == 0;
+        const int64_t Fv = ((int64_t)F + v - 1) / v * v;
+        const bool fits = (F % v == 0 && head_dim % v == 0) || (one_head && ldx >= Fv && ldy >= Fv);
+        const int64_t wcols = Fv < 512LL * v ? Fv : 512LL * v;
+        const bool ws_ok = !use_split || (plan->ws_cols % v == 0 && plan->ws_cols >= wcols);
+        return fits && ws_ok && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
+               ((uintptr_t)Y % (4 * v)) == 0;
     };
     while (vec > 1 && !ok(vec)) vec >>= 1;
 
@@ -451,9 +479,8 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     // hub rows: chunk partials + ordered fix-up (plan built once per graph on the host)
     SplitParams spl{};
     const SplitParams *sp = nullptr;
-    const gala_split_plan_t *plan = A->split;
     if (plan && plan->row_order && A->n_seg == 1) p.row_order = plan->row_order;
-    if (plan && plan->n_chunks > 0 && A->n_seg == 1 && !samp && !(flags & GALA_SPMM_EXACT)) {
+    if (use_split) {
         if (plan->threshold < 1 || plan->chunk < 1 || !plan->rows || !plan->row_chunk0 ||
             !plan->chunk_row || !plan->workspace)
             return GALA_ERR_INVALID_ARG;

@@ -60,11 +60,17 @@ void check(int status, const char *fn) {
                                        : std::string());
 }
 
+// a row-padded [N, F] view (see pad_rows4 below): row stride F rounded up to 4 floats
+bool row_padded(const torch::Tensor &x) {
+    return x.dim() == 2 && x.size(0) > 0 && x.stride(1) == 1 && x.size(1) % 4 != 0 &&
+           x.stride(0) == (x.size(1) + 3) / 4 * 4;
+}
+
 void check_dev(const torch::Tensor &t, torch::ScalarType ty, const char *name) {
     TORCH_CHECK(t.defined(), "gala: ", name, " is undefined");
     TORCH_CHECK(t.is_cuda() || t.is_cpu(), "gala: ", name, " is on unsupported device ", t.device());
     TORCH_CHECK(t.scalar_type() == ty, "gala: ", name, " has dtype ", t.scalar_type());
-    TORCH_CHECK(t.is_contiguous(), "gala: ", name, " must be contiguous");
+    TORCH_CHECK(t.is_contiguous() || row_padded(t), "gala: ", name, " must be contiguous");
 }
 
 // operand `t` must live on the graph's device (no implicit copies, no CPU fallback)
@@ -132,6 +138,29 @@ torch::TensorOptions fopts(const torch::Tensor &like) {
     return torch::TensorOptions().dtype(torch::kFloat).device(like.device());
 }
 
+// Row-padded feature matrices: an [N, F] view of storage whose row stride is F rounded up
+// to 4 floats.  With F % 4 != 0 (F = 47, the Products class count) the kernels then move
+// whole float4 vectors and a gathered row spans 2 cache lines instead of 2.4 on average;
+// the padding columns are read, zeroed before any dot product, and never written.
+
+// (row_padded() is defined above check_dev)
+// x itself when contiguous or row-padded, else a row-padded copy (GPU, one head only:
+// callers pass heads == 1) -- or a contiguous one on the CPU backend
+torch::Tensor pad_rows4(const torch::Tensor &x) {
+    if (row_padded(x)) return x;
+    if (!x.is_cuda() || x.dim() != 2 || x.size(1) % 4 == 0 || x.size(0) == 0) return x.contiguous();
+    const int64_t F = x.size(1);
+    auto v = torch::empty({x.size(0), (F + 3) / 4 * 4}, fopts(x)).narrow(1, 0, F);
+    v.copy_(x);
+    return v;
+}
+
+// an [nrows, F] output with x's row padding
+torch::Tensor rows_like(const torch::Tensor &x, int64_t nrows) {
+    if (row_padded(x)) return torch::empty({nrows, x.stride(0)}, fopts(x)).narrow(1, 0, x.size(1));
+    return torch::empty({nrows, x.size(1)}, fopts(x));
+}
+
 torch::Tensor row_sum_impl(const torch::Tensor &offsets, const torch::Tensor &cols,
                            const torch::Tensor &v, const torch::Tensor &bounds, int64_t nrows,
                            int64_t segments, float eps) {
@@ -192,7 +221,8 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
                         const torch::Tensor *src_scale, const torch::Tensor *dst_scale,
                         int64_t nsamples, int64_t ra, int64_t rb) {
     CsrView cv = view(offsets, cols, vals, bounds, segments, val_heads);
-    auto x = X.contiguous();
+    const bool padded = row_padded(X);
+    auto x = padded ? X : X.contiguous();
     check_dev(x, torch::kFloat, "input_dense");
     const int64_t nrows = cv.c.n_rows;
     // reference: dcols = input_dense.numel() / nrows (cuda.h:453-454)
@@ -203,7 +233,8 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
         cv.c.split = &sp->plan;
     }
     cv.c.n_cols = dcols ? x.numel() / dcols : 0;
-    auto out = torch::empty({nrows, dcols}, fopts(X));
+    auto out = padded ? rows_like(x, nrows) : torch::empty({nrows, dcols}, fopts(X));
+    const int64_t ldx = padded ? x.stride(0) : dcols, ldy = padded ? out.stride(0) : dcols;
     const float *ss = nullptr, *ds = nullptr;
     torch::Tensor ssc, dsc;
     if (src_scale) {
@@ -220,7 +251,7 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
     check_on(x, offsets, "input_dense");
     if (ss) check_on(ssc, offsets, "src_scale");
     if (ds) check_on(dsc, offsets, "dst_scale");
-    check(be(offsets).spmm(&cv.c, x.data_ptr<float>(), dcols, out.data_ptr<float>(), dcols,
+    check(be(offsets).spmm(&cv.c, x.data_ptr<float>(), ldx, out.data_ptr<float>(), ldy,
                            (int32_t)dcols, ss, ds, flags, (int32_t)nsamples, (int32_t)ra,
                            (int32_t)rb, stream_of(offsets)),
           "gala_spmm_f32");
@@ -231,6 +262,7 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
 
 // ---- split plans ----------------------------------------------------------------------
 void SplitState::ensure_workspace(int64_t F) {
+    F = (F + 3) / 4 * 4;  // chunk rows hold whole float4 vectors (padded rows included)
     if (plan.ws_cols >= F) return;
     ws = torch::empty({std::max<int64_t>(plan.n_chunks, 1) * F},
                       torch::TensorOptions().dtype(torch::kFloat).device(rows.device()));
@@ -596,11 +628,14 @@ struct GatGrads {
 // kernel, and is either recomputed again by the backward kernel (REF on one pattern) or
 // formed here for the other paths.
 GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tensor &x,
-                      const torch::Tensor &alpha, const torch::Tensor &dY, int64_t li,
+                      const torch::Tensor &alpha, const torch::Tensor &dY_in, int64_t li,
                       double slope, int64_t mode, int heads, const torch::Tensor &wR,
                       const torch::Tensor &bR) {
     Slot fw = slot(2 * li), bw = slot(2 * li + 1);
     const int64_t nrows = fw.off.numel() / fw.segs - 1, F = x.size(1);
+    // one head: dY row-padded like x (the dX SpMM gathers it), strides passed through
+    const torch::Tensor dY = heads == 1 ? pad_rows4(dY_in) : dY_in.contiguous();
+    const int64_t ldx = x.stride(0), lddy = dY.stride(0);
     CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
     cf.c.n_cols = x.size(0);
     with_workspace(cf, fw.off, 3 * heads);  // hub-row partials of the backward
@@ -622,7 +657,7 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
         auto daL = torch::empty_like(l);
         check(be(fw.off).gat_bwd_attn(&cf.c, l.data_ptr<float>(), wR.data_ptr<float>(),
                                       bR.defined() ? bR.data_ptr<float>() : nullptr,
-                                      x.data_ptr<float>(), F, dY.data_ptr<float>(), F, (int32_t)F,
+                                      x.data_ptr<float>(), ldx, dY.data_ptr<float>(), lddy, (int32_t)F,
                                       (float)slope, alpha.data_ptr<float>(), daL.data_ptr<float>(),
                                       stream_of(fw.off)),
               "gala_gat_bwd_attn_f32");
@@ -637,7 +672,7 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
         auto daL = torch::empty_like(l);
         torch::Tensor dz = fixed ? torch::empty_like(alpha) : torch::Tensor();
         const int st = be(fw.off).gat_bwd(&cf.c, l.data_ptr<float>(), r.data_ptr<float>(),
-                                          x.data_ptr<float>(), F, dY.data_ptr<float>(), F,
+                                          x.data_ptr<float>(), ldx, dY.data_ptr<float>(), lddy,
                                           (int32_t)F, heads, (float)slope, (int32_t)mode,
                                           alpha.data_ptr<float>(),
                                           fixed ? dz.data_ptr<float>() : nullptr,
@@ -659,7 +694,7 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
     cp.c.n_cols = x.size(0);
     with_workspace(cp, ps.off, 2 * heads);
     auto dalpha = torch::empty_like(alpha);
-    check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), F, x.data_ptr<float>(), F,
+    check(be(ps.off).sddmm(&cp.c, dY.data_ptr<float>(), lddy, x.data_ptr<float>(), ldx,
                            (int32_t)F, heads, dalpha.data_ptr<float>(), stream_of(ps.off)),
           "gala_sddmm_dot_f32");
     auto ds = torch::empty_like(alpha);
@@ -692,22 +727,24 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
                                  torch::Tensor X, int64_t li, double slope, int64_t mode) {
         Slot s = slot(2 * li);
         CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
-        auto l = aL.contiguous(), r = aR.contiguous(), x = X.contiguous();
+        auto l = aL.contiguous(), r = aR.contiguous();
+        const int64_t nrows = cv.c.n_rows;
+        const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
+        auto x = heads == 1 ? pad_rows4(X) : X.contiguous();
         check_dev(l, torch::kFloat, "attn_l");
         check_dev(r, torch::kFloat, "attn_r");
         check_dev(x, torch::kFloat, "X");
-        const int64_t nrows = cv.c.n_rows, F = x.size(1);
-        const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
+        const int64_t F = x.size(1);
         cv.c.n_cols = x.size(0);
         with_workspace(cv, s.off, F + 2 * heads);  // hub-row partials: acc[F], m[H], sum[H]
-        auto Y = torch::empty({nrows, F}, fopts(x));
+        auto Y = rows_like(x, nrows);
         auto alpha = torch::empty({s.cols.numel() * heads}, fopts(x));
         check_on(l, s.off, "attn_l");
         check_on(r, s.off, "attn_r");
         check_on(x, s.off, "X");
         check(be(s.off).gat_fwd(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
-                                F, (int32_t)F, heads, (float)slope, (int32_t)mode,
-                                Y.data_ptr<float>(), F, alpha.data_ptr<float>(), stream_of(s.off)),
+                                x.stride(0), (int32_t)F, heads, (float)slope, (int32_t)mode,
+                                Y.data_ptr<float>(), Y.stride(0), alpha.data_ptr<float>(), stream_of(s.off)),
               "gala_gat_fwd_f32");
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
@@ -719,7 +756,7 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         auto l = sv[0], r = sv[1], x = sv[2], alpha = sv[3];
-        GatGrads g = gat_backward(l, r, x, alpha, grad_outputs[0].contiguous(),
+        GatGrads g = gat_backward(l, r, x, alpha, grad_outputs[0],
                                   ctx->saved_data["li"].toInt(),
                                   ctx->saved_data["slope"].toDouble(),
                                   ctx->saved_data["mode"].toInt(),
@@ -740,7 +777,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
                                  int64_t mode) {
         Slot s = slot(2 * li);
         CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
-        auto l = aL.contiguous(), x = X.contiguous(), w = wR.contiguous();
+        auto l = aL.contiguous(), x = pad_rows4(X), w = wR.contiguous();
         torch::Tensor b = bR.defined() && bR.numel() > 0 ? bR.contiguous() : torch::Tensor();
         check_dev(l, torch::kFloat, "attn_l");
         check_dev(x, torch::kFloat, "X");
@@ -753,12 +790,12 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         if (b.defined()) check_on(b, s.off, "attn_r bias");
         cv.c.n_cols = x.size(0);
         with_workspace(cv, s.off, F + 2);
-        auto Y = torch::empty({nrows, F}, fopts(x));
+        auto Y = rows_like(x, nrows);
         auto alpha = torch::empty({s.cols.numel()}, fopts(x));
         check(be(s.off).gat_fwd_attn(&cv.c, l.data_ptr<float>(), w.data_ptr<float>(),
                                      b.defined() ? b.data_ptr<float>() : nullptr,
-                                     x.data_ptr<float>(), F, (int32_t)F, (float)slope,
-                                     (int32_t)mode, Y.data_ptr<float>(), F,
+                                     x.data_ptr<float>(), x.stride(0), (int32_t)F, (float)slope,
+                                     (int32_t)mode, Y.data_ptr<float>(), Y.stride(0),
                                      alpha.data_ptr<float>(), stream_of(s.off)),
               "gala_gat_fwd_attn_f32");
         ctx->saved_data["li"] = li;
@@ -773,7 +810,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         auto l = sv[0], x = sv[1], w = sv[2], alpha = sv[4];
         const bool has_bias = ctx->saved_data["has_bias"].toBool();
         torch::Tensor b = has_bias ? sv[3] : torch::Tensor();
-        GatGrads g = gat_backward(l, {}, x, alpha, grad_outputs[0].contiguous(),
+        GatGrads g = gat_backward(l, {}, x, alpha, grad_outputs[0],
                                   ctx->saved_data["li"].toInt(),
                                   ctx->saved_data["slope"].toDouble(),
                                   ctx->saved_data["mode"].toInt(), 1, w, b);
@@ -786,7 +823,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         const int64_t wsb = B.dense_ws(N, F, 1);
         TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
         auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(x));
-        check(B.dense_grad(N, F, 1, x.data_ptr<float>(), F, daR.data_ptr<float>(), 1,
+        check(B.dense_grad(N, F, 1, x.data_ptr<float>(), x.stride(0), daR.data_ptr<float>(), 1,
                            dW.data_ptr<float>(), db.data_ptr<float>(), 0, ws.data_ptr<float>(),
                            wsb, stream_of(x)),
               "gala_dense_grad_f32");

@@ -519,3 +519,81 @@ def test_dense_grad_strided_accumulate_and_no_bias():
     dW = dev(W0)
     ops.dense_grad(dev(X), dev(dY), bias=False, dW=dW, accumulate=True)
     np.testing.assert_allclose(host(dW), W0 + dY.astype(np.float64).T @ X, atol=2e-4, rtol=1e-5)
+
+
+def _padded(a, F, fill):
+    """[N, F] view of an [N, F rounded up to 4] buffer whose padding holds `fill`."""
+    Fp = (F + 3) // 4 * 4
+    buf = torch.full((a.shape[0], Fp), fill, device=DEV)
+    buf[:, :F] = dev(a)
+    return buf, buf[:, :F]
+
+
+@pytest.mark.parametrize("F", [3, 7, 33, 45, 47, 62])
+@pytest.mark.parametrize("hubs", [False, True])
+def test_padded_rows_float4_path(F, hubs):
+    """Row-padded operands (row stride F rounded up to 4, padding = NaN) take the float4
+    path with a partial last vector: SpMM (plain and weighted) stays bit-exact, the GAT
+    forward / backward (also with attention recompute) and SDDMM stay within TOL, and the
+    output padding is never written."""
+    g = powerlaw()
+    og = to_oracle(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if hubs:
+        dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+        assert dg.split_rows > 10
+    X = features(g.n_cols, F, seed=71)
+    _, Xp = _padded(X, F, float("nan"))
+    ybuf, Yp = _padded(np.zeros((g.n_rows, F), np.float32), F, 7.0)
+    # bit-identical to the unpadded (narrower-vector) launch on the same plan; that one is
+    # bit-exact vs the oracle without hub chunks, a reordered sum with them
+    def check(Y, val=None):
+        if hubs:
+            assert_reordered_sum(Y, g, X, val)
+        else:
+            np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g, val), X))
+    ops.spmm(dg, Xp, out=Yp)
+    np.testing.assert_array_equal(host(Yp), host(ops.spmm(dg, dev(X))))
+    check(host(Yp))
+    val = edge_values(g.nnz, seed=72)
+    gw = dg.with_values(dev(val))
+    ops.spmm(gw, Xp, out=Yp)
+    np.testing.assert_array_equal(host(Yp), host(ops.spmm(gw, dev(X))))
+    check(host(Yp), val)
+    assert bool(torch.all(ybuf[:, F:] == 7.0))
+    for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+        aL = features(g.n_rows, 1, seed=73)
+        aR = features(g.n_cols, 1, seed=74)
+        Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=1, slope=0.2, mode=mode)
+        Y, al = ops.gat_fwd(dg, dev(aL), dev(aR), Xp, slope=0.2, mode=mode, want_alpha=True)
+        assert Y.stride(0) == (F + 3) // 4 * 4
+        np.testing.assert_allclose(host(al), al_ref, **TOL)
+        np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+        dY = features(g.n_rows, F, seed=75)
+        _, dYp = _padded(dY, F, float("nan"))
+        dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=1, slope=0.2, mode=mode)
+        daL, dz = ops.gat_bwd(dg, dev(aL), dev(aR), Xp, dYp, dev(al_ref), slope=0.2, mode=mode)
+        np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+        if mode == _abi.GALA_SOFTMAX_FIXED:
+            np.testing.assert_allclose(host(dz), dz_ref, **TOL)
+        wR = features(1, F, seed=76).ravel() * 0.5
+        bR = np.array([0.1], np.float32)
+        aR2 = (X.astype(np.float64) @ wR.astype(np.float64) + 0.1).astype(np.float32)
+        Y2_ref, al2_ref = orc.gat_fwd(og, aL, aR2, X, heads=1, slope=0.2, mode=mode)
+        Y2, al2 = ops.gat_fwd_attn(dg, dev(aL), dev(wR), dev(bR), Xp, slope=0.2, mode=mode, want_alpha=True)
+        np.testing.assert_allclose(host(al2), al2_ref, **TOL)
+        np.testing.assert_allclose(host(Y2), Y2_ref, **TOL)
+        if mode == _abi.GALA_SOFTMAX_REF:
+            _, daL2_ref = orc.gat_bwd(og, aL, aR2, X, dY, al2_ref, heads=1, slope=0.2, mode=mode)
+            daL2 = ops.gat_bwd_attn(dg, dev(aL), dev(wR), dev(bR), Xp, dYp, dev(al2_ref), slope=0.2)
+            np.testing.assert_allclose(host(daL2), daL2_ref, **TOL)
+    A = features(g.n_rows, F, seed=77)
+    _, Ap = _padded(A, F, float("nan"))
+    np.testing.assert_allclose(host(ops.sddmm(dg, Ap, Xp)), orc.sddmm(og, A, X), **TOL)
+
+
+def test_pad_rows_helper():
+    X = torch.arange(2 * 47, dtype=torch.float32, device=DEV).reshape(2, 47)
+    P = ops.pad_rows(X)
+    assert P.shape == (2, 47) and P.stride(0) == 48 and torch.equal(P, X)
+    assert ops.pad_rows(P) is P

@@ -1,0 +1,6 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+for p in gat_products gcn_products; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/e2e_$p -o run -- $R/gala-gnn-acceleration-language_amd/progs/$p/gala_prog --synthetic --iters 20 > $R/gpurun_out/e2e_$p.log 2>&1 || exit $?
+done

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--F", default="8,16,32,64,128")
     ap.add_argument("--ops", default="spmm,spmm_scaled,degree,sddvv,softmax,sddmm,gat")
     ap.add_argument("--sort-rows", action="store_true")
+    ap.add_argument("--pad", action="store_true", help="row-padded X / Y (stride F rounded up to 4)")
     args = ap.parse_args()
     t0 = time.time()
     hg = layout.gen_graph(args.graph, args.n, args.u, seed=42)
@@ -60,7 +61,9 @@ def main():
     norm = ops.degree(dg, power=-0.5)
     for F in [int(f) for f in args.F.split(",")]:
         X = torch.rand((N, F), device="cuda") * 2 - 1
-        Y = torch.empty_like(X)
+        if args.pad:
+            X = ops.pad_rows(X)
+        Y = ops.spmm(dg, X)
         base = 4 * (N + 1) + 4 * E + 8 * N * F
         if "spmm" in todo:
             ms = timeit(lambda: ops.spmm(dg, X, out=Y))
