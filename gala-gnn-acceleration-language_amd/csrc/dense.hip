@@ -6,156 +6,286 @@
 // contraction runs over the N rows.  Measured on the Products GCN program, torch's bias
 // reduction over dim 0 takes 18.6 ms and the weight GEMM 3.3 ms (profiles/r01_e2e_*), for
 // 1.3 GB of input that HBM streams in ~0.2 ms.  Here the rows are split into P chunks
-// (split-K): every workgroup accumulates one (m, k) tile (64x64, or 32x128 for narrow M)
-// of one chunk in registers (4x4 per lane, both operands staged through LDS 32 rows at a
-// time, the next step prefetched into registers), writes the partial tile, and a second
-// kernel sums the P partials in a fixed order.  Deterministic: the same
-// shapes always use the same chunking and summation order.
+// (split-K) and a second kernel sums the P partials in a fixed order:
+//  * k_tn_mfma: every wave owns a (32 WM) x (32 WK) tile of dW for one row chunk and runs
+//    it on the exact-f32 matrix cores (v_mfma_f32_32x32x2_f32: each instruction takes two
+//    rows, operands straight from global memory -- lane l reads dY[n][m0 + l%32] and
+//    X[n][k0 + l%32] of row n = 2s + l/32, both 128-B coalesced -- no LDS); consecutive
+//    waves share a chunk, so a row's bytes are fetched once and re-read from cache;
+//  * k_tn_skinny: M <= 4 (the attention Linears, out = 1), lanes over K, see below.
+// Deterministic: the same shapes always use the same chunking and summation order (an
+// f32 MFMA is bit-for-bit a row-ordered fmaf chain).
 #include "gala_internal.h"
 
 namespace gala {
 namespace {
 
-constexpr int kRows = 32;    // rows staged in LDS per step
-constexpr int kPad = 4;
-constexpr int kRedLanes = 64; // lanes (one wave) per output in the partial-sum reduction
+constexpr int kStep = 2;      // rows per MFMA (the K of 32x32x2)
+constexpr int kInFlight = 4;  // MFMA steps whose operand loads are issued together
 
-// One TK x TM (k, m) tile of one row chunk.  Lane layout: (TK/4) x (TM/4) = 256 lanes,
-// each owning a 4x4 register block; the next 32-row step is loaded into registers while
-// the current one is consumed from LDS.
-template <int TK, int TM>
-__global__ __launch_bounds__(kBlock) void k_tn_partial(int64_t N, int32_t K, int32_t M,
-                                                       const float *__restrict__ X, int64_t ldx,
-                                                       const float *__restrict__ dY, int64_t ldy,
-                                                       int64_t rows_per_chunk,
-                                                       float *__restrict__ part,
-                                                       float *__restrict__ bpart) {
-    static_assert((TK / 4) * (TM / 4) == kBlock, "one 4x4 block per lane");
-    constexpr int LX = kRows * TK / kBlock, LY = kRows * TM / kBlock;  // staged values per lane
-    __shared__ float sx[kRows][TK + kPad];
-    __shared__ float sy[kRows][TM + kPad];
-    const int t = threadIdx.x;
-    const int tk = (t % (TK / 4)) * 4, tm = (t / (TK / 4)) * 4;
-    const int k0 = blockIdx.x * TK, m0 = blockIdx.y * TM;
-    const int64_t p = blockIdx.z;
-    const int64_t r0 = p * rows_per_chunk;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int WM, int WK>
+__global__ __launch_bounds__(kBlock) void k_tn_mfma(int64_t N, int32_t K, int32_t M,
+                                                    const float *__restrict__ X, int64_t ldx,
+                                                    const float *__restrict__ dY, int64_t ldy,
+                                                    int64_t rows_per_chunk, int32_t tiles_k,
+                                                    int32_t n_tg, int64_t n_work,
+                                                    float *__restrict__ part,
+                                                    float *__restrict__ bpart) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    if (w >= n_work) return;  // whole waves; no block-level synchronisation
+    const int64_t chunk = w / n_tg;
+    const int tg = (int)(w % n_tg);
+    const int m0 = (tg / tiles_k) * 32 * WM, k0 = (tg % tiles_k) * 32 * WK;
+    const int64_t r0 = chunk * rows_per_chunk;
     const int64_t r1 = r0 + rows_per_chunk < N ? r0 + rows_per_chunk : N;
-    float acc[4][4] = {};
-    float bacc[4] = {};
-    float rx[LX], ry[LY];
-    auto fetch = [&](int64_t rb) {
+    const int li = lane & 31, lh = lane >> 5;
+    bool mv[WM], kv[WK];
+    int64_t mo[WM], ko[WK];
 #pragma unroll
-        for (int i = 0; i < LX; ++i) {
-            const int e = t + i * kBlock, r = e / TK, c = e % TK;
-            const int64_t row = rb + r;
-            rx[i] = (row < r1 && k0 + c < K) ? X[row * ldx + k0 + c] : 0.0f;
-        }
+    for (int a = 0; a < WM; ++a) {
+        const int m = m0 + a * 32 + li;
+        mv[a] = m < M;
+        mo[a] = mv[a] ? m : 0;
+    }
 #pragma unroll
-        for (int i = 0; i < LY; ++i) {
-            const int e = t + i * kBlock, r = e / TM, c = e % TM;
-            const int64_t row = rb + r;
-            ry[i] = (row < r1 && m0 + c < M) ? dY[row * ldy + m0 + c] : 0.0f;
+    for (int b = 0; b < WK; ++b) {
+        const int k = k0 + b * 32 + li;
+        kv[b] = k < K;
+        ko[b] = kv[b] ? k : 0;
+    }
+    f32x16 acc[WM][WK];
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WK; ++b) acc[a][b] = f32x16(0.0f);
+    float bacc[WM] = {};
+    // software-pipelined: the next kInFlight steps' operands are loaded while the current
+    // ones feed the matrix cores
+    float av[kInFlight][WM], bv[kInFlight][WK];
+    auto load = [&](int64_t rb) {
+#pragma unroll
+        for (int u = 0; u < kInFlight; ++u) {
+            const int64_t n = rb + kStep * u + lh;
+            const bool ok = n < r1;
+#pragma unroll
+            for (int a = 0; a < WM; ++a) av[u][a] = (ok && mv[a]) ? dY[n * ldy + mo[a]] : 0.0f;
+#pragma unroll
+            for (int b = 0; b < WK; ++b) bv[u][b] = (ok && kv[b]) ? X[n * ldx + ko[b]] : 0.0f;
         }
     };
-    if (r0 < r1) fetch(r0);
-    for (int64_t rb = r0; rb < r1; rb += kRows) {
+    // (2 x 2 wave tiles are matrix-core bound and keep their occupancy instead)
+    constexpr bool kPipe = WM * WK < 4;
+    if (kPipe && r0 < r1) load(r0);
+    for (int64_t rb = r0; rb < r1; rb += kStep * kInFlight) {
+        if (!kPipe) load(rb);
+        float ca[kInFlight][WM], cb[kInFlight][WK];
 #pragma unroll
-        for (int i = 0; i < LX; ++i) {
-            const int e = t + i * kBlock;
-            sx[e / TK][e % TK] = rx[i];
+        for (int u = 0; u < kInFlight; ++u) {
+#pragma unroll
+            for (int a = 0; a < WM; ++a) ca[u][a] = av[u][a];
+#pragma unroll
+            for (int b = 0; b < WK; ++b) cb[u][b] = bv[u][b];
         }
+        if (kPipe && rb + kStep * kInFlight < r1) load(rb + kStep * kInFlight);
 #pragma unroll
-        for (int i = 0; i < LY; ++i) {
-            const int e = t + i * kBlock;
-            sy[e / TM][e % TM] = ry[i];
-        }
-        __syncthreads();
-        if (rb + kRows < r1) fetch(rb + kRows);  // in flight during the FMAs below
-#pragma unroll 8
-        for (int r = 0; r < kRows; ++r) {
-            const float4 xv = *reinterpret_cast<const float4 *>(&sx[r][tk]);
-            const float4 yv = *reinterpret_cast<const float4 *>(&sy[r][tm]);
-            const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
-            const float ys[4] = {yv.x, yv.y, yv.z, yv.w};
+        for (int u = 0; u < kInFlight; ++u) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < WM; ++a) {
+                bacc[a] += ca[u][a];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(ys[i], xs[j], acc[i][j]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) bacc[i] += ys[i];
-        }
-        __syncthreads();
-    }
-    // partial tile [M][K] of chunk p
-    float *out = part + p * (int64_t)M * K;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = m0 + tm + i;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int k = k0 + tk + j;
-            if (k < K) out[(int64_t)m * K + k] = acc[i][j];
+                for (int b = 0; b < WK; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[u][a], cb[u][b], acc[a][b], 0, 0, 0);
+            }
         }
     }
-    if (bpart && blockIdx.x == 0 && tk == 0) {
+    // C/D layout: column (k) = lane % 32, row (m) = (r & 3) + 8 (r >> 2) + 4 (lane / 32)
+    float *out = part + chunk * (int64_t)M * K;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (m0 + tm + i < M) bpart[p * M + m0 + tm + i] = bacc[i];
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int b = 0; b < WK; ++b) {
+            const int k = k0 + b * 32 + li;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m < M && k < K) out[(int64_t)m * K + k] = acc[a][b][r];
+            }
+        }
+    if (bpart && k0 == 0) {  // db: the two row parities (lane halves) of the k0 = 0 tile
+#pragma unroll
+        for (int a = 0; a < WM; ++a) {
+            const float s2 = bacc[a] + __shfl_xor(bacc[a], 32, kWave);
+            if (lh == 0 && mv[a]) bpart[chunk * M + mo[a]] = s2;
+        }
     }
 }
 
-// out[i] (+)= sum_p part[p][i]: one wave per output; lane g sums the residue class
-// p = g mod 64 in order (8 loads in flight), then a fixed xor butterfly adds the 64 lane
-// sums (deterministic for given shapes).  One wave per output keeps the ~1000 partials
-// of a chunk-split contraction from serialising in a handful of lanes.
-__global__ __launch_bounds__(kBlock) void k_tn_reduce(int64_t count, int64_t P,
-                                                      const float *__restrict__ part,
-                                                      float *__restrict__ out, int accum) {
-    constexpr int kOut = kBlock / kRedLanes;
-    const int g = threadIdx.x % kRedLanes;
-    const int64_t i = (int64_t)blockIdx.x * kOut + threadIdx.x / kRedLanes;
-    if (i >= count) return;  // whole waves exit together
+// Narrow outputs (M <= 4: the attention Linears, out = 1): a (k, m) tile would leave most
+// lanes idle and the kernel latency-bound.  Here KL lanes span a row's K columns (CH per
+// lane past 64), a wave covers 64/KL rows per step with 4 steps' loads in flight, and every
+// lane keeps M x CH accumulators; the block's lanes and waves are then summed through LDS
+// in a fixed order into the chunk's partial [M][K] (+ [M] bias) -- same partial layout and
+// reduction kernel as the tiles.
+template <int MM, int KL, int CH>
+__global__ __launch_bounds__(kBlock) void k_tn_skinny(int64_t N, int32_t K, int32_t M,
+                                                      const float *__restrict__ X, int64_t ldx,
+                                                      const float *__restrict__ dY, int64_t ldy,
+                                                      int64_t rows_per_chunk,
+                                                      float *__restrict__ part,
+                                                      float *__restrict__ bpart) {
+    constexpr int RPW = kWave / KL;              // rows per wave step
+    constexpr int RPB = RPW * (kBlock / kWave);  // rows per block step
+    constexpr int U = 4;                         // block steps in flight
+    __shared__ float red[RPB][MM][KL * CH + 1];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int kl = lane % KL, rs = wv * RPW + lane / KL;
+    const int64_t p = blockIdx.x;
+    const int64_t r0 = p * rows_per_chunk;
+    const int64_t r1 = r0 + rows_per_chunk < N ? r0 + rows_per_chunk : N;
+    float acc[MM][CH] = {};
+    float bacc[MM] = {};
+    for (int64_t rb = r0 + rs; rb < r1; rb += (int64_t)U * RPB) {
+        float x[U][CH], y[U][MM];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = rb + (int64_t)u * RPB;
+            const bool ok = row < r1;
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int k = j * KL + kl;
+                x[u][j] = (ok && k < K) ? X[row * ldx + k] : 0.0f;
+            }
+#pragma unroll
+            for (int m = 0; m < MM; ++m) y[u][m] = (ok && m < M) ? dY[row * ldy + m] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+#pragma unroll
+                for (int j = 0; j < CH; ++j) acc[m][j] = fmaf(y[u][m], x[u][j], acc[m][j]);
+                bacc[m] += y[u][m];
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int j = 0; j < CH; ++j) red[rs][m][j * KL + kl] = acc[m][j];
+    __syncthreads();
+    // thread t sums output (m, k) = t over the RPB row slots in order
+    for (int o = threadIdx.x; o < M * K; o += kBlock) {
+        const int m = o / K, k = o % K;
+        float s = 0.0f;
+        for (int r = 0; r < RPB; ++r) s += red[r][m][k];
+        part[p * (int64_t)M * K + o] = s;
+    }
+    if (bpart) {
+        __syncthreads();
+        if (kl == 0)
+#pragma unroll
+            for (int m = 0; m < MM; ++m) red[rs][m][0] = bacc[m];
+        __syncthreads();
+        if (threadIdx.x < M) {
+            float s = 0.0f;
+            for (int r = 0; r < RPB; ++r) s += red[r][threadIdx.x][0];
+            bpart[p * M + threadIdx.x] = s;
+        }
+    }
+}
+
+// out[i] (+)= sum_p part[p][i] in two coalesced passes (threads along i, so a block reads
+// 1 KB of one partial row per load): pass A sums runs of kRedChain partials into
+// part2[q][i], pass B sums the runs in order (pass A is skipped when P <= kRedChain).
+// Deterministic for given shapes.
+constexpr int kRedChain = 64;
+
+__device__ __forceinline__ float sum_strided(const float *__restrict__ a, int64_t stride,
+                                             int64_t n) {
     float s = 0.0f;
-    int64_t p = g;
-    for (; p + 7 * kRedLanes < P; p += 8 * kRedLanes) {
+    int64_t j = 0;
+    for (; j + 8 <= n; j += 8) {
         float v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = part[(p + k * kRedLanes) * count + i];
+        for (int k = 0; k < 8; ++k) v[k] = a[(j + k) * stride];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s += v[k];
     }
-    for (; p < P; p += kRedLanes) s += part[p * count + i];
-#pragma unroll
-    for (int o = kRedLanes / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (g == 0) out[i] = accum ? out[i] + s : s;
+    for (; j < n; ++j) s += a[j * stride];
+    return s;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tn_reduce_a(int64_t count, int64_t P,
+                                                        const float *__restrict__ part,
+                                                        float *__restrict__ part2) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const int64_t p0 = (int64_t)blockIdx.y * kRedChain;
+    const int64_t n = P - p0 < kRedChain ? P - p0 : kRedChain;
+    part2[(int64_t)blockIdx.y * count + i] = sum_strided(part + p0 * count + i, count, n);
+}
+
+__global__ __launch_bounds__(kBlock) void k_tn_reduce_b(int64_t count, int64_t Q,
+                                                        const float *__restrict__ part2,
+                                                        float *__restrict__ out, int accum) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const float s = sum_strided(part2 + i, count, Q);
+    out[i] = accum ? out[i] + s : s;
 }
 
 struct Plan {
-    int tk, tm;  // tile shape
-    int tiles_k, tiles_m;
+    bool skinny;      // M <= 4 and K <= 256: k_tn_skinny; else k_tn_mfma
+    int wm, wk;       // MFMA wave tile: (32 wm) x (32 wk)
+    int tiles_k, n_tg;  // wave tiles along K, per chunk
     int64_t P, rows_per_chunk;
 };
 
+constexpr int kSkinnyM = 4, kSkinnyK = 256;
+
 Plan plan_for(int64_t N, int32_t K, int32_t M) {
-    Plan pl;
-    // narrow outputs (M <= 32, e.g. hidden 32 or 16) take a 128 x 32 tile: no idle lanes
-    pl.tm = M <= 32 ? 32 : 64;
-    pl.tk = M <= 32 ? 128 : 64;
-    pl.tiles_k = (K + pl.tk - 1) / pl.tk;
-    pl.tiles_m = (M + pl.tm - 1) / pl.tm;
-    const int64_t tiles = (int64_t)pl.tiles_k * pl.tiles_m;
-    // ~4 workgroups per CU in total, each chunk a multiple of the LDS step
-    int64_t P = (1024 + tiles - 1) / tiles;
-    const int64_t max_p = (N + kRows - 1) / kRows;
-    if (P > max_p) P = max_p;
-    if (P < 1) P = 1;
-    int64_t rpc = (N + P - 1) / P;
-    rpc = (rpc + kRows - 1) / kRows * kRows;
-    P = (N + rpc - 1) / rpc;
-    pl.P = P < 1 ? 1 : P;
-    pl.rows_per_chunk = rpc < kRows ? kRows : rpc;
+    Plan pl{};
+    pl.skinny = M <= kSkinnyM && K <= kSkinnyK;
+    int64_t target;  // chunks
+    int64_t align;   // rows per chunk: a multiple of the kernel's row step
+    if (pl.skinny) {  // ~4 blocks per CU, chunks of whole block steps (4 x 4 waves x rows)
+        pl.tiles_k = pl.n_tg = 1;
+        target = 1024;
+        align = 64;
+    } else {          // ~8192 waves (32 per CU), consecutive waves on one chunk
+        pl.wm = M > 32 ? 2 : 1;
+        pl.wk = K > 32 ? 2 : 1;
+        pl.tiles_k = (K + 32 * pl.wk - 1) / (32 * pl.wk);
+        pl.n_tg = pl.tiles_k * ((M + 32 * pl.wm - 1) / (32 * pl.wm));
+        target = (8192 + pl.n_tg - 1) / pl.n_tg;
+        align = kStep * kInFlight;
+    }
+    int64_t rpc = (N + target - 1) / target;
+    rpc = (rpc + align - 1) / align * align;
+    pl.rows_per_chunk = rpc < align ? align : rpc;
+    pl.P = (N + pl.rows_per_chunk - 1) / pl.rows_per_chunk;
+    if (pl.P < 1) pl.P = 1;
     return pl;
+}
+
+// runs of kRedChain partials summed by pass A (1: pass B alone)
+int64_t red_runs(int64_t P) { return P <= kRedChain ? 1 : (P + kRedChain - 1) / kRedChain; }
+
+int reduce_partials(int64_t count, int64_t P, const float *part, float *part2, float *out,
+                    int accum, hipStream_t hs) {
+    const unsigned gx = (unsigned)((count + kBlock - 1) / kBlock);
+    const float *src = part;
+    int64_t n = P;
+    if (P > kRedChain) {
+        hipLaunchKernelGGL(k_tn_reduce_a, dim3(gx, (unsigned)red_runs(P)), dim3(kBlock), 0, hs,
+                           count, P, part, part2);
+        src = part2;
+        n = red_runs(P);
+    }
+    hipLaunchKernelGGL(k_tn_reduce_b, dim3(gx), dim3(kBlock), 0, hs, count, n, src, out, accum);
+    return launch_status();
 }
 
 }  // namespace
@@ -167,7 +297,7 @@ extern "C" int64_t gala_dense_grad_workspace(int64_t n_rows, int32_t K, int32_t 
     if (n_rows < 0 || K < 0 || M < 0) return -1;
     if (n_rows == 0 || K == 0 || M == 0) return 0;
     const Plan pl = plan_for(n_rows, K, M);
-    return (int64_t)sizeof(float) * pl.P * ((int64_t)M * K + M);
+    return (int64_t)sizeof(float) * (pl.P + red_runs(pl.P)) * ((int64_t)M * K + M);
 }
 
 extern "C" int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const float *X,
@@ -189,26 +319,45 @@ extern "C" int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const f
     }
     if (!X || !dY || !workspace) return GALA_ERR_INVALID_ARG;
     const Plan pl = plan_for(n_rows, K, M);
-    if (workspace_bytes < (int64_t)sizeof(float) * pl.P * ((int64_t)M * K + M))
+    const int64_t Q = red_runs(pl.P);
+    if (workspace_bytes < (int64_t)sizeof(float) * (pl.P + Q) * ((int64_t)M * K + M))
         return GALA_ERR_INVALID_ARG;
     float *part = (float *)workspace;
     float *bpart = part + pl.P * (int64_t)M * K;
-    const dim3 grid(pl.tiles_k, pl.tiles_m, (unsigned)pl.P);
-    if (pl.tm == 32)
-        hipLaunchKernelGGL((k_tn_partial<128, 32>), grid, dim3(kBlock), 0, hs, n_rows, K, M, X, ldx,
-                           dY, ldy, pl.rows_per_chunk, part, db ? bpart : nullptr);
-    else
-        hipLaunchKernelGGL((k_tn_partial<64, 64>), grid, dim3(kBlock), 0, hs, n_rows, K, M, X, ldx,
-                           dY, ldy, pl.rows_per_chunk, part, db ? bpart : nullptr);
+    float *part2 = bpart + pl.P * (int64_t)M;
+    float *bpart2 = part2 + Q * (int64_t)M * K;
+    if (pl.skinny) {
+        // KL lanes per row: the smallest power of two covering K, at most 64 (CH past it)
+        int kl = 1;
+        while (kl < K && kl < 64) kl <<= 1;
+        const int ch = (K + 63) / 64;
+        const dim3 g1((unsigned)pl.P);
+        float *bp = db ? bpart : nullptr;
+#define GALA_SK(KL, CH) hipLaunchKernelGGL((k_tn_skinny<kSkinnyM, KL, CH>), g1, dim3(kBlock), 0, hs, n_rows, \
+                                           K, M, X, ldx, dY, ldy, pl.rows_per_chunk, part, bp)
+        if (kl <= 8) GALA_SK(8, 1);
+        else if (kl == 16) GALA_SK(16, 1);
+        else if (kl == 32) GALA_SK(32, 1);
+        else if (ch == 1) GALA_SK(64, 1);
+        else if (ch == 2) GALA_SK(64, 2);
+        else if (ch == 3) GALA_SK(64, 3);
+        else GALA_SK(64, 4);
+#undef GALA_SK
+    } else {
+        const int64_t n_work = pl.P * pl.n_tg;
+        const dim3 g((unsigned)((n_work + kBlock / kWave - 1) / (kBlock / kWave)));
+        float *bp = db ? bpart : nullptr;
+#define GALA_MF(WM, WK) hipLaunchKernelGGL((k_tn_mfma<WM, WK>), g, dim3(kBlock), 0, hs, n_rows, K, M, X, ldx, \
+                                           dY, ldy, pl.rows_per_chunk, pl.tiles_k, pl.n_tg, n_work, part, bp)
+        if (pl.wm == 1 && pl.wk == 1) GALA_MF(1, 1);
+        else if (pl.wm == 1) GALA_MF(1, 2);
+        else if (pl.wk == 1) GALA_MF(2, 1);
+        else GALA_MF(2, 2);
+#undef GALA_MF
+    }
     int st = launch_status();
     if (st) return st;
-    const int64_t cw = (int64_t)M * K;
-    constexpr int kOut = kBlock / kRedLanes;
-    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((cw + kOut - 1) / kOut)), dim3(kBlock), 0,
-                       hs, cw, pl.P, part, dW, accumulate);
-    st = launch_status();
+    st = reduce_partials((int64_t)M * K, pl.P, part, part2, dW, accumulate, hs);
     if (st || !db) return st;
-    hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((M + kOut - 1) / kOut)), dim3(kBlock), 0,
-                       hs, (int64_t)M, pl.P, bpart, db, accumulate);
-    return launch_status();
+    return reduce_partials((int64_t)M, pl.P, bpart, bpart2, db, accumulate, hs);
 }

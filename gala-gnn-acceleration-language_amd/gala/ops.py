@@ -268,8 +268,9 @@ def edge_permute(perm, src, heads=1):
 
 def dense_grad(X, dY, bias=True, dW=None, db=None, accumulate=False):
     """FFN weight / bias gradients dW = dY^T X [M, K], db = dY.sum(0) (gala_dense_grad_f32)."""
-    X = X.contiguous()
-    dY = dY.contiguous()
+    # row strides pass through (row-padded views included); columns must be unit-stride
+    X = X if X.stride(1) == 1 else X.contiguous()
+    dY = dY if dY.stride(1) == 1 else dY.contiguous()
     N, K = X.shape
     M = dY.shape[1]
     if dW is None:
@@ -278,6 +279,7 @@ def dense_grad(X, dY, bias=True, dW=None, db=None, accumulate=False):
         db = torch.empty(M, device=X.device, dtype=torch.float32)
     wsb = _abi.lib().gala_dense_grad_workspace(N, K, M)
     ws = torch.empty(max(wsb // 4, 1), device=X.device, dtype=torch.float32)
-    _abi.call("gala_dense_grad_f32", N, K, M, _dp(X), K, _dp(dY), M, _dp(dW),
+    ldx, ldy = max(X.stride(0), K), max(dY.stride(0), M)  # (empty tensors report any stride)
+    _abi.call("gala_dense_grad_f32", N, K, M, _dp(X), ldx, _dp(dY), ldy, _dp(dW),
               _dp(db) if bias else None, int(accumulate), _dp(ws), wsb, _stream())
     return (dW, db) if bias else dW

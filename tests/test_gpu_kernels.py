@@ -493,7 +493,10 @@ def test_sddmm_split_hub_rows(F, heads):
 
 # ---- FFN gradients (gala_dense_grad_f32) ---------------------------------------------------
 @pytest.mark.parametrize("N,K,M", [(2708, 64, 32), (100000, 100, 32), (50000, 32, 47),
-                                   (20000, 602, 256), (33, 7, 1), (1, 1, 1), (0, 16, 8)])
+                                   (20000, 602, 256), (33, 7, 1), (1, 1, 1), (0, 16, 8),
+                                   # narrow outputs (k_tn_skinny): every KL / CH class
+                                   (100000, 32, 1), (100000, 47, 1), (70001, 5, 2), (3000, 16, 3),
+                                   (65537, 100, 4), (4099, 256, 1), (50, 129, 4), (0, 47, 1)])
 def test_dense_grad_matches_float64(N, K, M):
     """dW = dY^T X, db = sum_n dY: |err| <= 1e-5 * sum_n |dY||X| (fp32 accumulation bound)."""
     rng = np.random.default_rng(N + K + M)
@@ -519,6 +522,25 @@ def test_dense_grad_strided_accumulate_and_no_bias():
     dW = dev(W0)
     ops.dense_grad(dev(X), dev(dY), bias=False, dW=dW, accumulate=True)
     np.testing.assert_allclose(host(dW), W0 + dY.astype(np.float64).T @ X, atol=2e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("K,M", [(47, 1), (40, 12)])
+def test_dense_grad_row_strides(K, M):
+    """Row-padded / strided X and dY (NaN in the skipped columns) with accumulate."""
+    rng = np.random.default_rng(K + M)
+    N = 30000
+    X = rng.uniform(-1, 1, (N, K)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (N, M)).astype(np.float32)
+    Xb = torch.full((N, K + 5), float("nan"), device=DEV)
+    Xb[:, :K] = dev(X)
+    Yb = torch.full((N, M + 3), float("nan"), device=DEV)
+    Yb[:, :M] = dev(dY)
+    W0 = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    dW = dev(W0)
+    db = torch.zeros(M, device=DEV)
+    ops.dense_grad(Xb[:, :K], Yb[:, :M], dW=dW, db=db, accumulate=True)
+    np.testing.assert_allclose(host(dW), W0 + dY.astype(np.float64).T @ X, atol=2e-4, rtol=1e-5)
+    np.testing.assert_allclose(host(db), dY.astype(np.float64).sum(0), atol=1e-5 * N, rtol=1e-5)
 
 
 def _padded(a, F, fill):
