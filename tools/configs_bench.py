@@ -61,6 +61,17 @@ def gcn_step(name, hg, F, aggs=4):
             ops.spmm(dg, bufs[0], dst_scale=norm, out=dst)
             src = dst
     t = timeit(step)
+    # the same step replayed from one HIP graph (launch overhead off the timeline)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    tg = timeit(graph.replay)
+    emit(config=name, op=f"gcn_step_{aggs}_aggregations_hip_graph", ms=tg * 1e3, edges_per_s=aggs * E / tg)
     norm = ops.degree(dg, power=-0.5)
     tk = timeit(lambda: ops.spmm(dg, bufs[0], dst_scale=norm, out=bufs[1]), reps=20)
     alg = 4 * (N + 1) + 4 * E + 8 * N * F + 4 * N
