@@ -32,7 +32,8 @@ enum class Op {
     Add,            // a + b                                              (ADD_OP)
     // produced by the middle-end
     EdgeMul,        // w_e = a[row] * b[col] (sparse rewrite)             (AGGREGATE_EDGE_MUL_OP)
-    GcnAggregate,   // post * A (pre * x), fused ROW_BROADCAST/AGGREGATE chain
+    GcnAggregate,   // post * A (pre * x), fused ROW_BROADCAST/AGGREGATE chain; param 1:
+                    // x = relu(act * in[0]) first (in[3] = act | -1), the ReLU prologue
     GatAggregate,   // softmax(lrelu(aL[row] + aR[col])) weighted A x, fused
 };
 const char *op_name(Op op);
@@ -48,7 +49,7 @@ struct Value {
 
 struct Node {
     Op op;
-    std::vector<int> in;    // value ids; Aggregate: {x[, weights]}; GcnAggregate: {x, pre|-1, post|-1}
+    std::vector<int> in;    // value ids; Aggregate: {x[, weights]}; GcnAggregate: {x, pre|-1, post|-1[, act|-1]}
     int out = -1;
     double param = 0;       // Power exponent, LeakyRelu slope, ScaleEps initial eps
     int weight = -1;        // Ffn / ScaleEps: index into Module::weights

@@ -298,6 +298,31 @@ void fuse(Module &m) {
                               "aggregation" + (post >= 0 ? " + row-broadcast" : "") +
                               " -> gcn_aggregate");
     }
+    // GCN prologue: relu([act *] z) feeding only a GcnAggregate's (pre-scaled) input becomes
+    // one elementwise pass in front of the SpMM (pre * relu(act * z)); act must be a
+    // graph-invariant row vector (the layer's norm) -- its gradient is never needed
+    for (int i = 0; i < (int)m.nodes.size(); ++i) {
+        Node &agg = m.nodes[i];
+        if (agg.dead || agg.op != Op::GcnAggregate || agg.param != 0) continue;
+        const int x = agg.in[0];
+        const int ri = m.producer(x);
+        if (ri < 0 || m.nodes[ri].op != Op::Relu || m.uses(x).size() != 1 ||
+            m.nodes[ri].hoisted != agg.hoisted)
+            continue;
+        int z = m.nodes[ri].in[0], act = -1;
+        const int bi = m.producer(z);
+        if (bi >= 0 && m.nodes[bi].op == Op::RowBroadcast && m.uses(z).size() == 1 &&
+            m.nodes[bi].hoisted == agg.hoisted && m.values[m.nodes[bi].in[0]].invariant) {
+            act = m.nodes[bi].in[0];
+            z = m.nodes[bi].in[1];
+            m.nodes[bi].dead = true;
+        }
+        m.nodes[ri].dead = true;
+        agg.in = {z, agg.in[1], agg.in[2], act};
+        agg.param = 1;
+        m.notes.push_back(std::string("fuse: ") + (act >= 0 ? "row-broadcast + " : "") +
+                          "relu in front of gcn_aggregate -> one elementwise pass");
+    }
     // keep program order valid: a fused node must come after its inputs' producers
     for (int i = 0; i < (int)m.nodes.size(); ++i) {
         if (m.nodes[i].dead) continue;

@@ -169,6 +169,49 @@ extern "C" int gala_cpu_row_broadcast_f32(int64_t n_rows, int32_t F, const float
     return GALA_OK;
 }
 
+// torch.relu as its GPU kernel computes it (the HIP backend's relu_t): t > 0 ? t : +0, NaN passes
+static inline float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
+
+extern "C" int gala_cpu_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act,
+                                           const float *pre, const float *X, int64_t ldx,
+                                           float *Y, int64_t ldy, void *) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !Y) return GALA_ERR_INVALID_ARG;
+#pragma omp parallel for schedule(static, 1024)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const float a = act ? act[r] : 1.0f, b = pre ? pre[r] : 1.0f;
+        for (int32_t f = 0; f < F; ++f) {
+            float t = X[r * ldx + f];
+            if (act) t = a * t;
+            t = relu_t(t);
+            if (pre) t = b * t;
+            Y[r * ldy + f] = t;
+        }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_relu_scale_backward_f32(int64_t n_rows, int32_t F, const float *act,
+                                                const float *X, int64_t ldx, const float *G,
+                                                int64_t ldg, float *dX, int64_t lddx, void *) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldg < F || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !G || !dX) return GALA_ERR_INVALID_ARG;
+#pragma omp parallel for schedule(static, 1024)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const float a = act ? act[r] : 1.0f;
+        for (int32_t f = 0; f < F; ++f) {
+            float t = X[r * ldx + f];
+            if (act) t = a * t;
+            float d = relu_t(t) <= 0.0f ? 0.0f : G[r * ldg + f];
+            if (act) d = d * a;
+            dX[r * lddx + f] = d;
+        }
+    }
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col,
                                   int32_t heads, int32_t op, float slope, float *out_e, void *) {
     int st = check_csr(A);

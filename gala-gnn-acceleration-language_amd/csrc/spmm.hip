@@ -553,24 +553,124 @@ extern "C" int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int
     return launch_status();
 }
 
-// ---- ROW_BROADCAST: Y[r,:] = scale[r] * X[r,:] ----------------------------------------
+namespace gala {
+
+// ---- row-wise elementwise ops (ROW_BROADCAST and the GCN ReLU prologue) ----------------
+// Grid-stride over (row, vector) pairs with the row / column stepped incrementally (no
+// per-element 64-bit division).  A padded row's last vector (F % VEC != 0, strides padded
+// to VEC; checked on the host) computes on its padding and stores only the real columns.
 template <int VEC>
-__global__ __launch_bounds__(kBlock) void k_row_broadcast(int64_t n_rows, int32_t L,
-                                                          const float *scale, const float *X,
-                                                          int64_t ldx, float *Y, int64_t ldy) {
-    typedef typename VecT<VEC>::T V;
-    const int64_t total = n_rows * L;
-    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * kBlock) {
-        const int64_t r = t / L;
-        const int64_t c = (t - r * L) * VEC;
+__device__ __forceinline__ void store_cols(float *p, const typename VecT<VEC>::T &v, int nv) {
+    stv_n<VEC>(p, v, nv);
+}
+
+// ROW_BROADCAST: Y[r,:] = scale[r] * X[r,:]
+struct RowBroadcastOp {
+    const float *scale, *X;
+    float *Y;
+    int64_t ldx, ldy;
+    template <int VEC>
+    __device__ __forceinline__ void apply(int64_t r, int64_t c, int nv) const {
         const float s = scale[r];
-        V v = ldv<VEC>(X + r * ldx + c);
+        typename VecT<VEC>::T v = ldv<VEC>(X + r * ldx + c);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) el<VEC>(v, i) = __fmul_rn(s, el<VEC>(v, i));
-        stv<VEC>(Y + r * ldy + c, v);
+        store_cols<VEC>(Y + r * ldy + c, v, nv);
+    }
+};
+
+// torch.relu as its GPU kernel computes it: t > 0 ? t : +0, NaN passes through
+__device__ __forceinline__ float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
+
+// Y[r,:] = pre[r] * relu(act[r] * X[r,:]), each factor optional (absent: no rounding step)
+struct ScaleReluOp {
+    const float *act, *pre, *X;
+    float *Y;
+    int64_t ldx, ldy;
+    template <int VEC>
+    __device__ __forceinline__ void apply(int64_t r, int64_t c, int nv) const {
+        const float a = act ? act[r] : 1.0f, b = pre ? pre[r] : 1.0f;
+        typename VecT<VEC>::T v = ldv<VEC>(X + r * ldx + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            float t = el<VEC>(v, i);
+            if (act) t = __fmul_rn(a, t);
+            t = relu_t(t);
+            if (pre) t = __fmul_rn(b, t);
+            el<VEC>(v, i) = t;
+        }
+        store_cols<VEC>(Y + r * ldy + c, v, nv);
+    }
+};
+
+// its backward: dX[r,:] = act[r] * (act[r] * X[r,:] <= 0 ? 0 : G[r,:])
+// (threshold_backward on the ReLU output, then the product rule of act * X)
+struct ReluScaleBwdOp {
+    const float *act, *X, *G;
+    float *dX;
+    int64_t ldx, ldg, lddx;
+    template <int VEC>
+    __device__ __forceinline__ void apply(int64_t r, int64_t c, int nv) const {
+        const float a = act ? act[r] : 1.0f;
+        typename VecT<VEC>::T v = ldv<VEC>(X + r * ldx + c);
+        const typename VecT<VEC>::T g = ldv<VEC>(G + r * ldg + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            float t = el<VEC>(v, i);
+            if (act) t = __fmul_rn(a, t);
+            float d = relu_t(t) <= 0.0f ? 0.0f : reinterpret_cast<const float *>(&g)[i];
+            if (act) d = __fmul_rn(d, a);
+            el<VEC>(v, i) = d;
+        }
+        store_cols<VEC>(dX + r * lddx + c, v, nv);
+    }
+};
+
+template <int VEC, class Op>
+__global__ __launch_bounds__(kBlock) void k_rows(int64_t n_rows, int32_t F, int32_t L, Op op) {
+    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t r = t0 / L, c = t0 % L;
+    const int64_t dr = stride / L, dc = stride % L;
+    while (r < n_rows) {
+        const int64_t col = c * VEC;
+        op.template apply<VEC>(r, col, F - col < VEC ? (int)(F - col) : VEC);
+        c += dc;
+        r += dr;
+        if (c >= L) {
+            c -= L;
+            ++r;
+        }
     }
 }
+
+// widest vector for row ops over [n_rows, F] with the given strides / bases: VEC divides F,
+// or the rows are padded to it (every stride >= F rounded up to VEC)
+static int rows_vec(int32_t F, std::initializer_list<int64_t> lds, std::initializer_list<const void *> ptrs) {
+    for (int v = 4; v > 1; v >>= 1) {
+        const int64_t Fv = ((int64_t)F + v - 1) / v * v;
+        bool ok = true;
+        for (int64_t ld : lds) ok = ok && ld % v == 0 && (F % v == 0 || ld >= Fv);
+        for (const void *q : ptrs) ok = ok && ((uintptr_t)q % (4 * v)) == 0;
+        if (ok) return v;
+    }
+    return 1;
+}
+
+template <class Op>
+static int launch_rows(int64_t n_rows, int32_t F, int vec, const Op &op, void *stream) {
+    const int32_t L = (F + vec - 1) / vec;
+    const int64_t total = n_rows * L;
+    int64_t blocks = (total + kBlock - 1) / kBlock;
+    if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride: 16 workgroups per CU
+    hipStream_t hs = (hipStream_t)stream;
+    if (vec == 4) hipLaunchKernelGGL((k_rows<4, Op>), dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, F, L, op);
+    else if (vec == 2) hipLaunchKernelGGL((k_rows<2, Op>), dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, F, L, op);
+    else hipLaunchKernelGGL((k_rows<1, Op>), dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, F, L, op);
+    return launch_status();
+}
+
+}  // namespace gala
 
 extern "C" int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale,
                                       const float *X, int64_t ldx, float *Y, int64_t ldy,
@@ -578,20 +678,27 @@ extern "C" int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *sc
     if (n_rows < 0 || F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
     if (n_rows == 0 || F == 0) return GALA_OK;
     if (!scale || !X || !Y) return GALA_ERR_INVALID_ARG;
-    int vec = 4;
-    while (vec > 1 && (F % vec || ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) ||
-                       ((uintptr_t)Y % (4 * vec))))
-        vec >>= 1;
-    const int32_t L = F / vec;
-    const int64_t total = n_rows * L;
-    int64_t blocks = (total + kBlock - 1) / kBlock;
-    if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride: 16 workgroups per CU
-    hipStream_t hs = (hipStream_t)stream;
-    if (vec == 4)
-        hipLaunchKernelGGL(k_row_broadcast<4>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
-    else if (vec == 2)
-        hipLaunchKernelGGL(k_row_broadcast<2>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
-    else
-        hipLaunchKernelGGL(k_row_broadcast<1>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, L, scale, X, ldx, Y, ldy);
-    return launch_status();
+    return gala::launch_rows(n_rows, F, gala::rows_vec(F, {ldx, ldy}, {X, Y}),
+                             gala::RowBroadcastOp{scale, X, Y, ldx, ldy}, stream);
 }
+
+extern "C" int gala_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act,
+                                       const float *pre, const float *X, int64_t ldx, float *Y,
+                                       int64_t ldy, void *stream) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !Y) return GALA_ERR_INVALID_ARG;
+    return gala::launch_rows(n_rows, F, gala::rows_vec(F, {ldx, ldy}, {X, Y}),
+                             gala::ScaleReluOp{act, pre, X, Y, ldx, ldy}, stream);
+}
+
+extern "C" int gala_relu_scale_backward_f32(int64_t n_rows, int32_t F, const float *act,
+                                            const float *X, int64_t ldx, const float *G,
+                                            int64_t ldg, float *dX, int64_t lddx, void *stream) {
+    if (n_rows < 0 || F < 0 || ldx < F || ldg < F || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !G || !dX) return GALA_ERR_INVALID_ARG;
+    return gala::launch_rows(n_rows, F, gala::rows_vec(F, {ldx, ldg, lddx}, {X, G, dX}),
+                             gala::ReluScaleBwdOp{act, X, G, dX, ldx, ldg, lddx}, stream);
+}
+

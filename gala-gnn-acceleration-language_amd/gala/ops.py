@@ -181,6 +181,24 @@ def row_broadcast(scale, X, out=None) -> torch.Tensor:
     return out
 
 
+def row_scale_relu(X, act=None, pre=None, out=None) -> torch.Tensor:
+    """out[r, :] = pre[r] * relu(act[r] * X[r, :]) (gala_row_scale_relu_f32; factors optional)."""
+    if out is None:
+        out = _rows_like(X, X.shape[0])
+    _abi.call("gala_row_scale_relu_f32", X.shape[0], X.shape[1], _dp(act), _dp(pre), _dp(X), X.stride(0),
+              _dp(out), out.stride(0), _stream())
+    return out
+
+
+def relu_scale_backward(X, G, act=None, out=None) -> torch.Tensor:
+    """dX = act * (relu(act * X) <= 0 ? 0 : G) (gala_relu_scale_backward_f32)."""
+    if out is None:
+        out = _rows_like(X, X.shape[0])
+    _abi.call("gala_relu_scale_backward_f32", X.shape[0], X.shape[1], _dp(act), _dp(X), X.stride(0), _dp(G),
+              G.stride(0), _dp(out), out.stride(0), _stream())
+    return out
+
+
 def sddvv(g: DeviceGraph, a, b, op=_abi.GALA_SDDVV_ADD, heads=1, slope=0.2) -> torch.Tensor:
     out = torch.empty(g.nnz * heads, device=a.device, dtype=torch.float32)
     _abi.call("gala_sddvv_f32", g.csr(), _dp(a), _dp(b), heads, op, slope, _dp(out), _stream())

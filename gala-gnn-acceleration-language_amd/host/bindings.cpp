@@ -91,6 +91,13 @@ PYBIND11_MODULE(_gala_torch, m) {
           },
           py::arg("X"), py::arg("pre") = py::none(), py::arg("post") = py::none(),
           py::arg("li") = 0);
+    m.def("gcn_aggregate_relu_apply",
+          [opt](torch::Tensor x, std::optional<torch::Tensor> act, std::optional<torch::Tensor> pre,
+                std::optional<torch::Tensor> post, int64_t li) {
+              return gcn_aggregate_relu_apply(x, opt(act), opt(pre), opt(post), li);
+          },
+          py::arg("X"), py::arg("act") = py::none(), py::arg("pre") = py::none(),
+          py::arg("post") = py::none(), py::arg("li") = 0);
     m.def("ffn_apply",
           [opt](torch::Tensor x, torch::Tensor w, std::optional<torch::Tensor> b) {
               return ffn_apply(x, w, opt(b));

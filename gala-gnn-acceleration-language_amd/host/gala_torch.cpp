@@ -21,6 +21,8 @@ struct Backend {
     decltype(&gala_spmm_f32) spmm;
     decltype(&gala_degree_f32) degree;
     decltype(&gala_row_broadcast_f32) row_broadcast;
+    decltype(&gala_row_scale_relu_f32) scale_relu;
+    decltype(&gala_relu_scale_backward_f32) relu_bwd;
     decltype(&gala_sddvv_f32) sddvv;
     decltype(&gala_row_sum_f32) row_sum;
     decltype(&gala_row_scale_f32) row_scale;
@@ -35,12 +37,14 @@ struct Backend {
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
 };
-const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32, gala_sddvv_f32,
+const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
+                   gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_sddvv_f32,
                    gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
+                   gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
                    gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
@@ -863,6 +867,75 @@ struct GcnAggregate : public torch::autograd::Function<GcnAggregate> {
     }
 };
 
+// pre * relu(act * X) (gala_row_scale_relu_f32) and its backward (undefined factors: 1)
+torch::Tensor scale_relu(const torch::Tensor &X, const torch::Tensor &act, const torch::Tensor &pre) {
+    auto x = X.contiguous();
+    check_dev(x, torch::kFloat, "X");
+    const int64_t n = x.size(0), F = x.numel() / std::max<int64_t>(n, 1);
+    torch::Tensor a = act.defined() ? act.contiguous() : torch::Tensor();
+    torch::Tensor p = pre.defined() ? pre.contiguous() : torch::Tensor();
+    if (a.defined()) check_on(a, x, "act");
+    if (p.defined()) check_on(p, x, "pre");
+    auto out = torch::empty_like(x);
+    check(be(x).scale_relu(n, (int32_t)F, a.defined() ? a.data_ptr<float>() : nullptr,
+                           p.defined() ? p.data_ptr<float>() : nullptr, x.data_ptr<float>(), F,
+                           out.data_ptr<float>(), F, stream_of(x)),
+          "gala_row_scale_relu_f32");
+    return out;
+}
+
+torch::Tensor relu_scale_backward(const torch::Tensor &act, const torch::Tensor &X,
+                                  const torch::Tensor &G) {
+    auto x = X.contiguous(), g = G.contiguous();
+    check_dev(g, torch::kFloat, "grad");
+    check_on(g, x, "grad");
+    const int64_t n = x.size(0), F = x.numel() / std::max<int64_t>(n, 1);
+    torch::Tensor a = act.defined() ? act.contiguous() : torch::Tensor();
+    auto dx = torch::empty_like(x);
+    check(be(x).relu_bwd(n, (int32_t)F, a.defined() ? a.data_ptr<float>() : nullptr,
+                         x.data_ptr<float>(), F, g.data_ptr<float>(), F, dx.data_ptr<float>(), F,
+                         stream_of(x)),
+          "gala_relu_scale_backward_f32");
+    return dx;
+}
+
+// post * A (pre * relu(act * X)): the next layer's ReLU (and the row broadcast in front of
+// it) fused into the elementwise pass the aggregation needs anyway.  Backward: the
+// aggregation's backward gives G = pre * A_b (post * dY) (the gradient of relu(act * X)),
+// then one pass forms act * (relu(act * X) <= 0 ? 0 : G) -- the roundings of torch's
+// threshold_backward and mul backward.
+struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor act,
+                                 torch::Tensor pre, torch::Tensor post, int64_t li) {
+        auto &S = global_slots();
+        Slot s = slot(2 * li);
+        const bool has_act = act.numel() > 0, has_pre = pre.numel() > 0, has_post = post.numel() > 0;
+        auto x = X.contiguous();
+        auto xs = scale_relu(x, has_act ? act : torch::Tensor(), has_pre ? pre : torch::Tensor());
+        ctx->save_for_backward({x});
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["act"] = act.detach();
+        ctx->saved_data["pre"] = pre.detach();
+        ctx->saved_data["post"] = post.detach();
+        return spmm_impl(xs, s.off, s.cols, s.weighted ? &s.vals : nullptr, s.bounds, s.segs, 1,
+                         nullptr, has_post ? &post : nullptr, S.nsamples, S.ra, S.rb);
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        const int64_t li = ctx->saved_data["li"].toInt();
+        auto act = ctx->saved_data["act"].toTensor();
+        auto pre = ctx->saved_data["pre"].toTensor();
+        auto post = ctx->saved_data["post"].toTensor();
+        auto x = ctx->get_saved_variables()[0];
+        auto &S = global_slots();
+        Slot b = slot(2 * li + 1);
+        torch::Tensor dys = post.numel() > 0 ? row_broadcast(post, grad_outputs[0]) : grad_outputs[0];
+        auto G = spmm_impl(dys, b.off, b.cols, b.weighted ? &b.vals : nullptr, b.bounds, b.segs, 1,
+                           nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb);
+        return {relu_scale_backward(act.numel() > 0 ? act : torch::Tensor(), x, G), torch::Tensor(),
+                torch::Tensor(), torch::Tensor(), torch::Tensor()};
+    }
+};
+
 // FFN_OP with the weight / bias gradients on gala_dense_grad_f32 (split over rows) and dX
 // on the library GEMM; the forward is at::linear's addmm, bit for bit.
 struct Ffn : public torch::autograd::Function<Ffn> {
@@ -912,6 +985,14 @@ torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Ten
         return t.defined() ? t : torch::empty({0}, X.options().requires_grad(false));
     };
     return GcnAggregate::apply(X, absent(pre), absent(post), li);
+}
+
+torch::Tensor gcn_aggregate_relu_apply(torch::Tensor X, torch::Tensor act, torch::Tensor pre,
+                                       torch::Tensor post, int64_t li) {
+    auto absent = [&](const torch::Tensor &t) {
+        return t.defined() ? t : torch::empty({0}, X.options().requires_grad(false));
+    };
+    return GcnAggregateRelu::apply(X, absent(act), absent(pre), absent(post), li);
 }
 
 torch::Tensor aggregate_node_mul_sum_apply(torch::Tensor input_dense, int64_t li) {

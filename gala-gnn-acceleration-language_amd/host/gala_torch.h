@@ -124,6 +124,11 @@ torch::Tensor non_lnr_op_softmax_apply(torch::Tensor value_graph, int64_t li);
 // 2li+1); pre / post may be undefined.  Honours the slot's weights and kernel sampling.
 torch::Tensor gcn_aggregate_apply(torch::Tensor X, torch::Tensor pre, torch::Tensor post,
                                   int64_t li);
+// The same with the ReLU prologue of the next layer fused in front: post * A (pre *
+// relu(act * X)); act / pre / post may be undefined.  Forward and backward are
+// bit-identical to torch::relu(act * X) followed by gcn_aggregate_apply.
+torch::Tensor gcn_aggregate_relu_apply(torch::Tensor X, torch::Tensor act, torch::Tensor pre,
+                                       torch::Tensor post, int64_t li);
 // FFN_OP: X W^T + b (at::linear's forward) whose weight / bias gradients run on
 // gala_dense_grad_f32; bias may be undefined.
 torch::Tensor ffn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias);

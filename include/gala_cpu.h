@@ -33,6 +33,11 @@ int gala_cpu_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t fl
                         int32_t nsamp, void *stream);
 int gala_cpu_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale, const float *X,
                                int64_t ldx, float *Y, int64_t ldy, void *stream);
+int gala_cpu_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act, const float *pre,
+                                const float *X, int64_t ldx, float *Y, int64_t ldy, void *stream);
+int gala_cpu_relu_scale_backward_f32(int64_t n_rows, int32_t F, const float *act, const float *X,
+                                     int64_t ldx, const float *G, int64_t ldg, float *dX,
+                                     int64_t lddx, void *stream);
 int gala_cpu_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col,
                        int32_t heads, int32_t op, float slope, float *out_e, void *stream);
 int gala_cpu_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t heads, float eps,

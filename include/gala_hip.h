@@ -150,6 +150,26 @@ int gala_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags,
 int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale, const float *X,
                            int64_t ldx, float *Y, int64_t ldy, void *stream);
 
+/*
+ * Y[r, 0:F] = pre[r] * relu(act[r] * X[r, 0:F]), relu(t) = t > 0 ? t : +0 with NaN passing
+ * through (torch.relu's GPU kernel); act and/or pre may be NULL (no factor, no rounding step).
+ * Replaces: the elementwise chain the generated forward runs in front of a GCN
+ * aggregation -- ROW_BROADCAST (`norm * res`, common.h:1150-1169), NON_LNR_OP_RELU
+ * (common.h:1170-1174), and the next layer's ROW_BROADCAST -- as one pass, with the same
+ * roundings (bit-identical to the three torch ops).
+ */
+int gala_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act, const float *pre,
+                            const float *X, int64_t ldx, float *Y, int64_t ldy, void *stream);
+
+/*
+ * Backward of the ReLU prologue: dX[r, :] = act[r] * (act[r] * X[r, :] <= 0 ? 0 : G[r, :])
+ * (torch's threshold_backward on the ReLU output, then the product rule of act * X; act
+ * may be NULL).  G is the gradient of relu(act * X).
+ */
+int gala_relu_scale_backward_f32(int64_t n_rows, int32_t F, const float *act, const float *X,
+                                 int64_t ldx, const float *G, int64_t ldg, float *dX,
+                                 int64_t lddx, void *stream);
+
 /* ---- edge (SDDVV / SDDMM) ops -------------------------------------------------------- */
 #define GALA_SDDVV_ADD 0        /* out[e,h] = a[row,h] + b[col_e,h]   (cuda.h:679-698)     */
 #define GALA_SDDVV_MUL 1        /* out[e,h] = a[row,h] * b[col_e,h]   (cuda.h:848-867)     */

@@ -193,7 +193,11 @@ def run(ir, graphs: Graphs, X, params, segments=1):
             else:
                 y = _SlotSpmm.apply(a[0], graphs.matrix(gi), graphs.backward_matrix(gi))
         elif op == "GCN_AGGREGATE":
-            x = a[0] if a[1] is None else a[1] * a[0]
+            x = a[0]
+            if nd["param"] == 1:  # ReLU prologue: relu(act * x)
+                act = a[3] if len(a) > 3 else None
+                x = torch.relu(x if act is None else act * x)
+            x = x if a[1] is None else a[1] * x
             y = _SlotSpmm.apply(x, graphs.matrix(gi), graphs.backward_matrix(gi))
             if a[2] is not None:
                 y = a[2] * y

@@ -232,3 +232,25 @@ def test_status_codes_match_the_hip_abi():
     bad = HostCsr(layout.col_tile(g, 1000))
     bad.g.bounds[1] = g.nnz + 5
     assert L.gala_cpu_spmm_f32(bad.ref, P(X), 4, P(Y), 4, 4, None, None, 0, 0, 5, 7, None) == _abi.GALA_ERR_GRAPH
+
+
+def test_row_scale_relu_and_backward_match_numpy():
+    """pre * relu(act * X) and act * (relu(act * X) <= 0 ? 0 : G), bit for bit (float32 numpy
+    with the same rounding steps; torch.relu's GPU semantics: -0 -> +0, NaN passes)."""
+    rng = np.random.default_rng(3)
+    n, F = 500, 13
+    X = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    X[::5, 0] = -0.0
+    X[3, 2] = np.nan
+    act = rng.uniform(0.1, 2, n).astype(np.float32)
+    pre = rng.uniform(0.1, 2, n).astype(np.float32)
+    G = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    Y = np.empty_like(X)
+    _abi.call_cpu("gala_row_scale_relu_f32", n, F, P(act), P(pre), P(X), F, P(Y), F, None)
+    t = act[:, None] * X
+    r = np.where((t > 0) | np.isnan(t), t, np.float32(0))
+    np.testing.assert_array_equal(Y, pre[:, None] * r)
+    assert np.array_equal(np.signbit(Y), np.signbit(pre[:, None] * r))
+    dX = np.empty_like(X)
+    _abi.call_cpu("gala_relu_scale_backward_f32", n, F, P(act), P(X), F, P(G), F, P(dX), F, None)
+    np.testing.assert_array_equal(dX, np.where(r <= 0, np.float32(0), G) * act[:, None])

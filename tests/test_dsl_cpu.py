@@ -99,8 +99,11 @@ def test_flags_disable_passes(tmp_path):
     assert post["num_graphs"] == 1                             # no subgraphs
     assert post["sched"]["col_tile"] == 1000
     # no operator reordering: FFNs stay where the program put them
-    assert ops(post, False) == ["DEGREES", "POWER", "GCN_AGGREGATE", "FFN", "ROW_BROADCAST",
-                                "RELU", "GCN_AGGREGATE", "FFN", "ROW_BROADCAST"]
+    # (layer 1's `norm * res -> relu` fused in front of its aggregation: the ReLU prologue)
+    assert ops(post, False) == ["DEGREES", "POWER", "GCN_AGGREGATE", "FFN", "GCN_AGGREGATE", "FFN",
+                                "ROW_BROADCAST"]
+    relu_agg = [n for n in post["nodes"] if n["op"] == "GCN_AGGREGATE" and n["param"] == 1]
+    assert len(relu_agg) == 1 and relu_agg[0]["in"][3] >= 0     # with the row-broadcast act
     sp = galac(os.path.join(HERE, "dsl", "gcn_sparse.txt"), tmp_path)["post"]
     assert "AGGREGATE_EDGE_MUL" in ops(sp, True)
     assert ops(sp).count("AGGREGATE_MUL_SUM") == 2            # weighted, A_w x

@@ -653,3 +653,39 @@ def test_ops_capture_in_hip_graph():
         want = step()
         for a, b in zip(outs, want):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("F", [1, 7, 32, 47, 128])
+@pytest.mark.parametrize("padded", [False, True])
+def test_row_scale_relu_matches_torch_chain(F, padded):
+    """The GCN ReLU prologue pre * relu(act * X) and its backward are bit-identical to the
+    torch ops they replace (mul, relu, mul; relu's threshold_backward, mul backward),
+    including -0, NaN and exact zeros, and leave row padding untouched."""
+    n = 3000
+    rng = np.random.default_rng(F)
+    X = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    X[::7, 0] = 0.0
+    X[1::11, -1] = -0.0
+    X[5, 0] = np.nan
+    act = rng.uniform(0.1, 2, n).astype(np.float32)
+    pre = rng.uniform(0.1, 2, n).astype(np.float32)
+    G = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    if padded:
+        xb, Xd = _padded(X, F, 5.0)
+        _, Gd = _padded(G, F, 5.0)
+    else:
+        Xd, Gd = dev(X), dev(G)
+    a, p = dev(act), dev(pre)
+    for A, P in ((a, p), (None, p), (a, None), (None, None)):
+        t = Xd if A is None else A[:, None] * Xd
+        want = torch.relu(t) if P is None else P[:, None] * torch.relu(t)
+        got = ops.row_scale_relu(Xd, A, P)
+        assert torch.equal(torch.nan_to_num(got, nan=123.0), torch.nan_to_num(want, nan=123.0))
+        assert torch.equal(torch.signbit(got), torch.signbit(want))
+        r = torch.relu(t)
+        dt = torch.where(r <= 0, torch.zeros_like(Gd), Gd)
+        want_dx = dt if A is None else dt * A[:, None]
+        got_dx = ops.relu_scale_backward(Xd, Gd, A)
+        assert torch.equal(torch.nan_to_num(got_dx, nan=123.0), torch.nan_to_num(want_dx, nan=123.0))
+    if padded:
+        assert bool(torch.all(xb[:, F:] == 5.0))
