@@ -21,7 +21,12 @@ namespace gala {
 namespace {
 
 constexpr int kStep = 2;      // rows per MFMA (the K of 32x32x2)
-constexpr int kInFlight = 4;  // MFMA steps whose operand loads are issued together
+// MFMA steps whose operand loads are issued together: 4 for the small (pipelined) wave
+// tiles, 8 for 2 x 2 tiles, which wait for one batch at a time and need the longer run of
+// MFMAs per wait to keep the matrix cores busy at ~3 waves per SIMD
+template <int WM, int WK>
+constexpr int in_flight() { return WM * WK < 4 ? 4 : 8; }
+constexpr int kRowAlign = 16;  // rows per chunk: a multiple of every kStep * in_flight
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -42,6 +47,7 @@ __global__ __launch_bounds__(kBlock) void k_tn_mfma(int64_t N, int32_t K, int32_
     const int64_t r0 = chunk * rows_per_chunk;
     const int64_t r1 = r0 + rows_per_chunk < N ? r0 + rows_per_chunk : N;
     const int li = lane & 31, lh = lane >> 5;
+    constexpr int kInFlight = in_flight<WM, WK>();
     bool mv[WM], kv[WK];
     int64_t mo[WM], ko[WK];
 #pragma unroll
@@ -260,7 +266,7 @@ Plan plan_for(int64_t N, int32_t K, int32_t M) {
         pl.tiles_k = (K + 32 * pl.wk - 1) / (32 * pl.wk);
         pl.n_tg = pl.tiles_k * ((M + 32 * pl.wm - 1) / (32 * pl.wm));
         target = (8192 + pl.n_tg - 1) / pl.n_tg;
-        align = kStep * kInFlight;
+        align = kRowAlign;
     }
     int64_t rpc = (N + target - 1) / target;
     rpc = (rpc + align - 1) / align * align;
