@@ -52,6 +52,7 @@ struct SpmmParams {
     int32_t nsamp, ra, rb;
     int32_t split_threshold;  // > 0: rows longer than this are left to the split kernels
     const int32_t *row_order; // nullable: row group i handles row row_order[i]
+    int32_t xcd_order;        // 1: XCD-aware block order (logical_block_runs)
     SegTable seg;
 };
 
@@ -199,7 +200,9 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
     constexpr int RPW = kWave / G;
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
-    const int64_t wave = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x / kWave);
+    const int64_t blk = p.xcd_order ? logical_block_runs(blockIdx.x, gridDim.x, kXcdRun)
+                                    : (int64_t)blockIdx.x;
+    const int64_t wave = blk * (kBlock / kWave) + (threadIdx.x / kWave);
     const int64_t rid = wave * RPW + lane / G;
     if (rid >= p.n_rows) return;
     const int64_t row = p.row_order ? (int64_t)p.row_order[rid] : rid;
@@ -474,12 +477,16 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     p.rb = rb;
     p.split_threshold = 0;
     p.row_order = nullptr;
+    p.xcd_order = 1;  // off below when a degree-ordered row schedule is used (heavy rows first)
     hipStream_t hs = (hipStream_t)stream;
 
     // hub rows: chunk partials + ordered fix-up (plan built once per graph on the host)
     SplitParams spl{};
     const SplitParams *sp = nullptr;
-    if (plan && plan->row_order && A->n_seg == 1) p.row_order = plan->row_order;
+    if (plan && plan->row_order && A->n_seg == 1) {
+        p.row_order = plan->row_order;
+        p.xcd_order = 0;
+    }
     if (use_split) {
         if (plan->threshold < 1 || plan->chunk < 1 || !plan->rows || !plan->row_chunk0 ||
             !plan->chunk_row || !plan->workspace)

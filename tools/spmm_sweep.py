@@ -41,11 +41,21 @@ def main():
     ap.add_argument("--u", type=int, default=61_859_140)
     ap.add_argument("--F", default="8,16,32,64,128")
     ap.add_argument("--ops", default="spmm,spmm_scaled,degree,sddvv,softmax,sddmm,gat")
+    ap.add_argument("--band", type=int, default=4096, help="banded graph: neighbour offset bound")
     ap.add_argument("--sort-rows", action="store_true")
     ap.add_argument("--pad", action="store_true", help="row-padded X / Y (stride F rounded up to 4)")
     args = ap.parse_args()
     t0 = time.time()
-    hg = layout.gen_graph(args.graph, args.n, args.u, seed=42)
+    if args.graph == "banded":  # locality: every neighbour within +-band of its row
+        rng = np.random.default_rng(42)
+        m = 2 * args.u
+        src = rng.integers(0, args.n, m, dtype=np.int64)
+        dst = np.clip(src + rng.integers(-args.band, args.band + 1, m), 0, args.n - 1)
+        ids = np.arange(args.n, dtype=np.int64)
+        hg = layout.csr_build(args.n, args.n, np.concatenate([src, ids]).astype(np.int32),
+                              np.concatenate([dst, ids]).astype(np.int32))
+    else:
+        hg = layout.gen_graph(args.graph, args.n, args.u, seed=42)
     if args.sort_rows:  # experiment: rows relabelled by descending degree (stable)
         deg = np.diff(hg.rowptr)
         order = np.argsort(-deg, kind="stable")
