@@ -22,6 +22,7 @@ struct EdgeParams {
     const int32_t *col;
     int64_t n_rows;
     int32_t heads;
+    int32_t xcd_order;  // 1: XCD-aware block order (gala_internal.h); 0 on skewed graphs
     SegTable seg;
 };
 
@@ -37,7 +38,9 @@ __device__ __forceinline__ void row_range(const EdgeParams &p, int s, int64_t ro
 #define GALA_ROW_PROLOGUE(G)                                                          \
     const int lane = threadIdx.x & (kWave - 1);                                       \
     const int gl = lane & ((G)-1);                                                    \
-    const int64_t row = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) \
+    const int64_t blk_ = p.xcd_order ? logical_block_runs(blockIdx.x, gridDim.x, kXcdRun) \
+                                     : (int64_t)blockIdx.x;                           \
+    const int64_t row = (blk_ * (kBlock / kWave) + threadIdx.x / kWave)              \
                             * (kWave / (G)) + lane / (G);                             \
     const bool row_ok = row < p.n_rows;
 
@@ -1427,6 +1430,11 @@ static int edge_setup(const gala_csr_t *A, int32_t heads, EdgeParams *p) {
     p->col = A->col;
     p->n_rows = A->n_rows;
     p->heads = heads;
+    // XCD-aware row-block order (gala_internal.h); graphs with a hub / row-order plan are
+    // skewed (heavy rows cluster in id order) and keep the hardware order.  Banded
+    // Products-shaped graph, F = 32: SDDMM 1.83 -> 1.69 ms, GAT forward 1.65 -> 1.60 ms;
+    // uniform: within 1 % either way
+    p->xcd_order = A->split == nullptr;
     return fill_segments(A, 0, &p->seg);
 }
 
