@@ -1,0 +1,134 @@
+"""GPU: seeded random parity sweep over the operator surface (tuning-independent corners).
+
+Every case draws a graph (directed random rows with a chosen mean degree, optionally an
+R-MAT graph, a block of empty rows, a hub row longer than the split threshold), a width F,
+a head count, row padding, edge weights, a hub-row split plan with small chunks and column
+tiling, then checks the HIP path against the oracle:
+
+* bit-exact: degree, SpMM without hub chunks, row-scale / row-broadcast;
+* reordered sums (hub chunks): within the worst-case fp32 summation bound of the row,
+  |err| <= (deg + 1) 2^-24 sum|a x| + 1e-6 per entry;
+* TOL (1e-4 abs + rel): SDDMM, edge softmax fwd / bwd, fused GAT forward / backward.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as orc
+from gala import _abi, layout, ops
+from _graphs import to_oracle
+
+pytestmark = pytest.mark.gpu
+TOL = dict(atol=1e-4, rtol=1e-4)
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def _graph(rng):
+    kind = rng.choice(["random", "rmat", "empty_rows", "hub"])
+    n = int(rng.integers(1, 2500))
+    if kind == "rmat" and n >= 64:
+        return layout.gen_graph("rmat", n, int(rng.integers(n, 12 * n)), seed=int(rng.integers(1 << 30)))
+    deg = float(rng.uniform(0, 40))
+    m = int(deg * n)
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    if kind == "empty_rows":
+        src = src % max(1, n // 3)
+    if kind == "hub":
+        hub = np.full(int(rng.integers(300, 3000)), int(rng.integers(0, n)))
+        src = np.concatenate([src, hub])
+        dst = np.concatenate([dst, rng.integers(0, n, hub.shape[0])])
+    return layout.csr_build(n, n, src.astype(np.int32), dst.astype(np.int32))
+
+
+def _padded(a, fill=np.nan):
+    F = a.shape[1]
+    buf = torch.full((a.shape[0], (F + 3) // 4 * 4), float(fill), device="cuda")
+    buf[:, :F] = _dev(a)
+    return buf[:, :F]
+
+
+def _reordered_ok(Y, g, X, val=None):
+    import scipy.sparse as sp
+    v = np.ones(g.nnz) if val is None else val.astype(np.float64)
+    A = sp.csr_matrix((v, g.col.copy(), g.rowptr.copy()), shape=(g.n_rows, g.n_cols))
+    exact = A @ X.astype(np.float64)
+    mass = abs(A) @ np.abs(X.astype(np.float64))
+    # worst-case bound of any fp32 summation order over a row of n terms: n * 2^-24 * sum|a x|
+    n = np.diff(g.rowptr).astype(np.float64)[:, None]
+    assert np.all(np.abs(Y.astype(np.float64) - exact) <= (n + 1) * 2.0**-24 * mass + 1e-6)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("GALA_FUZZ_CASES", "96"))))
+def test_random_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    g = _graph(rng)
+    og = to_oracle(g)
+    heads = int(rng.choice([1, 1, 2, 4, 8]))
+    # multi-head widths: per-head lane counts are powers of two (the fused kernels' layout)
+    F = heads * int(rng.choice([1, 2, 4, 8, 16, 32])) if heads > 1 else int(rng.integers(1, 300))
+    pad = heads == 1 and F % 4 != 0 and bool(rng.integers(0, 2))
+    vec = 4 if (F % 4 == 0 or pad) else (2 if F % 2 == 0 else 1)
+    edge_ok = -(-F // vec) <= 64  # SDDMM / GAT row groups span at most one wave
+    split = bool(rng.integers(0, 2)) and g.nnz > 0
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if split:
+        dg.set_split_plan(g.rowptr, int(rng.integers(8, 200)), chunk=int(rng.choice([16, 32, 512])),
+                          row_order=bool(rng.integers(0, 2)))
+    chunked = dg.split_rows > 0
+    X = rng.uniform(-1, 1, (g.n_cols, F)).astype(np.float32)
+    Xd = _padded(X) if pad else _dev(X)
+
+    # degree: exact counts
+    np.testing.assert_array_equal(_host(ops.degree(dg)), orc.degree(og))
+    # SpMM, plain and weighted (one weight per edge)
+    val = rng.uniform(0, 1, g.nnz).astype(np.float32)
+    for w in (None, val):
+        gd = dg if w is None else dg.with_values(_dev(w))
+        Y = _host(ops.spmm(gd, Xd))
+        if chunked:
+            _reordered_ok(Y, g, X, w)
+        else:
+            np.testing.assert_array_equal(Y, orc.spmm(og if w is None else to_oracle(g, w), X))
+    # column-tiled layout (no split plan): segments summed in order, bit-exact
+    if g.n_cols > 1 and not chunked:
+        tg = layout.col_tile(g, int(rng.integers(1, g.n_cols)))
+        np.testing.assert_array_equal(_host(ops.spmm(ops.DeviceGraph.from_host(tg, split=False), _dev(X))),
+                                      orc.spmm(to_oracle(tg), X))
+    if g.nnz == 0:
+        return
+    s = rng.uniform(-3, 3, g.nnz * heads).astype(np.float32)
+    d = rng.uniform(-1, 1, g.nnz * heads).astype(np.float32)
+    for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+        a_ref = orc.softmax_fwd(og, s, heads=heads, mode=mode)
+        np.testing.assert_allclose(_host(ops.edge_softmax(dg, _dev(s), heads=heads, mode=mode)), a_ref, **TOL)
+        np.testing.assert_allclose(_host(ops.edge_softmax_bwd(dg, _dev(a_ref), _dev(d), heads=heads, mode=mode)),
+                                   orc.softmax_bwd(og, a_ref, d, heads=heads, mode=mode), **TOL)
+    if not edge_ok:
+        return
+    # SDDMM, edge softmax, fused GAT (REF and FIXED)
+    A = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    Ad = _padded(A) if pad else _dev(A)
+    np.testing.assert_allclose(_host(ops.sddmm(dg, Ad, Xd, heads=heads)), orc.sddmm(og, A, X, heads=heads), **TOL)
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    aR = rng.uniform(-1, 1, (g.n_cols, heads)).astype(np.float32)
+    for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+        Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=mode)
+        Yg, al = ops.gat_fwd(dg, _dev(aL), _dev(aR), Xd, heads=heads, slope=0.2, mode=mode, want_alpha=True)
+        np.testing.assert_allclose(_host(al), al_ref, **TOL)
+        np.testing.assert_allclose(_host(Yg), Y_ref, **TOL)
+        dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, X, A, al_ref, heads=heads, slope=0.2, mode=mode)
+        daL, dz = ops.gat_bwd(dg, _dev(aL), _dev(aR), Xd, Ad, _dev(al_ref), heads=heads, slope=0.2, mode=mode)
+        np.testing.assert_allclose(_host(daL), daL_ref, **TOL)
+        if mode == _abi.GALA_SOFTMAX_FIXED:
+            np.testing.assert_allclose(_host(dz), dz_ref, **TOL)
