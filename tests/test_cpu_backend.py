@@ -254,3 +254,60 @@ def test_row_scale_relu_and_backward_match_numpy():
     dX = np.empty_like(X)
     _abi.call_cpu("gala_relu_scale_backward_f32", n, F, P(act), P(X), F, P(G), F, P(dX), F, None)
     np.testing.assert_array_equal(dX, np.where(r <= 0, np.float32(0), G) * act[:, None])
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_case(seed):
+    """Seeded random sweep of the host backend (the GPU suite runs the same generator through
+    libgala_hip.so): random / R-MAT / empty-row / hub graphs, widths, 1-8 heads, strided
+    operands; bit-exact degree / SpMM / tiled SpMM, TOL for the reductions and GAT."""
+    import test_gpu_fuzz as fz
+    rng = np.random.default_rng(5000 + seed)
+    g = fz._graph(rng)
+    og = to_oracle(g)
+    heads = int(rng.choice([1, 1, 2, 4, 8]))
+    D = int(rng.choice([1, 2, 4, 8, 16, 32])) if heads > 1 else int(rng.integers(1, 120))
+    F = heads * D
+    ld = F + int(rng.integers(0, 5))  # strided rows
+    X = np.zeros((g.n_cols, ld), np.float32)
+    X[:, :F] = rng.uniform(-1, 1, (g.n_cols, F))
+    Xc = np.ascontiguousarray(X[:, :F])
+    deg = np.empty(g.n_rows, np.float32)
+    _abi.call_cpu("gala_degree_f32", HostCsr(g).ref, P(deg), 1.0, 0, 0, None)
+    np.testing.assert_array_equal(deg, orc.degree(og))
+    Y = np.full((g.n_rows, ld), 7.0, np.float32)
+    _abi.call_cpu("gala_spmm_f32", HostCsr(g).ref, P(X), ld, P(Y), ld, F, None, None, 0, 0, 5, 7, None)
+    np.testing.assert_array_equal(Y[:, :F], orc.spmm(og, Xc))
+    assert np.all(Y[:, F:] == 7.0)
+    if g.n_cols > 1:
+        tg = layout.col_tile(g, int(rng.integers(1, g.n_cols)))
+        np.testing.assert_array_equal(spmm_cpu(tg, Xc), orc.spmm(to_oracle(tg), Xc))
+    if g.nnz == 0:
+        return
+    s = rng.uniform(-3, 3, g.nnz * heads).astype(np.float32)
+    for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+        a = np.empty_like(s)
+        _abi.call_cpu("gala_edge_softmax_fwd_f32", HostCsr(g).ref, P(s), heads, mode, P(a), None)
+        np.testing.assert_allclose(a, orc.softmax_fwd(og, s, heads=heads, mode=mode), **TOL)
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    aR = rng.uniform(-1, 1, (g.n_cols, heads)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    out = np.empty(g.nnz * heads, np.float32)
+    _abi.call_cpu("gala_sddmm_dot_f32", HostCsr(g).ref, P(dY), F, P(X), ld, F, heads, P(out), None)
+    np.testing.assert_allclose(out, orc.sddmm(og, dY, Xc, heads=heads), **TOL)
+    for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+        Y_ref, al_ref = orc.gat_fwd(og, aL, aR, Xc, heads=heads, slope=0.2, mode=mode)
+        Yg = np.empty((g.n_rows, F), np.float32)
+        al = np.empty(g.nnz * heads, np.float32)
+        _abi.call_cpu("gala_gat_fwd_f32", HostCsr(g).ref, P(aL), P(aR), P(X), ld, F, heads, 0.2, mode,
+                      P(Yg), F, P(al), None)
+        np.testing.assert_allclose(al, al_ref, **TOL)
+        np.testing.assert_allclose(Yg, Y_ref, **TOL)
+        dz_ref, daL_ref = orc.gat_bwd(og, aL, aR, Xc, dY, al_ref, heads=heads, slope=0.2, mode=mode)
+        dz = np.empty(g.nnz * heads, np.float32)
+        daL = np.empty(g.n_rows * heads, np.float32)
+        _abi.call_cpu("gala_gat_bwd_f32", HostCsr(g).ref, P(aL), P(aR), P(X), ld, P(dY), F, F, heads, 0.2,
+                      mode, P(al_ref), P(dz), P(daL), None)
+        np.testing.assert_allclose(daL, daL_ref, **TOL)
+        if mode == _abi.GALA_SOFTMAX_FIXED:
+            np.testing.assert_allclose(dz, dz_ref, **TOL)
