@@ -441,6 +441,10 @@ torch::Tensor degrees() {
     return degree_norm(S.offset_graph[0], S.bounds[0], S.segments[0], 1.0, S.columns_graph[0]);
 }
 
+torch::Tensor cross_entropy(const torch::Tensor &pred, const torch::Tensor &labels) {
+    return -torch::log_softmax(pred, 1).gather(1, labels.reshape({-1, 1}).to(torch::kLong)).mean();
+}
+
 double get_time() { return omp_get_wtime(); }
 
 double calc_mean(const std::vector<double> &v) {

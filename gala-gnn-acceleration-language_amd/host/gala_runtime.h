@@ -82,6 +82,9 @@ torch::Tensor sampled_degrees(int64_t nsamples);
 // DEGREES: rows' edge counts of graph 0, summed over its segments (gala.cu:433-440)
 torch::Tensor degrees();
 
+// torch::nn::CrossEntropyLoss (mean reduction) as -mean(log_softmax(pred)[i, y_i]): the
+// same value and gradient without nll_loss's single-workgroup reduction kernels
+torch::Tensor cross_entropy(const torch::Tensor &pred, const torch::Tensor &labels);
 double get_time();
 double calc_mean(const std::vector<double> &v);
 int64_t device_memory_mb(const torch::Device &dev);  // printMemoryUsage (cuda.h:1000-1020):
