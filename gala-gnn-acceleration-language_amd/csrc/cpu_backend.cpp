@@ -212,6 +212,25 @@ extern "C" int gala_cpu_relu_scale_backward_f32(int64_t n_rows, int32_t F, const
     return GALA_OK;
 }
 
+extern "C" int gala_cpu_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X,
+                                    int64_t ldx, const float *W, const float *b, float *Y,
+                                    int64_t ldy, void *) {
+    if (n_rows < 0 || K < 0 || M < 0 || ldx < K || ldy < M) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || M == 0) return GALA_OK;
+    const int wm = (M + 31) / 32;
+    if (wm > 8 || (int64_t)((K + 1) & ~1) * 32 * wm > 16384) return GALA_ERR_UNSUPPORTED;
+    if (!Y || (K > 0 && (!X || !W))) return GALA_ERR_INVALID_ARG;
+    // bias first, then the products in k order: the matrix cores' fmaf chain
+#pragma omp parallel for schedule(static, 256)
+    for (int64_t n = 0; n < n_rows; ++n)
+        for (int32_t m = 0; m < M; ++m) {
+            float acc = b ? b[m] : 0.0f;
+            for (int32_t k = 0; k < K; ++k) acc = fmaf(X[n * ldx + k], W[(int64_t)m * K + k], acc);
+            Y[n * ldy + m] = acc;
+        }
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_sddvv_f32(const gala_csr_t *A, const float *a_row, const float *b_col,
                                   int32_t heads, int32_t op, float slope, float *out_e, void *) {
     int st = check_csr(A);

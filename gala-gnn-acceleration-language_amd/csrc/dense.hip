@@ -129,6 +129,87 @@ __global__ __launch_bounds__(kBlock) void k_tn_mfma(int64_t N, int32_t K, int32_
     }
 }
 
+// ---- FFN forward: Y[N, M] = X[N, K] W^T + b on the matrix cores ----------------------
+// A block walks groups of 4 row tiles (32 rows each, one per wave) grid-stride.  W^T lives
+// in LDS for the whole block (K*M <= kFwdMaxKM floats); each wave stages its 32 x K tile of
+// X in LDS with coalesced (float4 where aligned) loads -- consecutive rows are contiguous --
+// at an odd row stride, so the MFMA operand reads (lane l: row l%32, k = 2s + l/32) are
+// bank-conflict free.  One wave owns all M columns (WM tiles of 32); accumulators start at
+// the bias, and each 32x32 C tile is stored with 32 lanes on 32 consecutive columns of a row.
+constexpr int kFwdMaxKM = 16384;  // W^T floats in LDS (64 KB)
+
+template <int WM, int V>
+__global__ __launch_bounds__(kBlock) void k_ffn_fwd(int64_t N, int32_t K, int32_t M,
+                                                    const float *__restrict__ X, int64_t ldx,
+                                                    const float *__restrict__ W,
+                                                    const float *__restrict__ bias,
+                                                    float *__restrict__ Y, int64_t ldy) {
+    extern __shared__ float smem[];
+    constexpr int Mp = 32 * WM;
+    const int Kp = (K + 1) & ~1;       // whole MFMA steps (an odd tail k reads zeros)
+    const int KS = Kp + 1;             // odd LDS row stride of the X tiles
+    float *wt = smem;                  // wt[k * Mp + m] = W[m][k], zero padded
+    for (int t = threadIdx.x; t < Kp * Mp; t += kBlock) {
+        const int k = t / Mp, m = t % Mp;
+        wt[t] = (k < K && m < M) ? W[(int64_t)m * K + k] : 0.0f;
+    }
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int li = lane & 31, lh = lane >> 5;
+    float *xs = smem + Kp * Mp + wv * 32 * KS;
+    for (int t = lane; t < 32 * KS; t += kWave) xs[t] = 0.0f;  // the padding column stays 0
+    __syncthreads();
+    float bv[WM];
+#pragma unroll
+    for (int a = 0; a < WM; ++a) {
+        const int m = a * 32 + li;
+        bv[a] = (bias && m < M) ? bias[m] : 0.0f;
+    }
+    const int64_t tiles = (N + 31) / 32;
+    const int Kq = (K + V - 1) / V;    // V-float vectors per row
+    for (int64_t g0 = (int64_t)blockIdx.x * 4; g0 < tiles; g0 += (int64_t)gridDim.x * 4) {
+        const int64_t n0 = (g0 + wv) * 32;
+        // stage this wave's 32 x K tile (rows past N read as zeros)
+        for (int t = lane; t < 32 * Kq; t += kWave) {
+            const int r = t / Kq, c = (t - r * Kq) * V;
+            const int64_t n = n0 + r;
+            float v[V];
+            if (V == 4 && n < N) {
+                const float4 q = *reinterpret_cast<const float4 *>(X + n * ldx + c);
+                v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < V; ++i) v[i] = (n < N && c + i < K) ? X[n * ldx + c + i] : 0.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < V; ++i) xs[r * KS + c + i] = v[i];
+        }
+        __syncthreads();
+        f32x16 acc[WM];
+#pragma unroll
+        for (int a = 0; a < WM; ++a) acc[a] = f32x16(bv[a]);
+        const float *xrow = xs + li * KS + lh;
+        const float *wcol = wt + lh * Mp + li;
+        for (int s2 = 0; s2 < Kp; s2 += 2) {
+            const float xa = xrow[s2];
+#pragma unroll
+            for (int a = 0; a < WM; ++a)
+                acc[a] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, wcol[s2 * Mp + a * 32], acc[a], 0, 0, 0);
+        }
+        // C/D: column (m) = lane % 32, row (n) = (r & 3) + 8 (r >> 2) + 4 (lane / 32)
+#pragma unroll
+        for (int a = 0; a < WM; ++a) {
+            const int m = a * 32 + li;
+            if (m >= M) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t nr = n0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (nr < N) Y[nr * ldy + m] = acc[a][r];
+            }
+        }
+        __syncthreads();  // the tile buffers are refilled next round
+    }
+}
+
 // Narrow outputs (M <= 4: the attention Linears, out = 1): a (k, m) tile would leave most
 // lanes idle and the kernel latency-bound.  Here KL lanes span a row's K columns (CH per
 // lane past 64), a wave covers 64/KL rows per step with 4 steps' loads in flight, and every
@@ -366,4 +447,43 @@ extern "C" int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const f
     st = reduce_partials((int64_t)M * K, pl.P, part, part2, dW, accumulate, hs);
     if (st || !db) return st;
     return reduce_partials((int64_t)M, pl.P, bpart, bpart2, db, accumulate, hs);
+}
+
+extern "C" int gala_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,
+                                const float *W, const float *b, float *Y, int64_t ldy,
+                                void *stream) {
+    if (n_rows < 0 || K < 0 || M < 0 || ldx < K || ldy < M) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0 || M == 0) return GALA_OK;
+    const int wm = (M + 31) / 32;
+    if (wm > 8 || (int64_t)((K + 1) & ~1) * 32 * wm > kFwdMaxKM) return GALA_ERR_UNSUPPORTED;
+    if (!Y || (K > 0 && (!X || !W))) return GALA_ERR_INVALID_ARG;
+    const int64_t tiles = (n_rows + 31) / 32;
+    int64_t blocks = (tiles + 3) / 4;
+    if (blocks > 256 * 4) blocks = 256 * 4;  // blocks then walk 4-tile groups grid-stride
+    const int Kp = (K + 1) & ~1;
+    const size_t lds = sizeof(float) * ((size_t)Kp * 32 * wm + 4 * 32 * (size_t)(Kp + 1));
+    if (lds > 64 * 1024) return GALA_ERR_UNSUPPORTED;
+    const bool v4 = K % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X % 16) == 0;
+    hipStream_t hs = (hipStream_t)stream;
+#define GALA_FF(WMV)                                                                                          \
+    do {                                                                                                  \
+        if (v4)                                                                                           \
+            hipLaunchKernelGGL((k_ffn_fwd<WMV, 4>), dim3((unsigned)blocks), dim3(kBlock), lds, hs, n_rows, K, M, \
+                               X, ldx, W, b, Y, ldy);                                                     \
+        else                                                                                              \
+            hipLaunchKernelGGL((k_ffn_fwd<WMV, 1>), dim3((unsigned)blocks), dim3(kBlock), lds, hs, n_rows, K, M, \
+                               X, ldx, W, b, Y, ldy);                                                     \
+    } while (0)
+    switch (wm) {
+        case 1: GALA_FF(1); break;
+        case 2: GALA_FF(2); break;
+        case 3: GALA_FF(3); break;
+        case 4: GALA_FF(4); break;
+        case 5: GALA_FF(5); break;
+        case 6: GALA_FF(6); break;
+        case 7: GALA_FF(7); break;
+        default: GALA_FF(8); break;
+    }
+#undef GALA_FF
+    return launch_status();
 }

@@ -75,6 +75,7 @@ SIGNATURES = {
     "gala_spmm_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _P]),
     "gala_degree_f32": (ctypes.c_int, [_CSR, _P, _F, _I32, _I32, _P]),
     "gala_row_broadcast_f32": (ctypes.c_int, [_I64, _I32, _P, _P, _I64, _P, _I64, _P]),
+    "gala_ffn_fwd_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P]),
     "gala_row_scale_relu_f32": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _I64, _P, _I64, _P]),
     "gala_relu_scale_backward_f32": (ctypes.c_int, [_I64, _I32, _P, _P, _I64, _P, _I64, _P, _I64, _P]),
     "gala_sddvv_f32": (ctypes.c_int, [_CSR, _P, _P, _I32, _I32, _F, _P, _P]),
@@ -146,7 +147,7 @@ def call(fn: str, *args) -> int:
 
 # operators with a host-CPU counterpart gala_cpu_X in libgala_cpu.so (include/gala_cpu.h)
 CPU_OPS = ("gala_spmm_f32", "gala_degree_f32", "gala_row_broadcast_f32", "gala_row_scale_relu_f32",
-           "gala_relu_scale_backward_f32", "gala_sddvv_f32",
+           "gala_relu_scale_backward_f32", "gala_ffn_fwd_f32", "gala_sddvv_f32",
            "gala_row_sum_f32", "gala_row_scale_f32", "gala_sddmm_dot_f32",
            "gala_edge_softmax_fwd_f32", "gala_edge_softmax_bwd_f32", "gala_gat_fwd_f32",
            "gala_gat_bwd_f32", "gala_gat_fwd_attn_f32", "gala_gat_bwd_attn_f32",

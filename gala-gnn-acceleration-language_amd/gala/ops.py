@@ -284,6 +284,19 @@ def edge_permute(perm, src, heads=1):
     return dst
 
 
+def ffn_fwd(X, W, b=None, out=None):
+    """Y = X W^T + b on the matrix cores (gala_ffn_fwd_f32; W^T must fit 16K floats)."""
+    X = X if X.stride(1) == 1 else X.contiguous()
+    W = W.contiguous()
+    N, K = X.shape
+    M = W.shape[0]
+    if out is None:
+        out = torch.empty((N, M), device=X.device, dtype=torch.float32)
+    _abi.call("gala_ffn_fwd_f32", N, K, M, _dp(X), max(X.stride(0), K), _dp(W), _dp(b), _dp(out),
+              out.stride(0), _stream())
+    return out
+
+
 def dense_grad(X, dY, bias=True, dW=None, db=None, accumulate=False):
     """FFN weight / bias gradients dW = dY^T X [M, K], db = dY.sum(0) (gala_dense_grad_f32)."""
     # row strides pass through (row-padded views included); columns must be unit-stride

@@ -23,6 +23,7 @@ struct Backend {
     decltype(&gala_row_broadcast_f32) row_broadcast;
     decltype(&gala_row_scale_relu_f32) scale_relu;
     decltype(&gala_relu_scale_backward_f32) relu_bwd;
+    decltype(&gala_ffn_fwd_f32) ffn_fwd;
     decltype(&gala_sddvv_f32) sddvv;
     decltype(&gala_row_sum_f32) row_sum;
     decltype(&gala_row_scale_f32) row_scale;
@@ -38,13 +39,14 @@ struct Backend {
     decltype(&gala_dense_grad_f32) dense_grad;
 };
 const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
-                   gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_sddvv_f32,
+                   gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_ffn_fwd_f32,
+                   gala_sddvv_f32,
                    gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
-                   gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32,
+                   gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
                    gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
@@ -936,22 +938,45 @@ struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
     }
 };
 
-// FFN_OP with the weight / bias gradients on gala_dense_grad_f32 (split over rows) and dX
-// on the library GEMM; the forward is at::linear's addmm, bit for bit.
+// X W^T (+ b) for one Linear: on gala_ffn_fwd_f32 where it beats the library GEMM on this
+// chip -- a GPU operand with 33..64 outputs from at most 64 inputs (Products' 32 -> 47:
+// 0.28 vs 0.44 ms, tools/dense_bench.py) -- else at::addmm.
+torch::Tensor linear_fwd(const torch::Tensor &X, const torch::Tensor &W, const torch::Tensor &b) {
+    const bool has_b = b.defined() && b.numel() > 0;
+    const int64_t K = W.size(1), M = W.size(0);
+    if (X.is_cuda() && X.dim() == 2 && X.scalar_type() == torch::kFloat && X.stride(1) == 1 &&
+        M > 32 && M <= 64 && K <= 64) {
+        auto w = W.contiguous();
+        torch::Tensor bb = has_b ? b.contiguous() : torch::Tensor();
+        auto Y = torch::empty({X.size(0), M}, fopts(X));
+        const int st = be(X).ffn_fwd(X.size(0), (int32_t)K, (int32_t)M, X.data_ptr<float>(),
+                                     std::max<int64_t>(X.stride(0), K), w.data_ptr<float>(),
+                                     has_b ? bb.data_ptr<float>() : nullptr, Y.data_ptr<float>(), M,
+                                     stream_of(X));
+        if (st != GALA_ERR_UNSUPPORTED) {
+            check(st, "gala_ffn_fwd_f32");
+            return Y;
+        }
+    }
+    return has_b ? torch::addmm(b, X, W.t()) : X.mm(W.t());
+}
+
+// FFN_OP: forward linear_fwd (matrix cores for the narrow widths, else at::addmm); weight /
+// bias gradients on gala_dense_grad_f32 (split over rows); dX = dY W through linear_fwd
+// with W^T.
 struct Ffn : public torch::autograd::Function<Ffn> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor weight,
                                  torch::Tensor bias) {
         ctx->save_for_backward({X, weight});
         ctx->saved_data["has_bias"] = bias.defined() && bias.numel() > 0;
-        return bias.defined() && bias.numel() > 0 ? torch::addmm(bias, X, weight.t())
-                                                  : X.mm(weight.t());
+        return linear_fwd(X, weight, bias);
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         torch::Tensor X = sv[0].contiguous(), W = sv[1];
         torch::Tensor dY = grad_outputs[0].contiguous();
         const bool has_bias = ctx->saved_data["has_bias"].toBool();
-        torch::Tensor dX = ctx->needs_input_grad(0) ? dY.mm(W) : torch::Tensor();
+        torch::Tensor dX = ctx->needs_input_grad(0) ? linear_fwd(dY, W.t(), torch::Tensor()) : torch::Tensor();
         check_dev(X, torch::kFloat, "X");
         check_dev(dY, torch::kFloat, "dY");
         const int64_t N = X.size(0);

@@ -68,6 +68,8 @@ int gala_cpu_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float 
                               float *d_aL, void *stream);
 int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                               float *dst, void *stream);
+int gala_cpu_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,
+                         const float *W, const float *b, float *Y, int64_t ldy, void *stream);
 int64_t gala_cpu_dense_grad_workspace(int64_t n_rows, int32_t K, int32_t M);
 int gala_cpu_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,
                             const float *dY, int64_t ldy, float *dW, float *db,

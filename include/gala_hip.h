@@ -372,6 +372,16 @@ int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, in
                         void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * FFN forward on tall-skinny node matrices: Y[n, :] = X[n, 0:K] W^T + b, W [M, K] row-major
+ * (a torch Linear weight), b [M] or NULL.  Exact-f32 matrix cores, W^T held in LDS: K * M up
+ * to 16384 floats (rounded up to 32-column tiles), else GALA_ERR_UNSUPPORTED (callers use
+ * the library GEMM).  Replaces the forward of the generated programs' FFN_OP
+ * (common.h:1188-1242, torch::nn::Linear in the reference) and, with W^T, its dX.
+ */
+int gala_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,
+                     const float *W, const float *b, float *Y, int64_t ldy, void *stream);
+
+/*
  * One level of the training-subgraph transformation (getMaskSubgraphs,
  * tests/common.h:21-110; requested by middle-end.h:39-211 and emitted by
  * codegen/common.h:480-492): out = the rows i with mask[i] > 0 (all their edges, in

@@ -689,3 +689,35 @@ def test_row_scale_relu_matches_torch_chain(F, padded):
         assert torch.equal(torch.nan_to_num(got_dx, nan=123.0), torch.nan_to_num(want_dx, nan=123.0))
     if padded:
         assert bool(torch.all(xb[:, F:] == 5.0))
+
+
+@pytest.mark.parametrize("N,K,M", [(100000, 100, 32), (50000, 32, 47), (50000, 47, 32), (20000, 48, 128),
+                                   (7000, 32, 172), (3000, 32, 256), (33, 7, 3), (1, 1, 1), (0, 16, 8),
+                                   (4097, 5, 40)])
+def test_ffn_fwd_matches_float64(N, K, M):
+    """Y = X W^T + b on the matrix cores: |err| <= 1e-5 * sum_k |x w| + 1e-6 (fp32 chain)."""
+    rng = np.random.default_rng(N + 7 * K + M)
+    X = rng.uniform(-1, 1, (N, K)).astype(np.float32)
+    W = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    b = rng.uniform(-1, 1, M).astype(np.float32)
+    Y = host(ops.ffn_fwd(dev(X), dev(W), dev(b)))
+    want = X.astype(np.float64) @ W.astype(np.float64).T + b
+    mass = np.abs(X.astype(np.float64)) @ np.abs(W.astype(np.float64)).T + np.abs(b)
+    assert np.all(np.abs(Y - want) <= 1e-5 * mass + 1e-6)
+    Y2 = host(ops.ffn_fwd(dev(X), dev(W), None))  # no bias, and deterministic
+    assert np.all(np.abs(Y2 - (want - b)) <= 1e-5 * mass + 1e-6)
+
+
+def test_ffn_fwd_strided_and_unsupported():
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-1, 1, (5000, 47)).astype(np.float32)
+    W = rng.uniform(-1, 1, (40, 47)).astype(np.float32)
+    Xb = torch.full((5000, 48), float("nan"), device=DEV)
+    Xb[:, :47] = dev(X)
+    Yb = torch.full((5000, 44), 7.0, device=DEV)
+    ops.ffn_fwd(Xb[:, :47], dev(W), out=Yb[:, :40])
+    np.testing.assert_allclose(host(Yb[:, :40]), X.astype(np.float64) @ W.T.astype(np.float64), atol=1e-4, rtol=1e-5)
+    assert bool(torch.all(Yb[:, 40:] == 7.0))
+    with pytest.raises(_abi.GalaError):
+        ops.ffn_fwd(dev(rng.uniform(-1, 1, (10, 602)).astype(np.float32)),
+                    dev(rng.uniform(-1, 1, (256, 602)).astype(np.float32)))

@@ -34,9 +34,16 @@ def main():
         t_gala = timed(lambda: ops.dense_grad(X, dY))
         t_torch = timed(lambda: (dY.t().mm(X), dY.sum(0)))
         byts = 4 * N * (K + M)
-        print(json.dumps({"N": N, "K": K, "M": M, "gala_ms": round(t_gala, 4),
-                          "torch_ms": round(t_torch, 4),
-                          "gala_GBps": round(byts / t_gala / 1e6, 1)}), flush=True)
+        line = {"N": N, "K": K, "M": M, "gala_ms": round(t_gala, 4), "torch_ms": round(t_torch, 4),
+                "gala_GBps": round(byts / t_gala / 1e6, 1)}
+        W = torch.rand(M, K, device="cuda")  # forward Y = X W^T + b, where supported
+        b = torch.rand(M, device="cuda")
+        try:
+            line["fwd_gala_ms"] = round(timed(lambda: ops.ffn_fwd(X, W, b)), 4)
+            line["fwd_torch_ms"] = round(timed(lambda: torch.addmm(b, X, W.t())), 4)
+        except Exception:
+            pass
+        print(json.dumps(line), flush=True)
         del X, dY
 
 
