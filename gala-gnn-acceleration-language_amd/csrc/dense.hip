@@ -3,9 +3,9 @@
 // The generated programs' FFNs are torch Linear layers on [N, K] node features with
 // N = 10^5..10^8 and K, M <= a few hundred (gala.cu:415-420, common.h:1188-1242).  Their
 // backward needs dW[m, k] = sum_n dY[n, m] X[n, k] and db[m] = sum_n dY[n, m]: a GEMM whose
-// contraction runs over the N rows.  Measured on the Products GCN program, torch's bias
-// reduction over dim 0 takes 18.6 ms and the weight GEMM 3.3 ms (profiles/r01_e2e_*), for
-// 1.3 GB of input that HBM streams in ~0.2 ms.  Here the rows are split into P chunks
+// contraction runs over the N rows.  Measured on the Products GCN program before this
+// kernel, torch's bias reduction over dim 0 took 18.6 ms and the weight GEMM 3.3 ms, for
+// 1.3 GB of input that HBM streams in ~0.2 ms (tools/dense_bench.py times both).  Here the rows are split into P chunks
 // (split-K) and a second kernel sums the P partials in a fixed order:
 //  * k_tn_mfma: every wave owns a (32 WM) x (32 WK) tile of dW for one row chunk and runs
 //    it on the exact-f32 matrix cores (v_mfma_f32_32x32x2_f32: each instruction takes two
