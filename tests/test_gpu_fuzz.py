@@ -132,3 +132,69 @@ def test_random_case(seed):
         np.testing.assert_allclose(_host(daL), daL_ref, **TOL)
         if mode == _abi.GALA_SOFTMAX_FIXED:
             np.testing.assert_allclose(_host(dz), dz_ref, **TOL)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("GALA_FUZZ_CASES", "96")) // 2))
+def test_random_case_more_ops(seed):
+    """The rest of the surface on the same random graphs: kernel-sampled and multi-head
+    weighted SpMM with norms (bit-exact), the attention-recompute GAT kernels, the ReLU
+    prologue (bit-exact vs the torch chain), FFN forward / gradients (fp32 bounds)."""
+    rng = np.random.default_rng(77000 + seed)
+    g = _graph(rng)
+    og = to_oracle(g)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    F = int(rng.integers(1, 130))
+    X = rng.uniform(-1, 1, (g.n_cols, F)).astype(np.float32)
+    # kernel sampling (a6): nsamp draws per non-empty row, (ra * j + rb) mod deg
+    ns, ra, rb = int(rng.integers(1, 30)), int(rng.integers(1, 50)), int(rng.integers(0, 50))
+    np.testing.assert_array_equal(_host(ops.spmm(dg, _dev(X), nsamp=ns, ra=ra, rb=rb)),
+                                  orc.spmm(og, X, sample=True, nsamp=ns, ra=ra, rb=rb))
+    # multi-head weights with src / dst norms
+    H = int(rng.choice([1, 2, 4]))
+    D = int(rng.choice([1, 4, 8, 16]))
+    Xh = rng.uniform(-1, 1, (g.n_cols, H * D)).astype(np.float32)
+    val = rng.uniform(0, 1, g.nnz * H).astype(np.float32)
+    sn = rng.uniform(0.1, 1, g.n_cols).astype(np.float32)
+    dn = rng.uniform(0.1, 1, g.n_rows).astype(np.float32)
+    got = _host(ops.spmm(dg.with_values(_dev(val), val_heads=H), _dev(Xh), src_scale=_dev(sn), dst_scale=_dev(dn)))
+    np.testing.assert_array_equal(got, orc.spmm(to_oracle(g, val, H), Xh, src_scale=sn, dst_scale=dn))
+    # ReLU prologue: pre * relu(act * X) and its backward vs the torch chain, bit for bit
+    Xd, Gd = _dev(X), _dev(rng.uniform(-1, 1, (g.n_cols, F)).astype(np.float32))
+    act, pre = _dev(rng.uniform(0.1, 2, g.n_cols).astype(np.float32)), _dev(rng.uniform(0.1, 2, g.n_cols).astype(np.float32))
+    t = act[:, None] * Xd
+    assert torch.equal(ops.row_scale_relu(Xd, act, pre), pre[:, None] * torch.relu(t))
+    assert torch.equal(ops.relu_scale_backward(Xd, Gd, act),
+                       torch.where(torch.relu(t) <= 0, torch.zeros_like(Gd), Gd) * act[:, None])
+    # attention recompute (one head): aR = X wR + bR inside the kernels
+    if g.nnz and F <= 64:
+        aL = rng.uniform(-1, 1, (g.n_rows, 1)).astype(np.float32)
+        wR = (rng.uniform(-1, 1, F) * 0.5).astype(np.float32)
+        bR = np.array([0.1], np.float32)
+        aR = (X.astype(np.float64) @ wR.astype(np.float64) + 0.1).astype(np.float32)
+        for mode in (_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED):
+            Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=1, slope=0.2, mode=mode)
+            Y, al = ops.gat_fwd_attn(dg, _dev(aL), _dev(wR), _dev(bR), _dev(X), slope=0.2, mode=mode, want_alpha=True)
+            np.testing.assert_allclose(_host(al), al_ref, **TOL)
+            np.testing.assert_allclose(_host(Y), Y_ref, **TOL)
+        dY = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+        _, al_ref = orc.gat_fwd(og, aL, aR, X, heads=1, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+        _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=1, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+        daL = ops.gat_bwd_attn(dg, _dev(aL), _dev(wR), _dev(bR), _dev(X), _dev(dY), _dev(al_ref), slope=0.2)
+        np.testing.assert_allclose(_host(daL), daL_ref, **TOL)
+    # FFN: forward (where supported) and weight / bias gradients
+    N, K, M = g.n_cols, F, int(rng.integers(1, 70))
+    W = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    b = rng.uniform(-1, 1, M).astype(np.float32)
+    want = X.astype(np.float64) @ W.T.astype(np.float64) + b
+    mass = np.abs(X.astype(np.float64)) @ np.abs(W.T.astype(np.float64)) + np.abs(b)
+    try:
+        Y = _host(ops.ffn_fwd(_dev(X), _dev(W), _dev(b)))
+        assert np.all(np.abs(Y - want) <= (K + 1) * 2.0**-24 * mass + 1e-6)
+    except _abi.GalaError as e:
+        assert e.status == _abi.GALA_ERR_UNSUPPORTED
+    dY = rng.uniform(-1, 1, (N, M)).astype(np.float32)
+    dW, db = ops.dense_grad(_dev(X), _dev(dY))
+    gw = dY.astype(np.float64).T @ X.astype(np.float64)
+    gm = np.abs(dY.astype(np.float64)).T @ np.abs(X.astype(np.float64))
+    assert np.all(np.abs(_host(dW) - gw) <= (N + 1) * 2.0**-24 * gm + 1e-6)
+    np.testing.assert_allclose(_host(db), dY.astype(np.float64).sum(0), atol=(N + 1) * 2.0**-24 * N + 1e-6)
