@@ -9,52 +9,94 @@ One step = the hot-path work of one GCN-2 training epoch of the generated progra
     layer-2 forward   H2 = norm * A (norm * H1)         gala_spmm_f32 (dst norm fused),
     layer-2 backward dH1 = norm * A (norm * dH2)        F = 32, fp32
     layer-1 backward  dX = norm * A (norm * dH1)        (undirected: same CSR, gala.cu:403-413)
-Edges counted per step = 4 * E per GPU (the four aggregations; the degree pass is timed
-but not counted).  The dense layers and activations of the epoch are torch, not the
+Edges counted per step = 4 * E of the graph (the four aggregations; the degree pass is
+timed but not counted).  The dense layers and activations of the epoch are torch, not the
 hot path, and are not part of the step.
 
-N = 1: the ogbn-products-shaped graph (N=2,449,029 vertices, E=126,167,309 stored edges
-incl. self loops), uniform random symmetric edges, X ~ U[-1,1).
-N > 1 (one process per GPU, RCCL): weak scaling over vertex partitions (gala/dist.py):
-every GPU owns an ogbn-products-sized partition (same N and E per GPU); 10% of each
-partition's edges are cut edges to the other partitions' boundary vertices (10% of each
-partition), whose feature rows arrive by one RCCL all-gather per aggregation, overlapped
-with the local-edge SpMM.
+The graph: ogbn-products shape (N=2,449,029 vertices, E=126,167,309 stored edges incl.
+self loops), uniform random symmetric edges (seed 42), X ~ U[-1,1).  At N = 1 an R-MAT
+graph of the same shape is timed as a second family (field "rmat").
+
+N > 1 GPUs: STRONG scaling of that one graph (one process per GPU, RCCL over xGMI).
+Every rank partitions the same graph (gala/dist.py, gala/vertex_cut.py) and the bench
+times each candidate layout for a few steps, then runs the timed steps with the fastest:
+    halo-exact     row partition, the halo gathered first, one SpMM (bit-exact vs 1 GPU)
+    halo-overlap   row partition, own-column edges overlap the halo, halo edges after
+    halo-pipe      row partition, the halo all-gathered in 4 row chunks, each chunk's
+                   edges accumulated as it lands
+    vcut / vcut-pipe  column ownership, partial rows reduce-scattered (1 / 4 chunks,
+                   chunk k's reduce-scatter overlapping chunk k+1's SpMM)
+The JSON line carries every candidate's step time and the per-aggregation halo bytes and
+exchange time ("comm"), and the weak-scaling number of the earlier design (one
+Products-sized synthetic partition per GPU) as the secondary field "weak".
+
+Launch: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run on
+127.0.0.1) unless it already runs under a launcher (WORLD_SIZE set, which must equal N).
+`--device cpu` runs the same code on the host-CPU backend with gloo (plumbing checks only).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gala-gnn-acceleration-language_amd"))
 
-from gala import dist as gdist  # noqa: E402
-from gala import layout, ops  # noqa: E402
-
 PRODUCTS_N = 2_449_029
 PRODUCTS_E = 126_167_309          # 2 * 61,859,140 undirected + N self loops
 HBM_PEAK = 8.0e12                 # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PIPE_CHUNKS = 4
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def spmm_alg_bytes(n_rows, n_cols_read, nnz, F):
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n: int) -> int:
+    """Start n ranks of this script under torch.distributed.run (before any GPU call in
+    this process) and return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, min(16, (os.cpu_count() or 8) // n))))
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def spmm_alg_bytes(n_rows, n_cols_read, nnz, F, out_rows=None):
     """SURVEY §8(d) unweighted SpMM: 4(N+1) + 4E + 4*N*F (X read once) + 4*N*F (Y write),
     + 4N for the fused dst norm."""
-    return 4 * (n_rows + 1) + 4 * nnz + 4 * n_cols_read * F + 4 * n_rows * F + 4 * n_rows
+    out_rows = n_rows if out_rows is None else out_rows
+    return 4 * (n_rows + 1) + 4 * nnz + 4 * n_cols_read * F + 4 * out_rows * F + 4 * n_rows
 
 
-def cpu_baseline(g: layout.HostGraph, F: int, budget_s: float = 20.0):
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(g, F: int, budget_s: float = 20.0):
     """Reference CPU aggregation on the host cores (rank 0, N=1 only)."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     og = orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col, None)
@@ -70,10 +112,12 @@ def cpu_baseline(g: layout.HostGraph, F: int, budget_s: float = 20.0):
         fn()
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
-    return {"value": g.nnz / t, "unit": "edges/s", "cores": cores, "kind": kind,
+    return {"value": g.nnz / t, "unit": "edges/s", "cores": cores, "kind": kind, "cpu_model": cpu_model(),
             "sample": f"{len(times)} full-graph F={F} SpMM calls (E={g.nnz}) after 1 warm-up, median "
                       f"{t:.3f} s; " + ("reference gSpMM+wsumAgg (src/ops/aggregators.h) compiled from "
-                                        "/root/reference, OpenMP" if kind == "reference"
+                                        "/root/reference, OpenMP (oracle/_ref, shipped on purpose: "
+                                        "north_star asks for the reference CPU path timed in the same run)"
+                                        if kind == "reference"
                                         else "oracle restatement of gSpMM, OpenMP")}
 
 
@@ -90,12 +134,40 @@ def load_traffic(kernel_substr: str):
     return None
 
 
-def gather_ceiling(col, X, stream, reps=10):
+class Timer:
+    """HIP events on the current stream (device runs) or wall time (host runs)."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+
+    def __call__(self, fn, reps):
+        import numpy as np
+        import torch
+        if not self.cuda:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            return (time.perf_counter() - t0) / reps
+        stream = torch.cuda.current_stream()
+        ts = []
+        for _ in range(reps):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            ts.append((a, b))
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ts])) / 1e3
+
+
+def gather_ceiling(col, X, timer, reps=10):
     """Time (HIP events, same stream) an unordered gather of the very rows the SpMM fetches:
     X[col[e]] for every edge e, any order, no row bookkeeping, no output rows
     (tools/gather_ceiling.hip -> tools/libgala_probe.so).  The floor for any kernel that
     fetches one X row per edge.  None when the probe library was not built."""
     import ctypes
+    import torch
     path = os.path.join(ROOT, "tools", "libgala_probe.so")
     if not os.path.exists(path) or X.shape[1] not in (32, 128, 256):
         return None
@@ -106,107 +178,173 @@ def gather_ceiling(col, X, stream, reps=10):
                    ctypes.c_void_p]
     E, F = col.numel(), X.shape[1]
     out = torch.empty(((E + 63) // 64, F), device=X.device, dtype=torch.float32)
-    args = (col.data_ptr(), X.data_ptr(), E, F, out.data_ptr(), stream.cuda_stream)
+    args = (col.data_ptr(), X.data_ptr(), E, F, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     if fn(*args) != 0:
         return None
-    return event_time(lambda: fn(*args), reps, stream)
+    return timer(lambda: fn(*args), reps)
 
 
-def event_time(fn, reps, stream):
-    ts = []
-    for _ in range(reps):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        fn()
-        b.record(stream)
-        ts.append((a, b))
-    torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in ts])) / 1e3
+def products_graph(kind: str, scale: float):
+    from gala import layout
+    n = max(int(PRODUCTS_N * scale), 2)
+    E = n + 2 * ((int(PRODUCTS_E * scale) - n) // 2)
+    return layout.gen_graph(kind, n, (E - n) // 2, seed=42)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--F", type=int, default=32)
-    ap.add_argument("--scale", type=float, default=1.0, help="per-GPU graph size multiplier (debug)")
-    ap.add_argument("--cut-frac", type=float, default=0.1)
-    ap.add_argument("--boundary-frac", type=float, default=0.1)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+class OneGpuGCN:
+    """The single-device step: norm * A (norm * H) with the dst norm fused into the SpMM."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        import torch.distributed as dist
-        backend = os.environ.get("GALA_DIST_BACKEND", "nccl")  # gloo: 1-GPU rehearsal only
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+    def __init__(self, hg, F, be):
+        self.be, self.F = be, F
+        self.g = be.graph(hg)
+        self.norm = be.degree(self.g)
+        self.Xs = be.empty(hg.n_cols, F)
+        self.n = hg.n_rows
+        self.nnz = hg.nnz
 
-    n = int(PRODUCTS_N * args.scale)
-    E = n + 2 * ((int(PRODUCTS_E * args.scale) - n) // 2)
-    F = args.F
-    t0 = time.time()
-    part = gdist.make_partition(rank, world, n, E, cut_frac=args.cut_frac,
-                                boundary_frac=args.boundary_frac, seed=42)
-    hg = part.graph
-    log(f"[rank {rank}/{world}] partition n={hg.n_rows} cols={hg.n_cols} E={hg.nnz} "
-        f"(cut {part.n_cut_edges}) built in {time.time() - t0:.1f}s")
-    agg = gdist.DistGCNAggregator(part, F, dev)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    X = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
-    dY = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
-    H1, H2, G1, G0 = (torch.empty_like(X) for _ in range(4))
-    stream = torch.cuda.current_stream()
+    def refresh_norm(self):
+        self.norm = self.be.degree(self.g)          # recomputed every forward (gala.cu:433-440)
+
+    def __call__(self, H, out):
+        self.be.row_broadcast(self.norm, H, self.Xs)
+        return self.be.spmm(self.g, self.Xs, out, self.norm, False)
+
+
+def make_step(agg, X, dY, bufs):
+    H1, H2, G1, G0 = bufs
 
     def step():
-        agg.norm = ops.degree(agg.full, power=-0.5)   # recomputed every forward (gala.cu:433-440)
+        agg.refresh_norm()
         agg(X, H1)
         agg(H1, H2)
         agg(dY, G1)
         agg(G1, G0)
+    return step
 
-    for _ in range(args.warmup):
+
+def timed_steps(step, steps, warmup, sync, barrier, reduce_max):
+    for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
+    barrier()
+    sync()
     w0 = time.perf_counter()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - w0
-    if world > 1:
-        t = torch.tensor([wall], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        wall = float(t.item())
-    t_step = wall / args.steps
-    value = world * 4 * hg.nnz / t_step
+    sync()
+    barrier()
+    sync()
+    return reduce_max(time.perf_counter() - w0) / steps
 
-    # dominant kernel, measured live with HIP events on the launch stream: the local
-    # (segment-0) SpMM of one aggregation = the whole-graph SpMM at N = 1
-    seg0 = agg.segs[0]
-    Y = torch.empty_like(X)
-    t_kernel = event_time(lambda: ops.spmm(seg0, agg.Xs, dst_scale=agg.norm, out=Y), 10, stream)
-    alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, seg0.nnz, F)
-    achieved = alg / t_kernel
-    gather_bytes = 4 * (hg.n_rows + 1) + seg0.nnz * (4 + 4 * F) + 4 * hg.n_rows * F
-    traffic = load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>") if world == 1 else None
+
+# ---- strong-scaling candidates ---------------------------------------------------------------
+class HaloMode:
+    def __init__(self, name, part, F, be, comm, exact):
+        from gala import dist as gdist
+        self.name, self.part = name, part
+        self.agg = gdist.DistAggregator(part, F, be, comm, exact=exact)
+        self.be, self.comm, self.F = be, comm, F
+
+    def kernel(self, timer):
+        """(seconds, algorithmic bytes) of the rank's SpMM over all its edges."""
+        a, p = self.agg, self.part
+        Y = self.be.empty(p.n, self.F)
+        t = timer(lambda: self.be.spmm(a.graph, a.Xs, Y, a.norm, False), 10)
+        return t, spmm_alg_bytes(p.n, p.n + p.n_halo_rows, p.graph.nnz, self.F)
+
+    def exchange(self, timer):
+        a = self.agg
+        if a.exchange is None:
+            return 0.0
+        return timer(lambda: [self.comm.wait(w) for w in a.exchange.start(a.Xs)], 5)
+
+
+class VcutMode:
+    def __init__(self, name, part, F, be, comm):
+        from gala import vertex_cut as vc
+        self.name, self.part = name, part
+        self.agg = vc.VertexCutAggregator(part, F, be, comm)
+        self.be, self.comm, self.F = be, comm, F
+
+    def kernel(self, timer):
+        a, p = self.agg, self.part
+        rows = p.world * p.block
+
+        def run():
+            for k, gk in enumerate(a.graphs):
+                self.be.spmm(gk, a.Xs, a.partial[k * rows:(k + 1) * rows], None, False)
+        t = timer(run, 10)
+        nnz = sum(h.nnz for h in p.chunk_graphs)
+        alg = 4 * (p.partial_rows() + p.chunks) + 4 * nnz + 4 * p.n * self.F + 4 * p.partial_rows() * self.F
+        return t, alg
+
+    def exchange(self, timer):
+        a, p = self.agg, self.part
+        rows, c = p.world * p.block, p.block
+
+        def run():
+            self.comm.wait([self.comm.reduce_scatter(a.S[k * c:(k + 1) * c], a.partial[k * rows:(k + 1) * rows])
+                            for k in range(p.chunks)])
+        return timer(run, 5)
+
+
+def run_multi(args, rank, world, dev, be, timer, sync):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from gala import dist as gdist, vertex_cut as vc
+    from gala.comm import Comm
+
+    comm = Comm()
+    F = args.F
+    t0 = time.time()
+    g = products_graph("uniform", args.scale)
+    log(f"[rank {rank}/{world}] graph N={g.n_rows} E={g.nnz} built in {time.time() - t0:.1f}s")
+    bounds = gdist.row_bounds(g.rowptr, world)
+    t0 = time.time()
+    modes = []
+    pt1 = gdist.partition_graph(g, rank, world, bounds=bounds)
+    modes.append(HaloMode("halo-exact", pt1, F, be, comm, exact=True))
+    modes.append(HaloMode("halo-overlap", pt1, F, be, comm, exact=False))
+    if pt1.halo_mode == "dense":
+        ptk = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
+        modes.append(HaloMode("halo-pipe", ptk, F, be, comm, exact=False))
+    modes.append(VcutMode("vcut", vc.vertex_cut_partition(g, rank, world, 1, bounds), F, be, comm))
+    modes.append(VcutMode("vcut-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds), F, be, comm))
+    log(f"[rank {rank}] partitions ({[m.name for m in modes]}, halo {pt1.halo_mode}, "
+        f"{pt1.n_halo_rows} halo rows) in {time.time() - t0:.1f}s")
+    n = pt1.n
+    r0 = pt1.r0
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    # every rank draws the whole X so row r is the same on any number of ranks
+    Xall = torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1
+    X = Xall[r0:r0 + n].clone()
+    dY = (torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1)[r0:r0 + n].clone()
+    del Xall
+    bufs = [be.empty(n, F) for _ in range(4)]
+
+    def barrier():
+        dist.barrier()
+
+    def reduce_max(x):
+        t = torch.tensor([x], dtype=torch.float64, device=dev if be.name == "hip" and comm.rccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    cand = {}
+    for m in modes:
+        st = make_step(m.agg, X, dY, bufs)
+        cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
+        log(f"[rank {rank}] candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
+    forced = os.environ.get("GALA_DIST_MODE")
+    best = next(m for m in modes if m.name == (forced or min(cand, key=cand.get)))
+    step = make_step(best.agg, X, dY, bufs)
+    t_step = timed_steps(step, args.steps, args.warmup, sync, barrier, reduce_max)
+    value = 4 * g.nnz / t_step
+
+    t_kernel, alg = best.kernel(timer)
+    t_ex = best.exchange(timer)
+    ref_mode = modes[0]
     out = {
         "metric": "aggregated edges/sec, GCN-2 ogbn-products (4 F=32 aggregations per step)",
         "value": value,
@@ -216,43 +354,199 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": t_step * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: uniform random symmetric graph + self loops per GPU partition (seed 42), "
-                "X~U[-1,1) fp32; N>1 adds 10% cut edges between partitions' boundary vertices",
-        "config": {"workload": "GCN-2 ogbn-products-shaped hot path per GPU: degree + 2 fwd + 2 bwd "
-                               "norm-scaled SpMM aggregations, F=32",
-                   "n_vertices_per_gpu": hg.n_rows, "edges_per_gpu": hg.nnz, "F": F,
-                   "cut_edges_per_gpu": part.n_cut_edges,
-                   "parallelism": "1 GPU" if world == 1 else f"vertex partitions x{world}, RCCL all-gather halo"},
+        "data": "synthetic: one uniform random symmetric ogbn-products-shaped graph + self loops (seed 42), "
+                "partitioned across the ranks; X~U[-1,1) fp32",
+        "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
+                               "SpMM aggregations, F=32, one graph split over the GPUs",
+                   "n_vertices": g.n_rows, "edges": g.nnz, "F": F,
+                   "parallelism": f"{best.name} x{world} (RCCL)" if comm.rccl else f"{best.name} x{world} ({dist.get_backend()})"},
+        "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": alg / t_kernel / HBM_PEAK, "traffic": None,
+                     "kernel": f"gala::k_spmm_rowgroup (rank 0's SpMM launches of mode {best.name})",
+                     "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg},
+        "comm": {"mode": best.name, "backend": dist.get_backend(),
+                 "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
+                 "halo_bytes_per_aggregation_per_rank": best.agg.halo_bytes(),
+                 "exchange_ms_per_aggregation": t_ex * 1e3,
+                 "spmm_ms_per_aggregation": t_kernel * 1e3,
+                 "halo_layout": pt1.halo_mode, "halo_rows_rank0": pt1.n_halo_rows,
+                 "note": "halo-exact is bit-identical to one GPU; the other modes agree to fp32 rounding. "
+                         "Exchange time is the collective(s) of one aggregation alone; it overlaps the SpMM "
+                         "in the -overlap/-pipe modes."},
+    }
+    del modes, ref_mode
+    if not args.no_weak:
+        out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
+    return out
+
+
+def weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max):
+    """The secondary number: one ogbn-products-sized synthetic partition per GPU, 10% of its
+    edges cut edges to other partitions' boundary rows (all-gathered, overlapped)."""
+    import torch
+    from gala import dist as gdist
+    F = args.F
+    n = max(int(PRODUCTS_N * args.scale), 2)
+    E = n + 2 * ((int(PRODUCTS_E * args.scale) - n) // 2)
+    part = gdist.make_partition(rank, world, n, E, cut_frac=0.1, boundary_frac=0.1, seed=42)
+    agg = gdist.DistGCNAggregator(part, F, be, comm)
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    X = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
+    dY = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
+    bufs = [be.empty(n, F) for _ in range(4)]
+    t = timed_steps(make_step(agg, X, dY, bufs), max(args.steps // 2, 2), 2, sync, barrier, reduce_max)
+    return {"value": world * 4 * part.graph.nnz / t, "ms_per_step": t * 1e3, "edges_per_gpu": part.graph.nnz,
+            "cut_edges_per_gpu": part.n_cut_edges, "halo_bytes_per_aggregation_per_rank": agg.halo_bytes(),
+            "note": "weak scaling: every GPU owns its own Products-sized synthetic partition"}
+
+
+def run_single(args, dev, be, timer, sync):
+    import torch
+    F = args.F
+    t0 = time.time()
+    hg = products_graph("uniform", args.scale)
+    log(f"[bench] uniform graph N={hg.n_rows} E={hg.nnz} in {time.time() - t0:.1f}s")
+    agg = OneGpuGCN(hg, F, be)
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    X = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
+    dY = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
+    bufs = [be.empty(hg.n_rows, F) for _ in range(4)]
+    ident = lambda x: x  # noqa: E731
+    t_step = timed_steps(make_step(agg, X, dY, bufs), args.steps, args.warmup, sync, lambda: None, ident)
+    value = 4 * hg.nnz / t_step
+    Y = bufs[0]
+    t_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, Y, agg.norm, False), 10)
+    alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, hg.nnz, F)
+    achieved = alg / t_kernel
+    gather_bytes = 4 * (hg.n_rows + 1) + hg.nnz * (4 + 4 * F) + 4 * hg.n_rows * F
+    out = {
+        "metric": "aggregated edges/sec, GCN-2 ogbn-products (4 F=32 aggregations per step)",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: uniform random symmetric ogbn-products-shaped graph + self loops (seed 42), "
+                "X~U[-1,1) fp32",
+        "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
+                               "SpMM aggregations, F=32",
+                   "n_vertices": hg.n_rows, "edges": hg.nnz, "F": F, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK,
+                     "traffic": load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>") if be.name == "hip" else None,
                      "kernel": "gala::k_spmm_rowgroup<VEC=4,G=8,CH=1,U=4,unweighted> (gala_spmm_f32, F=32, dst norm)",
                      "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg,
                      "gather_model_GBps": gather_bytes / t_kernel / 1e9,
                      "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json); "
                                      "uniform random columns: each edge's 128-B X row misses L2"},
-        "event_ms_per_step": ev0.elapsed_time(ev1) / args.steps,
     }
-    t_ceil = gather_ceiling(seg0.col, agg.Xs, stream)
-    if t_ceil:
-        out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
-        out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_kernel
-        out["roofline"]["gather_ceiling_note"] = (
-            "same process and graph: X[col[e]] for every edge, unordered, no output rows "
-            "(tools/gather_ceiling.hip); the SpMM's floor on a graph without reuse")
-    if world > 1:
-        send = agg.Xs[:part.b]
-        recv = agg.Xs[part.n:]
-        t_ag = event_time(lambda: torch.distributed.all_gather_into_tensor(recv, send), 5, stream)
-        out["comm"] = {"all_gather_ms": t_ag * 1e3, "bytes_per_rank_recv": int(recv.numel() * 4),
-                       "algbw_GBps": recv.numel() * 4 / t_ag / 1e9}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if be.name == "hip":
+        t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
+        if t_ceil:
+            out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
+            out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_kernel
+            out["roofline"]["gather_ceiling_note"] = (
+                "same process and graph: X[col[e]] for every edge, unordered, no output rows "
+                "(tools/gather_ceiling.hip); the SpMM's floor on a graph without reuse")
+    if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(hg, F)
         except Exception as e:  # the baseline is reported, never the target
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    del agg, X, dY, bufs
+    if not args.no_rmat:
+        out["rmat"] = rmat_family(args, dev, be, timer, sync)
+    return out
+
+
+def rmat_family(args, dev, be, timer, sync):
+    """The same step on an R-MAT graph of the Products shape: skewed
+    degrees, so the SpMM runs the degree-ordered row schedule and the hub-row chunks."""
+    import torch
+    F = args.F
+    t0 = time.time()
+    hg = products_graph("rmat", args.scale)
+    log(f"[bench] R-MAT graph N={hg.n_rows} E={hg.nnz} in {time.time() - t0:.1f}s")
+    agg = OneGpuGCN(hg, F, be)
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    X = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
+    dY = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
+    bufs = [be.empty(hg.n_rows, F) for _ in range(4)]
+    steps = max(args.steps // 2, 2)
+    t_step = timed_steps(make_step(agg, X, dY, bufs), steps, 2, sync, lambda: None, lambda x: x)
+    t_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, bufs[0], agg.norm, False), 10)
+    alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, hg.nnz, F)
+    out = {"value": 4 * hg.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
+           "graph": f"R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops, N={hg.n_rows}, E={hg.nnz}, "
+                    f"max degree {int((hg.rowptr[1:] - hg.rowptr[:-1]).max())}",
+           "split_rows": getattr(agg.g, "split_rows", 0),
+           "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
+                        "alg_bytes_per_launch": alg,
+                        "kernel": "gala_spmm_f32 (degree-ordered k_spmm_rowgroup + hub-row k_spmm_chunk/fixup)"}}
+    if be.name == "hip":
+        t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
+        if t_ceil:
+            out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
+            out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_kernel
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--F", type=int, default=32)
+    ap.add_argument("--scale", type=float, default=1.0, help="graph size multiplier (debug)")
+    ap.add_argument("--calib-steps", type=int, default=3, help="timed steps per strong-scaling candidate")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the host-CPU backend over gloo (plumbing checks, not a measurement)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rmat", action="store_true")
+    ap.add_argument("--no-weak", action="store_true")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    rank = int(os.environ.get("RANK", "0"))
+
+    import torch
+    from gala.backend import make_backend
+
+    if args.device == "cuda":
+        local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        sync = torch.cuda.synchronize
+    else:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+    be = make_backend(dev)
+    timer = Timer(dev.type == "cuda")
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("GALA_DIST_BACKEND", "nccl" if dev.type == "cuda" else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        out = run_multi(args, rank, world, dev, be, timer, sync)
+    else:
+        out = run_single(args, dev, be, timer, sync)
+    if dev.type == "cpu":
+        out["device"] = "cpu (host-CPU backend plumbing run; not a GPU measurement)"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

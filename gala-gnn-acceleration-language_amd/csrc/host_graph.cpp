@@ -232,6 +232,13 @@ extern "C" int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected
     return GALA_OK;
 }
 
+extern "C" int32_t gala_host_split_threshold(int64_t n_rows, int64_t nnz) {
+    if (n_rows < 0 || nnz < 0) return GALA_ERR_INVALID_ARG;
+    const int64_t mean_up = (nnz + n_rows - 1) / (n_rows > 0 ? n_rows : 1);  // ceil(nnz / n)
+    const int64_t thr = 8 * mean_up > 1024 ? 8 * mean_up : 1024;
+    return thr > INT32_MAX ? INT32_MAX : (int32_t)thr;
+}
+
 extern "C" int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshold,
                                     int32_t chunk, int32_t *rows, int32_t *row_chunk0,
                                     int32_t *chunk_row, int64_t *n_rows_split,

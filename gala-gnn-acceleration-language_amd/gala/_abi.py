@@ -94,6 +94,7 @@ SIGNATURES = {
     "gala_host_col_tile": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _P, _P, _P, _P, _P]),
     "gala_host_sample_ab": (ctypes.c_int, [_I64, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "gala_host_split_plan": (ctypes.c_int, [_I64, _P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "gala_host_split_threshold": (ctypes.c_int32, [_I64, _I64]),
     "gala_host_csr_transpose": (ctypes.c_int, [_I64, _I64, _P, _P, _P, _P, _P]),
     "gala_host_row_order": (ctypes.c_int, [_I64, _P, _P]),
     "gala_host_gen_graph": (ctypes.c_int, [_I32, _I64, _I64, ctypes.c_uint64, _P, _P]),

@@ -1,0 +1,117 @@
+"""The local operator tables the multi-GPU aggregators run on.
+
+`HipBackend` launches the HIP kernels of libgala_hip.so on torch's current stream (device
+tensors, gala.ops).  `CpuBackend` runs the same operators on the host cores through
+libgala_cpu.so (include/gala_cpu.h: same signatures, same per-row order and rounding, so
+its results are bit-identical to the HIP kernels').  The CPU table exists for the CPU test
+suite and for plumbing runs of bench.py (`--device cpu`); it is chosen explicitly by the
+caller and is never a fallback for a missing HIP library.
+
+Both expose the four operations one GCN aggregation `norm * A (norm * H)` needs
+(codegen/gala.cu:433-456): graph upload, SpMM, ROW_BROADCAST and the degree pass.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi
+from .layout import HostGraph
+
+
+class HipBackend:
+    name = "hip"
+
+    def __init__(self, device="cuda"):
+        from . import ops
+        self.ops = ops
+        self.device = torch.device(device)
+
+    def graph(self, hg: HostGraph, split="auto"):
+        return self.ops.DeviceGraph.from_host(hg, self.device, split=split)
+
+    def spmm(self, g, X, out, dst_scale=None, accum=False):
+        return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)
+
+    def row_broadcast(self, scale, X, out):
+        return self.ops.row_broadcast(scale, X, out=out)
+
+    def degree(self, g, power=-0.5):
+        return self.ops.degree(g, power=power)
+
+    def empty(self, *shape):
+        return torch.empty(shape, device=self.device, dtype=torch.float32)
+
+    def synchronize(self):
+        torch.cuda.synchronize(self.device)
+
+
+class CpuGraph:
+    """A HostGraph with its gala_csr_t view (host pointers) for libgala_cpu.so."""
+
+    def __init__(self, hg: HostGraph):
+        self.hg = hg
+        self.n_rows, self.n_cols = hg.n_rows, hg.n_cols
+        self.rowptr = np.ascontiguousarray(hg.rowptr, np.int32)
+        self.col = np.ascontiguousarray(hg.col, np.int32)
+        self.bounds = None if hg.bounds is None else np.ascontiguousarray(hg.bounds, np.int32)
+        c = _abi.gala_csr_t()
+        c.n_rows, c.n_cols, c.nnz = hg.n_rows, hg.n_cols, int(self.col.shape[0])
+        c.rowptr = self.rowptr.ctypes.data if hg.n_rows > 0 else None
+        c.col = self.col.ctypes.data if self.col.shape[0] > 0 else None
+        c.val, c.val_heads, c.split = None, 1, None
+        c.n_seg = hg.n_seg
+        c.seg_bounds = None if self.bounds is None else self.bounds.ctypes.data
+        self.c = c
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.shape[0])
+
+    def csr(self):
+        return ctypes.byref(self.c)
+
+
+def _hp(t: torch.Tensor):
+    if t is None:
+        return None
+    if t.is_cuda:
+        raise ValueError("CpuBackend takes host tensors")
+    return t.data_ptr()
+
+
+class CpuBackend:
+    name = "cpu"
+    device = torch.device("cpu")
+
+    def graph(self, hg: HostGraph, split="auto"):
+        return CpuGraph(hg)
+
+    def spmm(self, g: CpuGraph, X, out, dst_scale=None, accum=False):
+        flags = _abi.GALA_SPMM_ACCUM if accum else 0
+        _abi.call_cpu("gala_spmm_f32", g.csr(), _hp(X), X.stride(0), _hp(out), out.stride(0), X.shape[1],
+                      None, _hp(dst_scale), flags, 0, 5, 7, None)
+        return out
+
+    def row_broadcast(self, scale, X, out):
+        _abi.call_cpu("gala_row_broadcast_f32", X.shape[0], X.shape[1], _hp(scale), _hp(X), X.stride(0),
+                      _hp(out), out.stride(0), None)
+        return out
+
+    def degree(self, g: CpuGraph, power=-0.5):
+        out = torch.empty(g.n_rows, dtype=torch.float32)
+        _abi.call_cpu("gala_degree_f32", g.csr(), _hp(out), power, 0, 0, None)
+        return out
+
+    def empty(self, *shape):
+        return torch.empty(shape, dtype=torch.float32)
+
+    def synchronize(self):
+        pass
+
+
+def make_backend(device) -> "HipBackend | CpuBackend":
+    d = torch.device(device)
+    return CpuBackend() if d.type == "cpu" else HipBackend(d)

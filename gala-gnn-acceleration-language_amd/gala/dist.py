@@ -1,32 +1,36 @@
-"""Vertex-partitioned multi-GPU aggregation (one process per GPU, RCCL over xGMI).
+"""Multi-GPU aggregation by vertex partitions (one process per GPU, RCCL over xGMI).
 
-SURVEY §8(e): graphs that shard naturally are cut into per-GPU partitions; a GPU owns
-its vertices' feature rows and all edges whose destination it owns.  Edges whose source
-lives on another GPU ("cut" edges) read that source's feature row from a halo buffer
-filled by one RCCL all-gather of every partition's boundary rows per aggregation.
+The reference is single-GPU (no collectives anywhere); this is new work
+scoped by SURVEY §8(e).  Two families live in this package:
 
-Per-rank layout (the reference's own column-tiled layout, src/ops/tiling.h:222-283, with
-two segments):
-    columns [0, n)            local vertices                       -> segment 0
-    columns [n, n + P*b)      all partitions' boundary rows, rank q's  -> segment 1
-                              block at n + q*b (the all-gather output)
-Boundary vertices of a partition are its first b vertices, so the send buffer is a
-contiguous slice of the (norm-prescaled) feature matrix: no pack kernel.
+* **Row partitions with a halo** (this module).  Rank p owns the vertex range
+  [bounds[p], bounds[p+1)) -- its rows of A (the destinations) and their feature rows.
+  The columns an own row reads from other ranks (the halo) are fetched once per
+  aggregation, then the rank runs the SpMM over its rows.  The halo arrives either
+    - "p2p":   each peer sends exactly the rows this rank's edges read (grouped RCCL
+               send/recv, request lists exchanged once at setup), or
+    - "dense": one RCCL all-gather of every rank's rows into a padded table (used when
+               the halo is most of the graph -- a uniform graph at any P -- where the
+               all-gather moves the same bytes with RCCL's best algorithm).  The table
+               may be gathered in K row chunks so SpMM work overlaps the transfer.
+  `exact` mode runs ONE SpMM over the rank's rows once the halo is complete.  Its column
+  ids are remapped but every row keeps its CSR edge order, so the result is bit-identical
+  to the one-GPU (and reference) aggregation.  Overlap mode runs the own-column edges
+  while the halo is in flight and accumulates each halo chunk's edges when it lands
+  (exact to fp32 rounding only: a row's sum is split into per-chunk partial sums).
+* **Vertex cut** (gala/vertex_cut.py): rank p owns the columns of its range; partial
+  rows are summed into their owners by RCCL reduce-scatter.
 
-One aggregation  Y = norm * A (norm * H):
-    Xs[0:n] = norm * H                         (gala_row_broadcast_f32)
-    all_gather(Xs[n:], Xs[0:b])                 comm stream (RCCL)      } overlapped
-    Y  = norm * A_local (Xs)                    compute stream, seg 0   }
-    Y += norm * A_halo  (Xs)                    after the all-gather, seg 1 (ACCUM)
+Layouts follow the reference's column-tiled CSR (src/ops/tiling.h:222-283): a group of
+edges selected by column range, relative row offsets, rows in global order.
 
-The synthetic partition generator (weak scaling: every rank owns an ogbn-products-sized
-partition) draws local edges uniformly inside the partition and cut edges between the
-boundary sets of two partitions; both endpoints' ranks derive the same cut edges from a
-counter-based hash, so the global graph is symmetric.
+The weak-scaling generator at the top (make_partition / DistGCNAggregator) builds one
+ogbn-products-sized partition per rank with synthetic cut edges; bench.py reports it as
+the secondary weak-scaling number next to the strong-scaling run of one graph.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -46,6 +50,14 @@ def _bounded(h: np.ndarray, n: int) -> np.ndarray:
     # high 32 bits * n >> 32 (n < 2^31): unbiased enough, deterministic, vectorised
     return ((h >> np.uint64(32)) * np.uint64(n)) >> np.uint64(32)
 
+
+# ---- weak scaling: one synthetic partition per rank ---------------------------------------
+# Per-rank layout (two column segments of the tiled layout):
+#     columns [0, n)            local vertices                        -> segment 0
+#     columns [n, n + P*b)      every partition's boundary rows, rank q's block at n + q*b
+#                               (the all-gather output)               -> segment 1
+# Boundary vertices of a partition are its first b vertices, so the all-gather's send
+# buffer is a contiguous slice of the (norm-prescaled) features: no pack kernel.
 
 def cut_edges(p: int, q: int, count: int, b: int, seed: int):
     """The `count` cut edges between boundary sets of partitions p < q (u in B_p, v in B_q)."""
@@ -144,72 +156,39 @@ def global_reference_graph(parts: list[Partition]) -> layout.HostGraph:
 
 
 class DistGCNAggregator:
-    """norm * A (norm * H) over a vertex-partitioned graph (see module docstring).
+    """norm * A (norm * H) over a synthetic weak-scaling Partition: the local-edge SpMM
+    (segment 0) overlaps the all-gather of the boundary rows, the cut edges (segment 1)
+    accumulate after it.  `backend` is gala.backend.HipBackend / CpuBackend."""
 
-    spmm(g, X, out, dst_scale, accum) and row_broadcast(scale, X, out) are the local
-    device ops (gala.ops on the GPU).  The CPU gloo test injects equivalent torch ops to
-    exercise the partitioning, the halo indexing and the exchange without a GPU."""
-
-    def __init__(self, part: Partition, F: int, device, spmm=None, row_broadcast=None,
-                 degree=None, group=None):
-        import torch
-        import torch.distributed as dist
-        self.torch, self.dist = torch, dist
-        self.part, self.F, self.group = part, F, group
-        if spmm is None:
-            from . import ops
-            spmm = lambda g, X, out, dst_scale, accum: ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)  # noqa: E731
-            row_broadcast = lambda s, X, out: ops.row_broadcast(s, X, out=out)  # noqa: E731
-            degree = lambda g: ops.degree(g, power=-0.5)  # noqa: E731
-            mk = lambda hg: ops.DeviceGraph.from_host(hg, device)  # noqa: E731
-        else:
-            mk = lambda hg: hg  # noqa: E731
-        self._spmm, self._rb = spmm, row_broadcast
+    def __init__(self, part: Partition, F: int, backend, comm=None):
+        self.part, self.F, self.be = part, F, backend
+        self.comm = comm
         g = part.graph
-        self.full = mk(g)
-        self.segs = [mk(segment_view(g, s)) for s in range(g.n_seg)] if g.n_seg > 1 else [self.full]
-        self.norm = degree(self.full)
-        self.Xs = torch.empty((part.n_cols, F), device=device, dtype=torch.float32)
-        self.is_cuda = torch.device(device).type == "cuda"
-        self.comm_stream = torch.cuda.Stream(device=device) if self.is_cuda else None
+        self.full = backend.graph(g)
+        self.segs = [backend.graph(segment_view(g, s)) for s in range(g.n_seg)] if g.n_seg > 1 else [self.full]
+        self.norm = backend.degree(self.full)
+        self.Xs = backend.empty(part.n_cols, F)
+
+    def refresh_norm(self):
+        """Recompute the degree norm (the generated forward does, gala.cu:433-440)."""
+        self.norm = self.be.degree(self.full)
 
     def __call__(self, H, out):
-        torch, p = self.torch, self.part
+        be, p = self.be, self.part
         n, b = p.n, p.b
-        self._rb(self.norm, H, self.Xs[:n])                         # Xs = norm * H
+        be.row_broadcast(self.norm, H, self.Xs[:n])                       # Xs = norm * H
         if p.world == 1:
-            return self._spmm(self.segs[0], self.Xs, out, self.norm, False)
-        send = self.Xs[:b]
-        recv = self.Xs[n:]
-        if self.is_cuda:
-            ready = torch.cuda.Event()
-            ready.record()
-            with torch.cuda.stream(self.comm_stream):
-                self.comm_stream.wait_event(ready)
-                work = self.dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
-            self._spmm(self.segs[0], self.Xs, out, self.norm, False)     # local edges
-            work.wait()                                                    # current stream waits
-        else:
-            self.dist.all_gather_into_tensor(recv, send, group=self.group)
-            self._spmm(self.segs[0], self.Xs, out, self.norm, False)
-        return self._spmm(self.segs[1], self.Xs, out, self.norm, True)  # cut edges, ACCUM
+            return be.spmm(self.segs[0], self.Xs, out, self.norm, False)
+        work = self.comm.all_gather(self.Xs[n:], self.Xs[:b])
+        be.spmm(self.segs[0], self.Xs, out, self.norm, False)             # local edges, overlapped
+        self.comm.wait([work])
+        return be.spmm(self.segs[1], self.Xs, out, self.norm, True)       # cut edges, ACCUM
+
+    def halo_bytes(self) -> int:
+        return 4 * self.F * self.part.b * (self.part.world - 1)
 
 
-# ---- partitioning a given graph ----------------------------------------------------------
-# SURVEY §8(e) for graphs that arrive whole (the reference's npy datasets, config 5): rank p
-# owns the contiguous vertex range [bounds[p], bounds[p+1)) -- cut where the stored-edge
-# count (plus one per row) crosses p/P of the total -- with all edges into those rows.
-# Each rank's feature buffer Xs holds, in GLOBAL id order,
-#     [ halo rows owned by ranks < p | own rows | halo rows owned by ranks > p ]
-# so the remap global id -> Xs row is monotone and a row's edges keep their CSR order:
-# one SpMM over `graph` sums every row in exactly the single-GPU (and reference) order,
-# which makes the distributed result bit-identical to the one-GPU result.  The halo rows
-# are fetched once per aggregation by point-to-point sends/receives straight into their
-# Xs slices (RCCL grouped send/recv: only the rows a peer actually needs cross xGMI).
-# Overlap mode instead runs the own-column edges (`own_graph`) while the halo is in
-# flight and accumulates the halo edges (`halo_graph`) afterwards: faster, but a row's
-# sum is then (own part) + (halo part), exact to fp32 rounding only.
-
+# ---- strong scaling: partitioning one given graph -----------------------------------------
 
 def row_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
     """[world+1] vertex-range cuts balancing stored edges + rows per rank (deterministic:
@@ -221,28 +200,39 @@ def row_bounds(rowptr: np.ndarray, world: int) -> np.ndarray:
     return np.concatenate([[0], cuts, [n]]).astype(np.int64)
 
 
-def _csr_select(rowptr: np.ndarray, col: np.ndarray, keep: np.ndarray, n_cols: int) -> layout.HostGraph:
-    """The rows' edges with keep[e] set, CSR order preserved."""
-    n = rowptr.shape[0] - 1
-    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
-    rp = np.zeros(n + 1, np.int64)
-    np.cumsum(np.bincount(rows[keep], minlength=n), out=rp[1:])
-    return layout.HostGraph(n, n_cols, rp.astype(np.int32), np.ascontiguousarray(col[keep], np.int32))
+def _rowptr_of_selected(rowptr: np.ndarray, keep: np.ndarray) -> np.ndarray:
+    """Row offsets of the CSR restricted to the edges with keep[e] (CSR order kept)."""
+    cs = np.zeros(keep.shape[0] + 1, np.int64)
+    np.cumsum(keep, out=cs[1:])
+    return (cs[rowptr.astype(np.int64)] - cs[int(rowptr[0])]).astype(np.int32)
 
 
 @dataclass
 class GraphPartition:
+    """Rank `rank`'s rows of one graph and the column layout of its feature buffer Xs.
+
+    halo_mode "p2p":   Xs = [halo rows of lower ranks | own rows | halo rows of higher
+                       ranks], in global id order (only the rows this rank reads).
+    halo_mode "dense": Xs = a padded table of ALL rows, gathered in `chunks` row chunks;
+                       owner q's local row j sits at k*P*c + q*c + (j - k*c), k = j // c,
+                       c = `block` rows per (rank, chunk).
+    `graph` has the rank's rows with every edge (global CSR order, remapped columns);
+    `groups[0]` its own-column edges and `groups[1 + k]` the edges into halo chunk k."""
     rank: int
     world: int
     bounds: np.ndarray          # int64 [world+1] global vertex ranges
-    lo: int                     # halo rows owned by lower ranks: Xs[0:lo]
-    halo: np.ndarray            # int64 global ids of all halo rows, ascending
-    recv_counts: np.ndarray     # int64 [world] halo rows owned by each rank (0 for self)
-    graph: layout.HostGraph     # own rows over the Xs columns, global edge order (exact)
-    own_graph: layout.HostGraph   # the edges into own columns (overlap mode, first)
-    halo_graph: layout.HostGraph  # the edges into halo columns (overlap mode, second)
-    split_threshold: int = 0      # the WHOLE graph's hub-row threshold (ops.DeviceGraph.from_host):
-                                  # the same rows split into the same chunks as on one GPU
+    halo_mode: str
+    chunks: int
+    block: int                  # dense: rows per (rank, chunk) block
+    lo: int                     # p2p: Xs row of own row 0
+    halo: np.ndarray            # p2p: int64 global ids of all halo rows, ascending
+    recv_counts: np.ndarray     # p2p: int64 [world] halo rows owned by each rank (0 for self)
+    n_cols: int                 # rows of Xs
+    graph: layout.HostGraph
+    groups: list = field(default_factory=list)
+    split_threshold: int = 0      # the WHOLE graph's hub-row threshold: the same rows split
+                                  # into the same chunks as on one GPU
+    n_halo_rows: int = 0          # distinct non-own rows this rank's edges read
 
     @property
     def r0(self) -> int:
@@ -253,15 +243,41 @@ class GraphPartition:
         return int(self.bounds[self.rank + 1] - self.bounds[self.rank])
 
     @property
-    def n_cols(self) -> int:
-        return self.n + int(self.halo.shape[0])
+    def own_graph(self) -> layout.HostGraph:
+        return self.groups[0]
+
+    @property
+    def halo_graph(self) -> layout.HostGraph:
+        if len(self.groups) != 2:
+            raise ValueError("halo_graph: one halo chunk only")
+        return self.groups[1]
+
+    def own_blocks(self):
+        """[(first own row, end own row, Xs row)] where the own rows are written."""
+        if self.halo_mode == "p2p":
+            return [(0, self.n, self.lo)]
+        c, P, p = self.block, self.world, self.rank
+        out = []
+        for k in range(self.chunks):
+            j0, j1 = k * c, min((k + 1) * c, self.n)
+            if j1 > j0:
+                out.append((j0, j1, k * P * c + p * c))
+        return out
+
+    def gather_slices(self):
+        """dense: [(table rows of chunk k, this rank's block in it)] for the all-gathers."""
+        c, P, p = self.block, self.world, self.rank
+        return [(slice(k * P * c, (k + 1) * P * c), slice(k * P * c + p * c, k * P * c + (p + 1) * c))
+                for k in range(self.chunks)]
 
     @property
     def own_slice(self) -> slice:
+        if self.halo_mode != "p2p":
+            raise ValueError("own rows are not contiguous in a dense table")
         return slice(self.lo, self.lo + self.n)
 
     def recv_offsets(self) -> np.ndarray:
-        """Xs row where the block received from rank q starts ([world])."""
+        """p2p: Xs row where the block received from rank q starts ([world])."""
         off = np.zeros(self.world, np.int64)
         pos = 0
         for q in range(self.world):
@@ -273,55 +289,103 @@ class GraphPartition:
         return off
 
     def xs_to_global(self) -> np.ndarray:
-        """Global vertex id of every Xs row (int64 [n_cols])."""
-        own = np.arange(self.r0, self.r0 + self.n, dtype=np.int64)
-        return np.concatenate([self.halo[:self.lo], own, self.halo[self.lo:]])
+        """Global vertex id held by every Xs row (int64 [n_cols]; -1 for padding)."""
+        if self.halo_mode == "p2p":
+            own = np.arange(self.r0, self.r0 + self.n, dtype=np.int64)
+            return np.concatenate([self.halo[:self.lo], own, self.halo[self.lo:]])
+        out = np.full(self.n_cols, -1, np.int64)
+        N = int(self.bounds[-1])
+        out[_dense_map(self.bounds, self.block, self.world, N)] = np.arange(N, dtype=np.int64)
+        return out
+
+    def halo_bytes(self, F: int) -> int:
+        """Bytes this rank receives per aggregation."""
+        if self.halo_mode == "p2p":
+            return 4 * F * int(self.recv_counts.sum())
+        return 4 * F * self.block * self.chunks * (self.world - 1)
 
 
-def partition_graph(g: layout.HostGraph, rank: int, world: int,
-                    bounds: np.ndarray | None = None) -> GraphPartition:
-    """Rank `rank`'s share of the square one-segment graph `g` (rows = destinations)."""
+def _dense_map(bounds: np.ndarray, c: int, P: int, N: int) -> np.ndarray:
+    """Global id -> dense-table row (int64 [N])."""
+    out = np.empty(N, np.int64)
+    for q in range(P):
+        j = np.arange(int(bounds[q + 1] - bounds[q]), dtype=np.int64)
+        k = j // c
+        out[int(bounds[q]):int(bounds[q + 1])] = k * P * c + q * c + (j - k * c)
+    return out
+
+
+def partition_graph(g: layout.HostGraph, rank: int, world: int, bounds: np.ndarray | None = None,
+                    halo_mode: str = "auto", chunks: int = 1, dense_frac: float = 0.5) -> GraphPartition:
+    """Rank `rank`'s share of the square one-segment graph `g` (rows = destinations).
+    halo_mode "auto" picks "dense" when the halo exceeds dense_frac of the other ranks'
+    rows (then an all-gather moves no more than point-to-point would); chunks > 1 needs
+    the dense table (the p2p layout has one halo group)."""
     if g.n_rows != g.n_cols or g.n_seg != 1:
         raise ValueError("partition_graph needs a square, one-segment CSR")
+    N = g.n_rows
     b = row_bounds(g.rowptr, world) if bounds is None else np.asarray(bounds, np.int64)
     r0, r1 = int(b[rank]), int(b[rank + 1])
-    e0, e1 = int(g.rowptr[r0]), int(g.rowptr[r1])
-    rp = (g.rowptr[r0:r1 + 1].astype(np.int64) - e0)
-    cols = g.col[e0:e1].astype(np.int64)
-    own = (cols >= r0) & (cols < r1)
-    halo = np.unique(cols[~own])
-    lo = int(np.searchsorted(halo, r0))
     n = r1 - r0
-    xs_col = np.where(own, lo + (cols - r0), 0)
-    hidx = np.searchsorted(halo, cols[~own])
-    xs_col[~own] = np.where(hidx < lo, hidx, hidx + n)
-    xs_col = xs_col.astype(np.int32)
-    n_cols = n + int(halo.shape[0])
-    owner = np.searchsorted(b, halo, side="right") - 1
-    recv_counts = np.bincount(owner, minlength=world).astype(np.int64)
-    graph = layout.HostGraph(n, n_cols, rp.astype(np.int32), xs_col)
-    thr = max(1024, 8 * int(np.ceil(g.nnz / max(g.n_rows, 1))))
-    return GraphPartition(rank, world, b, lo, halo, recv_counts, graph,
-                          _csr_select(rp, xs_col, own, n_cols), _csr_select(rp, xs_col, ~own, n_cols), thr)
+    e0, e1 = int(g.rowptr[r0]), int(g.rowptr[r1])
+    rp = (g.rowptr[r0:r1 + 1].astype(np.int64) - e0).astype(np.int32)
+    cols = g.col[e0:e1]
+    own = (cols >= r0) & (cols < r1)
+    used = np.zeros(N, bool)
+    used[cols] = True
+    used[r0:r1] = False
+    n_halo = int(used.sum())
+    if halo_mode == "auto":
+        halo_mode = "dense" if (chunks > 1 or n_halo > dense_frac * max(N - n, 1)) else "p2p"
+    if halo_mode == "p2p" and chunks != 1:
+        raise ValueError("the p2p halo has one chunk")
+    thr = layout.split_threshold(g.n_rows, g.nnz)
+    if halo_mode == "p2p":
+        halo = np.flatnonzero(used).astype(np.int64)
+        lo = int(np.searchsorted(halo, r0))
+        xmap = np.full(N, -1, np.int64)
+        xmap[halo[:lo]] = np.arange(lo)
+        xmap[r0:r1] = lo + np.arange(n)
+        xmap[halo[lo:]] = lo + n + np.arange(halo.shape[0] - lo)
+        n_cols = n + halo.shape[0]
+        owner = np.searchsorted(b, halo, side="right") - 1
+        recv_counts = np.bincount(owner, minlength=world).astype(np.int64)
+        block, K = 0, 1
+    else:
+        K = max(int(chunks), 1)
+        m = int(np.diff(b).max(initial=0))
+        block = max((m + K - 1) // K, 1)
+        xmap = _dense_map(b, block, world, N)
+        n_cols = K * world * block
+        halo, lo, recv_counts = np.zeros(0, np.int64), 0, np.zeros(world, np.int64)
+    xs_col = xmap[cols].astype(np.int32)
+    graph = layout.HostGraph(n, n_cols, rp, xs_col)
+    groups = [layout.HostGraph(n, n_cols, _rowptr_of_selected(rp, own), xs_col[own])]
+    if halo_mode == "p2p":
+        groups.append(layout.HostGraph(n, n_cols, _rowptr_of_selected(rp, ~own), xs_col[~own]))
+    else:
+        kcol = (xs_col // (world * block)).astype(np.int32)
+        for k in range(K):
+            sel = ~own & (kcol == k)
+            groups.append(layout.HostGraph(n, n_cols, _rowptr_of_selected(rp, sel), xs_col[sel]))
+    return GraphPartition(rank, world, b, halo_mode, K, block, lo, halo, recv_counts, n_cols, graph,
+                          groups, thr, n_halo)
 
 
 class HaloExchange:
-    """Per-aggregation halo fetch for a GraphPartition: rank p sends every peer exactly
-    the own rows that peer's edges read, received straight into the peer's Xs slices.
+    """p2p halo of a GraphPartition: rank p sends every peer exactly the own rows that
+    peer's edges read, received straight into the peer's Xs slices.  Setup exchanges the
+    request lists once (counts by all_to_all_single, ids by grouped send/recv); each call
+    packs the rows to send with one index_select and posts one grouped send/recv batch."""
 
-    Setup exchanges the request lists once (counts by all_to_all_single, ids by grouped
-    send/recv); each call packs the rows to send with one index_select and issues one
-    grouped batch of sends/receives (RCCL on the GPU, gloo on the CPU tests)."""
-
-    def __init__(self, part: GraphPartition, device, group=None):
+    def __init__(self, part: GraphPartition, comm, device):
         import torch
-        import torch.distributed as dist
-        self.torch, self.dist, self.part, self.group = torch, dist, part, group
+        self.torch, self.part, self.comm = torch, part, comm
         self.device = torch.device(device)
         P, p = part.world, part.rank
         recv = torch.from_numpy(part.recv_counts.copy()).to(self.device)
         send = torch.empty_like(recv)
-        dist.all_to_all_single(send, recv, group=group)
+        comm.all_to_all_single(send, recv)
         self.send_counts = send.cpu().numpy().astype(np.int64)
         self.recv_counts = part.recv_counts
         # my requests to q, as q-local row ids; q's requests to me -> my send rows
@@ -330,10 +394,7 @@ class HaloExchange:
                for q in range(P) if q != p and self.recv_counts[q] > 0}
         got = {q: torch.empty(int(self.send_counts[q]), dtype=torch.int64, device=self.device)
                for q in range(P) if q != p and self.send_counts[q] > 0}
-        ops = [dist.P2POp(dist.isend, req[q], q, group) for q in sorted(req)]
-        ops += [dist.P2POp(dist.irecv, got[q], q, group) for q in sorted(got)]
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
+        comm.wait(comm.exchange([(req[q], q) for q in sorted(req)], [(got[q], q) for q in sorted(got)]))
         self.send_peers = sorted(got)
         self.recv_peers = sorted(req)
         self.send_idx = (torch.cat([got[q] for q in self.send_peers]) if got
@@ -343,55 +404,71 @@ class HaloExchange:
         self.sendbuf = None
 
     def start(self, Xs):
-        """Pack and post the exchange for Xs (own rows already written); returns works."""
-        torch, dist, part = self.torch, self.dist, self.part
+        """Pack and post the exchange (own rows of Xs already written); [[works]]."""
+        torch, part = self.torch, self.part
         F = Xs.shape[1]
         if self.sendbuf is None or self.sendbuf.shape[1] != F:
             self.sendbuf = torch.empty((self.send_idx.shape[0], F), dtype=Xs.dtype, device=Xs.device)
         if self.send_idx.shape[0]:
             torch.index_select(Xs[part.own_slice], 0, self.send_idx, out=self.sendbuf)
-        ops = [dist.P2POp(dist.isend, self.sendbuf[self.send_off[i]:self.send_off[i + 1]], q, self.group)
-               for i, q in enumerate(self.send_peers)]
-        ops += [dist.P2POp(dist.irecv, Xs[self.recv_off[q]:self.recv_off[q] + self.recv_counts[q]], q, self.group)
-                for q in self.recv_peers]
-        return dist.batch_isend_irecv(ops) if ops else []
+        sends = [(self.sendbuf[self.send_off[i]:self.send_off[i + 1]], q) for i, q in enumerate(self.send_peers)]
+        recvs = [(Xs[self.recv_off[q]:self.recv_off[q] + self.recv_counts[q]], q) for q in self.recv_peers]
+        return [self.comm.exchange(sends, recvs)]
+
+
+class DenseHalo:
+    """dense halo: one all-gather per row chunk of the padded table (in place: each
+    rank's block of chunk k is already written where the gather puts it)."""
+
+    def __init__(self, part: GraphPartition, comm):
+        self.part, self.comm = part, comm
+        self.slices = part.gather_slices()
+
+    def start(self, Xs):
+        return [[self.comm.all_gather(Xs[t], Xs[own])] for t, own in self.slices]
 
 
 class DistAggregator:
-    """norm * A (norm * H) over a GraphPartition of a given graph (see the block comment
-    above partition_graph).  exact=True: one SpMM after the halo arrives, bit-identical
-    to the one-GPU aggregation; exact=False: own-column edges overlap the exchange.
-    spmm / row_broadcast / degree default to the HIP ops (injectable for CPU tests)."""
+    """norm * A (norm * H) over a GraphPartition of one graph (see the module docstring).
+    exact=True: one SpMM after the whole halo arrived, bit-identical to one GPU.
+    exact=False: own-column edges overlap the exchange; halo chunk k's edges accumulate
+    as soon as chunk k has landed.  `backend`: gala.backend.HipBackend / CpuBackend."""
 
-    def __init__(self, part: GraphPartition, F: int, device, exact: bool = True, spmm=None,
-                 row_broadcast=None, degree=None, group=None):
-        import torch
-        self.torch, self.part, self.F, self.exact = torch, part, F, exact
-        if spmm is None:
-            from . import ops
-            spmm = lambda g, X, out, dst_scale, accum: ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)  # noqa: E731
-            row_broadcast = lambda s, X, out: ops.row_broadcast(s, X, out=out)  # noqa: E731
-            degree = lambda g: ops.degree(g, power=-0.5)  # noqa: E731
-            mk = lambda hg: ops.DeviceGraph.from_host(hg, device, split=part.split_threshold)  # noqa: E731
+    def __init__(self, part: GraphPartition, F: int, backend, comm=None, exact: bool = True):
+        self.part, self.F, self.exact, self.be, self.comm = part, F, exact, backend, comm
+        thr = part.split_threshold
+        self.graph = backend.graph(part.graph, split=thr)
+        self.groups = None if exact else [backend.graph(h, split=thr) for h in part.groups]
+        self.norm = backend.degree(self.graph)          # own rows' full degrees
+        self.Xs = backend.empty(part.n_cols, F)
+        if part.halo_mode == "dense" and part.world > 1:
+            # padding rows are never read, but keep the table finite for debugging
+            self.Xs.zero_()
+        if part.world == 1:
+            self.exchange = None
+        elif part.halo_mode == "p2p":
+            self.exchange = HaloExchange(part, comm, backend.device)
         else:
-            mk = lambda hg: hg  # noqa: E731
-        self._spmm, self._rb = spmm, row_broadcast
-        self.graph = mk(part.graph)
-        self.own_graph = None if exact else mk(part.own_graph)
-        self.halo_graph = None if exact else mk(part.halo_graph)
-        self.norm = degree(self.graph)          # own rows' full degrees
-        self.Xs = torch.empty((part.n_cols, F), device=device, dtype=torch.float32)
-        self.exchange = HaloExchange(part, device, group) if part.world > 1 else None
+            self.exchange = DenseHalo(part, comm)
+        self._blocks = part.own_blocks()
+
+    def refresh_norm(self):
+        self.norm = self.be.degree(self.graph)
 
     def __call__(self, H, out):
-        p = self.part
-        self._rb(self.norm, H, self.Xs[p.own_slice])                 # own rows of Xs = norm * H
-        works = self.exchange.start(self.Xs) if self.exchange else []
+        be = self.be
+        for j0, j1, x0 in self._blocks:                               # own rows of Xs = norm * H
+            be.row_broadcast(self.norm[j0:j1], H[j0:j1], self.Xs[x0:x0 + (j1 - j0)])
+        chunks = self.exchange.start(self.Xs) if self.exchange else []
         if self.exact:
-            for w in works:
-                w.wait()
-            return self._spmm(self.graph, self.Xs, out, self.norm, False)
-        self._spmm(self.own_graph, self.Xs, out, self.norm, False)   # overlaps the exchange
-        for w in works:
-            w.wait()
-        return self._spmm(self.halo_graph, self.Xs, out, self.norm, True)
+            for works in chunks:
+                self.comm.wait(works)
+            return be.spmm(self.graph, self.Xs, out, self.norm, False)
+        be.spmm(self.groups[0], self.Xs, out, self.norm, False)      # overlaps the exchange
+        for k, works in enumerate(chunks):
+            self.comm.wait(works)
+            be.spmm(self.groups[1 + k], self.Xs, out, self.norm, True)
+        return out
+
+    def halo_bytes(self) -> int:
+        return self.part.halo_bytes(self.F) if self.part.world > 1 else 0

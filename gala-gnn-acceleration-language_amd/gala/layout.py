@@ -39,6 +39,14 @@ class HostGraph:
         return (rp[:, 1:] - rp[:, :-1]).sum(0)
 
 
+def split_threshold(n_rows: int, nnz: int) -> int:
+    """Hub-row threshold of a graph (gala_host_split_threshold: max(1024, 8*ceil(nnz/n))),
+    the one definition shared with the C++ mirror and the partitioners."""
+    t = int(_abi.lib().gala_host_split_threshold(int(n_rows), int(nnz)))
+    _abi.check("gala_host_split_threshold", min(t, 0))
+    return t
+
+
 def csr_build(n_rows: int, n_cols: int, src, dst, return_perm: bool = False):
     src = np.ascontiguousarray(src, np.int32)
     dst = np.ascontiguousarray(dst, np.int32)

@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _abi
-from .layout import HostGraph
+from .layout import HostGraph, split_threshold
 
 
 def _stream() -> int:
@@ -51,7 +51,7 @@ class DeviceGraph:
         if split and g.n_seg == 1 and g.n_rows > 0:
             deg = np.diff(g.rowptr)
             mean = g.nnz / max(g.n_rows, 1)
-            thr = max(1024, 8 * int(np.ceil(mean)))
+            thr = split_threshold(g.n_rows, g.nnz)
             if split != "auto":
                 thr = int(split)
             hubs = deg.max(initial=0) > thr

@@ -1,0 +1,150 @@
+"""Vertex-cut aggregation: column ownership + RCCL reduce-scatter of partial rows.
+
+SURVEY §8(e) / BASELINE north_star ("vertex-cut graph partitioning across the GPUs of one
+node with RCCL all-reduce of halo feature rows").  The reference's own column-tiled layout
+is the anchor: ord_col_tiling_torch (src/ops/tiling.h:222-283) cuts A by column ranges
+into segments with relative row offsets, and the DCSR variant ord_col_tiling_torch_dcsr
+(tiling.h:285-387) keeps only the rows with edges in a segment.  Here one segment is one
+rank:
+
+* rank p owns the vertex range V_p = [bounds[p], bounds[p+1)) -- the feature rows X[V_p]
+  (so no input halo at all) and every edge whose SOURCE (column) lies in V_p;
+* it computes partial sums  Y_p = A[:, V_p] (norm * H)[V_p]  for every row;
+* one reduce-scatter sums the partials into each row's owner: rank p receives
+  sum_q Y_q[V_p], which is exactly the next layer's input rows -- the layout is closed
+  under aggregation, nothing else moves.
+
+Partial rows are laid out in K row chunks so the reduce-scatter of chunk k overlaps the
+SpMM of chunk k+1: chunk k holds, for every owner q, the c = ceil(max|V_q| / K) rows
+j in [k*c, (k+1)*c) of V_q (padded), owner-major -- exactly the block layout
+reduce_scatter_tensor expects.  Every chunk is an ordinary CSR (rows in global order,
+columns local to V_p), so the SpMM kernel is the one-GPU kernel.
+
+Numerics: a row's sum is split into per-rank partial sums (each in CSR order) added by
+RCCL, so results agree with the one-GPU aggregation to fp32 rounding, not bit for bit
+(the row-partition `exact` mode in gala/dist.py is the bit-exact one).
+
+Degrees need no collective: the row structure of the owned rows (their rowptr slice) is
+partition metadata, and gala_degree_f32 only reads row offsets.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import layout
+from .dist import row_bounds
+
+
+@dataclass
+class VertexCutPartition:
+    rank: int
+    world: int
+    bounds: np.ndarray          # int64 [world+1] vertex ranges (rows owned = columns held)
+    chunks: int                 # K
+    block: int                  # c: rows per (owner, chunk)
+    chunk_graphs: list = field(default_factory=list)  # K x CSR [world*c rows, n local cols]
+    deg_graph: layout.HostGraph | None = None          # own rows' offsets (degree pass only)
+    split_threshold: int = 0
+    nnz: int = 0                # edges held by this rank
+
+    @property
+    def n(self) -> int:
+        return int(self.bounds[self.rank + 1] - self.bounds[self.rank])
+
+    @property
+    def r0(self) -> int:
+        return int(self.bounds[self.rank])
+
+    def partial_rows(self) -> int:
+        return self.chunks * self.world * self.block
+
+    def comm_bytes(self, F: int) -> int:
+        """Bytes this rank sends (= receives) per aggregation in the reduce-scatter."""
+        return 4 * F * self.chunks * self.block * (self.world - 1)
+
+
+def vertex_cut_partition(g: layout.HostGraph, rank: int, world: int, chunks: int = 1,
+                         bounds: np.ndarray | None = None) -> VertexCutPartition:
+    """Rank `rank`'s column share of the square one-segment graph `g`.  The vertex ranges
+    balance stored edges + rows like row_bounds (for a symmetric graph the column counts
+    equal the row counts)."""
+    if g.n_rows != g.n_cols or g.n_seg != 1:
+        raise ValueError("vertex_cut_partition needs a square, one-segment CSR")
+    N, P = g.n_rows, world
+    b = row_bounds(g.rowptr, world) if bounds is None else np.asarray(bounds, np.int64)
+    c0, c1 = int(b[rank]), int(b[rank + 1])
+    K = max(int(chunks), 1)
+    m = int(np.diff(b).max(initial=0))
+    c = max((m + K - 1) // K, 1)
+    rp = g.rowptr.astype(np.int64)
+    deg = np.diff(rp)
+    sel = (g.col >= c0) & (g.col < c1)
+    cs = np.zeros(g.nnz + 1, np.int64)
+    np.cumsum(sel, out=cs[1:])
+    cnt = cs[rp[1:]] - cs[rp[:-1]]                       # held edges per row
+    # chunk index and chunk-local row of every global row
+    rk = np.empty(N, np.int64)
+    pos = np.empty(N, np.int64)
+    for q in range(P):
+        j = np.arange(int(b[q + 1] - b[q]), dtype=np.int64)
+        rk[int(b[q]):int(b[q + 1])] = j // c
+        pos[int(b[q]):int(b[q + 1])] = q * c + j % c
+    edge_k = np.repeat(rk.astype(np.int32), deg) if K > 1 else None
+    graphs = []
+    for k in range(K):
+        rows_k = rk == k
+        counts = np.zeros(P * c, np.int64)
+        counts[pos[rows_k]] = cnt[rows_k]
+        rowptr = np.zeros(P * c + 1, np.int64)
+        np.cumsum(counts, out=rowptr[1:])
+        keep = sel if K == 1 else (sel & (edge_k == k))
+        cols = (g.col[keep] - c0).astype(np.int32)
+        graphs.append(layout.HostGraph(P * c, c1 - c0, rowptr.astype(np.int32), cols))
+    drp = (rp[c0:c1 + 1] - rp[c0]).astype(np.int32)
+    dg = layout.HostGraph(c1 - c0, N, drp, np.zeros(0, np.int32))
+    return VertexCutPartition(rank, world, b, K, c, graphs, dg, layout.split_threshold(g.n_rows, g.nnz),
+                              int(cs[-1]))
+
+
+class VertexCutAggregator:
+    """norm * A (norm * H) with column ownership (see the module docstring):
+        Xs        = norm[V_p] * H                            (ROW_BROADCAST)
+        Y_p^k     = A_k[:, V_p] Xs          k = 0..K-1      (SpMM, chunk k's rows)
+        S[k-th c] = reduce_scatter(Y^k)     overlapped with the next chunk's SpMM
+        out       = norm[V_p] * S[:n]                        (ROW_BROADCAST)
+    `backend`: gala.backend.HipBackend / CpuBackend; `comm`: gala.comm.Comm."""
+
+    def __init__(self, part: VertexCutPartition, F: int, backend, comm=None):
+        self.part, self.F, self.be, self.comm = part, F, backend, comm
+        thr = part.split_threshold
+        self.graphs = [backend.graph(h, split=thr) for h in part.chunk_graphs]
+        self.deg_graph = backend.graph(part.deg_graph, split=False)
+        self.norm = backend.degree(self.deg_graph)
+        self.Xs = backend.empty(part.n, F)
+        rows = part.world * part.block
+        self.partial = backend.empty(part.chunks * rows, F)
+        self.S = backend.empty(part.chunks * part.block, F)
+        self._rows = rows
+
+    def refresh_norm(self):
+        self.norm = self.be.degree(self.deg_graph)
+
+    def __call__(self, H, out):
+        be, p, c, rows = self.be, self.part, self.part.block, self._rows
+        be.row_broadcast(self.norm, H, self.Xs)
+        works = []
+        for k, gk in enumerate(self.graphs):
+            Yk = self.partial[k * rows:(k + 1) * rows]
+            be.spmm(gk, self.Xs, Yk, None, False)
+            if p.world > 1:
+                works.append(self.comm.reduce_scatter(self.S[k * c:(k + 1) * c], Yk))
+            else:
+                self.S[k * c:(k + 1) * c].copy_(Yk)
+        if works:
+            self.comm.wait(works)
+        return be.row_broadcast(self.norm, self.S[:p.n], out)
+
+    def halo_bytes(self) -> int:
+        return self.part.comm_bytes(self.F) if self.part.world > 1 else 0

@@ -288,7 +288,7 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
     const double mean = (double)nnz / (double)std::max<int64_t>(n, 1);
     int64_t max_deg = 0;
     for (int64_t i = 0; i < n; ++i) max_deg = std::max<int64_t>(max_deg, r[i + 1] - r[i]);
-    const int32_t thr = (int32_t)std::max<int64_t>(1024, 8 * ((nnz + n - 1) / std::max<int64_t>(n, 1)));
+    const int32_t thr = gala_host_split_threshold(n, nnz);
     const int32_t chunk = 512;
     const bool skewed = (double)max_deg > 4.0 * std::max(mean, 1.0);
     int64_t nr = 0, nc = 0;

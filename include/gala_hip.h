@@ -331,6 +331,14 @@ int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshol
                          int64_t *n_rows_split, int64_t *n_chunks);
 
 /*
+ * The hub-row threshold every caller uses for a graph of n_rows rows and nnz edges:
+ * max(1024, 8 * ceil(nnz / n_rows)).  One definition for the Python layer, the C++ operator
+ * mirror and the partitioners, so a partition of a graph splits exactly the rows the whole
+ * graph splits (bit-identical multi-GPU results).  Returns < 0 on negative sizes.
+ */
+int32_t gala_host_split_threshold(int64_t n_rows, int64_t nnz);
+
+/*
  * Row schedule for skewed graphs: order[] = the rows sorted by descending degree (stable
  * counting sort; degrees above 4096 share one bucket).  Degree-aware row binning
  * (SURVEY §7): rows that share a wavefront then have similar lengths.

@@ -1,0 +1,62 @@
+"""CPU: bench.py's launch contract (the driver runs `python bench.py --gpus N`).
+
+* `--gpus 2` without a launcher starts its own two ranks (torch.distributed.run on
+  127.0.0.1) and prints ONE JSON line with n_gpus 2, strong scaling of the one graph and
+  a `comm` block naming the chosen partitioning mode.  `--device cpu` runs the same code
+  on the host-CPU backend over gloo: a plumbing check, not a measurement.
+* Under a launcher, WORLD_SIZE must equal --gpus.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def _json_lines(out: str):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def test_bench_self_launches_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--scale", "0.002",
+                        "--steps", "2", "--warmup", "1", "--calib-steps", "1"],
+                       capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout                 # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
+    assert d["unit"] == "edges/s" and d["steps"] == 2 and d["warmup"] == 1
+    c = d["comm"]
+    assert c["mode"] in c["candidates_ms_per_step"]
+    assert set(c["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
+    assert c["halo_bytes_per_aggregation_per_rank"] > 0 and c["exchange_ms_per_aggregation"] > 0
+    assert d["config"]["edges"] > 0 and "weak" in d and d["weak"]["value"] > 0
+    assert d["roofline"]["alg_bytes_per_launch"] > 0
+
+
+def test_bench_single_rank_line():
+    r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--scale", "0.002", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert "rmat" in d and d["rmat"]["value"] > 0 and d["rmat"]["roofline"]["alg_bytes_per_launch"] > 0
+
+
+def test_bench_rejects_world_mismatch():
+    env = _env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--scale", "0.002"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -2,9 +2,9 @@
 
 Each rank builds its partition, exchanges boundary rows with all_gather_into_tensor and
 aggregates local + cut edges; the gathered result must equal norm * A (norm * X) on the
-assembled global graph.  The local kernels are replaced by float64 torch ops here (no
-GPU in this container) so the test exercises the partitioning, the halo column mapping,
-the collective and the two-segment accumulation order of the distributed path.
+assembled global graph.  The test exercises the partitioning, the halo column mapping,
+the collective and the two-segment accumulation order of the distributed path.  The
+local kernels run on the host-CPU backend (libgala_cpu.so).
 """
 import os
 import socket
@@ -17,6 +17,8 @@ import torch.multiprocessing as mp
 
 from gala import dist as gdist
 from gala import layout
+from gala.backend import CpuBackend
+from gala.comm import Comm
 
 N_LOCAL, EDGES, F = 600, 7000, 8
 
@@ -26,24 +28,6 @@ def _csr_mm(hg: layout.HostGraph, X: torch.Tensor) -> torch.Tensor:
     out = torch.zeros((hg.n_rows, X.shape[1]), dtype=torch.float64)
     out.index_add_(0, torch.from_numpy(rows), X.double()[torch.from_numpy(hg.col.astype(np.int64))])
     return out
-
-
-def _spmm(hg, X, out, dst_scale, accum):
-    y = dst_scale.double()[:, None] * _csr_mm(hg, X)
-    if accum:
-        out += y.to(out.dtype)
-    else:
-        out.copy_(y)
-    return out
-
-
-def _rb(s, X, out):
-    out.copy_(s[:, None] * X)
-    return out
-
-
-def _degree(hg):
-    return torch.from_numpy(hg.degrees().astype(np.float64) ** -0.5).float()
 
 
 def _features(world):
@@ -56,7 +40,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         part = gdist.make_partition(rank, world, N_LOCAL, EDGES, cut_frac=0.2, boundary_frac=0.1, seed=9)
-        agg = gdist.DistGCNAggregator(part, F, "cpu", spmm=_spmm, row_broadcast=_rb, degree=_degree)
+        agg = gdist.DistGCNAggregator(part, F, CpuBackend(), Comm())
         Xg = _features(world)
         H = torch.from_numpy(Xg[rank * N_LOCAL:(rank + 1) * N_LOCAL])
         Y = torch.empty((N_LOCAL, F))

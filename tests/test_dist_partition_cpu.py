@@ -1,14 +1,13 @@
-"""CPU: partitioning a given graph across ranks (gala/dist.py partition_graph / HaloExchange /
-DistAggregator, SURVEY §8(e) for whole datasets such as config 5's Papers100M).
+"""CPU: partitioning one given graph across ranks (gala/dist.py row partitions
+with a p2p or dense halo, gala/vertex_cut.py column ownership + reduce-scatter).
 
-* Layout invariants on one process: vertex ranges balanced by edges, the monotone
-  global -> Xs remap (every row keeps its CSR edge order), own/halo edge split, halo
-  bookkeeping.
-* gloo world 2 and 3: each rank fetches exactly its halo rows with grouped send/recv and
-  aggregates with the host-CPU backend (libgala_cpu.so, the same per-row order and
-  rounding as the HIP kernels).  exact mode must be BIT-identical to the one-process
-  aggregation of the whole graph; overlap mode (own edges first, halo edges accumulated
-  after) within fp32 rounding.
+* Layout invariants on one process: vertex ranges balanced by edges, every own row keeps
+  its global CSR edge order under the column remap, own/halo groups, halo bookkeeping;
+  the vertex cut holds every edge of the graph exactly once across ranks.
+* gloo world 2 and 3: the ranks aggregate with the host-CPU backend (libgala_cpu.so, the
+  same per-row order and rounding as the HIP kernels).  Row-partition `exact` mode (p2p
+  or dense halo) must be BIT-identical to the one-process aggregation of the whole graph;
+  overlap / chunked modes and the vertex cut agree to fp32 rounding.
 """
 import os
 import socket
@@ -19,53 +18,24 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from gala import _abi, dist as gdist, layout
+from gala import dist as gdist, layout, vertex_cut as vc
+from gala.backend import CpuBackend
+from gala.comm import Comm
 from _graphs import cora_like, features, powerlaw, with_empty_rows
 
 F = 12
 GRAPHS = {"cora": cora_like, "powerlaw": powerlaw, "empty_rows": with_empty_rows}
 
 
-# ---- host-CPU backend ops over torch CPU tensors (the injected local kernels) -----------
-class _Csr:
-    def __init__(self, g):
-        self.g = g
-        c = _abi.gala_csr_t()
-        c.n_rows, c.n_cols, c.nnz = g.n_rows, g.n_cols, g.nnz
-        c.rowptr, c.col, c.val = g.rowptr.ctypes.data, g.col.ctypes.data, None
-        c.val_heads, c.n_seg, c.seg_bounds, c.split = 1, 1, None, None
-        self.c = c
-
-
-def _spmm(g, X, out, dst_scale, accum):
-    import ctypes
-    A = _Csr(g)
-    flags = _abi.GALA_SPMM_ACCUM if accum else 0
-    _abi.call_cpu("gala_spmm_f32", ctypes.byref(A.c), X.data_ptr(), X.stride(0), out.data_ptr(),
-                  out.stride(0), X.shape[1], None, dst_scale.data_ptr(), flags, 0, 5, 7, None)
-    return out
-
-
-def _rb(s, X, out):
-    _abi.call_cpu("gala_row_broadcast_f32", X.shape[0], X.shape[1], s.data_ptr(), X.data_ptr(),
-                  X.stride(0), out.data_ptr(), out.stride(0), None)
-    return out
-
-
-def _degree(g):
-    import ctypes
-    out = torch.empty(g.n_rows)
-    _abi.call_cpu("gala_degree_f32", ctypes.byref(_Csr(g).c), out.data_ptr(), -0.5, 0, 0, None)
-    return out
-
-
 def _one_process(g, X, layers=2):
-    norm = _degree(g)
+    be = CpuBackend()
+    cg = be.graph(g)
+    norm = be.degree(cg)
     H = torch.from_numpy(X)
     outs = []
     for _ in range(layers):
-        Xs = _rb(norm, H, torch.empty_like(H))
-        H = _spmm(g, Xs, torch.empty_like(H), norm, False)
+        Xs = be.row_broadcast(norm, H, torch.empty_like(H))
+        H = be.spmm(cg, Xs, torch.empty_like(H), norm, False)
         outs.append(H.numpy().copy())
     return outs
 
@@ -73,7 +43,8 @@ def _one_process(g, X, layers=2):
 # ---- layout invariants ---------------------------------------------------------------------
 @pytest.mark.parametrize("name", list(GRAPHS))
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
-def test_partition_layout(name, world):
+@pytest.mark.parametrize("mode,chunks", [("p2p", 1), ("dense", 1), ("dense", 3)])
+def test_partition_layout(name, world, mode, chunks):
     g = GRAPHS[name]()
     b = gdist.row_bounds(g.rowptr, world)
     assert b[0] == 0 and b[-1] == g.n_rows and np.all(np.diff(b) >= 0)
@@ -83,32 +54,48 @@ def test_partition_layout(name, world):
         assert abs(int(w[b[p + 1]] - w[b[p]]) - w[-1] / world) <= heaviest + 1
     halo_total = 0
     for p in range(world):
-        pt = gdist.partition_graph(g, p, world)
+        pt = gdist.partition_graph(g, p, world, halo_mode=mode, chunks=chunks)
+        assert pt.halo_mode == mode
         r0, r1 = pt.r0, pt.r0 + pt.n
         x2g = pt.xs_to_global()
-        assert np.all(np.diff(x2g) > 0)                       # monotone remap
-        assert np.all((pt.halo < r0) | (pt.halo >= r1))
-        assert pt.lo == int(np.sum(pt.halo < r0))
-        assert int(pt.recv_counts.sum()) == pt.halo.shape[0] and pt.recv_counts[p] == 0
-        owner = np.searchsorted(pt.bounds, pt.halo, side="right") - 1
-        np.testing.assert_array_equal(np.bincount(owner, minlength=world), pt.recv_counts)
-        off = pt.recv_offsets()
-        for q in range(world):
-            if q != p and pt.recv_counts[q]:
-                blk = x2g[off[q]:off[q] + pt.recv_counts[q]]
-                assert np.all((blk >= pt.bounds[q]) & (blk < pt.bounds[q + 1]))
+        assert x2g.shape[0] == pt.n_cols
+        # own rows are written where own_blocks says
+        for j0, j1, x0 in pt.own_blocks():
+            np.testing.assert_array_equal(x2g[x0:x0 + j1 - j0], np.arange(r0 + j0, r0 + j1))
+        if mode == "p2p":
+            assert np.all(np.diff(x2g) > 0)                       # monotone remap
+            assert np.all((pt.halo < r0) | (pt.halo >= r1))
+            assert pt.lo == int(np.sum(pt.halo < r0))
+            assert int(pt.recv_counts.sum()) == pt.halo.shape[0] and pt.recv_counts[p] == 0
+            owner = np.searchsorted(pt.bounds, pt.halo, side="right") - 1
+            np.testing.assert_array_equal(np.bincount(owner, minlength=world), pt.recv_counts)
+            off = pt.recv_offsets()
+            for q in range(world):
+                if q != p and pt.recv_counts[q]:
+                    blk = x2g[off[q]:off[q] + pt.recv_counts[q]]
+                    assert np.all((blk >= pt.bounds[q]) & (blk < pt.bounds[q + 1]))
+            halo_total += pt.halo.shape[0]
+        else:
+            # every vertex has exactly one table row; the gather blocks are the owners'
+            real = x2g[x2g >= 0]
+            np.testing.assert_array_equal(np.sort(real), np.arange(g.n_rows))
+            for t, own in pt.gather_slices():
+                blk = x2g[own]
+                blk = blk[blk >= 0]
+                assert np.all((blk >= r0) & (blk < r1))
         # every own row keeps exactly its global edges, in CSR order
         e0, e1 = int(g.rowptr[r0]), int(g.rowptr[r1])
         np.testing.assert_array_equal(pt.graph.rowptr, g.rowptr[r0:r1 + 1] - e0)
         np.testing.assert_array_equal(x2g[pt.graph.col], g.col[e0:e1])
-        # own + halo split: same edges, own columns inside the own slice
-        og, hg = pt.own_graph, pt.halo_graph
-        assert og.nnz + hg.nnz == pt.graph.nnz
-        np.testing.assert_array_equal(np.diff(og.rowptr) + np.diff(hg.rowptr), np.diff(pt.graph.rowptr))
-        assert np.all((og.col >= pt.lo) & (og.col < pt.lo + pt.n))
-        assert np.all((hg.col < pt.lo) | (hg.col >= pt.lo + pt.n))
-        halo_total += pt.halo.shape[0]
-    if world == 1:
+        # groups: a partition of the row's edges, own columns first, order kept per group
+        assert len(pt.groups) == 1 + chunks
+        assert sum(h.nnz for h in pt.groups) == pt.graph.nnz
+        np.testing.assert_array_equal(sum(np.diff(h.rowptr) for h in pt.groups), np.diff(pt.graph.rowptr))
+        og = pt.groups[0]
+        assert np.all((x2g[og.col] >= r0) & (x2g[og.col] < r1))
+        for h in pt.groups[1:]:
+            assert np.all((x2g[h.col] < r0) | (x2g[h.col] >= r1))
+    if world == 1 and mode == "p2p":
         assert halo_total == 0
 
 
@@ -118,20 +105,74 @@ def test_partition_rejects_tiled_or_rectangular():
         gdist.partition_graph(layout.HostGraph(g.n_rows, g.n_cols + 1, g.rowptr, g.col), 0, 2)
     with pytest.raises(ValueError):
         gdist.partition_graph(layout.col_tile(g, 1000), 0, 2)
+    with pytest.raises(ValueError):
+        gdist.partition_graph(g, 0, 2, halo_mode="p2p", chunks=2)
+    with pytest.raises(ValueError):
+        vc.vertex_cut_partition(layout.col_tile(g, 1000), 0, 2)
+
+
+def test_dense_auto_mode_on_uniform_graph():
+    # a uniform graph's halo is nearly every other vertex: auto picks the all-gather table
+    g = cora_like()
+    assert gdist.partition_graph(g, 0, 2).halo_mode == "dense"
+    # a graph without cut edges has an empty halo: p2p
+    blocks = layout.csr_build(100, 100, np.arange(100, dtype=np.int32), np.arange(100, dtype=np.int32))
+    assert gdist.partition_graph(blocks, 0, 2).halo_mode == "p2p"
+
+
+@pytest.mark.parametrize("name", list(GRAPHS))
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (3, 2), (4, 3)])
+def test_vertex_cut_layout(name, world, chunks):
+    g = GRAPHS[name]()
+    seen = []
+    for p in range(world):
+        pt = vc.vertex_cut_partition(g, p, world, chunks=chunks)
+        c, P = pt.block, world
+        assert pt.chunks == chunks and len(pt.chunk_graphs) == chunks
+        assert c * chunks >= int(np.diff(pt.bounds).max())
+        # degree graph: own rows' full degrees
+        np.testing.assert_array_equal(np.diff(pt.deg_graph.rowptr),
+                                      np.diff(g.rowptr)[pt.r0:pt.r0 + pt.n])
+        total = 0
+        for k, h in enumerate(pt.chunk_graphs):
+            assert h.n_rows == P * c and h.n_cols == pt.n
+            assert h.nnz == 0 or (h.col.min() >= 0 and h.col.max() < pt.n)
+            rows = np.repeat(np.arange(h.n_rows), np.diff(h.rowptr))
+            q, jj = rows // c, rows % c
+            j = k * c + jj
+            assert np.all(j < np.diff(pt.bounds)[q])                 # padding rows stay empty
+            grow = pt.bounds[q] + j
+            seen.append(np.stack([grow, h.col.astype(np.int64) + pt.r0]))
+            total += h.nnz
+        assert total == pt.nnz
+    allp = np.concatenate(seen, axis=1)
+    rows = np.repeat(np.arange(g.n_rows), np.diff(g.rowptr))
+    ref = np.stack([rows, g.col.astype(np.int64)])
+    # every edge exactly once; and per row the held edges keep the CSR order
+    key = lambda a: np.lexsort((a[1], a[0]))  # noqa: E731
+    np.testing.assert_array_equal(allp[:, key(allp)], ref[:, key(ref)])
 
 
 # ---- gloo ranks -----------------------------------------------------------------------------
+MODES = [("p2p", 1, True), ("p2p", 1, False), ("dense", 1, True), ("dense", 1, False),
+         ("dense", 3, False), ("vcut", 1, None), ("vcut", 3, None)]
+
+
 def _worker(rank, world, port, name, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = GRAPHS[name]()
         X = features(g.n_rows, F, seed=11)
-        pt = gdist.partition_graph(g, rank, world)
+        be, comm = CpuBackend(), Comm()
         res = {}
-        for exact in (True, False):
-            agg = gdist.DistAggregator(pt, F, "cpu", exact=exact, spmm=_spmm, row_broadcast=_rb,
-                                       degree=_degree)
+        for mode, chunks, exact in MODES:
+            if mode == "vcut":
+                pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+                agg = vc.VertexCutAggregator(pt, F, be, comm)
+            else:
+                pt = gdist.partition_graph(g, rank, world, halo_mode=mode, chunks=chunks)
+                agg = gdist.DistAggregator(pt, F, be, comm, exact=exact)
             H = torch.from_numpy(X[pt.r0:pt.r0 + pt.n].copy())
             outs = []
             for _ in range(2):                          # two layers reuse the halo buffers
@@ -147,9 +188,9 @@ def _worker(rank, world, port, name, q):
                 ys = [torch.empty_like(pad) for _ in sizes]
                 dist.all_gather(ys, pad)
                 gathered.append(torch.cat([y[:s] for y, s in zip(ys, sizes)]).numpy())
-            res[exact] = gathered
+            res[(mode, chunks, exact)] = (gathered, agg.halo_bytes())
         if rank == 0:
-            q.put((res, [int(gdist.partition_graph(g, r, world).halo.shape[0]) for r in range(world)]))
+            q.put(res)
     finally:
         dist.destroy_process_group()
 
@@ -170,13 +211,17 @@ def test_distributed_aggregation_matches_one_process(world, name):
     procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res, halos = q.get(timeout=240)
+    res = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert sum(halos) > 0
     g = GRAPHS[name]()
     ref = _one_process(g, features(g.n_rows, F, seed=11))
-    for layer in range(2):
-        np.testing.assert_array_equal(res[True][layer], ref[layer])     # bit-identical
-        np.testing.assert_allclose(res[False][layer], ref[layer], rtol=1e-5, atol=1e-6)
+    for key, (got, hb) in res.items():
+        mode, chunks, exact = key
+        assert hb > 0, key
+        for layer in range(2):
+            if exact:
+                np.testing.assert_array_equal(got[layer], ref[layer], err_msg=str(key))  # bit-identical
+            else:
+                np.testing.assert_allclose(got[layer], ref[layer], rtol=1e-5, atol=1e-6, err_msg=str(key))

@@ -66,7 +66,7 @@ def test_partitioned_graph_matches_one_gpu(world, kind):
     ref = ops.spmm(dg, Xs_g, dst_scale=norm)
     split_seen = dg.split_rows
     for p in range(world):
-        pt = gdist.partition_graph(g, p, world)
+        pt = gdist.partition_graph(g, p, world, halo_mode="p2p")
         r0, r1 = pt.r0, pt.r0 + pt.n
         gg = ops.DeviceGraph.from_host(pt.graph, split=pt.split_threshold)
         split_seen -= gg.split_rows
@@ -82,3 +82,98 @@ def test_partitioned_graph_matches_one_gpu(world, kind):
         ops.spmm(hg, Xs, dst_scale=n_p, out=Y2, accum=True)
         torch.testing.assert_close(Y2, ref[r0:r1], rtol=1e-5, atol=1e-6)
     assert split_seen == 0      # the partitions split exactly the whole graph's hub rows
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4)])
+@pytest.mark.parametrize("kind", ["uniform", "rmat"])
+def test_dense_halo_matches_one_gpu(world, chunks, kind):
+    """The all-gather ("dense") halo layout, ranks simulated in-process: the padded table is
+    filled from the global scaled features through xs_to_global (what the chunked
+    all-gathers deliver).  One SpMM over the rank's rows is bit-identical to one GPU for any
+    chunking; the overlapped own + per-chunk accumulation agrees to fp32 rounding."""
+    from gala import layout
+    g = layout.gen_graph(kind, 6000, 60000, seed=4)
+    F = 32
+    X = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, (g.n_rows, F)).astype(np.float32)).cuda()
+    dg = ops.DeviceGraph.from_host(g)
+    norm = ops.degree(dg, power=-0.5)
+    Xs_g = ops.row_broadcast(norm, X)
+    ref = ops.spmm(dg, Xs_g, dst_scale=norm)
+    for p in range(world):
+        pt = gdist.partition_graph(g, p, world, halo_mode="dense", chunks=chunks)
+        r0, r1 = pt.r0, pt.r0 + pt.n
+        gg = ops.DeviceGraph.from_host(pt.graph, split=pt.split_threshold)
+        n_p = ops.degree(gg, power=-0.5)
+        assert torch.equal(n_p, norm[r0:r1])
+        x2g = torch.from_numpy(pt.xs_to_global()).cuda()
+        table = torch.zeros((pt.n_cols, F), device="cuda")
+        valid = x2g >= 0
+        table[valid] = Xs_g[x2g[valid]]
+        for j0, j1, x0 in pt.own_blocks():              # own rows written by the rank itself
+            ops.row_broadcast(n_p[j0:j1], X[r0 + j0:r0 + j1], out=table[x0:x0 + j1 - j0])
+        Y = ops.spmm(gg, table, dst_scale=n_p)
+        assert torch.equal(Y, ref[r0:r1])
+        Y2 = ops.spmm(ops.DeviceGraph.from_host(pt.groups[0], split=pt.split_threshold), table, dst_scale=n_p)
+        for h in pt.groups[1:]:
+            ops.spmm(ops.DeviceGraph.from_host(h, split=pt.split_threshold), table, dst_scale=n_p, out=Y2,
+                     accum=True)
+        torch.testing.assert_close(Y2, ref[r0:r1], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4), (4, 2)])
+@pytest.mark.parametrize("kind", ["uniform", "rmat"])
+def test_vertex_cut_matches_one_gpu(world, chunks, kind):
+    """Column ownership (gala/vertex_cut.py), ranks simulated in-process: every rank's chunk
+    SpMMs write partial rows over its own columns only; the reduce-scatter is the sum of the
+    partial buffers over ranks, block `owner` to the owner.  norm * sum agrees with the
+    one-GPU aggregation to fp32 rounding; degrees from the owned rows' offsets are exact."""
+    from gala import layout, vertex_cut as vc
+    g = layout.gen_graph(kind, 6000, 60000, seed=5)
+    F = 32
+    X = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, (g.n_rows, F)).astype(np.float32)).cuda()
+    dg = ops.DeviceGraph.from_host(g)
+    norm = ops.degree(dg, power=-0.5)
+    ref = ops.spmm(dg, ops.row_broadcast(norm, X), dst_scale=norm)
+    parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks) for p in range(world)]
+    c = parts[0].block
+    total = torch.zeros((chunks * world * c, F), device="cuda")
+    norms = []
+    for pt in parts:
+        r0, r1 = pt.r0, pt.r0 + pt.n
+        n_p = ops.degree(ops.DeviceGraph.from_host(pt.deg_graph, split=False), power=-0.5)
+        assert torch.equal(n_p, norm[r0:r1])
+        norms.append(n_p)
+        Xs = ops.row_broadcast(n_p, X[r0:r1])
+        rows = world * c
+        for k, h in enumerate(pt.chunk_graphs):
+            total[k * rows:(k + 1) * rows] += ops.spmm(ops.DeviceGraph.from_host(h, split=pt.split_threshold), Xs)
+    for q, pt in enumerate(parts):
+        S = torch.cat([total[k * world * c + q * c:k * world * c + (q + 1) * c] for k in range(chunks)])[:pt.n]
+        got = ops.row_broadcast(norms[q], S)
+        torch.testing.assert_close(got, ref[pt.r0:pt.r0 + pt.n], rtol=1e-5, atol=1e-6)
+
+
+def test_aggregator_classes_on_one_rank():
+    """DistAggregator / VertexCutAggregator through HipBackend at world 1 (no collectives):
+    the row partition is bit-identical, the chunked vertex cut within fp32 rounding."""
+    from gala import layout, vertex_cut as vc
+    from gala.backend import HipBackend
+    g = layout.gen_graph("rmat", 5000, 50000, seed=6)
+    F = 32
+    be = HipBackend("cuda")
+    X = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, (g.n_rows, F)).astype(np.float32)).cuda()
+    dg = ops.DeviceGraph.from_host(g)
+    norm = ops.degree(dg, power=-0.5)
+    ref = ops.spmm(dg, ops.row_broadcast(norm, X), dst_scale=norm)
+    agg = gdist.DistAggregator(gdist.partition_graph(g, 0, 1), F, be, None, exact=True)
+    Y = torch.empty_like(X)
+    agg(X, Y)
+    assert torch.equal(Y, ref)
+    agg2 = gdist.DistAggregator(gdist.partition_graph(g, 0, 1), F, be, None, exact=False)
+    Y2 = torch.empty_like(X)
+    agg2(X, Y2)
+    assert torch.equal(Y2, ref)                       # one group: the own edges are all edges
+    vagg = vc.VertexCutAggregator(vc.vertex_cut_partition(g, 0, 1, chunks=3), F, be, None)
+    Y3 = torch.empty_like(X)
+    vagg(X, Y3)
+    torch.testing.assert_close(Y3, ref, rtol=1e-5, atol=1e-6)
