@@ -69,8 +69,10 @@ extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ld
     if (samp && nsamp < 0) return GALA_ERR_INVALID_ARG;
     const bool w = A->val != nullptr;
     if (w && (A->val_heads < 1 || F % A->val_heads != 0)) return GALA_ERR_INVALID_ARG;
+    if (A->val_row_scale && !w) return GALA_ERR_INVALID_ARG;
     const int32_t H = w ? A->val_heads : 1, D = F / H;
     const bool accum = (flags & GALA_SPMM_ACCUM) != 0;
+    const float *rs = A->val_row_scale;  // factored values: w = val * rs[row] (rounded)
 #pragma omp parallel
     {
         std::vector<float> acc((size_t)F);
@@ -95,7 +97,7 @@ extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ld
                     const float sc = src_scale ? src_scale[c] : 1.0f;
                     if (w) {
                         for (int32_t h = 0; h < H; ++h) {
-                            const float wv = A->val[e * H + h];
+                            const float wv = rs ? A->val[e * H + h] * rs[r * H + h] : A->val[e * H + h];
                             if (src_scale)
                                 for (int32_t f = h * D; f < (h + 1) * D; ++f) a[f] = fmaf(wv, sc * xr[f], a[f]);
                             else
@@ -420,10 +422,9 @@ extern "C" int gala_cpu_edge_softmax_bwd_f32(const gala_csr_t *A, const float *a
     return GALA_OK;
 }
 
-extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                    const float *X, int64_t ldx, int32_t F, int32_t heads,
-                                    float slope, int32_t mode, float *Y, int64_t ldy,
-                                    float *alpha_out, void *) {
+static int cpu_gat_fwd(const gala_csr_t *A, const float *aL, const float *aR, const float *X,
+                       int64_t ldx, int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
+                       int64_t ldy, float *alpha_out, float *q_out) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1) return GALA_ERR_INVALID_ARG;
@@ -469,6 +470,7 @@ extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const 
                 const float q = 1.0f / den;
                 const bool empty = mode != GALA_SOFTMAX_REF && sum == 0.0f;
                 for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = empty ? 0.0f : acc[f] * q;
+                if (q_out) q_out[r * H + h] = q;
                 if (!alpha_out) continue;
                 for (int32_t s = 0; s < S; ++s) {
                     int64_t e0, e1;
@@ -476,7 +478,7 @@ extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const 
                     for (int64_t e = e0; e < e1; ++e) {
                         const float z = logit(e);
                         const float pe = mode == GALA_SOFTMAX_REF ? ref_exp(z) : expf(z - m);
-                        alpha_out[e * H + h] = pe * q;
+                        alpha_out[e * H + h] = q_out ? pe : pe * q;
                     }
                 }
             }
@@ -484,10 +486,17 @@ extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const 
     return GALA_OK;
 }
 
-extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                    const float *X, int64_t ldx, const float *dY, int64_t lddy,
-                                    int32_t F, int32_t heads, float slope, int32_t mode,
-                                    const float *alpha, float *d_logit, float *d_aL, void *) {
+extern "C" int gala_cpu_gat_fwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                    const float *X, int64_t ldx, int32_t F, int32_t heads,
+                                    float slope, int32_t mode, float *Y, int64_t ldy,
+                                    float *alpha_out, void *) {
+    return cpu_gat_fwd(A, aL, aR, X, ldx, F, heads, slope, mode, Y, ldy, alpha_out, nullptr);
+}
+
+static int cpu_gat_bwd(const gala_csr_t *A, const float *aL, const float *aR, const float *X,
+                       int64_t ldx, const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                       float slope, int32_t mode, const float *alpha, const float *q,
+                       float *d_logit, float *d_aL) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1) return GALA_ERR_INVALID_ARG;
@@ -505,6 +514,9 @@ extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const 
         for (int64_t r = 0; r < A->n_rows; ++r)
             for (int32_t h = 0; h < H; ++h) {
                 const float *dyr = dY + r * lddy + h * D;
+                const float qrh = q ? q[r * H + h] : 1.0f;
+                // factored attention (p, q): alpha = p * q, rounded like the materialised one
+                auto alp = [&](int64_t e) { return q ? alpha[e * H + h] * qrh : alpha[e * H + h]; };
                 // d alpha = edge_sddmm (cuda.h:808-845); sds = alpha*d alpha; acc = K7(sds)
                 float c = 0.0f;
                 sds.clear();
@@ -516,7 +528,7 @@ extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const 
                         const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
                         float d = 0.0f;
                         for (int32_t k = 0; k < D; ++k) d = fmaf(dyr[k], xr[k], d);
-                        const float v = alpha[e * H + h] * d;
+                        const float v = alp(e) * d;
                         sds.push_back(v);
                         local = local + v;
                     }
@@ -530,7 +542,7 @@ extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const 
                     row_range(A, s, r, e0, e1);
                     float local = eps;
                     for (int64_t e = e0; e < e1; ++e, ++i) {
-                        const float ds = sds[i] - alpha[e * H + h] * c;
+                        const float ds = sds[i] - alp(e) * c;
                         const float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
                         const float dz = z > 0.0f ? ds : ds * slope;
                         if (d_logit) d_logit[e * H + h] = dz;
@@ -542,6 +554,14 @@ extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const 
             }
     }
     return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_bwd_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                    const float *X, int64_t ldx, const float *dY, int64_t lddy,
+                                    int32_t F, int32_t heads, float slope, int32_t mode,
+                                    const float *alpha, float *d_logit, float *d_aL, void *) {
+    return cpu_gat_bwd(A, aL, aR, X, ldx, dY, lddy, F, heads, slope, mode, alpha, nullptr, d_logit,
+                       d_aL);
 }
 
 // aR[j] = <X[j, 0:F], wR> + bR: the attention Linear the *_attn entry points recompute
@@ -584,6 +604,113 @@ extern "C" int gala_cpu_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, c
     const std::vector<float> aR = attn_logits(A, wR, bR, X, ldx, F);
     return gala_cpu_gat_bwd_f32(A, aL, aR.data(), X, ldx, dY, lddy, F, 1, slope, GALA_SOFTMAX_REF,
                                 alpha, nullptr, d_aL, stream);
+}
+
+// aR[j,h] = <X[j, hD:(h+1)D], wR[hD:(h+1)D]> + bR[h]: the per-head attention logits of
+// the ex entry points' recompute (one head: attn_logits)
+static std::vector<float> attn_logits_heads(const gala_csr_t *A, const float *wR, const float *bR,
+                                            const float *X, int64_t ldx, int32_t F, int32_t H) {
+    std::vector<float> aR((size_t)A->n_cols * H);
+    const int32_t D = F / H;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t j = 0; j < A->n_cols; ++j)
+        for (int32_t h = 0; h < H; ++h) {
+            float d = 0.0f;
+            for (int32_t f = h * D; f < (h + 1) * D; ++f) d = fmaf(wR[f], X[j * ldx + f], d);
+            aR[(size_t)j * H + h] = d + (bR ? bR[h] : 0.0f);
+        }
+    return aR;
+}
+
+extern "C" int gala_cpu_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                       const float *wR, const float *bR, const float *X,
+                                       int64_t ldx, int32_t F, int32_t heads, float slope,
+                                       int32_t mode, float *Y, int64_t ldy, float *alpha_out,
+                                       float *q_out, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || F < 1 || F % heads != 0 || ldx < F) return GALA_ERR_INVALID_ARG;
+    if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aR && (!wR || (!X && A->n_cols > 0))) return GALA_ERR_INVALID_ARG;
+    std::vector<float> rc;
+    if (!aR) {
+        rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
+        aR = rc.data();
+    }
+    return cpu_gat_fwd(A, aL, aR, X, ldx, F, heads, slope, mode, Y, ldy, alpha_out, q_out);
+}
+
+extern "C" int gala_cpu_gat_bwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                       const float *wR, const float *bR, const float *X,
+                                       int64_t ldx, const float *dY, int64_t lddy, int32_t F,
+                                       int32_t heads, float slope, int32_t mode, const float *alpha,
+                                       const float *q, float *d_logit, float *d_aL, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || F < 1 || F % heads != 0 || ldx < F) return GALA_ERR_INVALID_ARG;
+    if (q && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
+    if (!aR && mode != GALA_SOFTMAX_REF) return GALA_ERR_UNSUPPORTED;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aR && (!wR || (!X && A->n_cols > 0))) return GALA_ERR_INVALID_ARG;
+    std::vector<float> rc;
+    if (!aR) {
+        rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
+        aR = rc.data();
+    }
+    return cpu_gat_bwd(A, aL, aR, X, ldx, dY, lddy, F, heads, slope, mode, alpha, q, d_logit, d_aL);
+}
+
+extern "C" int gala_cpu_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *wR, const float *bR, const float *X,
+                                          int64_t ldx, const float *dY, int64_t lddy, int32_t F,
+                                          int32_t heads, float slope, const float *q, float *dX,
+                                          int64_t lddx, float *d_aL, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || lddy < F || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || (!aR && !wR) || !q || !dY || !dX || !d_aL || (A->nnz > 0 && !X)) return GALA_ERR_INVALID_ARG;
+    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    std::vector<float> rc;
+    if (!aR) {
+        rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
+        aR = rc.data();
+    }
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+    // the recomputed alpha = fl(p * q), materialised on the host
+    std::vector<float> alpha((size_t)A->nnz * H);
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t s = 0; s < S; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e)
+                for (int32_t h = 0; h < H; ++h) {
+                    float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                    z = z > 0.0f ? z : z * slope;
+                    alpha[(size_t)e * H + h] = ref_exp(z) * q[r * H + h];
+                }
+        }
+    // dX = A_alpha dY on the forward pattern (sequential fma per row, the SpMM's order)
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r) {
+        float *out = dX + r * lddx;
+        for (int32_t f = 0; f < F; ++f) out[f] = 0.0f;
+        for (int32_t s = 0; s < S; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e) {
+                const float *yr = dY + (int64_t)A->col[e] * lddy;
+                for (int32_t h = 0; h < H; ++h) {
+                    const float w = alpha[(size_t)e * H + h];
+                    for (int32_t f = h * D; f < (h + 1) * D; ++f) out[f] = fmaf(w, yr[f], out[f]);
+                }
+            }
+        }
+    }
+    return cpu_gat_bwd(A, aL, aR, X, ldx, dY, lddy, F, heads, slope, GALA_SOFTMAX_REF, alpha.data(), nullptr,
+                       nullptr, d_aL);
 }
 
 extern "C" int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,

@@ -4,75 +4,13 @@
 // hub-row chunk partials, attention recompute (RC) and row-padded operands.
 // Replaces the torch compositions around the emitted GAT kernels
 // (src/codegen/common.h:622-675, 735-810, 835-894; cuda.h:505-524, 679-734, 808-845).
-#include "edge_common.h"
+#include "gat_common.h"
 
 namespace gala {
 
 // ---- fused GAT aggregation -----------------------------------------------------------
 // Row group of G lanes, lane g owns CH x VEC features (Lanes); U edges per batch: cols,
 // aR[col] and the X row slices are all loaded before the softmax updates.
-
-// RC (one head): the source logit aR[col] = <X[col,:], wR> + bR is recomputed from the X
-// row the aggregation gathers anyway (the DSL's attnR = dsl.nn.ffn(res, out=1) of the
-// aggregated `res`, tests/GALA-DSL/gat/*), instead of a separate random aR[col] read.
-template <int G, int VEC, int CH>
-__device__ __forceinline__ float attn_dot(const float (&w)[CH][VEC],
-                                          const typename GVec<VEC>::T (&x)[CH]) {
-    float d = 0.0f;
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const float *xv = reinterpret_cast<const float *>(&x[ch]);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) d = fmaf(w[ch][i], xv[i], d);
-    }
-    return group_sum<G>(d);
-}
-
-template <int G, int VEC, int CH>
-__device__ __forceinline__ void load_attn(const Lanes<G, VEC, CH> &ln, const float *wR,
-                                          float (&w)[CH][VEC]) {
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch)
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) w[ch][i] = ln.in(ch, i) ? wR[ln.off[ch] + i] : 0.0f;
-}
-
-// Operands of the fused GAT kernels (forward and backward).
-struct GatDev {
-    const float *aL, *aR, *wR, *bR;  // aR == nullptr: recompute aR from X, wR, bR (RC)
-    const float *X;
-    const float *dY, *alpha;         // backward
-    float *Y, *alpha_out;            // forward
-    float *d_logit, *d_aL;           // backward
-    int64_t ldx, ldy, lddy;
-    int32_t F;
-    float slope;
-};
-
-
-// The lane's share of one row (or one chunk of a hub row) for the GAT kernels.
-template <int G, int VEC, int CH, bool RC>
-struct GatLane {
-    Lanes<G, VEC, CH> ln;
-    int H, D, hh;
-    bool cv, leader;
-    float al, wb;
-    float w[CH][VEC];
-    __device__ __forceinline__ GatLane(const EdgeParams &p, const GatDev &d, int gl, int64_t row)
-        : ln(gl, d.F) {
-        H = p.heads;  // CH > 1 and RC only with H == 1
-        D = d.F / H;
-        cv = ln.valid[0];
-        hh = (int)(ln.off[0] / D);
-        leader = cv && (ln.off[0] % D) == 0;
-        al = d.aL[row * H + hh];
-        wb = 0.0f;
-        if (RC) {
-            load_attn<G, VEC, CH>(ln, d.wR, w);
-            wb = d.bR ? d.bR[0] : 0.0f;
-        }
-    }
-};
 
 // Running state of the forward for one row / chunk: per lane CH x VEC accumulators and the
 // head's (max, sum) of the softmax (FIXED: online, relative to m; REF: plain sums).
@@ -160,6 +98,135 @@ __device__ __forceinline__ void gat_fwd_range(const EdgeParams &p, const GatDev 
     }
 }
 
+// The same edges with the per-edge scalar work distributed over the head's HW lanes
+// (HW a power of two; HW = G for one head).  The lanes of a head own its features, so the
+// old loop repeated each edge's aR load, logit, LeakyReLU and exp on all HW lanes (8.77e9
+// -> 18.2e9 VALU instructions against the weighted SpMM at 8 heads).  Here edge k of a
+// U-edge batch is worked by lane k mod HW of the head group (its aR load, logit and exp),
+// and its exp term is broadcast to the group for the accumulation, which stays sequential
+// in CSR order (REF: bit-identical results to the per-lane loop).  The same lanes park the
+// terms in the alpha buffer: one coalesced (edge, head) store per batch.  FIXED mode takes
+// the batch's max over the group first and rescales the running state once per batch.
+template <int G, int VEC, int U, int MODE, int CH, bool RC, int HW>
+__device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const GatDev &d,
+                                                   const GatLane<G, VEC, CH, RC> &gl_, bool park,
+                                                   int64_t e0, int64_t e1, FwdState<VEC, CH> &st) {
+    typedef typename GVec<VEC>::T V;
+    constexpr int UH = (U < HW) ? U : HW;  // distinct edge owners per head group
+    constexpr int NK = U / UH;              // edges per owner lane
+    const int H = gl_.H, hh = gl_.hh;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int hl = lane & (HW - 1);
+    const int gbase = lane & ~(HW - 1);
+    const int kl = hl % UH;                // this lane's first edge of a batch
+    // owners hold their head's values: every lane for one head, valid lanes for several
+    const bool store = park && hl < UH && (H == 1 || gl_.cv);
+    const int32_t n = (int32_t)(e1 - e0);
+    // The parked terms of a batch are stored one batch late, after the next batch's loads
+    // are issued: stores count in vmcnt, and a store issued ahead of the loads made every
+    // batch wait out its write latency (8 heads: 3 ms over the no-alpha forward).
+    float pend[NK];
+    int32_t pend_j0 = -1;
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        int64_t c[U];
+        V x[U][CH];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+            c[k] = p.col[e0 + j];
+        }
+        float ar[NK];
+        if (!RC) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const int32_t j = (j0 + kl + i * UH < n) ? j0 + kl + i * UH : n - 1;
+                ar[i] = d.aR[(int64_t)p.col[e0 + j] * H + hh];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch)
+                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
+        if (store && pend_j0 >= 0) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i)  // a previous batch is always full
+                d.alpha_out[(e0 + pend_j0 + kl + i * UH) * H + hh] = pend[i];
+        }
+        if (RC) {  // the U source logits from the gathered rows (every lane of the head gets all)
+            float all[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) all[k] = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, x[k]), gl_.wb);
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                float v = all[0];
+#pragma unroll
+                for (int k = 1; k < U; ++k) v = (kl + i * UH == k) ? all[k] : v;
+                ar[i] = v;
+            }
+        }
+        float pe[NK], z[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            float t = __fadd_rn(gl_.al, ar[i]);
+            z[i] = t > 0.0f ? t : __fmul_rn(t, d.slope);
+        }
+        if (MODE == GALA_SOFTMAX_REF) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) pe[i] = ref_exp(z[i]);
+        } else {
+            float mb = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) mb = (j0 + kl + i * UH < n) ? fmaxf(mb, z[i]) : mb;
+#pragma unroll
+            for (int o = HW / 2; o >= 1; o >>= 1) mb = fmaxf(mb, __shfl_xor(mb, o, 64));
+            if (mb > st.m) {
+                const float r = (st.m == -INFINITY) ? 0.0f : expf(st.m - mb);
+                st.sum = __fmul_rn(st.sum, r);
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) st.acc[ch][i] = __fmul_rn(st.acc[ch][i], r);
+                st.m = mb;
+            }
+#pragma unroll
+            for (int i = 0; i < NK; ++i) pe[i] = expf(z[i] - st.m);
+        }
+        if (store) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) pend[i] = (MODE == GALA_SOFTMAX_REF) ? pe[i] : z[i];
+            pend_j0 = j0;
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const float pk = __shfl(pe[k / UH], gbase + (k % UH), 64);
+            if (j0 + k >= n) continue;
+            st.sum = __fadd_rn(st.sum, pk);
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) {
+                const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(pk, xv[i], st.acc[ch][i]);
+            }
+        }
+    }
+    if (store && pend_j0 >= 0) {
+#pragma unroll
+        for (int i = 0; i < NK; ++i)
+            if (pend_j0 + kl + i * UH < n) d.alpha_out[(e0 + pend_j0 + kl + i * UH) * H + hh] = pend[i];
+    }
+}
+
+template <int G, int VEC, int U, int MODE, int CH, bool RC, int HW>
+__device__ __forceinline__ void gat_fwd_edges(const EdgeParams &p, const GatDev &d,
+                                              const GatLane<G, VEC, CH, RC> &gl_, bool park,
+                                              int64_t e0, int64_t e1, FwdState<VEC, CH> &st) {
+    if constexpr (HW > 0)
+        gat_fwd_range_dist<G, VEC, U, MODE, CH, RC, HW>(p, d, gl_, park, e0, e1, st);
+    else
+        gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, park, e0, e1, st);
+}
+
 // Y[row] = acc * q with q = 1 / (sum [+ S * 1e-12 in REF mode]); returns q.
 template <int G, int VEC, int CH, bool RC, int MODE>
 __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
@@ -206,7 +273,7 @@ __device__ __forceinline__ void gat_alpha_rescale(float *ar, int64_t n, int gl, 
 
 // One pass per row: logits, LeakyReLU, softmax (REF exp-clamp / FIXED online max), the
 // alpha-weighted aggregation, then 1/sum; alpha (if requested) in a parked-value pass.
-template <int G, int VEC, int U, int MODE, int CH, bool RC>
+template <int G, int VEC, int U, int MODE, int CH, bool RC, int HW>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int32_t split_threshold) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
@@ -222,12 +289,14 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, park, e0, e1, st);
+        gat_fwd_edges<G, VEC, U, MODE, CH, RC, HW>(p, d, gl_, park, e0, e1, st);
     }
     const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, p.seg.n, st);
+    if (d.q_out && gl_.leader) d.q_out[row * H + gl_.hh] = q;  // factored: alpha = p * q
     if (!d.alpha_out) return;
     const int gbase = (threadIdx.x & (kWave - 1)) & ~(G - 1);
     if (park) {
+        if (d.q_out) return;  // the parked exp terms are the output
         const int h = gl % H;
         const int src = gbase + (h * D) / VEC;
         const float mh = __shfl(st.m, src, 64);
@@ -254,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
                 float z = __fadd_rn(alh, d.aR[(int64_t)p.col[e] * H + hd]);
                 z = z > 0.0f ? z : __fmul_rn(z, d.slope);
                 const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
-                d.alpha_out[e * H + hd] = __fmul_rn(pe, qh);
+                d.alpha_out[e * H + hd] = d.q_out ? pe : __fmul_rn(pe, qh);
             }
         }
     }
@@ -262,12 +331,12 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
 
 
 // hub rows, forward: chunk partial state -> ws[c] = {acc[F], m[H], sum[H]}
-template <int G, int VEC, int U, int MODE, int CH, bool RC>
+template <int G, int VEC, int U, int MODE, int CH, bool RC, int HW>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     FwdState<VEC, CH> st;
-    gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, d.alpha_out != nullptr, e0, e1, st);
+    gat_fwd_edges<G, VEC, U, MODE, CH, RC, HW>(p, d, gl_, d.alpha_out != nullptr, e0, e1, st);
     float *w = sp.ws + c * sp.ws_cols;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
@@ -317,7 +386,9 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
             }
     }
     const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, 1, st);
-    if (gl_.leader && d.alpha_out) {
+    if (gl_.leader && d.q_out) {
+        d.q_out[row * H + hh] = q;
+    } else if (gl_.leader && d.alpha_out) {
         float *w0 = sp.ws + c0 * sp.ws_cols;
         w0[F + hh] = st.m;
         w0[F + H + hh] = q;
@@ -362,6 +433,10 @@ __device__ __forceinline__ void gat_bwd_range(const EdgeParams &p, const GatDev 
             c[k] = p.col[e0 + j];
             a[k] = d.alpha[(e0 + j) * H + hh];
         }
+        if (d.q) {  // factored attention (p, q): alpha = p * q, rounded as materialised
+#pragma unroll
+            for (int k = 0; k < U; ++k) a[k] = __fmul_rn(a[k], gl_.qr);
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             if (!RC) ar[k] = d.aR[c[k] * H + hh];
@@ -371,7 +446,7 @@ __device__ __forceinline__ void gat_bwd_range(const EdgeParams &p, const GatDev 
         }
         if (RC) {
 #pragma unroll
-            for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<G, VEC, CH>(gl_.w, x[k]), gl_.wb);
+            for (int k = 0; k < U; ++k) ar[k] = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, x[k]), gl_.wb);
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -399,18 +474,6 @@ __device__ __forceinline__ void gat_bwd_range(const EdgeParams &p, const GatDev 
                 d.d_logit[(e0 + j0 + k) * H + hh] = sds;
             }
         }
-    }
-}
-
-template <int G, int VEC, int CH, bool RC>
-__device__ __forceinline__ void load_dy(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_, int64_t row,
-                                        float (&dy)[CH][VEC]) {
-    typedef typename GVec<VEC>::T V;
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-        const V t = *reinterpret_cast<const V *>(d.dY + row * d.lddy + gl_.ln.off[ch]);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.in(ch, i) ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
     }
 }
 
@@ -576,39 +639,68 @@ struct GatArgs {
 };
 
 
-template <int G, int VEC, int CH, bool RC, int MODE>
+template <int G, int VEC, int CH, bool RC, int HW, int MODE>
 static void launch_gat_mode(const GatArgs &a) {
     constexpr int U = 8;
-    hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, MODE, CH, RC>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
+    hipLaunchKernelGGL((k_gat_fwd<G, VEC, U, MODE, CH, RC, HW>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
                        0, a.hs, a.p, a.d, a.split ? a.sp.threshold : 0);
     if (!a.split) return;
-    hipLaunchKernelGGL((k_gat_fwd_chunk<G, VEC, U, MODE, CH, RC>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+    hipLaunchKernelGGL((k_gat_fwd_chunk<G, VEC, U, MODE, CH, RC, HW>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
                        dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
     hipLaunchKernelGGL((k_gat_fwd_fixup<G, VEC, MODE, CH, RC>), dim3(blocks_for_groups(a.sp.n_rows_split, G)),
                        dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
-    if (a.d.alpha_out)
+    if (a.d.alpha_out && !a.d.q_out)
         hipLaunchKernelGGL((k_gat_alpha_chunk<G, VEC, MODE>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
                            dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
 }
 
-template <int G, int VEC, int CH, bool RC>
+template <int G, int VEC, int CH, bool RC, int HW>
 static void launch_gat(const GatArgs &a) {
-    if (a.mode == GALA_SOFTMAX_REF) launch_gat_mode<G, VEC, CH, RC, GALA_SOFTMAX_REF>(a);
-    else launch_gat_mode<G, VEC, CH, RC, GALA_SOFTMAX_FIXED>(a);
+    if (a.mode == GALA_SOFTMAX_REF) launch_gat_mode<G, VEC, CH, RC, HW, GALA_SOFTMAX_REF>(a);
+    else launch_gat_mode<G, VEC, CH, RC, HW, GALA_SOFTMAX_FIXED>(a);
+}
+
+// several heads: HW = D / VEC lanes per head (a power of two below G) distribute the
+// per-edge softmax work; other head widths take the per-lane loop (HW = 0, no RC)
+template <int G, int VEC, bool RC>
+static int launch_gat_heads(const GatArgs &a, int hw) {
+    if constexpr (G >= 2) {
+        switch (hw) {
+            case 1: launch_gat<G, VEC, 1, RC, 1>(a); return GALA_OK;
+            case 2: if constexpr (G > 2) { launch_gat<G, VEC, 1, RC, 2>(a); return GALA_OK; } break;
+            case 4: if constexpr (G > 4) { launch_gat<G, VEC, 1, RC, 4>(a); return GALA_OK; } break;
+            case 8: if constexpr (G > 8) { launch_gat<G, VEC, 1, RC, 8>(a); return GALA_OK; } break;
+            case 16: if constexpr (G > 16) { launch_gat<G, VEC, 1, RC, 16>(a); return GALA_OK; } break;
+            case 32: if constexpr (G > 32) { launch_gat<G, VEC, 1, RC, 32>(a); return GALA_OK; } break;
+            default: break;
+        }
+    }
+    if (RC) return GALA_ERR_UNSUPPORTED;
+    launch_gat<G, VEC, 1, false, 0>(a);
+    return GALA_OK;
+}
+
+template <int G, int VEC, bool RC>
+static int launch_gat_g(const GatArgs &a, int heads, int hw) {
+    if (heads == 1) {
+        launch_gat<G, VEC, 1, RC, G>(a);
+        return GALA_OK;
+    }
+    return launch_gat_heads<G, VEC, RC>(a, hw);
 }
 
 template <int VEC, bool RC>
-static int gat_vec(const GatArgs &a, int L, int ch) {
-    if (ch == 2) launch_gat<16, VEC, 2, RC>(a);
-    else if (ch == 3) launch_gat<16, VEC, 3, RC>(a);
-    else if (ch == 4) launch_gat<16, VEC, 4, RC>(a);
-    else if (L <= 1) launch_gat<1, VEC, 1, RC>(a);
-    else if (L <= 2) launch_gat<2, VEC, 1, RC>(a);
-    else if (L <= 4) launch_gat<4, VEC, 1, RC>(a);
-    else if (L <= 8) launch_gat<8, VEC, 1, RC>(a);
-    else if (L <= 16) launch_gat<16, VEC, 1, RC>(a);
-    else if (L <= 32) launch_gat<32, VEC, 1, RC>(a);
-    else if (L <= 64) launch_gat<64, VEC, 1, RC>(a);
+static int gat_vec(const GatArgs &a, int L, int ch, int heads, int hw) {
+    if (ch == 2) launch_gat<16, VEC, 2, RC, 16>(a);
+    else if (ch == 3) launch_gat<16, VEC, 3, RC, 16>(a);
+    else if (ch == 4) launch_gat<16, VEC, 4, RC, 16>(a);
+    else if (L <= 1) launch_gat<1, VEC, 1, RC, 1>(a);
+    else if (L <= 2) return launch_gat_g<2, VEC, RC>(a, heads, hw);
+    else if (L <= 4) return launch_gat_g<4, VEC, RC>(a, heads, hw);
+    else if (L <= 8) return launch_gat_g<8, VEC, RC>(a, heads, hw);
+    else if (L <= 16) return launch_gat_g<16, VEC, RC>(a, heads, hw);
+    else if (L <= 32) return launch_gat_g<32, VEC, RC>(a, heads, hw);
+    else if (L <= 64) return launch_gat_g<64, VEC, RC>(a, heads, hw);
     else return GALA_ERR_UNSUPPORTED;
     return GALA_OK;
 }
@@ -617,7 +709,7 @@ static int gat_vec(const GatArgs &a, int L, int ch) {
 static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                         float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
-                        void *stream) {
+                        float *q_out, void *stream) {
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
@@ -625,6 +717,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
     int vec = 4;
@@ -640,14 +733,18 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     }
     a.mode = mode;
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
-    a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out;
+    a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out, a.d.q_out = q_out;
     a.hs = (hipStream_t)stream;
     a.split = (!alpha_out || G % heads == 0) && hub_split(A, (int64_t)F + 2 * heads, &a.sp);
     const bool rc = aR == nullptr;
+    // alpha of heads that do not divide the row group is formed by a per-head pass that
+    // re-reads aR: there is none to read when it is recomputed
+    if (rc && alpha_out && G % heads != 0) return GALA_ERR_UNSUPPORTED;
+    const int hw = (D % vec == 0) ? D / vec : 0;  // lanes per head (several heads)
     int r;
-    if (vec == 4) r = rc ? gat_vec<4, true>(a, L, ch) : gat_vec<4, false>(a, L, ch);
-    else if (vec == 2) r = rc ? gat_vec<2, true>(a, L, ch) : gat_vec<2, false>(a, L, ch);
-    else r = rc ? gat_vec<1, true>(a, L, ch) : gat_vec<1, false>(a, L, ch);
+    if (vec == 4) r = rc ? gat_vec<4, true>(a, L, ch, heads, hw) : gat_vec<4, false>(a, L, ch, heads, hw);
+    else if (vec == 2) r = rc ? gat_vec<2, true>(a, L, ch, heads, hw) : gat_vec<2, false>(a, L, ch, heads, hw);
+    else r = rc ? gat_vec<1, true>(a, L, ch, heads, hw) : gat_vec<1, false>(a, L, ch, heads, hw);
     if (r) return r;
     return launch_status();
 }
@@ -658,7 +755,16 @@ extern "C" int gala_gat_fwd_f32(const gala_csr_t *A, const float *aL, const floa
                                 float *alpha_out, void *stream) {
     if (!aR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, nullptr, nullptr, X, ldx, F, heads, slope, mode, Y, ldy,
-                        alpha_out, stream);
+                        alpha_out, nullptr, stream);
+}
+
+extern "C" int gala_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                   const float *wR, const float *bR, const float *X, int64_t ldx,
+                                   int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
+                                   int64_t ldy, float *alpha_out, float *q_out, void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope, mode,
+                        Y, ldy, alpha_out, q_out, stream);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
@@ -667,7 +773,7 @@ extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const
                                      float *alpha_out, void *stream) {
     if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, nullptr, wR, bR, X, ldx, F, 1, slope, mode, Y, ldy, alpha_out,
-                        stream);
+                        nullptr, stream);
 }
 
 template <int G, int VEC, int HW, int CH, bool RC, int MODE>
@@ -726,7 +832,8 @@ static int gat_bwd_vec(const GatArgs &a, int L, int hw, int ch) {
 static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                         const float *bR, const float *X, int64_t ldx, const float *dY,
                         int64_t lddy, int32_t F, int32_t heads, float slope, int32_t mode,
-                        const float *alpha, float *d_logit, float *d_aL, void *stream) {
+                        const float *alpha, const float *q, float *d_logit, float *d_aL,
+                        void *stream) {
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
@@ -736,7 +843,8 @@ static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (!aL || (!aR && !wR) || !dY || !d_aL || (A->nnz > 0 && (!X || !alpha)))
         return GALA_ERR_INVALID_ARG;
     if (mode == GALA_SOFTMAX_FIXED && !d_logit && A->nnz > 0) return GALA_ERR_INVALID_ARG;
-    if (!aR && (mode != GALA_SOFTMAX_REF || heads != 1)) return GALA_ERR_UNSUPPORTED;
+    if (!aR && mode != GALA_SOFTMAX_REF) return GALA_ERR_UNSUPPORTED;
+    if (q && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     int vec = 4;
     while (vec > 1 && (!(D % vec == 0 || (heads == 1 && ldx >= pad_to(F, vec) && lddy >= pad_to(F, vec))) ||
@@ -753,6 +861,7 @@ static int gat_bwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.mode = mode;
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
     a.d.slope = slope, a.d.dY = dY, a.d.lddy = lddy, a.d.alpha = alpha, a.d.d_logit = d_logit;
+    a.d.q = q;
     a.d.d_aL = d_aL;
     a.hs = (hipStream_t)stream;
     a.split = hub_split(A, 3 * (int64_t)heads, &a.sp);
@@ -771,7 +880,17 @@ extern "C" int gala_gat_bwd_f32(const gala_csr_t *A, const float *aL, const floa
                                 const float *alpha, float *d_logit, float *d_aL, void *stream) {
     if (!aR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_bwd_impl(A, aL, aR, nullptr, nullptr, X, ldx, dY, lddy, F, heads, slope, mode,
-                        alpha, d_logit, d_aL, stream);
+                        alpha, nullptr, d_logit, d_aL, stream);
+}
+
+extern "C" int gala_gat_bwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                   const float *wR, const float *bR, const float *X, int64_t ldx,
+                                   const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                                   float slope, int32_t mode, const float *alpha, const float *q,
+                                   float *d_logit, float *d_aL, void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_bwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, dY, lddy, F, heads,
+                        slope, mode, alpha, q, d_logit, d_aL, stream);
 }
 
 extern "C" int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
@@ -780,6 +899,6 @@ extern "C" int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const
                                      const float *alpha, float *d_aL, void *stream) {
     if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_bwd_impl(A, aL, nullptr, wR, bR, X, ldx, dY, lddy, F, 1, slope, GALA_SOFTMAX_REF,
-                        alpha, nullptr, d_aL, stream);
+                        alpha, nullptr, nullptr, d_aL, stream);
 }
 

@@ -1,0 +1,91 @@
+// gat_common.h -- shared by the fused GAT kernels (gat.hip: forward and the alpha-based
+// backward; gat_fused.hip: the REF backward with recomputed attention and fused dX): the
+// operand block, the per-lane view of a row, the attention recompute.
+#pragma once
+
+#include "edge_common.h"
+
+namespace gala {
+
+// RC (one head): the source logit aR[col] = <X[col,:], wR> + bR is recomputed from the X
+// row the aggregation gathers anyway (the DSL's attnR = dsl.nn.ffn(res, out=1) of the
+// aggregated `res`, tests/GALA-DSL/gat/*), instead of a separate random aR[col] read.
+// With several heads the dot runs over the head's HW lanes (its slice of X and wR): the
+// standard multi-head GAT source logit <X[col, hD:(h+1)D], wR[hD:(h+1)D]> + bR[h].
+template <int HW, int VEC, int CH>
+__device__ __forceinline__ float attn_dot(const float (&w)[CH][VEC],
+                                          const typename GVec<VEC>::T (&x)[CH]) {
+    float d = 0.0f;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const float *xv = reinterpret_cast<const float *>(&x[ch]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) d = fmaf(w[ch][i], xv[i], d);
+    }
+    return group_sum<HW>(d);
+}
+
+template <int G, int VEC, int CH>
+__device__ __forceinline__ void load_attn(const Lanes<G, VEC, CH> &ln, const float *wR,
+                                          float (&w)[CH][VEC]) {
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) w[ch][i] = ln.in(ch, i) ? wR[ln.off[ch] + i] : 0.0f;
+}
+
+// Operands of the fused GAT kernels (forward and backward).
+struct GatDev {
+    const float *aL, *aR, *wR, *bR;  // aR == nullptr: recompute aR from X, wR, bR (RC)
+    const float *X;
+    const float *dY, *alpha;         // backward (alpha: p when q != nullptr)
+    const float *q;                  // backward, nullable: alpha = p * q[row, h] (REF, factored)
+    float *Y, *alpha_out;            // forward (alpha_out: p when q_out != nullptr)
+    float *q_out;                    // forward, nullable: factored attention output (REF)
+    float *d_logit, *d_aL;           // backward
+    float *dX;                       // fused REF backward: dX = A_alpha dY (forward pattern)
+    int64_t ldx, ldy, lddy, lddx;
+    int32_t F;
+    float slope;
+};
+
+
+// The lane's share of one row (or one chunk of a hub row) for the GAT kernels.
+template <int G, int VEC, int CH, bool RC>
+struct GatLane {
+    Lanes<G, VEC, CH> ln;
+    int H, D, hh;
+    bool cv, leader;
+    float al, wb, qr;
+    float w[CH][VEC];
+    __device__ __forceinline__ GatLane(const EdgeParams &p, const GatDev &d, int gl, int64_t row)
+        : ln(gl, d.F) {
+        H = p.heads;  // CH > 1 and RC only with H == 1
+        D = d.F / H;
+        cv = ln.valid[0];
+        hh = (int)(ln.off[0] / D);
+        leader = cv && (ln.off[0] % D) == 0;
+        al = d.aL[row * H + hh];
+        qr = d.q ? d.q[row * H + hh] : 1.0f;
+        wb = 0.0f;
+        if (RC) {
+            load_attn<G, VEC, CH>(ln, d.wR, w);
+            wb = d.bR ? d.bR[hh] : 0.0f;
+        }
+    }
+};
+
+template <int G, int VEC, int CH, bool RC>
+__device__ __forceinline__ void load_dy(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_, int64_t row,
+                                        float (&dy)[CH][VEC]) {
+    typedef typename GVec<VEC>::T V;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const V t = *reinterpret_cast<const V *>(d.dY + row * d.lddy + gl_.ln.off[ch]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.in(ch, i) ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
+    }
+}
+
+
+}  // namespace gala

@@ -1,0 +1,332 @@
+// gat_fused.hip -- the REF-mode GAT backward in one pass per row, with the attention
+// recomputed instead of stored and the dX aggregation fused in.
+//
+// The reference's GAT backward (common.h:835-894, slot 2li+1 = the forward graph for the
+// undirected graphs it runs) is dX = A_alpha dY (a weighted SpMM over the saved alpha)
+// plus the edge chain edge_sddmm -> softmax bwd -> LeakyReLU bwd -> row sum.  Both walk
+// the same rows over the same edges.  Here one row group does both: per edge it gathers
+// X[col] (for d alpha = <dY[row], X[col]>) and dY[col] (for dX), and rebuilds
+// alpha = fl(min(exp(LeakyReLU(aL[row] + aR[col])), 1e12) * q[row]) from the forward's
+// per-row q = 1/(sum + 1e-12) -- the very product the forward would have stored -- so
+// the forward writes no alpha (4 B per edge and head) and nothing reads it back.  aR is
+// read, or recomputed per head from the gathered X row (wR, bR).
+//
+// Numerics: dX is accumulated sequentially in CSR order with fma(alpha, dY, acc), i.e.
+// bit-identical to gala_spmm_f32 over the materialised alpha (hub rows: the same chunk
+// partials and ordered fix-up).  d_aL's sums are taken per lane over the edges the lane
+// owns and combined at the end of the row: equal to the reference within fp32 rounding.
+#include "gat_common.h"
+
+namespace gala {
+
+struct FusedBwdState {
+    float acc = 0.0f, s_msds = 0.0f, s_ma = 0.0f;
+};
+
+// Edges [e0, e1) of `row`: dX accumulators and the lane's share of the REF sums.  Edge k of
+// a U-edge batch is owned by lane k mod UH of its head group: it loads / recomputes aR,
+// forms alpha and the LeakyReLU factor, and counts the edge's sds; alpha is broadcast to
+// the group for the dX accumulation.
+template <int G, int VEC, int U, int HW, int CH, bool RC>
+__device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const GatDev &d,
+                                                    const GatLane<G, VEC, CH, RC> &gl_,
+                                                    const float (&dy)[CH][VEC], int64_t e0,
+                                                    int64_t e1, FusedBwdState &st,
+                                                    float (&dxa)[CH][VEC]) {
+    typedef typename GVec<VEC>::T V;
+    constexpr int UH = (U < HW) ? U : HW;
+    constexpr int NK = U / UH;
+    const int H = gl_.H, hh = gl_.hh;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int hl = lane & (HW - 1);
+    const int gbase = lane & ~(HW - 1);
+    const int kl = hl % UH;
+    const bool owner = hl < UH;
+    const int32_t n = (int32_t)(e1 - e0);
+    for (int32_t j0 = 0; j0 < n; j0 += U) {
+        int64_t c[U];
+        V x[U][CH], yv[U][CH];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
+            c[k] = p.col[e0 + j];
+        }
+        float ar[NK];
+        if (!RC) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                const int32_t j = (j0 + kl + i * UH < n) ? j0 + kl + i * UH : n - 1;
+                ar[i] = d.aR[(int64_t)p.col[e0 + j] * H + hh];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) {
+                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
+                yv[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.dY + c[k] * d.lddy + gl_.ln.off[ch]));
+            }
+        if (RC) {
+            float all[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) all[k] = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, x[k]), gl_.wb);
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                float v = all[0];
+#pragma unroll
+                for (int k = 1; k < U; ++k) v = (kl + i * UH == k) ? all[k] : v;
+                ar[i] = v;
+            }
+        }
+        float a[NK];
+        bool pos[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            const float t = __fadd_rn(gl_.al, ar[i]);
+            pos[i] = t > 0.0f;
+            const float z = pos[i] ? t : __fmul_rn(t, d.slope);
+            a[i] = __fmul_rn(ref_exp(z), gl_.qr);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            float dd = 0.0f;
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) {
+                const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) dd = fmaf(dy[ch][i], xv[i], dd);
+            }
+            dd = group_sum<HW>(dd);
+            const float ak = __shfl(a[k / UH], gbase + (k % UH), 64);
+            if (j0 + k >= n) continue;
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch) {
+                const float *yk = reinterpret_cast<const float *>(&yv[k][ch]);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) dxa[ch][i] = fmaf(ak, yk[i], dxa[ch][i]);
+            }
+            if (owner && kl == k % UH) {
+                const int i = k / UH;
+                const float sds = __fmul_rn(a[i], dd);
+                st.acc += sds;
+                st.s_msds += pos[i] ? sds : __fmul_rn(sds, d.slope);
+                st.s_ma += pos[i] ? a[i] : __fmul_rn(a[i], d.slope);
+            }
+        }
+    }
+}
+
+template <int G, int VEC, int CH>
+__device__ __forceinline__ void store_dx(const GatDev &d, const Lanes<G, VEC, CH> &ln, float *base,
+                                         const float (&dxa)[CH][VEC]) {
+    typedef typename GVec<VEC>::T V;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        if (!ln.valid[ch]) continue;
+        V out;
+        float *ov = reinterpret_cast<float *>(&out);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) ov[i] = dxa[ch][i];
+        float *yp = base + ln.off[ch];
+        if (ln.nv[ch] == VEC) {
+            *reinterpret_cast<V *>(yp) = out;
+        } else {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                if (ln.in(ch, i)) yp[i] = ov[i];
+        }
+    }
+}
+
+template <int G, int VEC, int U, int HW, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d, int32_t split_threshold) {
+    GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
+    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
+        return;  // hub row: k_gat_bwd_fused_chunk / _fixup
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    float dy[CH][VEC], dxa[CH][VEC];
+    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dxa[ch][i] = 0.0f;
+    FusedBwdState st;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        gat_bwd_fused_range<G, VEC, U, HW, CH, RC>(p, d, gl_, dy, e0, e1, st, dxa);
+    }
+    store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
+    const float eps = (float)p.seg.n * 1e-12f;
+    const float acc = group_sum<HW>(st.acc) + eps;          // K7 on sds (common.h:793-794)
+    const float s1 = group_sum<HW>(st.s_msds), s2 = group_sum<HW>(st.s_ma);
+    if (gl_.leader) d.d_aL[row * gl_.H + gl_.hh] = (s1 - acc * s2) + eps;  // common.h:662-667
+}
+
+// hub rows: chunk partials -> ws[c] = {dX[F], acc[H], s_msds[H], s_ma[H]}
+template <int G, int VEC, int U, int HW, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_chunk(EdgeParams p, GatDev d, HubSplit sp) {
+    GALA_CHUNK_PROLOGUE(G);
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    float dy[CH][VEC], dxa[CH][VEC];
+    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dxa[ch][i] = 0.0f;
+    FusedBwdState st;
+    gat_bwd_fused_range<G, VEC, U, HW, CH, RC>(p, d, gl_, dy, e0, e1, st, dxa);
+    float *w = sp.ws + c * sp.ws_cols;
+    store_dx<G, VEC, CH>(d, gl_.ln, w, dxa);
+    const float acc = group_sum<HW>(st.acc);
+    const float s1 = group_sum<HW>(st.s_msds), s2 = group_sum<HW>(st.s_ma);
+    if (gl_.leader) {
+        const int F = d.F, H = gl_.H, hh = gl_.hh;
+        w[F + hh] = acc;
+        w[F + H + hh] = s1;
+        w[F + 2 * H + hh] = s2;
+    }
+}
+
+// hub rows: the chunk partials of a row summed in chunk order (dX: as k_spmm_fixup)
+template <int G, int VEC, int CH, bool RC>
+__global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_fixup(EdgeParams p, GatDev d, HubSplit sp) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = lane & (G - 1);
+    const int64_t ri = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * (kWave / G) + lane / G;
+    if (ri >= sp.n_rows_split) return;
+    const int64_t row = sp.rows[ri];
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    const int F = d.F, H = gl_.H, hh = gl_.hh;
+    float dxa[CH][VEC];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dxa[ch][i] = 0.0f;
+    float acc = 0.0f, s1 = 0.0f, s2 = 0.0f;
+    for (int64_t cc = sp.row_chunk0[ri]; cc < sp.row_chunk0[ri + 1]; ++cc) {
+        const float *w = sp.ws + cc * sp.ws_cols;
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                dxa[ch][i] = __fadd_rn(dxa[ch][i], gl_.ln.in(ch, i) ? w[gl_.ln.off[ch] + i] : 0.0f);
+        acc = __fadd_rn(acc, w[F + hh]);
+        s1 = __fadd_rn(s1, w[F + H + hh]);
+        s2 = __fadd_rn(s2, w[F + 2 * H + hh]);
+    }
+    store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
+    if (gl_.leader) {
+        acc = __fadd_rn(acc, 1e-12f);
+        d.d_aL[row * H + hh] = (s1 - acc * s2) + 1e-12f;
+    }
+}
+
+}  // namespace gala
+
+using namespace gala;
+
+namespace {
+
+struct FusedArgs {
+    EdgeParams p;
+    GatDev d;
+    HubSplit sp;
+    bool split;
+    hipStream_t hs;
+};
+
+template <int G, int VEC, int HW, int CH, bool RC>
+void launch_fused(const FusedArgs &a) {
+    constexpr int U = 8;
+    hipLaunchKernelGGL((k_gat_bwd_fused<G, VEC, U, HW, CH, RC>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
+                       0, a.hs, a.p, a.d, a.split ? a.sp.threshold : 0);
+    if (!a.split) return;
+    hipLaunchKernelGGL((k_gat_bwd_fused_chunk<G, VEC, U, HW, CH, RC>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+    hipLaunchKernelGGL((k_gat_bwd_fused_fixup<G, VEC, CH, RC>), dim3(blocks_for_groups(a.sp.n_rows_split, G)),
+                       dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+}
+
+template <int G, int VEC, bool RC>
+int fused_g(const FusedArgs &a, int heads, int hw) {
+    if (heads == 1) {
+        launch_fused<G, VEC, G, 1, RC>(a);
+        return GALA_OK;
+    }
+    if constexpr (G >= 2) {
+        switch (hw) {
+            case 1: launch_fused<G, VEC, 1, 1, RC>(a); return GALA_OK;
+            case 2: if constexpr (G > 2) { launch_fused<G, VEC, 2, 1, RC>(a); return GALA_OK; } break;
+            case 4: if constexpr (G > 4) { launch_fused<G, VEC, 4, 1, RC>(a); return GALA_OK; } break;
+            case 8: if constexpr (G > 8) { launch_fused<G, VEC, 8, 1, RC>(a); return GALA_OK; } break;
+            case 16: if constexpr (G > 16) { launch_fused<G, VEC, 16, 1, RC>(a); return GALA_OK; } break;
+            case 32: if constexpr (G > 32) { launch_fused<G, VEC, 32, 1, RC>(a); return GALA_OK; } break;
+            default: break;
+        }
+    }
+    return GALA_ERR_UNSUPPORTED;
+}
+
+template <int VEC, bool RC>
+int fused_vec(const FusedArgs &a, int L, int ch, int heads, int hw) {
+    if (ch == 2) launch_fused<16, VEC, 16, 2, RC>(a);
+    else if (ch == 3) launch_fused<16, VEC, 16, 3, RC>(a);
+    else if (ch == 4) launch_fused<16, VEC, 16, 4, RC>(a);
+    else if (L <= 1) launch_fused<1, VEC, 1, 1, RC>(a);
+    else if (L <= 2) return fused_g<2, VEC, RC>(a, heads, hw);
+    else if (L <= 4) return fused_g<4, VEC, RC>(a, heads, hw);
+    else if (L <= 8) return fused_g<8, VEC, RC>(a, heads, hw);
+    else if (L <= 16) return fused_g<16, VEC, RC>(a, heads, hw);
+    else if (L <= 32) return fused_g<32, VEC, RC>(a, heads, hw);
+    else if (L <= 64) return fused_g<64, VEC, RC>(a, heads, hw);
+    else return GALA_ERR_UNSUPPORTED;
+    return GALA_OK;
+}
+
+}  // namespace
+
+extern "C" int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                      const float *wR, const float *bR, const float *X,
+                                      int64_t ldx, const float *dY, int64_t lddy, int32_t F,
+                                      int32_t heads, float slope, const float *q, float *dX,
+                                      int64_t lddx, float *d_aL, void *stream) {
+    FusedArgs a{};
+    int st = edge_setup(A, heads, &a.p);
+    if (st) return st;
+    if (F < 1 || F % heads != 0 || ldx < F || lddy < F || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || (!aR && !wR) || !q || !dY || !dX || !d_aL || (A->nnz > 0 && !X)) return GALA_ERR_INVALID_ARG;
+    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // dY[col]: a square pattern
+    const int D = F / heads;
+    int vec = 4;
+    auto ok = [&](int v) {
+        const bool fits = D % v == 0 || (heads == 1 && ldx >= pad_to(F, v) && lddy >= pad_to(F, v) &&
+                                         lddx >= pad_to(F, v));
+        return fits && ldx % v == 0 && lddy % v == 0 && lddx % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
+               ((uintptr_t)dY % (4 * v)) == 0 && ((uintptr_t)dX % (4 * v)) == 0;
+    };
+    while (vec > 1 && !ok(vec)) vec >>= 1;
+    const int L = (F + vec - 1) / vec;
+    const int ch = narrow_chunks(heads, vec, L);
+    int G = 16;
+    if (ch == 1) {
+        G = 1;
+        while (G < L) G <<= 1;
+    }
+    const int hw = (D % vec == 0) ? D / vec : 0;
+    if (heads > 1 && (hw == 0 || (hw & (hw - 1)))) return GALA_ERR_UNSUPPORTED;
+    a.d.aL = aL, a.d.aR = aR, a.d.wR = aR ? nullptr : wR, a.d.bR = aR ? nullptr : bR;
+    a.d.X = X, a.d.ldx = ldx, a.d.F = F, a.d.slope = slope;
+    a.d.dY = dY, a.d.lddy = lddy, a.d.q = q, a.d.dX = dX, a.d.lddx = lddx, a.d.d_aL = d_aL;
+    a.hs = (hipStream_t)stream;
+    a.split = hub_split(A, pad_to(F, 4) + 3 * (int64_t)heads, &a.sp);
+    const bool rc = aR == nullptr;
+    int r;
+    if (vec == 4) r = rc ? fused_vec<4, true>(a, L, ch, heads, hw) : fused_vec<4, false>(a, L, ch, heads, hw);
+    else if (vec == 2) r = rc ? fused_vec<2, true>(a, L, ch, heads, hw) : fused_vec<2, false>(a, L, ch, heads, hw);
+    else r = rc ? fused_vec<1, true>(a, L, ch, heads, hw) : fused_vec<1, false>(a, L, ch, heads, hw);
+    if (r) return r;
+    return launch_status();
+}

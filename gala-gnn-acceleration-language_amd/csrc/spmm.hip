@@ -38,6 +38,7 @@ struct SpmmParams {
     const int32_t *rowptr;
     const int32_t *col;
     const float *val;
+    const float *val_rs;      // nullable [n_rows * val_heads]: w_e = val[e,h] * val_rs[row,h]
     const float *X;
     float *Y;
     const float *src_scale;
@@ -125,11 +126,16 @@ __device__ __forceinline__ void stv_n(float *p, const typename VecT<VEC>::T &v, 
 // order; the loads of U edges are issued before the first add of the batch.
 template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
 __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
-                                                 int64_t e0, int64_t e1,
+                                                 int64_t row, int64_t e0, int64_t e1,
                                                  typename VecT<VEC>::T (&acc)[CH]) {
     typedef typename VecT<VEC>::T V;
     const int32_t deg = (int32_t)(e1 - e0);
     const int32_t n = SAMP ? (deg > 0 ? p.nsamp : 0) : deg;
+    // factored edge values (the GAT forward's p with its per-row 1/sum q): w = p * q,
+    // rounded, i.e. exactly the materialised alpha
+    float rs[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) rs[ch] = (W && p.val_rs) ? p.val_rs[row * p.val_heads + cl.head[ch]] : 1.0f;
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         int32_t c[U];
         V x[U][CH];
@@ -143,6 +149,12 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
             c[k] = p.col[e];
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + cl.head[ch]] : 1.0f;
+        }
+        if (W && p.val_rs) {
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch) w[k][ch] = __fmul_rn(w[k][ch], rs[ch]);
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
@@ -217,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
     for (int s = 0; s < nseg; ++s) {
         const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
         const int64_t base = seg->base[s];
-        accumulate_range<VEC, G, CH, U, W, SAMP, SRCS>(p, cl, base + rp[row], base + rp[row + 1], acc);
+        accumulate_range<VEC, G, CH, U, W, SAMP, SRCS>(p, cl, row, base + rp[row], base + rp[row + 1], acc);
     }
     store_row<VEC, G, CH, W>(p, cl, row, acc);
 }
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_chunk(SpmmParams p, SplitParams
     V acc[CH];
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) acc[ch] = V(0.0f);
-    accumulate_range<VEC, G, CH, U, W, false, SRCS>(p, cl, e0, e1, acc);
+    accumulate_range<VEC, G, CH, U, W, false, SRCS>(p, cl, row, e0, e1, acc);
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
         if (cl.valid[ch]) stv<VEC>(sp.ws + c * sp.ws_cols + cl.off[ch], acc[ch]);
@@ -436,6 +448,7 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     if (samp && nsamp < 0) return GALA_ERR_INVALID_ARG;
     const bool w = A->val != nullptr;
     if (w && (A->val_heads < 1 || F % A->val_heads != 0)) return GALA_ERR_INVALID_ARG;
+    if (A->val_row_scale && !w) return GALA_ERR_INVALID_ARG;
     const int32_t head_dim = w ? F / A->val_heads : F;
 
     // widest vector that divides both strides with aligned bases and either divides F and
@@ -462,6 +475,7 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     p.rowptr = A->rowptr;
     p.col = A->col;
     p.val = A->val;
+    p.val_rs = A->val_row_scale;
     p.X = X;
     p.Y = Y;
     p.src_scale = src_scale;

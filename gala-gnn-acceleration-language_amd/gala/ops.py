@@ -31,9 +31,11 @@ def _dp(t):
 class DeviceGraph:
     """Device-resident graph (the generated code's global_*_graph slots, gala.cu:32-43)."""
 
-    def __init__(self, n_rows, n_cols, rowptr, col, val=None, n_seg=1, bounds=None, val_heads=1):
+    def __init__(self, n_rows, n_cols, rowptr, col, val=None, n_seg=1, bounds=None, val_heads=1,
+                 val_row_scale=None):
         self.n_rows, self.n_cols = int(n_rows), int(n_cols)
         self.rowptr, self.col, self.val = rowptr, col, val
+        self.val_row_scale = val_row_scale
         self.n_seg = int(n_seg)
         self.val_heads = int(val_heads)
         self.bounds = None if bounds is None else np.ascontiguousarray(bounds, np.int32)
@@ -99,9 +101,12 @@ class DeviceGraph:
     def nnz(self) -> int:
         return int(self.col.numel())
 
-    def with_values(self, val, val_heads=1) -> "DeviceGraph":
+    def with_values(self, val, val_heads=1, row_scale=None) -> "DeviceGraph":
+        """The same structure with edge values val [nnz, val_heads]; row_scale [n_rows,
+        val_heads] stores them factored (A_e,h = val[e,h] * row_scale[row,h], rounded: the
+        GAT forward's (p, q) output used as alpha)."""
         g = DeviceGraph(self.n_rows, self.n_cols, self.rowptr, self.col, val, self.n_seg,
-                        self.bounds, val_heads)
+                        self.bounds, val_heads, row_scale)
         g._split = self._split
         return g
 
@@ -124,6 +129,7 @@ class DeviceGraph:
             c.n_seg = self.n_seg
             c.seg_bounds = None if self.bounds is None else self.bounds.ctypes.data
             c.split = None
+            c.val_row_scale = _dp(self.val_row_scale)
             if self._split is not None:
                 c.split = ctypes.addressof(self._split["plan"])
             self._csr = c
@@ -276,6 +282,49 @@ def gat_bwd(g: DeviceGraph, aL, aR, X, dY, alpha, heads=1, slope=0.2, mode=_abi.
     _abi.call("gala_gat_bwd_f32", g.csr(3 * heads), _dp(aL), _dp(aR), _dp(X), X.stride(0), _dp(dY),
               dY.stride(0), F, heads, slope, mode, _dp(alpha), _dp(dz), _dp(d_aL), _stream())
     return d_aL, dz
+
+def gat_fwd_ex(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2,
+               mode=_abi.GALA_SOFTMAX_REF, want_alpha=False, factored=False):
+    """gala_gat_fwd_ex_f32: aR given, or recomputed per head from X (wR [F], bR [heads]).
+    factored=True (REF): returns (Y, p, q) with alpha = p * q; factored="q": (Y, q) only,
+    for gat_bwd_fused; else (Y, alpha) / Y."""
+    F = X.shape[1]
+    Y = _rows_like(X, g.n_rows)
+    alpha = (torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32)
+             if (want_alpha or factored == True) else None)  # noqa: E712
+    q = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if factored else None
+    _abi.call("gala_gat_fwd_ex_f32", g.csr(F + 2 * heads), _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X),
+              X.stride(0), F, heads, slope, mode, _dp(Y), Y.stride(0), _dp(alpha), _dp(q), _stream())
+    if factored == "q":
+        return Y, q
+    if factored:
+        return Y, alpha, q
+    return (Y, alpha) if want_alpha else Y
+
+
+def gat_bwd_ex(g: DeviceGraph, aL, X, dY, alpha, q=None, aR=None, wR=None, bR=None, heads=1, slope=0.2,
+               mode=_abi.GALA_SOFTMAX_REF, want_dz=False):
+    """gala_gat_bwd_ex_f32: (d_aL, dz or None); q given: alpha holds p (alpha = p * q)."""
+    F = X.shape[1]
+    d_aL = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    dz = (torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32)
+          if (want_dz or mode == _abi.GALA_SOFTMAX_FIXED) else None)
+    _abi.call("gala_gat_bwd_ex_f32", g.csr(3 * heads), _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X), X.stride(0),
+              _dp(dY), dY.stride(0), F, heads, slope, mode, _dp(alpha), _dp(q), _dp(dz), _dp(d_aL), _stream())
+    return d_aL, dz
+
+
+def gat_bwd_fused(g: DeviceGraph, aL, X, dY, q, aR=None, wR=None, bR=None, heads=1, slope=0.2):
+    """gala_gat_bwd_fused_f32 (REF): attention recomputed from (aL, aR | wR, bR, q); returns
+    (dX, d_aL) with dX = A_alpha dY on the forward pattern."""
+    F = X.shape[1]
+    dX = _rows_like(dY, g.n_rows)
+    d_aL = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    _abi.call("gala_gat_bwd_fused_f32", g.csr((F + 3) // 4 * 4 + 3 * heads), _dp(aL), _dp(aR), _dp(wR), _dp(bR),
+              _dp(X), X.stride(0), _dp(dY), dY.stride(0), F, heads, slope, _dp(q), _dp(dX), dX.stride(0),
+              _dp(d_aL), _stream())
+    return dX, d_aL
+
 
 def edge_permute(perm, src, heads=1):
     n = perm.numel()

@@ -34,6 +34,9 @@ struct Backend {
     decltype(&gala_gat_bwd_f32) gat_bwd;
     decltype(&gala_gat_fwd_attn_f32) gat_fwd_attn;
     decltype(&gala_gat_bwd_attn_f32) gat_bwd_attn;
+    decltype(&gala_gat_fwd_ex_f32) gat_fwd_ex;
+    decltype(&gala_gat_bwd_ex_f32) gat_bwd_ex;
+    decltype(&gala_gat_bwd_fused_f32) gat_bwd_fused;
     decltype(&gala_edge_permute_f32) permute;
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
@@ -44,6 +47,7 @@ const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
+                   gala_gat_fwd_ex_f32, gala_gat_bwd_ex_f32, gala_gat_bwd_fused_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
@@ -51,6 +55,7 @@ const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcas
                    gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
                    gala_cpu_gat_fwd_attn_f32, gala_cpu_gat_bwd_attn_f32,
+                   gala_cpu_gat_fwd_ex_f32, gala_cpu_gat_bwd_ex_f32, gala_cpu_gat_bwd_fused_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32};
 
@@ -225,8 +230,14 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
                         const torch::Tensor &cols, const torch::Tensor *vals,
                         const torch::Tensor &bounds, int64_t segments, int val_heads,
                         const torch::Tensor *src_scale, const torch::Tensor *dst_scale,
-                        int64_t nsamples, int64_t ra, int64_t rb) {
+                        int64_t nsamples, int64_t ra, int64_t rb,
+                        const torch::Tensor *val_row_scale = nullptr) {
     CsrView cv = view(offsets, cols, vals, bounds, segments, val_heads);
+    if (val_row_scale) {  // factored edge values (GAT p with its per-row q)
+        check_dev(*val_row_scale, torch::kFloat, "val_row_scale");
+        check_on(*val_row_scale, offsets, "val_row_scale");
+        cv.c.val_row_scale = val_row_scale->data_ptr<float>();
+    }
     const bool padded = row_padded(X);
     auto x = padded ? X : X.contiguous();
     check_dev(x, torch::kFloat, "input_dense");
@@ -629,12 +640,20 @@ struct GatGrads {
     torch::Tensor daL, daR, dX;
 };
 
+// alpha = p * q (rounded) of a factored attention output, materialised on the forward
+// pattern (gala_row_scale_f32: the same product the fused kernels form per edge)
+torch::Tensor materialise_alpha(const Slot &fw, const torch::Tensor &p, const torch::Tensor &q) {
+    auto a = p.clone();
+    return row_scale_impl(q, fw.off, fw.cols, a, fw.bounds, fw.off.numel() / fw.segs - 1, fw.segs);
+}
+
 // Backward of the fused GAT layer (both autograd Functions below).  r is the source logit
-// aR; with wR defined and r undefined, aR = X wR^T + bR was recomputed inside the forward
-// kernel, and is either recomputed again by the backward kernel (REF on one pattern) or
-// formed here for the other paths.
+// aR; with wR defined and r undefined, aR[j,h] = <X[j, head h], wR[head h]> + bR[h] was
+// recomputed inside the forward kernel, and is either recomputed again by the backward
+// kernel (REF on one pattern) or formed here for the other paths.  q defined: `alpha`
+// holds the forward's factored p (REF), alpha = p * q.
 GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tensor &x,
-                      const torch::Tensor &alpha, const torch::Tensor &dY_in, int64_t li,
+                      torch::Tensor alpha, torch::Tensor q, const torch::Tensor &dY_in, int64_t li,
                       double slope, int64_t mode, int heads, const torch::Tensor &wR,
                       const torch::Tensor &bR) {
     Slot fw = slot(2 * li), bw = slot(2 * li + 1);
@@ -650,27 +669,47 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
     TORCH_CHECK(!fixed || bw.perm.defined(),
                 "gala: FIXED-mode GAT backward needs the transposed graph and its edge "
                 "permutation in slot 2*li+1 (transpose_perm)");
+    const bool same = same_pattern(fw, bw);
+    // the factored (p, q) pair feeds the dX SpMM and the fused kernel directly when both run
+    // on the forward pattern; elsewhere alpha is materialised once
+    if (q.defined() && (fixed || !same)) {
+        alpha = materialise_alpha(fw, alpha, q);
+        q = torch::Tensor();
+    }
     // dX: reference multiplies by alpha on slot 2li+1's pattern (common.h:876);
     // FIXED: A^T with the transposed alpha
     torch::Tensor alpha_b = fixed ? permute_edges(bw.perm, alpha, heads) : alpha;
     torch::Tensor dX = spmm_impl(dY, bw.off, bw.cols, &alpha_b, bw.bounds, bw.segs, heads,
-                                 nullptr, nullptr, 0, 5, 7);
+                                 nullptr, nullptr, 0, 5, 7, q.defined() ? &q : nullptr);
     // one fused edge kernel for d alpha -> softmax bwd -> LeakyReLU bwd -> row sum when
     // every step runs on one pattern: FIXED always (slot 2li), REF when slot 2li+1 is
     // the forward graph itself (undirected graphs: cuda.h:1253-1257)
-    const bool same = same_pattern(fw, bw);
+    const float *qp = q.defined() ? q.data_ptr<float>() : nullptr;
     if (!r.defined() && !fixed && same) {
         auto daL = torch::empty_like(l);
-        check(be(fw.off).gat_bwd_attn(&cf.c, l.data_ptr<float>(), wR.data_ptr<float>(),
-                                      bR.defined() ? bR.data_ptr<float>() : nullptr,
-                                      x.data_ptr<float>(), ldx, dY.data_ptr<float>(), lddy, (int32_t)F,
-                                      (float)slope, alpha.data_ptr<float>(), daL.data_ptr<float>(),
-                                      stream_of(fw.off)),
-              "gala_gat_bwd_attn_f32");
-        return {daL, daL, dX};
+        const int st = be(fw.off).gat_bwd_ex(&cf.c, l.data_ptr<float>(), nullptr, wR.data_ptr<float>(),
+                                             bR.defined() ? bR.data_ptr<float>() : nullptr,
+                                             x.data_ptr<float>(), ldx, dY.data_ptr<float>(), lddy,
+                                             (int32_t)F, heads, (float)slope, GALA_SOFTMAX_REF,
+                                             alpha.data_ptr<float>(), qp, nullptr, daL.data_ptr<float>(),
+                                             stream_of(fw.off));
+        if (st != GALA_ERR_UNSUPPORTED) {
+            check(st, "gala_gat_bwd_ex_f32");
+            return {daL, daL, dX};
+        }
     }
-    if (!r.defined()) {  // the explicit source logits for the other paths
-        r = x.mv(wR.reshape({-1}));
+    if (q.defined()) {  // the paths below take alpha itself
+        alpha = materialise_alpha(fw, alpha, q);
+        q = torch::Tensor();
+        qp = nullptr;
+    }
+    if (!r.defined()) {  // the explicit (per-head) source logits for the other paths
+        if (heads == 1) {
+            r = x.mv(wR.reshape({-1}));
+        } else {
+            const int64_t D = F / heads;
+            r = (x.reshape({x.size(0), heads, D}) * wR.reshape({1, heads, D})).sum(2);
+        }
         if (bR.defined()) r = r + bR.reshape({-1});
         r = r.contiguous();
     }
@@ -727,46 +766,107 @@ GatGrads gat_backward(const torch::Tensor &l, torch::Tensor r, const torch::Tens
     return {daL, daR, dX};
 }
 
-// fused GAT layer: sddvv + LeakyReLU + edge softmax + weighted aggregation in one pass
+// One launch of the fused GAT forward (gala_gat_fwd_ex_f32) on slot 2li: aR, or its
+// per-head recompute from x (wR, bR).  alpha / q as the entry point documents.
+torch::Tensor gat_forward_launch(const Slot &s, const torch::Tensor &l, const torch::Tensor &r,
+                                 const torch::Tensor &x, const torch::Tensor &wR, const torch::Tensor &bR,
+                                 int heads, double slope, int64_t mode, float *alpha, float *q) {
+    CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+    const int64_t nrows = cv.c.n_rows, F = x.size(1);
+    cv.c.n_cols = x.size(0);
+    with_workspace(cv, s.off, F + 2 * heads);  // hub-row partials: acc[F], m[H], sum[H]
+    auto Y = rows_like(x, nrows);
+    check(be(s.off).gat_fwd_ex(&cv.c, l.data_ptr<float>(), r.defined() ? r.data_ptr<float>() : nullptr,
+                               r.defined() ? nullptr : wR.data_ptr<float>(),
+                               (!r.defined() && bR.defined()) ? bR.data_ptr<float>() : nullptr,
+                               x.data_ptr<float>(), x.stride(0), (int32_t)F, heads, (float)slope,
+                               (int32_t)mode, Y.data_ptr<float>(), Y.stride(0), alpha, q, stream_of(s.off)),
+          "gala_gat_fwd_ex_f32");
+    return Y;
+}
+
+// REF backward with the attention recomputed from the forward's q (the forward stored no
+// alpha): one kernel for dX and d_aL (= d_aR), gala_gat_bwd_fused_f32.  Returns false when
+// the kernel does not take this shape (then the caller rebuilds alpha).
+bool gat_backward_recompute(const torch::Tensor &l, const torch::Tensor &r, const torch::Tensor &x,
+                            const torch::Tensor &q, const torch::Tensor &dY_in, int64_t li, double slope,
+                            int heads, const torch::Tensor &wR, const torch::Tensor &bR, GatGrads &g) {
+    Slot fw = slot(2 * li);
+    const torch::Tensor dY = heads == 1 ? pad_rows4(dY_in) : dY_in.contiguous();
+    const int64_t F = x.size(1), nrows = fw.off.numel() / fw.segs - 1;
+    CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
+    cf.c.n_cols = x.size(0);
+    with_workspace(cf, fw.off, (F + 3) / 4 * 4 + 3 * heads);  // hub rows: dX[F] + 3 sums per head
+    check_on(dY, fw.off, "grad");
+    auto dX = rows_like(dY, nrows);
+    auto daL = torch::empty_like(l);
+    const int st = be(fw.off).gat_bwd_fused(&cf.c, l.data_ptr<float>(), r.defined() ? r.data_ptr<float>() : nullptr,
+                                            r.defined() ? nullptr : wR.data_ptr<float>(),
+                                            (!r.defined() && bR.defined()) ? bR.data_ptr<float>() : nullptr,
+                                            x.data_ptr<float>(), x.stride(0), dY.data_ptr<float>(), dY.stride(0),
+                                            (int32_t)F, heads, (float)slope, q.data_ptr<float>(),
+                                            dX.data_ptr<float>(), dX.stride(0), daL.data_ptr<float>(),
+                                            stream_of(fw.off));
+    if (st == GALA_ERR_UNSUPPORTED) return false;
+    check(st, "gala_gat_bwd_fused_f32");
+    g = {daL, daL, dX};
+    return true;
+}
+
+// REF on one pattern: the forward keeps only q (alpha is recomputed by the backward)
+bool recompute_attention(int64_t li, int64_t mode) {
+    return mode == GALA_SOFTMAX_REF && same_pattern(slot(2 * li), slot(2 * li + 1));
+}
+
+// fused GAT layer: sddvv + LeakyReLU + edge softmax + weighted aggregation in one pass.
+// REF mode keeps the attention factored (p per edge, q per row: no normalisation pass over
+// the edges); FIXED materialises alpha (its backward needs the transposed alpha).
 struct GatAggregate : public torch::autograd::Function<GatAggregate> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor aL, torch::Tensor aR,
                                  torch::Tensor X, int64_t li, double slope, int64_t mode) {
         Slot s = slot(2 * li);
-        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
         auto l = aL.contiguous(), r = aR.contiguous();
-        const int64_t nrows = cv.c.n_rows;
+        const int64_t nrows = s.off.numel() / s.segs - 1;
         const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
         auto x = heads == 1 ? pad_rows4(X) : X.contiguous();
         check_dev(l, torch::kFloat, "attn_l");
         check_dev(r, torch::kFloat, "attn_r");
         check_dev(x, torch::kFloat, "X");
-        const int64_t F = x.size(1);
-        cv.c.n_cols = x.size(0);
-        with_workspace(cv, s.off, F + 2 * heads);  // hub-row partials: acc[F], m[H], sum[H]
-        auto Y = rows_like(x, nrows);
-        auto alpha = torch::empty({s.cols.numel() * heads}, fopts(x));
         check_on(l, s.off, "attn_l");
         check_on(r, s.off, "attn_r");
         check_on(x, s.off, "X");
-        check(be(s.off).gat_fwd(&cv.c, l.data_ptr<float>(), r.data_ptr<float>(), x.data_ptr<float>(),
-                                x.stride(0), (int32_t)F, heads, (float)slope, (int32_t)mode,
-                                Y.data_ptr<float>(), Y.stride(0), alpha.data_ptr<float>(), stream_of(s.off)),
-              "gala_gat_fwd_f32");
+        // REF on one pattern: q only (the backward recomputes alpha); REF otherwise: the
+        // factored (p, q); FIXED: alpha itself (its backward permutes it onto A^T)
+        const bool recompute = recompute_attention(li, mode);
+        const bool factored = mode == GALA_SOFTMAX_REF;
+        auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
+        auto q = factored ? torch::empty({nrows * heads}, fopts(x)) : torch::empty({0}, fopts(x));
+        auto Y = gat_forward_launch(s, l, r, x, {}, {}, heads, slope, mode,
+                                    recompute ? nullptr : alpha.data_ptr<float>(),
+                                    factored ? q.data_ptr<float>() : nullptr);
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
         ctx->saved_data["mode"] = mode;
         ctx->saved_data["heads"] = (int64_t)heads;
-        ctx->save_for_backward({l, r, x, alpha});
+        ctx->save_for_backward({l, r, x, alpha, q});
         return Y;
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         auto l = sv[0], r = sv[1], x = sv[2], alpha = sv[3];
-        GatGrads g = gat_backward(l, r, x, alpha, grad_outputs[0],
-                                  ctx->saved_data["li"].toInt(),
-                                  ctx->saved_data["slope"].toDouble(),
-                                  ctx->saved_data["mode"].toInt(),
-                                  (int)ctx->saved_data["heads"].toInt(), {}, {});
+        torch::Tensor q = sv[4].numel() > 0 ? sv[4] : torch::Tensor();
+        const int64_t li = ctx->saved_data["li"].toInt(), mode = ctx->saved_data["mode"].toInt();
+        const double slope = ctx->saved_data["slope"].toDouble();
+        const int heads = (int)ctx->saved_data["heads"].toInt();
+        GatGrads g;
+        if (alpha.numel() == 0 && !gat_backward_recompute(l, r, x, q, grad_outputs[0], li, slope, heads, {}, {}, g)) {
+            // the fused kernel does not take this shape: rebuild the factored p
+            alpha = torch::empty({slot(2 * li).cols.numel() * heads}, fopts(x));
+            gat_forward_launch(slot(2 * li), l, r, x, {}, {}, heads, slope, mode, alpha.data_ptr<float>(),
+                               q.data_ptr<float>());
+        }
+        if (alpha.numel() > 0)
+            g = gat_backward(l, r, x, alpha, q, grad_outputs[0], li, slope, mode, heads, {}, {});
         return {g.daL.view_as(l), g.daR.view_as(r), g.dX, torch::Tensor(), torch::Tensor(),
                 torch::Tensor()};
     }
@@ -774,66 +874,87 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
 
 // The DSL's GAT layer (tests/GALA-DSL/gat/*: attnR = dsl.nn.ffn(res, out=1); ...;
 // res = aggregate_fn(G.graphs, res)): the source logit is a Linear of the aggregated rows,
-// so the kernels recompute aR[col] = <X[col], wR> + bR from the X row they gather instead
-// of reading aR (gala_gat_{fwd,bwd}_attn_f32).  The Linear's gradients follow from d_aR:
-// d wR = d_aR^T X (gala_dense_grad_f32), d bR = sum d_aR, dX += d_aR wR.
+// so the kernels recompute aR[col] from the X row they gather instead of reading aR
+// (gala_gat_{fwd,bwd}_ex_f32 with wR).  With H heads (the galac heads(H) extension) the
+// Linear is per head: aR[j,h] = <X[j, hD:(h+1)D], wR[hD:(h+1)D]> + bR[h], wR of F
+// elements, bR of H.  Its gradients follow from d_aR: d wR[head h] = sum_j d_aR[j,h]
+// X[j, head h], d bR = sum d_aR, dX[:, head h] += d_aR[:, h] wR[head h].
 struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor aL, torch::Tensor X,
                                  torch::Tensor wR, torch::Tensor bR, int64_t li, double slope,
                                  int64_t mode) {
         Slot s = slot(2 * li);
-        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
-        auto l = aL.contiguous(), x = pad_rows4(X), w = wR.contiguous();
+        auto l = aL.contiguous(), w = wR.contiguous();
         torch::Tensor b = bR.defined() && bR.numel() > 0 ? bR.contiguous() : torch::Tensor();
+        const int64_t nrows = s.off.numel() / s.segs - 1;
+        const int heads = (int)(l.numel() / std::max<int64_t>(nrows, 1));
+        auto x = heads == 1 ? pad_rows4(X) : X.contiguous();
         check_dev(l, torch::kFloat, "attn_l");
         check_dev(x, torch::kFloat, "X");
         check_dev(w, torch::kFloat, "attn_r weight");
-        const int64_t nrows = cv.c.n_rows, F = x.size(1);
-        TORCH_CHECK(l.numel() == nrows && w.numel() == F, "gala: gat_aggregate_ffn is one head");
+        const int64_t F = x.size(1);
+        TORCH_CHECK(l.numel() == nrows * heads && w.numel() == F && F % heads == 0,
+                    "gala: gat_aggregate_ffn: attn_l [N, H], attn_r weight of F = H*D elements");
+        TORCH_CHECK(!b.defined() || b.numel() == heads, "gala: gat_aggregate_ffn: attn_r bias of H elements");
         check_on(l, s.off, "attn_l");
         check_on(x, s.off, "X");
         check_on(w, s.off, "attn_r weight");
         if (b.defined()) check_on(b, s.off, "attn_r bias");
-        cv.c.n_cols = x.size(0);
-        with_workspace(cv, s.off, F + 2);
-        auto Y = rows_like(x, nrows);
-        auto alpha = torch::empty({s.cols.numel()}, fopts(x));
-        check(be(s.off).gat_fwd_attn(&cv.c, l.data_ptr<float>(), w.data_ptr<float>(),
-                                     b.defined() ? b.data_ptr<float>() : nullptr,
-                                     x.data_ptr<float>(), x.stride(0), (int32_t)F, (float)slope,
-                                     (int32_t)mode, Y.data_ptr<float>(), Y.stride(0),
-                                     alpha.data_ptr<float>(), stream_of(s.off)),
-              "gala_gat_fwd_attn_f32");
+        const bool recompute = recompute_attention(li, mode);
+        const bool factored = mode == GALA_SOFTMAX_REF;
+        auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
+        auto q = factored ? torch::empty({nrows * heads}, fopts(x)) : torch::empty({0}, fopts(x));
+        auto Y = gat_forward_launch(s, l, {}, x, w, b, heads, slope, mode,
+                                    recompute ? nullptr : alpha.data_ptr<float>(),
+                                    factored ? q.data_ptr<float>() : nullptr);
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
         ctx->saved_data["mode"] = mode;
+        ctx->saved_data["heads"] = (int64_t)heads;
         ctx->saved_data["has_bias"] = b.defined();
-        ctx->save_for_backward({l, x, w, b.defined() ? b : torch::empty({0}, fopts(x)), alpha});
+        ctx->save_for_backward({l, x, w, b.defined() ? b : torch::empty({0}, fopts(x)), alpha, q});
         return Y;
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         auto l = sv[0], x = sv[1], w = sv[2], alpha = sv[4];
+        torch::Tensor q = sv[5].numel() > 0 ? sv[5] : torch::Tensor();
         const bool has_bias = ctx->saved_data["has_bias"].toBool();
+        const int heads = (int)ctx->saved_data["heads"].toInt();
+        const int64_t li = ctx->saved_data["li"].toInt(), mode = ctx->saved_data["mode"].toInt();
+        const double slope = ctx->saved_data["slope"].toDouble();
         torch::Tensor b = has_bias ? sv[3] : torch::Tensor();
-        GatGrads g = gat_backward(l, {}, x, alpha, grad_outputs[0],
-                                  ctx->saved_data["li"].toInt(),
-                                  ctx->saved_data["slope"].toDouble(),
-                                  ctx->saved_data["mode"].toInt(), 1, w, b);
-        auto daR = g.daR.reshape({-1, 1}).contiguous();
+        GatGrads g;
+        if (alpha.numel() == 0 && !gat_backward_recompute(l, {}, x, q, grad_outputs[0], li, slope, heads, w, b, g)) {
+            alpha = torch::empty({slot(2 * li).cols.numel() * heads}, fopts(x));
+            gat_forward_launch(slot(2 * li), l, {}, x, w, b, heads, slope, mode, alpha.data_ptr<float>(),
+                               q.data_ptr<float>());
+        }
+        if (alpha.numel() > 0) g = gat_backward(l, {}, x, alpha, q, grad_outputs[0], li, slope, mode, heads, w, b);
         const int64_t N = x.size(0);
         const int32_t F = (int32_t)x.size(1);
-        auto dW = torch::empty({1, F}, fopts(x));
-        auto db = torch::empty({1}, fopts(x));
-        const Backend &B = be(x);
-        const int64_t wsb = B.dense_ws(N, F, 1);
-        TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
-        auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(x));
-        check(B.dense_grad(N, F, 1, x.data_ptr<float>(), x.stride(0), daR.data_ptr<float>(), 1,
-                           dW.data_ptr<float>(), db.data_ptr<float>(), 0, ws.data_ptr<float>(),
-                           wsb, stream_of(x)),
-              "gala_dense_grad_f32");
-        g.dX.addr_(daR.reshape({-1}), w.reshape({-1}));  // through aR = X wR^T + bR
+        torch::Tensor dW, db;
+        if (heads == 1) {
+            auto daR = g.daR.reshape({-1, 1}).contiguous();
+            dW = torch::empty({1, F}, fopts(x));
+            db = torch::empty({1}, fopts(x));
+            const Backend &B = be(x);
+            const int64_t wsb = B.dense_ws(N, F, 1);
+            TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
+            auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(x));
+            check(B.dense_grad(N, F, 1, x.data_ptr<float>(), x.stride(0), daR.data_ptr<float>(), 1,
+                               dW.data_ptr<float>(), db.data_ptr<float>(), 0, ws.data_ptr<float>(),
+                               wsb, stream_of(x)),
+                  "gala_dense_grad_f32");
+            g.dX.addr_(daR.reshape({-1}), w.reshape({-1}));  // through aR = X wR^T + bR
+        } else {  // per head: the block-diagonal Linear
+            const int64_t D = F / heads;
+            auto daR = g.daR.reshape({N, heads});
+            auto xr = x.reshape({N, heads, D});
+            dW = (daR.unsqueeze(2) * xr).sum(0).reshape(w.sizes());
+            db = daR.sum(0);
+            g.dX.view({N, heads, D}).add_(daR.unsqueeze(2) * w.reshape({1, heads, D}));
+        }
         return {g.daL.view_as(l), g.dX, dW.view_as(w), has_bias ? db.view_as(b) : torch::Tensor(),
                 torch::Tensor(), torch::Tensor(), torch::Tensor()};
     }

@@ -66,6 +66,20 @@ int gala_cpu_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float 
                               const float *bR, const float *X, int64_t ldx, const float *dY,
                               int64_t lddy, int32_t F, float slope, const float *alpha,
                               float *d_aL, void *stream);
+int gala_cpu_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                            const float *wR, const float *bR, const float *X, int64_t ldx,
+                            int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
+                            int64_t ldy, float *alpha_out, float *q_out, void *stream);
+int gala_cpu_gat_bwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                            const float *wR, const float *bR, const float *X, int64_t ldx,
+                            const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope,
+                            int32_t mode, const float *alpha, const float *q, float *d_logit,
+                            float *d_aL, void *stream);
+int gala_cpu_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                               const float *wR, const float *bR, const float *X, int64_t ldx,
+                               const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                               float slope, const float *q, float *dX, int64_t lddx,
+                               float *d_aL, void *stream);
 int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                               float *dst, void *stream);
 int gala_cpu_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GALA_ABI_VERSION 1
+#define GALA_ABI_VERSION 2
 
 typedef enum gala_status {
     GALA_OK = 0,
@@ -96,6 +96,12 @@ typedef struct gala_csr {
                                   NULL when n_seg == 1 (reference keeps `bounds` on the
                                   host: cuda.h:472-475 reads bounds_ptr on the CPU)        */
     const gala_split_plan_t *split; /* HOST pointer, NULL = no row splitting              */
+    const float *val_row_scale; /* device [n_rows*val_heads] or NULL: the edge values are
+                                   stored factored, A_e,h = val[e,h] * val_row_scale[row,h]
+                                   (rounded product).  The GAT forward's factored attention
+                                   output (gala_gat_fwd_ex_f32: p and q) is used this way as
+                                   the backward's alpha without materialising it.  Only the
+                                   SpMM and the GAT backward read it.                      */
 } gala_csr_t;
 
 /* ---- library information ------------------------------------------------------------ */
@@ -276,6 +282,51 @@ int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
                           const float *bR, const float *X, int64_t ldx, const float *dY,
                           int64_t lddy, int32_t F, float slope, const float *alpha, float *d_aL,
                           void *stream);
+
+/*
+ * The fused GAT forward / backward, general form (q_out may also be given with alpha_out
+ * NULL: then only Y and q are written, for gala_gat_bwd_fused_f32):
+ *   - the source logit comes from aR [n_cols, heads], or (aR == NULL) is recomputed from
+ *     the gathered rows per head: aR[j,h] = <X[j, hD:(h+1)D], wR[hD:(h+1)D]> + bR[h]
+ *     (bR nullable = 0; the multi-head GAT layer's attnR = a_r^h . res_j^h);
+ *   - the attention output is either alpha (q_out == NULL, as gala_gat_fwd_f32) or, in
+ *     REF mode, FACTORED: alpha_out receives p[e,h] = min(exp(s), 1e12) and q_out[r,h] =
+ *     1 / (S*1e-12 + sum_row p), so alpha = p * q (rounded) -- bit-identical to the
+ *     materialised alpha -- without the normalisation pass over the edges.  The backward
+ *     takes the same pair (q != NULL), and the dX SpMM reads it through
+ *     gala_csr_t.val = p, val_row_scale = q.
+ * Several heads need D = F/heads a multiple of the vector width with D/VEC a power of two
+ * for the recompute (else GALA_ERR_UNSUPPORTED).  Replaces the same chains as
+ * gala_gat_fwd_f32 / gala_gat_bwd_f32.
+ */
+int gala_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                        const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                        float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
+                        float *q_out, void *stream);
+int gala_gat_bwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                        const float *bR, const float *X, int64_t ldx, const float *dY,
+                        int64_t lddy, int32_t F, int32_t heads, float slope, int32_t mode,
+                        const float *alpha, const float *q, float *d_logit, float *d_aL,
+                        void *stream);
+
+/*
+ * REF-mode GAT backward with the attention RECOMPUTED and dX fused (square graph whose
+ * backward pattern is the forward one -- the undirected graphs the reference runs,
+ * cuda.h:1253-1257).  Per row r and head h, over the edges e = (r, c):
+ *   alpha = fl(min(exp(LeakyReLU(aL[r,h] + aR[c,h])), 1e12) * q[r,h])   (q: the forward's
+ *           q_out; aR or its per-head recompute from X as in gala_gat_fwd_ex_f32)
+ *   dX[r, head h] = sum_e alpha * dY[c, head h]       (bit-identical to gala_spmm_f32 over
+ *                                                      the materialised alpha)
+ *   d_aL[r,h] as gala_gat_bwd_f32 in REF mode (= d_aR), within fp32 rounding.
+ * With this the forward need not output alpha at all (gala_gat_fwd_ex_f32 with q_out and
+ * alpha_out NULL).  Replaces the backward of the emitted GAT layer: the weighted SpMM
+ * <K>_AutoGrad::backward (common.h:835-894) plus the edge chain of gala_gat_bwd_f32.
+ * Several heads need D/VEC a power of two (else GALA_ERR_UNSUPPORTED).
+ */
+int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                           const float *wR, const float *bR, const float *X, int64_t ldx,
+                           const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope,
+                           const float *q, float *dX, int64_t lddx, float *d_aL, void *stream);
 
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,

@@ -721,3 +721,132 @@ def test_ffn_fwd_strided_and_unsupported():
     with pytest.raises(_abi.GalaError):
         ops.ffn_fwd(dev(rng.uniform(-1, 1, (10, 602)).astype(np.float32)),
                     dev(rng.uniform(-1, 1, (256, 602)).astype(np.float32)))
+
+
+# ---- factored attention output (p, q) and the head-distributed forward ------------------
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (24, 3), (16, 8)])
+@pytest.mark.parametrize("split", [False, True])
+def test_gat_factored_alpha_bitexact(F, heads, split):
+    """REF mode, gala_gat_fwd_ex_f32 with q_out: alpha_out = p, q_out = 1/(sum + 1e-12),
+    and p * q (rounded) is BIT-identical to the materialised alpha of gala_gat_fwd_f32; Y
+    is identical too.  The backward on (p, q) equals the backward on alpha bit for bit, and
+    so does the dX SpMM over val = p with val_row_scale = q.  Against the oracle within the
+    tolerance (hub-row plan included)."""
+    g = powerlaw()
+    aL = features(g.n_rows, heads, seed=71)
+    aR = features(g.n_cols, heads, seed=72)
+    X = features(g.n_cols, F, seed=73)
+    dY = features(g.n_rows, F, seed=74)
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if split:
+        dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    Y, al = ops.gat_fwd(dg, dev(aL), dev(aR), dev(X), heads=heads, want_alpha=True)
+    Y2, p, q = ops.gat_fwd_ex(dg, dev(aL), dev(X), aR=dev(aR), heads=heads, factored=True)
+    assert torch.equal(Y, Y2)
+    rows = torch.from_numpy(np.repeat(np.arange(g.n_rows), np.diff(g.rowptr))).to(DEV)
+    alpha_f = (p.view(-1, heads) * q.view(-1, heads)[rows]).reshape(-1)
+    assert torch.equal(alpha_f, al)
+    Y_ref, al_ref = orc.gat_fwd(to_oracle(g), aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    np.testing.assert_allclose(host(Y2), Y_ref, **TOL)
+    np.testing.assert_allclose(host(alpha_f), al_ref, **TOL)
+    if 64 % heads == 0:   # the fused backward needs heads | lanes
+        d1, _ = ops.gat_bwd(dg, dev(aL), dev(aR), dev(X), dev(dY), al, heads=heads)
+        d2, _ = ops.gat_bwd_ex(dg, dev(aL), dev(X), dev(dY), p, q=q, aR=dev(aR), heads=heads)
+        assert torch.equal(d1, d2)
+    s1 = ops.spmm(dg.with_values(al, val_heads=heads), dev(dY))
+    s2 = ops.spmm(dg.with_values(p, val_heads=heads, row_scale=q), dev(dY))
+    assert torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
+@pytest.mark.parametrize("F,heads", [(256, 8), (64, 4), (32, 2), (48, 3)])
+def test_gat_multihead_attention_recompute(graph, mode, F, heads):
+    """gala_gat_fwd_ex_f32 with aR recomputed per head, aR[j,h] = <X[j, head h], wR[head h]>
+    + bR[h] (the multi-head GAT layer's source logit), against the oracle chain on that aR
+    (float64, rounded to fp32); REF backward with the same recompute on (p, q)."""
+    D = F // heads
+    aL = features(graph.n_rows, heads, seed=81)
+    X = features(graph.n_cols, F, seed=83)
+    dY = features(graph.n_rows, F, seed=84)
+    wR = features(1, F, seed=85).ravel() * 0.5
+    bR = features(1, heads, seed=86).ravel() * 0.1
+    aR = np.stack([X[:, h * D:(h + 1) * D].astype(np.float64) @ wR[h * D:(h + 1) * D].astype(np.float64) + bR[h]
+                   for h in range(heads)], 1).astype(np.float32)
+    og = to_oracle(graph)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=mode)
+    dg = ops.DeviceGraph.from_host(graph, split=False)
+    if 64 % heads:      # alpha of heads that do not divide the row group needs aR itself
+        with pytest.raises(_abi.GalaError):
+            ops.gat_fwd_ex(dg, dev(aL), dev(X), wR=dev(wR), bR=dev(bR), heads=heads, mode=mode, want_alpha=True)
+        Y = ops.gat_fwd_ex(dg, dev(aL), dev(X), wR=dev(wR), bR=dev(bR), heads=heads, mode=mode)
+        np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+        return
+    Y, al = ops.gat_fwd_ex(dg, dev(aL), dev(X), wR=dev(wR), bR=dev(bR), heads=heads, mode=mode, want_alpha=True)
+    np.testing.assert_allclose(host(al), al_ref, **TOL)
+    np.testing.assert_allclose(host(Y), Y_ref, **TOL)
+    if mode == _abi.GALA_SOFTMAX_REF and heads in (1, 2, 4, 8):  # fused backward: heads | lanes
+        _, p, q = ops.gat_fwd_ex(dg, dev(aL), dev(X), wR=dev(wR), bR=dev(bR), heads=heads, factored=True)
+        _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=mode)
+        daL, _ = ops.gat_bwd_ex(dg, dev(aL), dev(X), dev(dY), p, q=q, wR=dev(wR), bR=dev(bR), heads=heads)
+        np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+
+
+def test_gat_ex_rejects_bad_arguments():
+    g = cora_like()
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    aL, X = dev(features(g.n_rows, 1)), dev(features(g.n_cols, 32))
+    with pytest.raises(_abi.GalaError):    # factored output is REF only
+        ops.gat_fwd_ex(dg, aL, X, aR=dev(features(g.n_cols, 1)), mode=_abi.GALA_SOFTMAX_FIXED, factored=True)
+    with pytest.raises(_abi.GalaError):    # recompute needs wR
+        ops.gat_fwd_ex(dg, aL, X)
+    with pytest.raises(_abi.GalaError):    # val_row_scale without values
+        ops.spmm(ops.DeviceGraph(g.n_rows, g.n_cols, dg.rowptr, dg.col, None, val_row_scale=aL), X)
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (24, 3)])
+@pytest.mark.parametrize("layout_", ["plain", "tiled", "split"])
+@pytest.mark.parametrize("rc", [False, True])
+def test_gat_bwd_fused_recompute(F, heads, layout_, rc):
+    """gala_gat_bwd_fused_f32: alpha recomputed from (aL, aR | wR, bR) and the forward's q
+    (gala_gat_fwd_ex_f32 with q_out only).  dX is BIT-identical to the SpMM over the
+    materialised alpha; d_aL matches the alpha-based fused backward and the oracle within
+    the tolerance.  Plain, column-tiled and hub-row-split graphs."""
+    if rc and 64 % heads:
+        pytest.skip("recompute with heads that do not divide the row group: covered by the forward test")
+    g = powerlaw()
+    if layout_ == "tiled":
+        g = layout.col_tile(g, 1000)
+    D = F // heads
+    aL = features(g.n_rows, heads, seed=91)
+    X = features(g.n_cols, F, seed=93)
+    dY = features(g.n_rows, F, seed=94)
+    if rc:
+        wR = features(1, F, seed=95).ravel() * 0.5
+        bR = features(1, heads, seed=96).ravel() * 0.1
+        aR = np.stack([X[:, h * D:(h + 1) * D].astype(np.float64) @ wR[h * D:(h + 1) * D].astype(np.float64) + bR[h]
+                       for h in range(heads)], 1).astype(np.float32)
+        kw = dict(wR=dev(wR), bR=dev(bR))
+    else:
+        aR = features(g.n_cols, heads, seed=92)
+        kw = dict(aR=dev(aR))
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if layout_ == "split":
+        dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    Y, q = ops.gat_fwd_ex(dg, dev(aL), dev(X), heads=heads, factored="q", **kw)
+    Y2, p, q2 = ops.gat_fwd_ex(dg, dev(aL), dev(X), heads=heads, factored=True, **kw)
+    if layout_ == "split" and 8 % heads:
+        # alpha_out of heads that do not divide the row group runs hub rows unsplit
+        torch.testing.assert_close(Y, Y2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(q, q2, rtol=1e-5, atol=1e-6)
+    else:
+        assert torch.equal(Y, Y2) and torch.equal(q, q2)
+    dX, daL = ops.gat_bwd_fused(dg, dev(aL), dev(X), dev(dY), q, heads=heads, **kw)
+    dX_ref = ops.spmm(dg.with_values(p, val_heads=heads, row_scale=q), dev(dY))
+    assert torch.equal(dX, dX_ref)
+    og = to_oracle(g)
+    _, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+    with pytest.raises(_abi.GalaError):   # dY[col] needs a square pattern
+        rect = ops.DeviceGraph(g.n_rows, g.n_rows + 5, dg.rowptr, dg.col, n_seg=dg.n_seg, bounds=dg.bounds)
+        ops.gat_bwd_fused(rect, dev(aL), dev(np.vstack([X, X[:5]])), dev(dY), q, heads=heads, **kw)
