@@ -64,6 +64,8 @@ struct Weight {
     enum Type { Linear, Eps } type = Linear;
     int64_t in = 0, out = 0;
     double init = 0;        // Eps initial value
+    int64_t heads = 1;      // > 1: a multi-head attention vector (galac gat_heads(H)): weight
+                            // [1, in] read per head slice, bias [heads]; out = 1 per head
 };
 
 // Schedule and program-level settings (ModelConfig, ir/frontend_metadata.h:44-140, and
@@ -86,6 +88,8 @@ struct Schedule {
          train_code_motion = true;
     int64_t iterations = 0, validation_step = 0;
     int gat_mode = 0;              // 0 = reference gradients (GALA_SOFTMAX_REF), 1 = fixed
+    int64_t gat_heads = 1;         // galac extension gat_heads(H): attention layers but the
+                                   // last run H heads of `hs` features each
 };
 
 struct Module {

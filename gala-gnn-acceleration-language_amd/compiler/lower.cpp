@@ -93,7 +93,7 @@ std::string Module::dump() const {
                 o << " param=" << n.param;
             if (n.weight >= 0)
                 o << " w=" << weights[n.weight].name << "[" << weights[n.weight].in << "x"
-                  << weights[n.weight].out << "]";
+                  << weights[n.weight].out << (weights[n.weight].heads > 1 ? " per head" : "") << "]";
             if (n.op == Op::Aggregate || n.op == Op::GcnAggregate || n.op == Op::GatAggregate)
                 o << " graph=" << n.graph;
             if (n.layer >= 0) o << " layer=" << n.layer;
@@ -123,11 +123,12 @@ std::string Module::to_json() const {
       << ", \"label_size\": " << s.label_size << ", \"col_tile\": " << s.col_tile
       << ", \"data_sample\": " << s.data_sample << ", \"kernel_sample\": " << s.kernel_sample
       << ", \"dynamic_sample\": " << s.dynamic_sample << ", \"iterations\": " << s.iterations
-      << ", \"gat_mode\": " << s.gat_mode << "},\n \"weights\": [";
+      << ", \"gat_mode\": " << s.gat_mode << ", \"gat_heads\": " << s.gat_heads << "},\n \"weights\": [";
     for (size_t k = 0; k < weights.size(); ++k)
         o << (k ? ", " : "") << "{\"name\": " << str(weights[k].name) << ", \"type\": "
           << (weights[k].type == Weight::Linear ? "\"linear\"" : "\"eps\"") << ", \"in\": "
-          << weights[k].in << ", \"out\": " << weights[k].out << ", \"init\": " << weights[k].init << "}";
+          << weights[k].in << ", \"out\": " << weights[k].out << ", \"init\": " << weights[k].init
+          << ", \"heads\": " << weights[k].heads << "}";
     o << "],\n \"values\": [";
     for (size_t k = 0; k < values.size(); ++k) {
         const Value &v = values[k];
@@ -352,6 +353,12 @@ class Lowering {
         // galac extension: exact GAT gradients (GALA_SOFTMAX_FIXED) instead of the
         // reference's backward chain
         else if (cp == "gat_fixed_gradients") s.gat_mode = bool_arg(v, "gat_fixed_gradients") ? 1 : 0;
+        // galac extension: multi-head attention (the reference DSL is single-head,
+        // frontend.y:987-1008); BASELINE's 8-head GAT is gat_heads(8)
+        else if (cp == "gat_heads") {
+            s.gat_heads = int_arg(v, 0, "gat_heads");
+            if (s.gat_heads < 1 || s.gat_heads > 64) throw DslError(v.at, "gat_heads(H) needs 1 <= H <= 64");
+        }
         else throw DslError(v.at, "unsupported statement '" + (cp.empty() ? std::string("?") : cp) + "'");
     }
 
@@ -488,6 +495,7 @@ class Lowering {
         int edge_vals = -1;              // G.edges.vals once assigned
         int layer = 0;
         bool last = false;
+        int64_t heads = 1;               // attention heads of this layer (gat_heads)
     };
 
     int node(Op op, std::vector<int> in, const std::string &name, Kind k, int64_t width,
@@ -548,8 +556,14 @@ class Lowering {
         c.feats = c.in_feats = feats;
         c.layer = layer;
         c.last = layer == m_.num_layers - 1;
-        for (const auto &kv : c.env)
+        bool attention = false;
+        for (const auto &kv : c.env) {
             if (kv.second.t == Sym::Graph) c.gname = kv.first;
+            attention = attention || kv.second.t == Sym::EdgeFn;
+        }
+        // multi-head attention in every attention layer but the output layer (one head:
+        // the standard GAT output, BASELINE config 3's layer 2)
+        c.heads = (attention && !c.last) ? m_.sched.gat_heads : 1;
         if (c.gname.empty()) throw DslError(ld.at, "layer " + ld.name + " has no graph parameter");
         int out = -1;
         for (const StmtP &st : ld.body) {
@@ -705,8 +719,18 @@ class Lowering {
             // names as gala.cu's: efc<k> attention vectors (FFN_OP_EDGE), sfc<k> a second
             // FFN of the layer input (FFN_OP_SELF), fc<k> otherwise
             const char *prefix = out == 1 ? "efc" : (xv == c.in_feats && ffn_reads_input_twice(c) ? "sfc" : "fc");
-            const int w = new_weight(prefix, in, out);
-            return Sym::of_val(node(Op::Ffn, {xv}, out == 1 ? "attn" : "res", Kind::Node, out, c, 0, w));
+            if (c.heads > 1 && out == 1) {
+                // one attention vector per head over that head's slice of x
+                if (in % c.heads != 0)
+                    throw DslError(e.at, "gat_heads(" + std::to_string(c.heads) + "): attention input of " +
+                                             std::to_string(in) + " columns is not a whole number of heads");
+                const int w = new_weight(prefix, in, 1);
+                m_.weights[w].heads = c.heads;
+                return Sym::of_val(node(Op::Ffn, {xv}, "attn", Kind::Node, c.heads, c, 0, w));
+            }
+            const int64_t width = out == 1 ? 1 : out * c.heads;  // H heads of `out` features
+            const int w = new_weight(prefix, in, width);
+            return Sym::of_val(node(Op::Ffn, {xv}, out == 1 ? "attn" : "res", Kind::Node, width, c, 0, w));
         }
         if (cp == "dsl.nn.scalar") {
             const Expr *x = arg(e, 0);
@@ -721,7 +745,7 @@ class Lowering {
             if (!x) throw DslError(e.at, "softmax(G, edge_values)");
             const int xv = as_val(eval(*x, c), *x, "softmax");
             if (m_.values[xv].kind != Kind::Edge) throw DslError(x->at, "softmax needs edge values");
-            return Sym::of_val(node(Op::Softmax, {xv}, "attn", Kind::Edge, 1, c));
+            return Sym::of_val(node(Op::Softmax, {xv}, "attn", Kind::Edge, m_.values[xv].width, c));
         }
         if (cp == "dsl.non_ln.ReLU" || cp == "dsl.non_ln.LeakyReLU") {
             const Expr *x = arg(e, 0);
@@ -760,9 +784,11 @@ class Lowering {
                 const Expr *a = arg(e, 1), *b = arg(e, 2);
                 if (!a || !b) throw DslError(e.at, "edge_fn(G, a_src, a_dst)");
                 const int av = as_val(eval(*a, c), *a, "edge_fn"), bv = as_val(eval(*b, c), *b, "edge_fn");
-                const int s = node(Op::EdgeAdd, {av, bv}, "attn", Kind::Edge, 1, c);
+                const int64_t h = m_.values[av].width;
+                if (m_.values[bv].width != h) throw DslError(e.at, "edge_fn: source / destination logits differ in heads");
+                const int s = node(Op::EdgeAdd, {av, bv}, "attn", Kind::Edge, h, c);
                 // ATTN -> addLeakyReLU(0.2) (frontend.y:1000-1003, 786-800)
-                return Sym::of_val(node(Op::LeakyRelu, {s}, "attn", Kind::Edge, 1, c, 0.2));
+                return Sym::of_val(node(Op::LeakyRelu, {s}, "attn", Kind::Edge, h, c, 0.2));
             }
         }
         throw DslError(e.at, "unknown function '" + (cp.empty() ? std::string("?") : cp) + "'");

@@ -35,8 +35,10 @@ bool linear_unary(const Module &m, const Node &n) {
     // ops f with f(x W + b) handled like the reference: RowBroadcast (x is in[1]),
     // Aggregate (x is in[0]; any edge weights are fixed within a forward), ScaleEps
     if (n.dead) return false;
+    // per-head attention weights (gat_heads) scale each head's columns differently: an FFN
+    // that mixes heads does not commute with that aggregation
+    if (n.op == Op::Aggregate && n.in.size() > 1 && m.values[n.in[1]].width > 1) return false;
     return n.op == Op::RowBroadcast || n.op == Op::Aggregate || n.op == Op::ScaleEps;
-    (void)m;
 }
 
 int data_input_index(const Node &n) { return n.op == Op::RowBroadcast ? 1 : 0; }

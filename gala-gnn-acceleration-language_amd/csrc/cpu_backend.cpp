@@ -222,7 +222,9 @@ extern "C" int gala_cpu_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const 
     const int wm = (M + 31) / 32;
     if (wm > 8 || (int64_t)((K + 1) & ~1) * 32 * wm > 16384) return GALA_ERR_UNSUPPORTED;
     if (!Y || (K > 0 && (!X || !W))) return GALA_ERR_INVALID_ARG;
-    // bias first, then the products in k order: the matrix cores' fmaf chain
+    // bias first, then the products in k order.  The GPU kernel runs
+    // v_mfma_f32_32x32x2_f32, which adds two products per step with its own internal
+    // rounding, so CPU and GPU agree within fp32 summation tolerance, not bit for bit.
 #pragma omp parallel for schedule(static, 256)
     for (int64_t n = 0; n < n_rows; ++n)
         for (int32_t m = 0; m < M; ++m) {
@@ -425,6 +427,9 @@ extern "C" int gala_cpu_edge_softmax_bwd_f32(const gala_csr_t *A, const float *a
 static int cpu_gat_fwd(const gala_csr_t *A, const float *aL, const float *aR, const float *X,
                        int64_t ldx, int32_t F, int32_t heads, float slope, int32_t mode, float *Y,
                        int64_t ldy, float *alpha_out, float *q_out) {
+    const bool partial = (mode & GALA_GAT_PARTIAL) != 0;  // see gala_hip.h
+    mode &= ~GALA_GAT_PARTIAL;
+    if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1) return GALA_ERR_INVALID_ARG;
@@ -469,8 +474,8 @@ static int cpu_gat_fwd(const gala_csr_t *A, const float *aL, const float *aR, co
                 const float den = mode == GALA_SOFTMAX_REF ? sum + (float)S * 1e-12f : sum;
                 const float q = 1.0f / den;
                 const bool empty = mode != GALA_SOFTMAX_REF && sum == 0.0f;
-                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = empty ? 0.0f : acc[f] * q;
-                if (q_out) q_out[r * H + h] = q;
+                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = partial ? acc[f] : empty ? 0.0f : acc[f] * q;
+                if (q_out) q_out[r * H + h] = partial ? sum : q;
                 if (!alpha_out) continue;
                 for (int32_t s = 0; s < S; ++s) {
                     int64_t e0, e1;
@@ -630,7 +635,7 @@ extern "C" int gala_cpu_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, con
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F) return GALA_ERR_INVALID_ARG;
-    if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
+    if (q_out && (mode & ~GALA_GAT_PARTIAL) != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aR && (!wR || (!X && A->n_cols > 0))) return GALA_ERR_INVALID_ARG;
     std::vector<float> rc;

@@ -117,7 +117,6 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
     const int H = gl_.H, hh = gl_.hh;
     const int lane = threadIdx.x & (kWave - 1);
     const int hl = lane & (HW - 1);
-    const int gbase = lane & ~(HW - 1);
     const int kl = hl % UH;                // this lane's first edge of a batch
     // owners hold their head's values: every lane for one head, valid lanes for several
     const bool store = park && hl < UH && (H == 1 || gl_.cv);
@@ -130,11 +129,7 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         int64_t c[U];
         V x[U][CH];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
-            c[k] = p.col[e0 + j];
-        }
+        load_batch_cols<G, U>(p, e0, n, j0, c);
         float ar[NK];
         if (!RC) {
 #pragma unroll
@@ -197,10 +192,10 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
             for (int i = 0; i < NK; ++i) pend[i] = (MODE == GALA_SOFTMAX_REF) ? pe[i] : z[i];
             pend_j0 = j0;
         }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const float pk = __shfl(pe[k / UH], gbase + (k % UH), 64);
-            if (j0 + k >= n) continue;
+        static_for<0, U>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const float pk = group_bcast<HW, k % UH>(pe[k / UH]);
+            if (j0 + k >= n) return;
             st.sum = __fadd_rn(st.sum, pk);
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) {
@@ -208,7 +203,7 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
 #pragma unroll
                 for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(pk, xv[i], st.acc[ch][i]);
             }
-        }
+        });
     }
     if (store && pend_j0 >= 0) {
 #pragma unroll
@@ -227,13 +222,15 @@ __device__ __forceinline__ void gat_fwd_edges(const EdgeParams &p, const GatDev 
         gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, park, e0, e1, st);
 }
 
-// Y[row] = acc * q with q = 1 / (sum [+ S * 1e-12 in REF mode]); returns q.
+// Y[row] = acc * q with q = 1 / (sum [+ S * 1e-12 in REF mode]); returns q.  Partial
+// (GALA_GAT_PARTIAL, REF): Y = acc unnormalised and the raw sum is returned, for a caller
+// that adds the partial rows of several column ranges first (vertex cut).
 template <int G, int VEC, int CH, bool RC, int MODE>
 __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
                                                int64_t row, int nseg, const FwdState<VEC, CH> &st) {
     typedef typename GVec<VEC>::T V;
     const float den = (MODE == GALA_SOFTMAX_REF) ? st.sum + (float)nseg * 1e-12f : st.sum;
-    const float q = 1.0f / den;
+    const float q = d.partial ? 1.0f : 1.0f / den;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
         if (!gl_.ln.valid[ch]) continue;
@@ -241,7 +238,8 @@ __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G,
         float *ov = reinterpret_cast<float *>(&out);
 #pragma unroll
         for (int i = 0; i < VEC; ++i)
-            ov[i] = (MODE != GALA_SOFTMAX_REF && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
+            ov[i] = d.partial ? st.acc[ch][i]
+                    : (MODE != GALA_SOFTMAX_REF && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
         float *yp = d.Y + row * d.ldy + gl_.ln.off[ch];
         if (gl_.ln.nv[ch] == VEC) {
             *reinterpret_cast<V *>(yp) = out;
@@ -251,7 +249,7 @@ __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G,
                 if (gl_.ln.in(ch, i)) yp[i] = ov[i];
         }
     }
-    return q;
+    return d.partial ? st.sum : q;
 }
 
 // alpha of the parked (edge, head) values [t0, t1) of one row: lane g handles head g % H
@@ -713,11 +711,14 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
+    const bool partial = (mode & GALA_GAT_PARTIAL) != 0;
+    mode &= ~GALA_GAT_PARTIAL;
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
     if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
+    if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
     int vec = 4;
@@ -734,6 +735,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.mode = mode;
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
     a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out, a.d.q_out = q_out;
+    a.d.partial = partial ? 1 : 0;
     a.hs = (hipStream_t)stream;
     a.split = (!alpha_out || G % heads == 0) && hub_split(A, (int64_t)F + 2 * heads, &a.sp);
     const bool rc = aR == nullptr;

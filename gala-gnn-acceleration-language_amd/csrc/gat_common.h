@@ -3,6 +3,8 @@
 // operand block, the per-lane view of a row, the attention recompute.
 #pragma once
 
+#include <type_traits>
+
 #include "edge_common.h"
 
 namespace gala {
@@ -10,6 +12,48 @@ namespace gala {
 // RC (one head): the source logit aR[col] = <X[col,:], wR> + bR is recomputed from the X
 // row the aggregation gathers anyway (the DSL's attnR = dsl.nn.ffn(res, out=1) of the
 // aggregated `res`, tests/GALA-DSL/gat/*), instead of a separate random aR[col] read.
+// The columns of edges j0 .. j0+U-1 of a row (clamped to the row's last edge).  With one
+// row per wave (G = 64) they are wave-uniform: one coalesced load of the U columns, spread
+// to scalar registers with v_readlane, so the gathered rows' addresses are formed on the
+// scalar unit (about 6 VALU instructions per edge and lane otherwise).
+template <int G, int U>
+__device__ __forceinline__ void load_batch_cols(const EdgeParams &p, int64_t e0, int32_t n, int32_t j0,
+                                                int64_t (&c)[U]) {
+    if constexpr (G == 64) {
+        const int kk = threadIdx.x & (U - 1);
+        const int32_t cu = p.col[e0 + ((j0 + kk < n) ? j0 + kk : n - 1)];
+#pragma unroll
+        for (int k = 0; k < U; ++k) c[k] = __builtin_amdgcn_readlane(cu, k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < U; ++k) c[k] = p.col[e0 + ((j0 + k < n) ? j0 + k : n - 1)];
+    }
+}
+
+// Broadcast of lane SRC of each aligned group of HW lanes to the group, SRC a compile-time
+// constant: ds_swizzle in bitmask mode for HW <= 32 (no address VGPR, unlike ds_bpermute),
+// v_readlane for a whole wave (its value is wave-uniform).
+template <int HW, int SRC>
+__device__ __forceinline__ float group_bcast(float v) {
+    if constexpr (HW == 1) {
+        return v;
+    } else if constexpr (HW <= 32) {
+        constexpr int pattern = (0x1F & ~(HW - 1)) | (SRC << 5);  // lane' = (lane & and) | or
+        return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), pattern));
+    } else {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), SRC));
+    }
+}
+
+// f(std::integral_constant<int, K>) for K = B .. E-1 (compile-time loop index)
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for(Fn &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 // With several heads the dot runs over the head's HW lanes (its slice of X and wR): the
 // standard multi-head GAT source logit <X[col, hD:(h+1)D], wR[hD:(h+1)D]> + bR[h].
 template <int HW, int VEC, int CH>
@@ -47,6 +91,7 @@ struct GatDev {
     int64_t ldx, ldy, lddy, lddx;
     int32_t F;
     float slope;
+    int32_t partial;                 // forward, GALA_GAT_PARTIAL: unnormalised Y, raw sums in q_out
 };
 
 

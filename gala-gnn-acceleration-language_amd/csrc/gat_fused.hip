@@ -39,18 +39,13 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
     const int H = gl_.H, hh = gl_.hh;
     const int lane = threadIdx.x & (kWave - 1);
     const int hl = lane & (HW - 1);
-    const int gbase = lane & ~(HW - 1);
     const int kl = hl % UH;
     const bool owner = hl < UH;
     const int32_t n = (int32_t)(e1 - e0);
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         int64_t c[U];
         V x[U][CH], yv[U][CH];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int32_t j = (j0 + k < n) ? j0 + k : n - 1;
-            c[k] = p.col[e0 + j];
-        }
+        load_batch_cols<G, U>(p, e0, n, j0, c);
         float ar[NK];
         if (!RC) {
 #pragma unroll
@@ -87,8 +82,8 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
             const float z = pos[i] ? t : __fmul_rn(t, d.slope);
             a[i] = __fmul_rn(ref_exp(z), gl_.qr);
         }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
+        static_for<0, U>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
             float dd = 0.0f;
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) {
@@ -97,8 +92,8 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
                 for (int i = 0; i < VEC; ++i) dd = fmaf(dy[ch][i], xv[i], dd);
             }
             dd = group_sum<HW>(dd);
-            const float ak = __shfl(a[k / UH], gbase + (k % UH), 64);
-            if (j0 + k >= n) continue;
+            const float ak = group_bcast<HW, k % UH>(a[k / UH]);
+            if (j0 + k >= n) return;
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) {
                 const float *yk = reinterpret_cast<const float *>(&yv[k][ch]);
@@ -112,7 +107,7 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
                 st.s_msds += pos[i] ? sds : __fmul_rn(sds, d.slope);
                 st.s_ma += pos[i] ? a[i] : __fmul_rn(a[i], d.slope);
             }
-        }
+        });
     }
 }
 

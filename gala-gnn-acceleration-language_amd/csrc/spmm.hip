@@ -141,12 +141,23 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
         V x[U][CH];
         float w[U][CH];
         float sc[U];
+        // one row per wave (G = 64): a batch's columns are wave-uniform, so one coalesced
+        // load of U columns is spread to scalar registers (v_readlane) and the X row
+        // addresses are formed on the scalar unit instead of per lane
+        int32_t cu = 0;
+        if constexpr (G == 64 && !SAMP) {
+            const int kk = threadIdx.x & (U - 1);
+            cu = p.col[e0 + ((j0 + kk < n) ? j0 + kk : n - 1)];
+        }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             const int32_t jj = (j0 + k < n) ? j0 + k : n - 1;  // clamped: valid address
             const int32_t j = SAMP ? (p.ra * jj + p.rb) % deg : jj;
             const int64_t e = e0 + j;
-            c[k] = p.col[e];
+            if constexpr (G == 64 && !SAMP)
+                c[k] = __builtin_amdgcn_readlane(cu, k);
+            else
+                c[k] = p.col[e];
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + cl.head[ch]] : 1.0f;
         }

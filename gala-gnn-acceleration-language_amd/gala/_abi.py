@@ -29,6 +29,7 @@ GALA_SDDVV_MUL = 1
 GALA_SDDVV_ADD_LRELU = 2
 GALA_SOFTMAX_REF = 0
 GALA_SOFTMAX_FIXED = 1
+GALA_GAT_PARTIAL = 0x10
 
 
 class gala_split_plan_t(ctypes.Structure):

@@ -41,6 +41,10 @@ class HipBackend:
     def degree(self, g, power=-0.5):
         return self.ops.degree(g, power=power)
 
+    def gat_partial(self, g, aL, aR, X, heads, slope, Y, sums):
+        """REF GAT forward over one column range, unnormalised (GALA_GAT_PARTIAL)."""
+        return self.ops.gat_fwd_partial(g, aL, X, aR=aR, heads=heads, slope=slope, Y=Y, sums=sums)
+
     def empty(self, *shape):
         return torch.empty(shape, device=self.device, dtype=torch.float32)
 
@@ -104,6 +108,12 @@ class CpuBackend:
         out = torch.empty(g.n_rows, dtype=torch.float32)
         _abi.call_cpu("gala_degree_f32", g.csr(), _hp(out), power, 0, 0, None)
         return out
+
+    def gat_partial(self, g: CpuGraph, aL, aR, X, heads, slope, Y, sums):
+        _abi.call_cpu("gala_gat_fwd_ex_f32", g.csr(), _hp(aL), _hp(aR), None, None, _hp(X), X.stride(0), X.shape[1],
+                      heads, slope, _abi.GALA_SOFTMAX_REF | _abi.GALA_GAT_PARTIAL, _hp(Y), Y.stride(0), None,
+                      _hp(sums), None)
+        return Y, sums
 
     def empty(self, *shape):
         return torch.empty(shape, dtype=torch.float32)

@@ -314,6 +314,20 @@ def gat_bwd_ex(g: DeviceGraph, aL, X, dY, alpha, q=None, aR=None, wR=None, bR=No
     return d_aL, dz
 
 
+def gat_fwd_partial(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, Y=None, sums=None):
+    """REF forward over one column range (GALA_GAT_PARTIAL): returns (Y, sums) with Y[r] =
+    sum_e p_e X[col_e] unnormalised and sums[r, h] = sum_e p_e, for the vertex cut."""
+    F = X.shape[1]
+    if Y is None:
+        Y = _rows_like(X, g.n_rows)
+    if sums is None:
+        sums = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    _abi.call("gala_gat_fwd_ex_f32", g.csr(F + 2 * heads), _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X),
+              X.stride(0), F, heads, slope, _abi.GALA_SOFTMAX_REF | _abi.GALA_GAT_PARTIAL, _dp(Y), Y.stride(0),
+              None, _dp(sums), _stream())
+    return Y, sums
+
+
 def gat_bwd_fused(g: DeviceGraph, aL, X, dY, q, aR=None, wR=None, bR=None, heads=1, slope=0.2):
     """gala_gat_bwd_fused_f32 (REF): attention recomputed from (aL, aR | wR, bR, q); returns
     (dX, d_aL) with dX = A_alpha dY on the forward pattern."""

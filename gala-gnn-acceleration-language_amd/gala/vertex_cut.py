@@ -148,3 +148,57 @@ class VertexCutAggregator:
 
     def halo_bytes(self) -> int:
         return self.part.comm_bytes(self.F) if self.part.world > 1 else 0
+
+
+class VertexCutGat:
+    """The REF-mode GAT layer forward (edge softmax + attention-weighted aggregation) with
+    column ownership.  The softmax of a row spans every column range, so each rank computes
+    for its edges the UNNORMALISED partial rows and softmax sums (GALA_GAT_PARTIAL):
+        U_p[r] = sum_{e in row r, col in V_p} p_e X[col],   S_p[r, h] = sum p_e,
+        p_e = min(exp(LeakyReLU(aL[r] + aR[col])), 1e12)           (common.h:760-773)
+    and two reduce-scatters (the partial rows, and the [rows, H] softmax row statistics)
+    hand each owner  Y[r] = (sum_p U_p[r]) / (1e-12 + sum_p S_p[r])  -- REF has no max
+    subtraction, so partial sums simply add.  aL of every row arrives by an all-gather of
+    the owners' [n, H] blocks per chunk (small); aR and X of the own columns are local.
+    Forward only (the backward would reduce-scatter d_aL and all-gather dY rows)."""
+
+    def __init__(self, part: VertexCutPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
+        self.part, self.F, self.H, self.be, self.comm, self.slope = part, F, heads, backend, comm, slope
+        thr = part.split_threshold
+        self.graphs = [backend.graph(h, split=thr) for h in part.chunk_graphs]
+        P, c, K = part.world, part.block, part.chunks
+        self._rows = P * c
+        self.U = backend.empty(K * P * c, F)
+        self.S = backend.empty(K * P * c * heads)
+        self.Uown = backend.empty(K * c, F)
+        self.Sown = backend.empty(K * c * heads)
+        self.aLpad = backend.empty(K * c, heads)
+        self.aLall = backend.empty(K * P * c, heads)
+
+    def __call__(self, aL, aR, X):
+        """aL [n, H] (own rows), aR [n, H] and X [n, F] (own columns) -> Y [n, F] (own rows)."""
+        p, H, c, rows = self.part, self.H, self.part.block, self._rows
+        n = p.n
+        self.aLpad[:n].copy_(aL.reshape(n, H))
+        self.aLpad[n:].zero_()
+        works = []
+        for k, gk in enumerate(self.graphs):
+            al_k = self.aLall[k * rows:(k + 1) * rows]
+            if p.world > 1:
+                self.comm.wait([self.comm.all_gather(al_k, self.aLpad[k * c:(k + 1) * c])])
+            else:
+                al_k.copy_(self.aLpad[k * c:(k + 1) * c])
+            Uk = self.U[k * rows:(k + 1) * rows]
+            Sk = self.S[k * rows * H:(k + 1) * rows * H]
+            self.be.gat_partial(gk, al_k, aR, X, H, self.slope, Uk, Sk)
+            if p.world > 1:
+                works.append(self.comm.reduce_scatter(self.Uown[k * c:(k + 1) * c], Uk))
+                works.append(self.comm.reduce_scatter(self.Sown[k * c * H:(k + 1) * c * H], Sk))
+            else:
+                self.Uown[k * c:(k + 1) * c].copy_(Uk)
+                self.Sown[k * c * H:(k + 1) * c * H].copy_(Sk)
+        if works:
+            self.comm.wait(works)
+        q = 1.0 / (self.Sown[:n * H].view(n, H) + 1e-12)
+        D = self.F // H
+        return (self.Uown[:n].view(n, H, D) * q.view(n, H, 1)).reshape(n, self.F)

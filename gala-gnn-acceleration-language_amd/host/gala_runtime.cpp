@@ -201,6 +201,16 @@ Dataset from_files(const std::string &name, const std::string &dir, int64_t feat
     const int64_t nrows = src[0].item<int64_t>(), ncols = src[1].item<int64_t>();
     TORCH_CHECK(nrows == ncols, "gala: non-square adjacency in ", dir);
     const int64_t m = dst.numel();
+    // ids are range-checked before the int32 narrowing (a wrapped id could otherwise land on
+    // a valid-looking vertex and silently build another graph)
+    TORCH_CHECK(nrows >= 0 && nrows < INT32_MAX, "gala: ", dir, "Adj_src.npy: ", nrows,
+                " vertices exceed the int32 index contract");
+    if (m > 0) {
+        auto s = src.slice(0, 2);
+        TORCH_CHECK(s.min().item<int64_t>() >= 0 && s.max().item<int64_t>() < nrows &&
+                        dst.min().item<int64_t>() >= 0 && dst.max().item<int64_t>() < ncols,
+                    "gala: ", dir, "Adj_src.npy / Adj_dst.npy hold vertex ids outside [0, ", nrows, ")");
+    }
     auto s32 = src.slice(0, 2).to(torch::kInt).contiguous();
     auto d32 = dst.to(torch::kInt).contiguous();
     ds.n = nrows;

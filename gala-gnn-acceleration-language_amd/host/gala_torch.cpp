@@ -1065,7 +1065,13 @@ struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
 torch::Tensor linear_fwd(const torch::Tensor &X, const torch::Tensor &W, const torch::Tensor &b) {
     const bool has_b = b.defined() && b.numel() > 0;
     const int64_t K = W.size(1), M = W.size(0);
-    if (X.is_cuda() && X.dim() == 2 && X.scalar_type() == torch::kFloat && X.stride(1) == 1 &&
+    // the matrix-core kernel takes K and M from W and reads X rows / the bias on faith:
+    // every operand shape and device is checked here (mismatches go to at::addmm, which
+    // raises its usual shape error)
+    const bool shapes_ok = X.dim() == 2 && W.dim() == 2 && X.size(1) == K && W.device() == X.device() &&
+                           W.scalar_type() == torch::kFloat &&
+                           (!has_b || (b.numel() == M && b.device() == X.device() && b.scalar_type() == torch::kFloat));
+    if (shapes_ok && X.is_cuda() && X.scalar_type() == torch::kFloat && X.stride(1) == 1 &&
         M > 32 && M <= 64 && K <= 64) {
         auto w = W.contiguous();
         torch::Tensor bb = has_b ? b.contiguous() : torch::Tensor();
@@ -1164,6 +1170,21 @@ torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, tor
                                       torch::Tensor attn_r_bias, int64_t li, double slope,
                                       int64_t mode) {
     return GatAggregateFfn::apply(attn_l, X, attn_r_weight, attn_r_bias, li, slope, mode);
+}
+
+HeadAttnImpl::HeadAttnImpl(int64_t in, int64_t heads) {
+    TORCH_CHECK(heads >= 1 && in % heads == 0, "gala: HeadAttn(", in, ", ", heads, "): in is not a whole number of heads");
+    const double bound = 1.0 / std::sqrt((double)(in / heads));  // torch Linear(D, 1) init range
+    weight = register_parameter("weight", torch::empty({1, in}).uniform_(-bound, bound));
+    bias = register_parameter("bias", torch::empty({heads}).uniform_(-bound, bound));
+}
+
+torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias) {
+    const int64_t H = bias.numel(), F = weight.numel();
+    TORCH_CHECK(X.size(-1) == F && F % H == 0, "gala: head_attn_apply: X has ", X.size(-1),
+                " columns, the attention vectors ", F);
+    auto x = X.reshape({X.size(0), H, F / H});
+    return (x * weight.reshape({1, H, F / H})).sum(2) + bias.reshape({1, H});
 }
 
 }  // namespace gala

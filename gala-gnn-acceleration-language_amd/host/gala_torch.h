@@ -137,10 +137,22 @@ torch::Tensor ffn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bia
 // using the slot's transposed graph).
 torch::Tensor gat_aggregate_apply(torch::Tensor attn_l, torch::Tensor attn_r, torch::Tensor X,
                                   int64_t li, double slope, int64_t mode);
-// the same layer with attn_r = X attn_r_weight^T + attn_r_bias recomputed inside the kernels
-// (the DSL's attnR = dsl.nn.ffn(res, out=1) of the aggregated res; one head)
+// the same layer with attn_r recomputed inside the kernels from the rows they gather (the
+// DSL's attnR = dsl.nn.ffn(res, out=1) of the aggregated res).  One head: attn_r = X
+// attn_r_weight^T + attn_r_bias; H heads (attn_l [N, H], galac gat_heads(H)): per head h,
+// attn_r[:, h] = X[:, head h] . attn_r_weight[head h] + attn_r_bias[h].
 torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, torch::Tensor attn_r_weight,
                                       torch::Tensor attn_r_bias, int64_t li, double slope,
                                       int64_t mode);
+
+// Multi-head attention vectors (galac gat_heads(H)): weight [1, F] holds one vector of D =
+// F/H entries per head, bias [H].  Initialised like H Linear(D, 1) layers.
+struct HeadAttnImpl : torch::nn::Module {
+    torch::Tensor weight, bias;
+    HeadAttnImpl(int64_t in, int64_t heads);
+};
+TORCH_MODULE(HeadAttn);
+// [N, H]: out[:, h] = X[:, hD:(h+1)D] . weight[hD:(h+1)D] + bias[h] (torch ops, autograd)
+torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias);
 
 }  // namespace gala

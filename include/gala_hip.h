@@ -299,6 +299,11 @@ int gala_gat_bwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,
  * for the recompute (else GALA_ERR_UNSUPPORTED).  Replaces the same chains as
  * gala_gat_fwd_f32 / gala_gat_bwd_f32.
  */
+/* mode flag of gala_gat_fwd_ex_f32 (REF only, q_out required, alpha_out NULL): a PARTIAL
+ * forward over one column range of the graph -- Y[r] = sum_e p_e X[col_e] unnormalised and
+ * q_out[r,h] = sum_e p_e (no 1e-12) -- whose partial rows and sums the caller adds over the
+ * column ranges (the vertex-cut GAT, gala/vertex_cut.py) before Y = Y_sum / (sum + 1e-12). */
+#define GALA_GAT_PARTIAL 0x10
 int gala_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                         float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,

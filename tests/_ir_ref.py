@@ -51,11 +51,13 @@ def _csr(rowptr, col, n_cols, val=None):
 
 
 def _spmm(rowptr, col, x, w=None):
-    """sum_e w_e x[col_e] per row, differentiable in x and w (duplicate edges kept)."""
+    """sum_e w_e x[col_e] per row, differentiable in x and w (duplicate edges kept).
+    w [E] or [E, H]: head h weights columns hD:(h+1)D."""
     rows = _rows(rowptr)
     g = x[torch.as_tensor(np.asarray(col, np.int64))]
     if w is not None:
-        g = g * w.view(-1, 1)
+        H = w.numel() // max(g.shape[0], 1) if g.shape[0] else 1
+        g = (g.view(g.shape[0], H, -1) * w.reshape(-1, H, 1)).reshape(g.shape)
     return torch.zeros(len(rowptr) - 1, x.shape[1], dtype=x.dtype).index_add(0, rows, g)
 
 
@@ -203,26 +205,33 @@ def run(ir, graphs: Graphs, X, params, segments=1):
                 y = a[2] * y
         elif op == "GAT_AGGREGATE":
             rp, col = graphs.edges(gi)
+            H = a[0].numel() // graphs.n                  # heads (galac gat_heads)
             if nd["weight"]:  # gat_aggregate_ffn: attnR = Linear(X) of the aggregated rows
-                w = nd["weight"]
-                a[1] = a[2] @ params[w + ".weight"].T + params[w + ".bias"]
-            if ir["sched"]["gat_mode"] == 0:
-                y = _GatRef.apply(a[0], a[1], a[2], rp, col, graphs.n, nd["param"])
-            else:
-                alpha = _softmax(rp, _lrelu(a[0].view(-1)[_rows(rp)] +
-                                            a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)],
-                                            nd["param"]))
-                y = _spmm(rp, col, a[2], alpha)
+                a[1] = _ffn(a[2], params, nd["weight"], H)
+            D = a[2].shape[1] // H
+            aL, aR = a[0].reshape(graphs.n, H), a[1].reshape(-1, H)
+            heads = []
+            for h in range(H):                           # heads are independent
+                xh = a[2][:, h * D:(h + 1) * D]
+                if ir["sched"]["gat_mode"] == 0:
+                    heads.append(_GatRef.apply(aL[:, h].reshape(-1, 1), aR[:, h].reshape(-1, 1), xh, rp, col,
+                                               graphs.n, nd["param"]))
+                else:
+                    alpha = _softmax(rp, _lrelu(aL[:, h][_rows(rp)] + aR[:, h][torch.as_tensor(col, dtype=torch.long)],
+                                                nd["param"]))
+                    heads.append(_spmm(rp, col, xh, alpha))
+            y = heads[0] if H == 1 else torch.cat(heads, 1)
         elif op == "FFN":
-            w = nd["weight"]
-            y = a[0] @ params[w + ".weight"].T + params[w + ".bias"]
+            y = _ffn(a[0], params, nd["weight"], _heads(ir, nd["weight"]))
         elif op == "RELU":
             y = torch.relu(a[0])
         elif op == "LEAKY_RELU":
             y = _lrelu(a[0], nd["param"])
         elif op == "AGGREGATE_EDGE_SUM":
             rp, col = graphs.edges(gi)
-            y = a[0].view(-1)[_rows(rp)] + a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)]
+            H = a[0].numel() // graphs.n
+            y = (a[0].reshape(-1, H)[_rows(rp)] + a[1].reshape(-1, H)[torch.as_tensor(col, dtype=torch.long)])
+            y = y.reshape(-1) if H == 1 else y
         elif op == "AGGREGATE_EDGE_MUL":
             rp, col = graphs.edges(gi)
             y = a[0].view(-1)[_rows(rp)] * a[1].view(-1)[torch.as_tensor(col, dtype=torch.long)]
@@ -243,10 +252,29 @@ def _lrelu(x, slope):
     return torch.where(x > 0, x, x * slope)
 
 
+def _heads(ir, wname):
+    for w in ir["weights"]:
+        if w["name"] == wname:
+            return int(w.get("heads", 1))
+    return 1
+
+
+def _ffn(x, params, wname, heads):
+    """FFN: x W^T + b; with heads > 1 (gat_heads attention vectors) the per-head dot
+    out[:, h] = x[:, head h] . W[0, head h] + b[h]."""
+    W, b = params[wname + ".weight"], params[wname + ".bias"]
+    if heads == 1 or W.shape[0] != 1 or b.numel() != heads:
+        return x @ W.T + b
+    D = x.shape[1] // heads
+    return (x.reshape(x.shape[0], heads, D) * W.reshape(1, heads, D)).sum(2) + b.reshape(1, heads)
+
+
 def _softmax(rowptr, s):
+    """Per-row edge softmax of s [E] or [E, H] (each head on its own)."""
     p = torch.clamp(torch.exp(s), max=1e12)
     rows = _rows(rowptr)
-    r = torch.zeros(len(rowptr) - 1, dtype=s.dtype).index_add(0, rows, p) + 1e-12
+    shape = (len(rowptr) - 1,) + tuple(s.shape[1:])
+    r = torch.zeros(shape, dtype=s.dtype).index_add(0, rows, p) + 1e-12
     return p * (1.0 / r)[rows]
 
 
@@ -257,7 +285,7 @@ def init_params(ir, seed=0, zero_bias=False):
     for w in ir["weights"]:
         if w["type"] == "linear":
             p[w["name"] + ".weight"] = (torch.rand(w["out"], w["in"], generator=g, dtype=torch.float64) - 0.5) / np.sqrt(w["in"])
-            b = (torch.rand(w["out"], generator=g, dtype=torch.float64) - 0.5) / np.sqrt(w["in"])
+            b = (torch.rand(w["out"] * int(w.get("heads", 1)), generator=g, dtype=torch.float64) - 0.5) / np.sqrt(w["in"])
             p[w["name"] + ".bias"] = torch.zeros_like(b) if zero_bias else b
         else:
             p[w["name"]] = torch.tensor([float(w["init"])], dtype=torch.float64)

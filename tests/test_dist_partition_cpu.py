@@ -225,3 +225,65 @@ def test_distributed_aggregation_matches_one_process(world, name):
                 np.testing.assert_array_equal(got[layer], ref[layer], err_msg=str(key))  # bit-identical
             else:
                 np.testing.assert_allclose(got[layer], ref[layer], rtol=1e-5, atol=1e-6, err_msg=str(key))
+
+
+# ---- vertex-cut GAT forward: softmax row statistics reduce-scattered -----------------------
+H_GAT, F_GAT = 2, 8
+
+
+def _gat_inputs(g):
+    rng = np.random.default_rng(21)
+    aL = rng.uniform(-1, 1, (g.n_rows, H_GAT)).astype(np.float32)
+    aR = rng.uniform(-1, 1, (g.n_rows, H_GAT)).astype(np.float32)
+    X = rng.uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
+    return aL, aR, X
+
+
+def _gat_one_process(g):
+    from gala import _abi
+    aL, aR, X = _gat_inputs(g)
+    be = CpuBackend()
+    Y = torch.empty((g.n_rows, F_GAT))
+    _abi.call_cpu("gala_gat_fwd_f32", be.graph(g).csr(), aL.ctypes.data, aR.ctypes.data, X.ctypes.data, F_GAT,
+                  F_GAT, H_GAT, 0.2, _abi.GALA_SOFTMAX_REF, Y.data_ptr(), F_GAT, None, None)
+    return Y.numpy()
+
+
+def _gat_worker(rank, world, port, name, chunks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = GRAPHS[name]()
+        aL, aR, X = _gat_inputs(g)
+        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        gat = vc.VertexCutGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
+        Y = gat(torch.from_numpy(aL[own].copy()), torch.from_numpy(aR[own].copy()), torch.from_numpy(X[own].copy()))
+        sizes = [int(pt.bounds[r + 1] - pt.bounds[r]) for r in range(world)]
+        pad = torch.full((max(sizes), F_GAT), float("nan"))
+        pad[:pt.n] = Y
+        ys = [torch.empty_like(pad) for _ in sizes]
+        dist.all_gather(ys, pad)
+        if rank == 0:
+            q.put(torch.cat([y[:s] for y, s in zip(ys, sizes)]).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,chunks", [(2, "powerlaw", 1), (3, "cora", 2), (3, "empty_rows", 1)])
+def test_vertex_cut_gat_matches_one_process(world, name, chunks):
+    """REF GAT forward with column ownership (VertexCutGat): per-rank unnormalised partial
+    rows and softmax sums (GALA_GAT_PARTIAL on the host-CPU backend), reduce-scattered to
+    the row owners, equal the one-process fused forward within fp32 rounding."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, name, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _gat_one_process(GRAPHS[name]())
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)

@@ -81,6 +81,40 @@ def test_gat_lowering_fuses_attention(tmp_path):
     assert names == ["fc0", "efc0", "efc1", "fc1", "efc2", "efc3"]
 
 
+def test_gat_heads_extension(tmp_path):
+    """galac's gat_heads(H): the attention layers but the last run H heads of `hs`
+    features (fc0: 64 -> 4 x 8), one per-head attention vector per FFN(out=1) (weight
+    [1, 32] read per 8-column head slice, H biases), edge values of H columns; the output
+    layer keeps one head.  The fused ops carry the heads through the attention widths."""
+    ir = galac(os.path.join(HERE, "dsl", "gat_heads.txt"), tmp_path)
+    post = ir["post"]
+    assert post["sched"]["gat_heads"] == 4
+    w = {x["name"]: x for x in post["weights"]}
+    assert (w["fc0"]["in"], w["fc0"]["out"], w["fc0"]["heads"]) == (64, 32, 1)
+    assert (w["efc0"]["in"], w["efc0"]["out"], w["efc0"]["heads"]) == (32, 1, 4)
+    assert (w["efc1"]["heads"], w["fc1"]["in"], w["fc1"]["out"], w["efc2"]["heads"]) == (4, 32, 7, 1)
+    gat = [n for n in post["nodes"] if n["op"] == "GAT_AGGREGATE"]
+    assert len(gat) == 2
+    widths = [post["values"][n["in"][0]]["width"] for n in gat]
+    assert widths == [4, 1]                      # attnL of layer 1: [N, 4]; layer 2: [N, 1]
+    pre = ir["pre"]
+    edge = [pre["values"][n["out"]]["width"] for n in pre["nodes"] if n["op"] == "SOFTMAX"]
+    assert edge == [4, 1]
+
+
+def test_gat_heads_rejects_partial_heads(tmp_path):
+    src = open(os.path.join(HERE, "dsl", "gat_heads.txt")).read().replace("gat_heads(4);", "gat_heads(3);")
+    src = src.replace("l1 = L1(G, 8,", "l1 = L1(G, 8,")       # 3 x 8 = 24 columns: fine
+    prog = tmp_path / "h3.txt"
+    prog.write_text(src)
+    ir = galac(str(prog), tmp_path)
+    assert {x["name"]: x["out"] for x in ir["post"]["weights"]}["fc0"] == 24
+    bad = tmp_path / "h0.txt"
+    bad.write_text(src.replace("gat_heads(3);", "gat_heads(0);"))
+    r = subprocess.run([GALAC, str(bad), "--quiet", "--ir-json", str(tmp_path / "o.json")], capture_output=True, text=True)
+    assert r.returncode != 0 and "gat_heads" in r.stderr
+
+
 def test_gin_and_sage(tmp_path):
     gin = galac(os.path.join(HERE, "dsl", "gin.txt"), tmp_path)
     assert "SCALAR_ADD_EPS_MULTIPLY" in ops(gin["pre"])

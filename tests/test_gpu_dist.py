@@ -177,3 +177,55 @@ def test_aggregator_classes_on_one_rank():
     Y3 = torch.empty_like(X)
     vagg(X, Y3)
     torch.testing.assert_close(Y3, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("world,chunks", [(1, 2), (2, 1), (3, 4)])
+@pytest.mark.parametrize("heads,F", [(1, 32), (8, 256)])
+def test_vertex_cut_gat_matches_one_gpu(world, chunks, heads, F):
+    """REF GAT forward with column ownership, ranks simulated in-process: every rank's
+    GALA_GAT_PARTIAL launches over its own columns (aL of all rows = the all-gather);
+    adding the ranks' partial rows and softmax sums (the reduce-scatters) and normalising
+    equals the one-GPU fused forward and the oracle within the tolerance."""
+    from gala import layout, vertex_cut as vc
+    import oracle as orc_
+    g = layout.gen_graph("uniform", 3000, 20000, seed=9)
+    rng = np.random.default_rng(5)
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    aR = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    X = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    dg = ops.DeviceGraph.from_host(g)
+    Y1 = ops.gat_fwd(dg, torch.from_numpy(aL).cuda(), torch.from_numpy(aR).cuda(), torch.from_numpy(X).cuda(),
+                     heads=heads)
+    parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks) for p in range(world)]
+    c, rows = parts[0].block, world * parts[0].block
+    U = torch.zeros((chunks * rows, F), device="cuda")
+    S = torch.zeros((chunks * rows, heads), device="cuda")
+    # aL of every row in the partial graphs' (chunk, owner, row) layout
+    aL_rows = torch.zeros((chunks * rows, heads), device="cuda")
+    for pt in parts:
+        for j0, j1 in [(k * c, min((k + 1) * c, pt.n)) for k in range(chunks)]:
+            if j1 > j0:
+                k = j0 // c
+                aL_rows[k * rows + pt.rank * c:k * rows + pt.rank * c + (j1 - j0)] = \
+                    torch.from_numpy(aL[pt.r0 + j0:pt.r0 + j1]).cuda()
+    for pt in parts:
+        own = slice(pt.r0, pt.r0 + pt.n)
+        aRp, Xp = torch.from_numpy(aR[own].copy()).cuda(), torch.from_numpy(X[own].copy()).cuda()
+        for k, h in enumerate(pt.chunk_graphs):
+            gk = ops.DeviceGraph.from_host(h, split=pt.split_threshold)
+            Uk, Sk = ops.gat_fwd_partial(gk, aL_rows[k * rows:(k + 1) * rows].contiguous(), Xp, aR=aRp, heads=heads)
+            U[k * rows:(k + 1) * rows] += Uk
+            S[k * rows:(k + 1) * rows] += Sk.view(-1, heads)
+    D = F // heads
+    for pt in parts:
+        Uo = torch.cat([U[k * rows + pt.rank * c:k * rows + (pt.rank + 1) * c] for k in range(chunks)])[:pt.n]
+        So = torch.cat([S[k * rows + pt.rank * c:k * rows + (pt.rank + 1) * c] for k in range(chunks)])[:pt.n]
+        Y = (Uo.view(pt.n, heads, D) / (So + 1e-12).view(pt.n, heads, 1)).reshape(pt.n, F)
+        torch.testing.assert_close(Y, Y1[pt.r0:pt.r0 + pt.n], rtol=1e-5, atol=1e-6)
+    if world == 1:   # the class itself, on the HIP backend
+        from gala.backend import HipBackend
+        gat = vc.VertexCutGat(parts[0], F, heads, HipBackend("cuda"), None)
+        Yc = gat(torch.from_numpy(aL).cuda(), torch.from_numpy(aR).cuda(), torch.from_numpy(X).cuda())
+        torch.testing.assert_close(Yc, Y1, rtol=1e-5, atol=1e-6)
+    Yr, _ = orc_.gat_fwd(orc_.Graph(g.n_rows, g.n_cols, g.rowptr, g.col), aL, aR, X, heads=heads)
+    np.testing.assert_allclose(Y1.cpu().numpy(), Yr, atol=1e-4, rtol=1e-4)

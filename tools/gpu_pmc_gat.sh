@@ -1,6 +1,15 @@
 #!/bin/bash
-# PMC passes (one counter group per run) over tools/gat_h8_probe.py: wave-state breakdown
-# of the 8-head GAT forward vs the weighted SpMM of the same shape.
+# kernel trace + PMC passes (one counter group per run) over tools/gat_h8_probe.py: time,
+# instruction mix and wave states of the 8-head GAT forward vs the weighted SpMM of the
+# same shape, and the fused backward.
 R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/pmc_gat
+mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $R/gpurun_out/pmc_gat -o run -- python3 $R/tools/gat_h8_probe.py > $R/gpurun_out/pmc_gat.log 2>&1
+timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/tools/gat_h8_probe.py > $O/trace.log 2>&1 &&
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/waves -o run -- python3 $R/tools/gat_h8_probe.py > $O/waves.log 2>&1 &&
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o run -- python3 $R/tools/gat_h8_probe.py > $O/fetch.log 2>&1 &&
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o run -- python3 $R/tools/gat_h8_probe.py > $O/write.log 2>&1
+rc=$?
+echo pmc_rc=$rc
+exit $rc
