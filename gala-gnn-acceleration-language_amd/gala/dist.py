@@ -440,10 +440,8 @@ class DistAggregator:
         self.graph = backend.graph(part.graph, split=thr)
         self.groups = None if exact else [backend.graph(h, split=thr) for h in part.groups]
         self.norm = backend.degree(self.graph)          # own rows' full degrees
-        self.Xs = backend.empty(part.n_cols, F)
-        if part.halo_mode == "dense" and part.world > 1:
-            # padding rows are never read, but keep the table finite for debugging
-            self.Xs.zero_()
+        self._xs = {}
+        self.Xs = self._table(F)
         if part.world == 1:
             self.exchange = None
         elif part.halo_mode == "p2p":
@@ -452,22 +450,41 @@ class DistAggregator:
             self.exchange = DenseHalo(part, comm)
         self._blocks = part.own_blocks()
 
+    def _table(self, F):
+        """The feature buffer Xs of width F (one per width: a program's layers differ)."""
+        if F not in self._xs:
+            t = self.be.empty(self.part.n_cols, F)
+            if self.part.halo_mode == "dense" and self.part.world > 1:
+                t.zero_()  # padding rows are never read; keep the table finite
+            self._xs[F] = t
+        return self._xs[F]
+
     def refresh_norm(self):
         self.norm = self.be.degree(self.graph)
 
     def __call__(self, H, out):
+        """out = norm * A (norm * H) (the GCN aggregation with the graph's own norm)."""
+        return self.apply(H, out, self.norm, self.norm)
+
+    def apply(self, H, out, pre=None, post=None):
+        """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None), the
+        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) on a partition."""
         be = self.be
-        for j0, j1, x0 in self._blocks:                               # own rows of Xs = norm * H
-            be.row_broadcast(self.norm[j0:j1], H[j0:j1], self.Xs[x0:x0 + (j1 - j0)])
-        chunks = self.exchange.start(self.Xs) if self.exchange else []
+        Xs = self._table(H.shape[1])
+        for j0, j1, x0 in self._blocks:                               # own rows of Xs = pre * H
+            if pre is None:
+                Xs[x0:x0 + (j1 - j0)].copy_(H[j0:j1])
+            else:
+                be.row_broadcast(pre[j0:j1], H[j0:j1], Xs[x0:x0 + (j1 - j0)])
+        chunks = self.exchange.start(Xs) if self.exchange else []
         if self.exact:
             for works in chunks:
                 self.comm.wait(works)
-            return be.spmm(self.graph, self.Xs, out, self.norm, False)
-        be.spmm(self.groups[0], self.Xs, out, self.norm, False)      # overlaps the exchange
+            return be.spmm(self.graph, Xs, out, post, False)
+        be.spmm(self.groups[0], Xs, out, post, False)                # overlaps the exchange
         for k, works in enumerate(chunks):
             self.comm.wait(works)
-            be.spmm(self.groups[1 + k], self.Xs, out, self.norm, True)
+            be.spmm(self.groups[1 + k], Xs, out, post, True)
         return out
 
     def halo_bytes(self) -> int:

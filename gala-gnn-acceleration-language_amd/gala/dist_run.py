@@ -1,0 +1,293 @@
+"""Multi-rank runtime for galac programs: one process per GPU (torch.distributed, RCCL on
+the GPU, gloo on the host), each rank training the same model on its row partition of
+the graph.  BASELINE config 5 ("ogbn-papers100M GCN 3-layer across 8 MI355X") is
+    galac bench/dsl/gcn3_papers10.txt --ir-json prog.json
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m gala.dist_run prog.json --synthetic
+
+The generated C++ programs (galac's emitter) are single-device, like the reference's
+gala.cu.  This runtime executes the same post-pass IR (galac --ir-json) instead:
+  * node values are row-partitioned: rank p holds rows [bounds[p], bounds[p+1)) of every
+    [N, F] value (gala/dist.py row_bounds: balanced by stored edges + rows);
+  * every aggregation -- GCN_AGGREGATE post * A (pre * x), AGGREGATE_MUL_SUM -- is
+    gala/dist.py's DistAggregator in exact mode: the halo rows arrive (RCCL all-gather or
+    point-to-point), then ONE SpMM over the own rows, bit-identical to the one-GPU result;
+    its backward is the same operator on the gradient (undirected graphs: slot 2g+1 is the
+    forward graph, cuda.h:1253-1257, so pre and post swap places);
+  * FFN weights are replicated (same seed on every rank); each rank's loss is its own
+    training rows' share of the global mean cross entropy, and the weight gradients are
+    summed over the ranks (one all-reduce per weight) before the identical Adam steps
+    (lr 0.01, weight decay 5e-4, codegen/gala.cu:606-607).
+Training subgraphs (graph g > 0) run on the whole graph: they only drop rows no training
+row depends on, so the training rows' values are unchanged.  The column-tiled layout
+(col_tile) is a single-device layout and is not used.  GAT layers are not supported here.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import dist as gdist
+from . import layout
+from .backend import make_backend
+from .comm import Comm
+
+# (N, undirected edges, features, classes, train fraction) of the published shapes,
+# as host/gala_datasets.h
+SHAPES = {
+    "Cora": (2708, 5278, 1433, 7, 140.0 / 2708),
+    "Pubmed": (19717, 44324, 500, 3, 60.0 / 19717),
+    "Arxiv": (169343, 583122, 128, 40, 0.537),
+    "Products": (2449029, 61859140, 100, 47, 0.080),
+    "Reddit": (232965, 57307946, 602, 41, 0.660),
+    "Papers100M": (111059956, 807842936, 128, 172, 0.011),
+}
+SUPPORTED = {"INPUT", "DEGREES", "POWER", "ROW_BROADCAST", "GCN_AGGREGATE", "AGGREGATE_MUL_SUM", "FFN", "RELU",
+             "ADD", "SCALAR_ADD_EPS_MULTIPLY"}
+
+
+def _hash_uniform(rows: np.ndarray, cols: int, seed: int) -> np.ndarray:
+    """Deterministic U[-1, 1) features of the given rows (counter hash of (seed, row, col)),
+    so every rank draws exactly its own rows, whatever the number of ranks."""
+    k = (rows.astype(np.uint64)[:, None] * np.uint64(cols) + np.arange(cols, dtype=np.uint64)[None, :])
+    h = gdist._splitmix64(k ^ (np.uint64(seed) << np.uint64(40)))
+    return ((h >> np.uint64(40)).astype(np.float64) / float(1 << 24) * 2.0 - 1.0).astype(np.float32)
+
+
+def _hash_int(rows: np.ndarray, seed: int, mod: int) -> np.ndarray:
+    h = gdist._splitmix64(rows.astype(np.uint64) ^ (np.uint64(seed) << np.uint64(44)))
+    return ((h >> np.uint64(33)) % np.uint64(mod)).astype(np.int64)
+
+
+class _Agg(torch.autograd.Function):
+    """post * A (pre * x) on the partition; backward pre * A (post * dy) (undirected)."""
+
+    @staticmethod
+    def forward(ctx, x, agg, pre, post):
+        out = torch.empty_like(x)
+        agg.apply(x.contiguous(), out, pre, post)
+        ctx.agg, ctx.pre, ctx.post = agg, pre, post
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.empty_like(dy)
+        ctx.agg.apply(dy.contiguous(), dx, ctx.post, ctx.pre)
+        return dx, None, None, None
+
+
+class Program:
+    """One rank's share of a galac program (post-pass IR)."""
+
+    def __init__(self, ir: dict, graph: layout.HostGraph, X_own: torch.Tensor, labels_own: torch.Tensor,
+                 train_own: torch.Tensor, rank: int, world: int, device, seed: int = 0, group=None):
+        ops = {nd["op"] for nd in ir["nodes"]}
+        bad = ops - SUPPORTED
+        if bad:
+            raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE programs)")
+        if not ir["sched"]["undirected"]:
+            raise NotImplementedError("gala.dist_run: directed programs (the backward needs A^T)")
+        if ir["sched"]["kernel_sample"] or ir["sched"]["data_sample"]:
+            raise NotImplementedError("gala.dist_run: sampled programs")
+        self.ir, self.device = ir, torch.device(device)
+        self.be = make_backend(self.device)
+        self.comm = Comm(group) if world > 1 else None
+        self.rank, self.world = rank, world
+        self.part = gdist.partition_graph(graph, rank, world)
+        self.agg = gdist.DistAggregator(self.part, 1, self.be, self.comm, exact=True)
+        self.deg = torch.from_numpy(np.diff(self.part.graph.rowptr).astype(np.float32)).to(self.device).view(-1, 1)
+        self.X, self.labels, self.train = X_own, labels_own, train_own
+        # replicated weights, identical on every rank (same seed, same order as the IR)
+        torch.manual_seed(seed)
+        self.params = {}
+        self.modules = torch.nn.ModuleDict()
+        for w in ir["weights"]:
+            if w["type"] == "linear":
+                self.modules[w["name"]] = torch.nn.Linear(w["in"], w["out"])
+            else:
+                self.modules[w["name"]] = torch.nn.ParameterList([torch.nn.Parameter(torch.tensor([float(w["init"])]))])
+        self.modules.to(self.device)
+        n_train = torch.tensor([float(train_own.sum().item())], dtype=torch.float64,
+                               device=self.device if (self.comm and self.comm.rccl) else "cpu")
+        if world > 1:
+            dist.all_reduce(n_train, group=group)
+        self.n_train = float(n_train.item())
+        self.invariants = None
+
+    def _param(self, name):
+        m = self.modules[name]
+        return m[0] if isinstance(m, torch.nn.ParameterList) else m
+
+    def _vec(self, v):
+        return None if v is None else v.reshape(-1).contiguous()
+
+    def forward(self):
+        vals = {}
+        hoisted = self.invariants is None
+        for nd in self.ir["nodes"]:
+            out = nd["out"]
+            if nd.get("hoisted") and not hoisted:
+                vals[out] = self.invariants[out]
+                continue
+            op, a = nd["op"], [vals[i] if i >= 0 else None for i in nd["in"]]
+            if op == "INPUT":
+                y = self.X
+            elif op == "DEGREES":
+                y = self.deg
+            elif op == "POWER":
+                y = torch.pow(a[0], nd["param"])
+            elif op == "ROW_BROADCAST":
+                y = a[0] * a[1]
+            elif op == "GCN_AGGREGATE":
+                x = a[0]
+                if nd["param"] == 1:  # ReLU prologue: relu(act * x)
+                    act = a[3] if len(a) > 3 else None
+                    x = torch.relu(x if act is None else act * x)
+                y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
+            elif op == "AGGREGATE_MUL_SUM":
+                y = _Agg.apply(a[0], self.agg, None, None)
+            elif op == "FFN":
+                y = self.modules[nd["weight"]](a[0])
+            elif op == "RELU":
+                y = torch.relu(a[0])
+            elif op == "ADD":
+                y = a[0] + a[1]
+            elif op == "SCALAR_ADD_EPS_MULTIPLY":
+                y = (1 + self._param(nd["weight"])) * a[0]
+            vals[out] = y
+        if hoisted:  # training-invariant values (code motion): computed once
+            self.invariants = {nd["out"]: vals[nd["out"]].detach() for nd in self.ir["nodes"] if nd.get("hoisted")}
+        return vals[self.ir["output"]]
+
+    def loss(self, pred):
+        """This rank's share of the global mean cross entropy over the training rows."""
+        logp = torch.log_softmax(pred[self.train], 1)
+        return -logp.gather(1, self.labels[self.train].view(-1, 1)).sum() / self.n_train
+
+    def reduce_grads(self):
+        if self.world == 1:
+            return
+        for p in self.modules.parameters():
+            if p.grad is not None:
+                self.comm.wait([self.comm.all_reduce(p.grad)])
+
+
+def load(ir_path):
+    with open(ir_path) as f:
+        d = json.load(f)
+    return d.get("post", d)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("ir", help="galac --ir-json output (its post-pass IR is run)")
+    ap.add_argument("--data", help="dataset directory in the reference's npy format")
+    ap.add_argument("--synthetic", action="store_true", help="a seeded graph of the dataset's published shape")
+    ap.add_argument("--scale", type=float, default=1.0, help="synthetic graph size multiplier")
+    ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--dump", help="rank 0 writes an npz: predictions (all rows), losses, rowptr/col")
+    args = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if args.device == "cuda":
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        backend = os.environ.get("GALA_DIST_BACKEND", "nccl" if dev.type == "cuda" else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    ir = load(args.ir)
+    s = ir["sched"]
+    if args.data:
+        g = layout.load_npy_dataset(args.data)
+        X_all = np.load(os.path.join(args.data, "Feat.npy"), mmap_mode="r")
+        lab_all = np.load(os.path.join(args.data, "Lab.npy")).reshape(-1)
+        tr_all = np.load(os.path.join(args.data, "TnMsk.npy")).reshape(-1)
+    else:
+        if s["dataset"] not in SHAPES:
+            raise SystemExit(f"gala.dist_run: no published shape for dataset {s['dataset']!r}; pass --data")
+        n0, m0, _, _, frac = SHAPES[s["dataset"]]
+        n, m = max(int(n0 * args.scale), 2), max(int(m0 * args.scale), 1)
+        g = layout.gen_graph("uniform", n, m, seed=args.seed)
+        X_all = lab_all = tr_all = None
+    F, C = int(s["feat_size"]), int(s["label_size"])
+    bounds = gdist.row_bounds(g.rowptr, world)
+    r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+    rows = np.arange(r0, r1)
+    if X_all is None:
+        X = _hash_uniform(rows, F, args.seed)
+        labels = _hash_int(rows, args.seed + 1, C)
+        train = (_hash_int(rows, args.seed + 2, 1 << 20) < int(frac * (1 << 20))) | (rows == 0)
+    else:
+        X = np.ascontiguousarray(X_all[r0:r1], np.float32)
+        labels = lab_all[r0:r1].astype(np.int64)
+        train = tr_all[r0:r1] > 0
+    prog = Program(ir, g, torch.from_numpy(X).to(dev), torch.from_numpy(labels).to(dev),
+                   torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed)
+    init_weights = {k: v.detach().cpu().numpy().tolist() for k, v in prog.modules.state_dict().items()}
+    opt = torch.optim.Adam(prog.modules.parameters(), lr=0.01, weight_decay=5e-4)
+    iters = args.iters if args.iters is not None else max(int(s.get("iterations", 0)), 1)
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    fwd_t, ep_t, losses = [], [], []
+    for epoch in range(iters):
+        sync()
+        t0 = time.perf_counter()
+        pred = prog.forward()
+        sync()
+        t1 = time.perf_counter()
+        opt.zero_grad()
+        loss = prog.loss(pred)
+        loss.backward()
+        prog.reduce_grads()
+        opt.step()
+        sync()
+        t2 = time.perf_counter()
+        lt = loss.detach().reshape(1).to(torch.float64)
+        if world > 1:
+            lt = lt.to(dev) if prog.comm.rccl else lt.cpu()
+            dist.all_reduce(lt)
+        losses.append(float(lt.item()))
+        if epoch == 0:
+            first_pred = pred.detach()
+        fwd_t.append(t1 - t0)
+        ep_t.append(t2 - t0)
+    keep = slice(min(4, iters - 1), None)  # the reference drops its first epochs (gala.cu:613-637)
+    if args.dump:
+        sizes = [int(bounds[q + 1] - bounds[q]) for q in range(world)]
+        pr = first_pred
+        if world > 1:   # equal-sized blocks for all_gather: pad every rank's rows
+            gdev = dev if prog.comm.rccl else torch.device("cpu")
+            pad = torch.full((max(sizes), pr.shape[1]), float("nan"), device=gdev)
+            pad[:pr.shape[0]] = pr.to(gdev)
+            parts = [torch.empty_like(pad) for _ in sizes]
+            dist.all_gather(parts, pad)
+            pr = torch.cat([t[:n] for t, n in zip(parts, sizes)])
+        pr = pr.cpu()
+        if rank == 0:
+            np.savez(args.dump, prediction=pr.numpy(), losses=np.array(losses), rowptr=g.rowptr, col=g.col,
+                     weights=np.array(json.dumps(init_weights)))
+    if rank == 0:
+        print(json.dumps({"ranks": world, "vertices": g.n_rows, "edges": g.nnz, "halo": prog.part.halo_mode,
+                          "fwd_mean_s": float(np.mean(fwd_t[keep])), "epoch_mean_s": float(np.mean(ep_t[keep])),
+                          "loss_first": losses[0], "loss_last": losses[-1]}), flush=True)
+        print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

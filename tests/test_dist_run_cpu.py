@@ -1,0 +1,88 @@
+"""CPU: gala.dist_run, the multi-rank runtime of galac programs (BASELINE config 5's
+GCN-3 across GPUs), on the host-CPU backend over gloo.
+
+* world 1: the first forward equals the float64 executor of the program's IR
+  (tests/_ir_ref.py) on the runner's own graph, features and weights;
+* world 2 and 3 under torch.distributed.run: the first forward's predictions (gathered)
+  are the one-rank predictions -- the aggregations are exact-mode halo SpMMs, bit-identical
+  per row -- and the loss curve over the epochs agrees within fp32 rounding (the ranks'
+  loss shares and gradients are summed in a different order).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import _ir_ref as ref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
+GALAC = os.path.join(PKG, "gala", "galac")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ir(prog, tmp_path):
+    out = tmp_path / "ir.json"
+    r = subprocess.run([GALAC, os.path.join(HERE, "dsl", prog), "--quiet", "--ir-json", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return out
+
+
+def _run(ir, tmp_path, world, tag, iters=6):
+    dump = tmp_path / f"{tag}.npz"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable]
+    if world > 1:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr",
+                "127.0.0.1", f"--master-port={_free_port()}", "-m", "gala.dist_run"]
+    else:
+        cmd += ["-m", "gala.dist_run"]
+    cmd += [str(ir), "--synthetic", "--device", "cpu", "--iters", str(iters), "--dump", str(dump)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    summary = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert summary["ranks"] == world
+    return dict(np.load(dump)), summary
+
+
+@pytest.mark.parametrize("prog", ["gcn3.txt", "gin.txt"])
+def test_dist_run_one_rank_matches_ir_semantics(prog, tmp_path):
+    ir_path = _ir(prog, tmp_path)
+    d, _ = _run(ir_path, tmp_path, 1, "w1", iters=1)
+    ir = ref.load_ir(str(ir_path))["post"]
+    graphs = ref.Graphs(ir, d["rowptr"], d["col"], np.ones(len(d["rowptr"]) - 1, np.int32))
+    from gala import dist_run
+    rows = np.arange(len(d["rowptr"]) - 1)
+    s = ir["sched"]
+    X = torch.as_tensor(dist_run._hash_uniform(rows, s["feat_size"], 3), dtype=torch.float64)
+    W = {k: torch.tensor(np.asarray(v), dtype=torch.float64) for k, v in json.loads(str(d["weights"])).items()}
+    params = {k.replace(".0", ""): v for k, v in W.items()}   # eps ParameterList -> eps<k>
+    want = ref.run(ir, graphs, X, params)
+    np.testing.assert_allclose(d["prediction"], want.detach().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_run_ranks_match_one_rank(world, tmp_path):
+    ir_path = _ir("gcn3.txt", tmp_path)
+    d1, s1 = _run(ir_path, tmp_path, 1, "w1")
+    dn, sn = _run(ir_path, tmp_path, world, f"w{world}")
+    np.testing.assert_array_equal(dn["rowptr"], d1["rowptr"])
+    np.testing.assert_allclose(dn["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dn["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+    assert sn["loss_last"] < sn["loss_first"]            # it trains
