@@ -535,13 +535,19 @@ def main():
         sync = lambda: None  # noqa: E731
     be = make_backend(dev)
     timer = Timer(dev.type == "cuda")
-    if world > 1:
+    # GALA_BENCH_DIST=1 runs the partitioned path even on one rank (its collectives then go
+    # through RCCL at world 1: the API contract checks a one-GPU box can make)
+    distributed = world > 1 or os.environ.get("GALA_BENCH_DIST") == "1"
+    if distributed:
+        import datetime
         import torch.distributed as dist
         backend = os.environ.get("GALA_DIST_BACKEND", "nccl" if dev.type == "cuda" else "gloo")
+        kw = dict(timeout=datetime.timedelta(seconds=int(os.environ.get("GALA_DIST_TIMEOUT", "300"))))
+        if "MASTER_ADDR" not in os.environ:      # one rank without a launcher
+            kw.update(init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+            kw["device_id"] = dev
+        dist.init_process_group(backend, **kw)
         out = run_multi(args, rank, world, dev, be, timer, sync)
     else:
         out = run_single(args, dev, be, timer, sync)
@@ -549,7 +555,7 @@ def main():
         out["device"] = "cpu (host-CPU backend plumbing run; not a GPU measurement)"
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         torch.distributed.destroy_process_group()
 
 

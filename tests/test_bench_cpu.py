@@ -60,3 +60,16 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--scale", "0.002"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_bench_partitioned_path_on_one_rank():
+    """GALA_BENCH_DIST=1: the strong-scaling path on one rank without a launcher (the GPU
+    suite runs it over RCCL; here gloo on the host-CPU backend)."""
+    env = _env()
+    env["GALA_BENCH_DIST"] = "1"
+    r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--scale", "0.002", "--steps", "2",
+                        "--warmup", "1", "--calib-steps", "1"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["n_gpus"] == 1 and d["comm"]["backend"] == "gloo" and d["value"] > 0

@@ -229,3 +229,25 @@ def test_vertex_cut_gat_matches_one_gpu(world, chunks, heads, F):
         torch.testing.assert_close(Yc, Y1, rtol=1e-5, atol=1e-6)
     Yr, _ = orc_.gat_fwd(orc_.Graph(g.n_rows, g.n_cols, g.rowptr, g.col), aL, aR, X, heads=heads)
     np.testing.assert_allclose(Y1.cpu().numpy(), Yr, atol=1e-4, rtol=1e-4)
+
+
+def test_bench_partitioned_path_over_rccl_one_rank():
+    """bench.py's strong-scaling path (every candidate layout, the weak-scaling field) on one
+    rank with the RCCL backend (GALA_BENCH_DIST=1): the collectives' tensor contracts
+    (device tensors, in-place all-gather blocks, reduce-scatter blocks, the max-reduce of
+    the step time) go through RCCL itself.  The box has one GPU, so this is world 1."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "GALA_DIST_BACKEND")}
+    env["GALA_BENCH_DIST"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--scale", "0.05", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=200, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-4000:]
+    (d,) = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert d["n_gpus"] == 1 and d["scaling"] == "strong" and d["comm"]["backend"] == "nccl"
+    assert set(d["comm"]["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
+    assert d["value"] > 0 and d["weak"]["value"] > 0
