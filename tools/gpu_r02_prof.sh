@@ -17,5 +17,6 @@ python3 "$R/tools/pmc_traffic.py" "$OUT/prof_fetch" "$OUT/prof_write" "$OUT/traf
 cd "$R"
 GALA_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --scale 0.25 --steps 5 --warmup 2 \
     > "$OUT/r02_bench2_gloo.json" 2> "$OUT/r02_bench2_gloo.err" || exit $?
-cat "$OUT/r02_bench.json" "$OUT/traffic.log"
+timeout -k 10 300 python -u tools/rmat_sweep.py > "$OUT/r02_rmat_sweep.jsonl" 2> "$OUT/r02_rmat_sweep.err" || exit $?
+cat "$OUT/r02_bench.json" "$OUT/traffic.log" "$OUT/r02_rmat_sweep.jsonl"
 echo prof_done
