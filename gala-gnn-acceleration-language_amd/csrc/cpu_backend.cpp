@@ -718,6 +718,111 @@ extern "C" int gala_cpu_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, 
                        nullptr, d_aL);
 }
 
+// REF forward with the row statistics (gala_hip.h, gala_gat_fwd_stats_f32): Y and q as
+// cpu_gat_fwd, plus Ym = q * sum m p X and sma = q * sum m p (m the LeakyReLU factor)
+extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *wR, const float *bR, const float *X,
+                                          int64_t ldx, int32_t F, int32_t heads, float slope, float *Y,
+                                          int64_t ldy, float *q_out, float *Ym, int64_t ldym, float *sma,
+                                          float *aR_out, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldym < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || (!aR && !wR) || !Y || !q_out || !Ym || !sma || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (aR_out && (aR || !X)) return GALA_ERR_INVALID_ARG;
+    std::vector<float> rc;
+    if (!aR) {
+        rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
+        aR = rc.data();
+        if (aR_out) std::copy(rc.begin(), rc.begin() + A->n_rows * heads, aR_out);
+    }
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+#pragma omp parallel
+    {
+        std::vector<float> acc((size_t)D), accm((size_t)D);
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t r = 0; r < A->n_rows; ++r)
+            for (int32_t h = 0; h < H; ++h) {
+                std::fill(acc.begin(), acc.end(), 0.0f);
+                std::fill(accm.begin(), accm.end(), 0.0f);
+                float sum = 0.0f, sm = 0.0f;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) {
+                        const float t = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                        const bool pos = t > 0.0f;
+                        const float pe = ref_exp(pos ? t : t * slope);
+                        const float mp = pos ? pe : pe * slope;
+                        sum = sum + pe;
+                        sm = sm + mp;
+                        const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
+                        for (int32_t f = 0; f < D; ++f) {
+                            acc[f] = fmaf(pe, xr[f], acc[f]);
+                            accm[f] = fmaf(mp, xr[f], accm[f]);
+                        }
+                    }
+                }
+                const float q = 1.0f / (sum + (float)S * 1e-12f);
+                for (int32_t f = 0; f < D; ++f) {
+                    Y[r * ldy + h * D + f] = acc[f] * q;
+                    Ym[r * ldym + h * D + f] = accm[f] * q;
+                }
+                q_out[r * H + h] = q;
+                sma[r * H + h] = sm * q;
+            }
+    }
+    return GALA_OK;
+}
+
+// REF backward from the row statistics: dX as gala_cpu_gat_bwd_fused_f32, d_aL from
+// <dY, Y> and <dY, Ym>
+extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                                          float slope, const float *q, const float *Y, int64_t ldy,
+                                          const float *Ym, int64_t ldym, const float *sma, float *dX,
+                                          int64_t lddx, float *d_aL, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (heads < 1 || F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F)
+        return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || !aR || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
+    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+    const float eps = (float)S * 1e-12f;
+#pragma omp parallel for schedule(dynamic, kRowChunk)
+    for (int64_t r = 0; r < A->n_rows; ++r) {
+        float *out = dX + r * lddx;
+        for (int32_t f = 0; f < F; ++f) out[f] = 0.0f;
+        for (int32_t s = 0; s < S; ++s) {
+            int64_t e0, e1;
+            row_range(A, s, r, e0, e1);
+            for (int64_t e = e0; e < e1; ++e) {
+                const float *yr = dY + (int64_t)A->col[e] * lddy;
+                for (int32_t h = 0; h < H; ++h) {
+                    float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                    z = z > 0.0f ? z : z * slope;
+                    const float w = ref_exp(z) * q[r * H + h];
+                    for (int32_t f = h * D; f < (h + 1) * D; ++f) out[f] = fmaf(w, yr[f], out[f]);
+                }
+            }
+        }
+        for (int32_t h = 0; h < H; ++h) {
+            float syy = 0.0f, sym = 0.0f;
+            for (int32_t f = h * D; f < (h + 1) * D; ++f) {
+                syy = fmaf(dY[r * lddy + f], Y[r * ldy + f], syy);
+                sym = fmaf(dY[r * lddy + f], Ym[r * ldym + f], sym);
+            }
+            const float acc = syy + eps;
+            d_aL[r * H + h] = (sym - acc * sma[r * H + h]) + eps;
+        }
+    }
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,
                                          int32_t heads, float *dst, void *) {
     if (n < 0 || heads < 1) return GALA_ERR_INVALID_ARG;

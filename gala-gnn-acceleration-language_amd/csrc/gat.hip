@@ -14,15 +14,17 @@ namespace gala {
 
 // Running state of the forward for one row / chunk: per lane CH x VEC accumulators and the
 // head's (max, sum) of the softmax (FIXED: online, relative to m; REF: plain sums).
+// kRefStats adds the row statistics' sums: accm = sum m*p*X and sma = sum m*p (m the
+// LeakyReLU factor of the edge), both scaled by q at the store like acc and sum.
 template <int VEC, int CH>
 struct FwdState {
-    float acc[CH][VEC];
-    float m, sum;
-    __device__ __forceinline__ FwdState() : m(-INFINITY), sum(0.0f) {
+    float acc[CH][VEC], accm[CH][VEC];
+    float m, sum, sma;
+    __device__ __forceinline__ FwdState() : m(-INFINITY), sum(0.0f), sma(0.0f) {
 #pragma unroll
         for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) acc[ch][i] = 0.0f;
+            for (int i = 0; i < VEC; ++i) acc[ch][i] = accm[ch][i] = 0.0f;
     }
 };
 
@@ -61,7 +63,7 @@ __device__ __forceinline__ void gat_fwd_range(const EdgeParams &p, const GatDev 
             if (j0 + k >= n) continue;
             float z = __fadd_rn(gl_.al, ar[k]);
             z = z > 0.0f ? z : __fmul_rn(z, d.slope);
-            if (MODE == GALA_SOFTMAX_REF) {
+            if (ref_mode(MODE)) {
                 const float pe = ref_exp(z);
                 if (leader) d.alpha_out[(e0 + j0 + k) * H + hh] = pe;
                 st.sum = __fadd_rn(st.sum, pe);
@@ -161,12 +163,14 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
             }
         }
         float pe[NK], z[NK];
+        bool pos[NK];
 #pragma unroll
         for (int i = 0; i < NK; ++i) {
             float t = __fadd_rn(gl_.al, ar[i]);
-            z[i] = t > 0.0f ? t : __fmul_rn(t, d.slope);
+            pos[i] = t > 0.0f;
+            z[i] = pos[i] ? t : __fmul_rn(t, d.slope);
         }
-        if (MODE == GALA_SOFTMAX_REF) {
+        if (ref_mode(MODE)) {
 #pragma unroll
             for (int i = 0; i < NK; ++i) pe[i] = ref_exp(z[i]);
         } else {
@@ -189,12 +193,19 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
         }
         if (store) {
 #pragma unroll
-            for (int i = 0; i < NK; ++i) pend[i] = (MODE == GALA_SOFTMAX_REF) ? pe[i] : z[i];
+            for (int i = 0; i < NK; ++i) pend[i] = (ref_mode(MODE)) ? pe[i] : z[i];
             pend_j0 = j0;
+        }
+        float mp[NK];  // kRefStats: m * p, m = 1 on the LeakyReLU's positive side, else slope
+        if constexpr (MODE == kRefStats) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) mp[i] = pos[i] ? pe[i] : __fmul_rn(pe[i], d.slope);
         }
         static_for<0, U>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const float pk = group_bcast<HW, k % UH>(pe[k / UH]);
+            float mk = 0.0f;
+            if constexpr (MODE == kRefStats) mk = group_bcast<HW, k % UH>(mp[k / UH]);
             if (j0 + k >= n) return;
             st.sum = __fadd_rn(st.sum, pk);
 #pragma unroll
@@ -202,6 +213,15 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
                 const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
 #pragma unroll
                 for (int i = 0; i < VEC; ++i) st.acc[ch][i] = fmaf(pk, xv[i], st.acc[ch][i]);
+            }
+            if constexpr (MODE == kRefStats) {
+                st.sma = __fadd_rn(st.sma, mk);
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) st.accm[ch][i] = fmaf(mk, xv[i], st.accm[ch][i]);
+                }
             }
         });
     }
@@ -229,7 +249,7 @@ template <int G, int VEC, int CH, bool RC, int MODE>
 __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
                                                int64_t row, int nseg, const FwdState<VEC, CH> &st) {
     typedef typename GVec<VEC>::T V;
-    const float den = (MODE == GALA_SOFTMAX_REF) ? st.sum + (float)nseg * 1e-12f : st.sum;
+    const float den = (ref_mode(MODE)) ? st.sum + (float)nseg * 1e-12f : st.sum;
     const float q = d.partial ? 1.0f : 1.0f / den;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
@@ -239,7 +259,7 @@ __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G,
 #pragma unroll
         for (int i = 0; i < VEC; ++i)
             ov[i] = d.partial ? st.acc[ch][i]
-                    : (MODE != GALA_SOFTMAX_REF && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
+                    : (!ref_mode(MODE) && st.sum == 0.0f) ? 0.0f : __fmul_rn(st.acc[ch][i], q);
         float *yp = d.Y + row * d.ldy + gl_.ln.off[ch];
         if (gl_.ln.nv[ch] == VEC) {
             *reinterpret_cast<V *>(yp) = out;
@@ -248,7 +268,21 @@ __device__ __forceinline__ float gat_fwd_store(const GatDev &d, const GatLane<G,
             for (int i = 0; i < VEC; ++i)
                 if (gl_.ln.in(ch, i)) yp[i] = ov[i];
         }
+        if constexpr (MODE == kRefStats) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) ov[i] = __fmul_rn(st.accm[ch][i], q);
+            float *mp = d.ym_out + row * d.ldym + gl_.ln.off[ch];
+            if (gl_.ln.nv[ch] == VEC) {
+                *reinterpret_cast<V *>(mp) = out;
+            } else {
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    if (gl_.ln.in(ch, i)) mp[i] = ov[i];
+            }
+        }
     }
+    if constexpr (MODE == kRefStats)
+        if (gl_.leader) d.sma_out[row * gl_.H + gl_.hh] = __fmul_rn(st.sma, q);
     return d.partial ? st.sum : q;
 }
 
@@ -263,7 +297,7 @@ __device__ __forceinline__ void gat_alpha_rescale(float *ar, int64_t n, int gl, 
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int64_t t = t0 + gl + (int64_t)k * G;
-            const float pe = (MODE == GALA_SOFTMAX_REF) ? v[k] : expf(v[k] - mh);
+            const float pe = (ref_mode(MODE)) ? v[k] : expf(v[k] - mh);
             if (t < n) ar[t] = __fmul_rn(pe, qh);
         }
     }
@@ -275,9 +309,22 @@ template <int G, int VEC, int U, int MODE, int CH, bool RC, int HW>
 __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int32_t split_threshold) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
+    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
+    if constexpr (RC && MODE == kRefStats && HW > 0) {
+        // the row's own source logit, formed exactly as the per-edge recompute forms it
+        // (same lanes, same fma order and butterfly), for the backward's alpha
+        if (d.ar_out) {
+            typedef typename GVec<VEC>::T V;
+            V xr[CH];
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch)
+                xr[ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + row * d.ldx + gl_.ln.off[ch]));
+            const float a = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, xr), gl_.wb);
+            if (gl_.leader) d.ar_out[row * gl_.H + gl_.hh] = a;
+        }
+    }
     if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
         return;  // hub row: k_gat_fwd_chunk / _fixup / k_gat_alpha_chunk
-    const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     const int H = gl_.H, D = gl_.D;
     // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
     // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
@@ -320,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
             for (int64_t e = e0 + gl; e < e1; e += G) {
                 float z = __fadd_rn(alh, d.aR[(int64_t)p.col[e] * H + hd]);
                 z = z > 0.0f ? z : __fmul_rn(z, d.slope);
-                const float pe = (MODE == GALA_SOFTMAX_REF) ? ref_exp(z) : expf(z - mh);
+                const float pe = (ref_mode(MODE)) ? ref_exp(z) : expf(z - mh);
                 d.alpha_out[e * H + hd] = d.q_out ? pe : __fmul_rn(pe, qh);
             }
         }
@@ -345,6 +392,15 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_chunk(EdgeParams p, GatDev d
         w[d.F + gl_.hh] = st.m;
         w[d.F + gl_.H + gl_.hh] = st.sum;
     }
+    if constexpr (MODE == kRefStats) {  // ws[c] continues {accm[F], sma[H]}
+        float *wm = w + d.F + 2 * gl_.H;
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i)
+                if (gl_.ln.in(ch, i)) wm[gl_.ln.off[ch] + i] = st.accm[ch][i];
+        if (gl_.leader) wm[d.F + gl_.hh] = st.sma;
+    }
 }
 
 // hub rows, forward: combine the chunk partials in chunk order, store Y; (m, q) of every
@@ -364,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
         const float *w = sp.ws + cc * sp.ws_cols;
         const float mc = w[F + hh], sc = w[F + H + hh];
         float a = 1.0f, b = 1.0f;
-        if (MODE != GALA_SOFTMAX_REF) {
+        if (!ref_mode(MODE)) {
             if (mc == -INFINITY) continue;  // no edges in this chunk's partial
             const float mn = fmaxf(st.m, mc);
             a = (st.m == -INFINITY) ? 0.0f : expf(st.m - mn);
@@ -379,9 +435,18 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
 #pragma unroll
             for (int i = 0; i < VEC; ++i) {
                 const float v = gl_.ln.in(ch, i) ? w[gl_.ln.off[ch] + i] : 0.0f;
-                st.acc[ch][i] = (MODE == GALA_SOFTMAX_REF) ? __fadd_rn(st.acc[ch][i], v)
+                st.acc[ch][i] = (ref_mode(MODE)) ? __fadd_rn(st.acc[ch][i], v)
                                                            : fmaf(st.acc[ch][i], a, __fmul_rn(v, b));
             }
+        if constexpr (MODE == kRefStats) {
+            const float *wm = w + F + 2 * H;
+            st.sma = __fadd_rn(st.sma, wm[F + hh]);
+#pragma unroll
+            for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    st.accm[ch][i] = __fadd_rn(st.accm[ch][i], gl_.ln.in(ch, i) ? wm[gl_.ln.off[ch] + i] : 0.0f);
+        }
     }
     const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, 1, st);
     if (gl_.leader && d.q_out) {
@@ -654,6 +719,10 @@ static void launch_gat_mode(const GatArgs &a) {
 
 template <int G, int VEC, int CH, bool RC, int HW>
 static void launch_gat(const GatArgs &a) {
+    if (a.mode == kRefStats) {  // row statistics: the head-distributed loop only (HW > 0)
+        if constexpr (HW > 0) launch_gat_mode<G, VEC, CH, RC, HW, kRefStats>(a);
+        return;
+    }
     if (a.mode == GALA_SOFTMAX_REF) launch_gat_mode<G, VEC, CH, RC, HW, GALA_SOFTMAX_REF>(a);
     else launch_gat_mode<G, VEC, CH, RC, HW, GALA_SOFTMAX_FIXED>(a);
 }
@@ -673,7 +742,7 @@ static int launch_gat_heads(const GatArgs &a, int hw) {
             default: break;
         }
     }
-    if (RC) return GALA_ERR_UNSUPPORTED;
+    if (RC || a.mode == kRefStats) return GALA_ERR_UNSUPPORTED;
     launch_gat<G, VEC, 1, false, 0>(a);
     return GALA_OK;
 }
@@ -707,24 +776,33 @@ static int gat_vec(const GatArgs &a, int L, int ch, int heads, int hw) {
 static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                         float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
-                        float *q_out, void *stream) {
+                        float *q_out, void *stream, float *ym = nullptr, int64_t ldym = 0,
+                        float *sma = nullptr, float *ar_out = nullptr) {
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
     const bool partial = (mode & GALA_GAT_PARTIAL) != 0;
+    const bool stats = ym != nullptr;
     mode &= ~GALA_GAT_PARTIAL;
     if (mode != GALA_SOFTMAX_REF && mode != GALA_SOFTMAX_FIXED) return GALA_ERR_INVALID_ARG;
-    if (F < 1 || F % heads != 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (F < 1 || F % heads != 0 || ldx < F || ldy < F || (stats && ldym < F)) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
+    if (stats && (mode != GALA_SOFTMAX_REF || partial || alpha_out || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
+    if (stats && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // square pattern
+    if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
+    auto vec_ok = [&](int v) {
+        const bool fits = D % v == 0 || (heads == 1 && ldx >= pad_to(F, v) && ldy >= pad_to(F, v) &&
+                                         (!stats || ldym >= pad_to(F, v)));
+        return fits && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
+               ((uintptr_t)Y % (4 * v)) == 0 && (!stats || (ldym % v == 0 && ((uintptr_t)ym % (4 * v)) == 0));
+    };
     int vec = 4;
-    while (vec > 1 && (!(D % vec == 0 || (heads == 1 && ldx >= pad_to(F, vec) && ldy >= pad_to(F, vec))) ||
-                       ldx % vec || ldy % vec || ((uintptr_t)X % (4 * vec)) || ((uintptr_t)Y % (4 * vec))))
-        vec >>= 1;
+    while (vec > 1 && !vec_ok(vec)) vec >>= 1;
     const int L = (F + vec - 1) / vec;
     const int ch = narrow_chunks(heads, vec, L);
     int G = 16;
@@ -732,12 +810,15 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
         G = 1;
         while (G < L) G <<= 1;
     }
-    a.mode = mode;
+    a.mode = stats ? kRefStats : mode;
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
     a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out, a.d.q_out = q_out;
     a.d.partial = partial ? 1 : 0;
+    a.d.ym_out = ym, a.d.ldym = ldym, a.d.sma_out = sma, a.d.ar_out = ar_out;
     a.hs = (hipStream_t)stream;
-    a.split = (!alpha_out || G % heads == 0) && hub_split(A, (int64_t)F + 2 * heads, &a.sp);
+    // hub-row chunk partials: {acc[F], m[H], sum[H]} (+ {accm[F], sma[H]} with the statistics)
+    const int64_t ws_need = stats ? 2 * (int64_t)F + 3 * heads : (int64_t)F + 2 * heads;
+    a.split = (!alpha_out || G % heads == 0) && hub_split(A, ws_need, &a.sp);
     const bool rc = aR == nullptr;
     // alpha of heads that do not divide the row group is formed by a per-head pass that
     // re-reads aR: there is none to read when it is recomputed
@@ -767,6 +848,17 @@ extern "C" int gala_gat_fwd_ex_f32(const gala_csr_t *A, const float *aL, const f
     if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope, mode,
                         Y, ldy, alpha_out, q_out, stream);
+}
+
+extern "C" int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                      const float *wR, const float *bR, const float *X, int64_t ldx,
+                                      int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,
+                                      float *q_out, float *Ym, int64_t ldym, float *sma, float *aR_out,
+                                      void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if (!Ym && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
+                        GALA_SOFTMAX_REF, Y, ldy, nullptr, q_out, stream, Ym, ldym, sma, aR_out);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

@@ -92,7 +92,15 @@ struct GatDev {
     int32_t F;
     float slope;
     int32_t partial;                 // forward, GALA_GAT_PARTIAL: unnormalised Y, raw sums in q_out
+    // REF row statistics (gala_gat_{fwd,bwd}_stats_f32): Ym = sum m*alpha*X, sma = sum m*alpha
+    float *ym_out, *sma_out, *ar_out;  // forward (ar_out: the rows' recomputed aR, nullable)
+    const float *ys, *yms, *smas;      // backward: Y (ld ldy), Ym (ld ldym), sma
+    int64_t ldym;
 };
+
+// Internal forward MODE: REF softmax that also accumulates the row statistics.
+constexpr int kRefStats = 2;
+__host__ __device__ constexpr bool ref_mode(int mode) { return mode != GALA_SOFTMAX_FIXED; }
 
 
 // The lane's share of one row (or one chunk of a hub row) for the GAT kernels.

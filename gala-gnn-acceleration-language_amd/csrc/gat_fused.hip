@@ -27,7 +27,9 @@ struct FusedBwdState {
 // a U-edge batch is owned by lane k mod UH of its head group: it loads / recomputes aR,
 // forms alpha and the LeakyReLU factor, and counts the edge's sds; alpha is broadcast to
 // the group for the dX accumulation.
-template <int G, int VEC, int U, int HW, int CH, bool RC>
+// ST (row statistics, gala_gat_bwd_stats_f32): the d_aL sums come from the forward's rows,
+// so an edge needs dY[col] and aR[col] only -- no X[col] gather, no per-edge dot.
+template <int G, int VEC, int U, int HW, int CH, bool RC, bool ST>
 __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const GatDev &d,
                                                     const GatLane<G, VEC, CH, RC> &gl_,
                                                     const float (&dy)[CH][VEC], int64_t e0,
@@ -58,10 +60,11 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
         for (int k = 0; k < U; ++k)
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) {
-                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
+                if constexpr (!ST)
+                    x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
                 yv[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.dY + c[k] * d.lddy + gl_.ln.off[ch]));
             }
-        if (RC) {
+        if constexpr (RC && !ST) {
             float all[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) all[k] = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, x[k]), gl_.wb);
@@ -85,13 +88,15 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
         static_for<0, U>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             float dd = 0.0f;
+            if constexpr (!ST) {
 #pragma unroll
-            for (int ch = 0; ch < CH; ++ch) {
-                const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
+                for (int ch = 0; ch < CH; ++ch) {
+                    const float *xv = reinterpret_cast<const float *>(&x[k][ch]);
 #pragma unroll
-                for (int i = 0; i < VEC; ++i) dd = fmaf(dy[ch][i], xv[i], dd);
+                    for (int i = 0; i < VEC; ++i) dd = fmaf(dy[ch][i], xv[i], dd);
+                }
+                dd = group_sum<HW>(dd);
             }
-            dd = group_sum<HW>(dd);
             const float ak = group_bcast<HW, k % UH>(a[k / UH]);
             if (j0 + k >= n) return;
 #pragma unroll
@@ -100,7 +105,7 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
 #pragma unroll
                 for (int i = 0; i < VEC; ++i) dxa[ch][i] = fmaf(ak, yk[i], dxa[ch][i]);
             }
-            if (owner && kl == k % UH) {
+            if (!ST && owner && kl == k % UH) {
                 const int i = k / UH;
                 const float sds = __fmul_rn(a[i], dd);
                 st.acc += sds;
@@ -133,15 +138,46 @@ __device__ __forceinline__ void store_dx(const GatDev &d, const Lanes<G, VEC, CH
     }
 }
 
-template <int G, int VEC, int U, int HW, int CH, bool RC>
+// d_aL of one row from the forward's row statistics: <dY, Y> and <dY, Ym> per head
+template <int G, int VEC, int HW, int CH, bool RC>
+__device__ __forceinline__ void stats_d_al(const EdgeParams &p, const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
+                                           int64_t row, const float (&dy)[CH][VEC]) {
+    typedef typename GVec<VEC>::T V;
+    float syy = 0.0f, sym = 0.0f;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+        const V y = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.ys + row * d.ldy + gl_.ln.off[ch]));
+        const V ym = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.yms + row * d.ldym + gl_.ln.off[ch]));
+        const float *yv = reinterpret_cast<const float *>(&y);
+        const float *mv = reinterpret_cast<const float *>(&ym);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            syy = fmaf(dy[ch][i], yv[i], syy);
+            sym = fmaf(dy[ch][i], mv[i], sym);
+        }
+    }
+    const float eps = (float)p.seg.n * 1e-12f;
+    const float acc = group_sum<HW>(syy) + eps;  // K7 on sds (common.h:793-794)
+    const float s1 = group_sum<HW>(sym);
+    if (gl_.leader) {
+        const int64_t o = row * gl_.H + gl_.hh;
+        d.d_aL[o] = (s1 - acc * d.smas[o]) + eps;   // common.h:662-667
+    }
+}
+
+template <int G, int VEC, int U, int HW, int CH, bool RC, bool ST>
 __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d, int32_t split_threshold) {
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
-    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
-        return;  // hub row: k_gat_bwd_fused_chunk / _fixup
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     float dy[CH][VEC], dxa[CH][VEC];
-    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+    if constexpr (ST) {  // row-local: every row, hub rows included
+        load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+        stats_d_al<G, VEC, HW, CH, RC>(p, d, gl_, row, dy);
+    }
+    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
+        return;  // hub row: k_gat_bwd_fused_chunk / _fixup
+    if constexpr (!ST) load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
@@ -150,9 +186,10 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        gat_bwd_fused_range<G, VEC, U, HW, CH, RC>(p, d, gl_, dy, e0, e1, st, dxa);
+        gat_bwd_fused_range<G, VEC, U, HW, CH, RC, ST>(p, d, gl_, dy, e0, e1, st, dxa);
     }
     store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
+    if constexpr (ST) return;
     const float eps = (float)p.seg.n * 1e-12f;
     const float acc = group_sum<HW>(st.acc) + eps;          // K7 on sds (common.h:793-794)
     const float s1 = group_sum<HW>(st.s_msds), s2 = group_sum<HW>(st.s_ma);
@@ -160,20 +197,21 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d
 }
 
 // hub rows: chunk partials -> ws[c] = {dX[F], acc[H], s_msds[H], s_ma[H]}
-template <int G, int VEC, int U, int HW, int CH, bool RC>
+template <int G, int VEC, int U, int HW, int CH, bool RC, bool ST>
 __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_chunk(EdgeParams p, GatDev d, HubSplit sp) {
     GALA_CHUNK_PROLOGUE(G);
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     float dy[CH][VEC], dxa[CH][VEC];
-    load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
+    if constexpr (!ST) load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dxa[ch][i] = 0.0f;
     FusedBwdState st;
-    gat_bwd_fused_range<G, VEC, U, HW, CH, RC>(p, d, gl_, dy, e0, e1, st, dxa);
+    gat_bwd_fused_range<G, VEC, U, HW, CH, RC, ST>(p, d, gl_, dy, e0, e1, st, dxa);
     float *w = sp.ws + c * sp.ws_cols;
     store_dx<G, VEC, CH>(d, gl_.ln, w, dxa);
+    if constexpr (ST) return;  // ws[c] = {dX[F]}
     const float acc = group_sum<HW>(st.acc);
     const float s1 = group_sum<HW>(st.s_msds), s2 = group_sum<HW>(st.s_ma);
     if (gl_.leader) {
@@ -185,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_chunk(EdgeParams p, Ga
 }
 
 // hub rows: the chunk partials of a row summed in chunk order (dX: as k_spmm_fixup)
-template <int G, int VEC, int CH, bool RC>
+template <int G, int VEC, int CH, bool RC, bool ST>
 __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_fixup(EdgeParams p, GatDev d, HubSplit sp) {
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
@@ -207,12 +245,14 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_fixup(EdgeParams p, Ga
 #pragma unroll
             for (int i = 0; i < VEC; ++i)
                 dxa[ch][i] = __fadd_rn(dxa[ch][i], gl_.ln.in(ch, i) ? w[gl_.ln.off[ch] + i] : 0.0f);
-        acc = __fadd_rn(acc, w[F + hh]);
-        s1 = __fadd_rn(s1, w[F + H + hh]);
-        s2 = __fadd_rn(s2, w[F + 2 * H + hh]);
+        if constexpr (!ST) {
+            acc = __fadd_rn(acc, w[F + hh]);
+            s1 = __fadd_rn(s1, w[F + H + hh]);
+            s2 = __fadd_rn(s2, w[F + 2 * H + hh]);
+        }
     }
     store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
-    if (gl_.leader) {
+    if (!ST && gl_.leader) {
         acc = __fadd_rn(acc, 1e-12f);
         d.d_aL[row * H + hh] = (s1 - acc * s2) + 1e-12f;
     }
@@ -232,16 +272,25 @@ struct FusedArgs {
     hipStream_t hs;
 };
 
-template <int G, int VEC, int HW, int CH, bool RC>
-void launch_fused(const FusedArgs &a) {
+template <int G, int VEC, int HW, int CH, bool RC, bool ST>
+void launch_fused_st(const FusedArgs &a) {
     constexpr int U = 8;
-    hipLaunchKernelGGL((k_gat_bwd_fused<G, VEC, U, HW, CH, RC>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
+    hipLaunchKernelGGL((k_gat_bwd_fused<G, VEC, U, HW, CH, RC, ST>), dim3(blocks_for(a.p.n_rows, G)), dim3(kBlock),
                        0, a.hs, a.p, a.d, a.split ? a.sp.threshold : 0);
     if (!a.split) return;
-    hipLaunchKernelGGL((k_gat_bwd_fused_chunk<G, VEC, U, HW, CH, RC>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
+    hipLaunchKernelGGL((k_gat_bwd_fused_chunk<G, VEC, U, HW, CH, RC, ST>), dim3(blocks_for_groups(a.sp.n_chunks, G)),
                        dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
-    hipLaunchKernelGGL((k_gat_bwd_fused_fixup<G, VEC, CH, RC>), dim3(blocks_for_groups(a.sp.n_rows_split, G)),
+    hipLaunchKernelGGL((k_gat_bwd_fused_fixup<G, VEC, CH, RC, ST>), dim3(blocks_for_groups(a.sp.n_rows_split, G)),
                        dim3(kBlock), 0, a.hs, a.p, a.d, a.sp);
+}
+
+// RC: aR recomputed from X (never with the statistics, which read aR); !RC: the
+// statistics variant when the forward's rows are given (a.d.ys)
+template <int G, int VEC, int HW, int CH, bool RC>
+void launch_fused(const FusedArgs &a) {
+    if constexpr (RC) launch_fused_st<G, VEC, HW, CH, true, false>(a);
+    else if (a.d.ys) launch_fused_st<G, VEC, HW, CH, false, true>(a);
+    else launch_fused_st<G, VEC, HW, CH, false, false>(a);
 }
 
 template <int G, int VEC, bool RC>
@@ -281,6 +330,49 @@ int fused_vec(const FusedArgs &a, int L, int ch, int heads, int hw) {
 }
 
 }  // namespace
+
+static int fused_dispatch(FusedArgs &a, int F, int heads, int vec, bool rc) {
+    const int D = F / heads;
+    const int L = (F + vec - 1) / vec;
+    const int ch = narrow_chunks(heads, vec, L);
+    const int hw = (D % vec == 0) ? D / vec : 0;
+    if (heads > 1 && (hw == 0 || (hw & (hw - 1)))) return GALA_ERR_UNSUPPORTED;
+    int r;
+    if (vec == 4) r = rc ? fused_vec<4, true>(a, L, ch, heads, hw) : fused_vec<4, false>(a, L, ch, heads, hw);
+    else if (vec == 2) r = rc ? fused_vec<2, true>(a, L, ch, heads, hw) : fused_vec<2, false>(a, L, ch, heads, hw);
+    else r = rc ? fused_vec<1, true>(a, L, ch, heads, hw) : fused_vec<1, false>(a, L, ch, heads, hw);
+    if (r) return r;
+    return launch_status();
+}
+
+extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *dY,
+                                      int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
+                                      const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
+                                      const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
+    FusedArgs a{};
+    int st = edge_setup(A, heads, &a.p);
+    if (st) return st;
+    if (F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || !aR || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
+    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // dY[col]: a square pattern
+    const int D = F / heads;
+    auto ok = [&](int v) {
+        const bool fits = D % v == 0 || (heads == 1 && lddy >= pad_to(F, v) && ldy >= pad_to(F, v) &&
+                                         ldym >= pad_to(F, v) && lddx >= pad_to(F, v));
+        return fits && lddy % v == 0 && ldy % v == 0 && ldym % v == 0 && lddx % v == 0 &&
+               ((uintptr_t)dY % (4 * v)) == 0 && ((uintptr_t)Y % (4 * v)) == 0 &&
+               ((uintptr_t)Ym % (4 * v)) == 0 && ((uintptr_t)dX % (4 * v)) == 0;
+    };
+    int vec = 4;
+    while (vec > 1 && !ok(vec)) vec >>= 1;
+    a.d.aL = aL, a.d.aR = aR, a.d.F = F, a.d.slope = slope;
+    a.d.dY = dY, a.d.lddy = lddy, a.d.q = q, a.d.dX = dX, a.d.lddx = lddx, a.d.d_aL = d_aL;
+    a.d.ys = Y, a.d.ldy = ldy, a.d.yms = Ym, a.d.ldym = ldym, a.d.smas = sma;
+    a.hs = (hipStream_t)stream;
+    a.split = hub_split(A, pad_to(F, 4), &a.sp);  // hub rows: dX[F] chunk partials
+    return fused_dispatch(a, F, heads, vec, false);
+}
 
 extern "C" int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,
                                       const float *wR, const float *bR, const float *X,

@@ -340,6 +340,34 @@ def gat_bwd_fused(g: DeviceGraph, aL, X, dY, q, aR=None, wR=None, bR=None, heads
     return dX, d_aL
 
 
+def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, want_aR=False):
+    """gala_gat_fwd_stats_f32 (REF, square pattern): returns (Y, q, Ym, sma[, aR_out]) with
+    Ym[r] = sum_e m_e alpha_e X[col_e], sma[r, h] = sum_e m_e alpha_e (m_e the LeakyReLU
+    factor); aR_out (aR recomputed from wR, bR) the rows' own source logits."""
+    F = X.shape[1]
+    Y = _rows_like(X, g.n_rows)
+    Ym = _rows_like(X, g.n_rows)
+    q = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    sma = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+    aR_out = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if want_aR else None
+    _abi.call("gala_gat_fwd_stats_f32", g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR), _dp(wR),
+              _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(Y), Y.stride(0), _dp(q), _dp(Ym), Ym.stride(0),
+              _dp(sma), _dp(aR_out), _stream())
+    return (Y, q, Ym, sma, aR_out) if want_aR else (Y, q, Ym, sma)
+
+
+def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2):
+    """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
+    dY[col] only."""
+    F = dY.shape[1]
+    dX = _rows_like(dY, g.n_rows)
+    d_aL = torch.empty(g.n_rows * heads, device=dY.device, dtype=torch.float32)
+    _abi.call("gala_gat_bwd_stats_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(dY), dY.stride(0), F,
+              heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0), _dp(sma), _dp(dX), dX.stride(0),
+              _dp(d_aL), _stream())
+    return dX, d_aL
+
+
 def edge_permute(perm, src, heads=1):
     n = perm.numel()
     dst = torch.empty(n * heads, device=src.device, dtype=torch.float32)

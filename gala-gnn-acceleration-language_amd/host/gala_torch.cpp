@@ -37,6 +37,8 @@ struct Backend {
     decltype(&gala_gat_fwd_ex_f32) gat_fwd_ex;
     decltype(&gala_gat_bwd_ex_f32) gat_bwd_ex;
     decltype(&gala_gat_bwd_fused_f32) gat_bwd_fused;
+    decltype(&gala_gat_fwd_stats_f32) gat_fwd_stats;
+    decltype(&gala_gat_bwd_stats_f32) gat_bwd_stats;
     decltype(&gala_edge_permute_f32) permute;
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
@@ -48,6 +50,7 @@ const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
                    gala_gat_fwd_ex_f32, gala_gat_bwd_ex_f32, gala_gat_bwd_fused_f32,
+                   gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
@@ -56,6 +59,7 @@ const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcas
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
                    gala_cpu_gat_fwd_attn_f32, gala_cpu_gat_bwd_attn_f32,
                    gala_cpu_gat_fwd_ex_f32, gala_cpu_gat_bwd_ex_f32, gala_cpu_gat_bwd_fused_f32,
+                   gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32};
 
@@ -818,6 +822,71 @@ bool recompute_attention(int64_t li, int64_t mode) {
     return mode == GALA_SOFTMAX_REF && same_pattern(slot(2 * li), slot(2 * li + 1));
 }
 
+// The row-statistics variant of the recomputed REF layer (gala_gat_{fwd,bwd}_stats_f32):
+// the forward also keeps Ym = sum m*alpha*X and sma = sum m*alpha per row, and the backward
+// gathers dY[col] only.  GALA_GAT_ROWSTATS=0 keeps the X-gathering fused backward.
+bool rowstats_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("GALA_GAT_ROWSTATS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// What the row-statistics forward leaves for its backward.
+struct GatStats {
+    torch::Tensor Y, q, Ym, sma, aR;  // aR: the given logits, or the recomputed ones (RC)
+};
+
+// One launch of gala_gat_fwd_stats_f32 on slot 2li; false when the kernel does not take
+// this shape (the caller then takes the plain recomputed path).
+bool gat_forward_stats(const Slot &s, const torch::Tensor &l, const torch::Tensor &r, const torch::Tensor &x,
+                       const torch::Tensor &wR, const torch::Tensor &bR, int heads, double slope, GatStats &o) {
+    CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+    const int64_t nrows = cv.c.n_rows, F = x.size(1);
+    if (x.size(0) != nrows) return false;  // a square pattern only
+    cv.c.n_cols = x.size(0);
+    with_workspace(cv, s.off, 2 * ((F + 3) / 4 * 4) + 3 * heads);  // hub rows: {acc, m, sum, accm, sma}
+    auto Y = rows_like(x, nrows), Ym = rows_like(x, nrows);
+    auto q = torch::empty({nrows * heads}, fopts(x)), sma = torch::empty({nrows * heads}, fopts(x));
+    torch::Tensor aR = r.defined() ? r : torch::empty({nrows * heads}, fopts(x));
+    const int st = be(s.off).gat_fwd_stats(
+        &cv.c, l.data_ptr<float>(), r.defined() ? r.data_ptr<float>() : nullptr,
+        r.defined() ? nullptr : wR.data_ptr<float>(), (!r.defined() && bR.defined()) ? bR.data_ptr<float>() : nullptr,
+        x.data_ptr<float>(), x.stride(0), (int32_t)F, heads, (float)slope, Y.data_ptr<float>(), Y.stride(0),
+        q.data_ptr<float>(), Ym.data_ptr<float>(), Ym.stride(0), sma.data_ptr<float>(),
+        r.defined() ? nullptr : aR.data_ptr<float>(), stream_of(s.off));
+    if (st == GALA_ERR_UNSUPPORTED) return false;
+    check(st, "gala_gat_fwd_stats_f32");
+    o = {Y, q, Ym, sma, aR};
+    return true;
+}
+
+// REF backward from the row statistics: dX and d_aL (= d_aR) in one kernel that gathers
+// dY[col] only.
+bool gat_backward_stats(const torch::Tensor &l, const GatStats &o, const torch::Tensor &dY_in, int64_t li,
+                        double slope, int heads, GatGrads &g) {
+    Slot fw = slot(2 * li);
+    const torch::Tensor dY = heads == 1 ? pad_rows4(dY_in) : dY_in.contiguous();
+    const int64_t F = o.Y.size(1), nrows = fw.off.numel() / fw.segs - 1;
+    CsrView cf = view(fw.off, fw.cols, nullptr, fw.bounds, fw.segs);
+    cf.c.n_cols = dY.size(0);
+    with_workspace(cf, fw.off, (F + 3) / 4 * 4);  // hub rows: dX[F] chunk partials
+    check_on(dY, fw.off, "grad");
+    auto dX = rows_like(dY, nrows);
+    auto daL = torch::empty_like(l);
+    const int st = be(fw.off).gat_bwd_stats(&cf.c, l.data_ptr<float>(), o.aR.data_ptr<float>(),
+                                            dY.data_ptr<float>(), dY.stride(0), (int32_t)F, heads, (float)slope,
+                                            o.q.data_ptr<float>(), o.Y.data_ptr<float>(), o.Y.stride(0),
+                                            o.Ym.data_ptr<float>(), o.Ym.stride(0), o.sma.data_ptr<float>(),
+                                            dX.data_ptr<float>(), dX.stride(0), daL.data_ptr<float>(),
+                                            stream_of(fw.off));
+    if (st == GALA_ERR_UNSUPPORTED) return false;
+    check(st, "gala_gat_bwd_stats_f32");
+    g = {daL, daL, dX};
+    return true;
+}
+
 // fused GAT layer: sddvv + LeakyReLU + edge softmax + weighted aggregation in one pass.
 // REF mode keeps the attention factored (p per edge, q per row: no normalisation pass over
 // the edges); FIXED materialises alpha (its backward needs the transposed alpha).
@@ -839,26 +908,45 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         // factored (p, q); FIXED: alpha itself (its backward permutes it onto A^T)
         const bool recompute = recompute_attention(li, mode);
         const bool factored = mode == GALA_SOFTMAX_REF;
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["slope"] = slope;
+        ctx->saved_data["mode"] = mode;
+        ctx->saved_data["heads"] = (int64_t)heads;
+        GatStats o;
+        if (recompute && rowstats_enabled() && gat_forward_stats(s, l, r, x, {}, {}, heads, slope, o)) {
+            ctx->saved_data["stats"] = true;
+            ctx->save_for_backward({l, r, x, o.q, o.Y, o.Ym, o.sma});
+            return o.Y;
+        }
         auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
         auto q = factored ? torch::empty({nrows * heads}, fopts(x)) : torch::empty({0}, fopts(x));
         auto Y = gat_forward_launch(s, l, r, x, {}, {}, heads, slope, mode,
                                     recompute ? nullptr : alpha.data_ptr<float>(),
                                     factored ? q.data_ptr<float>() : nullptr);
-        ctx->saved_data["li"] = li;
-        ctx->saved_data["slope"] = slope;
-        ctx->saved_data["mode"] = mode;
-        ctx->saved_data["heads"] = (int64_t)heads;
         ctx->save_for_backward({l, r, x, alpha, q});
         return Y;
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
-        auto l = sv[0], r = sv[1], x = sv[2], alpha = sv[3];
-        torch::Tensor q = sv[4].numel() > 0 ? sv[4] : torch::Tensor();
         const int64_t li = ctx->saved_data["li"].toInt(), mode = ctx->saved_data["mode"].toInt();
         const double slope = ctx->saved_data["slope"].toDouble();
         const int heads = (int)ctx->saved_data["heads"].toInt();
+        auto l = sv[0], r = sv[1], x = sv[2];
         GatGrads g;
+        if (ctx->saved_data.count("stats")) {
+            const GatStats o{sv[4], sv[3], sv[5], sv[6], r};
+            if (!gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g) &&
+                !gat_backward_recompute(l, r, x, o.q, grad_outputs[0], li, slope, heads, {}, {}, g)) {
+                auto q = o.q.clone();  // rebuild the factored p (the forward writes the same q)
+                auto alpha = torch::empty({slot(2 * li).cols.numel() * heads}, fopts(x));
+                gat_forward_launch(slot(2 * li), l, r, x, {}, {}, heads, slope, mode, alpha.data_ptr<float>(),
+                                   q.data_ptr<float>());
+                g = gat_backward(l, r, x, alpha, q, grad_outputs[0], li, slope, mode, heads, {}, {});
+            }
+            return {g.daL.view_as(l), g.daR.view_as(r), g.dX, torch::Tensor(), torch::Tensor(), torch::Tensor()};
+        }
+        auto alpha = sv[3];
+        torch::Tensor q = sv[4].numel() > 0 ? sv[4] : torch::Tensor();
         if (alpha.numel() == 0 && !gat_backward_recompute(l, r, x, q, grad_outputs[0], li, slope, heads, {}, {}, g)) {
             // the fused kernel does not take this shape: rebuild the factored p
             alpha = torch::empty({slot(2 * li).cols.numel() * heads}, fopts(x));
@@ -902,30 +990,46 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         if (b.defined()) check_on(b, s.off, "attn_r bias");
         const bool recompute = recompute_attention(li, mode);
         const bool factored = mode == GALA_SOFTMAX_REF;
-        auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
-        auto q = factored ? torch::empty({nrows * heads}, fopts(x)) : torch::empty({0}, fopts(x));
-        auto Y = gat_forward_launch(s, l, {}, x, w, b, heads, slope, mode,
-                                    recompute ? nullptr : alpha.data_ptr<float>(),
-                                    factored ? q.data_ptr<float>() : nullptr);
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
         ctx->saved_data["mode"] = mode;
         ctx->saved_data["heads"] = (int64_t)heads;
         ctx->saved_data["has_bias"] = b.defined();
-        ctx->save_for_backward({l, x, w, b.defined() ? b : torch::empty({0}, fopts(x)), alpha, q});
+        const torch::Tensor b_saved = b.defined() ? b : torch::empty({0}, fopts(x));
+        GatStats o;
+        if (recompute && rowstats_enabled() && gat_forward_stats(s, l, {}, x, w, b, heads, slope, o)) {
+            // o.aR: the recomputed source logits, read by the backward
+            ctx->saved_data["stats"] = true;
+            ctx->save_for_backward({l, x, w, b_saved, o.aR, o.q, o.Y, o.Ym, o.sma});
+            return o.Y;
+        }
+        auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
+        auto q = factored ? torch::empty({nrows * heads}, fopts(x)) : torch::empty({0}, fopts(x));
+        auto Y = gat_forward_launch(s, l, {}, x, w, b, heads, slope, mode,
+                                    recompute ? nullptr : alpha.data_ptr<float>(),
+                                    factored ? q.data_ptr<float>() : nullptr);
+        ctx->save_for_backward({l, x, w, b_saved, alpha, q});
         return Y;
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
         auto l = sv[0], x = sv[1], w = sv[2], alpha = sv[4];
-        torch::Tensor q = sv[5].numel() > 0 ? sv[5] : torch::Tensor();
+        const bool stats = ctx->saved_data.count("stats") > 0;
+        torch::Tensor q = stats ? sv[5] : (sv[5].numel() > 0 ? sv[5] : torch::Tensor());
         const bool has_bias = ctx->saved_data["has_bias"].toBool();
         const int heads = (int)ctx->saved_data["heads"].toInt();
         const int64_t li = ctx->saved_data["li"].toInt(), mode = ctx->saved_data["mode"].toInt();
         const double slope = ctx->saved_data["slope"].toDouble();
         torch::Tensor b = has_bias ? sv[3] : torch::Tensor();
         GatGrads g;
-        if (alpha.numel() == 0 && !gat_backward_recompute(l, {}, x, q, grad_outputs[0], li, slope, heads, w, b, g)) {
+        bool done = false;
+        if (stats) {
+            const GatStats o{sv[6], q, sv[7], sv[8], sv[4]};
+            done = gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g);
+            alpha = torch::empty({0}, fopts(x));  // otherwise: the recomputed path below
+        }
+        if (!done && alpha.numel() == 0 && !gat_backward_recompute(l, {}, x, q, grad_outputs[0], li, slope, heads, w, b, g)) {
+            if (stats) q = q.clone();
             alpha = torch::empty({slot(2 * li).cols.numel() * heads}, fopts(x));
             gat_forward_launch(slot(2 * li), l, {}, x, w, b, heads, slope, mode, alpha.data_ptr<float>(),
                                q.data_ptr<float>());

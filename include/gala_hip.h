@@ -333,6 +333,40 @@ int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR
                            const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope,
                            const float *q, float *dX, int64_t lddx, float *d_aL, void *stream);
 
+/*
+ * REF-mode GAT with ROW STATISTICS (square pattern whose backward pattern is the forward
+ * one, as gala_gat_bwd_fused_f32).  The reference's d_aL row sum (common.h:622-675,
+ * 791-799, 835-894) is, per row r and head h, with m_e = 1 if aL[r,h] + aR[c_e,h] > 0 else
+ * slope (the LeakyReLU factor):
+ *   sum_e m_e ds_e = sum_e m_e alpha_e d_alpha_e - acc * sum_e m_e alpha_e,
+ *   acc = S*eps + sum_e alpha_e d_alpha_e,       d_alpha_e = <dY[r], X[c_e]>  (per head)
+ * and both edge sums regroup into row-local dot products with rows the forward can build
+ * from the X rows it gathers anyway:
+ *   sum_e alpha_e d_alpha_e     = <dY[r], Y[r]>,   Y[r]  = sum_e alpha_e X[c_e]
+ *   sum_e m_e alpha_e d_alpha_e = <dY[r], Ym[r]>,  Ym[r] = sum_e m_e alpha_e X[c_e]
+ * So the forward writes Ym (ld ldym) and sma[r,h] = sum_e m_e alpha_e beside Y and q, and
+ * the backward gathers dY[col] only (for dX) instead of dY[col] and X[col].  Equal to the
+ * reference within fp32 rounding (the sums are regrouped); dX is bit-identical to
+ * gala_gat_bwd_fused_f32's.
+ *
+ * gala_gat_fwd_stats_f32: Y, q_out as gala_gat_fwd_ex_f32 in REF mode with alpha_out NULL,
+ * plus Ym, sma.  aR or (aR NULL) its per-head recompute from X (wR, bR); aR_out (nullable)
+ * then receives every row's recomputed source logit, bit-identical to the per-edge
+ * recompute, for the backward.  Several heads need D/VEC a power of two (else
+ * GALA_ERR_UNSUPPORTED; the caller then takes gala_gat_fwd_ex_f32 + gala_gat_bwd_fused_f32).
+ * gala_gat_bwd_stats_f32: dX[r] = sum_e alpha_e dY[c_e] (alpha = fl(min(exp(LeakyReLU(
+ * aL + aR)), 1e12) * q), aR explicit) and d_aL[r,h] = (<dY,Ym>_h - (S*eps + <dY,Y>_h) *
+ * sma[r,h]) + S*eps (= d_aR in REF mode), eps = 1e-12.
+ */
+int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                           const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                           float slope, float *Y, int64_t ldy, float *q_out, float *Ym,
+                           int64_t ldym, float *sma, float *aR_out, void *stream);
+int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *dY,
+                           int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
+                           const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
+                           const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream);
+
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                           float *dst, void *stream);

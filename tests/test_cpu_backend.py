@@ -201,6 +201,43 @@ def test_gat_attention_recompute(graph, mode):
         np.testing.assert_allclose(daL, daL_ref, **TOL)
 
 
+@pytest.mark.parametrize("F,heads,rc", [(32, 1, False), (47, 1, True), (64, 4, False), (64, 4, True)])
+def test_gat_row_stats(graph, F, heads, rc):
+    """gala_cpu_gat_{fwd,bwd}_stats_f32: Y within tolerance of the oracle, dX = A_alpha dY,
+    d_aL from the row statistics within tolerance of the oracle's edge-by-edge chain."""
+    D = F // heads
+    aL = features(graph.n_rows, heads, seed=61)
+    X = features(graph.n_cols, F, seed=63)
+    dY = features(graph.n_rows, F, seed=64)
+    if rc:
+        wR = features(1, F, seed=65).ravel() * 0.5
+        bR = features(1, heads, seed=66).ravel() * 0.1
+        aR = np.stack([X[:, h * D:(h + 1) * D].astype(np.float64) @ wR[h * D:(h + 1) * D].astype(np.float64) + bR[h]
+                       for h in range(heads)], 1).astype(np.float32)
+    else:
+        wR = bR = None
+        aR = features(graph.n_cols, heads, seed=62)
+    og = to_oracle(graph)
+    Y_ref, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    n = graph.n_rows
+    Y, Ym = np.empty((n, F), np.float32), np.empty((n, F), np.float32)
+    q, sma = np.empty(n * heads, np.float32), np.empty(n * heads, np.float32)
+    aR_out = np.empty(n * heads, np.float32) if rc else None
+    _abi.call_cpu("gala_gat_fwd_stats_f32", HostCsr(graph).ref, P(aL), None if rc else P(aR), P(wR), P(bR), P(X),
+                  F, F, heads, 0.2, P(Y), F, P(q), P(Ym), F, P(sma), P(aR_out), None)
+    np.testing.assert_allclose(Y, Y_ref, **TOL)
+    aRx = aR_out if rc else aR
+    if rc:
+        np.testing.assert_allclose(aR_out.reshape(n, heads), aR, rtol=1e-5, atol=1e-5)
+    _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    dX, daL = np.empty((n, F), np.float32), np.empty(n * heads, np.float32)
+    _abi.call_cpu("gala_gat_bwd_stats_f32", HostCsr(graph).ref, P(aL), P(aRx), P(dY), F, F, heads, 0.2, P(q), P(Y),
+                  F, P(Ym), F, P(sma), P(dX), F, P(daL), None)
+    np.testing.assert_allclose(daL, daL_ref, **TOL)
+    gw = orc.Graph(og.n_rows, og.n_cols, og.rowptr, og.col, al_ref, og.n_seg, og.bounds, heads)
+    np.testing.assert_allclose(dX, orc.spmm(gw, dY), **TOL)
+
+
 def test_edge_permute_and_dense_grad():
     g = powerlaw()
     t, perm = layout.transpose(g)

@@ -850,3 +850,75 @@ def test_gat_bwd_fused_recompute(F, heads, layout_, rc):
     with pytest.raises(_abi.GalaError):   # dY[col] needs a square pattern
         rect = ops.DeviceGraph(g.n_rows, g.n_rows + 5, dg.rowptr, dg.col, n_seg=dg.n_seg, bounds=dg.bounds)
         ops.gat_bwd_fused(rect, dev(aL), dev(np.vstack([X, X[:5]])), dev(dY), q, heads=heads, **kw)
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (100, 1)])
+@pytest.mark.parametrize("layout_", ["plain", "tiled", "split"])
+@pytest.mark.parametrize("rc", [False, True])
+def test_gat_row_stats(F, heads, layout_, rc):
+    """gala_gat_fwd_stats_f32 / gala_gat_bwd_stats_f32: Y and q BIT-identical to the
+    factored forward, dX BIT-identical to the recomputed fused backward (so the RC forward's
+    aR_out equals the per-edge recompute), d_aL within the tolerance of the oracle's
+    edge-by-edge REF chain; Ym and sma against a float64 restatement."""
+    g = powerlaw()
+    if layout_ == "tiled":
+        g = layout.col_tile(g, 1000)
+    D = F // heads
+    aL = features(g.n_rows, heads, seed=91)
+    X = features(g.n_cols, F, seed=93)
+    dY = features(g.n_rows, F, seed=94)
+    if rc:
+        wR = features(1, F, seed=95).ravel() * 0.5
+        bR = features(1, heads, seed=96).ravel() * 0.1
+        aR = np.stack([X[:, h * D:(h + 1) * D].astype(np.float64) @ wR[h * D:(h + 1) * D].astype(np.float64) + bR[h]
+                       for h in range(heads)], 1).astype(np.float32)
+        kw = dict(wR=dev(wR), bR=dev(bR))
+    else:
+        aR = features(g.n_cols, heads, seed=92)
+        kw = dict(aR=dev(aR))
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if layout_ == "split":
+        dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    out = ops.gat_fwd_stats(dg, dev(aL), dev(X), heads=heads, want_aR=rc, **kw)
+    Y, q, Ym, sma = out[:4]
+    Y0, q0 = ops.gat_fwd_ex(dg, dev(aL), dev(X), heads=heads, factored="q", **kw)
+    assert torch.equal(Y, Y0) and torch.equal(q, q0)
+    aRd = out[4] if rc else dev(aR)
+    if rc:  # the recomputed logits: the float64 Linear within fp32 rounding
+        np.testing.assert_allclose(host(aRd).reshape(-1, heads), aR, rtol=1e-5, atol=1e-5)
+    # Ym, sma: sum_e m_e alpha_e X[col], sum_e m_e alpha_e (float64 restatement)
+    og = to_oracle(g)
+    _, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    rows = np.repeat(np.arange(g.n_rows), np.diff(g.rowptr[:g.n_rows + 1]).astype(np.int64)) \
+        if g.n_seg == 1 else None
+    if rows is not None:
+        t = aL[rows].astype(np.float64) + aR[g.col].astype(np.float64)
+        m = np.where(t > 0, 1.0, 0.2)
+        ma = m * al_ref.reshape(-1, heads).astype(np.float64)
+        sma_ref = np.zeros((g.n_rows, heads))
+        np.add.at(sma_ref, rows, ma)
+        Ym_ref = np.zeros((g.n_rows, F))
+        np.add.at(Ym_ref, rows, np.repeat(ma, D, axis=1) * X[g.col].astype(np.float64))
+        np.testing.assert_allclose(host(sma).reshape(-1, heads), sma_ref, rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(host(Ym), Ym_ref, rtol=1e-4, atol=1e-4)
+    dX, daL = ops.gat_bwd_stats(dg, dev(aL), aRd, dev(dY), q, Y, Ym, sma, heads=heads)
+    dX0, daL0 = ops.gat_bwd_fused(dg, dev(aL), dev(X), dev(dY), q, heads=heads, **kw)
+    assert torch.equal(dX, dX0)
+    _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    np.testing.assert_allclose(host(daL), daL_ref, **TOL)
+    np.testing.assert_allclose(host(daL), host(daL0), **TOL)
+
+
+def test_gat_row_stats_rejects_bad_arguments():
+    g = cora_like()
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    aL, X = dev(features(g.n_rows, 1)), dev(features(g.n_cols, 32))
+    aR = dev(features(g.n_cols, 1))
+    with pytest.raises(_abi.GalaError):    # a rectangular pattern: no dY[col] / own-row logits
+        rect = ops.DeviceGraph(g.n_rows, g.n_rows + 5, dg.rowptr, dg.col)
+        ops.gat_fwd_stats(rect, aL, dev(features(g.n_rows + 5, 32)), aR=dev(features(g.n_rows + 5, 1)))
+    with pytest.raises(_abi.GalaError):    # aR_out only with the recompute
+        ops.gat_fwd_stats(dg, aL, X, aR=aR, want_aR=True)
+    Y, q, Ym, sma = ops.gat_fwd_stats(dg, aL, X, aR=aR)
+    with pytest.raises(_abi.GalaError):    # the backward reads aR explicitly
+        ops.gat_bwd_stats(dg, aL, None, dev(features(g.n_rows, 32)), q, Y, Ym, sma)

@@ -3,7 +3,8 @@
 the fused forward with materialised alpha vs the factored (p, q) output, the weighted SpMM
 of the same shape (the forward's floor: same gathers, a stored weight instead of a
 softmax), the dX SpMM on (p, q) and the fused backward -- at 8 heads (F = 256) and one
-head (F = 32, with and without the attention recompute).  One JSON line per op."""
+head (F = 32, with and without the attention recompute), and the row-statistics forward /
+backward pair.  One JSON line per op."""
 import json
 import os
 import sys
@@ -63,6 +64,14 @@ def main():
             "gat_bwd_fused": timeit(lambda: ops.gat_bwd_fused(dg, aL, X, dY, q, aR=aR, heads=H)),
             "gat_bwd_fused_recompute": timeit(lambda: ops.gat_bwd_fused(dg, aL, X, dY, q, wR=wR, bR=bR, heads=H)),
         }
+        # the row-statistics pair (gala_gat_{fwd,bwd}_stats_f32)
+        Ys, qs, Ym, sma = ops.gat_fwd_stats(dg, aL, X, aR=aR, heads=H)
+        _, _, _, _, aRo = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+        rec["gat_fwd_stats"] = timeit(lambda: ops.gat_fwd_stats(dg, aL, X, aR=aR, heads=H))
+        rec["gat_fwd_stats_recompute"] = timeit(lambda: ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H,
+                                                                         want_aR=True))
+        rec["gat_bwd_stats"] = timeit(lambda: ops.gat_bwd_stats(dg, aL, aR, dY, qs, Ys, Ym, sma, heads=H))
+        del Ys, qs, Ym, sma, aRo
         for k, v in rec.items():
             line = {"op": k, "heads": H, "F": F, "ms": v, "N": N, "E": E}
             out.append(line)
