@@ -913,7 +913,9 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         ctx->saved_data["mode"] = mode;
         ctx->saved_data["heads"] = (int64_t)heads;
         GatStats o;
-        if (recompute && rowstats_enabled() && gat_forward_stats(s, l, r, x, {}, {}, heads, slope, o)) {
+        // the statistics only serve a backward: none without gradients (eval forwards)
+        const bool grad = ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2);
+        if (recompute && grad && rowstats_enabled() && gat_forward_stats(s, l, r, x, {}, {}, heads, slope, o)) {
             ctx->saved_data["stats"] = true;
             ctx->save_for_backward({l, r, x, o.q, o.Y, o.Ym, o.sma});
             return o.Y;
@@ -997,7 +999,9 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         ctx->saved_data["has_bias"] = b.defined();
         const torch::Tensor b_saved = b.defined() ? b : torch::empty({0}, fopts(x));
         GatStats o;
-        if (recompute && rowstats_enabled() && gat_forward_stats(s, l, {}, x, w, b, heads, slope, o)) {
+        const bool grad = ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2) ||
+                          ctx->needs_input_grad(3);
+        if (recompute && grad && rowstats_enabled() && gat_forward_stats(s, l, {}, x, w, b, heads, slope, o)) {
             // o.aR: the recomputed source logits, read by the backward
             ctx->saved_data["stats"] = true;
             ctx->save_for_backward({l, x, w, b_saved, o.aR, o.q, o.Y, o.Ym, o.sma});
