@@ -823,6 +823,37 @@ extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, 
     return GALA_OK;
 }
 
+extern "C" int gala_cpu_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,
+                                      const float *w, const float *b, float *out, void *) {
+    if (n_rows < 0 || F < 1 || heads < 1 || F % heads != 0 || ldx < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0) return GALA_OK;
+    if (!X || !w || !out) return GALA_ERR_INVALID_ARG;
+    const int32_t D = F / heads;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t r = 0; r < n_rows; ++r)
+        for (int32_t h = 0; h < heads; ++h) {
+            float acc = 0.0f;
+            for (int32_t d = 0; d < D; ++d) acc = fmaf(X[r * ldx + h * D + d], w[h * D + d], acc);
+            out[r * heads + h] = b ? acc + b[h] : acc;
+        }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float *g,
+                                          const float *w, float *dX, int64_t lddx, int32_t accumulate, void *) {
+    if (n_rows < 0 || F < 1 || heads < 1 || F % heads != 0 || lddx < F) return GALA_ERR_INVALID_ARG;
+    if (n_rows == 0) return GALA_OK;
+    if (!g || !w || !dX) return GALA_ERR_INVALID_ARG;
+    const int32_t D = F / heads;
+#pragma omp parallel for schedule(static, 4096)
+    for (int64_t r = 0; r < n_rows; ++r)
+        for (int32_t c = 0; c < F; ++c) {
+            const float m = g[r * heads + c / D] * w[c];
+            dX[r * lddx + c] = accumulate ? dX[r * lddx + c] + m : m;
+        }
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n,
                                          int32_t heads, float *dst, void *) {
     if (n < 0 || heads < 1) return GALA_ERR_INVALID_ARG;

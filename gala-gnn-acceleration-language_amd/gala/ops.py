@@ -368,6 +368,26 @@ def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2)
     return dX, d_aL
 
 
+def head_attn(X, w, b=None, heads=1):
+    """gala_head_attn_f32: out[r, h] = <X[r, head h], w[head h]> + b[h] ([N, heads])."""
+    N, F = X.shape
+    out = torch.empty((N, heads), device=X.device, dtype=torch.float32)
+    _abi.call("gala_head_attn_f32", N, F, heads, _dp(X), X.stride(0), _dp(w), _dp(b), _dp(out), _stream())
+    return out
+
+
+def head_attn_bwd(g, w, heads=1, dX=None, n_rows=None):
+    """gala_head_attn_bwd_f32: dX[r, head h] (+)= g[r, h] * w[head h] (accumulates into dX
+    when given)."""
+    F = w.numel()
+    N = g.numel() // heads if n_rows is None else n_rows
+    acc = dX is not None
+    if dX is None:
+        dX = torch.empty((N, F), device=g.device, dtype=torch.float32)
+    _abi.call("gala_head_attn_bwd_f32", N, F, heads, _dp(g), _dp(w), _dp(dX), dX.stride(0), int(acc), _stream())
+    return dX
+
+
 def edge_permute(perm, src, heads=1):
     n = perm.numel()
     dst = torch.empty(n * heads, device=src.device, dtype=torch.float32)

@@ -39,6 +39,8 @@ struct Backend {
     decltype(&gala_gat_bwd_fused_f32) gat_bwd_fused;
     decltype(&gala_gat_fwd_stats_f32) gat_fwd_stats;
     decltype(&gala_gat_bwd_stats_f32) gat_bwd_stats;
+    decltype(&gala_head_attn_f32) head_attn;
+    decltype(&gala_head_attn_bwd_f32) head_attn_bwd;
     decltype(&gala_edge_permute_f32) permute;
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
@@ -50,7 +52,8 @@ const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
                    gala_gat_fwd_ex_f32, gala_gat_bwd_ex_f32, gala_gat_bwd_fused_f32,
-                   gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32,
+                   gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_head_attn_f32,
+                   gala_head_attn_bwd_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
@@ -59,7 +62,8 @@ const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcas
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
                    gala_cpu_gat_fwd_attn_f32, gala_cpu_gat_bwd_attn_f32,
                    gala_cpu_gat_fwd_ex_f32, gala_cpu_gat_bwd_ex_f32, gala_cpu_gat_bwd_fused_f32,
-                   gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32,
+                   gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32, gala_cpu_head_attn_f32,
+                   gala_cpu_head_attn_bwd_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32};
 
@@ -644,6 +648,25 @@ struct GatGrads {
     torch::Tensor daL, daR, dX;
 };
 
+// Gradients of the per-head Linear(D, 1) out[r,h] = <x[r, head h], w[head h]> + b[h]:
+// dW[head h] = sum_r g[r,h] x[r, head h], db[h] = sum_r g[r,h] -- the block diagonal of
+// gala_dense_grad_f32's [heads, F] dW = g^T x.
+void head_linear_grads(const torch::Tensor &x, const torch::Tensor &g, const torch::Tensor &w, int heads,
+                       torch::Tensor &dW, torch::Tensor &db) {
+    const int64_t N = x.size(0);
+    const int32_t F = (int32_t)x.size(1), D = F / heads;
+    auto full = torch::empty({heads, F}, fopts(x));
+    db = torch::empty({heads}, fopts(x));
+    const Backend &B = be(x);
+    const int64_t wsb = B.dense_ws(N, F, heads);
+    TORCH_CHECK(wsb >= 0, "gala: gala_dense_grad_workspace failed");
+    auto ws = torch::empty({std::max<int64_t>(wsb / 4, 1)}, fopts(x));
+    check(B.dense_grad(N, F, heads, x.data_ptr<float>(), x.stride(0), g.data_ptr<float>(), heads,
+                       full.data_ptr<float>(), db.data_ptr<float>(), 0, ws.data_ptr<float>(), wsb, stream_of(x)),
+          "gala_dense_grad_f32");
+    dW = full.view({heads, heads, D}).diagonal(0, 0, 1).t().reshape(w.sizes());  // [h, h*D + d]
+}
+
 // alpha = p * q (rounded) of a factored attention output, materialised on the forward
 // pattern (gala_row_scale_f32: the same product the fused kernels form per edge)
 torch::Tensor materialise_alpha(const Slot &fw, const torch::Tensor &p, const torch::Tensor &q) {
@@ -1056,12 +1079,11 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
                   "gala_dense_grad_f32");
             g.dX.addr_(daR.reshape({-1}), w.reshape({-1}));  // through aR = X wR^T + bR
         } else {  // per head: the block-diagonal Linear
-            const int64_t D = F / heads;
-            auto daR = g.daR.reshape({N, heads});
-            auto xr = x.reshape({N, heads, D});
-            dW = (daR.unsqueeze(2) * xr).sum(0).reshape(w.sizes());
-            db = daR.sum(0);
-            g.dX.view({N, heads, D}).add_(daR.unsqueeze(2) * w.reshape({1, heads, D}));
+            auto daR = g.daR.reshape({N, heads}).contiguous();
+            head_linear_grads(x, daR, w, heads, dW, db);
+            check(be(x).head_attn_bwd(N, F, heads, daR.data_ptr<float>(), w.data_ptr<float>(),
+                                      g.dX.data_ptr<float>(), g.dX.stride(0), 1, stream_of(x)),
+                  "gala_head_attn_bwd_f32");  // dX[:, head h] += d_aR[:, h] wR[head h]
         }
         return {g.daL.view_as(l), g.dX, dW.view_as(w), has_bias ? db.view_as(b) : torch::Tensor(),
                 torch::Tensor(), torch::Tensor(), torch::Tensor()};
@@ -1287,12 +1309,47 @@ HeadAttnImpl::HeadAttnImpl(int64_t in, int64_t heads) {
     bias = register_parameter("bias", torch::empty({heads}).uniform_(-bound, bound));
 }
 
+// The per-head attention Linear (gala_head_attn_f32 forward; backward: dX by
+// gala_head_attn_bwd_f32, dW / db by the dense gradient kernel).
+struct HeadAttnFn : public torch::autograd::Function<HeadAttnFn> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor weight, torch::Tensor bias) {
+        auto x = X.contiguous(), w = weight.contiguous(), b = bias.contiguous();
+        const int64_t H = b.numel(), F = w.numel(), N = x.size(0);
+        check_dev(x, torch::kFloat, "X");
+        check_dev(w, torch::kFloat, "attention weight");
+        check_dev(b, torch::kFloat, "attention bias");
+        TORCH_CHECK(w.device() == x.device() && b.device() == x.device(), "gala: head_attn_apply: operands on ",
+                    x.device(), ", ", w.device(), ", ", b.device());
+        auto out = torch::empty({N, H}, fopts(x));
+        check(be(x).head_attn(N, (int32_t)F, (int32_t)H, x.data_ptr<float>(), x.stride(0), w.data_ptr<float>(),
+                              b.data_ptr<float>(), out.data_ptr<float>(), stream_of(x)),
+              "gala_head_attn_f32");
+        ctx->save_for_backward({x, w});
+        ctx->saved_data["heads"] = H;
+        return out;
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto sv = ctx->get_saved_variables();
+        auto x = sv[0], w = sv[1];
+        const int heads = (int)ctx->saved_data["heads"].toInt();
+        const int64_t N = x.size(0);
+        const int32_t F = (int32_t)x.size(1);
+        auto g = grad_outputs[0].contiguous();
+        auto dX = torch::empty({N, F}, fopts(x));
+        check(be(x).head_attn_bwd(N, F, heads, g.data_ptr<float>(), w.data_ptr<float>(), dX.data_ptr<float>(),
+                                  dX.stride(0), 0, stream_of(x)),
+              "gala_head_attn_bwd_f32");
+        torch::Tensor dW, db;
+        head_linear_grads(x, g, w, heads, dW, db);
+        return {dX, dW, db};
+    }
+};
+
 torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias) {
     const int64_t H = bias.numel(), F = weight.numel();
-    TORCH_CHECK(X.size(-1) == F && F % H == 0, "gala: head_attn_apply: X has ", X.size(-1),
+    TORCH_CHECK(X.dim() == 2 && X.size(-1) == F && F % H == 0, "gala: head_attn_apply: X has ", X.size(-1),
                 " columns, the attention vectors ", F);
-    auto x = X.reshape({X.size(0), H, F / H});
-    return (x * weight.reshape({1, H, F / H})).sum(2) + bias.reshape({1, H});
+    return HeadAttnFn::apply(X, weight, bias);
 }
 
 }  // namespace gala

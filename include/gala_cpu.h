@@ -90,6 +90,11 @@ int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float
                                float slope, const float *q, const float *Y, int64_t ldy,
                                const float *Ym, int64_t ldym, const float *sma, float *dX,
                                int64_t lddx, float *d_aL, void *stream);
+int gala_cpu_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,
+                           const float *w, const float *b, float *out, void *stream);
+int gala_cpu_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float *g,
+                               const float *w, float *dX, int64_t lddx, int32_t accumulate,
+                               void *stream);
 int gala_cpu_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                               float *dst, void *stream);
 int gala_cpu_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const float *X, int64_t ldx,

@@ -367,6 +367,22 @@ int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR
                            const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
                            const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream);
 
+/*
+ * Per-head attention logits of the multi-head GAT layer (galac gat_heads: the DSL's
+ * attnL / attnR = dsl.nn.ffn(res, out=1) applied per head, a torch::nn::Linear in the
+ * reference, common.h:1188-1242):
+ *   out[r*heads + h] = <X[r, hD:(h+1)D], w[hD:(h+1)D]> + b[h]     (b nullable; D = F/heads)
+ * summed sequentially over d (fma).  gala_head_attn_bwd_f32 is its input gradient:
+ *   dX[r, hD+d] = g[r*heads + h] * w[hD+d]      (accumulate != 0: dX += ..., one rounding
+ *                                                each for the product and the sum)
+ * The weight / bias gradients are gala_dense_grad_f32 with M = heads (the block diagonal
+ * of its [heads, F] result).
+ */
+int gala_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,
+                       const float *w, const float *b, float *out, void *stream);
+int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float *g, const float *w,
+                           float *dX, int64_t lddx, int32_t accumulate, void *stream);
+
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,
                           float *dst, void *stream);

@@ -238,6 +238,30 @@ def test_gat_row_stats(graph, F, heads, rc):
     np.testing.assert_allclose(dX, orc.spmm(gw, dY), **TOL)
 
 
+@pytest.mark.parametrize("F,heads", [(256, 8), (47, 1), (64, 4), (24, 3)])
+def test_head_attn(F, heads):
+    """gala_cpu_head_attn_f32 against a float64 restatement; its backward bit-exact (one
+    product and one sum per element, float32 numpy rounds the same way)."""
+    N = 1000
+    X = features(N, F, seed=71)
+    w = features(1, F, seed=72).ravel()
+    b = features(1, heads, seed=73).ravel()
+    D = F // heads
+    out = np.empty((N, heads), np.float32)
+    _abi.call_cpu("gala_head_attn_f32", N, F, heads, P(X), F, P(w), P(b), P(out), None)
+    ref = (X.astype(np.float64).reshape(N, heads, D) * w.astype(np.float64).reshape(1, heads, D)).sum(2) + b
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+    g = features(N, heads, seed=74)
+    dX = np.empty((N, F), np.float32)
+    _abi.call_cpu("gala_head_attn_bwd_f32", N, F, heads, P(g), P(w), P(dX), F, 0, None)
+    m = np.repeat(g, D, axis=1) * w[None, :]
+    assert np.array_equal(dX, m)
+    dX0 = features(N, F, seed=75)
+    dX = dX0.copy()
+    _abi.call_cpu("gala_head_attn_bwd_f32", N, F, heads, P(g), P(w), P(dX), F, 1, None)
+    assert np.array_equal(dX, dX0 + m)
+
+
 def test_edge_permute_and_dense_grad():
     g = powerlaw()
     t, perm = layout.transpose(g)

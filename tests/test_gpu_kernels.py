@@ -922,3 +922,24 @@ def test_gat_row_stats_rejects_bad_arguments():
     Y, q, Ym, sma = ops.gat_fwd_stats(dg, aL, X, aR=aR)
     with pytest.raises(_abi.GalaError):    # the backward reads aR explicitly
         ops.gat_bwd_stats(dg, aL, None, dev(features(g.n_rows, 32)), q, Y, Ym, sma)
+
+
+@pytest.mark.parametrize("F,heads", [(256, 8), (47, 1), (64, 4), (24, 3), (100, 1)])
+def test_head_attn(F, heads):
+    """gala_head_attn_f32 bit-identical to the CPU twin (the same sequential fma chain per
+    (row, head)); its backward bit-exact against float32 numpy (one product, one sum)."""
+    N = 3001
+    X = features(N, F, seed=71)
+    w = features(1, F, seed=72).ravel()
+    b = features(1, heads, seed=73).ravel()
+    D = F // heads
+    out = ops.head_attn(dev(X), dev(w), dev(b), heads=heads)
+    ref = np.empty((N, heads), np.float32)
+    _abi.call_cpu("gala_head_attn_f32", N, F, heads, X.ctypes.data, F, w.ctypes.data, b.ctypes.data,
+                  ref.ctypes.data, None)
+    assert np.array_equal(host(out), ref)
+    g = features(N, heads, seed=74)
+    m = np.repeat(g, D, axis=1) * w[None, :]
+    assert np.array_equal(host(ops.head_attn_bwd(dev(g), dev(w), heads=heads)), m)
+    dX0 = features(N, F, seed=75)
+    assert np.array_equal(host(ops.head_attn_bwd(dev(g), dev(w), heads=heads, dX=dev(dX0))), dX0 + m)

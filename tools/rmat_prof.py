@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""R-MAT Products-shape SpMM (bench.py's second family) for rocprofv3: the planned SpMM
+(degree order + hub chunks) 10x, then the gather probe 10x; prints the degree profile."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gala-gnn-acceleration-language_amd"))
+sys.path.insert(0, ROOT)
+from gala import ops  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    F = int(os.environ.get("GALA_F", "32"))
+    hg = bench.products_graph("rmat", 1.0)
+    deg = np.diff(hg.rowptr.astype(np.int64))
+    qs = np.percentile(deg, [10, 25, 50, 75, 90, 99, 99.9])
+    thr = 1024
+    print(json.dumps({"N": int(hg.n_rows), "E": int(hg.nnz), "deg_pct_10_25_50_75_90_99_999": qs.tolist(),
+                      "max": int(deg.max()), "edges_in_rows_gt_thr": float(deg[deg > thr].sum() / deg.sum()),
+                      "rows_deg_le_4": float((deg <= 4).mean()),
+                      "edges_in_rows_deg_le_16": float(deg[deg <= 16].sum() / deg.sum())}), flush=True)
+    timer = bench.Timer(True)
+    X = torch.rand((hg.n_rows, F), device="cuda") * 2 - 1
+    Y = torch.empty_like(X)
+    dg = ops.DeviceGraph.from_host(hg)
+    t = timer(lambda: ops.spmm(dg, X, out=Y), 10)
+    tc = bench.gather_ceiling(dg.col, X, timer)
+    print(json.dumps({"spmm_ms": t * 1e3, "split_rows": dg.split_rows,
+                      "gather_ms": None if tc is None else tc * 1e3}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
