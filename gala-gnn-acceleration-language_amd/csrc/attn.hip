@@ -9,9 +9,12 @@
 // are a broadcast product into an [N, H, D] temporary plus a reduction (forward) and two
 // more [N, F] passes (backward); here each is one pass over the rows.
 //
-// Forward layout: one thread per (row, head), threads of a wave walking consecutive
-// (row, head) pairs, so a wave reads 64 consecutive D-float head slices (contiguous rows)
-// with VEC-wide loads; the dot is a sequential fma chain over d (deterministic).
+// Forward layout: HW = D / VEC lanes per (row, head) pair (a power of two up to 64), each
+// lane one VEC-wide slice, so a wave reads 64 consecutive vectors (contiguous rows);
+// the pair's dot is each lane's fma chain over its slice, then an xor butterfly over the
+// HW lanes (deterministic).  Other head widths: one thread per pair, a sequential chain.
+// Backward: one thread per VEC-wide vector of dX, consecutive threads on consecutive
+// vectors (full-line stores).
 #include "gala_internal.h"
 
 namespace gala {
@@ -24,6 +27,26 @@ template <>
 struct AVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
 template <>
 struct AVec<4> { typedef float T __attribute__((ext_vector_type(4))); };
+
+template <int VEC, int HW>
+__global__ __launch_bounds__(kBlock) void k_head_attn_group(int64_t n_rows, int32_t H, int32_t D, const float *X,
+                                                            int64_t ldx, const float *w, const float *b, float *out) {
+    typedef typename AVec<VEC>::T V;
+    const int64_t pair = ((int64_t)blockIdx.x * kBlock + threadIdx.x) / HW;
+    const int gl = threadIdx.x & (HW - 1);
+    if (pair >= n_rows * H) return;  // whole groups leave together
+    const int64_t r = pair / H;
+    const int h = (int)(pair - r * H);
+    const int64_t c = (int64_t)h * D + gl * VEC;
+    const V x = *reinterpret_cast<const V *>(X + r * ldx + c);
+    const V v = *reinterpret_cast<const V *>(w + c);
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+        acc = fmaf(reinterpret_cast<const float *>(&x)[i], reinterpret_cast<const float *>(&v)[i], acc);
+    acc = group_sum<HW>(acc);
+    if (gl == 0) out[pair] = b ? __fadd_rn(acc, b[h]) : acc;
+}
 
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void k_head_attn(int64_t n_rows, int32_t H, int32_t D, const float *X,
@@ -46,29 +69,28 @@ __global__ __launch_bounds__(kBlock) void k_head_attn(int64_t n_rows, int32_t H,
     out[t] = b ? __fadd_rn(acc, b[h]) : acc;
 }
 
-// dX[r, c] (+)= g[r, c / D] * w[c]: grid-stride over (row, vector) pairs
+// dX[r, c] (+)= g[r, c / D] * w[c], one thread per vector
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void k_head_attn_bwd(int64_t n_rows, int32_t F, int32_t H, int32_t D,
                                                           const float *g, const float *w, float *dX,
                                                           int64_t lddx, int32_t accumulate) {
     typedef typename AVec<VEC>::T V;
     const int32_t L = F / VEC;
-    const int64_t total = n_rows * L;
-    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kBlock) {
-        const int64_t r = t / L;
-        const int32_t c = (int32_t)(t - r * L) * VEC;
-        const float gv = g[r * H + c / D];
-        const V wv = *reinterpret_cast<const V *>(w + c);
-        float *p = dX + r * lddx + c;
-        V o;
-        if (accumulate) o = *reinterpret_cast<const V *>(p);
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= n_rows * L) return;
+    const int64_t r = t / L;
+    const int32_t c = (int32_t)(t - r * L) * VEC;
+    const float gv = g[r * H + c / D];
+    const V wv = *reinterpret_cast<const V *>(w + c);
+    float *p = dX + r * lddx + c;
+    V o;
+    if (accumulate) o = *reinterpret_cast<const V *>(p);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            const float m = __fmul_rn(gv, reinterpret_cast<const float *>(&wv)[i]);
-            reinterpret_cast<float *>(&o)[i] = accumulate ? __fadd_rn(reinterpret_cast<float *>(&o)[i], m) : m;
-        }
-        *reinterpret_cast<V *>(p) = o;
+    for (int i = 0; i < VEC; ++i) {
+        const float m = __fmul_rn(gv, reinterpret_cast<const float *>(&wv)[i]);
+        reinterpret_cast<float *>(&o)[i] = accumulate ? __fadd_rn(reinterpret_cast<float *>(&o)[i], m) : m;
     }
+    *reinterpret_cast<V *>(p) = o;
 }
 
 static int attn_vec(int32_t D, std::initializer_list<int64_t> lds, std::initializer_list<const void *> ptrs) {
@@ -92,8 +114,29 @@ extern "C" int gala_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, cons
     const int32_t D = F / heads;
     const int vec = attn_vec(D, {ldx}, {X, w});
     const int64_t total = n_rows * heads;
-    const unsigned blocks = (unsigned)((total + kBlock - 1) / kBlock);
     hipStream_t hs = (hipStream_t)stream;
+    const int hw = D / vec;
+    if (hw <= 64 && (hw & (hw - 1)) == 0) {  // lanes per head: a power of two
+        const unsigned gb = (unsigned)((total * hw + kBlock - 1) / kBlock);
+#define GALA_ATTN_GROUP(V, W) hipLaunchKernelGGL((k_head_attn_group<V, W>), dim3(gb), dim3(kBlock), 0, hs, n_rows, heads, D, X, ldx, w, b, out)
+#define GALA_ATTN_HW(V)                                      \
+        switch (hw) {                                        \
+            case 1: GALA_ATTN_GROUP(V, 1); break;            \
+            case 2: GALA_ATTN_GROUP(V, 2); break;            \
+            case 4: GALA_ATTN_GROUP(V, 4); break;            \
+            case 8: GALA_ATTN_GROUP(V, 8); break;            \
+            case 16: GALA_ATTN_GROUP(V, 16); break;          \
+            case 32: GALA_ATTN_GROUP(V, 32); break;          \
+            default: GALA_ATTN_GROUP(V, 64); break;          \
+        }
+        if (vec == 4) { GALA_ATTN_HW(4) }
+        else if (vec == 2) { GALA_ATTN_HW(2) }
+        else { GALA_ATTN_HW(1) }
+#undef GALA_ATTN_HW
+#undef GALA_ATTN_GROUP
+        return launch_status();
+    }
+    const unsigned blocks = (unsigned)((total + kBlock - 1) / kBlock);
     if (vec == 4) hipLaunchKernelGGL(k_head_attn<4>, dim3(blocks), dim3(kBlock), 0, hs, n_rows, heads, D, X, ldx, w, b, out);
     else if (vec == 2) hipLaunchKernelGGL(k_head_attn<2>, dim3(blocks), dim3(kBlock), 0, hs, n_rows, heads, D, X, ldx, w, b, out);
     else hipLaunchKernelGGL(k_head_attn<1>, dim3(blocks), dim3(kBlock), 0, hs, n_rows, heads, D, X, ldx, w, b, out);
@@ -110,8 +153,7 @@ extern "C" int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, 
     const int32_t D = F / heads;
     const int vec = attn_vec(D, {lddx}, {w, dX});
     const int64_t total = n_rows * (F / vec);
-    int64_t blocks = (total + kBlock - 1) / kBlock;
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    const int64_t blocks = (total + kBlock - 1) / kBlock;
     hipStream_t hs = (hipStream_t)stream;
     if (vec == 4) hipLaunchKernelGGL(k_head_attn_bwd<4>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, F, heads, D, g, w, dX, lddx, accumulate);
     else if (vec == 2) hipLaunchKernelGGL(k_head_attn_bwd<2>, dim3((unsigned)blocks), dim3(kBlock), 0, hs, n_rows, F, heads, D, g, w, dX, lddx, accumulate);

@@ -724,7 +724,7 @@ extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, 
                                           const float *wR, const float *bR, const float *X,
                                           int64_t ldx, int32_t F, int32_t heads, float slope, float *Y,
                                           int64_t ldy, float *q_out, float *Ym, int64_t ldym, float *sma,
-                                          float *aR_out, void *) {
+                                          float *aR_out, float *p_out, void *) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldym < F) return GALA_ERR_INVALID_ARG;
@@ -756,6 +756,7 @@ extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, 
                         const bool pos = t > 0.0f;
                         const float pe = ref_exp(pos ? t : t * slope);
                         const float mp = pos ? pe : pe * slope;
+                        if (p_out) p_out[e * H + h] = pe;
                         sum = sum + pe;
                         sm = sm + mp;
                         const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
@@ -780,7 +781,7 @@ extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, 
 // REF backward from the row statistics: dX as gala_cpu_gat_bwd_fused_f32, d_aL from
 // <dY, Y> and <dY, Ym>
 extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                          const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                                          const float *pe, const float *dY, int64_t lddy, int32_t F, int32_t heads,
                                           float slope, const float *q, const float *Y, int64_t ldy,
                                           const float *Ym, int64_t ldym, const float *sma, float *dX,
                                           int64_t lddx, float *d_aL, void *) {
@@ -789,7 +790,7 @@ extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, 
     if (heads < 1 || F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F)
         return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
-    if (!aL || !aR || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
+    if (!aL || (!aR && !pe) || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
     if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
     const int32_t H = heads, D = F / H, S = A->n_seg;
     const float eps = (float)S * 1e-12f;
@@ -803,9 +804,14 @@ extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, 
             for (int64_t e = e0; e < e1; ++e) {
                 const float *yr = dY + (int64_t)A->col[e] * lddy;
                 for (int32_t h = 0; h < H; ++h) {
-                    float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
-                    z = z > 0.0f ? z : z * slope;
-                    const float w = ref_exp(z) * q[r * H + h];
+                    float w;
+                    if (pe) {
+                        w = pe[e * H + h] * q[r * H + h];
+                    } else {
+                        float z = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                        z = z > 0.0f ? z : z * slope;
+                        w = ref_exp(z) * q[r * H + h];
+                    }
                     for (int32_t f = h * D; f < (h + 1) * D; ++f) out[f] = fmaf(w, yr[f], out[f]);
                 }
             }

@@ -790,7 +790,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
-    if (stats && (mode != GALA_SOFTMAX_REF || partial || alpha_out || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
+    if (stats && (mode != GALA_SOFTMAX_REF || partial || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
     if (stats && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // square pattern
     if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
@@ -854,11 +854,11 @@ extern "C" int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, cons
                                       const float *wR, const float *bR, const float *X, int64_t ldx,
                                       int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,
                                       float *q_out, float *Ym, int64_t ldym, float *sma, float *aR_out,
-                                      void *stream) {
+                                      float *p_out, void *stream) {
     if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     if (!Ym && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
-                        GALA_SOFTMAX_REF, Y, ldy, nullptr, q_out, stream, Ym, ldym, sma, aR_out);
+                        GALA_SOFTMAX_REF, Y, ldy, p_out, q_out, stream, Ym, ldym, sma, aR_out);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

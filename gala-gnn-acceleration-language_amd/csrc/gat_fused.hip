@@ -49,11 +49,14 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
         V x[U][CH], yv[U][CH];
         load_batch_cols<G, U>(p, e0, n, j0, c);
         float ar[NK];
+        // ST with the forward's p (d.alpha): alpha = fl(p * q) from the edge-ordered p,
+        // no aR[col] gather
+        const bool from_p = ST && d.alpha != nullptr;
         if (!RC) {
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
                 const int32_t j = (j0 + kl + i * UH < n) ? j0 + kl + i * UH : n - 1;
-                ar[i] = d.aR[(int64_t)p.col[e0 + j] * H + hh];
+                ar[i] = from_p ? d.alpha[(e0 + j) * H + hh] : d.aR[(int64_t)p.col[e0 + j] * H + hh];
             }
         }
 #pragma unroll
@@ -83,7 +86,7 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
             const float t = __fadd_rn(gl_.al, ar[i]);
             pos[i] = t > 0.0f;
             const float z = pos[i] ? t : __fmul_rn(t, d.slope);
-            a[i] = __fmul_rn(ref_exp(z), gl_.qr);
+            a[i] = __fmul_rn(from_p ? ar[i] : ref_exp(z), gl_.qr);
         }
         static_for<0, U>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
@@ -345,8 +348,8 @@ static int fused_dispatch(FusedArgs &a, int F, int heads, int vec, bool rc) {
     return launch_status();
 }
 
-extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *dY,
-                                      int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
+extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                                      const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
                                       const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
                                       const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
     FusedArgs a{};
@@ -354,7 +357,7 @@ extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, cons
     if (st) return st;
     if (F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
-    if (!aL || !aR || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
+    if (!aL || (!aR && !pe) || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
     if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // dY[col]: a square pattern
     const int D = F / heads;
     auto ok = [&](int v) {
@@ -368,7 +371,7 @@ extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, cons
     while (vec > 1 && !ok(vec)) vec >>= 1;
     a.d.aL = aL, a.d.aR = aR, a.d.F = F, a.d.slope = slope;
     a.d.dY = dY, a.d.lddy = lddy, a.d.q = q, a.d.dX = dX, a.d.lddx = lddx, a.d.d_aL = d_aL;
-    a.d.ys = Y, a.d.ldy = ldy, a.d.yms = Ym, a.d.ldym = ldym, a.d.smas = sma;
+    a.d.ys = Y, a.d.ldy = ldy, a.d.yms = Ym, a.d.ldym = ldym, a.d.smas = sma, a.d.alpha = pe;
     a.hs = (hipStream_t)stream;
     a.split = hub_split(A, pad_to(F, 4), &a.sp);  // hub rows: dX[F] chunk partials
     return fused_dispatch(a, F, heads, vec, false);

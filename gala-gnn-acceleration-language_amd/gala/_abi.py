@@ -97,9 +97,9 @@ SIGNATURES = {
     "gala_gat_bwd_fused_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _P, _I64, _I32, _I32, _F, _P, _P,
                                               _I64, _P, _P]),
     "gala_gat_fwd_stats_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P, _I64, _P, _P,
-                                              _I64, _P, _P, _P]),
-    "gala_gat_bwd_stats_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _I64, _I32, _I32, _F, _P, _P, _I64, _P, _I64,
-                                              _P, _P, _I64, _P, _P]),
+                                              _I64, _P, _P, _P, _P]),
+    "gala_gat_bwd_stats_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P, _P, _I64, _P,
+                                              _I64, _P, _P, _I64, _P, _P]),
     "gala_head_attn_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _P, _P, _P]),
     "gala_head_attn_bwd_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _P, _P, _I64, _I32, _P]),
     "gala_edge_permute_f32": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P]),

@@ -340,29 +340,37 @@ def gat_bwd_fused(g: DeviceGraph, aL, X, dY, q, aR=None, wR=None, bR=None, heads
     return dX, d_aL
 
 
-def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, want_aR=False):
-    """gala_gat_fwd_stats_f32 (REF, square pattern): returns (Y, q, Ym, sma[, aR_out]) with
+def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, want_aR=False,
+                  want_p=False):
+    """gala_gat_fwd_stats_f32 (REF, square pattern): returns (Y, q, Ym, sma[, aR_out][, p]) with
     Ym[r] = sum_e m_e alpha_e X[col_e], sma[r, h] = sum_e m_e alpha_e (m_e the LeakyReLU
-    factor); aR_out (aR recomputed from wR, bR) the rows' own source logits."""
+    factor); aR_out (aR recomputed from wR, bR) the rows' own source logits; p the edges'
+    exp terms."""
     F = X.shape[1]
     Y = _rows_like(X, g.n_rows)
     Ym = _rows_like(X, g.n_rows)
     q = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
     sma = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
     aR_out = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if want_aR else None
+    p = torch.empty(g.nnz * heads, device=X.device, dtype=torch.float32) if want_p else None
     _abi.call("gala_gat_fwd_stats_f32", g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR), _dp(wR),
               _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(Y), Y.stride(0), _dp(q), _dp(Ym), Ym.stride(0),
-              _dp(sma), _dp(aR_out), _stream())
-    return (Y, q, Ym, sma, aR_out) if want_aR else (Y, q, Ym, sma)
+              _dp(sma), _dp(aR_out), _dp(p), _stream())
+    out = (Y, q, Ym, sma)
+    if want_aR:
+        out += (aR_out,)
+    if want_p:
+        out += (p,)
+    return out
 
 
-def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2):
+def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None):
     """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
-    dY[col] only."""
+    dY[col] only (alpha from aR, or from the forward's p when given)."""
     F = dY.shape[1]
     dX = _rows_like(dY, g.n_rows)
     d_aL = torch.empty(g.n_rows * heads, device=dY.device, dtype=torch.float32)
-    _abi.call("gala_gat_bwd_stats_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(dY), dY.stride(0), F,
+    _abi.call("gala_gat_bwd_stats_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(p), _dp(dY), dY.stride(0), F,
               heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0), _dp(sma), _dp(dX), dX.stride(0),
               _dp(d_aL), _stream())
     return dX, d_aL

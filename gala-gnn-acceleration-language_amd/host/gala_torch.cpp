@@ -859,7 +859,13 @@ bool rowstats_enabled() {
 // What the row-statistics forward leaves for its backward.
 struct GatStats {
     torch::Tensor Y, q, Ym, sma, aR;  // aR: the given logits, or the recomputed ones (RC)
+    torch::Tensor p;                  // narrow rows: the edges' exp terms (else empty)
 };
+
+// Narrow layers keep the forward's per-edge exp terms p (4 B per edge and head, written and
+// read in edge order) so the backward skips its aR[col] gather, which costs a whole cache
+// line per edge next to a 1-2 line row gather; wide rows hide that read.
+bool keep_edge_terms(int64_t F) { return F <= 64; }
 
 // One launch of gala_gat_fwd_stats_f32 on slot 2li; false when the kernel does not take
 // this shape (the caller then takes the plain recomputed path).
@@ -873,15 +879,17 @@ bool gat_forward_stats(const Slot &s, const torch::Tensor &l, const torch::Tenso
     auto Y = rows_like(x, nrows), Ym = rows_like(x, nrows);
     auto q = torch::empty({nrows * heads}, fopts(x)), sma = torch::empty({nrows * heads}, fopts(x));
     torch::Tensor aR = r.defined() ? r : torch::empty({nrows * heads}, fopts(x));
+    torch::Tensor p = keep_edge_terms(F) ? torch::empty({s.cols.numel() * heads}, fopts(x)) : torch::Tensor();
     const int st = be(s.off).gat_fwd_stats(
         &cv.c, l.data_ptr<float>(), r.defined() ? r.data_ptr<float>() : nullptr,
         r.defined() ? nullptr : wR.data_ptr<float>(), (!r.defined() && bR.defined()) ? bR.data_ptr<float>() : nullptr,
         x.data_ptr<float>(), x.stride(0), (int32_t)F, heads, (float)slope, Y.data_ptr<float>(), Y.stride(0),
         q.data_ptr<float>(), Ym.data_ptr<float>(), Ym.stride(0), sma.data_ptr<float>(),
-        r.defined() ? nullptr : aR.data_ptr<float>(), stream_of(s.off));
+        r.defined() ? nullptr : aR.data_ptr<float>(), p.defined() ? p.data_ptr<float>() : nullptr,
+        stream_of(s.off));
     if (st == GALA_ERR_UNSUPPORTED) return false;
     check(st, "gala_gat_fwd_stats_f32");
-    o = {Y, q, Ym, sma, aR};
+    o = {Y, q, Ym, sma, aR, p.defined() ? p : torch::empty({0}, fopts(x))};
     return true;
 }
 
@@ -899,6 +907,7 @@ bool gat_backward_stats(const torch::Tensor &l, const GatStats &o, const torch::
     auto dX = rows_like(dY, nrows);
     auto daL = torch::empty_like(l);
     const int st = be(fw.off).gat_bwd_stats(&cf.c, l.data_ptr<float>(), o.aR.data_ptr<float>(),
+                                            o.p.numel() > 0 ? o.p.data_ptr<float>() : nullptr,
                                             dY.data_ptr<float>(), dY.stride(0), (int32_t)F, heads, (float)slope,
                                             o.q.data_ptr<float>(), o.Y.data_ptr<float>(), o.Y.stride(0),
                                             o.Ym.data_ptr<float>(), o.Ym.stride(0), o.sma.data_ptr<float>(),
@@ -940,7 +949,7 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         const bool grad = ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2);
         if (recompute && grad && rowstats_enabled() && gat_forward_stats(s, l, r, x, {}, {}, heads, slope, o)) {
             ctx->saved_data["stats"] = true;
-            ctx->save_for_backward({l, r, x, o.q, o.Y, o.Ym, o.sma});
+            ctx->save_for_backward({l, r, x, o.q, o.Y, o.Ym, o.sma, o.p});
             return o.Y;
         }
         auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
@@ -959,7 +968,7 @@ struct GatAggregate : public torch::autograd::Function<GatAggregate> {
         auto l = sv[0], r = sv[1], x = sv[2];
         GatGrads g;
         if (ctx->saved_data.count("stats")) {
-            const GatStats o{sv[4], sv[3], sv[5], sv[6], r};
+            const GatStats o{sv[4], sv[3], sv[5], sv[6], r, sv[7]};
             if (!gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g) &&
                 !gat_backward_recompute(l, r, x, o.q, grad_outputs[0], li, slope, heads, {}, {}, g)) {
                 auto q = o.q.clone();  // rebuild the factored p (the forward writes the same q)
@@ -1027,7 +1036,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         if (recompute && grad && rowstats_enabled() && gat_forward_stats(s, l, {}, x, w, b, heads, slope, o)) {
             // o.aR: the recomputed source logits, read by the backward
             ctx->saved_data["stats"] = true;
-            ctx->save_for_backward({l, x, w, b_saved, o.aR, o.q, o.Y, o.Ym, o.sma});
+            ctx->save_for_backward({l, x, w, b_saved, o.aR, o.q, o.Y, o.Ym, o.sma, o.p});
             return o.Y;
         }
         auto alpha = recompute ? torch::empty({0}, fopts(x)) : torch::empty({s.cols.numel() * heads}, fopts(x));
@@ -1051,7 +1060,7 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         GatGrads g;
         bool done = false;
         if (stats) {
-            const GatStats o{sv[6], q, sv[7], sv[8], sv[4]};
+            const GatStats o{sv[6], q, sv[7], sv[8], sv[4], sv[9]};
             done = gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g);
             alpha = torch::empty({0}, fopts(x));  // otherwise: the recomputed path below
         }

@@ -84,9 +84,9 @@ int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float
                                const float *wR, const float *bR, const float *X, int64_t ldx,
                                int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,
                                float *q_out, float *Ym, int64_t ldym, float *sma, float *aR_out,
-                               void *stream);
+                               float *p_out, void *stream);
 int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                               const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                               const float *p, const float *dY, int64_t lddy, int32_t F, int32_t heads,
                                float slope, const float *q, const float *Y, int64_t ldy,
                                const float *Ym, int64_t ldym, const float *sma, float *dX,
                                int64_t lddx, float *d_aL, void *stream);

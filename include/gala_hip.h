@@ -352,27 +352,35 @@ int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR
  * gala_gat_fwd_stats_f32: Y, q_out as gala_gat_fwd_ex_f32 in REF mode with alpha_out NULL,
  * plus Ym, sma.  aR or (aR NULL) its per-head recompute from X (wR, bR); aR_out (nullable)
  * then receives every row's recomputed source logit, bit-identical to the per-edge
- * recompute, for the backward.  Several heads need D/VEC a power of two (else
+ * recompute, for the backward.  p_out (nullable, [nnz, heads]) receives the edges' exp
+ * terms p = min(exp(s), 1e12), as gala_gat_fwd_ex_f32's factored output; the backward
+ * then reads them in edge order instead of gathering aR[col] (cheaper for narrow rows,
+ * where that 4-B random read costs a cache line per edge next to a 1-2 line row gather).
+ * Several heads need D/VEC a power of two (else
  * GALA_ERR_UNSUPPORTED; the caller then takes gala_gat_fwd_ex_f32 + gala_gat_bwd_fused_f32).
  * gala_gat_bwd_stats_f32: dX[r] = sum_e alpha_e dY[c_e] (alpha = fl(min(exp(LeakyReLU(
- * aL + aR)), 1e12) * q), aR explicit) and d_aL[r,h] = (<dY,Ym>_h - (S*eps + <dY,Y>_h) *
+ * aL + aR)), 1e12) * q) from aR, or fl(p * q) when the forward's p is given (aR may then be
+ * NULL)) and d_aL[r,h] = (<dY,Ym>_h - (S*eps + <dY,Y>_h) *
  * sma[r,h]) + S*eps (= d_aR in REF mode), eps = 1e-12.
  */
 int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                            const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                            float slope, float *Y, int64_t ldy, float *q_out, float *Ym,
-                           int64_t ldym, float *sma, float *aR_out, void *stream);
-int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *dY,
-                           int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
-                           const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
-                           const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream);
+                           int64_t ldym, float *sma, float *aR_out, float *p_out, void *stream);
+int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *p,
+                           const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope,
+                           const float *q, const float *Y, int64_t ldy, const float *Ym,
+                           int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
+                           void *stream);
 
 /*
  * Per-head attention logits of the multi-head GAT layer (galac gat_heads: the DSL's
  * attnL / attnR = dsl.nn.ffn(res, out=1) applied per head, a torch::nn::Linear in the
  * reference, common.h:1188-1242):
  *   out[r*heads + h] = <X[r, hD:(h+1)D], w[hD:(h+1)D]> + b[h]     (b nullable; D = F/heads)
- * summed sequentially over d (fma).  gala_head_attn_bwd_f32 is its input gradient:
+ * (an fma chain over each lane's vector, then a fixed butterfly over the head's lanes:
+ * deterministic, within fp32 rounding of the sequential sum).  gala_head_attn_bwd_f32 is
+ * its input gradient:
  *   dX[r, hD+d] = g[r*heads + h] * w[hD+d]      (accumulate != 0: dX += ..., one rounding
  *                                                each for the product and the sum)
  * The weight / bias gradients are gala_dense_grad_f32 with M = heads (the block diagonal

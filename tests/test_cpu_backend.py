@@ -223,17 +223,23 @@ def test_gat_row_stats(graph, F, heads, rc):
     Y, Ym = np.empty((n, F), np.float32), np.empty((n, F), np.float32)
     q, sma = np.empty(n * heads, np.float32), np.empty(n * heads, np.float32)
     aR_out = np.empty(n * heads, np.float32) if rc else None
+    pe = np.empty(graph.nnz * heads, np.float32)
     _abi.call_cpu("gala_gat_fwd_stats_f32", HostCsr(graph).ref, P(aL), None if rc else P(aR), P(wR), P(bR), P(X),
-                  F, F, heads, 0.2, P(Y), F, P(q), P(Ym), F, P(sma), P(aR_out), None)
+                  F, F, heads, 0.2, P(Y), F, P(q), P(Ym), F, P(sma), P(aR_out), P(pe), None)
     np.testing.assert_allclose(Y, Y_ref, **TOL)
     aRx = aR_out if rc else aR
     if rc:
         np.testing.assert_allclose(aR_out.reshape(n, heads), aR, rtol=1e-5, atol=1e-5)
     _, daL_ref = orc.gat_bwd(og, aL, aR, X, dY, al_ref, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
     dX, daL = np.empty((n, F), np.float32), np.empty(n * heads, np.float32)
-    _abi.call_cpu("gala_gat_bwd_stats_f32", HostCsr(graph).ref, P(aL), P(aRx), P(dY), F, F, heads, 0.2, P(q), P(Y),
-                  F, P(Ym), F, P(sma), P(dX), F, P(daL), None)
+    _abi.call_cpu("gala_gat_bwd_stats_f32", HostCsr(graph).ref, P(aL), P(aRx), None, P(dY), F, F, heads, 0.2, P(q),
+                  P(Y), F, P(Ym), F, P(sma), P(dX), F, P(daL), None)
     np.testing.assert_allclose(daL, daL_ref, **TOL)
+    # alpha from the forward's p instead of aR: the same dX
+    dXp = np.empty((n, F), np.float32)
+    _abi.call_cpu("gala_gat_bwd_stats_f32", HostCsr(graph).ref, P(aL), None, P(pe), P(dY), F, F, heads, 0.2, P(q),
+                  P(Y), F, P(Ym), F, P(sma), P(dXp), F, P(daL), None)
+    assert np.array_equal(dXp, dX)
     gw = orc.Graph(og.n_rows, og.n_cols, og.rowptr, og.col, al_ref, og.n_seg, og.bounds, heads)
     np.testing.assert_allclose(dX, orc.spmm(gw, dY), **TOL)
 

@@ -71,7 +71,11 @@ def main():
         rec["gat_fwd_stats_recompute"] = timeit(lambda: ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H,
                                                                          want_aR=True))
         rec["gat_bwd_stats"] = timeit(lambda: ops.gat_bwd_stats(dg, aL, aR, dY, qs, Ys, Ym, sma, heads=H))
-        del Ys, qs, Ym, sma, aRo
+        pe = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_p=True)[-1]
+        rec["gat_fwd_stats_recompute_p"] = timeit(lambda: ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H,
+                                                                           want_aR=True, want_p=True))
+        rec["gat_bwd_stats_p"] = timeit(lambda: ops.gat_bwd_stats(dg, aL, None, dY, qs, Ys, Ym, sma, heads=H, p=pe))
+        del Ys, qs, Ym, sma, aRo, pe
         for k, v in rec.items():
             line = {"op": k, "heads": H, "F": F, "ms": v, "N": N, "E": E}
             out.append(line)
