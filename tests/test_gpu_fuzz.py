@@ -8,7 +8,8 @@ tiling, then checks the HIP path against the oracle:
 * bit-exact: degree, SpMM without hub chunks, row-scale / row-broadcast;
 * reordered sums (hub chunks): within the worst-case fp32 summation bound of the row,
   |err| <= (deg + 1) 2^-24 sum|a x| + 1e-6 per entry;
-* TOL (1e-4 abs + rel): SDDMM, edge softmax fwd / bwd, fused GAT forward / backward.
+* TOL (1e-4 abs + rel): SDDMM, edge softmax fwd / bwd, fused GAT forward / backward, the
+  REF row-statistics backward's d_aL (its Y / q / dX bit-equal to the fused path's).
 """
 import os
 
@@ -132,6 +133,29 @@ def test_random_case(seed):
         np.testing.assert_allclose(_host(daL), daL_ref, **TOL)
         if mode == _abi.GALA_SOFTMAX_FIXED:
             np.testing.assert_allclose(_host(dz), dz_ref, **TOL)
+    # REF row statistics (the graphs are square): Y / q bit-equal to the q-only forward, dX to
+    # the fused backward, the same dX from the parked p, d_aL within TOL of the oracle chain
+    Ys, q, Ym, sma, pe = ops.gat_fwd_stats(dg, _dev(aL), Xd, aR=_dev(aR), heads=heads, want_p=True)
+    Y0, q0 = ops.gat_fwd_ex(dg, _dev(aL), Xd, aR=_dev(aR), heads=heads, factored="q")
+    assert torch.equal(Ys, Y0) and torch.equal(q, q0)
+    dX, daL = ops.gat_bwd_stats(dg, _dev(aL), _dev(aR), Ad, q, Ys, Ym, sma, heads=heads)
+    dX0, _ = ops.gat_bwd_fused(dg, _dev(aL), Xd, Ad, q, aR=_dev(aR), heads=heads)
+    assert torch.equal(dX, dX0)
+    dXp, daLp = ops.gat_bwd_stats(dg, _dev(aL), None, Ad, q, Ys, Ym, sma, heads=heads, p=pe)
+    assert torch.equal(dXp, dX) and torch.equal(daLp, daL)
+    _, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    _, daL_ref = orc.gat_bwd(og, aL, aR, X, A, al_ref, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)
+    np.testing.assert_allclose(_host(daL), daL_ref, **TOL)
+    gw = orc.Graph(og.n_rows, og.n_cols, og.rowptr, og.col, al_ref, og.n_seg, og.bounds, heads)
+    np.testing.assert_allclose(_host(dX), orc.spmm(gw, A), **TOL)
+    # per-head attention logits and their input gradient
+    wA = rng.uniform(-1, 1, F).astype(np.float32)
+    bA = rng.uniform(-1, 1, heads).astype(np.float32)
+    ref = (X.astype(np.float64).reshape(-1, heads, F // heads) * wA.reshape(1, heads, -1)).sum(2) + bA
+    np.testing.assert_allclose(_host(ops.head_attn(Xd, _dev(wA), _dev(bA), heads=heads)), ref, rtol=1e-5, atol=1e-5)
+    gA = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    np.testing.assert_array_equal(_host(ops.head_attn_bwd(_dev(gA), _dev(wA), heads=heads)),
+                                  np.repeat(gA, F // heads, axis=1) * wA[None, :])
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("GALA_FUZZ_CASES", "96")) // 2))
