@@ -15,7 +15,9 @@ hot path, and are not part of the step.
 
 The graph: ogbn-products shape (N=2,449,029 vertices, E=126,167,309 stored edges incl.
 self loops), uniform random symmetric edges (seed 42), X ~ U[-1,1).  At N = 1 an R-MAT
-graph of the same shape is timed as a second family (field "rmat").
+graph of the same shape is timed as a second family (field "rmat"), and the SDDMM +
+edge-softmax half of the path as one 8-head GAT layer of config 3 on the same graph,
+forward + backward (field "gat", its own roofline and gather ceiling).
 
 N > 1 GPUs: STRONG scaling of that one graph (one process per GPU, RCCL over xGMI).
 Every rank partitions the same graph (gala/dist.py, gala/vertex_cut.py) and the bench
@@ -461,9 +463,72 @@ def run_single(args, dev, be, timer, sync):
             out["cpu_baseline"] = cpu_baseline(hg, F)
         except Exception as e:  # the baseline is reported, never the target
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
-    del agg, X, dY, bufs
+    del X, dY, bufs
+    if be.name == "hip" and not args.no_gat:
+        out["gat"] = gat_layer(args, agg.g, hg, dev, timer, sync)
+    del agg
     if not args.no_rmat:
         out["rmat"] = rmat_family(args, dev, be, timer, sync)
+    return out
+
+
+GAT_HEADS, GAT_HEAD_F = 8, 32   # BASELINE configs[2]: ogbn-products GAT, 8 heads x 32 (galac gat_heads(8))
+
+
+def gat_layer(args, dg, hg, dev, timer, sync):
+    """SDDMM + edge-softmax + aggregation throughput on the same graph: one 8-head GAT layer
+    of config 3 (bench/dsl/gat_products_h8.txt), forward + backward, as the generated
+    program runs it (REF undirected layer, source logit recomputed from X):
+        forward   gala_gat_fwd_stats_f32  per edge: logit aL[r] + <X[c], wR_h> + bR_h,
+                  LeakyReLU, exp, alpha * X[c] into Y and Ym; per row q = 1/sum, sum m*alpha
+        backward  gala_gat_bwd_stats_f32  per edge: alpha from aR[c], dX[r] += alpha*dY[c];
+                  per row d_aL from <dY[r], Y[r]>, <dY[r], Ym[r]>
+    (the edge chains of cuda.h:505-562,679-845 and common.h:622-894 fused).  value counts
+    2*E edges per step (the forward's and the backward's pass over every edge)."""
+    import torch
+    from gala import ops
+    H, F = GAT_HEADS, GAT_HEADS * GAT_HEAD_F
+    N, E = hg.n_rows, hg.nnz
+    gen = torch.Generator(device=dev).manual_seed(4321)
+    X = torch.rand((N, F), device=dev, generator=gen) * 2 - 1
+    dY = torch.rand((N, F), device=dev, generator=gen) * 2 - 1
+    aL = torch.rand((N, H), device=dev, generator=gen) - 0.5
+    wR = (torch.rand(F, device=dev, generator=gen) - 0.5) * 0.2
+    bR = torch.zeros(H, device=dev)
+    st = {}
+
+    def fwd():
+        st["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+
+    def bwd():
+        Y, q, Ym, sma, aRo = st["f"]
+        st["b"] = ops.gat_bwd_stats(dg, aL, aRo, dY, q, Y, Ym, sma, heads=H)
+
+    def step():
+        fwd()
+        bwd()
+    steps = max(args.steps // 2, 2)
+    t_step = timed_steps(step, steps, 2, sync, lambda: None, lambda x: x)
+    t_fwd = timer(fwd, 5)
+    t_bwd = timer(bwd, 5)
+    # forward stats kernel, SURVEY §8(d) model (X read once, no per-edge outputs):
+    # rowptr + col + X + Y + Ym + aL, q, sum m*alpha, aR_out per row and head + wR
+    alg = 4 * (N + 1) + 4 * E + 3 * 4 * N * F + 4 * 4 * N * H + 4 * F
+    out = {"value": 2 * E / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
+           "layer": f"GAT {H} heads x {GAT_HEAD_F} (F={F}), REF softmax, source logit recomputed; forward + backward",
+           "fwd_ms": t_fwd * 1e3, "bwd_ms": t_bwd * 1e3,
+           "roofline": {"bound": "hbm", "achieved": alg / t_fwd / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": alg / t_fwd / HBM_PEAK, "kernel_ms": t_fwd * 1e3, "alg_bytes_per_launch": alg,
+                        "traffic": load_traffic("k_gat_fwd<64, 4, 8, 2, 1, true, 8>"),
+                        "kernel": "gala::k_gat_fwd<64,4,8,2,1,true,8> (gala_gat_fwd_stats_f32, 8 heads, F=256)",
+                        "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json): 126 M "
+                                        "gathered 1-KB X rows; at the measured HBM copy rate"}}
+    t_ceil = gather_ceiling(dg.col, X, timer)
+    if t_ceil:
+        out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
+        out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_fwd
+    del st, X, dY
+    torch.cuda.empty_cache()
     return out
 
 
@@ -512,6 +577,7 @@ def main():
                     help="cpu: the host-CPU backend over gloo (plumbing checks, not a measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rmat", action="store_true")
+    ap.add_argument("--no-gat", action="store_true")
     ap.add_argument("--no-weak", action="store_true")
     args = ap.parse_args()
 
