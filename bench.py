@@ -17,7 +17,8 @@ The graph: ogbn-products shape (N=2,449,029 vertices, E=126,167,309 stored edges
 self loops), uniform random symmetric edges (seed 42), X ~ U[-1,1).  At N = 1 an R-MAT
 graph of the same shape is timed as a second family (field "rmat"), and the SDDMM +
 edge-softmax half of the path as one 8-head GAT layer of config 3 on the same graph,
-forward + backward (field "gat", its own roofline and gather ceiling).
+forward + backward (field "gat", its own roofline and gather ceiling; at N > 1 the same
+layer strong-scaled over the vertex cut).
 
 N > 1 GPUs: STRONG scaling of that one graph (one process per GPU, RCCL over xGMI).
 Every rank partitions the same graph (gala/dist.py, gala/vertex_cut.py) and the bench
@@ -380,8 +381,42 @@ def run_multi(args, rank, world, dev, be, timer, sync):
                          "in the -overlap/-pipe modes."},
     }
     del modes, ref_mode
+    if not args.no_gat:
+        out["gat"] = gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
     if not args.no_weak:
         out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
+    return out
+
+
+def gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max):
+    """The "gat" field at N > 1: the same 8-head GAT layer as at N = 1 (forward + backward,
+    REF, the source logit formed from X), strong-scaled over the one graph with north_star's
+    vertex cut (gala/vertex_cut.py VertexCutGat.forward_train / backward): every rank runs the
+    row-statistics forward and the backward's partial aggregation over the edges whose source
+    it owns, and reduce-scatters the partial rows to their owners."""
+    import torch
+    from gala import vertex_cut as vc
+    H, F = GAT_HEADS, GAT_HEADS * GAT_HEAD_F
+    part = vc.vertex_cut_partition(g, rank, world, 1, bounds)
+    layer = vc.VertexCutGat(part, F, H, be, comm)
+    n = part.n
+    gen = torch.Generator(device=dev).manual_seed(4321 + rank)
+    X = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
+    dY = torch.rand((n, F), device=dev, generator=gen) * 2 - 1
+    aL = torch.rand((n, H), device=dev, generator=gen) - 0.5
+    wR = (torch.rand(F, device=dev, generator=gen) - 0.5) * 0.2
+    bR = torch.zeros(H, device=dev)
+
+    def step():
+        layer.forward_train(aL, be.head_attn(X, wR, bR, H), X)
+        layer.backward(dY)
+    steps = max(args.steps // 2, 2)
+    t_step = timed_steps(step, steps, 2, sync, barrier, reduce_max)
+    out = {"value": 2 * g.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
+           "layer": f"GAT {H} heads x {GAT_HEAD_F} (F={F}), REF softmax; forward + backward",
+           "layout": f"vertex cut x{world}: row-statistics partials reduce-scattered to the row owners",
+           "comm_bytes_per_step_per_rank": part.comm_bytes(2 * F + 2 * H) + part.comm_bytes(F)}
+    del layer, X, dY
     return out
 
 

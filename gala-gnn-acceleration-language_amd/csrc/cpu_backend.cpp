@@ -720,17 +720,18 @@ extern "C" int gala_cpu_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, 
 
 // REF forward with the row statistics (gala_hip.h, gala_gat_fwd_stats_f32): Y and q as
 // cpu_gat_fwd, plus Ym = q * sum m p X and sma = q * sum m p (m the LeakyReLU factor)
-extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                          const float *wR, const float *bR, const float *X,
-                                          int64_t ldx, int32_t F, int32_t heads, float slope, float *Y,
-                                          int64_t ldy, float *q_out, float *Ym, int64_t ldym, float *sma,
-                                          float *aR_out, float *p_out, void *) {
+// partial (vertex cut): every output unnormalised (Y = sum p X, q_out = sum p, Ym = sum m p X,
+// sma = sum m p), for the rows' owners to add first (gala_cpu_gat_fwd_partial_stats_f32)
+static int cpu_gat_fwd_stats(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                             const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                             float slope, float *Y, int64_t ldy, float *q_out, float *Ym, int64_t ldym,
+                             float *sma, float *aR_out, float *p_out, bool partial) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldym < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || !q_out || !Ym || !sma || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
-    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (!partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
     if (aR_out && (aR || !X)) return GALA_ERR_INVALID_ARG;
     std::vector<float> rc;
     if (!aR) {
@@ -766,16 +767,34 @@ extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, 
                         }
                     }
                 }
-                const float q = 1.0f / (sum + (float)S * 1e-12f);
+                const float q = partial ? 1.0f : 1.0f / (sum + (float)S * 1e-12f);
                 for (int32_t f = 0; f < D; ++f) {
-                    Y[r * ldy + h * D + f] = acc[f] * q;
-                    Ym[r * ldym + h * D + f] = accm[f] * q;
+                    Y[r * ldy + h * D + f] = partial ? acc[f] : acc[f] * q;
+                    Ym[r * ldym + h * D + f] = partial ? accm[f] : accm[f] * q;
                 }
-                q_out[r * H + h] = q;
-                sma[r * H + h] = sm * q;
+                q_out[r * H + h] = partial ? sum : q;
+                sma[r * H + h] = partial ? sm : sm * q;
             }
     }
     return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *wR, const float *bR, const float *X,
+                                          int64_t ldx, int32_t F, int32_t heads, float slope, float *Y,
+                                          int64_t ldy, float *q_out, float *Ym, int64_t ldym, float *sma,
+                                          float *aR_out, float *p_out, void *) {
+    return cpu_gat_fwd_stats(A, aL, aR, wR, bR, X, ldx, F, heads, slope, Y, ldy, q_out, Ym, ldym, sma, aR_out,
+                             p_out, false);
+}
+
+extern "C" int gala_cpu_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                                  const float *wR, const float *bR, const float *X,
+                                                  int64_t ldx, int32_t F, int32_t heads, float slope, float *U,
+                                                  int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                                  float *msums, void *) {
+    return cpu_gat_fwd_stats(A, aL, aR, wR, bR, X, ldx, F, heads, slope, U, ldu, sums, Um, ldum, msums, nullptr,
+                             nullptr, true);
 }
 
 // REF backward from the row statistics: dX as gala_cpu_gat_bwd_fused_f32, d_aL from

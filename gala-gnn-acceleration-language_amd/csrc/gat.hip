@@ -790,8 +790,11 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (!aL || (!aR && !wR) || !Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
-    if (stats && (mode != GALA_SOFTMAX_REF || partial || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
-    if (stats && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // square pattern
+    if (stats && (mode != GALA_SOFTMAX_REF || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
+    if (stats && partial && (ar_out || alpha_out)) return GALA_ERR_INVALID_ARG;
+    // square pattern (the backward's dY[col] / aR_out of the row's own X); a vertex cut's
+    // partial forward reads X by column only
+    if (stats && !partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
     if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
@@ -859,6 +862,20 @@ extern "C" int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, cons
     if (!Ym && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
                         GALA_SOFTMAX_REF, Y, ldy, p_out, q_out, stream, Ym, ldym, sma, aR_out);
+}
+
+// The row-statistics forward over one column range of a vertex cut: every output unnormalised
+// (gat_fwd_store with d.partial), so the owners of the rows add the ranks' partials first.
+extern "C" int gala_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                              const float *wR, const float *bR, const float *X,
+                                              int64_t ldx, int32_t F, int32_t heads, float slope, float *U,
+                                              int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                              float *msums, void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if ((!Um || !sums || !msums) && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
+                        GALA_SOFTMAX_REF | GALA_GAT_PARTIAL, U, ldu, nullptr, sums, stream, Um, ldum, msums,
+                        nullptr);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

@@ -45,6 +45,19 @@ class HipBackend:
         """REF GAT forward over one column range, unnormalised (GALA_GAT_PARTIAL)."""
         return self.ops.gat_fwd_partial(g, aL, X, aR=aR, heads=heads, slope=slope, Y=Y, sums=sums)
 
+    def gat_partial_stats(self, g, aL, aR, X, heads, slope, U, sums, Um, msums):
+        """REF row-statistics forward over one column range, unnormalised (vertex cut)."""
+        return self.ops.gat_fwd_partial_stats(g, aL, X, aR=aR, heads=heads, slope=slope, U=U, sums=sums, Um=Um,
+                                              msums=msums)
+
+    def gat_bwd_stats(self, g, aL, aR, dY, q, Y, Ym, sma, heads, slope):
+        """(dX, d_aL) of the REF layer from its row statistics (gala_gat_bwd_stats_f32)."""
+        return self.ops.gat_bwd_stats(g, aL, aR, dY, q, Y, Ym, sma, heads=heads, slope=slope)
+
+    def head_attn(self, X, w, b, heads):
+        """[n, heads] per-head attention logits <X[:, head h], w_h> + b_h (gala_head_attn_f32)."""
+        return self.ops.head_attn(X, w, b, heads=heads)
+
     def empty(self, *shape):
         return torch.empty(shape, device=self.device, dtype=torch.float32)
 
@@ -114,6 +127,27 @@ class CpuBackend:
                       heads, slope, _abi.GALA_SOFTMAX_REF | _abi.GALA_GAT_PARTIAL, _hp(Y), Y.stride(0), None,
                       _hp(sums), None)
         return Y, sums
+
+    def gat_partial_stats(self, g: CpuGraph, aL, aR, X, heads, slope, U, sums, Um, msums):
+        _abi.call_cpu("gala_gat_fwd_partial_stats_f32", g.csr(), _hp(aL), _hp(aR), None, None, _hp(X), X.stride(0),
+                      X.shape[1], heads, slope, _hp(U), U.stride(0), _hp(sums), _hp(Um), Um.stride(0), _hp(msums),
+                      None)
+        return U, sums, Um, msums
+
+    def gat_bwd_stats(self, g: CpuGraph, aL, aR, dY, q, Y, Ym, sma, heads, slope):
+        F = dY.shape[1]
+        dX = torch.empty((g.n_rows, F), dtype=torch.float32)
+        d_aL = torch.empty(g.n_rows * heads, dtype=torch.float32)
+        _abi.call_cpu("gala_gat_bwd_stats_f32", g.csr(), _hp(aL), _hp(aR), None, _hp(dY), dY.stride(0), F, heads,
+                      slope, _hp(q), _hp(Y), Y.stride(0), _hp(Ym), Ym.stride(0), _hp(sma), _hp(dX), dX.stride(0),
+                      _hp(d_aL), None)
+        return dX, d_aL
+
+    def head_attn(self, X, w, b, heads):
+        out = torch.empty((X.shape[0], heads), dtype=torch.float32)
+        _abi.call_cpu("gala_head_attn_f32", X.shape[0], X.shape[1], heads, _hp(X), X.stride(0), _hp(w), _hp(b),
+                      _hp(out), None)
+        return out
 
     def empty(self, *shape):
         return torch.empty(shape, dtype=torch.float32)

@@ -364,6 +364,22 @@ def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slo
     return out
 
 
+def gat_fwd_partial_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, U=None, sums=None,
+                          Um=None, msums=None):
+    """gala_gat_fwd_partial_stats_f32 (vertex cut): the row-statistics forward over one
+    column range, unnormalised -- (U, sums, Um, msums) = (sum p X, sum p, sum m p X, sum m p)
+    per row (and head); U / Um may be strided views (e.g. the two halves of one buffer)."""
+    F = X.shape[1]
+    U = _rows_like(X, g.n_rows) if U is None else U
+    Um = _rows_like(X, g.n_rows) if Um is None else Um
+    sums = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if sums is None else sums
+    msums = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if msums is None else msums
+    _abi.call("gala_gat_fwd_partial_stats_f32", g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR),
+              _dp(wR), _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(U), U.stride(0), _dp(sums), _dp(Um),
+              Um.stride(0), _dp(msums), _stream())
+    return U, sums, Um, msums
+
+
 def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None):
     """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
     dY[col] only (alpha from aR, or from the forward's p when given)."""

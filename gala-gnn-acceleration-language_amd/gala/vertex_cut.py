@@ -160,7 +160,22 @@ class VertexCutGat:
     hand each owner  Y[r] = (sum_p U_p[r]) / (1e-12 + sum_p S_p[r])  -- REF has no max
     subtraction, so partial sums simply add.  aL of every row arrives by an all-gather of
     the owners' [n, H] blocks per chunk (small); aR and X of the own columns are local.
-    Forward only (the backward would reduce-scatter d_aL and all-gather dY rows)."""
+
+    Training (`forward_train` + `backward`, the REF layer of the generated programs with the
+    row statistics of gala_gat_{fwd,bwd}_stats_f32):
+      forward   gala_gat_fwd_partial_stats_f32 adds  Um_p[r] = sum m_e p_e X[col] and
+                M_p[r, h] = sum m_e p_e (m_e the LeakyReLU factor) to U_p and S_p; ONE
+                reduce-scatter of the packed [U | Um] rows (plus the two [rows, H] sums)
+                gives the owner q = 1/(S + 1e-12), Y = q U, Ym = q Um, sma = q M.
+      backward  the REF dX[r] = sum_e alpha_e dY[col_e] (A, not A^T: common.h:835-894) only
+                reads dY of the columns a rank holds -- its own rows -- so each rank runs the
+                same partial forward kernel with dY in place of X (P_p[r] = sum p_e dY[col])
+                and one reduce-scatter hands the owner dX = q P.  d_aL of a row needs no edge:
+                <dY, Ym> - (<dY, Y> + 1e-12) sma (+1e-12) per head, from the owner's rows
+                (gala_gat_bwd_stats_f32 on the owner's rows without edges).
+    No dY or X row crosses the links; per layer the collectives move (2F + 2H) floats per
+    row forward and F backward.  Results agree with one GPU to fp32 rounding (each row's
+    sums are regrouped by column range, and dX is q * sum p dY instead of sum fl(p q) dY)."""
 
     def __init__(self, part: VertexCutPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
         self.part, self.F, self.H, self.be, self.comm, self.slope = part, F, heads, backend, comm, slope
@@ -174,6 +189,8 @@ class VertexCutGat:
         self.Sown = backend.empty(K * c * heads)
         self.aLpad = backend.empty(K * c, heads)
         self.aLall = backend.empty(K * P * c, heads)
+        self._train = None   # buffers of forward_train / backward, allocated on first use
+        self.saved = None
 
     def __call__(self, aL, aR, X):
         """aL [n, H] (own rows), aR [n, H] and X [n, F] (own columns) -> Y [n, F] (own rows)."""
@@ -202,3 +219,83 @@ class VertexCutGat:
         q = 1.0 / (self.Sown[:n * H].view(n, H) + 1e-12)
         D = self.F // H
         return (self.Uown[:n].view(n, H, D) * q.view(n, H, 1)).reshape(n, self.F)
+
+    def _gather_aL(self, aL):
+        """aLall chunk by chunk (the [rows, H] logits of every destination row)."""
+        p, H, c, rows = self.part, self.H, self.part.block, self._rows
+        n = p.n
+        self.aLpad[:n].copy_(aL.reshape(n, H))
+        self.aLpad[n:].zero_()
+        for k in range(p.chunks):
+            al_k = self.aLall[k * rows:(k + 1) * rows]
+            if p.world > 1:
+                self.comm.wait([self.comm.all_gather(al_k, self.aLpad[k * c:(k + 1) * c])])
+            else:
+                al_k.copy_(self.aLpad[k * c:(k + 1) * c])
+
+    def _train_buffers(self):
+        if self._train is None:
+            be, p, H, F = self.be, self.part, self.H, self.F
+            K, P, c = p.chunks, p.world, p.block
+            own = layout.HostGraph(p.n, p.n, np.zeros(p.n + 1, np.int32), np.zeros(0, np.int32))
+            self._train = {
+                "UU": be.empty(K * P * c, 2 * F), "UUown": be.empty(K * c, 2 * F),
+                "M": be.empty(K * P * c * H), "Mown": be.empty(K * c * H),
+                "P": be.empty(K * P * c, F), "Pown": be.empty(K * c, F), "Ssc": be.empty(K * P * c * H),
+                "own": be.graph(own, split=False),
+            }
+        return self._train
+
+    def _owner_scale(self, q, T):
+        """q [n, H] times the [n, F] rows T per head (the owner's normalisation)."""
+        n, H = q.shape
+        return (T.reshape(n, H, self.F // H) * q.view(n, H, 1)).reshape(n, self.F)
+
+    def forward_train(self, aL, aR, X):
+        """aL [n, H] (own rows), aR [n, H], X [n, F] (own columns) -> Y [n, F]; keeps the
+        row statistics (q, Y, Ym, sma of the own rows) for `backward`."""
+        p, H, F, c, rows = self.part, self.H, self.F, self.part.block, self._rows
+        n, b = p.n, self._train_buffers()
+        self._gather_aL(aL)
+        works = []
+        for k, gk in enumerate(self.graphs):
+            UUk = b["UU"][k * rows:(k + 1) * rows]
+            Sk = self.S[k * rows * H:(k + 1) * rows * H]
+            Mk = b["M"][k * rows * H:(k + 1) * rows * H]
+            self.be.gat_partial_stats(gk, self.aLall[k * rows:(k + 1) * rows], aR, X, H, self.slope,
+                                      UUk[:, :F], Sk, UUk[:, F:], Mk)
+            dst = (b["UUown"][k * c:(k + 1) * c], self.Sown[k * c * H:(k + 1) * c * H],
+                   b["Mown"][k * c * H:(k + 1) * c * H])
+            for d, s in zip(dst, (UUk, Sk, Mk)):
+                if p.world > 1:
+                    works.append(self.comm.reduce_scatter(d, s))
+                else:
+                    d.copy_(s)
+        if works:
+            self.comm.wait(works)
+        q = 1.0 / (self.Sown[:n * H].view(n, H) + 1e-12)
+        Y = self._owner_scale(q, b["UUown"][:n, :F])
+        Ym = self._owner_scale(q, b["UUown"][:n, F:])
+        sma = b["Mown"][:n * H].view(n, H) * q
+        self.saved = (aL.reshape(n, H), aR, q, Y, Ym, sma)
+        return Y
+
+    def backward(self, dY):
+        """dY [n, F] of the own rows -> (dX [n, F], d_aL [n, H]) of the REF layer."""
+        p, H, F, c, rows = self.part, self.H, self.F, self.part.block, self._rows
+        n, b = p.n, self._train_buffers()
+        aL, aR, q, Y, Ym, sma = self.saved
+        works = []
+        for k, gk in enumerate(self.graphs):
+            Pk = b["P"][k * rows:(k + 1) * rows]
+            self.be.gat_partial(gk, self.aLall[k * rows:(k + 1) * rows], aR, dY, H, self.slope, Pk,
+                                b["Ssc"][k * rows * H:(k + 1) * rows * H])
+            if p.world > 1:
+                works.append(self.comm.reduce_scatter(b["Pown"][k * c:(k + 1) * c], Pk))
+            else:
+                b["Pown"][k * c:(k + 1) * c].copy_(Pk)
+        # the row-local d_aL needs no edge and overlaps the reduce-scatter
+        _, d_aL = self.be.gat_bwd_stats(b["own"], aL, aR, dY, q, Y, Ym, sma, H, self.slope)
+        if works:
+            self.comm.wait(works)
+        return self._owner_scale(q, b["Pown"][:n]), d_aL.view(n, H)

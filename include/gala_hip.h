@@ -372,6 +372,21 @@ int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR
                            const float *q, const float *Y, int64_t ldy, const float *Ym,
                            int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
                            void *stream);
+/*
+ * gala_gat_fwd_partial_stats_f32: gala_gat_fwd_stats_f32 over the columns one rank of a
+ * vertex cut holds, every output unnormalised so that the rows' owners add the ranks'
+ * partials before they divide (GALA_GAT_PARTIAL of gala_gat_fwd_ex_f32, plus the row
+ * statistics):  U[r] = sum_e p_e X[c_e],  sums[r,h] = sum_e p_e,  Um[r] = sum_e m_e p_e X[c_e],
+ * msums[r,h] = sum_e m_e p_e  (p_e = min(exp(LeakyReLU(aL[r] + aR[c_e])), 1e12), m_e the
+ * LeakyReLU factor).  The owner then forms q = 1 / (sum_p sums + S*1e-12), Y = q*U,
+ * Ym = q*Um, sma = q*msums: the inputs gala_gat_bwd_stats_f32 takes.  The REF softmax
+ * subtracts no row maximum (common.h:760-773), so partial sums simply add.  Replaces the
+ * torch softmax composition of common.h:735-810 for a row whose edges span several GPUs.
+ */
+int gala_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                                   const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                                   float slope, float *U, int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                   float *msums, void *stream);
 
 /*
  * Per-head attention logits of the multi-head GAT layer (galac gat_heads: the DSL's

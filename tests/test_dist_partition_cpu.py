@@ -287,3 +287,70 @@ def test_vertex_cut_gat_matches_one_process(world, name, chunks):
         assert p.exitcode == 0
     ref = _gat_one_process(GRAPHS[name]())
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+# ---- vertex-cut GAT training: row statistics forward + REF backward -------------------------
+def _gat_train_one_process(g):
+    """Y, dX, d_aL of the REF layer on one process (gala_cpu_gat_{fwd,bwd}_stats_f32)."""
+    from gala import _abi
+    aL, aR, X = _gat_inputs(g)
+    dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
+    be = CpuBackend()
+    cg = be.graph(g)
+    n = g.n_rows
+    Y, Ym = torch.empty((n, F_GAT)), torch.empty((n, F_GAT))
+    q, sma = torch.empty(n * H_GAT), torch.empty(n * H_GAT)
+    _abi.call_cpu("gala_gat_fwd_stats_f32", cg.csr(), aL.ctypes.data, aR.ctypes.data, None, None, X.ctypes.data,
+                  F_GAT, F_GAT, H_GAT, 0.2, Y.data_ptr(), F_GAT, q.data_ptr(), Ym.data_ptr(), F_GAT, sma.data_ptr(),
+                  None, None, None)
+    dX, d_aL = be.gat_bwd_stats(cg, torch.from_numpy(aL), torch.from_numpy(aR), torch.from_numpy(dY), q, Y, Ym,
+                                sma, H_GAT, 0.2)
+    return Y.numpy(), dX.numpy(), d_aL.view(n, H_GAT).numpy()
+
+
+def _gat_train_worker(rank, world, port, name, chunks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = GRAPHS[name]()
+        aL, aR, X = _gat_inputs(g)
+        dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
+        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        gat = vc.VertexCutGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
+        t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
+        Y = gat.forward_train(t(aL), t(aR), t(X))
+        dX, d_aL = gat.backward(t(dY))
+        sizes = [int(pt.bounds[r + 1] - pt.bounds[r]) for r in range(world)]
+        out = []
+        for T in (Y, dX, d_aL):
+            pad = torch.full((max(sizes), T.shape[1]), float("nan"))
+            pad[:pt.n] = T
+            ts = [torch.empty_like(pad) for _ in sizes]
+            dist.all_gather(ts, pad)
+            out.append(torch.cat([x[:s] for x, s in zip(ts, sizes)]).numpy())
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,chunks", [(1, "cora", 2), (2, "powerlaw", 1), (3, "cora", 2),
+                                                (3, "empty_rows", 1)])
+def test_vertex_cut_gat_training_matches_one_process(world, name, chunks):
+    """VertexCutGat.forward_train / backward (gala_gat_fwd_partial_stats_f32 partials, one
+    reduce-scatter per direction, d_aL from the owner's row statistics) against the
+    one-process row-statistics pair: Y, dX and d_aL within fp32 rounding."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gat_train_worker, args=(r, world, port, name, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _gat_train_one_process(GRAPHS[name]())
+    for a, b, what in zip(got, ref, ("Y", "dX", "d_aL")):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5, err_msg=what)

@@ -250,4 +250,72 @@ def test_bench_partitioned_path_over_rccl_one_rank():
     (d,) = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
     assert d["n_gpus"] == 1 and d["scaling"] == "strong" and d["comm"]["backend"] == "nccl"
     assert set(d["comm"]["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
-    assert d["value"] > 0 and d["weak"]["value"] > 0
+    assert d["value"] > 0 and d["weak"]["value"] > 0 and d["gat"]["value"] > 0
+
+
+@pytest.mark.parametrize("world,chunks", [(1, 2), (2, 1), (3, 4)])
+@pytest.mark.parametrize("heads,F", [(1, 32), (8, 256)])
+def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
+    """The vertex-cut GAT training pair, ranks simulated in-process on the HIP kernels:
+    gala_gat_fwd_partial_stats_f32 over every rank's columns, the partials added (the
+    reduce-scatter) and normalised by the owner give the one-GPU gala_gat_fwd_stats_f32's
+    Y, Ym, q and sma; the backward's partial P = sum p dY[col] (the partial forward on dY)
+    times q gives the one-GPU row-statistics backward's dX, and d_aL from the owner's rows
+    alone (an edgeless graph) its d_aL -- all within fp32 rounding.  world 1 also runs the
+    VertexCutGat class itself."""
+    from gala import layout, vertex_cut as vc
+    g = layout.gen_graph("uniform", 3000, 20000, seed=9)
+    rng = np.random.default_rng(6)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    aR = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    X = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    dg = ops.DeviceGraph.from_host(g)
+    Y1, q1, Ym1, sma1 = ops.gat_fwd_stats(dg, cu(aL), cu(X), aR=cu(aR), heads=heads)
+    dX1, daL1 = ops.gat_bwd_stats(dg, cu(aL), cu(aR), cu(dY), q1, Y1, Ym1, sma1, heads=heads)
+    parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks) for p in range(world)]
+    c, rows = parts[0].block, world * parts[0].block
+    aL_rows = torch.zeros((chunks * rows, heads), device="cuda")
+    for pt in parts:
+        for k in range(chunks):
+            j0, j1 = k * c, min((k + 1) * c, pt.n)
+            if j1 > j0:
+                aL_rows[k * rows + pt.rank * c:k * rows + pt.rank * c + (j1 - j0)] = cu(aL[pt.r0 + j0:pt.r0 + j1])
+    acc = {n_: torch.zeros((chunks * rows, F if n_ in ("U", "Um", "P") else heads), device="cuda")
+           for n_ in ("U", "Um", "S", "M", "P")}
+    for pt in parts:
+        own = slice(pt.r0, pt.r0 + pt.n)
+        for k, h in enumerate(pt.chunk_graphs):
+            gk = ops.DeviceGraph.from_host(h, split=pt.split_threshold)
+            al_k = aL_rows[k * rows:(k + 1) * rows].contiguous()
+            U, S, Um, M = ops.gat_fwd_partial_stats(gk, al_k, cu(X[own]), aR=cu(aR[own]), heads=heads)
+            P, _ = ops.gat_fwd_partial(gk, al_k, cu(dY[own]), aR=cu(aR[own]), heads=heads)
+            for n_, t in (("U", U), ("Um", Um), ("S", S), ("M", M), ("P", P)):
+                acc[n_][k * rows:(k + 1) * rows] += t.view(rows, -1)
+    D = F // heads
+    for pt in parts:
+        sl = slice(pt.r0, pt.r0 + pt.n)
+        o = {n_: torch.cat([t[k * rows + pt.rank * c:k * rows + (pt.rank + 1) * c] for k in range(chunks)])[:pt.n]
+             for n_, t in acc.items()}
+        q = 1.0 / (o["S"] + 1e-12)
+        sc = lambda T: (T.view(pt.n, heads, D) * q.view(pt.n, heads, 1)).reshape(pt.n, F)  # noqa: E731
+        Y, Ym, sma = sc(o["U"]), sc(o["Um"]), o["M"] * q
+        torch.testing.assert_close(Y, Y1[sl], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(Ym, Ym1[sl], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(q.reshape(-1), q1.view(-1, heads)[sl].reshape(-1), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(sma.reshape(-1), sma1.view(-1, heads)[sl].reshape(-1), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(sc(o["P"]), dX1[sl], rtol=1e-5, atol=1e-6)
+        eg = ops.DeviceGraph.from_host(layout.HostGraph(pt.n, pt.n, np.zeros(pt.n + 1, np.int32),
+                                                        np.zeros(0, np.int32)), split=False)
+        _, daL = ops.gat_bwd_stats(eg, cu(aL[sl]), cu(aR[sl]), cu(dY[sl]), q.contiguous(), Y, Ym,
+                                   sma.contiguous(), heads=heads)
+        torch.testing.assert_close(daL, daL1.view(-1, heads)[sl].reshape(-1), rtol=1e-4, atol=1e-4)
+    if world == 1:
+        from gala.backend import HipBackend
+        gat = vc.VertexCutGat(parts[0], F, heads, HipBackend("cuda"), None)
+        Yc = gat.forward_train(cu(aL), cu(aR), cu(X))
+        dXc, daLc = gat.backward(cu(dY))
+        torch.testing.assert_close(Yc, Y1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dXc, dX1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(daLc.reshape(-1), daL1, rtol=1e-4, atol=1e-4)
