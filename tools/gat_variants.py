@@ -2,7 +2,13 @@
 """Experiment driver: time the 8-head (F=256) and 1-head (F=32) GAT forward kernels of an
 alternative libgala_hip.so build (argv[1]: its directory) on the Products-shaped uniform
 graph; prints one JSON line per op.  Y rows of the first variant are kept in
-gpurun_out/gatv_ref_*.pt and later variants report their max deviation from them."""
+gpurun_out/gatv_ref_*.pt and later variants report their max deviation from them.
+
+A/B driver for kernel experiments: each variant is libgala_hip.so relinked with gat.hip
+built from a temporary patch (exp/<name>/).  The round-2 variants (batch size, occupancy
+hints, DPP reductions, column prefetch, no padding masks, no Ym / accm / aR_out, non-temporal
+stores; profiles/r02_gat_fwd_variants_stores.jsonl) changed nothing beyond
+1 %, so none of those patches is in the tree."""
 import json
 import os
 import sys
