@@ -591,7 +591,8 @@ def rmat_family(args, dev, be, timer, sync):
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
                         "alg_bytes_per_launch": alg,
-                        "kernel": "gala_spmm_f32 (degree-ordered k_spmm_rowgroup + hub-row k_spmm_chunk/fixup)"}}
+                        "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
+                                  "grid, then k_spmm_fixup)"}}
     if be.name == "hip":
         t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
         if t_ceil:

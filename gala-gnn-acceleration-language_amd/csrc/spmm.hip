@@ -217,21 +217,21 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
     }
 }
 
+// the rows of row block `bid` of `nb` (skipping hub rows)
 template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
-__global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
+__device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid, int64_t nb) {
     typedef typename VecT<VEC>::T V;
     constexpr int RPW = kWave / G;
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
-    const int64_t blk = p.xcd_order ? logical_block_runs(blockIdx.x, gridDim.x, kXcdRun)
-                                    : (int64_t)blockIdx.x;
+    const int64_t blk = p.xcd_order ? logical_block_runs(bid, nb, kXcdRun) : bid;
     const int64_t wave = blk * (kBlock / kWave) + (threadIdx.x / kWave);
     const int64_t rid = wave * RPW + lane / G;
     if (rid >= p.n_rows) return;
     const int64_t row = p.row_order ? (int64_t)p.row_order[rid] : rid;
     KernargSegPtr seg = kernarg_segtable(offsetof(SpmmParams, seg));
     if (p.split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > p.split_threshold)
-        return;  // hub row: done by k_spmm_chunk + k_spmm_fixup
+        return;  // hub row: its chunks (spmm_chunk_block) + k_spmm_fixup
     const Cols<VEC, G, CH, W> cl(p, gl);
     V acc[CH];
     init_acc<VEC, G, CH, W>(p, cl, row, acc);
@@ -243,6 +243,11 @@ __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
         accumulate_range<VEC, G, CH, U, W, SAMP, SRCS>(p, cl, row, base + rp[row], base + rp[row + 1], acc);
     }
     store_row<VEC, G, CH, W>(p, cl, row, acc);
+}
+
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+__global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
+    spmm_row_block<VEC, G, CH, U, W, SAMP, SRCS>(p, blockIdx.x, gridDim.x);
 }
 
 // ---- split rows: chunk partials + ordered fix-up ---------------------------------------
@@ -257,13 +262,14 @@ struct SplitParams {
     int32_t chunk;
 };
 
+// the 512-edge chunks of hub rows in chunk block `bid` -> their partial sums in ws
 template <int VEC, int G, int CH, int U, bool W, bool SRCS>
-__global__ __launch_bounds__(kBlock) void k_spmm_chunk(SpmmParams p, SplitParams sp) {
+__device__ __forceinline__ void spmm_chunk_block(const SpmmParams &p, const SplitParams &sp, int64_t bid) {
     typedef typename VecT<VEC>::T V;
     constexpr int RPW = kWave / G;
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = lane & (G - 1);
-    const int64_t c = ((int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave) * RPW + lane / G;
+    const int64_t c = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW + lane / G;
     if (c >= sp.n_chunks) return;
     const int32_t ri = sp.chunk_row[c];
     const int64_t row = sp.rows[ri];
@@ -279,6 +285,18 @@ __global__ __launch_bounds__(kBlock) void k_spmm_chunk(SpmmParams p, SplitParams
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
         if (cl.valid[ch]) stv<VEC>(sp.ws + c * sp.ws_cols + cl.off[ch], acc[ch]);
+}
+
+// A skewed graph's rows and hub-row chunks in ONE launch: the first `cb` blocks take the
+// chunks (the largest, evenly sized pieces, dispatched first), the rest the row blocks in the
+// plan's degree order.  One grid instead of two back to back: no drain / ramp between them.
+template <int VEC, int G, int CH, int U, bool W, bool SRCS>
+__global__ __launch_bounds__(kBlock) void k_spmm_rows_chunks(SpmmParams p, SplitParams sp, int64_t cb) {
+    const int64_t b = blockIdx.x;
+    if (b < cb)
+        spmm_chunk_block<VEC, G, CH, U, W, SRCS>(p, sp, b);
+    else
+        spmm_row_block<VEC, G, CH, U, W, false, SRCS>(p, b - cb, (int64_t)gridDim.x - cb);
 }
 
 template <int VEC, int G, int CH, bool W>
@@ -367,12 +385,14 @@ template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
 static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
     constexpr int rows_per_block = (kBlock / kWave) * (kWave / G);
     const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
-    hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
-                       dim3(kBlock), 0, st, p);
+    if (SAMP || !sp || sp->n_chunks <= 0) {
+        hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, st, p);
+    }
     if (!SAMP && sp && sp->n_chunks > 0) {
         const int64_t cb = (sp->n_chunks + rows_per_block - 1) / rows_per_block;
-        hipLaunchKernelGGL((k_spmm_chunk<VEC, G, CH, U, W, SRCS>), dim3((unsigned)cb), dim3(kBlock), 0,
-                           st, p, *sp);
+        hipLaunchKernelGGL((k_spmm_rows_chunks<VEC, G, CH, U, W, SRCS>), dim3((unsigned)(cb + blocks)),
+                           dim3(kBlock), 0, st, p, *sp, cb);
         const int64_t fb = (sp->n_rows_split + rows_per_block - 1) / rows_per_block;
         hipLaunchKernelGGL((k_spmm_fixup<VEC, G, CH, W>), dim3((unsigned)fb), dim3(kBlock), 0, st, p,
                            *sp);
