@@ -17,6 +17,11 @@ gala.cu.  This runtime executes the same post-pass IR (galac --ir-json) instead:
     training rows' share of the global mean cross entropy, and the weight gradients are
     summed over the ranks (one all-reduce per weight) before the identical Adam steps
     (lr 0.01, weight decay 5e-4, codegen/gala.cu:606-607).
+  * `--layout vcut` is north_star's vertex cut instead (gala/vertex_cut.py
+    VertexCutAggregator.apply): each rank holds the edges whose source it owns, computes
+    partial rows for every destination and one RCCL reduce-scatter sums them into the
+    owners' rows -- no halo; the sums regroup per rank, so results agree with one GPU to
+    fp32 rounding.
 Training subgraphs (graph g > 0) run on the whole graph: they only drop rows no training
 row depends on, so the training rows' values are unchanged.  The column-tiled layout
 (col_tile) is a single-device layout and is not used.  GAT layers are not supported here.
@@ -86,7 +91,8 @@ class Program:
     """One rank's share of a galac program (post-pass IR)."""
 
     def __init__(self, ir: dict, graph: layout.HostGraph, X_own: torch.Tensor, labels_own: torch.Tensor,
-                 train_own: torch.Tensor, rank: int, world: int, device, seed: int = 0, group=None):
+                 train_own: torch.Tensor, rank: int, world: int, device, seed: int = 0, group=None,
+                 layout_mode: str = "halo"):
         ops = {nd["op"] for nd in ir["nodes"]}
         bad = ops - SUPPORTED
         if bad:
@@ -99,9 +105,19 @@ class Program:
         self.be = make_backend(self.device)
         self.comm = Comm(group) if world > 1 else None
         self.rank, self.world = rank, world
-        self.part = gdist.partition_graph(graph, rank, world)
-        self.agg = gdist.DistAggregator(self.part, 1, self.be, self.comm, exact=True)
-        self.deg = torch.from_numpy(np.diff(self.part.graph.rowptr).astype(np.float32)).to(self.device).view(-1, 1)
+        self.layout = layout_mode
+        if layout_mode == "vcut":
+            from . import vertex_cut as vc
+            self.part = vc.vertex_cut_partition(graph, rank, world)
+            self.agg = vc.VertexCutAggregator(self.part, 1, self.be, self.comm)
+            own_rowptr = self.part.deg_graph.rowptr
+        elif layout_mode == "halo":
+            self.part = gdist.partition_graph(graph, rank, world)
+            self.agg = gdist.DistAggregator(self.part, 1, self.be, self.comm, exact=True)
+            own_rowptr = self.part.graph.rowptr
+        else:
+            raise ValueError(f"gala.dist_run: layout {layout_mode!r} (halo | vcut)")
+        self.deg = torch.from_numpy(np.diff(own_rowptr).astype(np.float32)).to(self.device).view(-1, 1)
         self.X, self.labels, self.train = X_own, labels_own, train_own
         # replicated weights, identical on every rank (same seed, same order as the IR)
         torch.manual_seed(seed)
@@ -194,6 +210,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--dump", help="rank 0 writes an npz: predictions (all rows), losses, rowptr/col")
+    ap.add_argument("--layout", default="halo", choices=["halo", "vcut"],
+                    help="halo: row partition + exact halo SpMM; vcut: vertex cut + reduce-scatter")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,7 +255,7 @@ def main(argv=None):
         labels = lab_all[r0:r1].astype(np.int64)
         train = tr_all[r0:r1] > 0
     prog = Program(ir, g, torch.from_numpy(X).to(dev), torch.from_numpy(labels).to(dev),
-                   torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed)
+                   torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed, layout_mode=args.layout)
     init_weights = {k: v.detach().cpu().numpy().tolist() for k, v in prog.modules.state_dict().items()}
     opt = torch.optim.Adam(prog.modules.parameters(), lr=0.01, weight_decay=5e-4)
     iters = args.iters if args.iters is not None else max(int(s.get("iterations", 0)), 1)
@@ -281,7 +299,8 @@ def main(argv=None):
             np.savez(args.dump, prediction=pr.numpy(), losses=np.array(losses), rowptr=g.rowptr, col=g.col,
                      weights=np.array(json.dumps(init_weights)))
     if rank == 0:
-        print(json.dumps({"ranks": world, "vertices": g.n_rows, "edges": g.nnz, "halo": prog.part.halo_mode,
+        print(json.dumps({"ranks": world, "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,
+                          "halo": prog.part.halo_mode if args.layout == "halo" else None,
                           "fwd_mean_s": float(np.mean(fwd_t[keep])), "epoch_mean_s": float(np.mean(ep_t[keep])),
                           "loss_first": losses[0], "loss_last": losses[-1]}), flush=True)
         print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)

@@ -122,29 +122,47 @@ class VertexCutAggregator:
         self.graphs = [backend.graph(h, split=thr) for h in part.chunk_graphs]
         self.deg_graph = backend.graph(part.deg_graph, split=False)
         self.norm = backend.degree(self.deg_graph)
-        self.Xs = backend.empty(part.n, F)
-        rows = part.world * part.block
-        self.partial = backend.empty(part.chunks * rows, F)
-        self.S = backend.empty(part.chunks * part.block, F)
-        self._rows = rows
+        self._rows = part.world * part.block
+        self._bufs = {}
+        self.Xs, self.partial, self.S = self._buffers(F)
+
+    def _buffers(self, F):
+        """(Xs [n, F], partial rows [K*P*c, F], owner rows [K*c, F]) of width F (a program's
+        layers differ in width)."""
+        if F not in self._bufs:
+            p, be = self.part, self.be
+            self._bufs[F] = (be.empty(p.n, F), be.empty(p.chunks * self._rows, F), be.empty(p.chunks * p.block, F))
+        return self._bufs[F]
 
     def refresh_norm(self):
         self.norm = self.be.degree(self.deg_graph)
 
     def __call__(self, H, out):
+        """out = norm * A (norm * H) with the graph's own norm (the GCN aggregation)."""
+        return self.apply(H, out, self.norm, self.norm)
+
+    def apply(self, H, out, pre=None, post=None):
+        """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None): the
+        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) with column ownership."""
         be, p, c, rows = self.be, self.part, self.part.block, self._rows
-        be.row_broadcast(self.norm, H, self.Xs)
+        Xs, partial, S = self._buffers(H.shape[1])
+        if pre is None:
+            Xs.copy_(H)
+        else:
+            be.row_broadcast(pre, H, Xs)
         works = []
         for k, gk in enumerate(self.graphs):
-            Yk = self.partial[k * rows:(k + 1) * rows]
-            be.spmm(gk, self.Xs, Yk, None, False)
+            Yk = partial[k * rows:(k + 1) * rows]
+            be.spmm(gk, Xs, Yk, None, False)
             if p.world > 1:
-                works.append(self.comm.reduce_scatter(self.S[k * c:(k + 1) * c], Yk))
+                works.append(self.comm.reduce_scatter(S[k * c:(k + 1) * c], Yk))
             else:
-                self.S[k * c:(k + 1) * c].copy_(Yk)
+                S[k * c:(k + 1) * c].copy_(Yk)
         if works:
             self.comm.wait(works)
-        return be.row_broadcast(self.norm, self.S[:p.n], out)
+        if post is None:
+            return out.copy_(S[:p.n])
+        return be.row_broadcast(post, S[:p.n], out)
 
     def halo_bytes(self) -> int:
         return self.part.comm_bytes(self.F) if self.part.world > 1 else 0

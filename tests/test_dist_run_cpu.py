@@ -42,7 +42,7 @@ def _ir(prog, tmp_path):
     return out
 
 
-def _run(ir, tmp_path, world, tag, iters=6):
+def _run(ir, tmp_path, world, tag, iters=6, extra=()):
     dump = tmp_path / f"{tag}.npz"
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["OMP_NUM_THREADS"] = "2"
@@ -53,7 +53,7 @@ def _run(ir, tmp_path, world, tag, iters=6):
                 "127.0.0.1", f"--master-port={_free_port()}", "-m", "gala.dist_run"]
     else:
         cmd += ["-m", "gala.dist_run"]
-    cmd += [str(ir), "--synthetic", "--device", "cpu", "--iters", str(iters), "--dump", str(dump)]
+    cmd += [str(ir), "--synthetic", "--device", "cpu", "--iters", str(iters), "--dump", str(dump), *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     summary = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
@@ -86,3 +86,17 @@ def test_dist_run_ranks_match_one_rank(world, tmp_path):
     np.testing.assert_allclose(dn["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(dn["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
     assert sn["loss_last"] < sn["loss_first"]            # it trains
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_dist_run_vertex_cut_matches_one_rank(world, tmp_path):
+    """`--layout vcut` (config 5's vertex cut: column ownership, partial rows
+    reduce-scattered to their owners) against the one-rank halo run: predictions and the
+    loss curve within fp32 rounding (each row's sum is regrouped by column range)."""
+    ir_path = _ir("gcn3.txt", tmp_path)
+    d1, _ = _run(ir_path, tmp_path, 1, "w1")
+    dn, sn = _run(ir_path, tmp_path, world, f"v{world}", extra=("--layout", "vcut"))
+    assert sn["layout"] == "vcut"
+    np.testing.assert_allclose(dn["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dn["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+    assert sn["loss_last"] < sn["loss_first"]

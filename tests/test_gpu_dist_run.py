@@ -19,7 +19,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run_gpu(ir, tmp_path, world, tag, iters=6):
+def _run_gpu(ir, tmp_path, world, tag, iters=6, extra=()):
     import subprocess
     import sys
     from test_dist_run_cpu import PKG, ROOT, _free_port
@@ -33,7 +33,7 @@ def _run_gpu(ir, tmp_path, world, tag, iters=6):
                 "127.0.0.1", f"--master-port={_free_port()}", "-m", "gala.dist_run"]
     else:
         cmd += ["-m", "gala.dist_run"]
-    cmd += [str(ir), "--synthetic", "--device", "cuda", "--iters", str(iters), "--dump", str(dump)]
+    cmd += [str(ir), "--synthetic", "--device", "cuda", "--iters", str(iters), "--dump", str(dump), *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     return dict(np.load(dump))
@@ -58,3 +58,14 @@ def test_dist_run_gpu_two_ranks_match_one(tmp_path):
     d2 = _run_gpu(ir_path, tmp_path, 2, "g2")
     np.testing.assert_allclose(d2["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+
+
+def test_dist_run_gpu_vertex_cut_matches_one_rank(tmp_path):
+    """`--layout vcut` on the HIP kernels: one rank (the class's own copy path) and two ranks
+    sharing the GPU over gloo, against the one-rank halo run within fp32 rounding."""
+    ir_path = _ir("gcn3.txt", tmp_path)
+    d1 = _run_gpu(ir_path, tmp_path, 1, "g1")
+    for world in (1, 2):
+        dv = _run_gpu(ir_path, tmp_path, world, f"v{world}", extra=("--layout", "vcut"))
+        np.testing.assert_allclose(dv["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(dv["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
