@@ -39,7 +39,8 @@ def timeit(fn, reps=10):
 
 def main():
     name = os.path.basename(os.path.abspath(sys.argv[1]))
-    hg = layout.gen_graph("uniform", 2_449_029, 61_859_140, seed=42)
+    kind = os.environ.get("GALA_GRAPH", "uniform")   # "rmat": skewed, with the hub-row plan
+    hg = layout.gen_graph(kind, 2_449_029, 61_859_140, seed=42)
     dg = ops.DeviceGraph.from_host(hg)
     N = hg.n_rows
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -56,12 +57,15 @@ def main():
             dev = float((Y[:20000] - R).abs().max())
         else:
             torch.save(Y[:20000].cpu(), ref)
-        rec = {"variant": name, "heads": H, "F": F,
+        dY = torch.rand((N, F), device="cuda", generator=g) * 2 - 1
+        _, q, Ym, sma, aRo = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+        rec = {"variant": name, "graph": kind, "heads": H, "F": F,
                "fwd_stats_rc_ms": timeit(lambda: ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)),
+               "bwd_stats_ms": timeit(lambda: ops.gat_bwd_stats(dg, aL, aRo, dY, q, Y, Ym, sma, heads=H)),
                "fwd_q_rc_ms": timeit(lambda: ops.gat_fwd_ex(dg, aL, X, wR=wR, bR=bR, heads=H, factored="q")),
                "max_dev_vs_first": dev}
         print(json.dumps(rec), flush=True)
-        del X, Y
+        del X, Y, dY, q, Ym, sma, aRo
         torch.cuda.empty_cache()
 
 
