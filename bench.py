@@ -408,7 +408,7 @@ def gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, r
     bR = torch.zeros(H, device=dev)
 
     def step():
-        layer.forward_train(aL, be.head_attn(X, wR, bR, H), X)
+        layer.forward_train(aL, None, X, wR, bR)   # source logits recomputed from X, as at N = 1
         layer.backward(dY)
     steps = max(args.steps // 2, 2)
     t_step = timed_steps(step, steps, 2, sync, barrier, reduce_max)

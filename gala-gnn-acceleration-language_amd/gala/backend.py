@@ -45,10 +45,11 @@ class HipBackend:
         """REF GAT forward over one column range, unnormalised (GALA_GAT_PARTIAL)."""
         return self.ops.gat_fwd_partial(g, aL, X, aR=aR, heads=heads, slope=slope, Y=Y, sums=sums)
 
-    def gat_partial_stats(self, g, aL, aR, X, heads, slope, U, sums, Um, msums):
-        """REF row-statistics forward over one column range, unnormalised (vertex cut)."""
-        return self.ops.gat_fwd_partial_stats(g, aL, X, aR=aR, heads=heads, slope=slope, U=U, sums=sums, Um=Um,
-                                              msums=msums)
+    def gat_partial_stats(self, g, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None):
+        """REF row-statistics forward over one column range, unnormalised (vertex cut); aR
+        None: recomputed per head from X (wR, bR)."""
+        return self.ops.gat_fwd_partial_stats(g, aL, X, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, U=U,
+                                              sums=sums, Um=Um, msums=msums)
 
     def gat_bwd_stats(self, g, aL, aR, dY, q, Y, Ym, sma, heads, slope):
         """(dX, d_aL) of the REF layer from its row statistics (gala_gat_bwd_stats_f32)."""
@@ -128,10 +129,10 @@ class CpuBackend:
                       _hp(sums), None)
         return Y, sums
 
-    def gat_partial_stats(self, g: CpuGraph, aL, aR, X, heads, slope, U, sums, Um, msums):
-        _abi.call_cpu("gala_gat_fwd_partial_stats_f32", g.csr(), _hp(aL), _hp(aR), None, None, _hp(X), X.stride(0),
-                      X.shape[1], heads, slope, _hp(U), U.stride(0), _hp(sums), _hp(Um), Um.stride(0), _hp(msums),
-                      None)
+    def gat_partial_stats(self, g: CpuGraph, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None):
+        _abi.call_cpu("gala_gat_fwd_partial_stats_f32", g.csr(), _hp(aL), _hp(aR), _hp(wR), _hp(bR), _hp(X),
+                      X.stride(0), X.shape[1], heads, slope, _hp(U), U.stride(0), _hp(sums), _hp(Um), Um.stride(0),
+                      _hp(msums), None)
         return U, sums, Um, msums
 
     def gat_bwd_stats(self, g: CpuGraph, aL, aR, dY, q, Y, Ym, sma, heads, slope):

@@ -269,9 +269,12 @@ class VertexCutGat:
         n, H = q.shape
         return (T.reshape(n, H, self.F // H) * q.view(n, H, 1)).reshape(n, self.F)
 
-    def forward_train(self, aL, aR, X):
+    def forward_train(self, aL, aR, X, wR=None, bR=None):
         """aL [n, H] (own rows), aR [n, H], X [n, F] (own columns) -> Y [n, F]; keeps the
-        row statistics (q, Y, Ym, sma of the own rows) for `backward`."""
+        row statistics (q, Y, Ym, sma of the own rows) for `backward`.  aR None: the source
+        logits are the per-head Linear (wR [F], bR [H]) of X, recomputed inside the kernel
+        from the gathered rows (the DSL's attnR = ffn(res, out=1)); the backward then takes
+        them from one gala_head_attn_f32 pass over the own rows."""
         p, H, F, c, rows = self.part, self.H, self.F, self.part.block, self._rows
         n, b = p.n, self._train_buffers()
         self._gather_aL(aL)
@@ -281,7 +284,7 @@ class VertexCutGat:
             Sk = self.S[k * rows * H:(k + 1) * rows * H]
             Mk = b["M"][k * rows * H:(k + 1) * rows * H]
             self.be.gat_partial_stats(gk, self.aLall[k * rows:(k + 1) * rows], aR, X, H, self.slope,
-                                      UUk[:, :F], Sk, UUk[:, F:], Mk)
+                                      UUk[:, :F], Sk, UUk[:, F:], Mk, wR=wR, bR=bR)
             dst = (b["UUown"][k * c:(k + 1) * c], self.Sown[k * c * H:(k + 1) * c * H],
                    b["Mown"][k * c * H:(k + 1) * c * H])
             for d, s in zip(dst, (UUk, Sk, Mk)):
@@ -289,6 +292,8 @@ class VertexCutGat:
                     works.append(self.comm.reduce_scatter(d, s))
                 else:
                     d.copy_(s)
+        if aR is None:   # the backward's source logits of the own columns
+            aR = self.be.head_attn(X, wR, bR, H)
         if works:
             self.comm.wait(works)
         q = 1.0 / (self.Sown[:n * H].view(n, H) + 1e-12)

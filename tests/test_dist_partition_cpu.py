@@ -290,25 +290,34 @@ def test_vertex_cut_gat_matches_one_process(world, name, chunks):
 
 
 # ---- vertex-cut GAT training: row statistics forward + REF backward -------------------------
-def _gat_train_one_process(g):
-    """Y, dX, d_aL of the REF layer on one process (gala_cpu_gat_{fwd,bwd}_stats_f32)."""
+def _gat_attn_weights():
+    rng = np.random.default_rng(23)
+    return rng.uniform(-0.5, 0.5, F_GAT).astype(np.float32), rng.uniform(-0.5, 0.5, H_GAT).astype(np.float32)
+
+
+def _gat_train_one_process(g, rc=False):
+    """Y, dX, d_aL of the REF layer on one process (gala_cpu_gat_{fwd,bwd}_stats_f32); rc:
+    the source logits recomputed from X (wR, bR)."""
     from gala import _abi
     aL, aR, X = _gat_inputs(g)
+    wR, bR = _gat_attn_weights()
     dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
     be = CpuBackend()
     cg = be.graph(g)
     n = g.n_rows
     Y, Ym = torch.empty((n, F_GAT)), torch.empty((n, F_GAT))
-    q, sma = torch.empty(n * H_GAT), torch.empty(n * H_GAT)
-    _abi.call_cpu("gala_gat_fwd_stats_f32", cg.csr(), aL.ctypes.data, aR.ctypes.data, None, None, X.ctypes.data,
+    q, sma, aRo = torch.empty(n * H_GAT), torch.empty(n * H_GAT), torch.empty(n * H_GAT)
+    _abi.call_cpu("gala_gat_fwd_stats_f32", cg.csr(), aL.ctypes.data, None if rc else aR.ctypes.data,
+                  wR.ctypes.data if rc else None, bR.ctypes.data if rc else None, X.ctypes.data,
                   F_GAT, F_GAT, H_GAT, 0.2, Y.data_ptr(), F_GAT, q.data_ptr(), Ym.data_ptr(), F_GAT, sma.data_ptr(),
-                  None, None, None)
-    dX, d_aL = be.gat_bwd_stats(cg, torch.from_numpy(aL), torch.from_numpy(aR), torch.from_numpy(dY), q, Y, Ym,
+                  aRo.data_ptr() if rc else None, None, None)
+    aR_b = aRo.view(n, H_GAT) if rc else torch.from_numpy(aR)
+    dX, d_aL = be.gat_bwd_stats(cg, torch.from_numpy(aL), aR_b, torch.from_numpy(dY), q, Y, Ym,
                                 sma, H_GAT, 0.2)
     return Y.numpy(), dX.numpy(), d_aL.view(n, H_GAT).numpy()
 
 
-def _gat_train_worker(rank, world, port, name, chunks, q):
+def _gat_train_worker(rank, world, port, name, chunks, q, rc=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -319,7 +328,11 @@ def _gat_train_worker(rank, world, port, name, chunks, q):
         own = slice(pt.r0, pt.r0 + pt.n)
         gat = vc.VertexCutGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
         t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
-        Y = gat.forward_train(t(aL), t(aR), t(X))
+        if rc:
+            wR, bR = _gat_attn_weights()
+            Y = gat.forward_train(t(aL), None, t(X), torch.from_numpy(wR), torch.from_numpy(bR))
+        else:
+            Y = gat.forward_train(t(aL), t(aR), t(X))
         dX, d_aL = gat.backward(t(dY))
         sizes = [int(pt.bounds[r + 1] - pt.bounds[r]) for r in range(world)]
         out = []
@@ -335,22 +348,23 @@ def _gat_train_worker(rank, world, port, name, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name,chunks", [(1, "cora", 2), (2, "powerlaw", 1), (3, "cora", 2),
-                                                (3, "empty_rows", 1)])
-def test_vertex_cut_gat_training_matches_one_process(world, name, chunks):
+@pytest.mark.parametrize("world,name,chunks,rc", [(1, "cora", 2, False), (2, "powerlaw", 1, False),
+                                                   (3, "cora", 2, False), (3, "empty_rows", 1, False),
+                                                   (2, "cora", 1, True), (3, "powerlaw", 2, True)])
+def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc):
     """VertexCutGat.forward_train / backward (gala_gat_fwd_partial_stats_f32 partials, one
     reduce-scatter per direction, d_aL from the owner's row statistics) against the
     one-process row-statistics pair: Y, dX and d_aL within fp32 rounding."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gat_train_worker, args=(r, world, port, name, chunks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gat_train_worker, args=(r, world, port, name, chunks, q, rc)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = _gat_train_one_process(GRAPHS[name]())
+    ref = _gat_train_one_process(GRAPHS[name](), rc)
     for a, b, what in zip(got, ref, ("Y", "dX", "d_aL")):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5, err_msg=what)

@@ -319,3 +319,13 @@ def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
         torch.testing.assert_close(Yc, Y1, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(dXc, dX1, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(daLc.reshape(-1), daL1, rtol=1e-4, atol=1e-4)
+        # the source logits recomputed from X inside the partial kernel (the DSL's shape)
+        wR = cu(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+        bR = cu(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+        Y2, q2, Ym2, sma2, aR2 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR, bR=bR, heads=heads, want_aR=True)
+        dX2, daL2 = ops.gat_bwd_stats(dg, cu(aL), aR2, cu(dY), q2, Y2, Ym2, sma2, heads=heads)
+        Yr = gat.forward_train(cu(aL), None, cu(X), wR, bR)
+        dXr, daLr = gat.backward(cu(dY))
+        torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dXr, dX2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(daLr.reshape(-1), daL2, rtol=1e-4, atol=1e-4)
