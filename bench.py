@@ -567,6 +567,14 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     return out
 
 
+def rmat_traffic():
+    """PMC bytes of one R-MAT SpMM call: the rows + hub chunks grid and the chunk fix-up
+    (tools/gpu_pmc_rmat.sh -> profiles/traffic.json), or None."""
+    a = load_traffic("k_spmm_rows_chunks<4, 8, 1, 4, false, false>")
+    b = load_traffic("k_spmm_fixup<4, 8, 1, false>")
+    return a + b if a is not None and b is not None else None
+
+
 def rmat_family(args, dev, be, timer, sync):
     """The same step on an R-MAT graph of the Products shape: skewed
     degrees, so the SpMM runs the degree-ordered row schedule and the hub-row chunks."""
@@ -590,7 +598,7 @@ def rmat_family(args, dev, be, timer, sync):
            "split_rows": getattr(agg.g, "split_rows", 0),
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
-                        "alg_bytes_per_launch": alg,
+                        "alg_bytes_per_launch": alg, "traffic": rmat_traffic() if be.name == "hip" else None,
                         "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
                                   "grid, then k_spmm_fixup)"}}
     if be.name == "hip":
