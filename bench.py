@@ -397,7 +397,8 @@ def gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, r
     import torch
     from gala import vertex_cut as vc
     H, F = GAT_HEADS, GAT_HEADS * GAT_HEAD_F
-    part = vc.vertex_cut_partition(g, rank, world, 1, bounds)
+    # destination rows in PIPE_CHUNKS blocks: block k's reduce-scatters overlap block k+1's kernels
+    part = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
     layer = vc.VertexCutGat(part, F, H, be, comm)
     n = part.n
     gen = torch.Generator(device=dev).manual_seed(4321 + rank)
@@ -414,7 +415,8 @@ def gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, r
     t_step = timed_steps(step, steps, 2, sync, barrier, reduce_max)
     out = {"value": 2 * g.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
            "layer": f"GAT {H} heads x {GAT_HEAD_F} (F={F}), REF softmax; forward + backward",
-           "layout": f"vertex cut x{world}: row-statistics partials reduce-scattered to the row owners",
+           "layout": f"vertex cut x{world}: row-statistics partials reduce-scattered to the row owners "
+                     f"in {PIPE_CHUNKS} overlapped row blocks",
            "comm_bytes_per_step_per_rank": part.comm_bytes(2 * F + 2 * H) + part.comm_bytes(F)}
     del layer, X, dY
     return out
@@ -631,6 +633,11 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
+    # the driver reads ONE JSON line on stdout: the libraries' own stdout banners (RCCL's
+    # version lines, gloo's connection lines) go to stderr, the result line to the real stdout
+    result_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     from gala.backend import make_backend
@@ -664,7 +671,7 @@ def main():
     if dev.type == "cpu":
         out["device"] = "cpu (host-CPU backend plumbing run; not a GPU measurement)"
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(result_fd, (json.dumps(out) + "\n").encode())
     if distributed:
         torch.distributed.destroy_process_group()
 
