@@ -305,6 +305,8 @@ class VertexCutGat:
 
     def backward(self, dY):
         """dY [n, F] of the own rows -> (dX [n, F], d_aL [n, H]) of the REF layer."""
+        if self.saved is None:
+            raise RuntimeError("VertexCutGat.backward: no forward_train to take the row statistics from")
         p, H, F, c, rows = self.part, self.H, self.F, self.part.block, self._rows
         n, b = p.n, self._train_buffers()
         aL, aR, q, Y, Ym, sma = self.saved
