@@ -329,3 +329,28 @@ def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
         torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(dXr, dX2, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(daLr.reshape(-1), daL2, rtol=1e-4, atol=1e-4)
+
+
+def test_bench_self_launch_two_ranks_on_one_gpu_gloo():
+    """`bench.py --gpus 2` as the driver runs it (no launcher: it starts its own two ranks)
+    on the HIP kernels, the two ranks sharing the box's one GPU over gloo: exactly one JSON
+    line on stdout, strong scaling of the one graph, every layout candidate timed, and the
+    GAT layer over the vertex cut."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["GALA_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--scale", "0.02", "--steps",
+                        "2", "--warmup", "1", "--no-weak"], capture_output=True, text=True, timeout=220, env=env,
+                       cwd=root)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["comm"]["backend"] == "gloo"
+    assert set(d["comm"]["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
+    assert d["value"] > 0 and d["gat"]["value"] > 0 and "vertex cut x2" in d["gat"]["layout"]
