@@ -97,31 +97,100 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def host_threads():
+    """Threads for the CPU baselines: every core of the affinity mask, capped by a cgroup CPU
+    quota and by OMP_NUM_THREADS when the pool sets one (the GPU box sets 16: its CPU share
+    per GPU, while the affinity mask shows the whole machine)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    c = orc.usable_cores()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    c["omp_num_threads_env"] = int(omp) if omp and omp.isdigit() else None
+    if c["omp_num_threads_env"]:
+        c["threads"] = min(c["threads"], c["omp_num_threads_env"])
+    return c
+
+
 def cpu_baseline(g, F: int, budget_s: float = 20.0):
-    """Reference CPU aggregation on the host cores (rank 0, N=1 only)."""
+    """Reference CPU aggregation on the host cores (rank 0, N=1 only): the reference's own
+    gSpMM + wsumAgg (src/ops/aggregators.h:55-127) built -O3 -march=x86-64-v4 -fopenmp from
+    /root/reference (oracle/build_ref.sh), or the oracle restatement when that library is
+    absent.  Only the gSpMM call is timed: the value array (all ones, as readSM_npy32's
+    set_all(1) leaves it) and Y are allocated and prefaulted before, and Y is re-zeroed
+    outside the timed region (the generated code hands gSpMM a zero-filled output)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
-    og = orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col, None)
-    X = np.random.default_rng(1234).uniform(-1, 1, (g.n_cols, F)).astype(np.float32)
+    cores = host_threads()
+    n = cores["threads"]
     kind = "reference" if orc.ref_available() else "port"
-    fn = (lambda: orc.ref_gspmm(og, X)) if kind == "reference" else (lambda: orc.gspmm(og, X))
-    cores = orc.ref_threads() if kind == "reference" else int(os.environ.get("OMP_NUM_THREADS", os.cpu_count()))
+    val = np.ones(g.nnz, np.float32)
+    og = orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col, val)
+    X = np.random.default_rng(1234).uniform(-1, 1, (g.n_cols, F)).astype(np.float32)
+    Y = np.zeros((g.n_rows, F), np.float32)
+    if kind == "reference":
+        orc.ref_set_threads(n)
+        fn = lambda: orc.ref_gspmm(og, X, Y)  # noqa: E731
+    else:
+        orc.set_threads(n)
+        fn = lambda: orc.lib().orc_gspmm(orc._i64(og.n_rows), orc._ptr(og.rowptr), orc._ptr(og.col),  # noqa: E731
+                                         orc._ptr(val), orc._ptr(X), orc._i32(F), orc._ptr(Y))
     fn()  # warm-up
     times = []
     t_start = time.perf_counter()
     while len(times) < 5 and (time.perf_counter() - t_start) < budget_s:
+        Y.fill(0.0)
         t0 = time.perf_counter()
         fn()
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
-    return {"value": g.nnz / t, "unit": "edges/s", "cores": cores, "kind": kind, "cpu_model": cpu_model(),
+    return {"value": g.nnz / t, "unit": "edges/s", "cores": n, "kind": kind, "cpu_model": cpu_model(),
+            "host_cores": cores,
             "sample": f"{len(times)} full-graph F={F} SpMM calls (E={g.nnz}) after 1 warm-up, median "
-                      f"{t:.3f} s; " + ("reference gSpMM+wsumAgg (src/ops/aggregators.h) compiled from "
-                                        "/root/reference, OpenMP (oracle/_ref, shipped on purpose: "
-                                        "north_star asks for the reference CPU path timed in the same run)"
-                                        if kind == "reference"
-                                        else "oracle restatement of gSpMM, OpenMP")}
+                      f"{t:.3f} s, gSpMM call only (val and Y preallocated); " +
+                      ("reference gSpMM+wsumAgg (src/ops/aggregators.h) compiled -O3 -march=x86-64-v4 -fopenmp "
+                       "from /root/reference (oracle/_ref, shipped on purpose: north_star asks for the "
+                       "reference CPU path timed in the same run)"
+                       if kind == "reference" else "oracle restatement of gSpMM, OpenMP")}
+
+
+def gat_cpu_baseline(hg, X, dY, aL, wR, bR, heads, budget_s: float = 12.0):
+    """Host-CPU baseline of the SDDMM + edge-softmax half (rank 0, N = 1): the REF GAT layer,
+    forward + backward, as the reference composes it pass by pass (K5 sddvv, LeakyReLU,
+    exp/clamp, K7 row sum, reciprocal, K8 row scale, weighted K1 SpMM; backward SpMM on the
+    forward alpha, K9 sddmm, softmax backward, LeakyReLU backward, K7), restated in C with
+    OpenMP (oracle/gala_oracle.c orc_gat_ref_layer; the reference has no CPU code for these
+    kernels, so kind "port").  Same graph and inputs as the GPU "gat" step, on a bounded
+    sample: the first rows of the graph (all their edges, sources anywhere in X), sized so
+    one call takes about budget_s / 3; value = 2 * sampled edges / median call time."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    cores = host_threads()
+    orc.set_threads(cores["threads"])
+    rp = hg.rowptr
+
+    def rows_for(edges):
+        return max(1, min(hg.n_rows, int(np.searchsorted(rp, edges))))
+    k0 = rows_for(min(hg.nnz, 1 << 19))
+    cal = orc.GatRefLayer(rp, hg.col, k0, X, dY, aL, wR, bR, heads)
+    t0 = time.perf_counter()
+    cal.run()                                    # warm-up + rate estimate
+    rate = cal.nnz / max(time.perf_counter() - t0, 1e-6)
+    del cal
+    k = rows_for(int(rate * budget_s / 3))
+    layer = orc.GatRefLayer(rp, hg.col, k, X, dY, aL, wR, bR, heads)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        layer.run()
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": 2 * layer.nnz / t, "unit": "edges/s", "cores": cores["threads"], "kind": "port",
+            "cpu_model": cpu_model(), "host_cores": cores,
+            "sample": f"rows [0, {k}) of the graph ({layer.nnz} edges, {layer.nnz / hg.nnz:.1%} of E), "
+                      f"3 calls after a {k0}-row warm-up, median {t:.3f} s per forward + backward; "
+                      "oracle orc_gat_ref_layer: the reference's GAT pass sequence restated, OpenMP"}
 
 
 def load_traffic(kernel_substr: str):
@@ -560,12 +629,29 @@ def gat_layer(args, dg, hg, dev, timer, sync):
                         "kernel": "gala::k_gat_fwd<64,4,8,2,1,true,8> (gala_gat_fwd_stats_f32, 8 heads, F=256)",
                         "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json): 126 M "
                                         "gathered 1-KB X rows; at the measured HBM copy rate"}}
+    # backward stats kernel: rowptr + col + dY, Y, Ym read once + dX written + aL, aR, q,
+    # sum m*alpha read + d_aL written per row and head (dY[c] gathered per edge: traffic)
+    alg_b = 4 * (N + 1) + 4 * E + 4 * 4 * N * F + 5 * 4 * N * H
+    out["bwd_roofline"] = {"bound": "hbm", "achieved": alg_b / t_bwd / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                           "frac": alg_b / t_bwd / HBM_PEAK, "kernel_ms": t_bwd * 1e3, "alg_bytes_per_launch": alg_b,
+                           "traffic": load_traffic("k_gat_bwd_fused<64, 4, 8, 8, 1, false, true>"),
+                           "kernel": "gala::k_gat_bwd_fused<64,4,8,8,1,false,true> (gala_gat_bwd_stats_f32, 8 heads, "
+                                     "F=256)"}
     t_ceil = gather_ceiling(dg.col, X, timer)
     if t_ceil:
         out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
         out["roofline"]["frac_of_gather_ceiling"] = t_ceil / t_fwd
-    del st, X, dY
+        out["bwd_roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
+        out["bwd_roofline"]["frac_of_gather_ceiling"] = t_ceil / t_bwd
+    del st
     torch.cuda.empty_cache()
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = gat_cpu_baseline(hg, X.cpu().numpy(), dY.cpu().numpy(), aL.cpu().numpy(),
+                                                   wR.cpu().numpy(), bR.cpu().numpy(), H)
+        except Exception as e:  # the baseline is reported, never the target
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    del X, dY
     return out
 
 

@@ -24,6 +24,7 @@
  * n_seg == 1 with seg_base == NULL is a plain CSR.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -241,6 +242,105 @@ void orc_softmax_bwd(int64_t n_rows, int32_t n_seg, const int32_t *rowptr,
                 }
         }
 }
+
+/* ---- CPU baseline of the SDDMM + edge-softmax half ------------------------------------
+ * One REF GAT layer (single segment CSR, H heads of D features), forward + backward, pass
+ * by pass exactly as the generated program composes it, every pass an
+ * OpenMP loop over the rows [0, n_rows).  Each pass is the restatement of one reference
+ * kernel or torch op, with the rounding of the single-pass functions above, so the result
+ * is bit-identical to composing orc_sddvv / orc_softmax_fwd / orc_spmm / orc_sddmm /
+ * orc_softmax_bwd / orc_row_sum (tests/test_cpu_baseline.py):
+ *   forward   aR[r] = <X[r, head h], wR_h> + bR_h   attnR = efc(res), per head (common.h:1248-1260)
+ *             s = aL[r] + aR[c]                    K5 sddvv_plus   (cuda.h:679-698)
+ *             t = LeakyReLU(s)                     torch           (common.h:1175-1184)
+ *             p = clamp(exp(t), 0, 1e12)           torch exp, clamp (common.h:760-766)
+ *             rs = 1e-12 + sum_row p; q = 1/rs     K7 + reciprocal (cuda.h:505-524; common.h:767-770)
+ *             alpha = p * q                        K8 in place     (cuda.h:525-562)
+ *             Y[r] = sum alpha_e X[c]              K1 weighted     (cuda.h:286-358)
+ *   backward  dX[r] = sum alpha_e dY[c]            SpMM on slot 2li+1, forward alpha (common.h:835-894)
+ *             da_e = <dY[r], X[c]>                 K9 sddmm        (cuda.h:699-734)
+ *             sds = alpha*da; acc = 1e-12 + sum_row sds; res = acc*alpha; ds = sds - res
+ *                                                  softmax bwd     (common.h:791-799)
+ *             dt = where(s > 0, ds, ds*slope)      LeakyReLU bwd
+ *             daL[r] = 1e-12 + sum_row dt          K7              (cuda.h:505-524)
+ * aR must hold the rows >= n_rows already (orc_head_attn); the layer recomputes rows
+ * [0, n_rows) itself, so a row sample does a proportional share of that pass.  Edge
+ * buffers s, pa (t -> p -> alpha), da (da -> sds -> ds -> dt), res: [nnz(n_rows), H]. */
+void orc_head_attn(int64_t r0, int64_t r1, const float *X, int64_t ldx, int32_t H, int32_t D,
+                   const float *wR, const float *bR, float *aR) {
+#pragma omp parallel for schedule(static)
+    for (int64_t r = r0; r < r1; ++r)
+        for (int32_t h = 0; h < H; ++h) {
+            float acc = 0.0f;
+            for (int32_t k = 0; k < D; ++k) acc = fmaf(X[r * ldx + h * D + k], wR[h * D + k], acc);
+            aR[r * H + h] = acc + (bR ? bR[h] : 0.0f);
+        }
+}
+
+#define ROWS_OMP _Pragma("omp parallel for schedule(dynamic, 256)") for (int64_t r = 0; r < n_rows; ++r)
+#define EDGES for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e)
+
+void orc_gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col, int32_t H,
+                       int32_t D, const float *aL, const float *X, const float *wR,
+                       const float *bR, const float *dY, float slope, float *aR, float *s,
+                       float *pa, float *da, float *res, float *q, float *Y, float *dX,
+                       float *daL) {
+    const int32_t F = H * D;
+    orc_head_attn(0, n_rows, X, F, H, D, wR, bR, aR);
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) s[e * H + h] = aL[r * H + h] + aR[(int64_t)col[e] * H + h];
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) {
+        const float v = s[e * H + h];
+        pa[e * H + h] = v > 0.0f ? v : v * slope;
+    }
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) pa[e * H + h] = expf(pa[e * H + h]);
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) pa[e * H + h] = pa[e * H + h] > 1e12f ? 1e12f : pa[e * H + h];
+    ROWS_OMP for (int32_t h = 0; h < H; ++h) {
+        float local = 1e-12f;
+        EDGES local = local + pa[e * H + h];
+        q[r * H + h] = 0.0f + local;
+    }
+    ROWS_OMP for (int32_t h = 0; h < H; ++h) q[r * H + h] = 1.0f / q[r * H + h];
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) pa[e * H + h] = pa[e * H + h] * q[r * H + h];
+    ROWS_OMP for (int32_t f = 0; f < F; ++f) {
+        float local = 0.0f;
+        EDGES local = fmaf(pa[e * H + f / D], X[(int64_t)col[e] * F + f], local);
+        Y[r * F + f] = local;
+    }
+    /* backward */
+    ROWS_OMP for (int32_t f = 0; f < F; ++f) {
+        float local = 0.0f;
+        EDGES local = fmaf(pa[e * H + f / D], dY[(int64_t)col[e] * F + f], local);
+        dX[r * F + f] = local;
+    }
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) {
+        float local = 0.0f;
+        for (int32_t k = h * D; k < (h + 1) * D; ++k)
+            local = fmaf(dY[r * F + k], X[(int64_t)col[e] * F + k], local);
+        da[e * H + h] = local;
+    }
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) da[e * H + h] = pa[e * H + h] * da[e * H + h];
+    ROWS_OMP for (int32_t h = 0; h < H; ++h) {
+        float local = 1e-12f;
+        EDGES local = local + da[e * H + h];
+        daL[r * H + h] = 0.0f + local;             /* acc, parked in daL until the last pass */
+    }
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) res[e * H + h] = pa[e * H + h] * daL[r * H + h];
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) da[e * H + h] = da[e * H + h] - res[e * H + h];
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) {
+        const float d = da[e * H + h];
+        da[e * H + h] = s[e * H + h] > 0.0f ? d : d * slope;
+    }
+    ROWS_OMP for (int32_t h = 0; h < H; ++h) {
+        float local = 1e-12f;
+        EDGES local = local + da[e * H + h];
+        daL[r * H + h] = 0.0f + local;
+    }
+}
+#undef ROWS_OMP
+#undef EDGES
+
+/* OpenMP team size for the CPU-baseline loops (bench.py: every core the process may use) */
+void orc_set_threads(int n) { omp_set_num_threads(n); }
 
 /* ---- graph layout -------------------------------------------------------------------- */
 

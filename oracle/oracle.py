@@ -183,6 +183,73 @@ def gat_bwd(g: Graph, aL, aR, X, dY, alpha, heads=1, slope=0.2, mode=0):
     return dz, daL
 
 
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(ctypes.c_int(int(n)))
+
+
+def head_attn(X, wR, bR, heads, r0=0, r1=None, aR=None):
+    """aR[r, h] = <X[r, head h], wR_h> + bR_h for rows [r0, r1) (attnR = efc(res) per head)."""
+    X = np.ascontiguousarray(X, np.float32)
+    r1 = X.shape[0] if r1 is None else r1
+    if aR is None:
+        aR = np.zeros((X.shape[0], heads), np.float32)
+    lib().orc_head_attn(_i64(r0), _i64(r1), _ptr(X), _i64(X.shape[1]), _i32(heads),
+                        _i32(X.shape[1] // heads), _ptr(np.ascontiguousarray(wR, np.float32)),
+                        _ptr(None if bR is None else np.ascontiguousarray(bR, np.float32)), _ptr(aR))
+    return aR
+
+
+class GatRefLayer:
+    """CPU baseline of the SDDMM + edge-softmax half (orc_gat_ref_layer): one REF GAT layer,
+    forward + backward, pass by pass as the generated program composes it, over the rows
+    [0, n_rows) of a CSR graph (a row sample of it when n_rows < the graph's).  Buffers are
+    allocated (and prefaulted) once here; run() touches only them."""
+
+    def __init__(self, rowptr, col, n_rows, X, dY, aL, wR, bR, heads, slope=0.2):
+        self.rowptr = np.ascontiguousarray(rowptr, np.int32)
+        self.col = np.ascontiguousarray(col, np.int32)
+        self.n_rows, self.H = int(n_rows), int(heads)
+        self.X = np.ascontiguousarray(X, np.float32)
+        self.dY = np.ascontiguousarray(dY, np.float32)
+        self.aL = np.ascontiguousarray(aL, np.float32)
+        self.wR = np.ascontiguousarray(wR, np.float32)
+        self.bR = None if bR is None else np.ascontiguousarray(bR, np.float32)
+        self.F = self.X.shape[1]
+        self.slope = slope
+        ne = int(self.rowptr[self.n_rows]) * self.H
+        self.nnz = int(self.rowptr[self.n_rows])
+        # attention logits of every source row; run() recomputes rows [0, n_rows) itself
+        self.aR = head_attn(self.X, self.wR, self.bR, self.H)
+        self.s, self.pa, self.da, self.res = (np.ones(ne, np.float32) for _ in range(4))
+        self.q = np.ones((self.n_rows, self.H), np.float32)
+        self.daL = np.ones((self.n_rows, self.H), np.float32)
+        self.Y = np.ones((self.n_rows, self.F), np.float32)
+        self.dX = np.ones((self.n_rows, self.F), np.float32)
+
+    def run(self):
+        lib().orc_gat_ref_layer(_i64(self.n_rows), _ptr(self.rowptr), _ptr(self.col), _i32(self.H),
+                                _i32(self.F // self.H), _ptr(self.aL), _ptr(self.X), _ptr(self.wR),
+                                _ptr(self.bR), _ptr(self.dY), ctypes.c_float(self.slope), _ptr(self.aR),
+                                _ptr(self.s), _ptr(self.pa), _ptr(self.da), _ptr(self.res), _ptr(self.q),
+                                _ptr(self.Y), _ptr(self.dX), _ptr(self.daL))
+        return self
+
+
+def usable_cores() -> dict:
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU quota when
+    one is set (a container's share can be far below the machine's CPU count)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": aff, "cgroup_cpu_limit": quota,
+            "threads": min(aff, quota) if quota else aff}
+
+
 def csr_build(n_rows, src, dst):
     src = np.ascontiguousarray(src, np.int32)
     dst = np.ascontiguousarray(dst, np.int32)
@@ -303,3 +370,7 @@ def ref_mask_subgraphs(g: Graph, mask, levels):
 
 def ref_threads() -> int:
     return int(ref().ref_omp_threads())
+
+
+def ref_set_threads(n: int) -> None:
+    ref().ref_set_threads(ctypes.c_int(int(n)))

@@ -164,3 +164,6 @@ extern "C" int ref_mask_subgraphs(int nrows, int nnz, const int *rowptr, const i
 }
 
 extern "C" int ref_omp_threads(void) { return omp_get_max_threads(); }
+
+// the CPU baseline runs gSpMM on every core the process may use (bench.py picks the count)
+extern "C" void ref_set_threads(int n) { omp_set_num_threads(n); }
