@@ -16,11 +16,16 @@ namespace gala {
 // head's (max, sum) of the softmax (FIXED: online, relative to m; REF: plain sums).
 // kRefStats adds the row statistics' sums: accm = sum m*p*X and sma = sum m*p (m the
 // LeakyReLU factor of the edge), both scaled by q at the store like acc and sum.
+// self_row >= 0 (RC row statistics with ar_out): the row's own recomputed source logit is
+// captured from its self-loop edge (ar_self, has_self), so the row's X line is not re-read.
 template <int VEC, int CH>
 struct FwdState {
     float acc[CH][VEC], accm[CH][VEC];
     float m, sum, sma;
-    __device__ __forceinline__ FwdState() : m(-INFINITY), sum(0.0f), sma(0.0f) {
+    int64_t self_row;
+    float ar_self;
+    bool has_self;
+    __device__ __forceinline__ FwdState() : m(-INFINITY), sum(0.0f), sma(0.0f), self_row(-1), ar_self(0.0f), has_self(false) {
 #pragma unroll
         for (int ch = 0; ch < CH; ++ch)
 #pragma unroll
@@ -154,6 +159,18 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
             float all[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) all[k] = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, x[k]), gl_.wb);
+            if constexpr (MODE == kRefStats) {
+                // the self-loop edge's logit is the row's own aR: the same gathered row, lanes,
+                // fma order and butterfly as the X[row] recompute it replaces (bit-identical)
+                if (st.self_row >= 0) {
+#pragma unroll
+                    for (int k = 0; k < U; ++k)
+                        if (j0 + k < n && c[k] == st.self_row) {
+                            st.ar_self = all[k];
+                            st.has_self = true;
+                        }
+                }
+            }
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
                 float v = all[0];
@@ -310,31 +327,44 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
-    if constexpr (RC && MODE == kRefStats && HW > 0) {
-        // the row's own source logit, formed exactly as the per-edge recompute forms it
-        // (same lanes, same fma order and butterfly), for the backward's alpha
-        if (d.ar_out) {
-            typedef typename GVec<VEC>::T V;
-            V xr[CH];
+    constexpr bool kArOut = RC && MODE == kRefStats && HW > 0;
+    // the row's own source logit for the backward's alpha, formed exactly as the per-edge
+    // recompute forms it (same lanes, same fma order and butterfly): taken from the row's
+    // self-loop edge when it has one (every GALA graph does, gala_export_npy.py:73-74),
+    // else (and for hub rows, whose edges the chunk kernels walk) from a read of X[row]
+    auto ar_from_row = [&]() {
+        typedef typename GVec<VEC>::T V;
+        V xr[CH];
 #pragma unroll
-            for (int ch = 0; ch < CH; ++ch)
-                xr[ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + row * d.ldx + gl_.ln.off[ch]));
-            const float a = __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, xr), gl_.wb);
+        for (int ch = 0; ch < CH; ++ch)
+            xr[ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + row * d.ldx + gl_.ln.off[ch]));
+        return __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, xr), gl_.wb);
+    };
+    const bool hub = split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold;
+    if constexpr (kArOut) {
+        if (d.ar_out && hub) {
+            const float a = ar_from_row();
             if (gl_.leader) d.ar_out[row * gl_.H + gl_.hh] = a;
         }
     }
-    if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
-        return;  // hub row: k_gat_fwd_chunk / _fixup / k_gat_alpha_chunk
+    if (hub) return;  // hub row: k_gat_fwd_chunk / _fixup / k_gat_alpha_chunk
     const int H = gl_.H, D = gl_.D;
     // With H | G the main pass parks each (edge, head)'s exp term (REF) or logit (FIXED)
     // in alpha_out (the head's first lane writes it) and the alpha pass rescales it in
     // place: a contiguous re-read of the row instead of a second col -> aR gather.
     const bool park = d.alpha_out != nullptr && (G % H) == 0;
     FwdState<VEC, CH> st;
+    if constexpr (kArOut) st.self_row = d.ar_out ? row : -1;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         gat_fwd_edges<G, VEC, U, MODE, CH, RC, HW>(p, d, gl_, park, e0, e1, st);
+    }
+    if constexpr (kArOut) {
+        if (d.ar_out) {
+            const float a = st.has_self ? st.ar_self : ar_from_row();
+            if (gl_.leader) d.ar_out[row * gl_.H + gl_.hh] = a;
+        }
     }
     const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, p.seg.n, st);
     if (d.q_out && gl_.leader) d.q_out[row * H + gl_.hh] = q;  // factored: alpha = p * q

@@ -952,3 +952,34 @@ def test_head_attn(F, heads):
     assert np.array_equal(host(ops.head_attn_bwd(dev(g), dev(w), heads=heads)), m)
     dX0 = features(N, F, seed=75)
     assert np.array_equal(host(ops.head_attn_bwd(dev(g), dev(w), heads=heads, dX=dev(dX0))), dX0 + m)
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (256, 8), (64, 4)])
+@pytest.mark.parametrize("split", [False, True])
+def test_gat_row_stats_aR_from_self_loop(F, heads, split):
+    """The statistics forward takes each row's own recomputed source logit (aR_out) from
+    the row's self-loop edge instead of re-reading X[row]; rows without a self-loop (and hub
+    rows) read X[row].  Both paths must give the same bits: a graph with every self-loop and
+    the same graph with the self-loops of every other row removed give identical aR_out,
+    and the backward over either stays bit-identical to the per-edge recompute."""
+    g1 = powerlaw()
+    rows = np.repeat(np.arange(g1.n_rows), np.diff(g1.rowptr).astype(np.int64))
+    loops = rows == g1.col
+    assert loops.sum() == g1.n_rows                      # every row carries one self-loop
+    keep = ~(loops & (rows % 2 == 0))
+    g2 = layout.csr_build(g1.n_rows, g1.n_cols, rows[keep].astype(np.int32), g1.col[keep])
+    X = dev(features(g1.n_cols, F, seed=93))
+    dY = dev(features(g1.n_rows, F, seed=94))
+    aL = dev(features(g1.n_rows, heads, seed=91))
+    kw = dict(wR=dev(features(1, F, seed=95).ravel() * 0.5), bR=dev(features(1, heads, seed=96).ravel() * 0.1))
+    aRs = []
+    for g in (g1, g2):
+        dg = ops.DeviceGraph.from_host(g, split=False)
+        if split:
+            dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+        Y, q, Ym, sma, aRo = ops.gat_fwd_stats(dg, aL, X, heads=heads, want_aR=True, **kw)
+        dX, _ = ops.gat_bwd_stats(dg, aL, aRo, dY, q, Y, Ym, sma, heads=heads)
+        dX0, _ = ops.gat_bwd_fused(dg, aL, X, dY, q, heads=heads, **kw)
+        assert torch.equal(dX, dX0)
+        aRs.append(aRo)
+    assert torch.equal(aRs[0], aRs[1])

@@ -1,0 +1,70 @@
+#!/bin/bash
+# Parameterised GPU job for `gpurun`: each argument is one step, run in order; the job
+# stops at the first step that fails (and never starts another GPU step after a fault,
+# abort or time limit).  Output goes to gpurun_out/.
+#
+#   tests            python -m pytest tests -m gpu            -> gpurun_out/pytest_gpu.log
+#   tests=EXPR       ... -k EXPR
+#   bench            python bench.py (N = 1 defaults)        -> gpurun_out/bench.json (+ .log)
+#   bench=ARGS       python bench.py ARGS (spaces as commas)
+#   prof             rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/prof_stats/
+#   pmc              FETCH_SIZE and WRITE_SIZE passes (one --pmc run each) of bench.py, then
+#                    tools/pmc_traffic.py                   -> gpurun_out/traffic.json
+#   py=SCRIPT,ARGS   python SCRIPT ARGS                      -> gpurun_out/<script>.log
+#
+# e.g. gpurun --timeout 900 -- 'bash tools/gpu_job.sh tests=gat bench prof'
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline"
+
+step() {  # name, limit, command...
+    local name=$1 lim=$2
+    shift 2
+    echo "[gpu_job] $name: $*"
+    timeout -k 10 "$lim" "$@"
+    local rc=$?
+    echo "[gpu_job] $name rc=$rc"
+    return $rc
+}
+
+for s in "$@"; do
+    case "$s" in
+    tests)
+        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread \
+            > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+        tail -3 "$OUT/pytest_gpu.log" ;;
+    tests=*)
+        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "${s#tests=}" \
+            > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+        tail -3 "$OUT/pytest_gpu.log" ;;
+    bench)
+        step bench 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; }
+        cat "$OUT/bench.json" ;;
+    bench=*)
+        a="${s#bench=}"
+        step bench 900 python -u bench.py ${a//,/ } > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; }
+        cat "$OUT/bench.json" ;;
+    prof)
+        (cd /tmp && step prof 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o run \
+            -- python3 "$GRAFT_REPO_ROOT/bench.py" $BENCH_PROF_ARGS > "$OUT/prof_stats.log" 2>&1) || exit 1 ;;
+    pmc)
+        (cd /tmp && step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/prof_fetch" -o run \
+            -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_fetch.log" 2>&1) || exit 1
+        (cd /tmp && step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/prof_write" -o run \
+            -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_write.log" 2>&1) || exit 1
+        python3 tools/pmc_traffic.py "$OUT/prof_fetch" "$OUT/prof_write" "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1 ;;
+    py=*)
+        a="${s#py=}"
+        scr="${a%%,*}"
+        rest=""
+        [ "$a" != "$scr" ] && rest="${a#*,}"
+        step "$scr" 900 python -u $scr ${rest//,/ } > "$OUT/$(basename "$scr" .py).log" 2>&1 \
+            || { tail -30 "$OUT/$(basename "$scr" .py).log"; exit 1; }
+        tail -5 "$OUT/$(basename "$scr" .py).log" ;;
+    *)
+        echo "[gpu_job] unknown step $s"; exit 2 ;;
+    esac
+done
+echo "[gpu_job] done"
