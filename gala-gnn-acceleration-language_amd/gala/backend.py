@@ -59,11 +59,27 @@ class HipBackend:
         """[n, heads] per-head attention logits <X[:, head h], w_h> + b_h (gala_head_attn_f32)."""
         return self.ops.head_attn(X, w, b, heads=heads)
 
+    def head_attn_bwd(self, g, w, heads, dX):
+        """dX[:, head h] += g[:, h] * w[head h] (gala_head_attn_bwd_f32, accumulating)."""
+        return self.ops.head_attn_bwd(g.contiguous(), w, heads=heads, dX=dX, n_rows=dX.shape[0])
+
+    def head_linear_grads(self, X, g, heads):
+        """(dW [F], db [H]) of the per-head attention Linear, d logit g [n, H]: the block
+        diagonal of dense_grad's [H, F] (head h's weights are columns h*D:(h+1)*D)."""
+        full, db = self.ops.dense_grad(X, g.contiguous())
+        return _block_diag(full, heads), db
+
     def empty(self, *shape):
         return torch.empty(shape, device=self.device, dtype=torch.float32)
 
     def synchronize(self):
         torch.cuda.synchronize(self.device)
+
+
+def _block_diag(full, heads):
+    F = full.shape[1]
+    D = F // heads
+    return full.view(heads, heads, D).diagonal(0, 0, 1).t().reshape(F).contiguous()
 
 
 class CpuGraph:
@@ -149,6 +165,23 @@ class CpuBackend:
         _abi.call_cpu("gala_head_attn_f32", X.shape[0], X.shape[1], heads, _hp(X), X.stride(0), _hp(w), _hp(b),
                       _hp(out), None)
         return out
+
+    def head_attn_bwd(self, g, w, heads, dX):
+        g = g.contiguous()
+        _abi.call_cpu("gala_head_attn_bwd_f32", dX.shape[0], w.numel(), heads, _hp(g), _hp(w), _hp(dX), dX.stride(0),
+                      1, None)
+        return dX
+
+    def head_linear_grads(self, X, g, heads):
+        g = g.contiguous()
+        N, K = X.shape
+        full = torch.empty((heads, K), dtype=torch.float32)
+        db = torch.empty(heads, dtype=torch.float32)
+        wsb = int(_abi.cpu_lib().gala_cpu_dense_grad_workspace(N, K, heads))
+        ws = torch.empty(max(wsb // 4, 1), dtype=torch.float32)
+        _abi.call_cpu("gala_dense_grad_f32", N, K, heads, _hp(X), X.stride(0), _hp(g), heads, _hp(full), _hp(db), 0,
+                      _hp(ws), wsb, None)
+        return _block_diag(full, heads), db
 
     def empty(self, *shape):
         return torch.empty(shape, dtype=torch.float32)

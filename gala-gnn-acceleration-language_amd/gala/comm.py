@@ -75,6 +75,18 @@ class Comm:
         dist.all_to_all_single(ho, self._host(inp), group=self.group)
         self._back(out, ho)
 
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+        """Uneven all-to-all of rows: inp's blocks of in_splits[q] rows go to rank q, out
+        receives out_splits[q] rows from rank q (in rank order).  Async on RCCL."""
+        if self.rccl:
+            return dist.all_to_all_single(out, inp, output_split_sizes=list(out_splits),
+                                          input_split_sizes=list(in_splits), group=self.group, async_op=True)
+        ho = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(ho, self._host(inp), output_split_sizes=list(out_splits),
+                               input_split_sizes=list(in_splits), group=self.group)
+        self._back(out, ho)
+        return None
+
     def exchange(self, sends, recvs):
         """Grouped point-to-point: sends = [(tensor, peer)], recvs = [(tensor, peer)]."""
         if self.rccl:

@@ -19,12 +19,18 @@ gala.cu.  This runtime executes the same post-pass IR (galac --ir-json) instead:
     (lr 0.01, weight decay 5e-4, codegen/gala.cu:606-607).
   * `--layout vcut` is north_star's vertex cut instead (gala/vertex_cut.py
     VertexCutAggregator.apply): each rank holds the edges whose source it owns, computes
-    partial rows for every destination and one RCCL reduce-scatter sums them into the
-    owners' rows -- no halo; the sums regroup per rank, so results agree with one GPU to
-    fp32 rounding.
+    partial rows for every destination and one RCCL reduce-scatter (`--exchange dense`) or
+    an all-to-all of only the rows it holds edges of (`sparse`; `auto` picks by the graph's
+    touched fraction) sums them into the owners' rows -- no halo; the sums regroup per
+    rank, so results agree with one GPU to fp32 rounding.
+  * GAT programs (GAT_AGGREGATE, REF softmax; config 3's gat_heads(H) included) run on the
+    vertex cut: each GAT layer is a VertexCutGat training pair wrapped as an autograd
+    Function (row-statistics forward, REF backward with dX, d_aL and, when the source logit
+    is the layer's attention Linear of X, that Linear's gradients); per-head attention
+    Linears (gat_heads) are the block-diagonal `HeadLinear`.
 Training subgraphs (graph g > 0) run on the whole graph: they only drop rows no training
 row depends on, so the training rows' values are unchanged.  The column-tiled layout
-(col_tile) is a single-device layout and is not used.  GAT layers are not supported here.
+(col_tile) is a single-device layout and is not used.
 """
 from __future__ import annotations
 
@@ -54,7 +60,7 @@ SHAPES = {
     "Papers100M": (111059956, 807842936, 128, 172, 0.011),
 }
 SUPPORTED = {"INPUT", "DEGREES", "POWER", "ROW_BROADCAST", "GCN_AGGREGATE", "AGGREGATE_MUL_SUM", "FFN", "RELU",
-             "ADD", "SCALAR_ADD_EPS_MULTIPLY"}
+             "ADD", "SCALAR_ADD_EPS_MULTIPLY", "GAT_AGGREGATE"}
 
 
 def _hash_uniform(rows: np.ndarray, cols: int, seed: int) -> np.ndarray:
@@ -87,16 +93,70 @@ class _Agg(torch.autograd.Function):
         return dx, None, None, None
 
 
+class HeadLinear(torch.nn.Module):
+    """gat_heads(H)'s attention vector Linear(F, 1) per head: out[:, h] = <x[:, head h],
+    w[head h]> + b[h] (weight [1, F], bias [H]; galac's HeadAttn, tests/_ir_ref.py _ffn)."""
+
+    def __init__(self, in_features: int, heads: int):
+        super().__init__()
+        k = 1.0 / np.sqrt(in_features // heads)
+        self.heads = heads
+        self.weight = torch.nn.Parameter(torch.empty(1, in_features).uniform_(-k, k))
+        self.bias = torch.nn.Parameter(torch.empty(heads).uniform_(-k, k))
+
+    def forward(self, x):
+        n, F = x.shape
+        H = self.heads
+        return (x.view(n, H, F // H) * self.weight.view(1, H, F // H)).sum(2) + self.bias.view(1, H)
+
+
+class _VcutGatFfn(torch.autograd.Function):
+    """GAT aggregation over the vertex cut with the source logit recomputed from x (the
+    DSL's attnR = ffn(res, out=1) of the aggregated res): inputs aL [n, H], x [n, F], the
+    attention Linear's w [1, F] and b [H]; REF backward (VertexCutGat.backward)."""
+
+    @staticmethod
+    def forward(ctx, aL, x, w, b, layer):
+        ctx.layer = layer
+        return layer.forward_train(aL.detach().contiguous(), None, x.detach().contiguous(),
+                                   w.detach().reshape(-1).contiguous(), b.detach().reshape(-1).contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        dX, d_aL, dW, db = ctx.layer.backward(dy.contiguous())
+        return d_aL, dX, dW.view(1, -1), db.view(-1), None
+
+
+class _VcutGat(torch.autograd.Function):
+    """GAT aggregation over the vertex cut with a given source logit aR [n, H]; the REF
+    backward returns the row sums as both d_aL and d_aR (common.h:622-675)."""
+
+    @staticmethod
+    def forward(ctx, aL, aR, x, layer):
+        ctx.layer = layer
+        return layer.forward_train(aL.detach().contiguous(), aR.detach().contiguous(), x.detach().contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        dX, d_aL = ctx.layer.backward(dy.contiguous())
+        return d_aL, d_aL.clone(), dX, None
+
+
 class Program:
     """One rank's share of a galac program (post-pass IR)."""
 
     def __init__(self, ir: dict, graph: layout.HostGraph, X_own: torch.Tensor, labels_own: torch.Tensor,
                  train_own: torch.Tensor, rank: int, world: int, device, seed: int = 0, group=None,
-                 layout_mode: str = "halo"):
+                 layout_mode: str = "halo", exchange: str = "auto"):
         ops = {nd["op"] for nd in ir["nodes"]}
         bad = ops - SUPPORTED
         if bad:
-            raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE programs)")
+            raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE / GAT programs)")
+        if "GAT_AGGREGATE" in ops:
+            if layout_mode != "vcut":
+                raise NotImplementedError("gala.dist_run: GAT programs run on the vertex cut (--layout vcut)")
+            if ir["sched"].get("gat_mode", 0) != 0:
+                raise NotImplementedError("gala.dist_run: FIXED-mode GAT (its backward needs A^T)")
         if not ir["sched"]["undirected"]:
             raise NotImplementedError("gala.dist_run: directed programs (the backward needs A^T)")
         if ir["sched"]["kernel_sample"] or ir["sched"]["data_sample"]:
@@ -108,8 +168,9 @@ class Program:
         self.layout = layout_mode
         if layout_mode == "vcut":
             from . import vertex_cut as vc
-            self.part = vc.vertex_cut_partition(graph, rank, world)
+            self.part = vc.vertex_cut_partition(graph, rank, world, exchange=exchange)
             self.agg = vc.VertexCutAggregator(self.part, 1, self.be, self.comm)
+            self._gat = {}
             own_rowptr = self.part.deg_graph.rowptr
         elif layout_mode == "halo":
             self.part = gdist.partition_graph(graph, rank, world)
@@ -124,7 +185,9 @@ class Program:
         self.params = {}
         self.modules = torch.nn.ModuleDict()
         for w in ir["weights"]:
-            if w["type"] == "linear":
+            if w["type"] == "linear" and int(w.get("heads", 1)) > 1 and w["out"] == 1:
+                self.modules[w["name"]] = HeadLinear(w["in"], int(w["heads"]))
+            elif w["type"] == "linear":
                 self.modules[w["name"]] = torch.nn.Linear(w["in"], w["out"])
             else:
                 self.modules[w["name"]] = torch.nn.ParameterList([torch.nn.Parameter(torch.tensor([float(w["init"])]))])
@@ -142,6 +205,14 @@ class Program:
 
     def _vec(self, v):
         return None if v is None else v.reshape(-1).contiguous()
+
+    def _gat_layer(self, nd, F, H):
+        """The VertexCutGat of one GAT_AGGREGATE node (its buffers are width-specific)."""
+        from . import vertex_cut as vc
+        key = nd["out"]
+        if key not in self._gat:
+            self._gat[key] = vc.VertexCutGat(self.part, F, H, self.be, self.comm, slope=float(nd["param"]))
+        return self._gat[key]
 
     def forward(self):
         vals = {}
@@ -168,6 +239,16 @@ class Program:
                 y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
             elif op == "AGGREGATE_MUL_SUM":
                 y = _Agg.apply(a[0], self.agg, None, None)
+            elif op == "GAT_AGGREGATE":
+                aL, x = a[0], a[2]
+                n = x.shape[0]
+                H = aL.numel() // max(n, 1)
+                layer = self._gat_layer(nd, x.shape[1], H)
+                if nd["weight"]:     # gat_aggregate_ffn: attnR = the Linear of x, recomputed
+                    m = self.modules[nd["weight"]]
+                    y = _VcutGatFfn.apply(aL.reshape(n, H), x, m.weight, m.bias, layer)
+                else:
+                    y = _VcutGat.apply(aL.reshape(n, H), a[1].reshape(n, H), x, layer)
             elif op == "FFN":
                 y = self.modules[nd["weight"]](a[0])
             elif op == "RELU":
@@ -212,6 +293,8 @@ def main(argv=None):
     ap.add_argument("--dump", help="rank 0 writes an npz: predictions (all rows), losses, rowptr/col")
     ap.add_argument("--layout", default="halo", choices=["halo", "vcut"],
                     help="halo: row partition + exact halo SpMM; vcut: vertex cut + reduce-scatter")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "dense", "sparse"],
+                    help="vcut: dense reduce-scatter, sparse DCSR all-to-all, or auto (touched fraction)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,7 +338,8 @@ def main(argv=None):
         labels = lab_all[r0:r1].astype(np.int64)
         train = tr_all[r0:r1] > 0
     prog = Program(ir, g, torch.from_numpy(X).to(dev), torch.from_numpy(labels).to(dev),
-                   torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed, layout_mode=args.layout)
+                   torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed, layout_mode=args.layout,
+                   exchange=args.exchange)
     init_weights = {k: v.detach().cpu().numpy().tolist() for k, v in prog.modules.state_dict().items()}
     opt = torch.optim.Adam(prog.modules.parameters(), lr=0.01, weight_decay=5e-4)
     iters = args.iters if args.iters is not None else max(int(s.get("iterations", 0)), 1)
@@ -301,6 +385,7 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps({"ranks": world, "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,
                           "halo": prog.part.halo_mode if args.layout == "halo" else None,
+                          "exchange": prog.part.exchange if args.layout == "vcut" else None,
                           "fwd_mean_s": float(np.mean(fwd_t[keep])), "epoch_mean_s": float(np.mean(ep_t[keep])),
                           "loss_first": losses[0], "loss_last": losses[-1]}), flush=True)
         print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)

@@ -21,6 +21,17 @@ def powerlaw(n=4096, m=30000, seed=7) -> layout.HostGraph:
     return layout.gen_graph("rmat", n, m, seed)
 
 
+def banded(n=3000, width=40, per_row=6, seed=5) -> layout.HostGraph:
+    """Symmetric graph with locality: every edge joins vertices at most `width` apart, plus
+    self loops (a few vertex ranges touch each row: the sparse vertex-cut exchange)."""
+    rng = np.random.default_rng(seed)
+    u = np.repeat(np.arange(n, dtype=np.int64), per_row)
+    v = np.clip(u + rng.integers(-width, width + 1, u.shape[0]), 0, n - 1)
+    src = np.concatenate([u, v, np.arange(n)]).astype(np.int32)
+    dst = np.concatenate([v, u, np.arange(n)]).astype(np.int32)
+    return layout.csr_build(n, n, src, dst)
+
+
 def with_empty_rows(n=700, m=3000, seed=3) -> layout.HostGraph:
     """Directed random graph (no self loops) with a block of empty rows + one heavy row."""
     rng = np.random.default_rng(seed)

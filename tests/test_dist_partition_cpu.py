@@ -21,10 +21,10 @@ import torch.multiprocessing as mp
 from gala import dist as gdist, layout, vertex_cut as vc
 from gala.backend import CpuBackend
 from gala.comm import Comm
-from _graphs import cora_like, features, powerlaw, with_empty_rows
+from _graphs import banded, cora_like, features, powerlaw, with_empty_rows
 
 F = 12
-GRAPHS = {"cora": cora_like, "powerlaw": powerlaw, "empty_rows": with_empty_rows}
+GRAPHS = {"cora": cora_like, "powerlaw": powerlaw, "empty_rows": with_empty_rows, "banded": banded}
 
 
 def _one_process(g, X, layers=2):
@@ -128,11 +128,12 @@ def test_vertex_cut_layout(name, world, chunks):
     for p in range(world):
         pt = vc.vertex_cut_partition(g, p, world, chunks=chunks)
         c, P = pt.block, world
-        assert pt.chunks == chunks and len(pt.chunk_graphs) == chunks
+        assert pt.chunks == chunks and len(pt.chunk_graphs) == chunks and pt.exchange == "dense"
         assert c * chunks >= int(np.diff(pt.bounds).max())
-        # degree graph: own rows' full degrees
-        np.testing.assert_array_equal(np.diff(pt.deg_graph.rowptr),
-                                      np.diff(g.rowptr)[pt.r0:pt.r0 + pt.n])
+        # degree graph: the own rows' full CSR (rowptr and col of matching length)
+        dg = pt.deg_graph
+        np.testing.assert_array_equal(np.diff(dg.rowptr), np.diff(g.rowptr)[pt.r0:pt.r0 + pt.n])
+        assert int(dg.rowptr[-1]) == dg.nnz
         total = 0
         for k, h in enumerate(pt.chunk_graphs):
             assert h.n_rows == P * c and h.n_cols == pt.n
@@ -153,9 +154,75 @@ def test_vertex_cut_layout(name, world, chunks):
     np.testing.assert_array_equal(allp[:, key(allp)], ref[:, key(ref)])
 
 
+@pytest.mark.parametrize("name", list(GRAPHS))
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (3, 2), (4, 3)])
+def test_vertex_cut_sparse_layout(name, world, chunks):
+    """DCSR send rows + receive CSR: a rank sends exactly the destination rows it holds
+    edges of (owner-major, ascending), every edge is held once, and what each owner's
+    receive CSR expects from source q in chunk k is what q sends it, row for row."""
+    g = GRAPHS[name]()
+    parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks, exchange="sparse") for p in range(world)]
+    rows_all = np.repeat(np.arange(g.n_rows), np.diff(g.rowptr))
+    seen = []
+    sent = {}                                     # (src, dst, k) -> global rows sent, in order
+    for pt in parts:
+        sp, p = pt.sparse, pt.rank
+        assert pt.exchange == "sparse" and len(sp.send_graphs) == chunks
+        for k, h in enumerate(sp.send_graphs):
+            rows = np.flatnonzero(np.repeat(True, h.n_rows))
+            # recover the compact rows' global ids from their dense-layout positions
+            d = sp.send_dense_rows[k] - k * world * pt.block
+            q, j = d // pt.block, k * pt.block + d % pt.block
+            grow = pt.bounds[q] + j
+            assert np.all(np.diff(grow) > 0)                          # owner-major, ascending
+            assert np.all(np.diff(h.rowptr) > 0)                      # only rows with a held edge
+            np.testing.assert_array_equal(np.bincount(q, minlength=world), sp.send_counts[k])
+            er = np.repeat(grow, np.diff(h.rowptr))
+            seen.append(np.stack([er, h.col.astype(np.int64) + pt.r0]))
+            for qq in range(world):
+                sent[(p, qq, k)] = grow[q == qq]
+        assert sum(h.nnz for h in sp.send_graphs) == pt.nnz
+    allp = np.concatenate(seen, axis=1)
+    ref = np.stack([rows_all, g.col.astype(np.int64)])
+    key = lambda a: np.lexsort((a[1], a[0]))  # noqa: E731
+    np.testing.assert_array_equal(allp[:, key(allp)], ref[:, key(ref)])
+    for pt in parts:                              # the receive side matches the senders
+        sp, p = pt.sparse, pt.rank
+        base = 0
+        slot_row = {}
+        for k in range(chunks):
+            for q in range(world):
+                blk = sent[(q, p, k)]
+                assert blk.shape[0] == sp.recv_counts[k, q]
+                for i, r in enumerate(blk):
+                    slot_row[base + i] = (int(r), q)
+                base += blk.shape[0]
+        rg = sp.recv_graph
+        assert rg.n_rows == pt.n
+        for r in range(pt.n):
+            ent = [slot_row[int(x)] for x in rg.col[rg.rowptr[r]:rg.rowptr[r + 1]]]
+            assert all(gr == pt.r0 + r for gr, _ in ent)
+            srcs = [q for _, q in ent]
+            assert srcs == sorted(set(srcs))                          # source-rank order, once each
+
+
+def test_touched_fraction_and_auto_exchange():
+    g = banded()
+    b = gdist.row_bounds(g.rowptr, 4)
+    f = vc.touched_fraction(g, b)
+    assert 0 < f < 0.1                                  # locality: few remote (row, rank) pairs
+    assert vc.vertex_cut_partition(g, 0, 4, exchange="auto").exchange == "sparse"
+    u = cora_like()
+    assert vc.touched_fraction(u, gdist.row_bounds(u.rowptr, 2)) > 0.5
+    assert vc.vertex_cut_partition(u, 0, 2, exchange="auto").exchange == "dense"
+    pt = vc.vertex_cut_partition(g, 1, 4, exchange="sparse")
+    assert pt.comm_bytes(F) < vc.vertex_cut_partition(g, 1, 4).comm_bytes(F) / 5
+
+
 # ---- gloo ranks -----------------------------------------------------------------------------
 MODES = [("p2p", 1, True), ("p2p", 1, False), ("dense", 1, True), ("dense", 1, False),
-         ("dense", 3, False), ("vcut", 1, None), ("vcut", 3, None)]
+         ("dense", 3, False), ("vcut", 1, None), ("vcut", 3, None), ("vcut-sparse", 1, None),
+         ("vcut-sparse", 3, None)]
 
 
 def _worker(rank, world, port, name, q):
@@ -167,8 +234,9 @@ def _worker(rank, world, port, name, q):
         be, comm = CpuBackend(), Comm()
         res = {}
         for mode, chunks, exact in MODES:
-            if mode == "vcut":
-                pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+            if mode.startswith("vcut"):
+                ex = "sparse" if mode == "vcut-sparse" else "dense"
+                pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks, exchange=ex)
                 agg = vc.VertexCutAggregator(pt, F, be, comm)
             else:
                 pt = gdist.partition_graph(g, rank, world, halo_mode=mode, chunks=chunks)
@@ -203,7 +271,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,name", [(2, "powerlaw"), (3, "cora"), (3, "empty_rows")])
+@pytest.mark.parametrize("world,name", [(2, "powerlaw"), (3, "cora"), (3, "empty_rows"), (3, "banded")])
 def test_distributed_aggregation_matches_one_process(world, name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -219,7 +287,7 @@ def test_distributed_aggregation_matches_one_process(world, name):
     ref = _one_process(g, features(g.n_rows, F, seed=11))
     for key, (got, hb) in res.items():
         mode, chunks, exact = key
-        assert hb > 0, key
+        assert hb > 0 or (mode == "vcut-sparse" and name == "banded"), key
         for layer in range(2):
             if exact:
                 np.testing.assert_array_equal(got[layer], ref[layer], err_msg=str(key))  # bit-identical
@@ -249,13 +317,13 @@ def _gat_one_process(g):
     return Y.numpy()
 
 
-def _gat_worker(rank, world, port, name, chunks, q):
+def _gat_worker(rank, world, port, name, chunks, q, exchange="dense"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = GRAPHS[name]()
         aL, aR, X = _gat_inputs(g)
-        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks, exchange=exchange)
         own = slice(pt.r0, pt.r0 + pt.n)
         gat = vc.VertexCutGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
         Y = gat(torch.from_numpy(aL[own].copy()), torch.from_numpy(aR[own].copy()), torch.from_numpy(X[own].copy()))
@@ -270,15 +338,17 @@ def _gat_worker(rank, world, port, name, chunks, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name,chunks", [(2, "powerlaw", 1), (3, "cora", 2), (3, "empty_rows", 1)])
-def test_vertex_cut_gat_matches_one_process(world, name, chunks):
+@pytest.mark.parametrize("world,name,chunks,exchange", [(2, "powerlaw", 1, "dense"), (3, "cora", 2, "dense"),
+                                                        (3, "empty_rows", 1, "dense"), (2, "powerlaw", 2, "sparse"),
+                                                        (3, "banded", 2, "sparse")])
+def test_vertex_cut_gat_matches_one_process(world, name, chunks, exchange):
     """REF GAT forward with column ownership (VertexCutGat): per-rank unnormalised partial
     rows and softmax sums (GALA_GAT_PARTIAL on the host-CPU backend), reduce-scattered to
     the row owners, equal the one-process fused forward within fp32 rounding."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, name, chunks, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, name, chunks, q, exchange)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -297,7 +367,8 @@ def _gat_attn_weights():
 
 def _gat_train_one_process(g, rc=False):
     """Y, dX, d_aL of the REF layer on one process (gala_cpu_gat_{fwd,bwd}_stats_f32); rc:
-    the source logits recomputed from X (wR, bR)."""
+    the source logits recomputed from X (wR, bR), dX then including the path through aR
+    (d_aR = d_aL in REF mode), plus the Linear's gradients dwR, dbR."""
     from gala import _abi
     aL, aR, X = _gat_inputs(g)
     wR, bR = _gat_attn_weights()
@@ -314,26 +385,40 @@ def _gat_train_one_process(g, rc=False):
     aR_b = aRo.view(n, H_GAT) if rc else torch.from_numpy(aR)
     dX, d_aL = be.gat_bwd_stats(cg, torch.from_numpy(aL), aR_b, torch.from_numpy(dY), q, Y, Ym,
                                 sma, H_GAT, 0.2)
-    return Y.numpy(), dX.numpy(), d_aL.view(n, H_GAT).numpy()
+    d_aL = d_aL.view(n, H_GAT).numpy()
+    out = [Y.numpy(), dX.numpy(), d_aL]
+    if rc:   # float64 restatement of the Linear's backward over all rows
+        D = F_GAT // H_GAT
+        g64 = d_aL.astype(np.float64)
+        dX = dX.numpy().astype(np.float64) + np.repeat(g64, D, 1) * np.tile(wR.astype(np.float64), 1)
+        out[1] = dX
+        dW = (np.repeat(g64, D, 1) * X.astype(np.float64)).sum(0)
+        out += [dW, g64.sum(0)]
+    return out
 
 
-def _gat_train_worker(rank, world, port, name, chunks, q, rc=False):
+def _gat_train_worker(rank, world, port, name, chunks, q, rc=False, exchange="dense"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = GRAPHS[name]()
         aL, aR, X = _gat_inputs(g)
         dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
-        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks)
+        pt = vc.vertex_cut_partition(g, rank, world, chunks=chunks, exchange=exchange)
         own = slice(pt.r0, pt.r0 + pt.n)
         gat = vc.VertexCutGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
         t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
+        grads = []
         if rc:
             wR, bR = _gat_attn_weights()
             Y = gat.forward_train(t(aL), None, t(X), torch.from_numpy(wR), torch.from_numpy(bR))
+            dX, d_aL, dW, db = gat.backward(t(dY))
+            for G in (dW, db):                  # the caller's all-reduce of the Linear's grads
+                dist.all_reduce(G)
+                grads.append(G.numpy().copy())
         else:
             Y = gat.forward_train(t(aL), t(aR), t(X))
-        dX, d_aL = gat.backward(t(dY))
+            dX, d_aL = gat.backward(t(dY))
         sizes = [int(pt.bounds[r + 1] - pt.bounds[r]) for r in range(world)]
         out = []
         for T in (Y, dX, d_aL):
@@ -343,22 +428,26 @@ def _gat_train_worker(rank, world, port, name, chunks, q, rc=False):
             dist.all_gather(ts, pad)
             out.append(torch.cat([x[:s] for x, s in zip(ts, sizes)]).numpy())
         if rank == 0:
-            q.put(out)
+            q.put(out + grads)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name,chunks,rc", [(1, "cora", 2, False), (2, "powerlaw", 1, False),
-                                                   (3, "cora", 2, False), (3, "empty_rows", 1, False),
-                                                   (2, "cora", 1, True), (3, "powerlaw", 2, True)])
-def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc):
+@pytest.mark.parametrize("world,name,chunks,rc,exchange",
+                         [(1, "cora", 2, False, "dense"), (2, "powerlaw", 1, False, "dense"),
+                          (3, "cora", 2, False, "dense"), (3, "empty_rows", 1, False, "dense"),
+                          (2, "cora", 1, True, "dense"), (3, "powerlaw", 2, True, "dense"),
+                          (2, "powerlaw", 2, False, "sparse"), (3, "banded", 2, True, "sparse")])
+def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc, exchange):
     """VertexCutGat.forward_train / backward (gala_gat_fwd_partial_stats_f32 partials, one
-    reduce-scatter per direction, d_aL from the owner's row statistics) against the
-    one-process row-statistics pair: Y, dX and d_aL within fp32 rounding."""
+    exchange per direction, d_aL from the owner's row statistics) against the one-process
+    row-statistics pair: Y, dX and d_aL within fp32 rounding; with the source logits
+    recomputed, dX includes the path through aR and the Linear's gradients match."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gat_train_worker, args=(r, world, port, name, chunks, q, rc)) for r in range(world)]
+    procs = [ctx.Process(target=_gat_train_worker, args=(r, world, port, name, chunks, q, rc, exchange))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -366,5 +455,5 @@ def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc):
         p.join(timeout=60)
         assert p.exitcode == 0
     ref = _gat_train_one_process(GRAPHS[name](), rc)
-    for a, b, what in zip(got, ref, ("Y", "dX", "d_aL")):
-        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5, err_msg=what)
+    for a, b, what in zip(got, ref, ("Y", "dX", "d_aL", "dwR", "dbR")):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4, err_msg=what)

@@ -22,10 +22,10 @@ BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline"
 step() {  # name, limit, command...
     local name=$1 lim=$2
     shift 2
-    echo "[gpu_job] $name: $*"
+    echo "[gpu_job] $name: $*" >&2
     timeout -k 10 "$lim" "$@"
     local rc=$?
-    echo "[gpu_job] $name rc=$rc"
+    echo "[gpu_job] $name rc=$rc" >&2
     return $rc
 }
 
