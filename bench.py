@@ -339,39 +339,27 @@ class VcutMode:
         self.be, self.comm, self.F = be, comm, F
 
     def kernel(self, timer):
-        a, p = self.agg, self.part
-        rows = p.world * p.block
-
-        def run():
-            for k, gk in enumerate(a.graphs):
-                self.be.spmm(gk, a.Xs, a.partial[k * rows:(k + 1) * rows], None, False)
-        t = timer(run, 10)
-        nnz = sum(h.nnz for h in p.chunk_graphs)
-        alg = 4 * (p.partial_rows() + p.chunks) + 4 * nnz + 4 * p.n * self.F + 4 * p.partial_rows() * self.F
+        """(seconds, algorithmic bytes) of the rank's partial-row SpMMs (every chunk)."""
+        p = self.part
+        t = timer(lambda: self.agg.local_spmm(), 10)
+        rows = p.partial_rows()
+        alg = 4 * (rows + p.chunks) + 4 * p.chunk_nnz() + 4 * p.n * self.F + 4 * rows * self.F
         return t, alg
 
     def exchange(self, timer):
-        a, p = self.agg, self.part
-        rows, c = p.world * p.block, p.block
-
-        def run():
-            self.comm.wait([self.comm.reduce_scatter(a.S[k * c:(k + 1) * c], a.partial[k * rows:(k + 1) * rows])
-                            for k in range(p.chunks)])
-        return timer(run, 5)
+        return timer(lambda: self.agg.exchange_only(), 5)
 
 
-def run_multi(args, rank, world, dev, be, timer, sync):
-    import numpy as np
+def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max):
+    """Strong scaling of one Products-shaped graph of family `kind` over the ranks: every
+    candidate layout timed for a few steps, the timed steps on the fastest.  Returns
+    (result fields, graph, bounds)."""
     import torch
-    import torch.distributed as dist
     from gala import dist as gdist, vertex_cut as vc
-    from gala.comm import Comm
-
-    comm = Comm()
     F = args.F
     t0 = time.time()
-    g = products_graph("uniform", args.scale)
-    log(f"[rank {rank}/{world}] graph N={g.n_rows} E={g.nnz} built in {time.time() - t0:.1f}s")
+    g = products_graph(kind, args.scale)
+    log(f"[rank {rank}/{world}] {kind} graph N={g.n_rows} E={g.nnz} built in {time.time() - t0:.1f}s")
     bounds = gdist.row_bounds(g.rowptr, world)
     t0 = time.time()
     modes = []
@@ -383,10 +371,15 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         modes.append(HaloMode("halo-pipe", ptk, F, be, comm, exact=False))
     modes.append(VcutMode("vcut", vc.vertex_cut_partition(g, rank, world, 1, bounds), F, be, comm))
     modes.append(VcutMode("vcut-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds), F, be, comm))
-    log(f"[rank {rank}] partitions ({[m.name for m in modes]}, halo {pt1.halo_mode}, "
-        f"{pt1.n_halo_rows} halo rows) in {time.time() - t0:.1f}s")
-    n = pt1.n
-    r0 = pt1.r0
+    frac = vc.touched_fraction(g, bounds) if world > 1 else 0.0
+    if frac < 0.9:      # the DCSR exchange can only win when some partial rows are empty
+        modes.append(VcutMode("vcut-sparse", vc.vertex_cut_partition(g, rank, world, 1, bounds, "sparse"), F, be,
+                              comm))
+        modes.append(VcutMode("vcut-sparse-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds,
+                                                                         "sparse"), F, be, comm))
+    log(f"[rank {rank}] {kind} partitions ({[m.name for m in modes]}, halo {pt1.halo_mode}, "
+        f"{pt1.n_halo_rows} halo rows, touched fraction {frac:.3f}) in {time.time() - t0:.1f}s")
+    n, r0 = pt1.n, pt1.r0
     gen = torch.Generator(device=dev).manual_seed(1234)
     # every rank draws the whole X so row r is the same on any number of ranks
     Xall = torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1
@@ -394,6 +387,54 @@ def run_multi(args, rank, world, dev, be, timer, sync):
     dY = (torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1)[r0:r0 + n].clone()
     del Xall
     bufs = [be.empty(n, F) for _ in range(4)]
+    cand = {}
+    for m in modes:
+        st = make_step(m.agg, X, dY, bufs)
+        cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
+        log(f"[rank {rank}] {kind} candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
+    forced = os.environ.get("GALA_DIST_MODE")
+    name = forced if forced in cand else min(cand, key=cand.get)
+    best = next(m for m in modes if m.name == name)
+    t_step = timed_steps(make_step(best.agg, X, dY, bufs), args.steps if kind == "uniform" else max(args.steps // 2, 2),
+                         args.warmup if kind == "uniform" else 2, sync, barrier, reduce_max)
+    t_kernel, alg = best.kernel(timer)
+    t_ex = best.exchange(timer) if world > 1 else 0.0
+    out = {"value": 4 * g.nnz / t_step, "ms_per_step": t_step * 1e3,
+           "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": alg / t_kernel / HBM_PEAK, "traffic": None,
+                        "kernel": f"gala::k_spmm_rowgroup (rank 0's SpMM launches of mode {best.name})",
+                        "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg},
+           "comm": {"mode": best.name, "backend": dist_backend(),
+                    "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
+                    "halo_bytes_per_aggregation_per_rank": best.agg.halo_bytes(),
+                    "exchange_ms_per_aggregation": t_ex * 1e3,
+                    "spmm_ms_per_aggregation": t_kernel * 1e3,
+                    "halo_layout": pt1.halo_mode, "halo_rows_rank0": pt1.n_halo_rows,
+                    "vcut_touched_fraction": frac,
+                    "note": "halo-exact is bit-identical to one GPU; the other modes agree to fp32 rounding. "
+                            "Exchange time is the collective(s) of one aggregation alone; it overlaps the SpMM "
+                            "in the -overlap/-pipe modes. vcut-sparse: DCSR partial rows (only rows with a held "
+                            "edge) sent by all-to-all, timed when the touched fraction is below 0.9."}}
+    if comm.rccl:
+        out["comm"]["rccl_note"] = "RCCL collectives over the node's GPUs"
+    else:
+        out["comm"]["rccl_note"] = f"{dist_backend()} rehearsal: host-staged collectives, not RCCL over xGMI"
+    del modes, best, bufs, X, dY
+    return out, g, bounds
+
+
+def dist_backend():
+    import torch.distributed as dist
+    return dist.get_backend()
+
+
+def run_multi(args, rank, world, dev, be, timer, sync):
+    import torch
+    import torch.distributed as dist
+    from gala.comm import Comm
+
+    comm = Comm()
+    F = args.F
 
     def barrier():
         dist.barrier()
@@ -403,28 +444,15 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    cand = {}
-    for m in modes:
-        st = make_step(m.agg, X, dY, bufs)
-        cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
-        log(f"[rank {rank}] candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
-    forced = os.environ.get("GALA_DIST_MODE")
-    best = next(m for m in modes if m.name == (forced or min(cand, key=cand.get)))
-    step = make_step(best.agg, X, dY, bufs)
-    t_step = timed_steps(step, args.steps, args.warmup, sync, barrier, reduce_max)
-    value = 4 * g.nnz / t_step
-
-    t_kernel, alg = best.kernel(timer)
-    t_ex = best.exchange(timer)
-    ref_mode = modes[0]
+    fam, g, bounds = strong_family(args, "uniform", rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
     out = {
         "metric": "aggregated edges/sec, GCN-2 ogbn-products (4 F=32 aggregations per step)",
-        "value": value,
+        "value": fam["value"],
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": t_step * 1e3,
+        "ms_per_step": fam["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -434,24 +462,21 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
                                "SpMM aggregations, F=32, one graph split over the GPUs",
                    "n_vertices": g.n_rows, "edges": g.nnz, "F": F,
-                   "parallelism": f"{best.name} x{world} (RCCL)" if comm.rccl else f"{best.name} x{world} ({dist.get_backend()})"},
-        "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": alg / t_kernel / HBM_PEAK, "traffic": None,
-                     "kernel": f"gala::k_spmm_rowgroup (rank 0's SpMM launches of mode {best.name})",
-                     "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg},
-        "comm": {"mode": best.name, "backend": dist.get_backend(),
-                 "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
-                 "halo_bytes_per_aggregation_per_rank": best.agg.halo_bytes(),
-                 "exchange_ms_per_aggregation": t_ex * 1e3,
-                 "spmm_ms_per_aggregation": t_kernel * 1e3,
-                 "halo_layout": pt1.halo_mode, "halo_rows_rank0": pt1.n_halo_rows,
-                 "note": "halo-exact is bit-identical to one GPU; the other modes agree to fp32 rounding. "
-                         "Exchange time is the collective(s) of one aggregation alone; it overlaps the SpMM "
-                         "in the -overlap/-pipe modes."},
+                   "parallelism": f"{fam['comm']['mode']} x{world} (RCCL)" if comm.rccl
+                   else f"{fam['comm']['mode']} x{world} ({dist.get_backend()})"},
+        "roofline": fam["roofline"],
+        "comm": fam["comm"],
     }
-    del modes, ref_mode
     if not args.no_gat:
         out["gat"] = gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
+    del g
+    if not args.no_rmat:
+        rm, gr, _ = strong_family(args, "rmat", rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+        rm["graph"] = (f"R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops, N={gr.n_rows}, E={gr.nnz}, "
+                       f"max degree {int((gr.rowptr[1:] - gr.rowptr[:-1]).max())}")
+        rm["unit"] = "edges/s"
+        out["rmat"] = rm
+        del gr
     if not args.no_weak:
         out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
     return out

@@ -315,6 +315,21 @@ def _dense_map(bounds: np.ndarray, c: int, P: int, N: int) -> np.ndarray:
     return out
 
 
+def halo_fractions(g: layout.HostGraph, bounds: np.ndarray) -> np.ndarray:
+    """Per rank: distinct non-own rows its edges read / the other ranks' rows.  Every rank
+    computes the same array from the same graph, so choices made from it agree."""
+    N, P = g.n_rows, bounds.shape[0] - 1
+    out = np.zeros(P)
+    used = np.zeros(N, bool)
+    for q in range(P):
+        r0, r1 = int(bounds[q]), int(bounds[q + 1])
+        used[:] = False
+        used[g.col[int(g.rowptr[r0]):int(g.rowptr[r1])]] = True
+        used[r0:r1] = False
+        out[q] = used.sum() / max(N - (r1 - r0), 1)
+    return out
+
+
 def partition_graph(g: layout.HostGraph, rank: int, world: int, bounds: np.ndarray | None = None,
                     halo_mode: str = "auto", chunks: int = 1, dense_frac: float = 0.5) -> GraphPartition:
     """Rank `rank`'s share of the square one-segment graph `g` (rows = destinations).
@@ -336,7 +351,8 @@ def partition_graph(g: layout.HostGraph, rank: int, world: int, bounds: np.ndarr
     used[r0:r1] = False
     n_halo = int(used.sum())
     if halo_mode == "auto":
-        halo_mode = "dense" if (chunks > 1 or n_halo > dense_frac * max(N - n, 1)) else "p2p"
+        # one decision for all ranks (their collectives must match): the largest halo share
+        halo_mode = "dense" if (chunks > 1 or halo_fractions(g, b).max() > dense_frac) else "p2p"
     if halo_mode == "p2p" and chunks != 1:
         raise ValueError("the p2p halo has one chunk")
     thr = layout.split_threshold(g.n_rows, g.nnz)

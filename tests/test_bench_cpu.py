@@ -43,6 +43,11 @@ def test_bench_self_launches_ranks():
     assert c["halo_bytes_per_aggregation_per_rank"] > 0 and c["exchange_ms_per_aggregation"] > 0
     assert d["config"]["edges"] > 0 and "weak" in d and d["weak"]["value"] > 0
     assert d["roofline"]["alg_bytes_per_launch"] > 0
+    # the skewed family strong-scaled too, with its own candidates and chosen layout
+    rm = d["rmat"]
+    assert rm["value"] > 0 and rm["comm"]["mode"] in rm["comm"]["candidates_ms_per_step"]
+    assert "R-MAT" in rm["graph"] and 0.0 <= rm["comm"]["vcut_touched_fraction"] <= 1.0
+    assert "rehearsal" in c["rccl_note"]          # gloo: labelled as a rehearsal, not RCCL
 
 
 def test_bench_single_rank_line():

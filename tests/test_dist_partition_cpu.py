@@ -457,3 +457,14 @@ def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc, ex
     ref = _gat_train_one_process(GRAPHS[name](), rc)
     for a, b, what in zip(got, ref, ("Y", "dX", "d_aL", "dwR", "dbR")):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4, err_msg=what)
+
+
+def test_auto_halo_mode_is_one_choice_for_all_ranks():
+    """The halo layout choice is made from every rank's halo share, so all ranks agree
+    (their collectives must match) even on a skewed graph whose ranks' halos differ."""
+    g = powerlaw()
+    for world in (2, 3, 4):
+        modes = {gdist.partition_graph(g, p, world).halo_mode for p in range(world)}
+        assert len(modes) == 1
+        fr = gdist.halo_fractions(g, gdist.row_bounds(g.rowptr, world))
+        assert modes == {"dense" if fr.max() > 0.5 else "p2p"}

@@ -354,3 +354,78 @@ def test_bench_self_launch_two_ranks_on_one_gpu_gloo():
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["comm"]["backend"] == "gloo"
     assert set(d["comm"]["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
     assert d["value"] > 0 and d["gat"]["value"] > 0 and "vertex cut x2" in d["gat"]["layout"]
+    rm = d["rmat"]                                     # the skewed family at n_gpus 2
+    assert rm["value"] > 0 and rm["comm"]["mode"] in rm["comm"]["candidates_ms_per_step"]
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 2), (4, 3)])
+@pytest.mark.parametrize("kind", ["banded", "rmat"])
+def test_vertex_cut_sparse_exchange_matches_one_gpu(world, chunks, kind):
+    """The sparse (DCSR) vertex-cut exchange, ranks simulated in-process on the HIP kernels:
+    every rank's SpMMs write only the destination rows it holds edges of, the all-to-all is
+    the re-slicing of those blocks by (chunk, source rank), and the owner's receive-CSR SpMM
+    (norm fused) equals the one-GPU aggregation to fp32 rounding."""
+    from gala import layout, vertex_cut as vc
+    from _graphs import banded
+    g = banded(n=6000, width=60) if kind == "banded" else layout.gen_graph("rmat", 6000, 60000, seed=5)
+    F = 32
+    X = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, (g.n_rows, F)).astype(np.float32)).cuda()
+    dg = ops.DeviceGraph.from_host(g)
+    norm = ops.degree(dg, power=-0.5)
+    ref = ops.spmm(dg, ops.row_broadcast(norm, X), dst_scale=norm)
+    parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks, exchange="sparse") for p in range(world)]
+    sends = []
+    for pt in parts:
+        Xs = ops.row_broadcast(norm[pt.r0:pt.r0 + pt.n], X[pt.r0:pt.r0 + pt.n])
+        blocks = []
+        for k, h in enumerate(pt.sparse.send_graphs):
+            Yk = ops.spmm(ops.DeviceGraph.from_host(h, split=pt.split_threshold), Xs)
+            off = np.concatenate([[0], np.cumsum(pt.sparse.send_counts[k])])
+            blocks.append([Yk[off[q]:off[q + 1]] for q in range(world)])
+        sends.append(blocks)
+    for pt in parts:
+        recv = torch.cat([sends[q][k][pt.rank] for k in range(chunks) for q in range(world)])
+        if recv.shape[0] == 0:
+            recv = torch.zeros((1, F), device="cuda")
+        got = ops.spmm(ops.DeviceGraph.from_host(pt.sparse.recv_graph, split=False), recv,
+                       dst_scale=norm[pt.r0:pt.r0 + pt.n])
+        torch.testing.assert_close(got, ref[pt.r0:pt.r0 + pt.n], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("heads,F", [(1, 32), (8, 256)])
+def test_vertex_cut_sparse_classes_on_one_rank(heads, F):
+    """VertexCutAggregator and the VertexCutGat training pair with the sparse exchange at
+    world 1 on the HIP backend (the receive-CSR SpMMs, the aL index gather, the attention
+    Linear's backward) against the one-GPU operators."""
+    from gala import layout, vertex_cut as vc
+    from gala.backend import HipBackend
+    g = layout.gen_graph("rmat", 4000, 40000, seed=8)
+    be = HipBackend("cuda")
+    rng = np.random.default_rng(7)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    X = cu(rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32))
+    dY = cu(rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32))
+    aL = cu(rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32))
+    wR = cu(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR = cu(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+    dg = ops.DeviceGraph.from_host(g)
+    norm = ops.degree(dg, power=-0.5)
+    ref = ops.spmm(dg, ops.row_broadcast(norm, X), dst_scale=norm)
+    pt = vc.vertex_cut_partition(g, 0, 1, chunks=2, exchange="sparse")
+    agg = vc.VertexCutAggregator(pt, F, be, None)
+    Y = torch.empty_like(X)
+    agg(X, Y)
+    torch.testing.assert_close(Y, ref, rtol=1e-5, atol=1e-6)
+    Y2, q2, Ym2, sma2, aR2 = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=heads, want_aR=True)
+    dX2, daL2 = ops.gat_bwd_stats(dg, aL, aR2, dY, q2, Y2, Ym2, sma2, heads=heads)
+    dX2 = ops.head_attn_bwd(daL2.view(-1, heads), wR, heads=heads, dX=dX2.clone())
+    gat = vc.VertexCutGat(pt, F, heads, be, None)
+    Yr = gat.forward_train(aL, None, X, wR, bR)
+    dXr, daLr, dW, db = gat.backward(dY)
+    torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(daLr.reshape(-1), daL2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dXr, dX2, rtol=1e-4, atol=1e-5)
+    D = F // heads
+    g64 = daL2.view(-1, heads).double()
+    torch.testing.assert_close(dW.double(), (g64.repeat_interleave(D, 1) * X.double()).sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db.double(), g64.sum(0), rtol=1e-4, atol=1e-3)

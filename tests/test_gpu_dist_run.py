@@ -69,3 +69,23 @@ def test_dist_run_gpu_vertex_cut_matches_one_rank(tmp_path):
         dv = _run_gpu(ir_path, tmp_path, world, f"v{world}", extra=("--layout", "vcut"))
         np.testing.assert_allclose(dv["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(dv["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+
+
+def test_dist_run_gpu_gat_program(tmp_path):
+    """A GAT program (gat_heads: 4 heads) on the vertex cut through the HIP kernels: one rank
+    against the float64 IR executor, two ranks sharing the GPU over gloo (dense and sparse
+    exchange) against one rank."""
+    from gala import dist_run
+    ir_path = _ir("gat_heads.txt", tmp_path)
+    d1 = _run_gpu(ir_path, tmp_path, 1, "g1", extra=("--layout", "vcut"))
+    ir = ref.load_ir(str(ir_path))["post"]
+    graphs = ref.Graphs(ir, d1["rowptr"], d1["col"], np.ones(len(d1["rowptr"]) - 1, np.int32))
+    X = torch.as_tensor(dist_run._hash_uniform(np.arange(len(d1["rowptr"]) - 1), ir["sched"]["feat_size"], 3),
+                        dtype=torch.float64)
+    params = {k: torch.tensor(np.asarray(v), dtype=torch.float64) for k, v in json.loads(str(d1["weights"])).items()}
+    want = ref.run(ir, graphs, X, params)
+    np.testing.assert_allclose(d1["prediction"], want.detach().numpy(), rtol=1e-4, atol=1e-4)
+    for ex in ("dense", "sparse"):
+        d2 = _run_gpu(ir_path, tmp_path, 2, f"g2{ex}", extra=("--layout", "vcut", "--exchange", ex))
+        np.testing.assert_allclose(d2["prediction"], d1["prediction"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
