@@ -263,6 +263,29 @@ def products_graph(kind: str, scale: float):
     return layout.gen_graph(kind, n, (E - n) // 2, seed=42)
 
 
+def data_dir(args):
+    """The real dataset to run on: --data DIR, else Data/Products/ next to this script (the
+    reference's layout, scripts/Data/gala_export_npy.py:100-112) when it holds the graph."""
+    if args.data:
+        return args.data
+    d = os.path.join(ROOT, "Data", "Products")
+    return d if os.path.exists(os.path.join(d, "Adj_src.npy")) else None
+
+
+def headline_graph(args):
+    """(graph, data description): the npy dataset when one is given / present, else the
+    synthetic uniform Products-shaped graph."""
+    d = data_dir(args)
+    if d is None:
+        return products_graph("uniform", args.scale), None
+    from gala import layout
+    g = layout.load_npy_dataset(d)
+    if g.n_rows != g.n_cols:
+        raise SystemExit(f"bench.py: {d} holds a {g.n_rows} x {g.n_cols} graph; the aggregation needs it square")
+    return g, (f"real: {os.path.abspath(d)} (Adj_src/Adj_dst.npy, gala_export_npy.py format: CSR rows = src, "
+               f"values 1); X~U[-1,1) fp32")
+
+
 class OneGpuGCN:
     """The single-device step: norm * A (norm * H) with the dst norm fused into the SpMM."""
 
@@ -358,7 +381,7 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
     from gala import dist as gdist, vertex_cut as vc
     F = args.F
     t0 = time.time()
-    g = products_graph(kind, args.scale)
+    g, real = headline_graph(args) if kind == "uniform" else (products_graph(kind, args.scale), None)
     log(f"[rank {rank}/{world}] {kind} graph N={g.n_rows} E={g.nnz} built in {time.time() - t0:.1f}s")
     bounds = gdist.row_bounds(g.rowptr, world)
     t0 = time.time()
@@ -399,7 +422,7 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
                          args.warmup if kind == "uniform" else 2, sync, barrier, reduce_max)
     t_kernel, alg = best.kernel(timer)
     t_ex = best.exchange(timer) if world > 1 else 0.0
-    out = {"value": 4 * g.nnz / t_step, "ms_per_step": t_step * 1e3,
+    out = {"value": 4 * g.nnz / t_step, "ms_per_step": t_step * 1e3, "real_data": real,
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "traffic": None,
                         "kernel": f"gala::k_spmm_rowgroup (rank 0's SpMM launches of mode {best.name})",
@@ -457,8 +480,8 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: one uniform random symmetric ogbn-products-shaped graph + self loops (seed 42), "
-                "partitioned across the ranks; X~U[-1,1) fp32",
+        "data": fam.pop("real_data") or ("synthetic: one uniform random symmetric ogbn-products-shaped graph + self "
+                                         "loops (seed 42), partitioned across the ranks; X~U[-1,1) fp32"),
         "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
                                "SpMM aggregations, F=32, one graph split over the GPUs",
                    "n_vertices": g.n_rows, "edges": g.nnz, "F": F,
@@ -472,6 +495,7 @@ def run_multi(args, rank, world, dev, be, timer, sync):
     del g
     if not args.no_rmat:
         rm, gr, _ = strong_family(args, "rmat", rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+        rm.pop("real_data")
         rm["graph"] = (f"R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops, N={gr.n_rows}, E={gr.nnz}, "
                        f"max degree {int((gr.rowptr[1:] - gr.rowptr[:-1]).max())}")
         rm["unit"] = "edges/s"
@@ -540,7 +564,7 @@ def run_single(args, dev, be, timer, sync):
     import torch
     F = args.F
     t0 = time.time()
-    hg = products_graph("uniform", args.scale)
+    hg, real = headline_graph(args)
     log(f"[bench] uniform graph N={hg.n_rows} E={hg.nnz} in {time.time() - t0:.1f}s")
     agg = OneGpuGCN(hg, F, be)
     gen = torch.Generator(device=dev).manual_seed(1234)
@@ -567,8 +591,8 @@ def run_single(args, dev, be, timer, sync):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: uniform random symmetric ogbn-products-shaped graph + self loops (seed 42), "
-                "X~U[-1,1) fp32",
+        "data": real or "synthetic: uniform random symmetric ogbn-products-shaped graph + self loops (seed 42), "
+                        "X~U[-1,1) fp32",
         "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
                                "SpMM aggregations, F=32",
                    "n_vertices": hg.n_rows, "edges": hg.nnz, "F": F, "parallelism": "1 GPU"},
@@ -736,6 +760,8 @@ def main():
     ap.add_argument("--no-rmat", action="store_true")
     ap.add_argument("--no-gat", action="store_true")
     ap.add_argument("--no-weak", action="store_true")
+    ap.add_argument("--data", help="dataset directory in the reference's npy format (Adj_src.npy, Adj_dst.npy); "
+                                   "default: Data/Products/ when present, else the synthetic graph")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -79,3 +79,31 @@ def test_bench_partitioned_path_on_one_rank():
     assert r.returncode == 0, r.stderr[-3000:]
     (d,) = _json_lines(r.stdout)
     assert d["n_gpus"] == 1 and d["comm"]["backend"] == "gloo" and d["value"] > 0
+
+
+def _write_npy_dataset(d, n=1500, m=6000, seed=4):
+    """A small dataset in the reference's on-disk format (scripts/Data/gala_export_npy.py:
+    100-112): Adj_src.npy = uint32 [n_rows, n_cols, src...], Adj_dst.npy = uint32 [dst...],
+    symmetric edges + self loops."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    u, v = rng.integers(0, n, m), rng.integers(0, n, m)
+    src = np.concatenate([u, v, np.arange(n)]).astype(np.uint32)
+    dst = np.concatenate([v, u, np.arange(n)]).astype(np.uint32)
+    np.save(os.path.join(d, "Adj_src.npy"), np.concatenate([[n, n], src]).astype(np.uint32))
+    np.save(os.path.join(d, "Adj_dst.npy"), dst)
+    return n, src.shape[0]
+
+
+def test_bench_real_data(tmp_path):
+    """--data DIR: the headline step runs on the dataset's graph (read through the runtime's
+    npy loader) and the line names it; one rank and two self-launched ranks."""
+    n, e = _write_npy_dataset(str(tmp_path))
+    for extra in ((), ("--gpus", "2", "--calib-steps", "1", "--no-weak", "--no-gat")):
+        r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--data", str(tmp_path), "--steps", "2",
+                            "--warmup", "1", "--no-cpu-baseline", "--no-rmat", *extra],
+                           capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        (d,) = _json_lines(r.stdout)
+        assert d["config"]["n_vertices"] == n and d["config"]["edges"] == e
+        assert d["data"].startswith("real: ") and str(tmp_path) in d["data"]
