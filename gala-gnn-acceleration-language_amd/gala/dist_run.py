@@ -63,6 +63,21 @@ SUPPORTED = {"INPUT", "DEGREES", "POWER", "ROW_BROADCAST", "GCN_AGGREGATE", "AGG
              "ADD", "SCALAR_ADD_EPS_MULTIPLY", "GAT_AGGREGATE"}
 
 
+def dataset_shape(name: str):
+    """(N, undirected edges, features, classes, train fraction) of a dataset name, as
+    host/gala_datasets.h: the published shapes, and papers100M_<p> for the p% node
+    subgraph of ogbn-papers100M (get_large_sampled_datasets.py:68; an induced subgraph
+    keeps about p^2 of the edges)."""
+    if name in SHAPES:
+        return SHAPES[name]
+    pre = "papers100M_"
+    if name.startswith(pre) and len(name) > len(pre):
+        p = float(name[len(pre):]) / 100.0
+        n0, m0, F, C, frac = SHAPES["Papers100M"]
+        return int(n0 * p), int(m0 * p * p), F, C, frac
+    return None
+
+
 def _hash_uniform(rows: np.ndarray, cols: int, seed: int) -> np.ndarray:
     """Deterministic U[-1, 1) features of the given rows (counter hash of (seed, row, col)),
     so every rank draws exactly its own rows, whatever the number of ranks."""
@@ -163,7 +178,7 @@ class Program:
             raise NotImplementedError("gala.dist_run: sampled programs")
         self.ir, self.device = ir, torch.device(device)
         self.be = make_backend(self.device)
-        self.comm = Comm(group) if world > 1 else None
+        self.comm = Comm(group) if dist.is_initialized() else None
         self.rank, self.world = rank, world
         self.layout = layout_mode
         if layout_mode == "vcut":
@@ -194,7 +209,7 @@ class Program:
         self.modules.to(self.device)
         n_train = torch.tensor([float(train_own.sum().item())], dtype=torch.float64,
                                device=self.device if (self.comm and self.comm.rccl) else "cpu")
-        if world > 1:
+        if self.comm is not None:
             dist.all_reduce(n_train, group=group)
         self.n_train = float(n_train.item())
         self.invariants = None
@@ -268,7 +283,7 @@ class Program:
         return -logp.gather(1, self.labels[self.train].view(-1, 1)).sum() / self.n_train
 
     def reduce_grads(self):
-        if self.world == 1:
+        if self.comm is None:
             return
         for p in self.modules.parameters():
             if p.grad is not None:
@@ -291,8 +306,12 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--dump", help="rank 0 writes an npz: predictions (all rows), losses, rowptr/col")
+    ap.add_argument("--dump-stride", type=int, default=1,
+                    help="dump the predictions of every k-th row only (rows in 'rows'; large graphs)")
     ap.add_argument("--layout", default="halo", choices=["halo", "vcut"],
                     help="halo: row partition + exact halo SpMM; vcut: vertex cut + reduce-scatter")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the collectives even on one rank (RCCL at world 1 on one GPU)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "dense", "sparse"],
                     help="vcut: dense reduce-scatter, sparse DCSR all-to-all, or auto (touched fraction)")
     args = ap.parse_args(argv)
@@ -305,12 +324,19 @@ def main(argv=None):
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    distributed = world > 1 or args.dist
+    if distributed:
         backend = os.environ.get("GALA_DIST_BACKEND", "nccl" if dev.type == "cuda" else "gloo")
+        kw = {}
+        if "MASTER_ADDR" not in os.environ:      # one rank without a launcher
+            import socket
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            kw = dict(init_method=f"tcp://127.0.0.1:{so.getsockname()[1]}", rank=0, world_size=1)
+            so.close()
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+            kw["device_id"] = dev
+        dist.init_process_group(backend, **kw)
     ir = load(args.ir)
     s = ir["sched"]
     if args.data:
@@ -319,9 +345,10 @@ def main(argv=None):
         lab_all = np.load(os.path.join(args.data, "Lab.npy")).reshape(-1)
         tr_all = np.load(os.path.join(args.data, "TnMsk.npy")).reshape(-1)
     else:
-        if s["dataset"] not in SHAPES:
+        shape = dataset_shape(s["dataset"])
+        if shape is None:
             raise SystemExit(f"gala.dist_run: no published shape for dataset {s['dataset']!r}; pass --data")
-        n0, m0, _, _, frac = SHAPES[s["dataset"]]
+        n0, m0, _, _, frac = shape
         n, m = max(int(n0 * args.scale), 2), max(int(m0 * args.scale), 1)
         g = layout.gen_graph("uniform", n, m, seed=args.seed)
         X_all = lab_all = tr_all = None
@@ -359,7 +386,7 @@ def main(argv=None):
         sync()
         t2 = time.perf_counter()
         lt = loss.detach().reshape(1).to(torch.float64)
-        if world > 1:
+        if distributed:
             lt = lt.to(dev) if prog.comm.rccl else lt.cpu()
             dist.all_reduce(lt)
         losses.append(float(lt.item()))
@@ -380,16 +407,18 @@ def main(argv=None):
             pr = torch.cat([t[:n] for t, n in zip(parts, sizes)])
         pr = pr.cpu()
         if rank == 0:
-            np.savez(args.dump, prediction=pr.numpy(), losses=np.array(losses), rowptr=g.rowptr, col=g.col,
-                     weights=np.array(json.dumps(init_weights)))
+            rows_d = np.arange(0, g.n_rows, max(args.dump_stride, 1))
+            np.savez(args.dump, prediction=pr.numpy()[rows_d], rows=rows_d, losses=np.array(losses),
+                     rowptr=g.rowptr, col=g.col, weights=np.array(json.dumps(init_weights)))
     if rank == 0:
-        print(json.dumps({"ranks": world, "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,
+        print(json.dumps({"ranks": world, "backend": dist.get_backend() if distributed else None,
+                          "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,
                           "halo": prog.part.halo_mode if args.layout == "halo" else None,
                           "exchange": prog.part.exchange if args.layout == "vcut" else None,
                           "fwd_mean_s": float(np.mean(fwd_t[keep])), "epoch_mean_s": float(np.mean(ep_t[keep])),
                           "loss_first": losses[0], "loss_last": losses[-1]}), flush=True)
         print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

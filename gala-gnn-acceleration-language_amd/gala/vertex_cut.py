@@ -138,7 +138,7 @@ def vertex_cut_partition(g: layout.HostGraph, rank: int, world: int, chunks: int
     deg = np.diff(rp)
     frac = touched_fraction(g, b) if (exchange == "auto" or exchange == "sparse") else 1.0
     if exchange == "auto":
-        exchange = "sparse" if frac < sparse_frac else "dense"
+        exchange = "sparse" if (P > 1 and frac < sparse_frac) else "dense"
     if exchange not in ("dense", "sparse"):
         raise ValueError(f"vertex_cut_partition: exchange {exchange!r} (dense | sparse | auto)")
     sel = (g.col >= c0) & (g.col < c1)
@@ -256,7 +256,7 @@ class _PartialRows:
         """Chunk k's collective (async on RCCL; None when done in place)."""
         a, b = self._send[k]
         c, d = self._recv[k]
-        if self.part.world == 1:
+        if self.comm is None:       # one rank without collectives
             recv[c:d].copy_(send[a:b])
             return None
         if self.sparse:
@@ -405,7 +405,7 @@ class VertexCutGat(_PartialRows):
         works = []
         for k in range(K):
             al_k = self.aLall[k * rows:(k + 1) * rows]
-            if p.world > 1:
+            if self.comm is not None:
                 works.append(self.comm.all_gather(al_k, self.aLpad[k * c:(k + 1) * c]))
             else:
                 al_k.copy_(self.aLpad[k * c:(k + 1) * c])

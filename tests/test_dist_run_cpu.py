@@ -141,3 +141,15 @@ def test_dist_run_gat_needs_vertex_cut(tmp_path):
     r = subprocess.run([sys.executable, "-m", "gala.dist_run", str(ir_path), "--synthetic", "--device", "cpu",
                         "--iters", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode != 0 and "vertex cut" in r.stderr
+
+
+def test_dist_run_collectives_at_world_one(tmp_path):
+    """--dist: the collectives run even on one rank (the GPU box's one-GPU RCCL check; here
+    gloo).  A one-rank collective moves the rows unchanged, so the run is bit-identical to
+    the one without collectives."""
+    ir_path = _ir("gat_heads.txt", tmp_path)
+    d0, _ = _run(ir_path, tmp_path, 1, "nodist", iters=2, extra=("--layout", "vcut", "--exchange", "sparse"))
+    d1, s1 = _run(ir_path, tmp_path, 1, "dist", iters=2, extra=("--layout", "vcut", "--exchange", "sparse", "--dist"))
+    assert s1["backend"] == "gloo"
+    np.testing.assert_array_equal(d1["prediction"], d0["prediction"])
+    np.testing.assert_array_equal(d1["losses"], d0["losses"])

@@ -19,14 +19,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run_gpu(ir, tmp_path, world, tag, iters=6, extra=()):
+def _run_gpu(ir, tmp_path, world, tag, iters=6, extra=(), backend="gloo"):
     import subprocess
     import sys
     from test_dist_run_cpu import PKG, ROOT, _free_port
     dump = tmp_path / f"{tag}.npz"
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
-    env["GALA_DIST_BACKEND"] = "gloo"
+    env["GALA_DIST_BACKEND"] = backend
     cmd = [sys.executable]
     if world > 1:
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr",
@@ -89,3 +89,61 @@ def test_dist_run_gpu_gat_program(tmp_path):
         d2 = _run_gpu(ir_path, tmp_path, 2, f"g2{ex}", extra=("--layout", "vcut", "--exchange", ex))
         np.testing.assert_allclose(d2["prediction"], d1["prediction"], rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+
+
+def _khop_induced(rowptr, col, seeds, hops):
+    """Rows within `hops` of the seeds and the induced CSR on them (local ids): rows at
+    distance < hops keep every edge, which is all a `hops`-layer forward of the seeds reads."""
+    cur = np.unique(np.asarray(seeds, np.int64))
+    allr = cur
+    for _ in range(hops):
+        nb = np.concatenate([col[rowptr[r]:rowptr[r + 1]] for r in cur]).astype(np.int64)
+        cur = np.setdiff1d(np.unique(nb), allr)
+        allr = np.union1d(allr, cur)
+    loc = {int(r): i for i, r in enumerate(allr)}
+    rp, cl = [0], []
+    for r in allr:
+        cs = [loc[int(c)] for c in col[rowptr[r]:rowptr[r + 1]] if int(c) in loc]
+        cl += cs
+        rp.append(len(cl))
+    return allr, np.asarray(rp, np.int64), np.asarray(cl, np.int64)
+
+
+@pytest.mark.timeout(500)
+def test_dist_run_config5_shape_at_size(tmp_path):
+    """Config 5's program (bench/dsl/gcn3_papers10.txt, GCN-3 hidden 128, 172 classes) at
+    1.1 M rows (--scale 0.1 of the 10 % papers100M shape) through the multi-rank runtime on
+    the one GPU: the vertex cut over RCCL at world 1 (--dist: its reduce-scatters run)
+    against the halo layout's exact mode (sampled rows' predictions and the loss curve
+    within fp32 rounding), and the halo run's first forward against the float64 IR executor
+    on sampled rows (their 3-hop induced subgraph, true degrees)."""
+    from gala import dist_run
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ir_path = tmp_path / "p10.json"
+    import subprocess
+    from test_dist_run_cpu import GALAC
+    r = subprocess.run([GALAC, os.path.join(root, "bench", "dsl", "gcn3_papers10.txt"), "--quiet", "--ir-json",
+                        str(ir_path)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    common = ("--scale", "0.1", "--dump-stride", "997")
+    dh = _run_gpu(ir_path, tmp_path, 1, "halo", iters=3, extra=common)
+    dv = _run_gpu(ir_path, tmp_path, 1, "vcut", iters=3, extra=common + ("--layout", "vcut", "--dist"),
+                  backend="nccl")
+    n = len(dh["rowptr"]) - 1
+    assert n >= 1_000_000
+    np.testing.assert_array_equal(dv["rows"], dh["rows"])
+    np.testing.assert_allclose(dv["prediction"], dh["prediction"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dv["losses"], dh["losses"], rtol=1e-4, atol=1e-6)
+    ir = ref.load_ir(str(ir_path))["post"]
+    seeds = dh["rows"][:: max(len(dh["rows"]) // 6, 1)][:6]
+    rowptr, col = dh["rowptr"].astype(np.int64), dh["col"]
+    rows, rp, cl = _khop_induced(rowptr, col, seeds, 3)
+    graphs = ref.Graphs(ir, rp, cl, np.ones(len(rows), np.int32))
+    graphs.deg0 = torch.as_tensor(np.diff(rowptr)[rows].astype(np.float64)).view(-1, 1)   # true degrees
+    X = torch.as_tensor(dist_run._hash_uniform(rows, ir["sched"]["feat_size"], 3), dtype=torch.float64)
+    params = {k: torch.tensor(np.asarray(v), dtype=torch.float64) for k, v in json.loads(str(dh["weights"])).items()}
+    want = ref.run(ir, graphs, X, params).detach().numpy()
+    at = {int(r): i for i, r in enumerate(rows)}
+    got_at = {int(r): i for i, r in enumerate(dh["rows"])}
+    for s in seeds:
+        np.testing.assert_allclose(dh["prediction"][got_at[int(s)]], want[at[int(s)]], rtol=1e-4, atol=1e-4)
