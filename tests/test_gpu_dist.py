@@ -325,9 +325,10 @@ def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
         Y2, q2, Ym2, sma2, aR2 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR, bR=bR, heads=heads, want_aR=True)
         dX2, daL2 = ops.gat_bwd_stats(dg, cu(aL), aR2, cu(dY), q2, Y2, Ym2, sma2, heads=heads)
         Yr = gat.forward_train(cu(aL), None, cu(X), wR, bR)
-        dXr, daLr = gat.backward(cu(dY))
+        dXr, daLr, _, _ = gat.backward(cu(dY))       # dX includes the path through aR = X wR + bR
+        dX2 = ops.head_attn_bwd(daL2.view(-1, heads), wR, heads=heads, dX=dX2.clone())
         torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
-        torch.testing.assert_close(dXr, dX2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dXr, dX2, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(daLr.reshape(-1), daL2, rtol=1e-4, atol=1e-4)
 
 
