@@ -59,6 +59,14 @@ class HipBackend:
         """[n, heads] per-head attention logits <X[:, head h], w_h> + b_h (gala_head_attn_f32)."""
         return self.ops.head_attn(X, w, b, heads=heads)
 
+    def row_scale_relu(self, act, pre, X, out):
+        """out = pre * relu(act * X) (gala_row_scale_relu_f32: the ReLU prologue)."""
+        return self.ops.row_scale_relu(X, act, pre, out=out)
+
+    def relu_scale_backward(self, act, X, G, out):
+        """out = act * (relu(act * X) <= 0 ? 0 : G) (gala_relu_scale_backward_f32)."""
+        return self.ops.relu_scale_backward(X, G, act, out=out)
+
     def head_attn_bwd(self, g, w, heads, dX):
         """dX[:, head h] += g[:, h] * w[head h] (gala_head_attn_bwd_f32, accumulating)."""
         return self.ops.head_attn_bwd(g.contiguous(), w, heads=heads, dX=dX, n_rows=dX.shape[0])
@@ -164,6 +172,16 @@ class CpuBackend:
         out = torch.empty((X.shape[0], heads), dtype=torch.float32)
         _abi.call_cpu("gala_head_attn_f32", X.shape[0], X.shape[1], heads, _hp(X), X.stride(0), _hp(w), _hp(b),
                       _hp(out), None)
+        return out
+
+    def row_scale_relu(self, act, pre, X, out):
+        _abi.call_cpu("gala_row_scale_relu_f32", X.shape[0], X.shape[1], _hp(act), _hp(pre), _hp(X), X.stride(0),
+                      _hp(out), out.stride(0), None)
+        return out
+
+    def relu_scale_backward(self, act, X, G, out):
+        _abi.call_cpu("gala_relu_scale_backward_f32", X.shape[0], X.shape[1], _hp(act), _hp(X), X.stride(0), _hp(G),
+                      G.stride(0), _hp(out), out.stride(0), None)
         return out
 
     def head_attn_bwd(self, g, w, heads, dX):

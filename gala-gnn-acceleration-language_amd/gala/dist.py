@@ -482,13 +482,17 @@ class DistAggregator:
         """out = norm * A (norm * H) (the GCN aggregation with the graph's own norm)."""
         return self.apply(H, out, self.norm, self.norm)
 
-    def apply(self, H, out, pre=None, post=None):
+    def apply(self, H, out, pre=None, post=None, relu=False, act=None):
         """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None), the
-        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) on a partition."""
+        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) on a partition.  relu:
+        the ReLU prologue, pre * relu(act * H) in the same pass."""
         be = self.be
         Xs = self._table(H.shape[1])
+        sl = lambda v, a, b: None if v is None else v[a:b]  # noqa: E731
         for j0, j1, x0 in self._blocks:                               # own rows of Xs = pre * H
-            if pre is None:
+            if relu:
+                be.row_scale_relu(sl(act, j0, j1), sl(pre, j0, j1), H[j0:j1], Xs[x0:x0 + (j1 - j0)])
+            elif pre is None:
                 Xs[x0:x0 + (j1 - j0)].copy_(H[j0:j1])
             else:
                 be.row_broadcast(pre[j0:j1], H[j0:j1], Xs[x0:x0 + (j1 - j0)])

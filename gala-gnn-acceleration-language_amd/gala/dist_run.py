@@ -108,6 +108,43 @@ class _Agg(torch.autograd.Function):
         return dx, None, None, None
 
 
+class _AggRelu(torch.autograd.Function):
+    """post * A (pre * relu(act * x)) on the partition, the ReLU prologue fused into the
+    aggregation's elementwise pass (as the generated programs' gcn_aggregate_relu_apply);
+    backward: relu_scale_backward(pre * A (post * dy)) (undirected)."""
+
+    @staticmethod
+    def forward(ctx, x, act, agg, pre, post):
+        out = torch.empty_like(x)
+        agg.apply(x.contiguous(), out, pre, post, relu=True, act=act)
+        ctx.save_for_backward(x)
+        ctx.agg, ctx.act, ctx.pre, ctx.post = agg, act, pre, post
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        g = torch.empty_like(dy)
+        ctx.agg.apply(dy.contiguous(), g, ctx.post, ctx.pre)
+        dx = torch.empty_like(x)
+        ctx.agg.be.relu_scale_backward(ctx.act, x.contiguous(), g, dx)
+        return dx, None, None, None, None
+
+
+def _mirror():
+    """The C++ operator mirror (gala._gala_torch): the same FFN / attention-Linear autograd
+    ops a generated program calls (narrow-output MFMA forward, dense-gradient kernels)."""
+    from . import _gala_torch
+    return _gala_torch
+
+
+class FfnLinear(torch.nn.Linear):
+    """FFN_OP through the operator mirror's ffn_apply (host/gala_torch.cpp Ffn)."""
+
+    def forward(self, x):
+        return _mirror().ffn_apply(x.contiguous(), self.weight, self.bias)
+
+
 class HeadLinear(torch.nn.Module):
     """gat_heads(H)'s attention vector Linear(F, 1) per head: out[:, h] = <x[:, head h],
     w[head h]> + b[h] (weight [1, F], bias [H]; galac's HeadAttn, tests/_ir_ref.py _ffn)."""
@@ -120,9 +157,7 @@ class HeadLinear(torch.nn.Module):
         self.bias = torch.nn.Parameter(torch.empty(heads).uniform_(-k, k))
 
     def forward(self, x):
-        n, F = x.shape
-        H = self.heads
-        return (x.view(n, H, F // H) * self.weight.view(1, H, F // H)).sum(2) + self.bias.view(1, H)
+        return _mirror().head_attn_apply(x.contiguous(), self.weight, self.bias)
 
 
 class _VcutGatFfn(torch.autograd.Function):
@@ -203,7 +238,7 @@ class Program:
             if w["type"] == "linear" and int(w.get("heads", 1)) > 1 and w["out"] == 1:
                 self.modules[w["name"]] = HeadLinear(w["in"], int(w["heads"]))
             elif w["type"] == "linear":
-                self.modules[w["name"]] = torch.nn.Linear(w["in"], w["out"])
+                self.modules[w["name"]] = FfnLinear(w["in"], w["out"])
             else:
                 self.modules[w["name"]] = torch.nn.ParameterList([torch.nn.Parameter(torch.tensor([float(w["init"])]))])
         self.modules.to(self.device)
@@ -248,10 +283,15 @@ class Program:
                 y = a[0] * a[1]
             elif op == "GCN_AGGREGATE":
                 x = a[0]
-                if nd["param"] == 1:  # ReLU prologue: relu(act * x)
+                if nd["param"] == 1:  # ReLU prologue: relu(act * x), fused into the aggregation
                     act = a[3] if len(a) > 3 else None
-                    x = torch.relu(x if act is None else act * x)
-                y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
+                    if act is not None and act.requires_grad:
+                        x = torch.relu(act * x)
+                        y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
+                    else:
+                        y = _AggRelu.apply(x, self._vec(act), self.agg, self._vec(a[1]), self._vec(a[2]))
+                else:
+                    y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
             elif op == "AGGREGATE_MUL_SUM":
                 y = _Agg.apply(a[0], self.agg, None, None)
             elif op == "GAT_AGGREGATE":

@@ -325,12 +325,15 @@ class VertexCutAggregator(_PartialRows):
         _, partial, S = self._buffers(F or self.F)
         self.wait([self.post(partial, S, k) for k in range(len(self.graphs))])
 
-    def apply(self, H, out, pre=None, post=None):
+    def apply(self, H, out, pre=None, post=None, relu=False, act=None):
         """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None): the
-        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) with column ownership."""
+        generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) with column ownership.
+        relu: the ReLU prologue, out = post * A (pre * relu(act * H)) (one elementwise pass)."""
         be = self.be
         Xs, partial, S = self._buffers(H.shape[1])
-        if pre is None:
+        if relu:
+            be.row_scale_relu(act, pre, H, Xs)
+        elif pre is None:
             Xs.copy_(H)
         else:
             be.row_broadcast(pre, H, Xs)

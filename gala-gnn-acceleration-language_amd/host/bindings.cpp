@@ -103,6 +103,7 @@ PYBIND11_MODULE(_gala_torch, m) {
               return ffn_apply(x, w, opt(b));
           },
           py::arg("X"), py::arg("weight"), py::arg("bias") = py::none());
+    m.def("head_attn_apply", &head_attn_apply, py::arg("X"), py::arg("weight"), py::arg("bias"));
     m.def("gat_aggregate_apply", &gat_aggregate_apply, py::arg("attn_l"), py::arg("attn_r"),
           py::arg("X"), py::arg("li"), py::arg("slope") = 0.2, py::arg("mode") = 0);
     m.def("gat_aggregate_ffn_apply", &gat_aggregate_ffn_apply, py::arg("attn_l"), py::arg("X"),

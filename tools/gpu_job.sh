@@ -11,12 +11,16 @@
 #   pmc              FETCH_SIZE and WRITE_SIZE passes (one --pmc run each) of bench.py, then
 #                    tools/pmc_traffic.py                   -> gpurun_out/traffic.json
 #   py=SCRIPT,ARGS   python SCRIPT ARGS                      -> gpurun_out/<script>.log
+#   sh=CMD           a preparation command, no GPU (commas as spaces)
+#   profcmd=TAG,CMD  rocprofv3 --kernel-trace --stats of CMD (commas as spaces; the program
+#                    itself right after --)                  -> gpurun_out/prof_TAG/
 #
 # e.g. gpurun --timeout 900 -- 'bash tools/gpu_job.sh tests=gat bench prof'
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+export PYTHONPATH="$GRAFT_REPO_ROOT/gala-gnn-acceleration-language_amd${PYTHONPATH:+:$PYTHONPATH}"
 BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline"
 
 step() {  # name, limit, command...
@@ -55,6 +59,17 @@ for s in "$@"; do
         (cd /tmp && step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/prof_write" -o run \
             -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_write.log" 2>&1) || exit 1
         python3 tools/pmc_traffic.py "$OUT/prof_fetch" "$OUT/prof_write" "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1 ;;
+    profcmd=*)
+        # profcmd=TAG,prog,args...: rocprofv3 kernel-trace stats of any command (commas = spaces)
+        a="${s#profcmd=}"
+        tag="${a%%,*}"
+        rest="${a#*,}"
+        (cd /tmp && step "prof_$tag" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o run \
+            -- ${rest//,/ } > "$OUT/prof_$tag.log" 2>&1) || { tail -20 "$OUT/prof_$tag.log"; exit 1; } ;;
+    sh=*)
+        # sh=CMD: a host-side preparation command (commas = spaces), e.g. galac
+        a="${s#sh=}"
+        step sh 300 ${a//,/ } || exit 1 ;;
     py=*)
         a="${s#py=}"
         scr="${a%%,*}"
