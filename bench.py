@@ -528,7 +528,7 @@ def gat_vertex_cut(args, g, rank, world, dev, be, comm, bounds, sync, barrier, r
 
     def step():
         layer.forward_train(aL, None, X, wR, bR)   # source logits recomputed from X, as at N = 1
-        layer.backward(dY)
+        layer.backward(dY, linear=False)           # the aggregation's backward, as gala_gat_bwd_stats_f32
     steps = max(args.steps // 2, 2)
     t_step = timed_steps(step, steps, 2, sync, barrier, reduce_max)
     out = {"value": 2 * g.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,

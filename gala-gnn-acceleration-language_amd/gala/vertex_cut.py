@@ -269,13 +269,15 @@ class _PartialRows:
             if w is not None:
                 w.wait()
 
-    def own_rows(self, recv, out, post=None):
-        """out [n, W] = post * (the summed partial rows of the own vertices)."""
+    def own_rows(self, recv, out, post=None, view_ok=False):
+        """out [n, W] = post * (the summed partial rows of the own vertices).  view_ok: the
+        dense exchange without a post scale may hand back recv[:n] itself (the own rows are
+        its first n rows), saving a copy; the caller then reads it before the next exchange."""
         n = self.part.n
         if self.sparse:
             return self.be.spmm(self.recv_graph, recv, out, post, False)
         if post is None:
-            return out.copy_(recv[:n])
+            return recv[:n] if view_ok else out.copy_(recv[:n])
         return self.be.row_broadcast(post, recv[:n], out)
 
 
@@ -448,8 +450,8 @@ class VertexCutGat(_PartialRows):
                                 self.send_rows(S, k))
             works += [self.post(U, Ur, k), self.post(S, Sr, k)]
         self.wait(works)
-        self.own_rows(Ur, Uo)
-        self.own_rows(Sr, So)
+        Uo = self.own_rows(Ur, Uo, view_ok=True)
+        So = self.own_rows(Sr, So, view_ok=True)
         return self._owner_scale(1.0 / (So + 1e-12), Uo)
 
     # -- training pair -----------------------------------------------------------------------
@@ -486,7 +488,7 @@ class VertexCutGat(_PartialRows):
         if aR is None:   # the backward's source logits of the own columns
             aR = self.be.head_attn(X, wR, bR, H)
         self.wait(works)
-        UUo, So, Mo = self.own_rows(b["UUr"], b["UUo"]), self.own_rows(b["Sr"], b["So"]), self.own_rows(b["Mr"], b["Mo"])
+        UUo, So, Mo = (self.own_rows(b[r], b[o], view_ok=True) for r, o in (("UUr", "UUo"), ("Sr", "So"), ("Mr", "Mo")))
         q = 1.0 / (So + 1e-12)
         Y = self._owner_scale(q, UUo[:, :F])
         Ym = self._owner_scale(q, UUo[:, F:])
@@ -503,10 +505,11 @@ class VertexCutGat(_PartialRows):
         rows = self.part.world * self.part.block
         return al_snap[k * rows:(k + 1) * rows]
 
-    def backward(self, dY):
+    def backward(self, dY, linear=True):
         """dY [n, F] of the own rows -> (dX [n, F], d_aL [n, H]) of the REF layer; with the
-        source logits recomputed (forward_train's wR given) -> (dX, d_aL, dwR, dbR), dX then
-        including the path through aR = X wR + bR, dwR / dbR this rank's rows' share."""
+        source logits recomputed (forward_train's wR given) and `linear` -> (dX, d_aL, dwR,
+        dbR), dX then including the path through aR = X wR + bR, dwR / dbR this rank's rows'
+        share (linear=False: the aggregation's own backward only, as gala_gat_bwd_stats_f32)."""
         if self.saved is None:
             raise RuntimeError("VertexCutGat.backward: no forward_train to take the row statistics from")
         H, n, b = self.H, self.part.n, self._train_buffers()
@@ -520,11 +523,12 @@ class VertexCutGat(_PartialRows):
         _, d_aL = self.be.gat_bwd_stats(b["own"], aL, aR, dY, q, Y, Ym, sma, H, self.slope)
         d_aL = d_aL.view(n, H)
         grads = None
-        if wR is not None:   # REF: d_aR = d_aL; through aR = X wR + bR (per head)
+        linear = linear and wR is not None
+        if linear:   # REF: d_aR = d_aL; through aR = X wR + bR (per head)
             grads = self.be.head_linear_grads(X, d_aL, H)
         self.wait(works)
-        dX = self._owner_scale(q, self.own_rows(b["Pr"], b["Po"]))
-        if wR is None:
+        dX = self._owner_scale(q, self.own_rows(b["Pr"], b["Po"], view_ok=True))
+        if not linear:
             return dX, d_aL
         self.be.head_attn_bwd(d_aL, wR, H, dX)
         return (dX, d_aL) + tuple(grads)
