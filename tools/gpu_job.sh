@@ -7,6 +7,8 @@
 #   tests=EXPR       ... -k EXPR
 #   bench            python bench.py (N = 1 defaults)        -> gpurun_out/bench.json (+ .log)
 #   bench=ARGS       python bench.py ARGS (spaces as commas)
+#   benchdist        GALA_BENCH_DIST=1 bench.py: the strong-scaling path over RCCL at world 1
+#                                                            -> gpurun_out/bench_dist.json
 #   prof             rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/prof_stats/
 #   pmc              FETCH_SIZE and WRITE_SIZE passes (one --pmc run each) of bench.py, then
 #                    tools/pmc_traffic.py                   -> gpurun_out/traffic.json
@@ -50,6 +52,11 @@ for s in "$@"; do
         a="${s#bench=}"
         step bench 900 python -u bench.py ${a//,/ } > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; }
         cat "$OUT/bench.json" ;;
+    benchdist)
+        # the partitioned path on this one GPU (RCCL at world 1: the collectives run)
+        GALA_BENCH_DIST=1 step benchdist 900 python -u bench.py --no-cpu-baseline > "$OUT/bench_dist.json" \
+            2> "$OUT/bench_dist.log" || { tail -30 "$OUT/bench_dist.log"; exit 1; }
+        cat "$OUT/bench_dist.json" ;;
     prof)
         (cd /tmp && step prof 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_stats" -o run \
             -- python3 "$GRAFT_REPO_ROOT/bench.py" $BENCH_PROF_ARGS > "$OUT/prof_stats.log" 2>&1) || exit 1 ;;
