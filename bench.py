@@ -220,17 +220,19 @@ class Timer:
             for _ in range(reps):
                 fn()
             return (time.perf_counter() - t0) / reps
+        # the kernels run on torch's current stream (gala.ops passes it to the C ABI).  One
+        # untimed call is queued first, so the stream is busy when the first event is
+        # recorded and the host's launch latency never shows as idle time between events
         stream = torch.cuda.current_stream()
-        ts = []
+        fn()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
         for _ in range(reps):
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record(stream)
             fn()
-            b.record(stream)
-            ts.append((a, b))
+        b.record(stream)
         torch.cuda.synchronize()
-        return float(np.mean([a.elapsed_time(b) for a, b in ts])) / 1e3
+        return a.elapsed_time(b) / 1e3 / reps
 
 
 def gather_ceiling(col, X, timer, reps=10):
