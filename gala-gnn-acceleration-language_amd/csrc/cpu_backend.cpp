@@ -725,19 +725,25 @@ extern "C" int gala_cpu_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, 
 static int cpu_gat_fwd_stats(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                              const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                              float slope, float *Y, int64_t ldy, float *q_out, float *Ym, int64_t ldym,
-                             float *sma, float *aR_out, float *p_out, bool partial) {
+                             float *sma, float *aR_out, float *p_out, bool partial,
+                             const int32_t *self_col = nullptr) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldym < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || !q_out || !Ym || !sma || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     if (!partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
-    if (aR_out && (aR || !X)) return GALA_ERR_INVALID_ARG;
+    if (aR_out && (aR || !X || (partial && !self_col))) return GALA_ERR_INVALID_ARG;
     std::vector<float> rc;
     if (!aR) {
         rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
         aR = rc.data();
-        if (aR_out) std::copy(rc.begin(), rc.begin() + A->n_rows * heads, aR_out);
+        if (aR_out && !self_col) std::copy(rc.begin(), rc.begin() + A->n_rows * heads, aR_out);
+        if (aR_out && self_col)  // the own vertices' logits (a vertex cut's rows are not its columns)
+            for (int64_t r = 0; r < A->n_rows; ++r)
+                if (self_col[r] >= 0)
+                    std::copy(rc.begin() + (int64_t)self_col[r] * heads, rc.begin() + ((int64_t)self_col[r] + 1) * heads,
+                              aR_out + (int64_t)self_col[r] * heads);
     }
     const int32_t H = heads, D = F / H, S = A->n_seg;
 #pragma omp parallel
@@ -795,6 +801,16 @@ extern "C" int gala_cpu_gat_fwd_partial_stats_f32(const gala_csr_t *A, const flo
                                                   float *msums, void *) {
     return cpu_gat_fwd_stats(A, aL, aR, wR, bR, X, ldx, F, heads, slope, U, ldu, sums, Um, ldum, msums, nullptr,
                              nullptr, true);
+}
+
+extern "C" int gala_cpu_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                                     const float *wR, const float *bR, const float *X,
+                                                     int64_t ldx, int32_t F, int32_t heads, float slope, float *U,
+                                                     int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                                     float *msums, const int32_t *self_col, float *aR_out, void *) {
+    if (aR_out && !self_col) return GALA_ERR_INVALID_ARG;
+    return cpu_gat_fwd_stats(A, aL, aR, wR, bR, X, ldx, F, heads, slope, U, ldu, sums, Um, ldum, msums, aR_out,
+                             nullptr, true, self_col);
 }
 
 // REF backward from the row statistics: dX as gala_cpu_gat_bwd_fused_f32, d_aL from

@@ -16,8 +16,9 @@ namespace gala {
 // head's (max, sum) of the softmax (FIXED: online, relative to m; REF: plain sums).
 // kRefStats adds the row statistics' sums: accm = sum m*p*X and sma = sum m*p (m the
 // LeakyReLU factor of the edge), both scaled by q at the store like acc and sum.
-// self_row >= 0 (RC row statistics with ar_out): the row's own recomputed source logit is
-// captured from its self-loop edge (ar_self, has_self), so the row's X line is not re-read.
+// self_row >= 0 (RC row statistics with ar_out): the column of the row's own vertex; its
+// recomputed source logit is captured from the self-loop edge (ar_self, has_self), so the
+// vertex's X line is not re-read.
 template <int VEC, int CH>
 struct FwdState {
     float acc[CH][VEC], accm[CH][VEC];
@@ -328,23 +329,26 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     if (!row_ok) return;
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     constexpr bool kArOut = RC && MODE == kRefStats && HW > 0;
-    // the row's own source logit for the backward's alpha, formed exactly as the per-edge
+    // the own vertex's source logit for the backward's alpha, formed exactly as the per-edge
     // recompute forms it (same lanes, same fma order and butterfly): taken from the row's
     // self-loop edge when it has one (every GALA graph does, gala_export_npy.py:73-74),
-    // else (and for hub rows, whose edges the chunk kernels walk) from a read of X[row]
-    auto ar_from_row = [&]() {
+    // else (and for hub rows, whose edges the chunk kernels walk) from a read of X[own].
+    // The own vertex is the row itself on one GPU, self_col[row] over a vertex cut (whose
+    // rows are destinations and whose columns are the rank's vertices).
+    const int64_t own = !kArOut || !d.ar_out ? -1 : d.self_col ? (int64_t)d.self_col[row] : row;
+    auto ar_of_own = [&]() {
         typedef typename GVec<VEC>::T V;
         V xr[CH];
 #pragma unroll
         for (int ch = 0; ch < CH; ++ch)
-            xr[ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + row * d.ldx + gl_.ln.off[ch]));
+            xr[ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + own * d.ldx + gl_.ln.off[ch]));
         return __fadd_rn(attn_dot<HW, VEC, CH>(gl_.w, xr), gl_.wb);
     };
     const bool hub = split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold;
     if constexpr (kArOut) {
-        if (d.ar_out && hub) {
-            const float a = ar_from_row();
-            if (gl_.leader) d.ar_out[row * gl_.H + gl_.hh] = a;
+        if (own >= 0 && hub) {
+            const float a = ar_of_own();
+            if (gl_.leader) d.ar_out[own * gl_.H + gl_.hh] = a;
         }
     }
     if (hub) return;  // hub row: k_gat_fwd_chunk / _fixup / k_gat_alpha_chunk
@@ -354,16 +358,16 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     // place: a contiguous re-read of the row instead of a second col -> aR gather.
     const bool park = d.alpha_out != nullptr && (G % H) == 0;
     FwdState<VEC, CH> st;
-    if constexpr (kArOut) st.self_row = d.ar_out ? row : -1;
+    if constexpr (kArOut) st.self_row = own;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
         gat_fwd_edges<G, VEC, U, MODE, CH, RC, HW>(p, d, gl_, park, e0, e1, st);
     }
     if constexpr (kArOut) {
-        if (d.ar_out) {
-            const float a = st.has_self ? st.ar_self : ar_from_row();
-            if (gl_.leader) d.ar_out[row * gl_.H + gl_.hh] = a;
+        if (own >= 0) {
+            const float a = st.has_self ? st.ar_self : ar_of_own();
+            if (gl_.leader) d.ar_out[own * gl_.H + gl_.hh] = a;
         }
     }
     const float q = gat_fwd_store<G, VEC, CH, RC, MODE>(d, gl_, row, p.seg.n, st);
@@ -807,7 +811,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                         float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
                         float *q_out, void *stream, float *ym = nullptr, int64_t ldym = 0,
-                        float *sma = nullptr, float *ar_out = nullptr) {
+                        float *sma = nullptr, float *ar_out = nullptr, const int32_t *self_col = nullptr) {
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
@@ -821,7 +825,8 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (q_out && mode != GALA_SOFTMAX_REF) return GALA_ERR_INVALID_ARG;
     if (partial && (mode != GALA_SOFTMAX_REF || !q_out || alpha_out)) return GALA_ERR_INVALID_ARG;
     if (stats && (mode != GALA_SOFTMAX_REF || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
-    if (stats && partial && (ar_out || alpha_out)) return GALA_ERR_INVALID_ARG;
+    // a partial pattern's rows are not its columns: aR_out needs the own-vertex map
+    if (stats && partial && (alpha_out || (ar_out && !self_col))) return GALA_ERR_INVALID_ARG;
     // square pattern (the backward's dY[col] / aR_out of the row's own X); a vertex cut's
     // partial forward reads X by column only
     if (stats && !partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
@@ -847,7 +852,7 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.d.aL = aL, a.d.aR = aR, a.d.wR = wR, a.d.bR = bR, a.d.X = X, a.d.ldx = ldx, a.d.F = F;
     a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out, a.d.q_out = q_out;
     a.d.partial = partial ? 1 : 0;
-    a.d.ym_out = ym, a.d.ldym = ldym, a.d.sma_out = sma, a.d.ar_out = ar_out;
+    a.d.ym_out = ym, a.d.ldym = ldym, a.d.sma_out = sma, a.d.ar_out = ar_out, a.d.self_col = self_col;
     a.hs = (hipStream_t)stream;
     // hub-row chunk partials: {acc[F], m[H], sum[H]} (+ {accm[F], sma[H]} with the statistics)
     const int64_t ws_need = stats ? 2 * (int64_t)F + 3 * heads : (int64_t)F + 2 * heads;
@@ -906,6 +911,23 @@ extern "C" int gala_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
                         GALA_SOFTMAX_REF | GALA_GAT_PARTIAL, U, ldu, nullptr, sums, stream, Um, ldum, msums,
                         nullptr);
+}
+
+// The same with the rank's own vertices' recomputed source logits: row r's own vertex is
+// column self_col[r] (-1: none); aR_out[self_col[r] * heads + h] is written bit-identical to
+// the logit the kernel forms for that column's edges (the backward's alpha then matches).
+extern "C" int gala_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                                 const float *wR, const float *bR, const float *X,
+                                                 int64_t ldx, int32_t F, int32_t heads, float slope, float *U,
+                                                 int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                                 float *msums, const int32_t *self_col, float *aR_out,
+                                                 void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if ((!Um || !sums || !msums) && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if (aR_out && !self_col) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
+                        GALA_SOFTMAX_REF | GALA_GAT_PARTIAL, U, ldu, nullptr, sums, stream, Um, ldum, msums,
+                        aR_out, self_col);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

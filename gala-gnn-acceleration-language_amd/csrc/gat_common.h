@@ -94,6 +94,8 @@ struct GatDev {
     int32_t partial;                 // forward, GALA_GAT_PARTIAL: unnormalised Y, raw sums in q_out
     // REF row statistics (gala_gat_{fwd,bwd}_stats_f32): Ym = sum m*alpha*X, sma = sum m*alpha
     float *ym_out, *sma_out, *ar_out;  // forward (ar_out: the rows' recomputed aR, nullable)
+    const int32_t *self_col;           // forward with ar_out, nullable: the column of each row's own
+                                       // vertex (-1: not held); NULL = the row itself (square)
     const float *ys, *yms, *smas;      // backward: Y (ld ldy), Ym (ld ldym), sma
     int64_t ldym;
 };

@@ -45,11 +45,13 @@ class HipBackend:
         """REF GAT forward over one column range, unnormalised (GALA_GAT_PARTIAL)."""
         return self.ops.gat_fwd_partial(g, aL, X, aR=aR, heads=heads, slope=slope, Y=Y, sums=sums)
 
-    def gat_partial_stats(self, g, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None):
+    def gat_partial_stats(self, g, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None,
+                          self_col=None, aR_out=None):
         """REF row-statistics forward over one column range, unnormalised (vertex cut); aR
-        None: recomputed per head from X (wR, bR)."""
+        None: recomputed per head from X (wR, bR), and with self_col / aR_out the own
+        vertices' recomputed logits are written out."""
         return self.ops.gat_fwd_partial_stats(g, aL, X, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, U=U,
-                                              sums=sums, Um=Um, msums=msums)
+                                              sums=sums, Um=Um, msums=msums, self_col=self_col, aR_out=aR_out)
 
     def gat_bwd_stats(self, g, aL, aR, dY, q, Y, Ym, sma, heads, slope):
         """(dX, d_aL) of the REF layer from its row statistics (gala_gat_bwd_stats_f32)."""
@@ -153,10 +155,11 @@ class CpuBackend:
                       _hp(sums), None)
         return Y, sums
 
-    def gat_partial_stats(self, g: CpuGraph, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None):
-        _abi.call_cpu("gala_gat_fwd_partial_stats_f32", g.csr(), _hp(aL), _hp(aR), _hp(wR), _hp(bR), _hp(X),
+    def gat_partial_stats(self, g: CpuGraph, aL, aR, X, heads, slope, U, sums, Um, msums, wR=None, bR=None,
+                          self_col=None, aR_out=None):
+        _abi.call_cpu("gala_gat_fwd_partial_stats_ex_f32", g.csr(), _hp(aL), _hp(aR), _hp(wR), _hp(bR), _hp(X),
                       X.stride(0), X.shape[1], heads, slope, _hp(U), U.stride(0), _hp(sums), _hp(Um), Um.stride(0),
-                      _hp(msums), None)
+                      _hp(msums), _hp(self_col), _hp(aR_out), None)
         return U, sums, Um, msums
 
     def gat_bwd_stats(self, g: CpuGraph, aL, aR, dY, q, Y, Ym, sma, heads, slope):

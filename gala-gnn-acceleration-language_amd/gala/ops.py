@@ -365,18 +365,23 @@ def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slo
 
 
 def gat_fwd_partial_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, U=None, sums=None,
-                          Um=None, msums=None):
+                          Um=None, msums=None, self_col=None, aR_out=None):
     """gala_gat_fwd_partial_stats_f32 (vertex cut): the row-statistics forward over one
     column range, unnormalised -- (U, sums, Um, msums) = (sum p X, sum p, sum m p X, sum m p)
-    per row (and head); U / Um may be strided views (e.g. the two halves of one buffer)."""
+    per row (and head); U / Um may be strided views (e.g. the two halves of one buffer).
+    self_col (int32 [rows], -1 = none) + aR_out ([n_cols, heads]): the own vertices'
+    recomputed source logits (gala_gat_fwd_partial_stats_ex_f32)."""
     F = X.shape[1]
     U = _rows_like(X, g.n_rows) if U is None else U
     Um = _rows_like(X, g.n_rows) if Um is None else Um
     sums = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if sums is None else sums
     msums = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32) if msums is None else msums
-    _abi.call("gala_gat_fwd_partial_stats_f32", g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR),
-              _dp(wR), _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(U), U.stride(0), _dp(sums), _dp(Um),
-              Um.stride(0), _dp(msums), _stream())
+    args = (g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X), X.stride(0), F,
+            heads, slope, _dp(U), U.stride(0), _dp(sums), _dp(Um), Um.stride(0), _dp(msums))
+    if self_col is None and aR_out is None:
+        _abi.call("gala_gat_fwd_partial_stats_f32", *args, _stream())
+    else:
+        _abi.call("gala_gat_fwd_partial_stats_ex_f32", *args, _dp(self_col), _dp(aR_out), _stream())
     return U, sums, Um, msums
 
 

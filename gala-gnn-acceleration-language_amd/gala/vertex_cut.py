@@ -55,6 +55,7 @@ class SparseExchange:
     recv_counts: np.ndarray
     recv_graph: layout.HostGraph
     send_dense_rows: list       # per chunk: int64 row of every compact row in the dense layout
+    send_self_cols: list        # per chunk: int32 own-vertex column of every compact row (-1: none)
 
 
 @dataclass
@@ -93,6 +94,17 @@ class VertexCutPartition:
             sc[:, self.rank] = 0
             return 4 * F * int(sc.sum())
         return 4 * F * self.chunks * self.block * (self.world - 1)
+
+    def self_cols(self, k: int) -> np.ndarray:
+        """int32 [rows of chunk k]: the local column of each partial row's own vertex, -1
+        for rows of other owners (the own-vertex map of gala_gat_fwd_partial_stats_ex_f32)."""
+        if self.exchange == "sparse":
+            return self.sparse.send_self_cols[k]
+        P, c, p = self.world, self.block, self.rank
+        out = np.full(P * c, -1, np.int32)
+        j = np.arange(k * c, min((k + 1) * c, self.n), dtype=np.int32)
+        out[p * c + (j - k * c)] = j
+        return out
 
     def chunk_nnz(self) -> int:
         gs = self.sparse.send_graphs if self.exchange == "sparse" else self.chunk_graphs
@@ -176,12 +188,16 @@ def _sparse_exchange(g, b, rank, K, c, sel, cnt, rk, pos, edge_k) -> SparseExcha
     P = b.shape[0] - 1
     c0, c1 = int(b[rank]), int(b[rank + 1])
     owner_of = lambda r: np.searchsorted(b, r, side="right") - 1  # noqa: E731
+    # the rows a rank holds edges of, and always its own rows: each own vertex then has a
+    # compact row for its own source logit (VertexCutGat's aR_out), at the cost of a local copy
     touched = cnt > 0
-    send_graphs, dense_rows = [], []
+    touched[c0:c1] = True
+    send_graphs, dense_rows, self_rows = [], [], []
     send_counts = np.zeros((K, P), np.int64)
     for k in range(K):
         rows = np.flatnonzero(touched & (rk == k))              # owner-major, ascending
         send_counts[k] = np.bincount(owner_of(rows), minlength=P)[:P]
+        self_rows.append(np.where((rows >= c0) & (rows < c1), rows - c0, -1).astype(np.int32))
         rowptr = np.zeros(rows.shape[0] + 1, np.int64)
         np.cumsum(cnt[rows], out=rowptr[1:])
         keep = sel if K == 1 else (sel & (edge_k == k))
@@ -195,6 +211,7 @@ def _sparse_exchange(g, b, rank, K, c, sel, cnt, rk, pos, edge_k) -> SparseExcha
     lrow = np.repeat(np.arange(n, dtype=np.int64), np.diff(g.rowptr[c0:c1 + 1].astype(np.int64)))
     T = np.zeros((n, P), bool)
     T[lrow, owner_of(g.col[e0:e1])] = True
+    T[:, rank] = True                                           # the own rows always come back
     recv_counts = np.zeros((K, P), np.int64)
     cols = []
     base = 0
@@ -209,7 +226,7 @@ def _sparse_exchange(g, b, rank, K, c, sel, cnt, rk, pos, edge_k) -> SparseExcha
     np.cumsum(T.sum(1), out=rowptr[1:])
     col = np.concatenate(cols).astype(np.int32) if cols else np.zeros(0, np.int32)
     recv = layout.HostGraph(n, max(base, 1), rowptr.astype(np.int32), col)
-    return SparseExchange(send_graphs, send_counts, recv_counts, recv, dense_rows)
+    return SparseExchange(send_graphs, send_counts, recv_counts, recv, dense_rows, self_rows)
 
 
 class _PartialRows:
@@ -389,12 +406,14 @@ class VertexCutGat(_PartialRows):
         P, c, K = part.world, part.block, part.chunks
         self.aLpad = backend.empty(K * c, heads)
         self.aLall = backend.empty(K * P * c, heads)
+        import torch
+        dev = getattr(backend, "device", torch.device("cpu"))
         if self.sparse:
-            import torch
-            dev = getattr(backend, "device", torch.device("cpu"))
             self._al_idx = [torch.from_numpy(np.ascontiguousarray(r, np.int64)).to(dev)
                             for r in part.sparse.send_dense_rows]
             self.aLsend = backend.empty(self.n_send, heads)
+        # each own vertex's row in some chunk: the partial forward writes its source logit
+        self._self_col = [torch.from_numpy(np.ascontiguousarray(part.self_cols(k))).to(dev) for k in range(K)]
         self._fw = None      # eval-forward buffers
         self._train = None   # forward_train / backward buffers, allocated on first use
         self.saved = None
@@ -474,19 +493,22 @@ class VertexCutGat(_PartialRows):
         """aL [n, H] (own rows), aR [n, H], X [n, F] (own columns) -> Y [n, F]; keeps the
         row statistics (q, Y, Ym, sma of the own rows) for `backward`.  aR None: the source
         logits are the per-head Linear (wR [F], bR [H]) of X, recomputed inside the kernel
-        from the gathered rows (the DSL's attnR = ffn(res, out=1)); the backward then takes
-        them from one gala_head_attn_f32 pass over the own rows."""
+        from the gathered rows (the DSL's attnR = ffn(res, out=1)); the same kernels also
+        write the own vertices' logits (each from its self-loop edge, gala_gat_fwd_partial_
+        stats_ex_f32), which the backward's alpha reuses bit for bit."""
         H, F, n, b = self.H, self.F, self.part.n, self._train_buffers()
         al_works = self._post_aL(aL)
         works = []
+        aR_own = self.be.empty(n, H) if aR is None else None
         for k, gk in enumerate(self.graphs):
             UUk = self.send_rows(b["UU"], k)
             self.be.gat_partial_stats(gk, self._chunk_aL(k, al_works), aR, X, H, self.slope, UUk[:, :F],
                                       self.send_rows(b["S"], k), UUk[:, F:], self.send_rows(b["M"], k),
-                                      wR=wR, bR=bR)
+                                      wR=wR, bR=bR, self_col=self._self_col[k] if aR is None else None,
+                                      aR_out=aR_own)
             works += [self.post(b["UU"], b["UUr"], k), self.post(b["S"], b["Sr"], k), self.post(b["M"], b["Mr"], k)]
-        if aR is None:   # the backward's source logits of the own columns
-            aR = self.be.head_attn(X, wR, bR, H)
+        if aR is None:   # the backward's source logits of the own columns: the forward's own
+            aR = aR_own
         self.wait(works)
         UUo, So, Mo = (self.own_rows(b[r], b[o], view_ok=True) for r, o in (("UUr", "UUo"), ("Sr", "So"), ("Mr", "Mo")))
         q = 1.0 / (So + 1e-12)

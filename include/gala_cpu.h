@@ -94,6 +94,11 @@ int gala_cpu_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *aL, con
                                        const float *wR, const float *bR, const float *X, int64_t ldx,
                                        int32_t F, int32_t heads, float slope, float *U, int64_t ldu,
                                        float *sums, float *Um, int64_t ldum, float *msums, void *stream);
+int gala_cpu_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *wR, const float *bR, const float *X, int64_t ldx,
+                                          int32_t F, int32_t heads, float slope, float *U, int64_t ldu,
+                                          float *sums, float *Um, int64_t ldum, float *msums,
+                                          const int32_t *self_col, float *aR_out, void *stream);
 int gala_cpu_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,
                            const float *w, const float *b, float *out, void *stream);
 int gala_cpu_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float *g,

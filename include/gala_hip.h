@@ -387,6 +387,19 @@ int gala_gat_fwd_partial_stats_f32(const gala_csr_t *A, const float *aL, const f
                                    const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                                    float slope, float *U, int64_t ldu, float *sums, float *Um, int64_t ldum,
                                    float *msums, void *stream);
+/*
+ * gala_gat_fwd_partial_stats_ex_f32: the same, and with the source logits recomputed (aR
+ * NULL, wR given) also the rank's own vertices' logits: a vertex cut's rows are destination
+ * rows and its columns the rank's vertices, so self_col[r] names the column of row r's own
+ * vertex (-1 when the rank does not own it).  aR_out[self_col[r]*heads + h] is the logit the
+ * kernel forms for that column's edges, taken from the row's self-loop edge (else from the
+ * vertex's X row), bit for bit: the backward's alpha uses exactly the forward's logits.
+ * aR_out needs self_col (and the recompute).
+ */
+int gala_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                                      const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                                      float slope, float *U, int64_t ldu, float *sums, float *Um, int64_t ldum,
+                                      float *msums, const int32_t *self_col, float *aR_out, void *stream);
 
 /*
  * Per-head attention logits of the multi-head GAT layer (galac gat_heads: the DSL's

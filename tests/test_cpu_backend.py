@@ -378,3 +378,42 @@ def test_random_case(seed):
         np.testing.assert_allclose(daL, daL_ref, **TOL)
         if mode == _abi.GALA_SOFTMAX_FIXED:
             np.testing.assert_allclose(dz, dz_ref, **TOL)
+
+
+def test_partial_stats_own_vertex_logits():
+    """gala_cpu_gat_fwd_partial_stats_ex_f32: with self_col the recomputed logits of the own
+    vertices are written (the vertex cut's backward reuses them); aR_out without self_col is
+    refused for a partial pattern."""
+    import torch
+    from gala import vertex_cut as vc
+    from gala.backend import CpuBackend
+    g = powerlaw(n=1500, m=9000)
+    H, F = 2, 16
+    rng = np.random.default_rng(8)
+    X = torch.from_numpy(rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32))
+    aL = torch.from_numpy(rng.uniform(-1, 1, (g.n_rows, H)).astype(np.float32))
+    wR = torch.from_numpy(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR = torch.from_numpy(rng.uniform(-0.5, 0.5, H).astype(np.float32))
+    be = CpuBackend()
+    want = be.head_attn(X, wR, bR, H)        # the CPU twin recomputes with the same dot
+    for exchange in ("dense", "sparse"):
+        for p in range(3):
+            pt = vc.vertex_cut_partition(g, p, 3, chunks=2, exchange=exchange)
+            own = slice(pt.r0, pt.r0 + pt.n)
+            got = torch.full((pt.n, H), float("nan"))
+            hs = pt.sparse.send_graphs if exchange == "sparse" else pt.chunk_graphs
+            for k, h in enumerate(hs):
+                cg = be.graph(h)
+                U, Um = torch.empty((h.n_rows, F)), torch.empty((h.n_rows, F))
+                S, M = torch.empty(h.n_rows * H), torch.empty(h.n_rows * H)
+                al = torch.zeros((h.n_rows, H))
+                be.gat_partial_stats(cg, al, None, X[own].contiguous(), H, 0.2, U, S, Um, M, wR=wR, bR=bR,
+                                     self_col=torch.from_numpy(pt.self_cols(k)), aR_out=got)
+            np.testing.assert_allclose(got.numpy(), want[own].numpy(), rtol=1e-6, atol=1e-6)
+    with pytest.raises(_abi.GalaError):
+        cg = be.graph(pt.sparse.send_graphs[0])
+        n0 = pt.sparse.send_graphs[0].n_rows
+        _abi.call_cpu("gala_gat_fwd_partial_stats_ex_f32", cg.csr(), torch.zeros(n0 * H).data_ptr(), None,
+                      wR.data_ptr(), bR.data_ptr(), X[own].contiguous().data_ptr(), F, F, H, 0.2,
+                      torch.empty(n0, F).data_ptr(), F, torch.empty(n0 * H).data_ptr(), torch.empty(n0, F).data_ptr(),
+                      F, torch.empty(n0 * H).data_ptr(), None, torch.empty(pt.n * H).data_ptr(), None)

@@ -158,8 +158,9 @@ def test_vertex_cut_layout(name, world, chunks):
 @pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (3, 2), (4, 3)])
 def test_vertex_cut_sparse_layout(name, world, chunks):
     """DCSR send rows + receive CSR: a rank sends exactly the destination rows it holds
-    edges of (owner-major, ascending), every edge is held once, and what each owner's
-    receive CSR expects from source q in chunk k is what q sends it, row for row."""
+    edges of and its own rows (owner-major, ascending), every edge is held once, and what
+    each owner's receive CSR expects from source q in chunk k is what q sends it, row for
+    row."""
     g = GRAPHS[name]()
     parts = [vc.vertex_cut_partition(g, p, world, chunks=chunks, exchange="sparse") for p in range(world)]
     rows_all = np.repeat(np.arange(g.n_rows), np.diff(g.rowptr))
@@ -175,7 +176,9 @@ def test_vertex_cut_sparse_layout(name, world, chunks):
             q, j = d // pt.block, k * pt.block + d % pt.block
             grow = pt.bounds[q] + j
             assert np.all(np.diff(grow) > 0)                          # owner-major, ascending
-            assert np.all(np.diff(h.rowptr) > 0)                      # only rows with a held edge
+            # only rows with a held edge, plus the rank's own rows (their own-vertex logits)
+            assert np.all((np.diff(h.rowptr) > 0) | (q == p))
+            np.testing.assert_array_equal(sp.send_self_cols[k], np.where(q == p, grow - pt.r0, -1))
             np.testing.assert_array_equal(np.bincount(q, minlength=world), sp.send_counts[k])
             er = np.repeat(grow, np.diff(h.rowptr))
             seen.append(np.stack([er, h.col.astype(np.int64) + pt.r0]))

@@ -311,6 +311,19 @@ def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
         _, daL = ops.gat_bwd_stats(eg, cu(aL[sl]), cu(aR[sl]), cu(dY[sl]), q.contiguous(), Y, Ym,
                                    sma.contiguous(), heads=heads)
         torch.testing.assert_close(daL, daL1.view(-1, heads)[sl].reshape(-1), rtol=1e-4, atol=1e-4)
+    # the own vertices' recomputed logits (gala_gat_fwd_partial_stats_ex_f32 with self_col):
+    # every rank's chunks write exactly the one-GPU statistics forward's aR_out of its rows
+    wR0 = cu(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR0 = cu(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+    *_, aR0 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR0, bR=bR0, heads=heads, want_aR=True)
+    for pt in parts:
+        own = slice(pt.r0, pt.r0 + pt.n)
+        got = torch.full((pt.n, heads), float("nan"), device="cuda")
+        for k, h in enumerate(pt.chunk_graphs):
+            gk = ops.DeviceGraph.from_host(h, split=pt.split_threshold)
+            ops.gat_fwd_partial_stats(gk, aL_rows[k * rows:(k + 1) * rows].contiguous(), cu(X[own]), wR=wR0,
+                                      bR=bR0, heads=heads, self_col=cu(pt.self_cols(k)), aR_out=got)
+        assert torch.equal(got.reshape(-1), aR0.view(-1, heads)[own].reshape(-1))
     if world == 1:
         from gala.backend import HipBackend
         gat = vc.VertexCutGat(parts[0], F, heads, HipBackend("cuda"), None)
@@ -325,6 +338,7 @@ def test_vertex_cut_gat_training_matches_one_gpu(world, chunks, heads, F):
         Y2, q2, Ym2, sma2, aR2 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR, bR=bR, heads=heads, want_aR=True)
         dX2, daL2 = ops.gat_bwd_stats(dg, cu(aL), aR2, cu(dY), q2, Y2, Ym2, sma2, heads=heads)
         Yr = gat.forward_train(cu(aL), None, cu(X), wR, bR)
+        assert torch.equal(gat.saved[1].reshape(-1), aR2)   # the forward's own-vertex logits, bit for bit
         dXr, daLr, _, _ = gat.backward(cu(dY))       # dX includes the path through aR = X wR + bR
         dX2 = ops.head_attn_bwd(daL2.view(-1, heads), wR, heads=heads, dX=dX2.clone())
         torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
@@ -422,6 +436,7 @@ def test_vertex_cut_sparse_classes_on_one_rank(heads, F):
     dX2 = ops.head_attn_bwd(daL2.view(-1, heads), wR, heads=heads, dX=dX2.clone())
     gat = vc.VertexCutGat(pt, F, heads, be, None)
     Yr = gat.forward_train(aL, None, X, wR, bR)
+    assert torch.equal(gat.saved[1].reshape(-1), aR2)       # own-vertex logits from the compact rows
     dXr, daLr, dW, db = gat.backward(dY)
     torch.testing.assert_close(Yr, Y2, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(daLr.reshape(-1), daL2, rtol=1e-4, atol=1e-4)
