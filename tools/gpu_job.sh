@@ -4,7 +4,7 @@
 # abort or time limit).  Output goes to gpurun_out/.
 #
 #   tests            python -m pytest tests -m gpu            -> gpurun_out/pytest_gpu.log
-#   tests=EXPR       ... -k EXPR
+#   tests=EXPR       ... -k EXPR ("_or_" stands for " or ")
 #   bench            python bench.py (N = 1 defaults)        -> gpurun_out/bench.json (+ .log)
 #   bench=ARGS       python bench.py ARGS (spaces as commas)
 #   benchdist        GALA_BENCH_DIST=1 bench.py: the strong-scaling path over RCCL at world 1
@@ -42,7 +42,8 @@ for s in "$@"; do
             > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
         tail -3 "$OUT/pytest_gpu.log" ;;
     tests=*)
-        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "${s#tests=}" \
+        k="${s#tests=}"
+        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "${k//_or_/ or }" \
             > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
         tail -3 "$OUT/pytest_gpu.log" ;;
     bench)
