@@ -732,7 +732,7 @@ static int cpu_gat_fwd_stats(const gala_csr_t *A, const float *aL, const float *
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldym < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !wR) || !Y || !q_out || !Ym || !sma || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
-    if (!partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (!partial && !self_col && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
     if (aR_out && (aR || !X || (partial && !self_col))) return GALA_ERR_INVALID_ARG;
     std::vector<float> rc;
     if (!aR) {
@@ -813,20 +813,29 @@ extern "C" int gala_cpu_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const 
                              nullptr, true, self_col);
 }
 
+extern "C" int gala_cpu_gat_fwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                             const float *wR, const float *bR, const float *X, int64_t ldx,
+                                             int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,
+                                             float *q_out, float *Ym, int64_t ldym, float *sma,
+                                             const int32_t *self_col, float *aR_out, float *p_out, void *) {
+    return cpu_gat_fwd_stats(A, aL, aR, wR, bR, X, ldx, F, heads, slope, Y, ldy, q_out, Ym, ldym, sma, aR_out,
+                             p_out, false, self_col);
+}
+
 // REF backward from the row statistics: dX as gala_cpu_gat_bwd_fused_f32, d_aL from
-// <dY, Y> and <dY, Ym>
-extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
-                                          const float *pe, const float *dY, int64_t lddy, int32_t F, int32_t heads,
-                                          float slope, const float *q, const float *Y, int64_t ldy,
-                                          const float *Ym, int64_t ldym, const float *sma, float *dX,
-                                          int64_t lddx, float *d_aL, void *) {
+// <dY, Y> and <dY, Ym>; dY_rows: the rows' own dY when dY is a gathered table
+static int cpu_gat_bwd_stats(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                             const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
+                             float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
+                             int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL) {
     int st = check_csr(A);
     if (st) return st;
     if (heads < 1 || F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F)
         return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !pe) || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
-    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (!dY_rows && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    const float *dYr = dY_rows ? dY_rows : dY;
     const int32_t H = heads, D = F / H, S = A->n_seg;
     const float eps = (float)S * 1e-12f;
 #pragma omp parallel for schedule(dynamic, kRowChunk)
@@ -854,14 +863,32 @@ extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, 
         for (int32_t h = 0; h < H; ++h) {
             float syy = 0.0f, sym = 0.0f;
             for (int32_t f = h * D; f < (h + 1) * D; ++f) {
-                syy = fmaf(dY[r * lddy + f], Y[r * ldy + f], syy);
-                sym = fmaf(dY[r * lddy + f], Ym[r * ldym + f], sym);
+                syy = fmaf(dYr[r * lddy + f], Y[r * ldy + f], syy);
+                sym = fmaf(dYr[r * lddy + f], Ym[r * ldym + f], sym);
             }
             const float acc = syy + eps;
             d_aL[r * H + h] = (sym - acc * sma[r * H + h]) + eps;
         }
     }
     return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                          const float *pe, const float *dY, int64_t lddy, int32_t F, int32_t heads,
+                                          float slope, const float *q, const float *Y, int64_t ldy,
+                                          const float *Ym, int64_t ldym, const float *sma, float *dX,
+                                          int64_t lddx, float *d_aL, void *) {
+    return cpu_gat_bwd_stats(A, aL, aR, pe, dY, lddy, nullptr, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
+                             d_aL);
+}
+
+extern "C" int gala_cpu_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                             const float *pe, const float *dY, int64_t lddy, const float *dY_rows,
+                                             int32_t F, int32_t heads, float slope, const float *q, const float *Y,
+                                             int64_t ldy, const float *Ym, int64_t ldym, const float *sma,
+                                             float *dX, int64_t lddx, float *d_aL, void *) {
+    return cpu_gat_bwd_stats(A, aL, aR, pe, dY, lddy, dY_rows, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
+                             d_aL);
 }
 
 extern "C" int gala_cpu_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,

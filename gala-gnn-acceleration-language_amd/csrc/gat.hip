@@ -827,9 +827,10 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (stats && (mode != GALA_SOFTMAX_REF || !q_out || !sma)) return GALA_ERR_INVALID_ARG;
     // a partial pattern's rows are not its columns: aR_out needs the own-vertex map
     if (stats && partial && (alpha_out || (ar_out && !self_col))) return GALA_ERR_INVALID_ARG;
-    // square pattern (the backward's dY[col] / aR_out of the row's own X); a vertex cut's
-    // partial forward reads X by column only
-    if (stats && !partial && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    // square pattern (the backward's dY[col] / aR_out of the row's own X) unless self_col
+    // maps each row to its own column (a halo table); a vertex cut's partial forward reads
+    // X by column only
+    if (stats && !partial && !self_col && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
     if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
@@ -897,6 +898,19 @@ extern "C" int gala_gat_fwd_stats_f32(const gala_csr_t *A, const float *aL, cons
     if (!Ym && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
                         GALA_SOFTMAX_REF, Y, ldy, p_out, q_out, stream, Ym, ldym, sma, aR_out);
+}
+
+// The statistics forward over a gathered table (a row partition's halo): row r's own vertex
+// is column self_col[r], which lets the pattern be rectangular; aR_out is column-indexed.
+extern "C" int gala_gat_fwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                         const float *wR, const float *bR, const float *X, int64_t ldx,
+                                         int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,
+                                         float *q_out, float *Ym, int64_t ldym, float *sma,
+                                         const int32_t *self_col, float *aR_out, float *p_out, void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if (!Ym && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
+                        GALA_SOFTMAX_REF, Y, ldy, p_out, q_out, stream, Ym, ldym, sma, aR_out, self_col);
 }
 
 // The row-statistics forward over one column range of a vertex cut: every output unnormalised

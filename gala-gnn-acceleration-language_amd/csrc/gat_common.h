@@ -97,6 +97,8 @@ struct GatDev {
     const int32_t *self_col;           // forward with ar_out, nullable: the column of each row's own
                                        // vertex (-1: not held); NULL = the row itself (square)
     const float *ys, *yms, *smas;      // backward: Y (ld ldy), Ym (ld ldym), sma
+    const float *dy_rows;              // backward, nullable: the rows' own dY (row r at dy_rows + r*lddy)
+                                       // when dY is a gathered table whose row r is not column r
     int64_t ldym;
 };
 
@@ -134,9 +136,10 @@ template <int G, int VEC, int CH, bool RC>
 __device__ __forceinline__ void load_dy(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_, int64_t row,
                                         float (&dy)[CH][VEC]) {
     typedef typename GVec<VEC>::T V;
+    const float *base = d.dy_rows ? d.dy_rows : d.dY;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
-        const V t = *reinterpret_cast<const V *>(d.dY + row * d.lddy + gl_.ln.off[ch]);
+        const V t = *reinterpret_cast<const V *>(base + row * d.lddy + gl_.ln.off[ch]);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dy[ch][i] = gl_.ln.in(ch, i) ? reinterpret_cast<const float *>(&t)[i] : 0.0f;
     }

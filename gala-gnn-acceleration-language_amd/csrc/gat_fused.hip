@@ -348,17 +348,20 @@ static int fused_dispatch(FusedArgs &a, int F, int heads, int vec, bool rc) {
     return launch_status();
 }
 
-extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
-                                      const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
-                                      const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
-                                      const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
+static int bwd_stats_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                          const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
+                          float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
+                          int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
     FusedArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
     if (F < 1 || F % heads != 0 || lddy < F || ldy < F || ldym < F || lddx < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!aL || (!aR && !pe) || !q || !dY || !Y || !Ym || !sma || !dX || !d_aL) return GALA_ERR_INVALID_ARG;
-    if (A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;  // dY[col]: a square pattern
+    // dY[col] and dY[row] are one array for a square pattern; a gathered table (a row
+    // partition's halo) passes the rows' own dY apart
+    if (!dY_rows && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (dY_rows && ((uintptr_t)dY_rows % 16) != ((uintptr_t)dY % 16)) return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     auto ok = [&](int v) {
         const bool fits = D % v == 0 || (heads == 1 && lddy >= pad_to(F, v) && ldy >= pad_to(F, v) &&
@@ -372,9 +375,27 @@ extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, cons
     a.d.aL = aL, a.d.aR = aR, a.d.F = F, a.d.slope = slope;
     a.d.dY = dY, a.d.lddy = lddy, a.d.q = q, a.d.dX = dX, a.d.lddx = lddx, a.d.d_aL = d_aL;
     a.d.ys = Y, a.d.ldy = ldy, a.d.yms = Ym, a.d.ldym = ldym, a.d.smas = sma, a.d.alpha = pe;
+    a.d.dy_rows = dY_rows;
     a.hs = (hipStream_t)stream;
     a.split = hub_split(A, pad_to(F, 4), &a.sp);  // hub rows: dX[F] chunk partials
     return fused_dispatch(a, F, heads, vec, false);
+}
+
+extern "C" int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                                      const float *dY, int64_t lddy, int32_t F, int32_t heads, float slope, const float *q,
+                                      const float *Y, int64_t ldy, const float *Ym, int64_t ldym,
+                                      const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
+    return bwd_stats_impl(A, aL, aR, pe, dY, lddy, nullptr, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
+                          d_aL, stream);
+}
+
+extern "C" int gala_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                                         const float *dY, int64_t lddy, const float *dY_rows, int32_t F,
+                                         int32_t heads, float slope, const float *q, const float *Y, int64_t ldy,
+                                         const float *Ym, int64_t ldym, const float *sma, float *dX, int64_t lddx,
+                                         float *d_aL, void *stream) {
+    return bwd_stats_impl(A, aL, aR, pe, dY, lddy, dY_rows, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
+                          d_aL, stream);
 }
 
 extern "C" int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,

@@ -61,6 +61,15 @@ class HipBackend:
         """[n, heads] per-head attention logits <X[:, head h], w_h> + b_h (gala_head_attn_f32)."""
         return self.ops.head_attn(X, w, b, heads=heads)
 
+    def gat_stats_table(self, g, aL, aR, X, heads, slope, self_col, aR_out, wR=None, bR=None):
+        """REF statistics forward over a gathered table (gala_gat_fwd_stats_ex_f32)."""
+        return self.ops.gat_fwd_stats(g, aL, X, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, self_col=self_col,
+                                      aR_out=aR_out)
+
+    def gat_bwd_stats_table(self, g, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope):
+        """(dX, d_aL) over a gathered table (gala_gat_bwd_stats_ex_f32)."""
+        return self.ops.gat_bwd_stats(g, aL, aR, dY, q, Y, Ym, sma, heads=heads, slope=slope, dY_rows=dY_rows)
+
     def row_scale_relu(self, act, pre, X, out):
         """out = pre * relu(act * X) (gala_row_scale_relu_f32: the ReLU prologue)."""
         return self.ops.row_scale_relu(X, act, pre, out=out)
@@ -169,6 +178,23 @@ class CpuBackend:
         _abi.call_cpu("gala_gat_bwd_stats_f32", g.csr(), _hp(aL), _hp(aR), None, _hp(dY), dY.stride(0), F, heads,
                       slope, _hp(q), _hp(Y), Y.stride(0), _hp(Ym), Ym.stride(0), _hp(sma), _hp(dX), dX.stride(0),
                       _hp(d_aL), None)
+        return dX, d_aL
+
+    def gat_stats_table(self, g: CpuGraph, aL, aR, X, heads, slope, self_col, aR_out, wR=None, bR=None):
+        n, F = g.n_rows, X.shape[1]
+        Y, Ym = torch.empty((n, F)), torch.empty((n, F))
+        q, sma = torch.empty(n * heads), torch.empty(n * heads)
+        _abi.call_cpu("gala_gat_fwd_stats_ex_f32", g.csr(), _hp(aL), _hp(aR), _hp(wR), _hp(bR), _hp(X), X.stride(0),
+                      F, heads, slope, _hp(Y), F, _hp(q), _hp(Ym), F, _hp(sma), _hp(self_col), _hp(aR_out), None, None)
+        return Y, q, Ym, sma
+
+    def gat_bwd_stats_table(self, g: CpuGraph, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope):
+        F = dY.shape[1]
+        dX = torch.empty((g.n_rows, F), dtype=torch.float32)
+        d_aL = torch.empty(g.n_rows * heads, dtype=torch.float32)
+        _abi.call_cpu("gala_gat_bwd_stats_ex_f32", g.csr(), _hp(aL), _hp(aR), None, _hp(dY), dY.stride(0),
+                      _hp(dY_rows), F, heads, slope, _hp(q), _hp(Y), Y.stride(0), _hp(Ym), Ym.stride(0), _hp(sma),
+                      _hp(dX), dX.stride(0), _hp(d_aL), None)
         return dX, d_aL
 
     def head_attn(self, X, w, b, heads):

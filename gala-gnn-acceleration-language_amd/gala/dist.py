@@ -509,3 +509,96 @@ class DistAggregator:
 
     def halo_bytes(self) -> int:
         return self.part.halo_bytes(self.F) if self.part.world > 1 else 0
+
+
+class HaloGat:
+    """The REF GAT layer's training pair over a row partition with a halo, computed exactly as
+    one GPU computes it.  Rank p gathers the feature rows its edges read (the halo: the
+    all-gather table or the p2p rows of a GraphPartition), then runs the one-GPU statistics
+    kernels over its own rows with the pattern's columns indexing the gathered table
+    (gala_gat_{fwd,bwd}_stats_ex_f32: self_col maps each row to its own table column, the
+    backward reads the rows' own dY apart from the table).  Every row keeps its CSR edge
+    order and the whole graph's hub-row chunks, so Y, dX and d_aL are BIT-identical to the
+    one-GPU pair.  Per layer it moves F + H floats per halo row forward (X, and the source
+    logits the forward recomputed for the backward) and F backward (dY); the vertex cut
+    (gala/vertex_cut.py VertexCutGat) moves 2F + 2H partial floats per row forward.
+
+      forward_train(aL, aR, X[, wR, bR]) -> Y      (aR None: recomputed from X per head)
+      backward(dY[, linear]) -> (dX, d_aL[, dwR, dbR])
+    X may already be written into `own_rows(F)` (the own block of the table) to skip a copy."""
+
+    def __init__(self, part: GraphPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
+        import torch
+        if part.chunks != 1:
+            raise ValueError("HaloGat: one halo chunk (the kernels read the whole table)")
+        self.part, self.F, self.H, self.be, self.comm, self.slope = part, F, heads, backend, comm, slope
+        self.graph = backend.graph(part.graph, split=part.split_threshold)
+        (j0, j1, x0), = part.own_blocks()
+        self.x0 = x0
+        dev = getattr(backend, "device", torch.device("cpu"))
+        self.self_col = torch.arange(x0, x0 + part.n, dtype=torch.int32, device=dev)
+        if comm is None:
+            self.exchange = None
+        elif part.halo_mode == "p2p":
+            self.exchange = HaloExchange(part, comm, backend.device)
+        else:
+            self.exchange = DenseHalo(part, comm)
+        zero = part.halo_mode == "dense" and part.world > 1   # padding rows: keep the table finite
+        self.Xs, self.dYs, self.As = (backend.empty(part.n_cols, w) for w in (F, F, heads))
+        if zero:
+            for t in (self.Xs, self.dYs, self.As):
+                t.zero_()
+        self.saved = None
+
+    def own_rows(self, which="X"):
+        """The own block of the X (or dY) table: write the layer input there to skip a copy."""
+        t = self.Xs if which == "X" else self.dYs
+        return t[self.x0:self.x0 + self.part.n]
+
+    def _gather(self, table, rows):
+        own = table[self.x0:self.x0 + self.part.n]
+        if rows is not None and rows.data_ptr() != own.data_ptr():
+            own.copy_(rows)
+        return [w for works in (self.exchange.start(table) if self.exchange else []) for w in works]
+
+    @staticmethod
+    def _wait(works):
+        for w in works:
+            if w is not None:
+                w.wait()
+
+    def forward_train(self, aL, aR, X, wR=None, bR=None):
+        n, H = self.part.n, self.H
+        self._wait(self._gather(self.Xs, X))
+        if aR is not None:                   # a given source logit: its table too
+            self._wait(self._gather(self.As, aR.reshape(n, H)))
+            ar_works = []
+            Y, q, Ym, sma = self.be.gat_stats_table(self.graph, aL, self.As, self.Xs, H, self.slope, self.self_col,
+                                                    None)
+        else:                                # recomputed in the kernel; the own logits written out
+            Y, q, Ym, sma = self.be.gat_stats_table(self.graph, aL, None, self.Xs, H, self.slope, self.self_col,
+                                                    self.As, wR=wR, bR=bR)
+            ar_works = self._gather(self.As, None)   # the backward's logits of the halo rows
+        self.saved = (aL, q, Y, Ym, sma, wR, ar_works)
+        return Y
+
+    def backward(self, dY, linear=True):
+        if self.saved is None:
+            raise RuntimeError("HaloGat.backward: no forward_train to take the row statistics from")
+        aL, q, Y, Ym, sma, wR, ar_works = self.saved
+        n, H = self.part.n, self.H
+        works = self._gather(self.dYs, dY)
+        self._wait(ar_works)
+        self._wait(works)
+        dX, d_aL = self.be.gat_bwd_stats_table(self.graph, aL, self.As, self.dYs, self.own_rows("dY"), q, Y, Ym,
+                                               sma, H, self.slope)
+        d_aL = d_aL.view(n, H)
+        if not (linear and wR is not None):
+            return dX, d_aL
+        dW, db = self.be.head_linear_grads(self.own_rows("X"), d_aL, H)   # REF: d_aR = d_aL
+        self.be.head_attn_bwd(d_aL, wR, H, dX)
+        return dX, d_aL, dW, db
+
+    def halo_bytes(self) -> int:
+        """Bytes this rank receives per forward + backward (X and dY rows, the logits)."""
+        return self.part.halo_bytes(2 * self.F + self.H) if self.part.world > 1 else 0

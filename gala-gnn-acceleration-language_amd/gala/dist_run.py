@@ -23,11 +23,12 @@ gala.cu.  This runtime executes the same post-pass IR (galac --ir-json) instead:
     an all-to-all of only the rows it holds edges of (`sparse`; `auto` picks by the graph's
     touched fraction) sums them into the owners' rows -- no halo; the sums regroup per
     rank, so results agree with one GPU to fp32 rounding.
-  * GAT programs (GAT_AGGREGATE, REF softmax; config 3's gat_heads(H) included) run on the
-    vertex cut: each GAT layer is a VertexCutGat training pair wrapped as an autograd
-    Function (row-statistics forward, REF backward with dX, d_aL and, when the source logit
-    is the layer's attention Linear of X, that Linear's gradients); per-head attention
-    Linears (gat_heads) are the block-diagonal `HeadLinear`.
+  * GAT programs (GAT_AGGREGATE, REF softmax; config 3's gat_heads(H) included): each GAT
+    layer is a training pair wrapped as an autograd Function (row-statistics forward, REF
+    backward with dX, d_aL and, when the source logit is the layer's attention Linear of X,
+    that Linear's gradients) -- gala/dist.py HaloGat on the halo layout (the one-GPU kernels
+    over a gathered table: bit-identical to one rank), VertexCutGat on the vertex cut;
+    per-head attention Linears (gat_heads) are the block-diagonal `HeadLinear`.
 Training subgraphs (graph g > 0) run on the whole graph: they only drop rows no training
 row depends on, so the training rows' values are unchanged.  The column-tiled layout
 (col_tile) is a single-device layout and is not used.
@@ -161,7 +162,7 @@ class HeadLinear(torch.nn.Module):
 
 
 class _VcutGatFfn(torch.autograd.Function):
-    """GAT aggregation over the vertex cut with the source logit recomputed from x (the
+    """GAT aggregation over ranks (HaloGat or VertexCutGat) with the source logit recomputed from x (the
     DSL's attnR = ffn(res, out=1) of the aggregated res): inputs aL [n, H], x [n, F], the
     attention Linear's w [1, F] and b [H]; REF backward (VertexCutGat.backward)."""
 
@@ -178,7 +179,7 @@ class _VcutGatFfn(torch.autograd.Function):
 
 
 class _VcutGat(torch.autograd.Function):
-    """GAT aggregation over the vertex cut with a given source logit aR [n, H]; the REF
+    """GAT aggregation over ranks (HaloGat or VertexCutGat) with a given source logit aR [n, H]; the REF
     backward returns the row sums as both d_aL and d_aR (common.h:622-675)."""
 
     @staticmethod
@@ -203,8 +204,6 @@ class Program:
         if bad:
             raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE / GAT programs)")
         if "GAT_AGGREGATE" in ops:
-            if layout_mode != "vcut":
-                raise NotImplementedError("gala.dist_run: GAT programs run on the vertex cut (--layout vcut)")
             if ir["sched"].get("gat_mode", 0) != 0:
                 raise NotImplementedError("gala.dist_run: FIXED-mode GAT (its backward needs A^T)")
         if not ir["sched"]["undirected"]:
@@ -226,6 +225,7 @@ class Program:
             self.part = gdist.partition_graph(graph, rank, world)
             self.agg = gdist.DistAggregator(self.part, 1, self.be, self.comm, exact=True)
             own_rowptr = self.part.graph.rowptr
+            self._gat = {}
         else:
             raise ValueError(f"gala.dist_run: layout {layout_mode!r} (halo | vcut)")
         self.deg = torch.from_numpy(np.diff(own_rowptr).astype(np.float32)).to(self.device).view(-1, 1)
@@ -257,11 +257,13 @@ class Program:
         return None if v is None else v.reshape(-1).contiguous()
 
     def _gat_layer(self, nd, F, H):
-        """The VertexCutGat of one GAT_AGGREGATE node (its buffers are width-specific)."""
+        """The GAT layer of one GAT_AGGREGATE node (its buffers are width-specific): HaloGat on
+        the row partition (bit-identical to one rank), VertexCutGat on the vertex cut."""
         from . import vertex_cut as vc
         key = nd["out"]
         if key not in self._gat:
-            self._gat[key] = vc.VertexCutGat(self.part, F, H, self.be, self.comm, slope=float(nd["param"]))
+            cls = vc.VertexCutGat if self.layout == "vcut" else gdist.HaloGat
+            self._gat[key] = cls(self.part, F, H, self.be, self.comm, slope=float(nd["param"]))
         return self._gat[key]
 
     def forward(self):

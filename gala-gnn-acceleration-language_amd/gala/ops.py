@@ -341,11 +341,22 @@ def gat_bwd_fused(g: DeviceGraph, aL, X, dY, q, aR=None, wR=None, bR=None, heads
 
 
 def gat_fwd_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, heads=1, slope=0.2, want_aR=False,
-                  want_p=False):
+                  want_p=False, self_col=None, aR_out=None):
     """gala_gat_fwd_stats_f32 (REF, square pattern): returns (Y, q, Ym, sma[, aR_out][, p]) with
     Ym[r] = sum_e m_e alpha_e X[col_e], sma[r, h] = sum_e m_e alpha_e (m_e the LeakyReLU
     factor); aR_out (aR recomputed from wR, bR) the rows' own source logits; p the edges'
-    exp terms."""
+    exp terms.  self_col (int32 [rows]): X is a gathered table whose column self_col[r] is
+    row r's own vertex (gala_gat_fwd_stats_ex_f32); aR_out is then a caller-given
+    column-indexed [n_cols, heads] buffer, written at the own columns."""
+    if self_col is not None:
+        F = X.shape[1]
+        Y, Ym = _rows_like(X, g.n_rows), _rows_like(X, g.n_rows)
+        q = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+        sma = torch.empty(g.n_rows * heads, device=X.device, dtype=torch.float32)
+        _abi.call("gala_gat_fwd_stats_ex_f32", g.csr(2 * ((F + 3) // 4 * 4) + 3 * heads), _dp(aL), _dp(aR), _dp(wR),
+                  _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(Y), Y.stride(0), _dp(q), _dp(Ym), Ym.stride(0),
+                  _dp(sma), _dp(self_col), _dp(aR_out), None, _stream())
+        return Y, q, Ym, sma
     F = X.shape[1]
     Y = _rows_like(X, g.n_rows)
     Ym = _rows_like(X, g.n_rows)
@@ -385,12 +396,18 @@ def gat_fwd_partial_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, head
     return U, sums, Um, msums
 
 
-def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None):
+def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None, dY_rows=None):
     """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
-    dY[col] only (alpha from aR, or from the forward's p when given)."""
+    dY[col] only (alpha from aR, or from the forward's p when given).  dY_rows: dY is a
+    gathered table and dY_rows the rows' own dY (gala_gat_bwd_stats_ex_f32)."""
     F = dY.shape[1]
     dX = _rows_like(dY, g.n_rows)
     d_aL = torch.empty(g.n_rows * heads, device=dY.device, dtype=torch.float32)
+    if dY_rows is not None:
+        _abi.call("gala_gat_bwd_stats_ex_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(p), _dp(dY),
+                  dY.stride(0), _dp(dY_rows), F, heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0),
+                  _dp(sma), _dp(dX), dX.stride(0), _dp(d_aL), _stream())
+        return dX, d_aL
     _abi.call("gala_gat_bwd_stats_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(p), _dp(dY), dY.stride(0), F,
               heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0), _dp(sma), _dp(dX), dX.stride(0),
               _dp(d_aL), _stream())

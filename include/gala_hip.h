@@ -373,6 +373,24 @@ int gala_gat_bwd_stats_f32(const gala_csr_t *A, const float *aL, const float *aR
                            int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
                            void *stream);
 /*
+ * The same pair over a gathered feature table (a row partition's halo, gala/dist.py
+ * HaloGat): the pattern's columns index the table (n_cols >= n_rows), so a row is no longer
+ * its own column.  gala_gat_fwd_stats_ex_f32: self_col[r] = the table column of row r's own
+ * vertex (NULL: r itself, square pattern), aR_out column-indexed ([n_cols, heads], written at
+ * the own columns).  gala_gat_bwd_stats_ex_f32: dY is the gathered table (dY[c] per edge),
+ * dY_rows the rows' own dY (row r at dY_rows + r*lddy, e.g. the table's own block; NULL:
+ * dY itself, square pattern).  Results equal the one-GPU pair's on the same rows bit for bit.
+ */
+int gala_gat_fwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
+                              const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
+                              float slope, float *Y, int64_t ldy, float *q_out, float *Ym, int64_t ldym,
+                              float *sma, const int32_t *self_col, float *aR_out, float *p_out, void *stream);
+int gala_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *p,
+                              const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
+                              float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
+                              int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
+                              void *stream);
+/*
  * gala_gat_fwd_partial_stats_f32: gala_gat_fwd_stats_f32 over the columns one rank of a
  * vertex cut holds, every output unnormalised so that the rows' owners add the ranks'
  * partials before they divide (GALA_GAT_PARTIAL of gala_gat_fwd_ex_f32, plus the row

@@ -471,3 +471,69 @@ def test_auto_halo_mode_is_one_choice_for_all_ranks():
         assert len(modes) == 1
         fr = gdist.halo_fractions(g, gdist.row_bounds(g.rowptr, world))
         assert modes == {"dense" if fr.max() > 0.5 else "p2p"}
+
+
+# ---- halo GAT: the one-GPU statistics kernels over a gathered table ----------------------------
+def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = GRAPHS[name]()
+        aL, aR, X = _gat_inputs(g)
+        dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
+        pt = gdist.partition_graph(g, rank, world, halo_mode=halo_mode)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        gat = gdist.HaloGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
+        t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
+        grads = []
+        if rc:
+            wR, bR = _gat_attn_weights()
+            gat.own_rows("X").copy_(t(X))               # written in place: no copy in forward_train
+            Y = gat.forward_train(t(aL), None, gat.own_rows("X"), torch.from_numpy(wR), torch.from_numpy(bR))
+            dX, d_aL, dW, db = gat.backward(t(dY))
+            for G in (dW, db):
+                dist.all_reduce(G)
+                grads.append(G.numpy().copy())
+        else:
+            Y = gat.forward_train(t(aL), t(aR), t(X))
+            dX, d_aL = gat.backward(t(dY))
+        sizes = [int(pt.bounds[r + 1] - pt.bounds[r]) for r in range(world)]
+        out = []
+        for T in (Y, dX, d_aL):
+            pad = torch.full((max(sizes), T.shape[1]), float("nan"))
+            pad[:pt.n] = T
+            ts = [torch.empty_like(pad) for _ in sizes]
+            dist.all_gather(ts, pad)
+            out.append(torch.cat([x[:s] for x, s in zip(ts, sizes)]).numpy())
+        if rank == 0:
+            q.put(out + grads)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,rc,halo_mode", [(2, "powerlaw", False, "p2p"), (3, "cora", True, "dense"),
+                                                     (3, "banded", True, "p2p"), (2, "empty_rows", False, "dense")])
+def test_halo_gat_bit_identical_to_one_process(world, name, rc, halo_mode):
+    """HaloGat (gala/dist.py): each rank runs the one-process statistics kernels over its rows
+    with the pattern's columns in the gathered table (gala_cpu_gat_{fwd,bwd}_stats_ex_f32):
+    Y, dX and d_aL are bit-identical to the one-process pair, the Linear's gradients within
+    fp32 rounding (summed over ranks)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_gat_worker, args=(r, world, port, name, rc, halo_mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _gat_train_one_process(GRAPHS[name](), rc)
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[2], ref[2])
+    if rc:     # the one-process reference adds the Linear path in float64
+        np.testing.assert_allclose(got[1], ref[1], rtol=1e-5, atol=1e-6)
+        for a, b in zip(got[3:], ref[3:]):
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+    else:
+        np.testing.assert_array_equal(got[1], ref[1])

@@ -368,7 +368,7 @@ def test_bench_self_launch_two_ranks_on_one_gpu_gloo():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["comm"]["backend"] == "gloo"
     assert set(d["comm"]["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
-    assert d["value"] > 0 and d["gat"]["value"] > 0 and "vertex cut x2" in d["gat"]["layout"]
+    assert d["value"] > 0 and d["gat"]["value"] > 0 and set(d["gat"]["candidates_ms_per_step"]) == {"halo", "vcut"}
     rm = d["rmat"]                                     # the skewed family at n_gpus 2
     assert rm["value"] > 0 and rm["comm"]["mode"] in rm["comm"]["candidates_ms_per_step"]
 
@@ -445,3 +445,50 @@ def test_vertex_cut_sparse_classes_on_one_rank(heads, F):
     g64 = daL2.view(-1, heads).double()
     torch.testing.assert_close(dW.double(), (g64.repeat_interleave(D, 1) * X.double()).sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db.double(), g64.sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("world,halo", [(1, "p2p"), (2, "dense"), (3, "p2p"), (4, "dense")])
+@pytest.mark.parametrize("kind,heads,F", [("uniform", 8, 256), ("rmat", 1, 32), ("rmat", 4, 64)])
+def test_halo_gat_bit_identical_to_one_gpu(world, halo, kind, heads, F):
+    """The halo GAT pair, ranks simulated in-process on the HIP kernels: rank p's table holds
+    every row its edges read (the exchange is a gather by global id), and
+    gala_gat_{fwd,bwd}_stats_ex_f32 over its rows (self_col = the own block of the table,
+    dY_rows = the table's own rows) give Y, q, Ym, sma, aR_out, dX and d_aL BIT-identical
+    to the one-GPU pair -- hub-row chunks included (the whole graph's threshold).  world 1
+    also runs the HaloGat class."""
+    from gala import layout
+    g = layout.gen_graph(kind, 5000, 50000, seed=12)
+    rng = np.random.default_rng(9)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    X = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    wR = cu(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR = cu(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+    dg = ops.DeviceGraph.from_host(g)                    # the whole graph's hub plan
+    Y1, q1, Ym1, sma1, aR1 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR, bR=bR, heads=heads, want_aR=True)
+    dX1, daL1 = ops.gat_bwd_stats(dg, cu(aL), aR1, cu(dY), q1, Y1, Ym1, sma1, heads=heads)
+    for p in range(world):
+        pt = gdist.partition_graph(g, p, world, halo_mode=halo)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        x2g = torch.from_numpy(np.maximum(pt.xs_to_global(), 0)).cuda()
+        Xs, dYs = cu(X)[x2g].contiguous(), cu(dY)[x2g].contiguous()
+        (_, _, x0), = pt.own_blocks()
+        gp = ops.DeviceGraph.from_host(pt.graph, split=pt.split_threshold)
+        sc = torch.arange(x0, x0 + pt.n, dtype=torch.int32, device="cuda")
+        As = torch.full((pt.n_cols, heads), float("nan"), device="cuda")
+        Y, q, Ym, sma = ops.gat_fwd_stats(gp, cu(aL[own]), Xs, wR=wR, bR=bR, heads=heads, self_col=sc, aR_out=As)
+        assert torch.equal(Y, Y1[own]) and torch.equal(Ym, Ym1[own])
+        assert torch.equal(q.view(-1, heads), q1.view(-1, heads)[own])
+        assert torch.equal(sma.view(-1, heads), sma1.view(-1, heads)[own])
+        assert torch.equal(As[x0:x0 + pt.n], aR1.view(-1, heads)[own])
+        Aall = aR1.view(-1, heads)[x2g].contiguous()         # the exchanged logits table
+        dX, daL = ops.gat_bwd_stats(gp, cu(aL[own]), Aall, dYs, q, Y, Ym, sma, heads=heads,
+                                    dY_rows=dYs[x0:x0 + pt.n])
+        assert torch.equal(dX, dX1[own]) and torch.equal(daL.view(-1, heads), daL1.view(-1, heads)[own])
+        if world == 1:
+            from gala.backend import HipBackend
+            hg = gdist.HaloGat(pt, F, heads, HipBackend("cuda"), None)
+            Yc = hg.forward_train(cu(aL), None, cu(X), wR, bR)
+            dXc, daLc = hg.backward(cu(dY), linear=False)
+            assert torch.equal(Yc, Y1) and torch.equal(dXc, dX1) and torch.equal(daLc.reshape(-1), daL1)

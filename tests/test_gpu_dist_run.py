@@ -72,9 +72,9 @@ def test_dist_run_gpu_vertex_cut_matches_one_rank(tmp_path):
 
 
 def test_dist_run_gpu_gat_program(tmp_path):
-    """A GAT program (gat_heads: 4 heads) on the vertex cut through the HIP kernels: one rank
-    against the float64 IR executor, two ranks sharing the GPU over gloo (dense and sparse
-    exchange) against one rank."""
+    """A GAT program (gat_heads: 4 heads) through the HIP kernels: the vertex cut at one rank
+    against the float64 IR executor; two ranks sharing the GPU over gloo (the vertex cut with
+    the dense and the sparse exchange, and the halo layout's HaloGat) against one rank."""
     from gala import dist_run
     ir_path = _ir("gat_heads.txt", tmp_path)
     d1 = _run_gpu(ir_path, tmp_path, 1, "g1", extra=("--layout", "vcut"))
@@ -85,8 +85,9 @@ def test_dist_run_gpu_gat_program(tmp_path):
     params = {k: torch.tensor(np.asarray(v), dtype=torch.float64) for k, v in json.loads(str(d1["weights"])).items()}
     want = ref.run(ir, graphs, X, params)
     np.testing.assert_allclose(d1["prediction"], want.detach().numpy(), rtol=1e-4, atol=1e-4)
-    for ex in ("dense", "sparse"):
-        d2 = _run_gpu(ir_path, tmp_path, 2, f"g2{ex}", extra=("--layout", "vcut", "--exchange", ex))
+    for extra in (("--layout", "vcut", "--exchange", "dense"), ("--layout", "vcut", "--exchange", "sparse"),
+                  ("--layout", "halo")):
+        d2 = _run_gpu(ir_path, tmp_path, 2, "g2" + extra[-1], extra=extra)
         np.testing.assert_allclose(d2["prediction"], d1["prediction"], rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
 
