@@ -206,6 +206,16 @@ def load_traffic(kernel_substr: str):
     return None
 
 
+def with_traffic_rate(roof: dict) -> dict:
+    """north_star's "rocprof achieved HBM GB/s against the chip's peak": the PMC bytes per
+    launch (roof["traffic"]) over this run's kernel time, and its fraction of the peak."""
+    if roof.get("traffic"):
+        rate = roof["traffic"] / (roof["kernel_ms"] / 1e3)
+        roof["traffic_GBps"] = rate / 1e9
+        roof["traffic_frac_of_peak"] = rate / HBM_PEAK
+    return roof
+
+
 class Timer:
     """HIP events on the current stream (device runs) or wall time (host runs)."""
 
@@ -627,6 +637,7 @@ def run_single(args, dev, be, timer, sync):
                      "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json); "
                                      "uniform random columns: each edge's 128-B X row misses L2"},
     }
+    with_traffic_rate(out["roofline"])
     if be.name == "hip":
         t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
         if t_ceil:
@@ -708,6 +719,8 @@ def gat_layer(args, dg, hg, dev, timer, sync):
                            "traffic": load_traffic("k_gat_bwd_fused<64, 4, 8, 8, 1, false, true>"),
                            "kernel": "gala::k_gat_bwd_fused<64,4,8,8,1,false,true> (gala_gat_bwd_stats_f32, 8 heads, "
                                      "F=256)"}
+    with_traffic_rate(out["roofline"])
+    with_traffic_rate(out["bwd_roofline"])
     t_ceil = gather_ceiling(dg.col, X, timer)
     if t_ceil:
         out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
@@ -760,6 +773,7 @@ def rmat_family(args, dev, be, timer, sync):
                         "alg_bytes_per_launch": alg, "traffic": rmat_traffic() if be.name == "hip" else None,
                         "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
                                   "grid, then k_spmm_fixup)"}}
+    with_traffic_rate(out["roofline"])
     if be.name == "hip":
         t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
         if t_ceil:
