@@ -569,6 +569,8 @@ class HaloGat:
 
     def forward_train(self, aL, aR, X, wR=None, bR=None):
         n, H = self.part.n, self.H
+        if self.saved is not None:   # a previous forward's logits exchange may still read As
+            self._wait(self.saved[-1])
         self._wait(self._gather(self.Xs, X))
         if aR is not None:                   # a given source logit: its table too
             self._wait(self._gather(self.As, aR.reshape(n, H)))
