@@ -20,12 +20,20 @@ j in [k*c, (k+1)*c) of V_q (padded), owner-major -- exactly the block layout
 reduce_scatter_tensor expects.  Every chunk is an ordinary CSR (rows in global order,
 columns local to V_p), so the SpMM kernel is the one-GPU kernel.
 
-Numerics: a row's sum is split into per-rank partial sums (each in CSR order) added by
-RCCL, so results agree with the one-GPU aggregation to fp32 rounding, not bit for bit
-(the row-partition `exact` mode in gala/dist.py is the bit-exact one).
+The sparse exchange (exchange="sparse", the DCSR variant): a rank computes partial rows
+only for the destination rows it holds edges of (plus its own rows), sends each owner its
+block with one uneven all_to_all_single per chunk, and the owner sums what it receives
+with an SpMM over a receive CSR (each row's partials in source-rank order).  "auto" picks
+it when the graph's touched fraction is low (banded / skewed graphs); a uniform graph
+touches every (row, rank) pair and keeps the dense reduce-scatter.
 
-Degrees need no collective: the row structure of the owned rows (their rowptr slice) is
-partition metadata, and gala_degree_f32 only reads row offsets.
+Numerics: a row's sum is split into per-rank partial sums (each in CSR order) added by
+RCCL (or by the receive SpMM), so results agree with the one-GPU aggregation to fp32
+rounding, not bit for bit (the row-partition `exact` mode in gala/dist.py is the bit-exact
+one).
+
+Degrees need no collective: the owned rows' full CSR (a slice of the whole graph) is
+partition metadata.
 """
 from __future__ import annotations
 
