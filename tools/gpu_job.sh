@@ -14,6 +14,7 @@
 #                    tools/pmc_traffic.py                   -> gpurun_out/traffic.json
 #   py=SCRIPT,ARGS   python SCRIPT ARGS                      -> gpurun_out/<script>.log
 #   sh=CMD           a preparation command, no GPU (commas as spaces)
+#   env=NAME=VALUE   export a variable for the following steps
 #   profcmd=TAG,CMD  rocprofv3 --kernel-trace --stats of CMD (commas as spaces; the program
 #                    itself right after --)                  -> gpurun_out/prof_TAG/
 #
@@ -74,6 +75,9 @@ for s in "$@"; do
         rest="${a#*,}"
         (cd /tmp && step "prof_$tag" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o run \
             -- ${rest//,/ } > "$OUT/prof_$tag.log" 2>&1) || { tail -20 "$OUT/prof_$tag.log"; exit 1; } ;;
+    env=*)
+        # env=NAME=VALUE: exported for the steps after it
+        export "${s#env=}" ;;
     sh=*)
         # sh=CMD: a host-side preparation command (commas = spaces), e.g. galac
         a="${s#sh=}"
