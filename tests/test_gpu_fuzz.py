@@ -222,3 +222,50 @@ def test_random_case_more_ops(seed):
     gm = np.abs(dY.astype(np.float64)).T @ np.abs(X.astype(np.float64))
     assert np.all(np.abs(_host(dW) - gw) <= (N + 1) * 2.0**-24 * gm + 1e-6)
     np.testing.assert_allclose(_host(db), dY.astype(np.float64).sum(0), atol=(N + 1) * 2.0**-24 * N + 1e-6)
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("GALA_FUZZ_CASES", "96")) // 4))
+def test_random_case_halo_table(seed):
+    """The table-indexed statistics pair (gala_gat_{fwd,bwd}_stats_ex_f32) on a random row
+    partition of a random graph: each rank's rows over its gathered table equal the one-GPU
+    pair's rows bit for bit (Y, q, Ym, sma, the recomputed own logits, dX, d_aL), with the
+    whole graph's hub-row plan (small chunks) or none."""
+    from gala import dist as gdist
+    rng = np.random.default_rng(7000 + seed)
+    g = _graph(rng)
+    if g.n_rows < 2:
+        return
+    heads = int(rng.choice([1, 2, 4, 8]))
+    D = int(rng.choice([4, 8, 16, 32]))
+    F = heads * D
+    world = int(rng.integers(1, 5))
+    halo = str(rng.choice(["p2p", "dense"]))
+    aL = rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32)
+    X = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    dY = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    wR = _dev(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR = _dev(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+    thr = int(rng.choice([0, 64]))
+    dg = ops.DeviceGraph.from_host(g, split=thr if thr else False)
+    try:
+        Y1, q1, Ym1, sma1, aR1 = ops.gat_fwd_stats(dg, _dev(aL), _dev(X), wR=wR, bR=bR, heads=heads, want_aR=True)
+    except _abi.GalaError:      # head widths the statistics kernels refuse (D/VEC not a power of two)
+        return
+    dX1, daL1 = ops.gat_bwd_stats(dg, _dev(aL), aR1, _dev(dY), q1, Y1, Ym1, sma1, heads=heads)
+    for p in range(world):
+        pt = gdist.partition_graph(g, p, world, halo_mode=halo)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        x2g = torch.from_numpy(np.maximum(pt.xs_to_global(), 0)).cuda()
+        Xs, dYs = _dev(X)[x2g].contiguous(), _dev(dY)[x2g].contiguous()
+        (_, _, x0), = pt.own_blocks()
+        gp = ops.DeviceGraph.from_host(pt.graph, split=thr if thr else False)
+        sc = torch.arange(x0, x0 + pt.n, dtype=torch.int32, device="cuda")
+        As = torch.zeros((pt.n_cols, heads), device="cuda")
+        Y, q, Ym, sma = ops.gat_fwd_stats(gp, _dev(aL[own]), Xs, wR=wR, bR=bR, heads=heads, self_col=sc, aR_out=As)
+        assert torch.equal(Y, Y1[own]) and torch.equal(Ym, Ym1[own])
+        assert torch.equal(q.view(-1, heads), q1.view(-1, heads)[own])
+        assert torch.equal(sma.view(-1, heads), sma1.view(-1, heads)[own])
+        assert torch.equal(As[x0:x0 + pt.n], aR1.view(-1, heads)[own])
+        dX, daL = ops.gat_bwd_stats(gp, _dev(aL[own]), aR1.view(-1, heads)[x2g].contiguous(), dYs, q, Y, Ym, sma,
+                                    heads=heads, dY_rows=dYs[x0:x0 + pt.n])
+        assert torch.equal(dX, dX1[own]) and torch.equal(daL.view(-1, heads), daL1.view(-1, heads)[own])
