@@ -264,6 +264,15 @@ class GraphPartition:
                 out.append((j0, j1, k * P * c + p * c))
         return out
 
+    def own_offset(self) -> int:
+        """Table row of own row 0 when the own rows are one block (p2p, or dense with one
+        chunk); defined for a rank without rows too."""
+        if self.halo_mode == "p2p":
+            return self.lo
+        if self.chunks != 1:
+            raise ValueError("own rows are one block only with one chunk")
+        return self.rank * self.block
+
     def gather_slices(self):
         """dense: [(table rows of chunk k, this rank's block in it)] for the all-gathers."""
         c, P, p = self.block, self.world, self.rank
@@ -533,8 +542,7 @@ class HaloGat:
             raise ValueError("HaloGat: one halo chunk (the kernels read the whole table)")
         self.part, self.F, self.H, self.be, self.comm, self.slope = part, F, heads, backend, comm, slope
         self.graph = backend.graph(part.graph, split=part.split_threshold)
-        (j0, j1, x0), = part.own_blocks()
-        self.x0 = x0
+        self.x0 = x0 = part.own_offset()
         dev = getattr(backend, "device", torch.device("cpu"))
         self.self_col = torch.arange(x0, x0 + part.n, dtype=torch.int32, device=dev)
         if comm is None:

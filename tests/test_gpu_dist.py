@@ -473,7 +473,7 @@ def test_halo_gat_bit_identical_to_one_gpu(world, halo, kind, heads, F):
         own = slice(pt.r0, pt.r0 + pt.n)
         x2g = torch.from_numpy(np.maximum(pt.xs_to_global(), 0)).cuda()
         Xs, dYs = cu(X)[x2g].contiguous(), cu(dY)[x2g].contiguous()
-        (_, _, x0), = pt.own_blocks()
+        x0 = pt.own_offset()
         gp = ops.DeviceGraph.from_host(pt.graph, split=pt.split_threshold)
         sc = torch.arange(x0, x0 + pt.n, dtype=torch.int32, device="cuda")
         As = torch.full((pt.n_cols, heads), float("nan"), device="cuda")

@@ -257,7 +257,7 @@ def test_random_case_halo_table(seed):
         own = slice(pt.r0, pt.r0 + pt.n)
         x2g = torch.from_numpy(np.maximum(pt.xs_to_global(), 0)).cuda()
         Xs, dYs = _dev(X)[x2g].contiguous(), _dev(dY)[x2g].contiguous()
-        (_, _, x0), = pt.own_blocks()
+        x0 = pt.own_offset()
         gp = ops.DeviceGraph.from_host(pt.graph, split=thr if thr else False)
         sc = torch.arange(x0, x0 + pt.n, dtype=torch.int32, device="cuda")
         As = torch.zeros((pt.n_cols, heads), device="cuda")
