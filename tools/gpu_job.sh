@@ -5,6 +5,7 @@
 #
 #   tests            python -m pytest tests -m gpu            -> gpurun_out/pytest_gpu.log
 #   tests=EXPR       ... -k EXPR ("_or_" stands for " or ")
+#   smoke            __graft_entry__.smoke()                -> gpurun_out/smoke.log
 #   bench            python bench.py (N = 1 defaults)        -> gpurun_out/bench.json (+ .log)
 #   bench=ARGS       python bench.py ARGS (spaces as commas)
 #   benchdist        GALA_BENCH_DIST=1 bench.py: the strong-scaling path over RCCL at world 1
@@ -47,6 +48,10 @@ for s in "$@"; do
         step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "${k//_or_/ or }" \
             > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
         tail -3 "$OUT/pytest_gpu.log" ;;
+    smoke)
+        step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+            || { tail -30 "$OUT/smoke.log"; exit 1; }
+        tail -1 "$OUT/smoke.log" ;;
     bench)
         step bench 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.log" || { tail -30 "$OUT/bench.log"; exit 1; }
         cat "$OUT/bench.json" ;;
