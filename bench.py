@@ -846,7 +846,8 @@ def main():
     if rank == 0:
         os.write(result_fd, (json.dumps(out) + "\n").encode())
     if distributed:
-        torch.distributed.destroy_process_group()
+        from gala.comm import shutdown
+        shutdown()
 
 
 if __name__ == "__main__":

@@ -105,3 +105,12 @@ class Comm:
 
     def barrier(self) -> None:
         dist.barrier(group=self.group)
+
+
+def shutdown() -> None:
+    """Tear the process group down on every rank together.  A rank that destroys its gloo
+    group while a peer is still busy (rank 0 writing a dump) can die in gloo's teardown
+    ('terminate called without an active exception'), so all ranks meet at a barrier first."""
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()

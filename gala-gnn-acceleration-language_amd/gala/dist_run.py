@@ -461,7 +461,8 @@ def main(argv=None):
                           "loss_first": losses[0], "loss_last": losses[-1]}), flush=True)
         print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)
     if distributed:
-        dist.destroy_process_group()
+        from .comm import shutdown
+        shutdown()
 
 
 if __name__ == "__main__":

@@ -53,6 +53,7 @@ def _worker(rank, world, port, q):
         dist.all_gather(ys2, Y2)
         if rank == 0:
             q.put((torch.cat(ys).numpy(), torch.cat(ys2).numpy(), part.n_cut_edges))
+        dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
 

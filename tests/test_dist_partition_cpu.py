@@ -262,6 +262,7 @@ def _worker(rank, world, port, name, q):
             res[(mode, chunks, exact)] = (gathered, agg.halo_bytes())
         if rank == 0:
             q.put(res)
+        dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
 
@@ -337,6 +338,7 @@ def _gat_worker(rank, world, port, name, chunks, q, exchange="dense"):
         dist.all_gather(ys, pad)
         if rank == 0:
             q.put(torch.cat([y[:s] for y, s in zip(ys, sizes)]).numpy())
+        dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
 
@@ -432,6 +434,7 @@ def _gat_train_worker(rank, world, port, name, chunks, q, rc=False, exchange="de
             out.append(torch.cat([x[:s] for x, s in zip(ts, sizes)]).numpy())
         if rank == 0:
             q.put(out + grads)
+        dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
 
@@ -507,6 +510,7 @@ def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q):
             out.append(torch.cat([x[:s] for x, s in zip(ts, sizes)]).numpy())
         if rank == 0:
             q.put(out + grads)
+        dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
 
