@@ -32,8 +32,11 @@ class HipBackend:
     def graph(self, hg: HostGraph, split="auto"):
         return self.ops.DeviceGraph.from_host(hg, self.device, split=split)
 
-    def spmm(self, g, X, out, dst_scale=None, accum=False):
-        return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)
+    def spmm(self, g, X, out, dst_scale=None, accum=False, samp=None):
+        """samp (nsamp, ra, rb): the kernel-sampled aggregation (GALA_SPMM_SAMPLE)."""
+        if samp is None:
+            return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)
+        return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum, nsamp=samp[0], ra=samp[1], rb=samp[2])
 
     def row_broadcast(self, scale, X, out):
         return self.ops.row_broadcast(scale, X, out=out)
@@ -142,10 +145,11 @@ class CpuBackend:
     def graph(self, hg: HostGraph, split="auto"):
         return CpuGraph(hg)
 
-    def spmm(self, g: CpuGraph, X, out, dst_scale=None, accum=False):
-        flags = _abi.GALA_SPMM_ACCUM if accum else 0
+    def spmm(self, g: CpuGraph, X, out, dst_scale=None, accum=False, samp=None):
+        flags = (_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if samp is not None else 0)
+        ns, ra, rb = samp if samp is not None else (0, 5, 7)
         _abi.call_cpu("gala_spmm_f32", g.csr(), _hp(X), X.stride(0), _hp(out), out.stride(0), X.shape[1],
-                      None, _hp(dst_scale), flags, 0, 5, 7, None)
+                      None, _hp(dst_scale), flags, ns, ra, rb, None)
         return out
 
     def row_broadcast(self, scale, X, out):

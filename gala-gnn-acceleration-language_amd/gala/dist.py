@@ -491,10 +491,15 @@ class DistAggregator:
         """out = norm * A (norm * H) (the GCN aggregation with the graph's own norm)."""
         return self.apply(H, out, self.norm, self.norm)
 
-    def apply(self, H, out, pre=None, post=None, relu=False, act=None):
+    def apply(self, H, out, pre=None, post=None, relu=False, act=None, samp=None):
         """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None), the
         generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) on a partition.  relu:
-        the ReLU prologue, pre * relu(act * H) in the same pass."""
+        the ReLU prologue, pre * relu(act * H) in the same pass.  samp (nsamp, ra, rb): the
+        kernel-sampled aggregation (cuda.h:313-321), exact mode only -- a row's samples are
+        picked by position among all its edges, which the exact layout keeps in CSR order, so
+        it samples the same edges as one GPU."""
+        if samp is not None and not self.exact:
+            raise ValueError("DistAggregator: kernel sampling needs exact mode (one SpMM over the rows' edges)")
         be = self.be
         Xs = self._table(H.shape[1])
         sl = lambda v, a, b: None if v is None else v[a:b]  # noqa: E731
@@ -509,7 +514,7 @@ class DistAggregator:
         if self.exact:
             for works in chunks:
                 self.comm.wait(works)
-            return be.spmm(self.graph, Xs, out, post, False)
+            return be.spmm(self.graph, Xs, out, post, False, samp)
         be.spmm(self.groups[0], Xs, out, post, False)                # overlaps the exchange
         for k, works in enumerate(chunks):
             self.comm.wait(works)

@@ -12,7 +12,14 @@ gala.cu.  This runtime executes the same post-pass IR (galac --ir-json) instead:
     gala/dist.py's DistAggregator in exact mode: the halo rows arrive (RCCL all-gather or
     point-to-point), then ONE SpMM over the own rows, bit-identical to the one-GPU result;
     its backward is the same operator on the gradient (undirected graphs: slot 2g+1 is the
-    forward graph, cuda.h:1253-1257, so pre and post swap places);
+    forward graph, cuda.h:1253-1257, so pre and post swap places) or, for a directed
+    program, the same aggregation over A^T's own partition (the same vertex ranges);
+  * sampled programs: G.sample(k) (inplace_sample_graph_ab, tiling.h:454-508) samples the
+    whole graph identically on every rank before it is partitioned; aggrFn.sample(k)
+    (kernel sampling, cuda.h:313-321) runs the sampled SpMM over each rank's rows, whose
+    CSR edge lists are whole, so every row samples the same edges as on one GPU (row
+    partition only; .dynamic() redraws ra / rb before each forward from one seeded stream
+    that every rank shares);
   * FFN weights are replicated (same seed on every rank); each rank's loss is its own
     training rows' share of the global mean cross entropy, and the weight gradients are
     summed over the ranks (one all-reduce per weight) before the identical Adam steps
@@ -55,13 +62,14 @@ from .comm import Comm
 SHAPES = {
     "Cora": (2708, 5278, 1433, 7, 140.0 / 2708),
     "Pubmed": (19717, 44324, 500, 3, 60.0 / 19717),
+    "CoraFull": (19793, 63421, 8710, 70, 0.70),
     "Arxiv": (169343, 583122, 128, 40, 0.537),
     "Products": (2449029, 61859140, 100, 47, 0.080),
     "Reddit": (232965, 57307946, 602, 41, 0.660),
     "Papers100M": (111059956, 807842936, 128, 172, 0.011),
 }
-SUPPORTED = {"INPUT", "DEGREES", "POWER", "ROW_BROADCAST", "GCN_AGGREGATE", "AGGREGATE_MUL_SUM", "FFN", "RELU",
-             "ADD", "SCALAR_ADD_EPS_MULTIPLY", "GAT_AGGREGATE"}
+SUPPORTED = {"INPUT", "DEGREES", "FULL", "POWER", "ROW_BROADCAST", "GCN_AGGREGATE", "AGGREGATE_MUL_SUM", "FFN", "RELU",
+             "ADD", "SCALAR_ADD_EPS_MULTIPLY", "GAT_AGGREGATE", "AGGREGATE_EDGE_MUL"}
 
 
 def dataset_shape(name: str):
@@ -92,44 +100,60 @@ def _hash_int(rows: np.ndarray, seed: int, mod: int) -> np.ndarray:
     return ((h >> np.uint64(33)) % np.uint64(mod)).astype(np.int64)
 
 
+class _EdgeMul:
+    """AGGREGATE_EDGE_MUL's edge values r[row] * c[col] (the sparse rewrite's
+    norm_i * norm_j, middle-end.h; cuda.h:870-952), kept factored: an AGGREGATE_MUL_SUM over
+    them runs as r * A (c * x), which is what the rewrite started from, so no per-edge array
+    and no halo of c is needed (agrees with the edge-weighted sum to fp32 rounding)."""
+
+    def __init__(self, row, col):
+        self.row, self.col = row, col
+
+    def detach(self):
+        return self
+
+
 class _Agg(torch.autograd.Function):
-    """post * A (pre * x) on the partition; backward pre * A (post * dy) (undirected)."""
+    """post * A (pre * x) on the partition; backward pre * B (post * dy) with B the
+    aggregation of slot 2g+1: A itself for an undirected program (cuda.h:1253-1257), A^T
+    (its own partition) for a directed one.  samp (nsamp, ra, rb): kernel sampling, the
+    same (ra, rb) in the backward (the reference reads the global ra / rb there too)."""
 
     @staticmethod
-    def forward(ctx, x, agg, pre, post):
+    def forward(ctx, x, agg, agg_b, pre, post, samp):
         out = torch.empty_like(x)
-        agg.apply(x.contiguous(), out, pre, post)
-        ctx.agg, ctx.pre, ctx.post = agg, pre, post
+        agg.apply(x.contiguous(), out, pre, post, samp=samp)
+        ctx.agg_b, ctx.pre, ctx.post, ctx.samp = agg_b, pre, post, samp
         return out
 
     @staticmethod
     def backward(ctx, dy):
         dx = torch.empty_like(dy)
-        ctx.agg.apply(dy.contiguous(), dx, ctx.post, ctx.pre)
-        return dx, None, None, None
+        ctx.agg_b.apply(dy.contiguous(), dx, ctx.post, ctx.pre, samp=ctx.samp)
+        return dx, None, None, None, None, None
 
 
 class _AggRelu(torch.autograd.Function):
     """post * A (pre * relu(act * x)) on the partition, the ReLU prologue fused into the
     aggregation's elementwise pass (as the generated programs' gcn_aggregate_relu_apply);
-    backward: relu_scale_backward(pre * A (post * dy)) (undirected)."""
+    backward: relu_scale_backward(pre * B (post * dy)), B as in _Agg."""
 
     @staticmethod
-    def forward(ctx, x, act, agg, pre, post):
+    def forward(ctx, x, act, agg, agg_b, pre, post, samp):
         out = torch.empty_like(x)
-        agg.apply(x.contiguous(), out, pre, post, relu=True, act=act)
+        agg.apply(x.contiguous(), out, pre, post, relu=True, act=act, samp=samp)
         ctx.save_for_backward(x)
-        ctx.agg, ctx.act, ctx.pre, ctx.post = agg, act, pre, post
+        ctx.agg_b, ctx.act, ctx.pre, ctx.post, ctx.samp = agg_b, act, pre, post, samp
         return out
 
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         g = torch.empty_like(dy)
-        ctx.agg.apply(dy.contiguous(), g, ctx.post, ctx.pre)
+        ctx.agg_b.apply(dy.contiguous(), g, ctx.post, ctx.pre, samp=ctx.samp)
         dx = torch.empty_like(x)
-        ctx.agg.be.relu_scale_backward(ctx.act, x.contiguous(), g, dx)
-        return dx, None, None, None, None
+        ctx.agg_b.be.relu_scale_backward(ctx.act, x.contiguous(), g, dx)
+        return dx, None, None, None, None, None, None
 
 
 def _mirror():
@@ -193,41 +217,70 @@ class _VcutGat(torch.autograd.Function):
         return d_aL, d_aL.clone(), dX, None
 
 
+def check_program(ir: dict, layout_mode: str = "halo") -> None:
+    """Raise NotImplementedError when this runtime cannot run the (post-pass) program on the
+    given layout; the message names what is missing."""
+    ops = {nd["op"] for nd in ir["nodes"]}
+    bad = ops - SUPPORTED
+    if bad:
+        raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE / GAT programs)")
+    s = ir["sched"]
+    if "GAT_AGGREGATE" in ops:
+        if s.get("gat_mode", 0) != 0:
+            raise NotImplementedError("gala.dist_run: FIXED-mode GAT (its backward needs A^T)")
+        if not s["undirected"]:
+            # the reference's directed REF backward applies the forward-order alpha to the
+            # transposed pattern's edge positions (common.h:835-894 on slot 2g+1)
+            raise NotImplementedError("gala.dist_run: directed GAT programs")
+        if s["kernel_sample"]:
+            raise NotImplementedError("gala.dist_run: kernel-sampled GAT programs")
+    if s["kernel_sample"] and layout_mode == "vcut":
+        raise NotImplementedError("gala.dist_run: kernel sampling on the vertex cut (a row's samples are "
+                                  "picked among all its edges, which the cut splits by owner); use --layout halo")
+
+
 class Program:
     """One rank's share of a galac program (post-pass IR)."""
 
     def __init__(self, ir: dict, graph: layout.HostGraph, X_own: torch.Tensor, labels_own: torch.Tensor,
                  train_own: torch.Tensor, rank: int, world: int, device, seed: int = 0, group=None,
-                 layout_mode: str = "halo", exchange: str = "auto"):
-        ops = {nd["op"] for nd in ir["nodes"]}
-        bad = ops - SUPPORTED
-        if bad:
-            raise NotImplementedError(f"gala.dist_run: unsupported ops {sorted(bad)} (GCN / GIN / SAGE / GAT programs)")
-        if "GAT_AGGREGATE" in ops:
-            if ir["sched"].get("gat_mode", 0) != 0:
-                raise NotImplementedError("gala.dist_run: FIXED-mode GAT (its backward needs A^T)")
-        if not ir["sched"]["undirected"]:
-            raise NotImplementedError("gala.dist_run: directed programs (the backward needs A^T)")
-        if ir["sched"]["kernel_sample"] or ir["sched"]["data_sample"]:
-            raise NotImplementedError("gala.dist_run: sampled programs")
+                 layout_mode: str = "halo", exchange: str = "auto", train_all=None):
+        """train_all: () -> bool [N] of every vertex's training flag, needed only by a
+        directed program with training subgraphs (its levels are built from the global mask)."""
+        check_program(ir, layout_mode)
+        s = ir["sched"]
+        self.directed = not s["undirected"]
+        self.ksamp, self.dynamic = int(s["kernel_sample"]), bool(s["dynamic_sample"])
         self.ir, self.device = ir, torch.device(device)
         self.be = make_backend(self.device)
         self.comm = Comm(group) if dist.is_initialized() else None
         self.rank, self.world = rank, world
         self.layout = layout_mode
-        if layout_mode == "vcut":
-            from . import vertex_cut as vc
-            self.part = vc.vertex_cut_partition(graph, rank, world, exchange=exchange)
-            self.agg = vc.VertexCutAggregator(self.part, 1, self.be, self.comm)
-            self._gat = {}
-            own_rowptr = self.part.deg_graph.rowptr
-        elif layout_mode == "halo":
-            self.part = gdist.partition_graph(graph, rank, world)
-            self.agg = gdist.DistAggregator(self.part, 1, self.be, self.comm, exact=True)
-            own_rowptr = self.part.graph.rowptr
-            self._gat = {}
-        else:
+        if layout_mode not in ("halo", "vcut"):
             raise ValueError(f"gala.dist_run: layout {layout_mode!r} (halo | vcut)")
+        self._exchange = exchange
+        self.part, self.agg = self._partition(graph, None)
+        own_rowptr = self.part.deg_graph.rowptr if layout_mode == "vcut" else self.part.graph.rowptr
+        self._gat = {}
+        # the aggregation pair (forward, slot 2g+1 backward) of every graph g of the program
+        self.aggs = {0: (self.agg, self._partition(layout.transpose(graph)[0], self.part.bounds)[1]
+                         if self.directed else self.agg)}
+        L = int(ir.get("num_graphs", 1)) - 1
+        if self.directed and L > 0:
+            # training subgraphs (getMaskSubgraphs, tests/common.h:21-110): on an undirected
+            # graph a level keeps every row a training row depends on, so graph 0 gives the
+            # training rows the same values; on a directed one it does not, so each level
+            # gets its own partitions (the same vertex ranges)
+            levels = layout.mask_subgraphs(graph, np.asarray(train_all(), np.int32), L)
+            for c in range(L):
+                sub = levels[L - 1 - c]
+                self.aggs[1 + c] = (self._partition(sub, self.part.bounds)[1],
+                                    self._partition(layout.transpose(sub)[0], self.part.bounds)[1])
+        # kernel sampling: (nsamp, ra, rb), ra / rb redrawn before every forward when dynamic
+        # (rt::next_forward; the same seeded draws on every rank)
+        self.samp = (self.ksamp, 5, 7) if self.ksamp else None
+        self._rng = np.random.default_rng(seed + 17)
+        self.samples = []
         self.deg = torch.from_numpy(np.diff(own_rowptr).astype(np.float32)).to(self.device).view(-1, 1)
         self.X, self.labels, self.train = X_own, labels_own, train_own
         # replicated weights, identical on every rank (same seed, same order as the IR)
@@ -249,6 +302,15 @@ class Program:
         self.n_train = float(n_train.item())
         self.invariants = None
 
+    def _partition(self, g, bounds):
+        """(partition, aggregator) of graph g on this rank in the program's layout."""
+        if self.layout == "vcut":
+            from . import vertex_cut as vc
+            part = vc.vertex_cut_partition(g, self.rank, self.world, bounds=bounds, exchange=self._exchange)
+            return part, vc.VertexCutAggregator(part, 1, self.be, self.comm)
+        part = gdist.partition_graph(g, self.rank, self.world, bounds=bounds)
+        return part, gdist.DistAggregator(part, 1, self.be, self.comm, exact=True)
+
     def _param(self, name):
         m = self.modules[name]
         return m[0] if isinstance(m, torch.nn.ParameterList) else m
@@ -267,6 +329,11 @@ class Program:
         return self._gat[key]
 
     def forward(self):
+        if self.samp is not None and self.dynamic:
+            ra, rb = (int(v) for v in self._rng.integers(0, 101, 2))
+            self.samp = (self.ksamp, ra, rb)
+        if self.samp is not None:
+            self.samples.append(self.samp[1:])
         vals = {}
         hoisted = self.invariants is None
         for nd in self.ir["nodes"]:
@@ -279,23 +346,35 @@ class Program:
                 y = self.X
             elif op == "DEGREES":
                 y = self.deg
+            elif op == "FULL":    # FULL_OP: the sampled degree, nsamples per row (one segment)
+                y = torch.full((self.deg.shape[0], 1), float(nd["param"]), device=self.device)
             elif op == "POWER":
                 y = torch.pow(a[0], nd["param"])
             elif op == "ROW_BROADCAST":
                 y = a[0] * a[1]
             elif op == "GCN_AGGREGATE":
                 x = a[0]
+                fw, bw = self.aggs.get(nd["graph"], self.aggs[0])
                 if nd["param"] == 1:  # ReLU prologue: relu(act * x), fused into the aggregation
                     act = a[3] if len(a) > 3 else None
                     if act is not None and act.requires_grad:
                         x = torch.relu(act * x)
-                        y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
+                        y = _Agg.apply(x, fw, bw, self._vec(a[1]), self._vec(a[2]), self.samp)
                     else:
-                        y = _AggRelu.apply(x, self._vec(act), self.agg, self._vec(a[1]), self._vec(a[2]))
+                        y = _AggRelu.apply(x, self._vec(act), fw, bw, self._vec(a[1]), self._vec(a[2]), self.samp)
                 else:
-                    y = _Agg.apply(x, self.agg, self._vec(a[1]), self._vec(a[2]))
+                    y = _Agg.apply(x, fw, bw, self._vec(a[1]), self._vec(a[2]), self.samp)
             elif op == "AGGREGATE_MUL_SUM":
-                y = _Agg.apply(a[0], self.agg, None, None)
+                w = a[1] if len(a) > 1 else None
+                if w is not None and not isinstance(w, _EdgeMul):
+                    raise NotImplementedError("gala.dist_run: AGGREGATE_MUL_SUM over computed edge values")
+                fw, bw = self.aggs.get(nd["graph"], self.aggs[0])
+                pre, post = (w.col, w.row) if w is not None else (None, None)
+                y = _Agg.apply(a[0], fw, bw, pre, post, self.samp)
+            elif op == "AGGREGATE_EDGE_MUL":
+                if a[0].requires_grad or a[1].requires_grad:
+                    raise NotImplementedError("gala.dist_run: AGGREGATE_EDGE_MUL of trained values")
+                y = _EdgeMul(self._vec(a[0]), self._vec(a[1]))
             elif op == "GAT_AGGREGATE":
                 aL, x = a[0], a[2]
                 n = x.shape[0]
@@ -347,7 +426,9 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=None)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
-    ap.add_argument("--dump", help="rank 0 writes an npz: predictions (all rows), losses, rowptr/col")
+    ap.add_argument("--dump", help="rank 0 writes an npz: the first forward's predictions (all rows), the losses, "
+                                   "the first epoch's weight gradients (grad:<name>), rowptr/col, the initial "
+                                   "weights, the kernel-sampling (ra, rb) of every forward")
     ap.add_argument("--dump-stride", type=int, default=1,
                     help="dump the predictions of every k-th row only (rows in 'rows'; large graphs)")
     ap.add_argument("--layout", default="halo", choices=["halo", "vcut"],
@@ -394,6 +475,9 @@ def main(argv=None):
         n, m = max(int(n0 * args.scale), 2), max(int(m0 * args.scale), 1)
         g = layout.gen_graph("uniform", n, m, seed=args.seed)
         X_all = lab_all = tr_all = None
+    g_in = g                     # the dump's graph: the program's input, before data sampling
+    if int(s["data_sample"]) > 0:   # G.sample(k): inplace_sample_graph_ab(5, 7) on every rank alike
+        g = layout.sample_ab(g, int(s["data_sample"]), 5, 7)
     F, C = int(s["feat_size"]), int(s["label_size"])
     bounds = gdist.row_bounds(g.rowptr, world)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
@@ -406,9 +490,16 @@ def main(argv=None):
         X = np.ascontiguousarray(X_all[r0:r1], np.float32)
         labels = lab_all[r0:r1].astype(np.int64)
         train = tr_all[r0:r1] > 0
+    if tr_all is None:
+        def train_all():
+            every = np.arange(g.n_rows)
+            return (_hash_int(every, args.seed + 2, 1 << 20) < int(frac * (1 << 20))) | (every == 0)
+    else:
+        def train_all():
+            return tr_all > 0
     prog = Program(ir, g, torch.from_numpy(X).to(dev), torch.from_numpy(labels).to(dev),
                    torch.from_numpy(train).to(dev), rank, world, dev, seed=args.seed, layout_mode=args.layout,
-                   exchange=args.exchange)
+                   exchange=args.exchange, train_all=train_all)
     init_weights = {k: v.detach().cpu().numpy().tolist() for k, v in prog.modules.state_dict().items()}
     opt = torch.optim.Adam(prog.modules.parameters(), lr=0.01, weight_decay=5e-4)
     iters = args.iters if args.iters is not None else max(int(s.get("iterations", 0)), 1)
@@ -424,6 +515,9 @@ def main(argv=None):
         loss = prog.loss(pred)
         loss.backward()
         prog.reduce_grads()
+        if epoch == 0:   # the first epoch's summed weight gradients (the dump's grad:<name>)
+            first_grads = {k: v.grad.detach().cpu().numpy() for k, v in prog.modules.named_parameters()
+                           if v.grad is not None}
         opt.step()
         sync()
         t2 = time.perf_counter()
@@ -451,7 +545,9 @@ def main(argv=None):
         if rank == 0:
             rows_d = np.arange(0, g.n_rows, max(args.dump_stride, 1))
             np.savez(args.dump, prediction=pr.numpy()[rows_d], rows=rows_d, losses=np.array(losses),
-                     rowptr=g.rowptr, col=g.col, weights=np.array(json.dumps(init_weights)))
+                     rowptr=g_in.rowptr, col=g_in.col, weights=np.array(json.dumps(init_weights)),
+                     samples=np.array(prog.samples, np.int64).reshape(-1, 2),
+                     **{"grad:" + k: v for k, v in first_grads.items()})
     if rank == 0:
         print(json.dumps({"ranks": world, "backend": dist.get_backend() if distributed else None,
                           "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,

@@ -352,10 +352,14 @@ class VertexCutAggregator(_PartialRows):
         _, partial, S = self._buffers(F or self.F)
         self.wait([self.post(partial, S, k) for k in range(len(self.graphs))])
 
-    def apply(self, H, out, pre=None, post=None, relu=False, act=None):
+    def apply(self, H, out, pre=None, post=None, relu=False, act=None, samp=None):
         """out = post * A (pre * H) over the own rows (pre / post: [n] vectors or None): the
         generated programs' GCN_AGGREGATE (codegen/gala.cu:442-456) with column ownership.
-        relu: the ReLU prologue, out = post * A (pre * relu(act * H)) (one elementwise pass)."""
+        relu: the ReLU prologue, out = post * A (pre * relu(act * H)) (one elementwise pass).
+        Kernel sampling is refused: a row's samples are picked by position among ALL its
+        edges (cuda.h:313-321), which the cut splits by owner."""
+        if samp is not None:
+            raise NotImplementedError("VertexCutAggregator: kernel sampling (use the row partition)")
         be = self.be
         Xs, partial, S = self._buffers(H.shape[1])
         if relu:

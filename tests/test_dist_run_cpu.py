@@ -19,6 +19,7 @@ import pytest
 import torch
 
 import _ir_ref as ref
+from _dist_check import check_dist_dump as _check_ir
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -61,20 +62,91 @@ def _run(ir, tmp_path, world, tag, iters=6, extra=()):
     return dict(np.load(dump)), summary
 
 
-@pytest.mark.parametrize("prog", ["gcn3.txt", "gin.txt"])
-def test_dist_run_one_rank_matches_ir_semantics(prog, tmp_path):
+@pytest.mark.parametrize("prog,lay", [("gcn3.txt", "halo"), ("gin.txt", "halo"), ("gcn3.txt", "vcut"),
+                                      ("gcn_ksample.txt", "halo"), ("gcn_ksample_dyn.txt", "halo"),
+                                      ("gcn_gsample.txt", "halo"), ("gcn_gsample.txt", "vcut"),
+                                      ("gcn_sparse.txt", "halo"), ("gcn_sparse.txt", "vcut"),
+                                      ("gat_heads.txt", "halo"), ("gat.txt", "vcut")])
+def test_dist_run_one_rank_matches_ir_semantics(prog, lay, tmp_path):
+    """World 1 against the float64 IR executor: forward, loss and weight gradients.
+    gcn_sparse: the sparse rewrite (AGGREGATE_EDGE_MUL of the norms, then the edge-weighted
+    aggregation), run factored.  The sampled programs: G.sample(4) (the whole graph sampled before partitioning) and
+    aggrFn.sample(5) (kernel sampling over each row's whole edge list; .dynamic() with the
+    (ra, rb) the run drew)."""
     ir_path = _ir(prog, tmp_path)
-    d, _ = _run(ir_path, tmp_path, 1, "w1", iters=1)
+    d, s = _run(ir_path, tmp_path, 1, "w1", iters=1, extra=("--layout", lay))
+    assert s["layout"] == lay
+    if "dyn" in prog:
+        assert d["samples"].shape == (1, 2)
+    _check_ir(ir_path, d)
+
+
+def _directed_dataset(path, ir_path, n=400, m=2400, seed=5):
+    """A small DIRECTED graph in the reference's npy format (gala_export_npy.py:100-171):
+    random arcs plus self loops, so A^T differs from A."""
     ir = ref.load_ir(str(ir_path))["post"]
-    graphs = ref.Graphs(ir, d["rowptr"], d["col"], np.ones(len(d["rowptr"]) - 1, np.int32))
-    from gala import dist_run
-    rows = np.arange(len(d["rowptr"]) - 1)
     s = ir["sched"]
-    X = torch.as_tensor(dist_run._hash_uniform(rows, s["feat_size"], 3), dtype=torch.float64)
-    W = {k: torch.tensor(np.asarray(v), dtype=torch.float64) for k, v in json.loads(str(d["weights"])).items()}
-    params = {k.replace(".0", ""): v for k, v in W.items()}   # eps ParameterList -> eps<k>
-    want = ref.run(ir, graphs, X, params)
-    np.testing.assert_allclose(d["prediction"], want.detach().numpy(), rtol=1e-4, atol=1e-4)
+    rng = np.random.default_rng(seed)
+    src = np.concatenate([rng.integers(0, n, m), np.arange(n)]).astype(np.uint32)
+    dst = np.concatenate([(src[:m] + rng.integers(1, 40, m)) % n, np.arange(n)]).astype(np.uint32)
+    path.mkdir()
+    np.save(path / "Adj_src.npy", np.concatenate([[n, n], src]).astype(np.uint32))
+    np.save(path / "Adj_dst.npy", dst)
+    X = rng.uniform(-1, 1, (n, s["feat_size"])).astype(np.float32)
+    lab = rng.integers(0, s["label_size"], n).astype(np.int64)
+    train = rng.random(n) < 0.3
+    np.save(path / "Feat.npy", X)
+    np.save(path / "Lab.npy", lab.reshape(-1, 1))
+    np.save(path / "TnMsk.npy", train.astype(np.int32).reshape(-1, 1))
+    return X, lab, train
+
+
+@pytest.mark.parametrize("lay", ["halo", "vcut"])
+def test_dist_run_directed_matches_ir_semantics(lay, tmp_path):
+    """A directed program (set_undirected(false)) on a directed graph: the backward
+    aggregates over A^T (slot 2g+1, its own partition of the same vertex ranges); world 1
+    against the IR executor, gradients included."""
+    ir_path = _ir("gcn_directed.txt", tmp_path)
+    inputs = _directed_dataset(tmp_path / "Data", ir_path)
+    d, s = _run(ir_path, tmp_path, 1, "w1", iters=1, extra=("--layout", lay, "--data", str(tmp_path / "Data")))
+    r = d["rowptr"]
+    assert not np.array_equal(np.diff(r), np.bincount(d["col"], minlength=len(r) - 1))   # really directed
+    _check_ir(ir_path, d, inputs)
+
+
+@pytest.mark.parametrize("prog,world,extra", [
+    ("gcn_ksample_dyn.txt", 3, ()),
+    ("gcn_ksample.txt", 2, ()),
+    ("gcn_gsample.txt", 2, ("--layout", "vcut", "--exchange", "sparse")),
+    ("gcn_sparse.txt", 3, ()),
+    ("gcn_directed.txt", 3, ("--data", "DATA")),
+    ("gcn_directed.txt", 2, ("--data", "DATA", "--layout", "vcut")),
+])
+def test_dist_run_sampled_directed_ranks_match_one_rank(prog, world, extra, tmp_path):
+    """Sampled and directed programs over N ranks against one rank: the row partition's
+    first forward bit-identical (exact-mode SpMMs; kernel sampling picks the same edges of
+    every row; dynamic sampling draws the same (ra, rb) on every rank), the vertex cut
+    within fp32 rounding, and the loss curves within the rounding of the cross-rank sums."""
+    ir_path = _ir(prog, tmp_path)
+    if "DATA" in extra:
+        _directed_dataset(tmp_path / "Data", ir_path)
+        extra = tuple(str(tmp_path / "Data") if e == "DATA" else e for e in extra)
+    one = tuple(e for e in extra if e not in ("--exchange", "sparse"))
+    d1, _ = _run(ir_path, tmp_path, 1, "w1", extra=one)
+    dn, sn = _run(ir_path, tmp_path, world, f"w{world}", extra=extra)
+    np.testing.assert_array_equal(dn["samples"], d1["samples"])
+    if "vcut" in extra:
+        np.testing.assert_allclose(dn["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
+    else:
+        np.testing.assert_array_equal(dn["prediction"], d1["prediction"])
+    np.testing.assert_allclose(dn["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+    assert sn["loss_last"] < sn["loss_first"]
+
+
+def test_dist_run_refuses_kernel_sampling_on_the_vertex_cut(tmp_path):
+    ir_path = _ir("gcn_ksample.txt", tmp_path)
+    with pytest.raises(AssertionError, match="kernel sampling on the vertex cut"):
+        _run(ir_path, tmp_path, 1, "w1", iters=1, extra=("--layout", "vcut"))
 
 
 @pytest.mark.parametrize("world", [2, 3])

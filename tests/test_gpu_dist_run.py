@@ -148,3 +148,38 @@ def test_dist_run_config5_shape_at_size(tmp_path):
     got_at = {int(r): i for i, r in enumerate(dh["rows"])}
     for s in seeds:
         np.testing.assert_allclose(dh["prediction"][got_at[int(s)]], want[at[int(s)]], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("prog,lay", [("gcn_ksample_dyn.txt", "halo"), ("gcn_ksample.txt", "halo"),
+                                      ("gcn_gsample.txt", "vcut"), ("gcn_sparse.txt", "halo"),
+                                      ("gcn3.txt", "vcut"), ("gat_heads.txt", "halo")])
+def test_dist_run_gpu_programs_match_ir_with_gradients(prog, lay, tmp_path):
+    """The HIP kernels under the multi-rank runtime at one rank: sampled (kernel, dynamic,
+    graph), sparse-rewrite, GCN-3 on the vertex cut and the 4-head GAT on the row partition,
+    against the float64 IR executor -- forward, loss and the first epoch's weight gradients."""
+    from _dist_check import check_dist_dump
+    ir_path = _ir(prog, tmp_path)
+    d = _run_gpu(ir_path, tmp_path, 1, "g1", iters=1, extra=("--layout", lay))
+    check_dist_dump(ir_path, d)
+
+
+@pytest.mark.parametrize("lay", ["halo", "vcut"])
+def test_dist_run_gpu_directed_program(lay, tmp_path):
+    """A directed program on a directed npy graph: the backward over A^T's partition."""
+    from _dist_check import check_dist_dump
+    from test_dist_run_cpu import _directed_dataset
+    ir_path = _ir("gcn_directed.txt", tmp_path)
+    inputs = _directed_dataset(tmp_path / "Data", ir_path)
+    d = _run_gpu(ir_path, tmp_path, 1, "g1", iters=1, extra=("--layout", lay, "--data", str(tmp_path / "Data")))
+    check_dist_dump(ir_path, d, inputs)
+
+
+def test_dist_run_gpu_dynamic_sampling_two_ranks_bit_identical(tmp_path):
+    """Dynamic kernel sampling over two ranks sharing the GPU: the same (ra, rb) draws and
+    the first forward bit-identical to one rank."""
+    ir_path = _ir("gcn_ksample_dyn.txt", tmp_path)
+    d1 = _run_gpu(ir_path, tmp_path, 1, "g1")
+    d2 = _run_gpu(ir_path, tmp_path, 2, "g2")
+    np.testing.assert_array_equal(d2["samples"], d1["samples"])
+    np.testing.assert_array_equal(d2["prediction"], d1["prediction"])
+    np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
