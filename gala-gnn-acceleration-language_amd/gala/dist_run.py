@@ -558,7 +558,9 @@ def main(argv=None):
         print(f"{np.mean(fwd_t[keep]):.6g},{np.mean(ep_t[keep]):.6g}", flush=True)
     if distributed:
         from .comm import shutdown
+        print(f"[gala.dist_run rank {rank}] epochs done", file=sys.stderr, flush=True)
         shutdown()
+        print(f"[gala.dist_run rank {rank}] process group closed", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
