@@ -443,6 +443,9 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
                     "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
                     "halo_bytes_per_aggregation_per_rank": best.agg.halo_bytes(),
                     "exchange_ms_per_aggregation": t_ex * 1e3,
+                    # the link rate the exchange achieved: this rank's exchanged bytes over the
+                    # time of one aggregation's collectives alone (xGMI under RCCL)
+                    "exchange_GBps_per_rank": (best.agg.halo_bytes() / t_ex / 1e9) if t_ex > 0 else None,
                     "spmm_ms_per_aggregation": t_kernel * 1e3,
                     "halo_layout": pt1.halo_mode, "halo_rows_rank0": pt1.n_halo_rows,
                     "vcut_touched_fraction": frac,
