@@ -38,11 +38,14 @@ def run_prog(name, tmp_path, *extra, timeout=300):
 
 
 def check_against_ir(name, d):
-    ir = ref.load_ir(os.path.join(PKG, "progs", name, "ir.json"))["post"]
-    if ir["sched"]["dynamic_sample"]:
-        assert np.isfinite(d["loss"]).all()
-        return
-    graphs = ref.Graphs(ir, d["rowptr"], d["col"], d["train_mask"].astype(np.int32))
+    check_against_ir_file(os.path.join(PKG, "progs", name, "ir.json"), d)
+
+
+def check_against_ir_file(ir_path, d):
+    ir = ref.load_ir(ir_path)["post"]
+    # kernel sampling: the (ra, rb) the run used (dynamic sampling draws them per forward)
+    ra, rb = (int(v) for v in d["sample_ab"]) if "sample_ab" in d else (5, 7)
+    graphs = ref.Graphs(ir, d["rowptr"], d["col"], d["train_mask"].astype(np.int32), ra=ra, rb=rb)
     X = torch.as_tensor(d["t_iden"], dtype=torch.float64)
     params = {k[6:]: torch.tensor(v, dtype=torch.float64, requires_grad=True)
               for k, v in d.items() if k.startswith("param:")}

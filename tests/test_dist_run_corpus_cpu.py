@@ -1,7 +1,7 @@
 """CPU: the reference's DSL corpus (tests/GALA-DSL, 114 programs: GCN / GAT / GIN / SAGE on
 six datasets plus the sampling, scalability, memory and speed-up ablations) runs unchanged
-through galac and the multi-rank runtime gala.dist_run, and each program computes what its
-IR means.
+through galac -- as the generated single-device program and under the multi-rank runtime
+gala.dist_run -- and each program computes what its IR means.
 
 Only in this container: the corpus is read from /root/reference (it never travels to the
 GPU box, and no copy of it is kept here), so the tests skip without it.
@@ -13,7 +13,10 @@ GPU box, and no copy of it is kept here), so the tests skip without it.
   with the fewest weights -- runs one epoch on the host-CPU backend at world 1 on a
   synthetic graph of its dataset's shape scaled to about 1200 vertices, and its first
   forward, loss and weight gradients must equal the float64 executor of its IR
-  (tests/_dist_check.py).
+  (tests/_dist_check.py);
+* the same representatives as generated programs (galac -> gala.cpp -> g++ over
+  libgala_torch.so, built in a scratch directory by tools/corpus_progs.py) run one epoch on
+  the host-CPU backend, their --dump checked the same way (tests/_dsl_check.py).
 """
 import glob
 import json
@@ -94,3 +97,17 @@ def test_every_corpus_class_matches_its_ir_semantics(corpus, tmp_path, monkeypat
             raise AssertionError(f"{name} ({lay}): {e}") from None
         checked.append(name)
     assert len(checked) == len(corpus) >= 25
+
+
+def test_every_corpus_class_runs_as_a_generated_program(tmp_path):
+    """tools/corpus_progs.py: one generated program per structural class, built and run on
+    the host backend, forward / loss / weight gradients against the IR executor."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    import corpus_progs
+    out = tmp_path / "corpus.jsonl"
+    assert corpus_progs.main(["-j", "8", "--out", str(out)]) == 0
+    rows = [json.loads(line) for line in out.read_text().splitlines()]
+    assert len(rows) >= 25 and all(r["status"] == "ok" for r in rows)
+    assert sum(r["members"] for r in rows) == len(CORPUS)
+
