@@ -183,3 +183,22 @@ def test_dist_run_gpu_dynamic_sampling_two_ranks_bit_identical(tmp_path):
     np.testing.assert_array_equal(d2["samples"], d1["samples"])
     np.testing.assert_array_equal(d2["prediction"], d1["prediction"])
     np.testing.assert_allclose(d2["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("prog,lay", [("gcn_directed.txt", "halo"), ("gcn_directed.txt", "vcut"),
+                                      ("gcn_ksample_dyn.txt", "halo"), ("gcn_sparse.txt", "vcut")])
+def test_dist_run_gpu_rccl_world_one_matches_no_collectives(prog, lay, tmp_path):
+    """RCCL at world 1 (--dist: every collective of the layout runs, the transposed
+    partitions' included): a one-rank collective moves rows unchanged, so the run is
+    bit-identical to the same run without collectives."""
+    extra = ("--layout", lay)
+    if prog == "gcn_directed.txt":
+        from test_dist_run_cpu import _directed_dataset
+        _directed_dataset(tmp_path / "Data", _ir(prog, tmp_path))
+        extra += ("--data", str(tmp_path / "Data"))
+    ir_path = _ir(prog, tmp_path)
+    d0 = _run_gpu(ir_path, tmp_path, 1, "plain", iters=3, extra=extra)
+    d1 = _run_gpu(ir_path, tmp_path, 1, "rccl", iters=3, extra=extra + ("--dist",), backend="nccl")
+    np.testing.assert_array_equal(d1["prediction"], d0["prediction"])
+    np.testing.assert_array_equal(d1["samples"], d0["samples"])
+    np.testing.assert_allclose(d1["losses"], d0["losses"], rtol=1e-6, atol=0)
