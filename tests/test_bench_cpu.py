@@ -22,14 +22,26 @@ def _env():
     return env
 
 
+def _run_ranks(args, env, timeout=600):
+    """bench.py with self-launched gloo ranks.  About one gloo launch in a hundred here dies
+    inside gloo's own threads (SIGABRT, "terminate called without an active exception");
+    such a launch is repeated once, any other failure is reported as it is."""
+    for attempt in range(2):
+        r = subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=env,
+                           cwd=ROOT)
+        if r.returncode == 0 or attempt or "terminate called without an active exception" not in r.stderr:
+            return r
+        print("gloo launch aborted in gloo's threads; repeated once:\n" + r.stderr[-1500:], file=sys.stderr)
+    return r
+
+
 def _json_lines(out: str):
     return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
 
 
 def test_bench_self_launches_ranks():
-    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--scale", "0.002",
-                        "--steps", "2", "--warmup", "1", "--calib-steps", "1"],
-                       capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    r = _run_ranks(["--gpus", "2", "--device", "cpu", "--scale", "0.002", "--steps", "2", "--warmup", "1",
+                    "--calib-steps", "1"], _env())
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout                 # rank 0 only
@@ -43,6 +55,7 @@ def test_bench_self_launches_ranks():
     assert c["mode"] in c["candidates_ms_per_step"]
     assert set(c["candidates_ms_per_step"]) >= {"halo-exact", "halo-overlap", "vcut", "vcut-pipe"}
     assert c["halo_bytes_per_aggregation_per_rank"] > 0 and c["exchange_ms_per_aggregation"] > 0
+    assert c["exchange_GBps_per_rank"] > 0
     assert d["config"]["edges"] > 0 and "weak" in d and d["weak"]["value"] > 0
     assert d["roofline"]["alg_bytes_per_launch"] > 0
     # the skewed family strong-scaled too, with its own candidates and chosen layout
@@ -102,9 +115,8 @@ def test_bench_real_data(tmp_path):
     npy loader) and the line names it; one rank and two self-launched ranks."""
     n, e = _write_npy_dataset(str(tmp_path))
     for extra in ((), ("--gpus", "2", "--calib-steps", "1", "--no-weak", "--no-gat")):
-        r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--data", str(tmp_path), "--steps", "2",
-                            "--warmup", "1", "--no-cpu-baseline", "--no-rmat", *extra],
-                           capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+        r = _run_ranks(["--device", "cpu", "--data", str(tmp_path), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-rmat", *extra], _env())
         assert r.returncode == 0, r.stderr[-3000:]
         (d,) = _json_lines(r.stdout)
         assert d["config"]["n_vertices"] == n and d["config"]["edges"] == e
