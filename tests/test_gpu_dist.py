@@ -13,6 +13,15 @@ from gala import ops
 pytestmark = pytest.mark.gpu
 
 
+def _assert_matches_oracle(g, X, norm, got_rows, r0):
+    """The vertex cut's owner rows against the ORACLE's GCN aggregation of the whole graph
+    (norm * A (norm * X), orc_gspmm order) at north_star's tolerance: |err| <= 1e-4 abs +
+    1e-4 rel -- an anchor that does not go through the one-GPU HIP result."""
+    want = orc.spmm(orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col), X.cpu().numpy(),
+                    src_scale=norm.cpu().numpy(), dst_scale=norm.cpu().numpy())[r0:r0 + got_rows.shape[0]]
+    np.testing.assert_allclose(got_rows.cpu().numpy(), want, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_simulated_ranks_match_global_oracle(world):
     n, E, F = 3000, 40000, 32
@@ -151,6 +160,7 @@ def test_vertex_cut_matches_one_gpu(world, chunks, kind):
         S = torch.cat([total[k * world * c + q * c:k * world * c + (q + 1) * c] for k in range(chunks)])[:pt.n]
         got = ops.row_broadcast(norms[q], S)
         torch.testing.assert_close(got, ref[pt.r0:pt.r0 + pt.n], rtol=1e-5, atol=1e-6)
+        _assert_matches_oracle(g, X, norm, got, pt.r0)
 
 
 def test_aggregator_classes_on_one_rank():
@@ -405,6 +415,7 @@ def test_vertex_cut_sparse_exchange_matches_one_gpu(world, chunks, kind):
         got = ops.spmm(ops.DeviceGraph.from_host(pt.sparse.recv_graph, split=False), recv,
                        dst_scale=norm[pt.r0:pt.r0 + pt.n])
         torch.testing.assert_close(got, ref[pt.r0:pt.r0 + pt.n], rtol=1e-5, atol=1e-6)
+        _assert_matches_oracle(g, X, norm, got, pt.r0)
 
 
 @pytest.mark.parametrize("heads,F", [(1, 32), (8, 256)])
