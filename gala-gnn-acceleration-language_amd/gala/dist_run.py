@@ -230,8 +230,9 @@ def check_program(ir: dict, layout_mode: str = "halo") -> None:
             raise NotImplementedError("gala.dist_run: FIXED-mode GAT (its backward needs A^T)")
         if not s["undirected"]:
             # the reference's directed REF backward applies the forward-order alpha to the
-            # transposed pattern's edge positions (common.h:835-894 on slot 2g+1)
-            raise NotImplementedError("gala.dist_run: directed GAT programs")
+            # transposed pattern's edge positions (common.h:835-894 on slot 2g+1): every rank
+            # would need the whole alpha; the generated single-device program runs them
+            raise NotImplementedError("gala.dist_run: directed GAT programs (run the generated program)")
         if s["kernel_sample"]:
             raise NotImplementedError("gala.dist_run: kernel-sampled GAT programs")
     if s["kernel_sample"] and layout_mode == "vcut":

@@ -115,15 +115,20 @@ class Graphs:
         rp, col = self.edges(gi)
         return _csr(rp, col, self.n, val)
 
-    def backward_matrix(self, gi):
+    def backward_edges(self, gi):
+        """The pattern of slot 2g+1: graph g itself for graph 0 of an undirected program,
+        its transpose (buildTranspose) otherwise."""
         if gi == 0 and self.undirected:
-            return self.matrix(gi)
+            return self.edges(gi)
         g = self.host[gi]
         t, _ = layout.transpose(layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, g.col))
         if self.ks > 0:
-            rp, col = sampled_graph(t.rowptr, t.col, self.ks, self.ra, self.rb)
-            return _csr(rp, col, self.n)
-        return _csr(t.rowptr, t.col, self.n)
+            return sampled_graph(t.rowptr, t.col, self.ks, self.ra, self.rb)
+        return t.rowptr, t.col
+
+    def backward_matrix(self, gi):
+        rp, col = self.backward_edges(gi)
+        return _csr(rp, col, self.n)
 
 
 class _SlotSpmm(torch.autograd.Function):
@@ -140,25 +145,30 @@ class _SlotSpmm(torch.autograd.Function):
 
 
 class _GatRef(torch.autograd.Function):
-    """GAT aggregation with the reference's backward chain (`ref` mode):
-    dX = A_alpha dY on slot 2g+1's pattern, d alpha_e = <dY_row, X_col>,
-    ds = alpha*dalpha - alpha*(1e-12 + sum_row alpha*dalpha), dz = LeakyReLU'(z) ds,
-    daL = daR = 1e-12 + sum_row dz."""
+    """GAT aggregation with the reference's backward chain (SURVEY.md §8a, `ref` mode;
+    common.h:835-894): every backward step runs on slot 2g+1's pattern (rp_b, col_b) with
+    the forward's alpha taken by edge POSITION -- dX = A_b(alpha) dY, d alpha_e =
+    <dY_row, X_col> (edge_sddmm), ds = alpha*dalpha - alpha*(1e-12 + sum_row alpha*dalpha),
+    dz = LeakyReLU'(z) ds with z at the same position of the forward pattern,
+    daL = daR = 1e-12 + sum_row dz.  On an undirected graph slot 2g+1 is the forward graph;
+    on a directed one it is the transpose and the positions pair unrelated edges, as the
+    reference does."""
 
     @staticmethod
-    def forward(ctx, aL, aR, x, rp, col, n, slope):
+    def forward(ctx, aL, aR, x, rp, col, n, slope, rp_b=None, col_b=None):
         rows = _rows(rp)
         colt = torch.as_tensor(col, dtype=torch.long)
         z = aL.view(-1)[rows] + aR.view(-1)[colt]
         alpha = _softmax(rp, _lrelu(z, slope))
         ctx.save_for_backward(x, alpha, z)
-        ctx.rp, ctx.col, ctx.n, ctx.slope = rp, colt, n, slope
+        rp_b, col_b = (rp, col) if rp_b is None else (rp_b, col_b)
+        ctx.rp_b, ctx.col_b, ctx.n, ctx.slope = rp_b, torch.as_tensor(col_b, dtype=torch.long), n, slope
         return _csr(rp, col, n, alpha) @ x
 
     @staticmethod
     def backward(ctx, dy):
         x, alpha, z = ctx.saved_tensors
-        rp, col, n = ctx.rp, ctx.col, ctx.n
+        rp, col, n = ctx.rp_b, ctx.col_b, ctx.n
         rows = _rows(rp)
         dx = _csr(rp, col.numpy(), n, alpha) @ dy
         dalpha = (dy[rows] * x[col]).sum(1)
@@ -167,7 +177,7 @@ class _GatRef(torch.autograd.Function):
         ds = sds - alpha * acc[rows]
         dz = torch.where(z > 0, ds, ds * ctx.slope)
         da = (torch.zeros(n, dtype=dy.dtype).index_add(0, rows, dz) + 1e-12).view(-1, 1)
-        return da, da.clone(), dx, None, None, None, None
+        return da, da.clone(), dx, None, None, None, None, None, None
 
 
 def run(ir, graphs: Graphs, X, params, segments=1):
@@ -205,6 +215,7 @@ def run(ir, graphs: Graphs, X, params, segments=1):
                 y = a[2] * y
         elif op == "GAT_AGGREGATE":
             rp, col = graphs.edges(gi)
+            rp_b, col_b = graphs.backward_edges(gi)
             H = a[0].numel() // graphs.n                  # heads (galac gat_heads)
             if nd["weight"]:  # gat_aggregate_ffn: attnR = Linear(X) of the aggregated rows
                 a[1] = _ffn(a[2], params, nd["weight"], H)
@@ -215,7 +226,7 @@ def run(ir, graphs: Graphs, X, params, segments=1):
                 xh = a[2][:, h * D:(h + 1) * D]
                 if ir["sched"]["gat_mode"] == 0:
                     heads.append(_GatRef.apply(aL[:, h].reshape(-1, 1), aR[:, h].reshape(-1, 1), xh, rp, col,
-                                               graphs.n, nd["param"]))
+                                               graphs.n, nd["param"], rp_b, col_b))
                 else:
                     alpha = _softmax(rp, _lrelu(aL[:, h][_rows(rp)] + aR[:, h][torch.as_tensor(col, dtype=torch.long)],
                                                 nd["param"]))
