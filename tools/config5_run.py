@@ -8,7 +8,10 @@ line per run:
   gcn3_papers10  gala.dist_run --layout vcut --dist: the vertex cut with its collectives
                  over RCCL at world 1 (dense reduce-scatter, and the sparse all-to-all)
   gat_products_h8  the generated binary, then gala.dist_run --layout vcut --dist (config 3's
-                 8-head GAT program as VertexCutGat layers)
+                 8-head GAT program as VertexCutGat layers) and the halo layout over RCCL
+                 (HaloGat layers)
+  sage_reddit_sampled  config 4 (kernel-sampled SAGE on the Reddit shape): the generated
+                 binary, then gala.dist_run on the row partition, alone and over RCCL
 Epoch times are the programs' own means (first epochs dropped, as gala.cu:613-637).
 """
 import json
@@ -42,7 +45,7 @@ def main():
     env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
     env.pop("GALA_DIST_BACKEND", None)
     irs = {}
-    for prog in ("gcn3_papers10", "gat_products_h8"):
+    for prog in ("gcn3_papers10", "gat_products_h8", "sage_reddit_sampled"):
         irs[prog] = f"/tmp/{prog}.json"
         subprocess.run([GALAC, os.path.join(ROOT, "bench", "dsl", f"{prog}.txt"), "--quiet", "--ir-json",
                         irs[prog]], check=True)
@@ -62,7 +65,16 @@ def main():
         ("gat_products_h8 dist_run vcut dense RCCL world1",
          dr + [irs["gat_products_h8"], "--synthetic", "--iters", iters, "--layout", "vcut", "--dist",
                "--exchange", "dense"]),
+        ("gat_products_h8 dist_run halo RCCL world1",
+         dr + [irs["gat_products_h8"], "--synthetic", "--iters", iters, "--dist"]),
+        ("sage_reddit_sampled generated binary", [os.path.join(PKG, "progs", "sage_reddit_sampled", "gala_prog"),
+                                                  "--synthetic", "--iters", iters]),
+        ("sage_reddit_sampled dist_run halo world1", dr + [irs["sage_reddit_sampled"], "--synthetic", "--iters", iters]),
+        ("sage_reddit_sampled dist_run halo RCCL world1",
+         dr + [irs["sage_reddit_sampled"], "--synthetic", "--iters", iters, "--dist"]),
     ]
+    only = sys.argv[2:]
+    steps = [s for s in steps if not only or any(s[0].startswith(o) for o in only)]
     for tag, cmd in steps:
         if run(tag, cmd, env) != 0:
             return 1
