@@ -851,6 +851,11 @@ def main():
     if distributed:
         from gala.comm import shutdown
         shutdown()
+        # no library destructors after the process group is closed: a gloo rank could abort
+        # in one at interpreter exit (gala/dist_run.py); the result line is already written
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

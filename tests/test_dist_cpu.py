@@ -56,6 +56,9 @@ def _worker(rank, world, port, q):
         dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)   # skip library destructors: a gloo rank can abort in one at interpreter exit
 
 
 def _free_port():

@@ -265,6 +265,9 @@ def _worker(rank, world, port, name, q):
         dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)   # skip library destructors: a gloo rank can abort in one at interpreter exit
 
 
 def _free_port():
@@ -341,6 +344,9 @@ def _gat_worker(rank, world, port, name, chunks, q, exchange="dense"):
         dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)   # skip library destructors: a gloo rank can abort in one at interpreter exit
 
 
 @pytest.mark.parametrize("world,name,chunks,exchange", [(2, "powerlaw", 1, "dense"), (3, "cora", 2, "dense"),
@@ -437,6 +443,9 @@ def _gat_train_worker(rank, world, port, name, chunks, q, rc=False, exchange="de
         dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)   # skip library destructors: a gloo rank can abort in one at interpreter exit
 
 
 @pytest.mark.parametrize("world,name,chunks,rc,exchange",
@@ -513,6 +522,9 @@ def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q):
         dist.barrier()      # every rank tears down together (gloo)
     finally:
         dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)   # skip library destructors: a gloo rank can abort in one at interpreter exit
 
 
 @pytest.mark.parametrize("world,name,rc,halo_mode", [(2, "powerlaw", False, "p2p"), (3, "cora", True, "dense"),
