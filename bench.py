@@ -291,11 +291,18 @@ def headline_graph(args):
     if d is None:
         return products_graph("uniform", args.scale), None
     from gala import layout
-    g = layout.load_npy_dataset(d)
+    if d.endswith(".mtx"):    # a Matrix Market graph, as the reference's readSM reads it
+        g = layout.load_mtx(d)
+        g.val = None           # the GCN step aggregates the pattern (values 1, like readSM_npy32)
+        desc = (f"real: {os.path.abspath(d)} (Matrix Market, readSM / MtxIO semantics: 1-based, "
+                f"symmetric files mirrored; the pattern aggregated); X~U[-1,1) fp32")
+    else:
+        g = layout.load_npy_dataset(d)
+        desc = (f"real: {os.path.abspath(d)} (Adj_src/Adj_dst.npy, gala_export_npy.py format: CSR rows = src, "
+                f"values 1); X~U[-1,1) fp32")
     if g.n_rows != g.n_cols:
         raise SystemExit(f"bench.py: {d} holds a {g.n_rows} x {g.n_cols} graph; the aggregation needs it square")
-    return g, (f"real: {os.path.abspath(d)} (Adj_src/Adj_dst.npy, gala_export_npy.py format: CSR rows = src, "
-               f"values 1); X~U[-1,1) fp32")
+    return g, desc
 
 
 class OneGpuGCN:
@@ -799,8 +806,9 @@ def main():
     ap.add_argument("--no-rmat", action="store_true")
     ap.add_argument("--no-gat", action="store_true")
     ap.add_argument("--no-weak", action="store_true")
-    ap.add_argument("--data", help="dataset directory in the reference's npy format (Adj_src.npy, Adj_dst.npy); "
-                                   "default: Data/Products/ when present, else the synthetic graph")
+    ap.add_argument("--data", help="dataset directory in the reference's npy format (Adj_src.npy, Adj_dst.npy) "
+                                   "or a Matrix Market .mtx graph; default: Data/Products/ when present, else "
+                                   "the synthetic graph")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -14,6 +14,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <string>
 #include <vector>
 
 #include "../../include/gala_hip.h"
@@ -317,3 +321,105 @@ extern "C" int gala_host_mask_subgraph(int64_t n_rows, const int32_t *rowptr, co
     }
     return GALA_OK;
 }
+
+// ---- Matrix Market (readSM -> MtxIO::readMM, src/utils/mtx_io.h:199-499) ----------------
+namespace {
+
+struct MtxHeader {
+    int64_t n_rows = 0, n_cols = 0, nnz = 0;
+    int32_t field = 0, symmetry = 0;
+};
+
+// Header line "%%MatrixMarket matrix coordinate <field> <symmetry>", then comment lines
+// (first character '%'), then the size line "rows cols nnz" -- as readHeaderMM,
+// skipCommentsMM and readCooSizeMM parse them (mtx_io.h:199-270).
+int mtx_header(std::ifstream &in, MtxHeader &h) {
+    std::string line;
+    if (std::getline(in, line).eof()) return GALA_ERR_INVALID_ARG;
+    char id[64] = {0}, object[64] = {0}, format[64] = {0}, field[64] = {0}, sym[64] = {0};
+    if (sscanf(line.c_str(), "%63s %63s %63s %63s %63s", id, object, format, field, sym) != 5)
+        return GALA_ERR_INVALID_ARG;
+    if (strcmp(object, "matrix") != 0) return GALA_ERR_INVALID_ARG;
+    if (strcmp(format, "array") == 0) return GALA_ERR_UNSUPPORTED;  // dense: not a graph
+    if (strcmp(format, "coordinate") != 0) return GALA_ERR_INVALID_ARG;
+    if (strcmp(field, "pattern") == 0) h.field = 0;
+    else if (strcmp(field, "integer") == 0) h.field = 1;
+    else if (strcmp(field, "real") == 0) h.field = 2;
+    else if (strcmp(field, "double") == 0) h.field = 3;
+    else if (strcmp(field, "complex") == 0) return GALA_ERR_UNSUPPORTED;
+    else return GALA_ERR_INVALID_ARG;
+    if (strcmp(sym, "general") == 0) h.symmetry = 0;
+    else if (strcmp(sym, "symmetric") == 0) h.symmetry = 1;
+    else if (strcmp(sym, "skew-symmetric") == 0) h.symmetry = 2;
+    else if (strcmp(sym, "hermitian") == 0) return GALA_ERR_UNSUPPORTED;
+    else return GALA_ERR_INVALID_ARG;
+    while (!std::getline(in, line).eof())
+        if (line.empty() || line[0] != '%') break;
+    unsigned long long nr = 0, nc = 0, nz = 0;
+    if (sscanf(line.c_str(), "%llu %llu %llu", &nr, &nc, &nz) != 3) return GALA_ERR_INVALID_ARG;
+    if (nr > (unsigned long long)INT32_MAX || nc > (unsigned long long)INT32_MAX ||
+        nz > (unsigned long long)INT64_MAX / 2)
+        return GALA_ERR_UNSUPPORTED;
+    h.n_rows = (int64_t)nr;
+    h.n_cols = (int64_t)nc;
+    h.nnz = (int64_t)nz;
+    return GALA_OK;
+}
+
+}  // namespace
+
+extern "C" int gala_host_mtx_info(const char *path, int64_t *n_rows, int64_t *n_cols, int64_t *nnz,
+                                  int32_t *field, int32_t *symmetry, int64_t *capacity) {
+    if (!path || !n_rows || !n_cols || !nnz || !field || !symmetry || !capacity) return GALA_ERR_INVALID_ARG;
+    std::ifstream in(path);
+    if (!in.good()) return GALA_ERR_INVALID_ARG;
+    MtxHeader h;
+    const int st = mtx_header(in, h);
+    if (st != GALA_OK) return st;
+    *n_rows = h.n_rows;
+    *n_cols = h.n_cols;
+    *nnz = h.nnz;
+    *field = h.field;
+    *symmetry = h.symmetry;
+    *capacity = h.symmetry ? 2 * h.nnz : h.nnz;
+    return GALA_OK;
+}
+
+extern "C" int gala_host_mtx_read(const char *path, int32_t *rows, int32_t *cols, float *vals,
+                                  int64_t capacity, int64_t *count_out) {
+    if (!path || !rows || !cols || !count_out || capacity < 0) return GALA_ERR_INVALID_ARG;
+    std::ifstream in(path);
+    if (!in.good()) return GALA_ERR_INVALID_ARG;
+    MtxHeader h;
+    const int st = mtx_header(in, h);
+    if (st != GALA_OK) return st;
+    if (capacity < (h.symmetry ? 2 * h.nnz : h.nnz)) return GALA_ERR_INVALID_ARG;
+    std::string line;
+    int64_t index = 0;
+    // readMM's loop (mtx_io.h:404-447): an entry line is used only when getline did not
+    // reach the end of the file while reading it
+    for (int64_t li = 0; li < h.nnz && !std::getline(in, line).eof(); ++li) {
+        long long r = 0, c = 0, iv = 0;
+        double dv = 0.0;
+        int got;
+        if (h.field == 0) got = sscanf(line.c_str(), "%lld %lld", &r, &c) == 2;
+        else if (h.field == 1) got = sscanf(line.c_str(), "%lld %lld %lld", &r, &c, &iv) == 3;
+        else got = sscanf(line.c_str(), "%lld %lld %lf", &r, &c, &dv) == 3;
+        if (!got) return GALA_ERR_INVALID_ARG;
+        if (r < 1 || r > h.n_rows || c < 1 || c > h.n_cols) return GALA_ERR_GRAPH;
+        const float v = h.field == 0 ? 1.0f : h.field == 1 ? (float)iv : (float)dv;
+        rows[index] = (int32_t)(r - 1);
+        cols[index] = (int32_t)(c - 1);
+        if (vals) vals[index] = v;
+        ++index;
+        if (h.symmetry && r != c) {  // the mirror, same value (mtx_io.h:435-445)
+            rows[index] = (int32_t)(c - 1);
+            cols[index] = (int32_t)(r - 1);
+            if (vals) vals[index] = v;
+            ++index;
+        }
+    }
+    *count_out = index;
+    return GALA_OK;
+}
+

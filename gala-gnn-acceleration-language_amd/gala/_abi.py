@@ -121,6 +121,8 @@ SIGNATURES = {
     "gala_host_row_order": (ctypes.c_int, [_I64, _P, _P]),
     "gala_host_gen_graph": (ctypes.c_int, [_I32, _I64, _I64, ctypes.c_uint64, _P, _P]),
     "gala_host_mask_subgraph": (ctypes.c_int, [_I64, _P, _P, _P, _P, _P, _P]),
+    "gala_host_mtx_info": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _P, _P, _P]),
+    "gala_host_mtx_read": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _I64, _P]),
     "gala_dense_grad_workspace": (ctypes.c_int64, [_I64, _I32, _I32]),
     "gala_dense_grad_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _I64, _P, _P, _I32, _P, _I64, _P]),
 }

@@ -421,7 +421,8 @@ def load(ir_path):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("ir", help="galac --ir-json output (its post-pass IR is run)")
-    ap.add_argument("--data", help="dataset directory in the reference's npy format")
+    ap.add_argument("--data", help="dataset directory in the reference's npy format, or a Matrix Market .mtx "
+                                   "graph (then with synthetic features, labels and training rows)")
     ap.add_argument("--synthetic", action="store_true", help="a seeded graph of the dataset's published shape")
     ap.add_argument("--scale", type=float, default=1.0, help="synthetic graph size multiplier")
     ap.add_argument("--iters", type=int, default=None)
@@ -463,7 +464,14 @@ def main(argv=None):
         dist.init_process_group(backend, **kw)
     ir = load(args.ir)
     s = ir["sched"]
-    if args.data:
+    if args.data and args.data.endswith(".mtx"):
+        # a Matrix Market graph (readSM / MtxIO semantics; the pattern), synthetic features
+        g = layout.load_mtx(args.data)
+        g.val = None
+        shape = dataset_shape(s["dataset"])
+        frac = shape[4] if shape else 0.1
+        X_all = lab_all = tr_all = None
+    elif args.data:
         g = layout.load_npy_dataset(args.data)
         X_all = np.load(os.path.join(args.data, "Feat.npy"), mmap_mode="r")
         lab_all = np.load(os.path.join(args.data, "Lab.npy")).reshape(-1)

@@ -7,6 +7,7 @@ inplace_sample_graph_ab (src/ops/tiling.h:454-508).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 
@@ -130,6 +131,44 @@ def gen_graph(kind: str, n: int, n_undirected: int, seed: int = 42) -> HostGraph
     dst = np.empty(m, np.int32)
     _abi.call("gala_host_gen_graph", k, n, n_undirected, seed, _p(src), _p(dst))
     return csr_build(n, n, src, dst)
+
+
+MTX_FIELDS = ("pattern", "integer", "real", "double")
+MTX_SYMMETRY = ("general", "symmetric", "skew-symmetric")
+
+
+def mtx_info(path: str) -> dict:
+    """Header of a Matrix Market file (gala_host_mtx_info)."""
+    v = [ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()]
+    _abi.call("gala_host_mtx_info", os.fsencode(path), *[ctypes.addressof(x) for x in v])
+    return {"n_rows": v[0].value, "n_cols": v[1].value, "nnz": v[2].value, "field": MTX_FIELDS[v[3].value],
+            "symmetry": MTX_SYMMETRY[v[4].value], "capacity": v[5].value}
+
+
+def read_mtx_coo(path: str):
+    """(info, rows, cols, vals) of a Matrix Market file: the reference's MtxIO entries
+    (src/utils/mtx_io.h:199-499), 0-based, file order, (skew-)symmetric mirrors included;
+    vals None for a pattern file."""
+    info = mtx_info(path)
+    cap = max(info["capacity"], 1)
+    rows = np.empty(cap, np.int32)
+    cols = np.empty(cap, np.int32)
+    vals = np.empty(cap, np.float32)
+    n = ctypes.c_int64()
+    _abi.call("gala_host_mtx_read", os.fsencode(path), _p(rows), _p(cols), _p(vals), cap, ctypes.addressof(n))
+    k = n.value
+    return info, rows[:k], cols[:k], (None if info["field"] == "pattern" else vals[:k])
+
+
+def load_mtx(path: str) -> HostGraph:
+    """A Matrix Market graph as the reference's readSM builds it (src/utils/common.h:397-416:
+    MtxIO entries -> CSRCMatrix::build(CSR), rows sorted, columns ascending, values carried;
+    a pattern file has no values, i.e. an unweighted graph)."""
+    info, rows, cols, vals = read_mtx_coo(path)
+    g, perm = csr_build(info["n_rows"], info["n_cols"], rows, cols, return_perm=True)
+    if vals is not None:
+        g.val = np.ascontiguousarray(vals[perm])
+    return g
 
 
 def load_npy_dataset(path: str) -> HostGraph:

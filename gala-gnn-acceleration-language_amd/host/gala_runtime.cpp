@@ -143,6 +143,8 @@ inline uint64_t mix64(uint64_t x) {
 }
 inline double unit(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
 
+void synthetic_nodes(Dataset &ds, const DatasetShape &s, const RunArgs &a);
+
 Dataset synthetic(const std::string &name, const RunArgs &a, int64_t feat_size,
                   int64_t label_size) {
     DatasetShape s = shape_of(name);
@@ -163,6 +165,14 @@ Dataset synthetic(const std::string &name, const RunArgs &a, int64_t feat_size,
     check(gala_host_csr_build(n, n, m, src.data(), dst.data(), ds.rowptr.data_ptr<int32_t>(),
                               ds.col.data_ptr<int32_t>(), nullptr),
           "gala_host_csr_build");
+    synthetic_nodes(ds, s, a);
+    return ds;
+}
+
+// Seeded features U[-1, 1), labels and train / valid / test masks of the dataset's shape for
+// the ds.n vertices of ds (a synthetic graph, or a Matrix Market graph without node data).
+void synthetic_nodes(Dataset &ds, const DatasetShape &s, const RunArgs &a) {
+    const int64_t n = ds.n;
     ds.feat = torch::empty({n, s.feat}, torch::kFloat);
     float *fp = ds.feat.data_ptr<float>();
     const uint64_t fseed = mix64(0xFEA7ULL + a.seed);
@@ -185,6 +195,34 @@ Dataset synthetic(const std::string &name, const RunArgs &a, int64_t feat_size,
         te[i] = !tr[i] && !va[i];
     }
     ds.classes = s.classes;
+}
+
+// A Matrix Market graph (the reference's readSM -> MtxIO, src/utils/common.h:397-416;
+// gala_host_mtx_read), its pattern as the adjacency; node data synthetic of the program's
+// dataset shape (feature / label sizes from the program).
+Dataset from_mtx(const std::string &name, const std::string &path, const RunArgs &a, int64_t feat_size,
+                 int64_t label_size) {
+    int64_t nr = 0, nc = 0, nnz = 0, cap = 0;
+    int32_t field = 0, sym = 0;
+    check(gala_host_mtx_info(path.c_str(), &nr, &nc, &nnz, &field, &sym, &cap), "gala_host_mtx_info");
+    TORCH_CHECK(nr == nc, "gala: non-square Matrix Market graph ", path);
+    std::vector<int32_t> rows(std::max<int64_t>(cap, 1)), cols(std::max<int64_t>(cap, 1));
+    int64_t m = 0;
+    check(gala_host_mtx_read(path.c_str(), rows.data(), cols.data(), nullptr, cap, &m), "gala_host_mtx_read");
+    Dataset ds;
+    ds.name = name;
+    ds.source = path;
+    ds.n = nr;
+    ds.rowptr = torch::empty({nr + 1}, torch::kInt);
+    ds.col = torch::empty({m}, torch::kInt);
+    check(gala_host_csr_build(nr, nc, m, rows.data(), cols.data(), ds.rowptr.data_ptr<int32_t>(),
+                              ds.col.data_ptr<int32_t>(), nullptr),
+          "gala_host_csr_build");
+    DatasetShape s{};
+    if (!dataset_shape(name, &s)) s = DatasetShape{nr, 0, 16, 2, 0.5, 0.2};
+    if (feat_size > 0) s.feat = feat_size;
+    if (label_size > 0) s.classes = label_size;
+    synthetic_nodes(ds, s, a);
     return ds;
 }
 
@@ -308,7 +346,11 @@ RunArgs parse_args(int argc, char **argv) {
             TORCH_CHECK(i + 1 < argc, "gala: ", k, " needs a value");
             return argv[++i];
         };
-        if (k == "--data") a.data_dir = with_slash(val());
+        if (k == "--data") {  // a dataset directory, or a Matrix Market graph file
+            a.data_dir = val();
+            if (a.data_dir.size() < 4 || a.data_dir.compare(a.data_dir.size() - 4, 4, ".mtx") != 0)
+                a.data_dir = with_slash(a.data_dir);
+        }
         else if (k == "--synthetic") a.synthetic = true;
         else if (k == "--scale") a.scale = std::stod(val());
         else if (k == "--iters") a.iters = std::stoll(val());
@@ -337,6 +379,9 @@ void sync(const torch::Device &dev) {
 Dataset load_dataset(const std::string &name, const RunArgs &args, int64_t feat_size,
                      int64_t label_size, const std::string &opt_input) {
     if (!args.synthetic) {
+        const std::string &d0 = args.data_dir;
+        if (d0.size() >= 4 && d0.compare(d0.size() - 4, 4, ".mtx") == 0)
+            return from_mtx(name, d0, args, feat_size, label_size);
         std::vector<std::string> dirs;
         if (!args.data_dir.empty()) dirs.push_back(args.data_dir);
         if (!opt_input.empty()) dirs.push_back(with_slash(opt_input));

@@ -526,6 +526,28 @@ int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected, uint64_t 
                         int32_t *src, int32_t *dst);
 
 /*
+ * Matrix Market graphs: the reference's readSM -> MtxIO::readMtx / readMM
+ * (src/utils/common.h:397-416, src/utils/mtx_io.h:199-499), coordinate format.
+ * gala_host_mtx_info reads the header and the size line:
+ *   field     0 pattern, 1 integer, 2 real, 3 double (complex: GALA_ERR_UNSUPPORTED)
+ *   symmetry  0 general, 1 symmetric, 2 skew-symmetric (hermitian: GALA_ERR_UNSUPPORTED)
+ *   capacity  COO entries gala_host_mtx_read may write: nnz, twice that when symmetric.
+ * "array" (dense) files are GALA_ERR_UNSUPPORTED; a missing or malformed file is
+ * GALA_ERR_INVALID_ARG.
+ * gala_host_mtx_read writes the entries 0-based in file order; an off-diagonal entry of a
+ * (skew-)symmetric file is followed by its mirror with the SAME value (the reference does
+ * not negate skew-symmetric mirrors).  As in the reference, the entry lines are read while
+ * each ends in a newline: a last line without one is not read.  vals may be NULL; for a
+ * pattern file it receives 1.0f (the reference leaves pattern values unallocated).
+ * Indices outside [1, n] are GALA_ERR_GRAPH (the reference does not check them).
+ * *count_out = entries written.
+ */
+int gala_host_mtx_info(const char *path, int64_t *n_rows, int64_t *n_cols, int64_t *nnz, int32_t *field,
+                       int32_t *symmetry, int64_t *capacity);
+int gala_host_mtx_read(const char *path, int32_t *rows, int32_t *cols, float *vals, int64_t capacity,
+                       int64_t *count_out);
+
+/*
  * FFN (torch Linear) gradients of a tall-skinny node matrix: dW[m,k] = sum_n dY[n,m]
  * X[n,k] ([M,K] row-major, the Linear weight layout) and, if db != NULL, db[m] =
  * sum_n dY[n,m].  accumulate != 0 adds into dW / db.  The rows are split into chunks

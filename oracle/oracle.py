@@ -312,6 +312,35 @@ def ref_csr_build(n_rows, n_cols, src, dst):
     return rp, col, val
 
 
+def ref_read_mtx(path, cap):
+    """The reference's MtxIO::readMtx (src/utils/mtx_io.h:199-499): (n_rows, n_cols, rows,
+    cols, vals or None) of the COO entries in file order, mirrors included."""
+    rows = np.zeros(cap, np.int32)
+    cols = np.zeros(cap, np.int32)
+    vals = np.zeros(cap, np.float32)
+    nr, nc, nv = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    st = ref().ref_read_mtx(str(path).encode(), ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(nv), _ptr(rows),
+                            _ptr(cols), _ptr(vals), ctypes.c_int64(cap))
+    if st < 0:
+        raise RuntimeError(f"ref_read_mtx: {st}")
+    n = nv.value
+    return nr.value, nc.value, rows[:n], cols[:n], (vals[:n] if st == 1 else None)
+
+
+def ref_read_sm_mtx(path, n_rows, cap):
+    """The reference's readSM (src/utils/common.h:397-416): MtxIO -> CSRCMatrix::build(CSR);
+    (rowptr, col, val or None)."""
+    rp = np.zeros(n_rows + 1, np.int32)
+    col = np.zeros(cap, np.int32)
+    val = np.zeros(cap, np.float32)
+    st = ref().ref_read_sm_mtx(str(path).encode(), _ptr(rp), _ptr(col), _ptr(val), ctypes.c_int64(n_rows + 1),
+                               ctypes.c_int64(cap))
+    if st < 0:
+        raise RuntimeError(f"ref_read_sm_mtx: {st}")
+    n = int(rp[-1])
+    return rp, col[:n], (val[:n] if st == 1 else None)
+
+
 def ref_gspmm(g: Graph, X, Y=None):
     X = np.ascontiguousarray(X, np.float32)
     val = g.val if g.val is not None else np.ones(g.nnz, np.float32)

@@ -13,6 +13,7 @@
 //   static_ord_col_breakpoints + ord_col_tiling_torch  src/ops/tiling.h:1594-1608, 222-283
 //   inplace_sample_graph_ab   src/ops/tiling.h:454-508
 //   getMaskSubgraphs + buildTranspose  src/utils/common.h:26-129 (same as tests/common.h:21-124)
+//   readSM (Matrix Market)    src/utils/common.h:397-416 -> MtxIO::readMtx src/utils/mtx_io.h:199-499
 #include <malloc.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -167,3 +168,36 @@ extern "C" int ref_omp_threads(void) { return omp_get_max_threads(); }
 
 // the CPU baseline runs gSpMM on every core the process may use (bench.py picks the count)
 extern "C" void ref_set_threads(int n) { omp_set_num_threads(n); }
+
+// Matrix Market: the reference's MtxIO reader (src/utils/mtx_io.h:199-499) -- the COO
+// entries in file order, mirrors of (skew-)symmetric files included -- and readSM's CSR
+// (src/utils/common.h:397-416: MtxIO -> CSRCMatrix::build(CSR)).  Returns 1 when the file
+// has values, 0 for a pattern file, < 0 on a reader error or too small a capacity.
+extern "C" int ref_read_mtx(const char *path, int64_t *nrows, int64_t *ncols, int64_t *nvals, int *rows,
+                            int *cols, float *vals, int64_t cap) {
+    MtxIO<int, int, float> reader;
+    if (reader.readMtx(std::string(path)) != IO_INFO::SUCCESS) return -1;
+    int nr, nc, nv, size;
+    int *r, *c;
+    float *v;
+    reader.getData(nr, nc, nv, size, r, c, v);
+    *nrows = nr;
+    *ncols = nc;
+    *nvals = nv;
+    if (nv > cap) return -2;
+    memcpy(rows, r, (int64_t)nv * sizeof(int));
+    memcpy(cols, c, (int64_t)nv * sizeof(int));
+    if (v && vals) memcpy(vals, v, (int64_t)nv * sizeof(float));
+    return v ? 1 : 0;
+}
+
+extern "C" int ref_read_sm_mtx(const char *path, int *rowptr, int *col, float *val, int64_t cap_rows,
+                               int64_t cap_nnz) {
+    SM A;
+    readSM<SM>(std::string(path), &A);
+    if ((int64_t)A.nrows() + 1 > cap_rows || (int64_t)A.nvals() > cap_nnz) return -2;
+    memcpy(rowptr, A.offset_ptr(), ((int64_t)A.nrows() + 1) * sizeof(int));
+    memcpy(col, A.ids_ptr(), (int64_t)A.nvals() * sizeof(int));
+    if (val && A.vals_ptr()) memcpy(val, A.vals_ptr(), (int64_t)A.nvals() * sizeof(float));
+    return A.vals_ptr() ? 1 : 0;
+}

@@ -121,3 +121,30 @@ def test_bench_real_data(tmp_path):
         (d,) = _json_lines(r.stdout)
         assert d["config"]["n_vertices"] == n and d["config"]["edges"] == e
         assert d["data"].startswith("real: ") and str(tmp_path) in d["data"]
+
+
+def test_bench_matrix_market_graph(tmp_path):
+    """--data FILE.mtx: the headline step on a Matrix Market graph (symmetric pattern file,
+    mirrored as the reference's readSM does), one rank."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    n, m = 1200, 5000
+    r = rng.integers(1, n + 1, m)
+    c = rng.integers(1, n + 1, m)
+    lo, hi = np.maximum(r, c), np.minimum(r, c)
+    keep = np.unique(np.stack([lo, hi], 1), axis=0)
+    lines = ["%%MatrixMarket matrix coordinate pattern symmetric", f"{n} {n} {keep.shape[0] + n}"]
+    lines += [f"{a} {b}" for a, b in keep if a != b] + [f"{i} {i}" for i in range(1, n + 1)]
+    lines[1] = f"{n} {n} {len(lines) - 2}"
+    p = tmp_path / "g.mtx"
+    p.write_text("\n".join(lines) + "\n")
+    from gala import layout
+    g = layout.load_mtx(str(p))
+    res = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--data", str(p), "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline", "--no-rmat"], capture_output=True, text=True, timeout=600, env=_env(),
+                         cwd=ROOT)
+    assert res.returncode == 0, res.stderr[-3000:]
+    (d,) = _json_lines(res.stdout)
+    assert d["config"]["n_vertices"] == n and d["config"]["edges"] == g.nnz
+    assert "Matrix Market" in d["data"]
+

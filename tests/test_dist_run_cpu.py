@@ -236,3 +236,21 @@ def test_dist_run_collectives_at_world_one(tmp_path):
     assert s1["backend"] == "gloo"
     np.testing.assert_array_equal(d1["prediction"], d0["prediction"])
     np.testing.assert_array_equal(d1["losses"], d0["losses"])
+
+
+def test_dist_run_on_a_matrix_market_graph(tmp_path):
+    """--data FILE.mtx: the program on a Matrix Market graph (read as the reference's readSM
+    does; a symmetric pattern file, mirrored) with synthetic features: world 1 against the
+    IR executor, world 2 bit-identical to world 1."""
+    rng = np.random.default_rng(2)
+    n = 700
+    r, c = rng.integers(1, n + 1, 3000), rng.integers(1, n + 1, 3000)
+    pairs = np.unique(np.stack([np.maximum(r, c), np.minimum(r, c)], 1), axis=0)
+    ent = [f"{a} {b}" for a, b in pairs if a != b] + [f"{i} {i}" for i in range(1, n + 1)]
+    p = tmp_path / "g.mtx"
+    p.write_text("\n".join(["%%MatrixMarket matrix coordinate pattern symmetric", f"{n} {n} {len(ent)}"] + ent) + "\n")
+    ir_path = _ir("gcn.txt", tmp_path)
+    d1, _ = _run(ir_path, tmp_path, 1, "m1", iters=3, extra=("--data", str(p)))
+    _check_ir(ir_path, d1)
+    d2, _ = _run(ir_path, tmp_path, 2, "m2", iters=3, extra=("--data", str(p)))
+    np.testing.assert_array_equal(d2["prediction"], d1["prediction"])

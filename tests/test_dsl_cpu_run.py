@@ -107,3 +107,31 @@ def test_directed_program_on_a_directed_graph(name, tmp_path):
     rp = d["rowptr"]
     assert not np.array_equal(np.diff(rp), np.bincount(d["col"], minlength=len(rp) - 1))
     check_against_ir(name, d)
+
+
+def test_program_on_a_matrix_market_graph(tmp_path):
+    """--data FILE.mtx: a generated program on a Matrix Market graph (the reference's readSM
+    semantics: 1-based entries, a symmetric file mirrored; the pattern is the adjacency) with
+    synthetic node data; the graph is the one layout.load_mtx builds, and one epoch matches
+    the IR executor."""
+    from _dsl_check import check_against_ir
+    from gala import layout
+    import _ir_ref as ref
+    rng = np.random.default_rng(8)
+    n = 600
+    r, c = rng.integers(1, n + 1, 2500), rng.integers(1, n + 1, 2500)
+    pairs = np.unique(np.stack([np.maximum(r, c), np.minimum(r, c)], 1), axis=0)
+    ent = [f"{a} {b}" for a, b in pairs if a != b] + [f"{i} {i}" for i in range(1, n + 1)]
+    p = tmp_path / "g.mtx"
+    p.write_text("\n".join(["%%MatrixMarket matrix coordinate pattern symmetric", "% test", f"{n} {n} {len(ent)}"]
+                           + ent) + "\n")
+    exe = os.path.join(PKG, "progs", "gcn", "gala_prog")
+    dump = tmp_path / "d.dump"
+    res = subprocess.run([exe, "--data", str(p), "--device", "cpu", "--seed", "3", "--iters", "1", "--dump",
+                          str(dump)], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = ref.read_dump(str(dump))
+    g = layout.load_mtx(str(p))
+    np.testing.assert_array_equal(d["rowptr"], g.rowptr)
+    np.testing.assert_array_equal(d["col"], g.col)
+    check_against_ir("gcn", d)
