@@ -328,20 +328,22 @@ namespace {
 struct MtxHeader {
     int64_t n_rows = 0, n_cols = 0, nnz = 0;
     int32_t field = 0, symmetry = 0;
+    bool dense = false;
 };
 
 // Header line "%%MatrixMarket matrix coordinate <field> <symmetry>", then comment lines
 // (first character '%'), then the size line "rows cols nnz" -- as readHeaderMM,
 // skipCommentsMM and readCooSizeMM parse them (mtx_io.h:199-270).
-int mtx_header(std::ifstream &in, MtxHeader &h) {
+int mtx_header(std::ifstream &in, MtxHeader &h, bool want_dense = false) {
     std::string line;
     if (std::getline(in, line).eof()) return GALA_ERR_INVALID_ARG;
     char id[64] = {0}, object[64] = {0}, format[64] = {0}, field[64] = {0}, sym[64] = {0};
     if (sscanf(line.c_str(), "%63s %63s %63s %63s %63s", id, object, format, field, sym) != 5)
         return GALA_ERR_INVALID_ARG;
     if (strcmp(object, "matrix") != 0) return GALA_ERR_INVALID_ARG;
-    if (strcmp(format, "array") == 0) return GALA_ERR_UNSUPPORTED;  // dense: not a graph
-    if (strcmp(format, "coordinate") != 0) return GALA_ERR_INVALID_ARG;
+    h.dense = strcmp(format, "array") == 0;
+    if (!h.dense && strcmp(format, "coordinate") != 0) return GALA_ERR_INVALID_ARG;
+    if (h.dense != want_dense) return GALA_ERR_UNSUPPORTED;  // a graph reader on dense data, or back
     if (strcmp(field, "pattern") == 0) h.field = 0;
     else if (strcmp(field, "integer") == 0) h.field = 1;
     else if (strcmp(field, "real") == 0) h.field = 2;
@@ -353,10 +355,17 @@ int mtx_header(std::ifstream &in, MtxHeader &h) {
     else if (strcmp(sym, "skew-symmetric") == 0) h.symmetry = 2;
     else if (strcmp(sym, "hermitian") == 0) return GALA_ERR_UNSUPPORTED;
     else return GALA_ERR_INVALID_ARG;
+    if (h.dense && (h.field == 0 || h.symmetry != 0)) return GALA_ERR_UNSUPPORTED;  // mtx_io.h:323-330
     while (!std::getline(in, line).eof())
         if (line.empty() || line[0] != '%') break;
     unsigned long long nr = 0, nc = 0, nz = 0;
-    if (sscanf(line.c_str(), "%llu %llu %llu", &nr, &nc, &nz) != 3) return GALA_ERR_INVALID_ARG;
+    if (h.dense) {  // readArrSizeMM: "rows cols", nvals = rows * cols
+        if (sscanf(line.c_str(), "%llu %llu", &nr, &nc) != 2) return GALA_ERR_INVALID_ARG;
+        if (nr > (unsigned long long)INT32_MAX || nc > (unsigned long long)INT32_MAX) return GALA_ERR_UNSUPPORTED;
+        nz = nr * nc;
+    } else if (sscanf(line.c_str(), "%llu %llu %llu", &nr, &nc, &nz) != 3) {
+        return GALA_ERR_INVALID_ARG;
+    }
     if (nr > (unsigned long long)INT32_MAX || nc > (unsigned long long)INT32_MAX ||
         nz > (unsigned long long)INT64_MAX / 2)
         return GALA_ERR_UNSUPPORTED;
@@ -418,6 +427,50 @@ extern "C" int gala_host_mtx_read(const char *path, int32_t *rows, int32_t *cols
             if (vals) vals[index] = v;
             ++index;
         }
+    }
+    *count_out = index;
+    return GALA_OK;
+}
+
+extern "C" int gala_host_mtx_dense_info(const char *path, int64_t *n_rows, int64_t *n_cols) {
+    if (!path || !n_rows || !n_cols) return GALA_ERR_INVALID_ARG;
+    std::ifstream in(path);
+    if (!in.good()) return GALA_ERR_INVALID_ARG;
+    MtxHeader h;
+    const int st = mtx_header(in, h, true);
+    if (st != GALA_OK) return st;
+    *n_rows = h.n_rows;
+    *n_cols = h.n_cols;
+    return GALA_OK;
+}
+
+extern "C" int gala_host_mtx_read_dense(const char *path, float *out, int64_t n_rows, int64_t n_cols,
+                                        int64_t *count_out) {
+    if (!path || !count_out || n_rows < 0 || n_cols < 0 || (!out && n_rows * n_cols > 0))
+        return GALA_ERR_INVALID_ARG;
+    std::ifstream in(path);
+    if (!in.good()) return GALA_ERR_INVALID_ARG;
+    MtxHeader h;
+    const int st = mtx_header(in, h, true);
+    if (st != GALA_OK) return st;
+    if (h.n_rows != n_rows || h.n_cols != n_cols) return GALA_ERR_INVALID_ARG;
+    std::fill(out, out + n_rows * n_cols, 0.0f);
+    std::string line;
+    int64_t index = 0;
+    // the array branch of readMM (mtx_io.h:343-363): column-major entries, each line used
+    // only when a newline ends it
+    for (; index < h.nnz && !std::getline(in, line).eof(); ++index) {
+        long long iv = 0;
+        double dv = 0.0;
+        float v;
+        if (h.field == 1) {
+            if (sscanf(line.c_str(), "%lld", &iv) != 1) return GALA_ERR_INVALID_ARG;
+            v = (float)iv;
+        } else {
+            if (sscanf(line.c_str(), "%lf", &dv) != 1) return GALA_ERR_INVALID_ARG;
+            v = (float)dv;
+        }
+        out[(index % n_rows) * n_cols + index / n_rows] = v;
     }
     *count_out = index;
     return GALA_OK;

@@ -123,6 +123,8 @@ SIGNATURES = {
     "gala_host_mask_subgraph": (ctypes.c_int, [_I64, _P, _P, _P, _P, _P, _P]),
     "gala_host_mtx_info": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _P, _P, _P]),
     "gala_host_mtx_read": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _I64, _P]),
+    "gala_host_mtx_dense_info": (ctypes.c_int, [ctypes.c_char_p, _P, _P]),
+    "gala_host_mtx_read_dense": (ctypes.c_int, [ctypes.c_char_p, _P, _I64, _I64, _P]),
     "gala_dense_grad_workspace": (ctypes.c_int64, [_I64, _I32, _I32]),
     "gala_dense_grad_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _I64, _P, _P, _I32, _P, _I64, _P]),
 }

@@ -171,6 +171,17 @@ def load_mtx(path: str) -> HostGraph:
     return g
 
 
+def load_mtx_dense(path: str) -> np.ndarray:
+    """A dense Matrix Market "array" file as float32 [rows, cols] (the reference's readDM
+    without RNPY, src/utils/common.h:146-183: column-major entries placed row-major)."""
+    nr, nc = ctypes.c_int64(), ctypes.c_int64()
+    _abi.call("gala_host_mtx_dense_info", os.fsencode(path), ctypes.addressof(nr), ctypes.addressof(nc))
+    out = np.empty((nr.value, nc.value), np.float32)
+    k = ctypes.c_int64()
+    _abi.call("gala_host_mtx_read_dense", os.fsencode(path), _p(out), nr.value, nc.value, ctypes.addressof(k))
+    return out
+
+
 def load_npy_dataset(path: str) -> HostGraph:
     """The reference's on-disk format (scripts/Data/gala_export_npy.py:104-171):
     Adj_src.npy = uint32 [nrows, ncols, src...], Adj_dst.npy = uint32 [dst...]."""

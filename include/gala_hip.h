@@ -548,6 +548,18 @@ int gala_host_mtx_read(const char *path, int32_t *rows, int32_t *cols, float *va
                        int64_t *count_out);
 
 /*
+ * A dense Matrix Market "array" file (features; the reference's readDM without RNPY,
+ * src/utils/common.h:146-183 -> MtxIO::readMM's array branch, mtx_io.h:316-363):
+ * gala_host_mtx_dense_info gives its shape, gala_host_mtx_read_dense writes it row-major into
+ * out[n_rows * n_cols] (the file lists it column by column).  Integer, real and double
+ * fields, general symmetry only (else GALA_ERR_UNSUPPORTED, as the reference refuses them);
+ * entries the file does not hold (it ends early, or its last line lacks a newline, which
+ * the reference then does not read) are set to 0.  *count_out = entries read.
+ */
+int gala_host_mtx_dense_info(const char *path, int64_t *n_rows, int64_t *n_cols);
+int gala_host_mtx_read_dense(const char *path, float *out, int64_t n_rows, int64_t n_cols, int64_t *count_out);
+
+/*
  * FFN (torch Linear) gradients of a tall-skinny node matrix: dW[m,k] = sum_n dY[n,m]
  * X[n,k] ([M,K] row-major, the Linear weight layout) and, if db != NULL, db[m] =
  * sum_n dY[n,m].  accumulate != 0 adds into dW / db.  The rows are split into chunks

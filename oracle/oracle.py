@@ -327,6 +327,17 @@ def ref_read_mtx(path, cap):
     return nr.value, nc.value, rows[:n], cols[:n], (vals[:n] if st == 1 else None)
 
 
+def ref_read_mtx_dense(path, cap):
+    """The reference's MtxIO on a dense "array" file (readDM without RNPY): float32 [r, c]."""
+    out = np.zeros(cap, np.float32)
+    nr, nc = ctypes.c_int64(), ctypes.c_int64()
+    st = ref().ref_read_mtx_dense(str(path).encode(), ctypes.byref(nr), ctypes.byref(nc), _ptr(out),
+                                  ctypes.c_int64(cap))
+    if st < 0:
+        raise RuntimeError(f"ref_read_mtx_dense: {st}")
+    return out[:nr.value * nc.value].reshape(nr.value, nc.value)
+
+
 def ref_read_sm_mtx(path, n_rows, cap):
     """The reference's readSM (src/utils/common.h:397-416): MtxIO -> CSRCMatrix::build(CSR);
     (rowptr, col, val or None)."""

@@ -201,3 +201,21 @@ extern "C" int ref_read_sm_mtx(const char *path, int *rowptr, int *col, float *v
     if (val && A.vals_ptr()) memcpy(val, A.vals_ptr(), (int64_t)A.nvals() * sizeof(float));
     return A.vals_ptr() ? 1 : 0;
 }
+
+// A dense Matrix Market "array" file through the reference's MtxIO (the array branch of
+// readMM, src/utils/mtx_io.h:316-363: column-major entries placed row-major), which readDM
+// uses when RNPY is not defined (src/utils/common.h:146-183).  Returns 0, < 0 on errors.
+extern "C" int ref_read_mtx_dense(const char *path, int64_t *nrows, int64_t *ncols, float *out, int64_t cap) {
+    MtxIO<int, int64_t, float> reader;
+    if (reader.readMtx(std::string(path)) != IO_INFO::SUCCESS) return -1;
+    int nr, nc;
+    int64_t nv, size;
+    int *r, *c;
+    float *v;
+    reader.getData(nr, nc, nv, size, r, c, v);
+    *nrows = nr;
+    *ncols = nc;
+    if ((int64_t)nr * nc > cap || !v) return -2;
+    memcpy(out, v, (int64_t)nr * nc * sizeof(float));
+    return 0;
+}
