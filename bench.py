@@ -411,6 +411,10 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
     if pt1.halo_mode == "dense":
         ptk = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
         modes.append(HaloMode("halo-pipe", ptk, F, be, comm, exact=False))
+        # finer chunks leave less of the first chunk's transfer and the last chunk's SpMM
+        # outside the overlap, at more (smaller) collectives: both are timed
+        pt8 = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=2 * PIPE_CHUNKS)
+        modes.append(HaloMode(f"halo-pipe{2 * PIPE_CHUNKS}", pt8, F, be, comm, exact=False))
     modes.append(VcutMode("vcut", vc.vertex_cut_partition(g, rank, world, 1, bounds), F, be, comm))
     modes.append(VcutMode("vcut-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds), F, be, comm))
     frac = vc.touched_fraction(g, bounds) if world > 1 else 0.0
