@@ -519,13 +519,15 @@ def run_multi(args, rank, world, dev, be, timer, sync):
     if not args.no_gat:
         out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
     del g
-    if not args.no_rmat:
-        rm, gr, _ = strong_family(args, "rmat", rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+    for kind in ("rmat", "banded"):   # the skewed family, and one that shards naturally
+        if getattr(args, f"no_{kind}"):
+            continue
+        rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
         rm.pop("real_data")
-        rm["graph"] = (f"R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops, N={gr.n_rows}, E={gr.nnz}, "
+        rm["graph"] = (f"{FAMILY_GRAPH[kind]}, N={gr.n_rows}, E={gr.nnz}, "
                        f"max degree {int((gr.rowptr[1:] - gr.rowptr[:-1]).max())}")
         rm["unit"] = "edges/s"
-        out["rmat"] = rm
+        out[kind] = rm
         del gr
     if not args.no_weak:
         out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
@@ -669,8 +671,9 @@ def run_single(args, dev, be, timer, sync):
     if be.name == "hip" and not args.no_gat:
         out["gat"] = gat_layer(args, agg.g, hg, dev, timer, sync)
     del agg
-    if not args.no_rmat:
-        out["rmat"] = rmat_family(args, dev, be, timer, sync)
+    for kind in ("rmat", "banded"):
+        if not getattr(args, f"no_{kind}"):
+            out[kind] = rmat_family(args, dev, be, timer, sync, kind)
     return out
 
 
@@ -761,14 +764,23 @@ def rmat_traffic():
     return a + b if a is not None and b is not None else None
 
 
-def rmat_family(args, dev, be, timer, sync):
-    """The same step on an R-MAT graph of the Products shape: skewed
-    degrees, so the SpMM runs the degree-ordered row schedule and the hub-row chunks."""
+FAMILY_GRAPH = {
+    "rmat": "R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops",
+    "banded": "banded (every edge's ends at most min(8192, n/256) ids apart: a graph with locality, as a "
+              "locality-preserving vertex order gives; it shards naturally) symmetrised + self loops",
+}
+
+
+def rmat_family(args, dev, be, timer, sync, kind="rmat"):
+    """The same step on another graph of the Products shape: R-MAT:
+    skewed degrees, so the SpMM runs the degree-ordered row schedule and the hub-row chunks;
+    or banded: neighbours within min(8192, n/256) ids, so a row's X rows share the L2 (the locality the
+    uniform graph lacks)."""
     import torch
     F = args.F
     t0 = time.time()
-    hg = products_graph("rmat", args.scale)
-    log(f"[bench] R-MAT graph N={hg.n_rows} E={hg.nnz} in {time.time() - t0:.1f}s")
+    hg = products_graph(kind, args.scale)
+    log(f"[bench] {kind} graph N={hg.n_rows} E={hg.nnz} in {time.time() - t0:.1f}s")
     agg = OneGpuGCN(hg, F, be)
     gen = torch.Generator(device=dev).manual_seed(1234)
     X = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
@@ -779,14 +791,16 @@ def rmat_family(args, dev, be, timer, sync):
     t_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, bufs[0], agg.norm, False), 10)
     alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, hg.nnz, F)
     out = {"value": 4 * hg.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
-           "graph": f"R-MAT a=0.57 b=0.19 c=0.19 symmetrised + self loops, N={hg.n_rows}, E={hg.nnz}, "
+           "graph": f"{FAMILY_GRAPH[kind]}, N={hg.n_rows}, E={hg.nnz}, "
                     f"max degree {int((hg.rowptr[1:] - hg.rowptr[:-1]).max())}",
            "split_rows": getattr(agg.g, "split_rows", 0),
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
-                        "alg_bytes_per_launch": alg, "traffic": rmat_traffic() if be.name == "hip" else None,
+                        "alg_bytes_per_launch": alg,
+                        "traffic": rmat_traffic() if (be.name == "hip" and kind == "rmat") else None,
                         "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
-                                  "grid, then k_spmm_fixup)"}}
+                                  "grid, then k_spmm_fixup)" if kind == "rmat" else
+                                  "gala_spmm_f32 (k_spmm_rowgroup, XCD-ordered row blocks)"}}
     with_traffic_rate(out["roofline"])
     if be.name == "hip":
         t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
@@ -808,6 +822,7 @@ def main():
                     help="cpu: the host-CPU backend over gloo (plumbing checks, not a measurement)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rmat", action="store_true")
+    ap.add_argument("--no-banded", action="store_true")
     ap.add_argument("--no-gat", action="store_true")
     ap.add_argument("--no-weak", action="store_true")
     ap.add_argument("--data", help="dataset directory in the reference's npy format (Adj_src.npy, Adj_dst.npy) "

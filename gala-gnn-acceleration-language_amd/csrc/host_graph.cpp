@@ -190,8 +190,7 @@ extern "C" int gala_host_csr_transpose(int64_t n_rows, int64_t n_cols, const int
 
 extern "C" int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected, uint64_t seed,
                                    int32_t *src, int32_t *dst) {
-    if (n < 1 || n_undirected < 0 || !src || !dst || (kind != 0 && kind != 1))
-        return GALA_ERR_INVALID_ARG;
+    if (n < 1 || n_undirected < 0 || !src || !dst || kind < 0 || kind > 2) return GALA_ERR_INVALID_ARG;
     if (2 * n_undirected + n > INT32_MAX || n >= INT32_MAX) return GALA_ERR_UNSUPPORTED;
     const double a = 0.57, b = 0.19, c = 0.19;
 #pragma omp parallel for schedule(static)
@@ -200,6 +199,13 @@ extern "C" int gala_host_gen_graph(int32_t kind, int64_t n, int64_t n_undirected
         if (kind == 0) {
             u = bounded(hash2(seed, 2 * (uint64_t)k), n);
             v = n > 1 ? (u + 1 + bounded(hash2(seed, 2 * (uint64_t)k + 1), n - 1)) % n : u;
+        } else if (kind == 2) {
+            // banded: the other end within band = min(8192, max(16, n / 256)) ids, on the side
+            // that stays inside [0, n)
+            const int64_t band = std::min<int64_t>(8192, std::max<int64_t>(16, n / 256));
+            u = bounded(hash2(seed ^ 0xBA4DULL, 2 * (uint64_t)k), n);
+            const int64_t off = 1 + bounded(hash2(seed ^ 0xBA4DULL, 2 * (uint64_t)k + 1), std::min(band, n));
+            v = u + off < n ? u + off : (u - off >= 0 ? u - off : u);
         } else {
             // recursive quadrant descent of generate_rmat (generator.h:62-80)
             int64_t sr = 0, er = n - 1, sc = 0, ec = n - 1;

@@ -124,8 +124,9 @@ def mask_subgraphs(g: HostGraph, mask: np.ndarray, levels: int):
 
 
 def gen_graph(kind: str, n: int, n_undirected: int, seed: int = 42) -> HostGraph:
-    """Deterministic synthetic graph: 'uniform' (random symmetric + self loops) or 'rmat'."""
-    k = {"uniform": 0, "rmat": 1}[kind]
+    """Deterministic synthetic graph: 'uniform' (random symmetric + self loops), 'rmat', or
+    'banded' (every edge's ends at most min(8192, max(16, n/256)) ids apart)."""
+    k = {"uniform": 0, "rmat": 1, "banded": 2}[kind]
     m = 2 * n_undirected + n
     src = np.empty(m, np.int32)
     dst = np.empty(m, np.int32)

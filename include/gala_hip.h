@@ -518,7 +518,9 @@ int gala_host_csr_transpose(int64_t n_rows, int64_t n_cols, const int32_t *rowpt
  * Deterministic synthetic graphs (counter-based hash RNG, thread-count independent):
  *   kind 0: uniform random symmetric edges + one self loop per vertex;
  *   kind 1: R-MAT (a=0.57,b=0.19,c=0.19; src/utils/generator.h:37-118) symmetrised
- *           + self loops.
+ *           + self loops;
+ *   kind 2: banded: the two ends of an edge at most min(8192, max(16, n/256)) ids apart (locality,
+ *           the shape a locality-preserving vertex order gives), symmetrised + self loops.
  * n_undirected undirected edges -> 2*n_undirected + n vertices directed COO entries
  * written to src/dst (capacity 2*n_undirected + n).
  */

@@ -63,6 +63,11 @@ def test_bench_self_launches_ranks():
     assert rm["value"] > 0 and rm["comm"]["mode"] in rm["comm"]["candidates_ms_per_step"]
     assert "R-MAT" in rm["graph"] and 0.0 <= rm["comm"]["vcut_touched_fraction"] <= 1.0
     assert "rehearsal" in c["rccl_note"]          # gloo: labelled as a rehearsal, not RCCL
+    # the family that shards naturally: a row partition with a point-to-point halo of the
+    # band's boundary rows only
+    bd = d["banded"]
+    assert bd["value"] > 0 and bd["comm"]["halo_layout"] == "p2p" and "banded" in bd["graph"]
+    assert bd["comm"]["halo_bytes_per_aggregation_per_rank"] < c["halo_bytes_per_aggregation_per_rank"]
 
 
 def test_bench_single_rank_line():
@@ -73,6 +78,7 @@ def test_bench_single_rank_line():
     (d,) = _json_lines(r.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert "rmat" in d and d["rmat"]["value"] > 0 and d["rmat"]["roofline"]["alg_bytes_per_launch"] > 0
+    assert d["banded"]["value"] > 0 and "banded" in d["banded"]["graph"]
 
 
 def test_bench_rejects_world_mismatch():

@@ -381,6 +381,8 @@ def test_bench_self_launch_two_ranks_on_one_gpu_gloo():
     assert d["value"] > 0 and d["gat"]["value"] > 0 and set(d["gat"]["candidates_ms_per_step"]) == {"halo", "vcut"}
     rm = d["rmat"]                                     # the skewed family at n_gpus 2
     assert rm["value"] > 0 and rm["comm"]["mode"] in rm["comm"]["candidates_ms_per_step"]
+    bd = d["banded"]                                   # and the one that shards naturally
+    assert bd["value"] > 0 and bd["comm"]["mode"] in bd["comm"]["candidates_ms_per_step"]
 
 
 @pytest.mark.parametrize("world,chunks", [(2, 1), (3, 2), (4, 3)])
