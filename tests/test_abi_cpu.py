@@ -84,6 +84,13 @@ def test_generator_deterministic_and_symmetric():
     r = layout.gen_graph("rmat", 4096, 20000, seed=1)
     deg = r.degrees()
     assert deg.max() > 20 * np.median(deg)  # skewed
+    for n in (3000, 5_000_000):             # banded: |u - v| <= min(8192, max(16, n / 256))
+        band = min(8192, max(16, n // 256))
+        bg = layout.gen_graph("banded", n, 4 * n if n < 10000 else 200_000, seed=2)
+        rows = np.repeat(np.arange(n), np.diff(bg.rowptr))
+        assert np.abs(rows - bg.col).max() <= band and bg.nnz == 2 * (4 * n if n < 10000 else 200_000) + n
+        t, _ = layout.transpose(bg)
+        np.testing.assert_array_equal(t.col, bg.col)
 
 
 def test_transpose_roundtrip():
