@@ -433,11 +433,19 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
     dY = (torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1)[r0:r0 + n].clone()
     del Xall
     bufs = [be.empty(n, F) for _ in range(4)]
-    cand = {}
+    cand, failed = {}, {}
     for m in modes:
-        st = make_step(m.agg, X, dY, bufs)
-        cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
-        log(f"[rank {rank}] {kind} candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
+        # a layout that raises (on every rank alike: the same code on the same graph) is
+        # skipped and reported; the others are still timed
+        try:
+            st = make_step(m.agg, X, dY, bufs)
+            cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
+            log(f"[rank {rank}] {kind} candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
+        except Exception as e:  # noqa: BLE001
+            failed[m.name] = repr(e)[:300]
+            log(f"[rank {rank}] {kind} candidate {m.name} failed: {failed[m.name]}")
+    if not cand:
+        raise RuntimeError(f"bench.py: every {kind} layout failed: {failed}")
     forced = os.environ.get("GALA_DIST_MODE")
     name = forced if forced in cand else min(cand, key=cand.get)
     best = next(m for m in modes if m.name == name)
@@ -460,6 +468,7 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
                     "spmm_ms_per_aggregation": t_kernel * 1e3,
                     "halo_layout": pt1.halo_mode, "halo_rows_rank0": pt1.n_halo_rows,
                     "vcut_touched_fraction": frac,
+                    "failed_candidates": failed,
                     "note": "halo-exact is bit-identical to one GPU; the other modes agree to fp32 rounding. "
                             "Exchange time is the collective(s) of one aggregation alone; it overlaps the SpMM "
                             "in the -overlap/-pipe modes. vcut-sparse: DCSR partial rows (only rows with a held "
@@ -517,12 +526,19 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         "comm": fam["comm"],
     }
     if not args.no_gat:
-        out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
+        try:
+            out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
+        except Exception as e:  # noqa: BLE001  (reported; the headline line stays)
+            out["gat"] = {"error": repr(e)[:500]}
     del g
     for kind in ("rmat", "banded"):   # the skewed family, and one that shards naturally
         if getattr(args, f"no_{kind}"):
             continue
-        rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+        try:    # a secondary family that fails on every rank is reported; the headline line stays
+            rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+        except Exception as e:  # noqa: BLE001
+            out[kind] = {"error": repr(e)[:500]}
+            continue
         rm.pop("real_data")
         rm["graph"] = (f"{FAMILY_GRAPH[kind]}, N={gr.n_rows}, E={gr.nnz}, "
                        f"max degree {int((gr.rowptr[1:] - gr.rowptr[:-1]).max())}")
@@ -530,7 +546,10 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         out[kind] = rm
         del gr
     if not args.no_weak:
-        out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
+        try:
+            out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
+        except Exception as e:  # noqa: BLE001
+            out["weak"] = {"error": repr(e)[:500]}
     return out
 
 
