@@ -392,6 +392,13 @@ class VcutMode:
         return timer(lambda: self.agg.exchange_only(), 5)
 
 
+def _recoverable(e: Exception) -> bool:
+    """Whether bench.py may go on after `e`: a Python-level failure of one layout yes; a GPU
+    runtime error (a fault leaves the device unusable) or an RCCL error never."""
+    text = repr(e)
+    return not any(k in text for k in ("HIP", "hip", "CUDA", "cuda", "NCCL", "nccl", "RCCL"))
+
+
 def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max):
     """Strong scaling of one Products-shaped graph of family `kind` over the ranks: every
     candidate layout timed for a few steps, the timed steps on the fastest.  Returns
@@ -442,6 +449,8 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
             cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
             log(f"[rank {rank}] {kind} candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
         except Exception as e:  # noqa: BLE001
+            if not _recoverable(e):
+                raise
             failed[m.name] = repr(e)[:300]
             log(f"[rank {rank}] {kind} candidate {m.name} failed: {failed[m.name]}")
     if not cand:
@@ -529,6 +538,8 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         try:
             out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
         except Exception as e:  # noqa: BLE001  (reported; the headline line stays)
+            if not _recoverable(e):
+                raise
             out["gat"] = {"error": repr(e)[:500]}
     del g
     for kind in ("rmat", "banded"):   # the skewed family, and one that shards naturally
@@ -537,6 +548,8 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         try:    # a secondary family that fails on every rank is reported; the headline line stays
             rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
         except Exception as e:  # noqa: BLE001
+            if not _recoverable(e):
+                raise
             out[kind] = {"error": repr(e)[:500]}
             continue
         rm.pop("real_data")
@@ -549,6 +562,8 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         try:
             out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
         except Exception as e:  # noqa: BLE001
+            if not _recoverable(e):
+                raise
             out["weak"] = {"error": repr(e)[:500]}
     return out
 
