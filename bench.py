@@ -831,7 +831,8 @@ def rmat_family(args, dev, be, timer, sync, kind="rmat"):
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
                         "alg_bytes_per_launch": alg,
-                        "traffic": rmat_traffic() if (be.name == "hip" and kind == "rmat") else None,
+                        "traffic": (None if be.name != "hip" else rmat_traffic() if kind == "rmat" else
+                                    load_traffic("banded|void gala::k_spmm_rowgroup<4, 8, 1, 4, false, false, false>")),
                         "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
                                   "grid, then k_spmm_fixup)" if kind == "rmat" else
                                   "gala_spmm_f32 (k_spmm_rowgroup, XCD-ordered row blocks)"}}

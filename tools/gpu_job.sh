@@ -18,6 +18,7 @@
 #   env=NAME=VALUE   export a variable for the following steps
 #   profcmd=TAG,CMD  rocprofv3 --kernel-trace --stats of CMD (commas as spaces; the program
 #                    itself right after --)                  -> gpurun_out/prof_TAG/
+#   pmccmd=TAG,CMD   FETCH_SIZE / WRITE_SIZE passes of CMD  -> gpurun_out/traffic_TAG.json
 #
 # e.g. gpurun --timeout 900 -- 'bash tools/gpu_job.sh tests=gat bench prof'
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -25,7 +26,11 @@ OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export PYTHONPATH="$GRAFT_REPO_ROOT/gala-gnn-acceleration-language_amd${PYTHONPATH:+:$PYTHONPATH}"
-BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline"
+BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-banded"
+# the banded family's SpMM has the uniform one's kernel name: rocprof and PMC runs of
+# bench.py leave it out, so a kernel's average / bytes are the headline graph's (the banded
+# graph's own: pmccmd=banded,python3,<repo>/tools/banded_spmm.py,banded)
+BENCH_PMC_ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-banded"
 
 step() {  # name, limit, command...
     local name=$1 lim=$2
@@ -69,9 +74,9 @@ for s in "$@"; do
             -- python3 "$GRAFT_REPO_ROOT/bench.py" $BENCH_PROF_ARGS > "$OUT/prof_stats.log" 2>&1) || exit 1 ;;
     pmc)
         (cd /tmp && step fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/prof_fetch" -o run \
-            -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_fetch.log" 2>&1) || exit 1
+            -- python3 "$GRAFT_REPO_ROOT/bench.py" $BENCH_PMC_ARGS > "$OUT/prof_fetch.log" 2>&1) || exit 1
         (cd /tmp && step write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/prof_write" -o run \
-            -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_write.log" 2>&1) || exit 1
+            -- python3 "$GRAFT_REPO_ROOT/bench.py" $BENCH_PMC_ARGS > "$OUT/prof_write.log" 2>&1) || exit 1
         python3 tools/pmc_traffic.py "$OUT/prof_fetch" "$OUT/prof_write" "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1 ;;
     profcmd=*)
         # profcmd=TAG,prog,args...: rocprofv3 kernel-trace stats of any command (commas = spaces)
@@ -80,6 +85,18 @@ for s in "$@"; do
         rest="${a#*,}"
         (cd /tmp && step "prof_$tag" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$tag" -o run \
             -- ${rest//,/ } > "$OUT/prof_$tag.log" 2>&1) || { tail -20 "$OUT/prof_$tag.log"; exit 1; } ;;
+    pmccmd=*)
+        # pmccmd=TAG,prog,args...: the FETCH_SIZE and WRITE_SIZE passes (one --pmc run each) of
+        # any command, then tools/pmc_traffic.py           -> gpurun_out/traffic_TAG.json
+        a="${s#pmccmd=}"
+        tag="${a%%,*}"
+        rest="${a#*,}"
+        (cd /tmp && step "fetch_$tag" 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+            -d "$OUT/pmc_${tag}_fetch" -o run -- ${rest//,/ } > "$OUT/pmc_${tag}_fetch.log" 2>&1) || exit 1
+        (cd /tmp && step "write_$tag" 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+            -d "$OUT/pmc_${tag}_write" -o run -- ${rest//,/ } > "$OUT/pmc_${tag}_write.log" 2>&1) || exit 1
+        python3 tools/pmc_traffic.py "$OUT/pmc_${tag}_fetch" "$OUT/pmc_${tag}_write" "$OUT/traffic_$tag.json" \
+            > "$OUT/traffic_$tag.log" 2>&1 ;;
     env=*)
         # env=NAME=VALUE: exported for the steps after it
         export "${s#env=}" ;;
