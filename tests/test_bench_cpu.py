@@ -72,7 +72,7 @@ def test_bench_self_launches_ranks():
 
 def test_bench_single_rank_line():
     r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--scale", "0.002", "--steps", "2",
-                        "--warmup", "1", "--no-cpu-baseline"],
+                        "--warmup", "1", "--no-cpu-baseline", "--banded"],
                        capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     (d,) = _json_lines(r.stdout)
