@@ -1,12 +1,16 @@
 """CPU: gala.dist_run, the multi-rank runtime of galac programs (BASELINE config 5's
 GCN-3 across GPUs), on the host-CPU backend over gloo.
 
-* world 1: the first forward equals the float64 executor of the program's IR
-  (tests/_ir_ref.py) on the runner's own graph, features and weights;
+* world 1: the first forward, the loss and the first epoch's weight gradients equal the
+  float64 executor of the program's IR (tests/_ir_ref.py, tests/_dist_check.py) on the
+  runner's own graph, features and weights -- GCN-3, GIN, GAT (1 and 4 heads), the sparse
+  rewrite, graph and kernel sampling (static and dynamic), a directed program on a
+  directed npy graph and a Matrix Market graph, on both layouts where they apply;
 * world 2 and 3 under torch.distributed.run: the first forward's predictions (gathered)
-  are the one-rank predictions -- the aggregations are exact-mode halo SpMMs, bit-identical
-  per row -- and the loss curve over the epochs agrees within fp32 rounding (the ranks'
-  loss shares and gradients are summed in a different order).
+  are the one-rank predictions -- the row partition's aggregations are exact-mode halo
+  SpMMs, bit-identical per row; the vertex cut agrees within fp32 rounding -- and the loss
+  curve over the epochs agrees within fp32 rounding (the ranks' loss shares and gradients
+  are summed in a different order).
 """
 import json
 import os
