@@ -570,12 +570,15 @@ def run_multi(args, rank, world, dev, be, timer, sync):
 
 def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max):
     """The "gat" field at N > 1: the same 8-head GAT layer as at N = 1 (forward + backward,
-    REF, the source logit formed from X), strong-scaled over the one graph.  Two layouts are
+    REF, the source logit formed from X), strong-scaled over the one graph.  The layouts are
     timed for a few steps and the faster runs the timed steps:
       halo   the row partition gathers the X rows its edges read (then the source logits,
              and dY in the backward) and runs the one-GPU statistics kernels over its rows
              (gala/dist.py HaloGat): bit-identical to one GPU, F + H (forward) and F
              (backward) floats per halo row;
+      halo-overlap  the same exchange, the own-column edges' partial statistics run while
+             it is in flight and the halo columns' after it (gala/dist.py HaloGatOverlap;
+             fp32 rounding of one GPU, each row's sums regrouped);
       vcut   north_star's vertex cut (gala/vertex_cut.py VertexCutGat): the row-statistics
              forward and the backward's partial aggregation over the edges whose source a
              rank owns, 2F + 2H (forward) and F (backward) partial floats per row
@@ -591,6 +594,8 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     layers = {}
     hpart = gdist.partition_graph(g, rank, world, bounds=bounds)
     layers["halo"] = gdist.HaloGat(hpart, F, H, be, comm)
+    if world > 1:
+        layers["halo-overlap"] = gdist.HaloGatOverlap(hpart, F, H, be, comm)
     vpart = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
     layers["vcut"] = vc.VertexCutGat(vpart, F, H, be, comm)
     X = layers["halo"].own_rows("X")              # the layer input, written into the table
@@ -609,12 +614,15 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     t_step = timed_steps(step_of(layers[best]), steps, 2, sync, barrier, reduce_max)
     comm_bytes = {"halo": hpart.halo_bytes(2 * F + H) if world > 1 else 0,
                   "vcut": vpart.comm_bytes(2 * F + 2 * H) + vpart.comm_bytes(F)}
+    comm_bytes["halo-overlap"] = comm_bytes["halo"]
+    desc = {"halo": "row partition, gathered X / logits / dY rows, the one-GPU kernels (bit-identical)",
+            "halo-overlap": "row partition, gathered X / logits / dY rows; own-column partial statistics "
+                            "overlap the exchange (fp32 rounding of one GPU)",
+            "vcut": f"vertex cut, row-statistics partials reduce-scattered to the row owners in {PIPE_CHUNKS} "
+                    f"overlapped row blocks"}
     out = {"value": 2 * g.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
            "layer": f"GAT {H} heads x {GAT_HEAD_F} (F={F}), REF softmax; forward + backward",
-           "layout": f"{best} x{world}: " + ("row partition, gathered X / logits / dY rows, the one-GPU kernels "
-                                             "(bit-identical)" if best == "halo" else
-                                             f"vertex cut, row-statistics partials reduce-scattered to the row "
-                                             f"owners in {PIPE_CHUNKS} overlapped row blocks"),
+           "layout": f"{best} x{world}: " + desc[best],
            "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
            "comm_bytes_per_step_per_rank": comm_bytes[best],
            "comm_bytes_per_step_per_rank_candidates": comm_bytes}

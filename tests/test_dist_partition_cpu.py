@@ -486,7 +486,7 @@ def test_auto_halo_mode_is_one_choice_for_all_ranks():
 
 
 # ---- halo GAT: the one-GPU statistics kernels over a gathered table ----------------------------
-def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q):
+def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q, cls="HaloGat"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -495,7 +495,7 @@ def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q):
         dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
         pt = gdist.partition_graph(g, rank, world, halo_mode=halo_mode)
         own = slice(pt.r0, pt.r0 + pt.n)
-        gat = gdist.HaloGat(pt, F_GAT, H_GAT, CpuBackend(), Comm())
+        gat = getattr(gdist, cls)(pt, F_GAT, H_GAT, CpuBackend(), Comm())
         t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
         grads = []
         if rc:
@@ -553,3 +553,26 @@ def test_halo_gat_bit_identical_to_one_process(world, name, rc, halo_mode):
             np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
     else:
         np.testing.assert_array_equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("world,name,rc,halo_mode", [(2, "powerlaw", False, "p2p"), (3, "cora", True, "dense"),
+                                                     (3, "banded", True, "p2p"), (2, "empty_rows", False, "dense")])
+def test_halo_gat_overlap_matches_one_process(world, name, rc, halo_mode):
+    """HaloGatOverlap (gala/dist.py): the own-column partial statistics overlap the exchange and
+    the halo columns' partials are added after it -- each row's sums regrouped, so Y, dX and
+    d_aL agree with the one-process pair to fp32 rounding (not bit for bit)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_gat_worker, args=(r, world, port, name, rc, halo_mode, q, "HaloGatOverlap"))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _gat_train_one_process(GRAPHS[name](), rc)
+    for a, b in zip(got, ref):
+        assert np.isfinite(a).all()
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(b).max())))

@@ -505,3 +505,41 @@ def test_halo_gat_bit_identical_to_one_gpu(world, halo, kind, heads, F):
             Yc = hg.forward_train(cu(aL), None, cu(X), wR, bR)
             dXc, daLc = hg.backward(cu(dY), linear=False)
             assert torch.equal(Yc, Y1) and torch.equal(dXc, dX1) and torch.equal(daLc.reshape(-1), daL1)
+
+
+@pytest.mark.parametrize("world,halo", [(1, "p2p"), (2, "dense"), (3, "p2p"), (4, "dense")])
+@pytest.mark.parametrize("kind,heads,F", [("uniform", 8, 256), ("rmat", 1, 32), ("rmat", 4, 64)])
+def test_halo_gat_overlap_matches_one_gpu(world, halo, kind, heads, F):
+    """HaloGatOverlap, ranks simulated in-process (comm None; the tables pre-filled with the
+    rows the exchange would deliver): own-column partial statistics, then the halo
+    columns', normalised by the sum -- Y, dX, d_aL within fp32 rounding of the one-GPU pair
+    (each row's sums regrouped), the own logits written bit for bit."""
+    from gala import layout
+    from gala.backend import HipBackend
+    g = layout.gen_graph(kind, 5000, 50000, seed=12)
+    rng = np.random.default_rng(9)
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    aL = cu(rng.uniform(-1, 1, (g.n_rows, heads)).astype(np.float32))
+    X = cu(rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32))
+    dY = cu(rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32))
+    wR = cu(rng.uniform(-0.5, 0.5, F).astype(np.float32))
+    bR = cu(rng.uniform(-0.5, 0.5, heads).astype(np.float32))
+    dg = ops.DeviceGraph.from_host(g)
+    Y1, q1, Ym1, sma1, aR1 = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=heads, want_aR=True)
+    dX1, daL1 = ops.gat_bwd_stats(dg, aL, aR1, dY, q1, Y1, Ym1, sma1, heads=heads)
+    A1 = aR1.view(-1, heads)
+    for p in range(world):
+        pt = gdist.partition_graph(g, p, world, halo_mode=halo)
+        own = slice(pt.r0, pt.r0 + pt.n)
+        x2g = torch.from_numpy(np.maximum(pt.xs_to_global(), 0)).cuda()
+        hg = gdist.HaloGatOverlap(pt, F, heads, HipBackend("cuda"), None)
+        hg.Xs.copy_(X[x2g])
+        hg.dYs.copy_(dY[x2g])
+        hg.As.copy_(A1[x2g])
+        hg.As[hg.x0:hg.x0 + pt.n] = float("nan")          # the forward writes the own block
+        Y = hg.forward_train(aL[own], None, X[own], wR, bR)
+        assert torch.equal(hg.As[hg.x0:hg.x0 + pt.n], A1[own])
+        dX, daL = hg.backward(dY[own], linear=False)
+        torch.testing.assert_close(Y, Y1[own], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(dX, dX1[own], rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(daL.reshape(-1), daL1.view(-1, heads)[own].reshape(-1), rtol=1e-4, atol=1e-4)
