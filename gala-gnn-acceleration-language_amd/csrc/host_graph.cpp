@@ -428,6 +428,7 @@ extern "C" int gala_host_mtx_read(const char *path, int32_t *rows, int32_t *cols
         if (vals) vals[index] = v;
         ++index;
         if (h.symmetry && r != c) {  // the mirror, same value (mtx_io.h:435-445)
+            if (c > h.n_rows || r > h.n_cols) return GALA_ERR_GRAPH;  // a non-square "symmetric" file
             rows[index] = (int32_t)(c - 1);
             cols[index] = (int32_t)(r - 1);
             if (vals) vals[index] = v;
