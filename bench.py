@@ -594,8 +594,7 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     layers = {}
     hpart = gdist.partition_graph(g, rank, world, bounds=bounds)
     layers["halo"] = gdist.HaloGat(hpart, F, H, be, comm)
-    if world > 1:
-        layers["halo-overlap"] = gdist.HaloGatOverlap(hpart, F, H, be, comm)
+    layers["halo-overlap"] = gdist.HaloGatOverlap(hpart, F, H, be, comm)
     vpart = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
     layers["vcut"] = vc.VertexCutGat(vpart, F, H, be, comm)
     X = layers["halo"].own_rows("X")              # the layer input, written into the table
