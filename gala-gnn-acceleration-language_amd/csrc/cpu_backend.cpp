@@ -813,6 +813,66 @@ extern "C" int gala_cpu_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const 
                              nullptr, true, self_col);
 }
 
+// gala_gat_fwd_continue_f32 (gala_hip.h): every row's sums start at the partials of an
+// earlier pass over other columns (which may alias the outputs), then take this pattern's
+// edges in CSR order; Ym NULL: the plain REF forward
+extern "C" int gala_cpu_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                             const float *wR, const float *bR, const float *X, int64_t ldx,
+                                             int32_t F, int32_t heads, float slope, const float *U0,
+                                             int64_t ldu0, const float *S0, const float *Um0, int64_t ldum0,
+                                             const float *M0, float *Y, int64_t ldy, float *q_out, float *Ym,
+                                             int64_t ldym, float *sma, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    const bool stats = Ym != nullptr;
+    if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldu0 < F) return GALA_ERR_INVALID_ARG;
+    if ((Um0 != nullptr) != stats || (stats && (ldym < F || ldum0 < F || !M0 || !sma || !q_out)))
+        return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!aL || (!aR && !wR) || !Y || !U0 || !S0 || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
+    std::vector<float> rc;
+    if (!aR) {
+        rc = attn_logits_heads(A, wR, bR, X, ldx, F, heads);
+        aR = rc.data();
+    }
+    const int32_t H = heads, D = F / H, S = A->n_seg;
+#pragma omp parallel
+    {
+        std::vector<float> acc((size_t)D), accm((size_t)D);
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t r = 0; r < A->n_rows; ++r)
+            for (int32_t h = 0; h < H; ++h) {
+                std::copy(U0 + r * ldu0 + h * D, U0 + r * ldu0 + (h + 1) * D, acc.begin());
+                if (stats) std::copy(Um0 + r * ldum0 + h * D, Um0 + r * ldum0 + (h + 1) * D, accm.begin());
+                float sum = S0[r * H + h], sm = stats ? M0[r * H + h] : 0.0f;
+                for (int32_t s = 0; s < S; ++s) {
+                    int64_t e0, e1;
+                    row_range(A, s, r, e0, e1);
+                    for (int64_t e = e0; e < e1; ++e) {
+                        const float t = aL[r * H + h] + aR[(int64_t)A->col[e] * H + h];
+                        const bool pos = t > 0.0f;
+                        const float pe = ref_exp(pos ? t : t * slope);
+                        const float mp = pos ? pe : pe * slope;
+                        sum = sum + pe;
+                        sm = sm + mp;
+                        const float *xr = X + (int64_t)A->col[e] * ldx + h * D;
+                        for (int32_t f = 0; f < D; ++f) {
+                            acc[f] = fmaf(pe, xr[f], acc[f]);
+                            if (stats) accm[f] = fmaf(mp, xr[f], accm[f]);
+                        }
+                    }
+                }
+                const float q = 1.0f / (sum + (float)S * 1e-12f);
+                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = acc[f] * q;
+                if (stats)
+                    for (int32_t f = 0; f < D; ++f) Ym[r * ldym + h * D + f] = accm[f] * q;
+                if (q_out) q_out[r * H + h] = q;
+                if (stats) sma[r * H + h] = sm * q;
+            }
+    }
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_gat_fwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR,
                                              const float *wR, const float *bR, const float *X, int64_t ldx,
                                              int32_t F, int32_t heads, float slope, float *Y, int64_t ldy,

@@ -260,6 +260,37 @@ __device__ __forceinline__ void gat_fwd_edges(const EdgeParams &p, const GatDev 
         gat_fwd_range<G, VEC, U, MODE, CH, RC>(p, d, gl_, park, e0, e1, st);
 }
 
+// A continuation's starting state (d.init_acc set, REF): the row's partials of the earlier pass.
+template <int G, int VEC, int CH, bool RC, int MODE>
+__device__ __forceinline__ void gat_fwd_init(const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_, int64_t row,
+                                             FwdState<VEC, CH> &st) {
+    typedef typename GVec<VEC>::T V;
+    if (!d.init_acc) return;
+    auto load = [&](const float *base, int64_t ld, float (&dst)[CH][VEC]) {
+#pragma unroll
+        for (int ch = 0; ch < CH; ++ch) {
+            if (!gl_.ln.valid[ch]) continue;
+            const float *src = base + row * ld + gl_.ln.off[ch];
+            if (gl_.ln.nv[ch] == VEC) {
+                const V v = *reinterpret_cast<const V *>(src);
+                const float *vv = reinterpret_cast<const float *>(&v);
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) dst[ch][i] = vv[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < VEC; ++i)
+                    if (gl_.ln.in(ch, i)) dst[ch][i] = src[i];
+            }
+        }
+    };
+    load(d.init_acc, d.ld_init, st.acc);
+    if (gl_.cv) st.sum = d.init_sum[row * gl_.H + gl_.hh];
+    if constexpr (MODE == kRefStats) {
+        load(d.init_accm, d.ld_initm, st.accm);
+        if (gl_.cv) st.sma = d.init_sma[row * gl_.H + gl_.hh];
+    }
+}
+
 // Y[row] = acc * q with q = 1 / (sum [+ S * 1e-12 in REF mode]); returns q.  Partial
 // (GALA_GAT_PARTIAL, REF): Y = acc unnormalised and the raw sum is returned, for a caller
 // that adds the partial rows of several column ranges first (vertex cut).
@@ -358,6 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd(EdgeParams p, GatDev d, int3
     // place: a contiguous re-read of the row instead of a second col -> aR gather.
     const bool park = d.alpha_out != nullptr && (G % H) == 0;
     FwdState<VEC, CH> st;
+    if constexpr (ref_mode(MODE)) gat_fwd_init<G, VEC, CH, RC, MODE>(d, gl_, row, st);
     if constexpr (kArOut) st.self_row = own;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
@@ -449,6 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_gat_fwd_fixup(EdgeParams p, GatDev d
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     const int F = d.F, H = gl_.H, hh = gl_.hh;
     FwdState<VEC, CH> st;
+    if constexpr (ref_mode(MODE)) gat_fwd_init<G, VEC, CH, RC, MODE>(d, gl_, row, st);
     const int64_t c0 = sp.row_chunk0[ri], c1 = sp.row_chunk0[ri + 1];
     for (int64_t cc = c0; cc < c1; ++cc) {
         const float *w = sp.ws + cc * sp.ws_cols;
@@ -811,7 +844,10 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
                         const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
                         float slope, int32_t mode, float *Y, int64_t ldy, float *alpha_out,
                         float *q_out, void *stream, float *ym = nullptr, int64_t ldym = 0,
-                        float *sma = nullptr, float *ar_out = nullptr, const int32_t *self_col = nullptr) {
+                        float *sma = nullptr, float *ar_out = nullptr, const int32_t *self_col = nullptr,
+                        const float *init_acc = nullptr, int64_t ld_init = 0, const float *init_sum = nullptr,
+                        const float *init_accm = nullptr, int64_t ld_initm = 0,
+                        const float *init_sma = nullptr) {
     GatArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
@@ -830,15 +866,22 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     // square pattern (the backward's dY[col] / aR_out of the row's own X) unless self_col
     // maps each row to its own column (a halo table); a vertex cut's partial forward reads
     // X by column only
-    if (stats && !partial && !self_col && A->n_cols > A->n_rows && A->nnz > 0) return GALA_ERR_INVALID_ARG;
+    if (stats && !partial && !self_col && !init_acc && A->n_cols > A->n_rows && A->nnz > 0)
+        return GALA_ERR_INVALID_ARG;
     if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
+    // a continuation: REF, normalised, no alpha; the statistics need their two partials too
+    if (init_acc && (mode != GALA_SOFTMAX_REF || partial || alpha_out || ar_out || !init_sum || ld_init < F ||
+                     (stats && (!init_accm || !init_sma || ld_initm < F)) || (!stats && (init_accm || init_sma))))
+        return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
     // VEC divides D, or (one head) fits padded rows: ldx, ldy >= F rounded up to VEC
     auto vec_ok = [&](int v) {
         const bool fits = D % v == 0 || (heads == 1 && ldx >= pad_to(F, v) && ldy >= pad_to(F, v) &&
                                          (!stats || ldym >= pad_to(F, v)));
         return fits && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
-               ((uintptr_t)Y % (4 * v)) == 0 && (!stats || (ldym % v == 0 && ((uintptr_t)ym % (4 * v)) == 0));
+               ((uintptr_t)Y % (4 * v)) == 0 && (!stats || (ldym % v == 0 && ((uintptr_t)ym % (4 * v)) == 0)) &&
+               (!init_acc || (ld_init % v == 0 && ((uintptr_t)init_acc % (4 * v)) == 0)) &&
+               (!init_accm || (ld_initm % v == 0 && ((uintptr_t)init_accm % (4 * v)) == 0));
     };
     int vec = 4;
     while (vec > 1 && !vec_ok(vec)) vec >>= 1;
@@ -854,6 +897,8 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     a.d.slope = slope, a.d.Y = Y, a.d.ldy = ldy, a.d.alpha_out = alpha_out, a.d.q_out = q_out;
     a.d.partial = partial ? 1 : 0;
     a.d.ym_out = ym, a.d.ldym = ldym, a.d.sma_out = sma, a.d.ar_out = ar_out, a.d.self_col = self_col;
+    a.d.init_acc = init_acc, a.d.ld_init = ld_init, a.d.init_sum = init_sum;
+    a.d.init_accm = init_accm, a.d.ld_initm = ld_initm, a.d.init_sma = init_sma;
     a.hs = (hipStream_t)stream;
     // hub-row chunk partials: {acc[F], m[H], sum[H]} (+ {accm[F], sma[H]} with the statistics)
     const int64_t ws_need = stats ? 2 * (int64_t)F + 3 * heads : (int64_t)F + 2 * heads;
@@ -942,6 +987,23 @@ extern "C" int gala_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const floa
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
                         GALA_SOFTMAX_REF | GALA_GAT_PARTIAL, U, ldu, nullptr, sums, stream, Um, ldum, msums,
                         aR_out, self_col);
+}
+
+// The REF forward continued from an earlier pass's partials over other columns (a row
+// partition's own columns while the halo is in flight): Y = q (U0 + sum p X) with
+// q = 1 / (S0 + sum p + 1e-12); with Ym the row statistics likewise from (Um0, M0).
+extern "C" int gala_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                         const float *wR, const float *bR, const float *X, int64_t ldx,
+                                         int32_t F, int32_t heads, float slope, const float *U0, int64_t ldu0,
+                                         const float *S0, const float *Um0, int64_t ldum0, const float *M0,
+                                         float *Y, int64_t ldy, float *q_out, float *Ym, int64_t ldym,
+                                         float *sma, void *stream) {
+    if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if ((!U0 || !S0) && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    if ((Ym != nullptr) != (Um0 != nullptr)) return GALA_ERR_INVALID_ARG;
+    return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
+                        GALA_SOFTMAX_REF, Y, ldy, nullptr, q_out, stream, Ym, ldym, sma, nullptr, nullptr, U0,
+                        ldu0, S0, Um0, ldum0, M0);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

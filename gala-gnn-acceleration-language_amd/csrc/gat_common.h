@@ -100,6 +100,12 @@ struct GatDev {
     const float *dy_rows;              // backward, nullable: the rows' own dY (row r at dy_rows + r*lddy)
                                        // when dY is a gathered table whose row r is not column r
     int64_t ldym;
+    // forward continuation (gala_gat_fwd_continue_f32, REF): each row's state starts from the
+    // unnormalised partials {sum p X, sum p[, sum m p X, sum m p]} of an earlier pass over
+    // other columns; they may alias Y, q_out, Ym and sma (each lane reads its own elements
+    // before it writes them)
+    const float *init_acc, *init_sum, *init_accm, *init_sma;
+    int64_t ld_init, ld_initm;
 };
 
 // Internal forward MODE: REF softmax that also accumulates the row statistics.

@@ -623,13 +623,13 @@ class HaloGatOverlap(HaloGat):
     """HaloGat with the halo exchange hidden behind the own-column edges.  The forward runs
     the unnormalised row statistics of the edges into the rank's own columns
     (gala_gat_fwd_partial_stats_ex_f32 over part.groups[0], which also writes the own
-    vertices' logits) while the X rows are in flight, then those of the halo columns, and
-    normalises the two partial sums as the vertex cut's owner does (q = 1 / (S + 1e-12),
-    Y = q U, Ym = q Um, sma = q M; GAT REF subtracts no row maximum, common.h:760-773, so
-    the partials simply add).  The backward likewise: sum_e p_e dY[c] over the own columns
-    and the row-local d_aL overlap the dY exchange, the halo columns follow, dX = q (P0 + P1).
-    The exchange and the bytes are HaloGat's; each row's sum is regrouped (own columns, then
-    halo columns), so results agree with one GPU to fp32 rounding, not bit for bit."""
+    vertices' logits) while the X rows are in flight, then continues every row from those
+    partials over the halo columns and normalises (gala_gat_fwd_continue_f32, in place; GAT
+    REF subtracts no row maximum, common.h:760-773, so the partial sums simply add).  The
+    backward likewise: sum_e p_e dY[c] over the own columns and the row-local d_aL overlap
+    the dY exchange, the halo columns continue it, dX = q (P_own + P_halo).  The exchange
+    and the bytes are HaloGat's; each row's sums are grouped per column range, so results
+    agree with one GPU to fp32 rounding, not bit for bit."""
 
     def __init__(self, part: GraphPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
         super().__init__(part, F, heads, backend, comm, slope)
@@ -639,22 +639,10 @@ class HaloGatOverlap(HaloGat):
         n = part.n
         self.own_graph = backend.graph(layout.HostGraph(n, n, np.zeros(n + 1, np.int32), np.zeros(0, np.int32)),
                                        split=False)
-        self.bufs = None
-
-    def _buffers(self):
-        if self.bufs is None:
-            n, F, H, be = self.part.n, self.F, self.H, self.be
-            self.bufs = {k: be.empty(n, w) for k, w in (("U0", F), ("Um0", F), ("U1", F), ("Um1", F), ("S0", H),
-                                                          ("M0", H), ("S1", H), ("M1", H), ("P0", F), ("P1", F),
-                                                          ("Ssc", H))}
-        return self.bufs
-
-    def _scale(self, q, T):
-        n, H = q.shape
-        return (T.reshape(n, H, self.F // H) * q.view(n, H, 1)).reshape(n, self.F)
+        self.Ssc = backend.empty(n, heads)
 
     def forward_train(self, aL, aR, X, wR=None, bR=None):
-        n, H, b = self.part.n, self.H, self._buffers()
+        n, H, F, be = self.part.n, self.H, self.F, self.be
         if self.saved is not None:
             self._wait(self.saved[-1])
         works = self._gather(self.Xs, X)
@@ -664,17 +652,13 @@ class HaloGatOverlap(HaloGat):
         else:
             kw = {"wR": wR, "bR": bR}
         At = self.As if aR is not None else None
-        self.be.gat_partial_stats(self.groups[0], aL, At, self.Xs, H, self.slope, b["U0"], b["S0"], b["Um0"],
-                                  b["M0"], self_col=None if aR is not None else self.self_col,
-                                  aR_out=None if aR is not None else self.As, **kw)
+        Y, Ym, q, sma = be.empty(n, F), be.empty(n, F), be.empty(n, H), be.empty(n, H)
+        be.gat_partial_stats(self.groups[0], aL, At, self.Xs, H, self.slope, Y, q, Ym, sma,
+                             self_col=None if aR is not None else self.self_col,
+                             aR_out=None if aR is not None else self.As, **kw)
         self._wait(works)
-        self.be.gat_partial_stats(self.groups[1], aL, At, self.Xs, H, self.slope, b["U1"], b["S1"], b["Um1"],
-                                  b["M1"], **kw)
+        be.gat_continue(self.groups[1], aL, At, self.Xs, H, self.slope, Y, q, Ym, sma, **kw)
         ar_works = self._gather(self.As, None) if aR is None else []
-        q = 1.0 / (b["S0"] + b["S1"] + 1e-12)
-        Y = self._scale(q, b["U0"] + b["U1"])
-        Ym = self._scale(q, b["Um0"] + b["Um1"])
-        sma = (b["M0"] + b["M1"]) * q
         self.saved = (aL, q, Y, Ym, sma, wR, ar_works)
         return Y
 
@@ -682,19 +666,19 @@ class HaloGatOverlap(HaloGat):
         if self.saved is None:
             raise RuntimeError("HaloGatOverlap.backward: no forward_train to take the row statistics from")
         aL, q, Y, Ym, sma, wR, ar_works = self.saved
-        n, H, b = self.part.n, self.H, self._buffers()
+        n, H, be = self.part.n, self.H, self.be
         works = self._gather(self.dYs, dY)
         # the own columns' logits were written by this rank's forward; the halo's may still be in flight
-        self.be.gat_partial(self.groups[0], aL, self.As, self.dYs, H, self.slope, b["P0"], b["Ssc"])
-        _, d_aL = self.be.gat_bwd_stats(self.own_graph, aL, self.As[self.x0:self.x0 + n], self.own_rows("dY"), q, Y,
-                                        Ym, sma, H, self.slope)
+        dX = be.empty(n, self.F)
+        be.gat_partial(self.groups[0], aL, self.As, self.dYs, H, self.slope, dX, self.Ssc)
+        _, d_aL = be.gat_bwd_stats(self.own_graph, aL, self.As[self.x0:self.x0 + n], self.own_rows("dY"), q, Y, Ym,
+                                   sma, H, self.slope)
         self._wait(ar_works)
         self._wait(works)
-        self.be.gat_partial(self.groups[1], aL, self.As, self.dYs, H, self.slope, b["P1"], b["Ssc"])
-        dX = self._scale(q, b["P0"] + b["P1"])
+        be.gat_continue(self.groups[1], aL, self.As, self.dYs, H, self.slope, dX, self.Ssc)
         d_aL = d_aL.view(n, H)
         if not (linear and wR is not None):
             return dX, d_aL
-        dW, db = self.be.head_linear_grads(self.own_rows("X"), d_aL, H)
-        self.be.head_attn_bwd(d_aL, wR, H, dX)
+        dW, db = be.head_linear_grads(self.own_rows("X"), d_aL, H)
+        be.head_attn_bwd(d_aL, wR, H, dX)
         return dX, d_aL, dW, db

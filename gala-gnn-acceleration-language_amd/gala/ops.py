@@ -396,6 +396,25 @@ def gat_fwd_partial_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, head
     return U, sums, Um, msums
 
 
+def gat_fwd_continue(g: DeviceGraph, aL, X, U0, S0, aR=None, wR=None, bR=None, heads=1, slope=0.2, Um0=None,
+                     M0=None, Y=None, q=None, Ym=None, sma=None):
+    """gala_gat_fwd_continue_f32: the REF forward (Um0 None) or the row-statistics forward of
+    rows whose first column range already gave the partials (U0, S0[, Um0, M0]); the outputs
+    default to those buffers (in place).  Returns (Y, q) or (Y, q, Ym, sma)."""
+    F = X.shape[1]
+    Y = U0 if Y is None else Y
+    q = S0 if q is None else q
+    if Um0 is not None:
+        Ym = Um0 if Ym is None else Ym
+        sma = M0 if sma is None else sma
+    w = (F + 3) // 4 * 4
+    _abi.call("gala_gat_fwd_continue_f32", g.csr(2 * w + 3 * heads if Um0 is not None else w + 2 * heads),
+              _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(U0), U0.stride(0),
+              _dp(S0), _dp(Um0), Um0.stride(0) if Um0 is not None else 0, _dp(M0), _dp(Y), Y.stride(0), _dp(q),
+              _dp(Ym), Ym.stride(0) if Ym is not None else 0, _dp(sma), _stream())
+    return (Y, q) if Um0 is None else (Y, q, Ym, sma)
+
+
 def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None, dY_rows=None):
     """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
     dY[col] only (alpha from aR, or from the forward's p when given).  dY_rows: dY is a

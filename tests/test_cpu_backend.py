@@ -417,3 +417,48 @@ def test_partial_stats_own_vertex_logits():
                       wR.data_ptr(), bR.data_ptr(), X[own].contiguous().data_ptr(), F, F, H, 0.2,
                       torch.empty(n0, F).data_ptr(), F, torch.empty(n0 * H).data_ptr(), torch.empty(n0, F).data_ptr(),
                       F, torch.empty(n0 * H).data_ptr(), None, torch.empty(pt.n * H).data_ptr(), None)
+
+
+def _split_by_column(g, keep):
+    """The edges of g whose column satisfies keep(col), as a CSR over the same rows / columns."""
+    sel = keep(g.col)
+    rp = np.concatenate([[0], np.cumsum(sel)])[g.rowptr].astype(np.int32)
+    return layout.HostGraph(g.n_rows, g.n_cols, rp, g.col[sel].astype(np.int32))
+
+
+@pytest.mark.parametrize("rc", [False, True])
+@pytest.mark.parametrize("which", ["powerlaw", "empty_rows"])
+def test_gat_continue_matches_one_pass(rc, which):
+    """gala_cpu_gat_fwd_continue_f32: partials over the even columns, then the odd columns
+    continued from them in place, equal the one-pass statistics forward (Y, q, Ym, sma) and
+    the plain REF forward to fp32 rounding; a half-given statistics pair is refused."""
+    import torch
+    from gala.backend import CpuBackend
+    g = powerlaw(n=1500, m=9000) if which == "powerlaw" else with_empty_rows()
+    H, F = 2, 16
+    rng = np.random.default_rng(5)
+    t = lambda a: torch.from_numpy(a.astype(np.float32))  # noqa: E731
+    X, aL = t(rng.uniform(-1, 1, (g.n_rows, F))), t(rng.uniform(-1, 1, (g.n_rows, H)))
+    wR, bR = t(rng.uniform(-0.5, 0.5, F)), t(rng.uniform(-0.5, 0.5, H))
+    be = CpuBackend()
+    aR = None if rc else be.head_attn(X, wR, bR, H)
+    kw = {"wR": wR, "bR": bR} if rc else {}
+    full = be.graph(g)
+    want = be.gat_stats_table(full, aL, aR, X, H, 0.2, None, None, **kw)
+    g0, g1 = (be.graph(_split_by_column(g, f)) for f in (lambda c: c % 2 == 0, lambda c: c % 2 == 1))
+    U, Um, S, M = torch.empty((g.n_rows, F)), torch.empty((g.n_rows, F)), torch.empty(g.n_rows * H), \
+        torch.empty(g.n_rows * H)
+    be.gat_partial_stats(g0, aL, aR, X, H, 0.2, U, S, Um, M, **kw)
+    got = be.gat_continue(g1, aL, aR, X, H, 0.2, U, S, Um, M, **kw)
+    for a, b in zip(got, want):
+        np.testing.assert_allclose(a.numpy().reshape(-1), b.numpy().reshape(-1), rtol=2e-5, atol=1e-6)
+    Ar = aR if aR is not None else be.head_attn(X, wR, bR, H)
+    Y, s = torch.empty((g.n_rows, F)), torch.empty(g.n_rows * H)
+    be.gat_partial(g0, aL, Ar, X, H, 0.2, Y, s)
+    Y, q = be.gat_continue(g1, aL, Ar, X, H, 0.2, Y, s)
+    np.testing.assert_allclose(Y.numpy(), want[0].numpy(), rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(q.numpy(), want[1].numpy().reshape(-1), rtol=2e-5, atol=0)
+    with pytest.raises(_abi.GalaError):
+        _abi.call_cpu("gala_gat_fwd_continue_f32", g1.csr(), aL.data_ptr(), Ar.data_ptr(), None, None,
+                      X.data_ptr(), F, F, H, 0.2, U.data_ptr(), F, S.data_ptr(), None, 0, None, U.data_ptr(), F,
+                      S.data_ptr(), Um.data_ptr(), F, M.data_ptr(), None)

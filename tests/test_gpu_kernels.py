@@ -986,3 +986,44 @@ def test_gat_row_stats_aR_from_self_loop(F, heads, split):
         assert torch.equal(dX, dX0)
         aRs.append(aRo)
     assert torch.equal(aRs[0], aRs[1])
+
+
+def _split_by_column(g, keep):
+    sel = keep(g.col)
+    rp = np.concatenate([[0], np.cumsum(sel)])[g.rowptr].astype(np.int32)
+    return layout.HostGraph(g.n_rows, g.n_cols, rp, g.col[sel].astype(np.int32))
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4)])
+@pytest.mark.parametrize("rc", [False, True])
+def test_gat_continue_matches_one_pass(F, heads, rc):
+    """gala_gat_fwd_continue_f32: the even columns' partials (gala_gat_fwd_partial_stats_f32 /
+    GALA_GAT_PARTIAL), then the odd columns continued from them in place -- hub rows cut into
+    chunks on both halves (threshold 64, 32-edge chunks: the fixup starts from the partials)
+    -- equal the one-pass statistics forward and the plain REF forward to fp32 rounding."""
+    g = powerlaw()
+    aL = dev(features(g.n_rows, heads, seed=71))
+    X = dev(features(g.n_cols, F, seed=73))
+    wR = dev(features(1, F, seed=74).ravel() * 0.5)
+    bR = dev(features(1, heads, seed=75).ravel())
+    aR = None if rc else ops.head_attn(X, wR, bR, heads=heads)
+    kw = {"wR": wR, "bR": bR} if rc else {}
+    dg = ops.DeviceGraph.from_host(g)
+    want = ops.gat_fwd_stats(dg, aL, X, aR=aR, heads=heads, **kw)[:4]
+    halves = []
+    for keep in (lambda c: c % 2 == 0, lambda c: c % 2 == 1):
+        h = _split_by_column(g, keep)
+        d = ops.DeviceGraph.from_host(h, split=False)
+        d.set_split_plan(h.rowptr, 64, chunk=32, row_order=True)
+        assert d.split_rows > 5
+        halves.append(d)
+    U, S, Um, M = ops.gat_fwd_partial_stats(halves[0], aL, X, aR=aR, heads=heads, **kw)
+    got = ops.gat_fwd_continue(halves[1], aL, X, U, S, aR=aR, heads=heads, Um0=Um, M0=M, **kw)
+    assert got[0].data_ptr() == U.data_ptr() and got[3].data_ptr() == M.data_ptr()   # in place
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a.reshape(-1), b.reshape(-1), rtol=2e-5, atol=1e-6)
+    Ar = aR if aR is not None else ops.head_attn(X, wR, bR, heads=heads)
+    Y, s = ops.gat_fwd_partial(halves[0], aL, X, aR=Ar, heads=heads)
+    Y, q = ops.gat_fwd_continue(halves[1], aL, X, Y, s, aR=Ar, heads=heads)
+    torch.testing.assert_close(Y, want[0], rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(q.reshape(-1), want[1].reshape(-1), rtol=2e-5, atol=0.0)

@@ -2,9 +2,9 @@
 """The compute one rank of a P-rank row partition spends in the GAT training pair, without
 the exchange (comm None; config 3's 8-head layer on the Products shape): HaloGat (the one-GPU
 statistics kernels over the gathered table) against HaloGatOverlap (own-column partial
-statistics, then halo-column partials, normalised in torch) -- the price of making the
-exchange overlappable.  Also the own-column share of each pass, the part that can hide the
-exchange.  HIP events, median of reps.  One JSON line per P."""
+statistics, then the halo columns continued from them, gala_gat_fwd_continue_f32) -- the
+price of making the exchange overlappable.  Also the own-column share of each pass, the
+part that can hide the exchange.  HIP events, median of reps.  One JSON line per P."""
 import json
 import os
 import sys
@@ -57,15 +57,15 @@ def main():
                 lay.backward(dY, linear=False)
             res[name + "_pair_ms"] = med(pair, reps)
             if name == "halo_overlap":
-                b = lay._buffers()
+                U, Um, S, M = be.empty(n, F), be.empty(n, F), be.empty(n, H), be.empty(n, H)
                 res["own_fwd_partial_ms"] = med(lambda: be.gat_partial_stats(
-                    lay.groups[0], aL, None, lay.Xs, H, 0.2, b["U0"], b["S0"], b["Um0"], b["M0"], wR=wR, bR=bR,
-                    self_col=lay.self_col, aR_out=lay.As), reps)
-                res["halo_fwd_partial_ms"] = med(lambda: be.gat_partial_stats(
-                    lay.groups[1], aL, None, lay.Xs, H, 0.2, b["U1"], b["S1"], b["Um1"], b["M1"], wR=wR, bR=bR),
-                    reps)
+                    lay.groups[0], aL, None, lay.Xs, H, 0.2, U, S, Um, M, wR=wR, bR=bR, self_col=lay.self_col,
+                    aR_out=lay.As), reps)
+                res["halo_fwd_continue_ms"] = med(lambda: be.gat_continue(
+                    lay.groups[1], aL, None, lay.Xs, H, 0.2, U, S, Um, M, wR=wR, bR=bR), reps)
+                Pb = be.empty(n, F)
                 res["own_bwd_partial_ms"] = med(lambda: be.gat_partial(
-                    lay.groups[0], aL, lay.As, lay.dYs, H, 0.2, b["P0"], b["Ssc"]), reps)
+                    lay.groups[0], aL, lay.As, lay.dYs, H, 0.2, Pb, lay.Ssc), reps)
             del lay
             torch.cuda.empty_cache()
         print(json.dumps({"probe": "halo_gat_overlap", "world": P, "rank": 0, "n_rows": n, "n_cols": pt.n_cols,
