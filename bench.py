@@ -577,8 +577,10 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
              (gala/dist.py HaloGat): bit-identical to one GPU, F + H (forward) and F
              (backward) floats per halo row;
       halo-overlap  the same exchange, the own-column edges' partial statistics run while
-             it is in flight and the halo columns' after it (gala/dist.py HaloGatOverlap;
-             fp32 rounding of one GPU, each row's sums regrouped);
+             it is in flight and the halo columns continue them after it (gala/dist.py
+             HaloGatOverlap; fp32 rounding of one GPU, each row's sums grouped per range);
+      halo-overlap-pipe  (dense halo, N > 1) the table all-gathered in PIPE_CHUNKS row
+             chunks, each chunk's edges continued as it lands;
       vcut   north_star's vertex cut (gala/vertex_cut.py VertexCutGat): the row-statistics
              forward and the backward's partial aggregation over the edges whose source a
              rank owns, 2F + 2H (forward) and F (backward) partial floats per row
@@ -595,6 +597,10 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     hpart = gdist.partition_graph(g, rank, world, bounds=bounds)
     layers["halo"] = gdist.HaloGat(hpart, F, H, be, comm)
     layers["halo-overlap"] = gdist.HaloGatOverlap(hpart, F, H, be, comm)
+    ppart = None
+    if world > 1 and hpart.halo_mode == "dense":    # the all-gather in row chunks, pipelined
+        ppart = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
+        layers["halo-overlap-pipe"] = gdist.HaloGatOverlap(ppart, F, H, be, comm)
     vpart = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
     layers["vcut"] = vc.VertexCutGat(vpart, F, H, be, comm)
     X = layers["halo"].own_rows("X")              # the layer input, written into the table
@@ -614,9 +620,13 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     comm_bytes = {"halo": hpart.halo_bytes(2 * F + H) if world > 1 else 0,
                   "vcut": vpart.comm_bytes(2 * F + 2 * H) + vpart.comm_bytes(F)}
     comm_bytes["halo-overlap"] = comm_bytes["halo"]
+    if ppart is not None:
+        comm_bytes["halo-overlap-pipe"] = ppart.halo_bytes(2 * F + H)
     desc = {"halo": "row partition, gathered X / logits / dY rows, the one-GPU kernels (bit-identical)",
             "halo-overlap": "row partition, gathered X / logits / dY rows; own-column partial statistics "
                             "overlap the exchange (fp32 rounding of one GPU)",
+            "halo-overlap-pipe": f"row partition, the X / dY table all-gathered in {PIPE_CHUNKS} row chunks, each "
+                                 f"chunk's edges continued as it lands (fp32 rounding of one GPU)",
             "vcut": f"vertex cut, row-statistics partials reduce-scattered to the row owners in {PIPE_CHUNKS} "
                     f"overlapped row blocks"}
     out = {"value": 2 * g.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
@@ -625,7 +635,7 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
            "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
            "comm_bytes_per_step_per_rank": comm_bytes[best],
            "comm_bytes_per_step_per_rank_candidates": comm_bytes}
-    del layers, X, dY
+    del layers, X, dY, ppart
     return out
 
 

@@ -815,16 +815,17 @@ extern "C" int gala_cpu_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const 
 
 // gala_gat_fwd_continue_f32 (gala_hip.h): every row's sums start at the partials of an
 // earlier pass over other columns (which may alias the outputs), then take this pattern's
-// edges in CSR order; Ym NULL: the plain REF forward
+// edges in CSR order; Ym NULL: the plain REF forward; flags GALA_GAT_PARTIAL: unnormalised
 extern "C" int gala_cpu_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const float *aR,
                                              const float *wR, const float *bR, const float *X, int64_t ldx,
-                                             int32_t F, int32_t heads, float slope, const float *U0,
-                                             int64_t ldu0, const float *S0, const float *Um0, int64_t ldum0,
+                                             int32_t F, int32_t heads, float slope, int32_t flags,
+                                             const float *U0, int64_t ldu0, const float *S0, const float *Um0, int64_t ldum0,
                                              const float *M0, float *Y, int64_t ldy, float *q_out, float *Ym,
                                              int64_t ldym, float *sma, void *) {
     int st = check_csr(A);
     if (st) return st;
-    const bool stats = Ym != nullptr;
+    const bool stats = Ym != nullptr, partial = flags == GALA_GAT_PARTIAL;
+    if (flags != 0 && !partial) return GALA_ERR_INVALID_ARG;
     if (heads < 1 || F < 1 || F % heads != 0 || ldx < F || ldy < F || ldu0 < F) return GALA_ERR_INVALID_ARG;
     if ((Um0 != nullptr) != stats || (stats && (ldym < F || ldum0 < F || !M0 || !sma || !q_out)))
         return GALA_ERR_INVALID_ARG;
@@ -862,12 +863,12 @@ extern "C" int gala_cpu_gat_fwd_continue_f32(const gala_csr_t *A, const float *a
                         }
                     }
                 }
-                const float q = 1.0f / (sum + (float)S * 1e-12f);
-                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = acc[f] * q;
+                const float q = partial ? 1.0f : 1.0f / (sum + (float)S * 1e-12f);
+                for (int32_t f = 0; f < D; ++f) Y[r * ldy + h * D + f] = partial ? acc[f] : acc[f] * q;
                 if (stats)
-                    for (int32_t f = 0; f < D; ++f) Ym[r * ldym + h * D + f] = accm[f] * q;
-                if (q_out) q_out[r * H + h] = q;
-                if (stats) sma[r * H + h] = sm * q;
+                    for (int32_t f = 0; f < D; ++f) Ym[r * ldym + h * D + f] = partial ? accm[f] : accm[f] * q;
+                if (q_out) q_out[r * H + h] = partial ? sum : q;
+                if (stats) sma[r * H + h] = partial ? sm : sm * q;
             }
     }
     return GALA_OK;

@@ -869,8 +869,8 @@ static int gat_fwd_impl(const gala_csr_t *A, const float *aL, const float *aR, c
     if (stats && !partial && !self_col && !init_acc && A->n_cols > A->n_rows && A->nnz > 0)
         return GALA_ERR_INVALID_ARG;
     if (ar_out && (!stats || aR || !X)) return GALA_ERR_INVALID_ARG;
-    // a continuation: REF, normalised, no alpha; the statistics need their two partials too
-    if (init_acc && (mode != GALA_SOFTMAX_REF || partial || alpha_out || ar_out || !init_sum || ld_init < F ||
+    // a continuation: REF, no alpha; the statistics need their two partials too
+    if (init_acc && (mode != GALA_SOFTMAX_REF || alpha_out || ar_out || !init_sum || ld_init < F ||
                      (stats && (!init_accm || !init_sma || ld_initm < F)) || (!stats && (init_accm || init_sma))))
         return GALA_ERR_INVALID_ARG;
     const int D = F / heads;
@@ -992,18 +992,21 @@ extern "C" int gala_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const floa
 // The REF forward continued from an earlier pass's partials over other columns (a row
 // partition's own columns while the halo is in flight): Y = q (U0 + sum p X) with
 // q = 1 / (S0 + sum p + 1e-12); with Ym the row statistics likewise from (Um0, M0).
+// flags GALA_GAT_PARTIAL: the sums continued but left unnormalised (q_out = the raw sum),
+// for a further range (a halo arriving in chunks).
 extern "C" int gala_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const float *aR,
                                          const float *wR, const float *bR, const float *X, int64_t ldx,
-                                         int32_t F, int32_t heads, float slope, const float *U0, int64_t ldu0,
+                                         int32_t F, int32_t heads, float slope, int32_t flags,
+                                         const float *U0, int64_t ldu0,
                                          const float *S0, const float *Um0, int64_t ldum0, const float *M0,
                                          float *Y, int64_t ldy, float *q_out, float *Ym, int64_t ldym,
                                          float *sma, void *stream) {
     if (!aR && !wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
     if ((!U0 || !S0) && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
-    if ((Ym != nullptr) != (Um0 != nullptr)) return GALA_ERR_INVALID_ARG;
+    if ((Ym != nullptr) != (Um0 != nullptr) || (flags & ~GALA_GAT_PARTIAL) != 0) return GALA_ERR_INVALID_ARG;
     return gat_fwd_impl(A, aL, aR, aR ? nullptr : wR, aR ? nullptr : bR, X, ldx, F, heads, slope,
-                        GALA_SOFTMAX_REF, Y, ldy, nullptr, q_out, stream, Ym, ldym, sma, nullptr, nullptr, U0,
-                        ldu0, S0, Um0, ldum0, M0);
+                        GALA_SOFTMAX_REF | flags, Y, ldy, nullptr, q_out, stream, Ym, ldym, sma, nullptr, nullptr,
+                        U0, ldu0, S0, Um0, ldum0, M0);
 }
 
 extern "C" int gala_gat_fwd_attn_f32(const gala_csr_t *A, const float *aL, const float *wR,

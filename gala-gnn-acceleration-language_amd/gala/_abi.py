@@ -108,7 +108,7 @@ SIGNATURES = {
                                                       _P, _P, _I64, _P, _P]),
     "gala_gat_fwd_partial_stats_ex_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P,
                                                          _I64, _P, _P, _I64, _P, _P, _P, _P]),
-    "gala_gat_fwd_continue_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P, _I64, _P,
+    "gala_gat_fwd_continue_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _I32, _P, _I64, _P,
                                                  _P, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
     "gala_head_attn_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _P, _P, _P]),
     "gala_head_attn_bwd_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _P, _P, _I64, _I32, _P]),

@@ -56,11 +56,11 @@ class HipBackend:
         return self.ops.gat_fwd_partial_stats(g, aL, X, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, U=U,
                                               sums=sums, Um=Um, msums=msums, self_col=self_col, aR_out=aR_out)
 
-    def gat_continue(self, g, aL, aR, X, heads, slope, U0, S0, Um0=None, M0=None, wR=None, bR=None):
+    def gat_continue(self, g, aL, aR, X, heads, slope, U0, S0, Um0=None, M0=None, wR=None, bR=None, partial=False):
         """REF forward (or, with Um0 / M0, the row statistics) continued from the partials of
-        an earlier column range, in place (gala_gat_fwd_continue_f32)."""
+        an earlier column range, in place (gala_gat_fwd_continue_f32; partial: unnormalised)."""
         return self.ops.gat_fwd_continue(g, aL, X, U0, S0, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, Um0=Um0,
-                                         M0=M0)
+                                         M0=M0, partial=partial)
 
     def gat_bwd_stats(self, g, aL, aR, dY, q, Y, Ym, sma, heads, slope):
         """(dX, d_aL) of the REF layer from its row statistics (gala_gat_bwd_stats_f32)."""
@@ -181,9 +181,10 @@ class CpuBackend:
                       _hp(msums), _hp(self_col), _hp(aR_out), None)
         return U, sums, Um, msums
 
-    def gat_continue(self, g: CpuGraph, aL, aR, X, heads, slope, U0, S0, Um0=None, M0=None, wR=None, bR=None):
+    def gat_continue(self, g: CpuGraph, aL, aR, X, heads, slope, U0, S0, Um0=None, M0=None, wR=None, bR=None,
+                     partial=False):
         _abi.call_cpu("gala_gat_fwd_continue_f32", g.csr(), _hp(aL), _hp(aR), _hp(wR), _hp(bR), _hp(X), X.stride(0),
-                      X.shape[1], heads, slope, _hp(U0), U0.stride(0), _hp(S0), _hp(Um0),
+                      X.shape[1], heads, slope, _abi.GALA_GAT_PARTIAL if partial else 0, _hp(U0), U0.stride(0), _hp(S0), _hp(Um0),
                       Um0.stride(0) if Um0 is not None else 0, _hp(M0), _hp(U0), U0.stride(0), _hp(S0), _hp(Um0),
                       Um0.stride(0) if Um0 is not None else 0, _hp(M0), None)
         return (U0, S0) if Um0 is None else (U0, S0, Um0, M0)

@@ -541,15 +541,19 @@ class HaloGat:
       backward(dY[, linear]) -> (dX, d_aL[, dwR, dbR])
     X may already be written into `own_rows(F)` (the own block of the table) to skip a copy."""
 
+    _chunked = False      # HaloGatOverlap takes a table gathered in row chunks
+
     def __init__(self, part: GraphPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
         import torch
-        if part.chunks != 1:
+        if part.chunks != 1 and not self._chunked:
             raise ValueError("HaloGat: one halo chunk (the kernels read the whole table)")
         self.part, self.F, self.H, self.be, self.comm, self.slope = part, F, heads, backend, comm, slope
         self.graph = backend.graph(part.graph, split=part.split_threshold)
-        self.x0 = x0 = part.own_offset()
+        self.x0 = part.own_offset() if part.chunks == 1 else None
         dev = getattr(backend, "device", torch.device("cpu"))
-        self.self_col = torch.arange(x0, x0 + part.n, dtype=torch.int32, device=dev)
+        # the table row of every own row (one block unless the table is gathered in chunks)
+        sc = np.concatenate([np.arange(x, x + j1 - j0) for j0, j1, x in part.own_blocks()] or [np.zeros(0)])
+        self.self_col = torch.from_numpy(sc.astype(np.int32)).to(dev)
         if comm is None:
             self.exchange = None
         elif part.halo_mode == "p2p":
@@ -620,34 +624,52 @@ class HaloGat:
 
 
 class HaloGatOverlap(HaloGat):
-    """HaloGat with the halo exchange hidden behind the own-column edges.  The forward runs
-    the unnormalised row statistics of the edges into the rank's own columns
+    """HaloGat with the halo exchange hidden behind the edges already computable.  The
+    forward runs the unnormalised row statistics of the edges into the rank's own columns
     (gala_gat_fwd_partial_stats_ex_f32 over part.groups[0], which also writes the own
     vertices' logits) while the X rows are in flight, then continues every row from those
-    partials over the halo columns and normalises (gala_gat_fwd_continue_f32, in place; GAT
-    REF subtracts no row maximum, common.h:760-773, so the partial sums simply add).  The
-    backward likewise: sum_e p_e dY[c] over the own columns and the row-local d_aL overlap
-    the dY exchange, the halo columns continue it, dX = q (P_own + P_halo).  The exchange
-    and the bytes are HaloGat's; each row's sums are grouped per column range, so results
-    agree with one GPU to fp32 rounding, not bit for bit."""
+    partials over each halo chunk as it lands (gala_gat_fwd_continue_f32, in place:
+    unnormalised for all but the last chunk, normalised after it; GAT REF subtracts no row
+    maximum, common.h:760-773, so the sums simply continue).  With a dense table gathered in
+    K row chunks (partition_graph(..., chunks=K)) the all-gathers pipeline against the
+    chunks' edges.  The backward likewise: sum_e p_e dY[c] over the own columns and the
+    row-local d_aL overlap the dY exchange, each halo chunk continues it, dX = q (P_own +
+    P_halo).  Each row's sums are grouped per column range, so results agree with one GPU to
+    fp32 rounding, not bit for bit."""
+    _chunked = True
 
     def __init__(self, part: GraphPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):
         super().__init__(part, F, heads, backend, comm, slope)
-        if len(part.groups) != 2:
-            raise ValueError("HaloGatOverlap: one own-column and one halo group")
         self.groups = [backend.graph(h, split=part.split_threshold) for h in part.groups]
         n = part.n
         self.own_graph = backend.graph(layout.HostGraph(n, n, np.zeros(n + 1, np.int32), np.zeros(0, np.int32)),
                                        split=False)
         self.Ssc = backend.empty(n, heads)
+        self.blocks = part.own_blocks()
+
+    def own_rows(self, which="X"):
+        if self.part.chunks != 1:
+            raise ValueError("HaloGatOverlap: the own rows are not one block of a chunked table")
+        return super().own_rows(which)
+
+    def _start(self, table, rows):
+        """Own rows written into the table, the exchange started: one work list per halo chunk."""
+        if rows is not None:
+            for j0, j1, x in self.blocks:
+                dst = table[x:x + j1 - j0]
+                if dst.data_ptr() != rows[j0:j1].data_ptr():
+                    dst.copy_(rows[j0:j1])
+        chunks = self.exchange.start(table) if self.exchange else []
+        return [chunks[k] if k < len(chunks) else [] for k in range(len(self.groups) - 1)]
 
     def forward_train(self, aL, aR, X, wR=None, bR=None):
         n, H, F, be = self.part.n, self.H, self.F, self.be
         if self.saved is not None:
             self._wait(self.saved[-1])
-        works = self._gather(self.Xs, X)
+        chunks = self._start(self.Xs, X)
         if aR is not None:                   # given source logits: their (small) table first
-            self._wait(self._gather(self.As, aR.reshape(n, H)))
+            for works in self._start(self.As, aR.reshape(n, H)):
+                self._wait(works)
             kw = {}
         else:
             kw = {"wR": wR, "bR": bR}
@@ -656,29 +678,34 @@ class HaloGatOverlap(HaloGat):
         be.gat_partial_stats(self.groups[0], aL, At, self.Xs, H, self.slope, Y, q, Ym, sma,
                              self_col=None if aR is not None else self.self_col,
                              aR_out=None if aR is not None else self.As, **kw)
-        self._wait(works)
-        be.gat_continue(self.groups[1], aL, At, self.Xs, H, self.slope, Y, q, Ym, sma, **kw)
-        ar_works = self._gather(self.As, None) if aR is None else []
-        self.saved = (aL, q, Y, Ym, sma, wR, ar_works)
+        last = len(chunks) - 1
+        for k, works in enumerate(chunks):
+            self._wait(works)
+            be.gat_continue(self.groups[1 + k], aL, At, self.Xs, H, self.slope, Y, q, Ym, sma, partial=k < last,
+                            **kw)
+        ar_works = [w for works in self._start(self.As, None) for w in works] if aR is None else []
+        self.saved = (aL, q, Y, Ym, sma, wR, X, ar_works)
         return Y
 
     def backward(self, dY, linear=True):
         if self.saved is None:
             raise RuntimeError("HaloGatOverlap.backward: no forward_train to take the row statistics from")
-        aL, q, Y, Ym, sma, wR, ar_works = self.saved
+        aL, q, Y, Ym, sma, wR, X, ar_works = self.saved
         n, H, be = self.part.n, self.H, self.be
-        works = self._gather(self.dYs, dY)
+        chunks = self._start(self.dYs, dY)
         # the own columns' logits were written by this rank's forward; the halo's may still be in flight
         dX = be.empty(n, self.F)
         be.gat_partial(self.groups[0], aL, self.As, self.dYs, H, self.slope, dX, self.Ssc)
-        _, d_aL = be.gat_bwd_stats(self.own_graph, aL, self.As[self.x0:self.x0 + n], self.own_rows("dY"), q, Y, Ym,
-                                   sma, H, self.slope)
+        _, d_aL = be.gat_bwd_stats(self.own_graph, aL, self.As, dY, q, Y, Ym, sma, H, self.slope)
         self._wait(ar_works)
-        self._wait(works)
-        be.gat_continue(self.groups[1], aL, self.As, self.dYs, H, self.slope, dX, self.Ssc)
+        last = len(chunks) - 1
+        for k, works in enumerate(chunks):
+            self._wait(works)
+            be.gat_continue(self.groups[1 + k], aL, self.As, self.dYs, H, self.slope, dX, self.Ssc,
+                            partial=k < last)
         d_aL = d_aL.view(n, H)
         if not (linear and wR is not None):
             return dX, d_aL
-        dW, db = be.head_linear_grads(self.own_rows("X"), d_aL, H)
+        dW, db = be.head_linear_grads(X, d_aL, H)
         be.head_attn_bwd(d_aL, wR, H, dX)
         return dX, d_aL, dW, db

@@ -397,10 +397,11 @@ def gat_fwd_partial_stats(g: DeviceGraph, aL, X, aR=None, wR=None, bR=None, head
 
 
 def gat_fwd_continue(g: DeviceGraph, aL, X, U0, S0, aR=None, wR=None, bR=None, heads=1, slope=0.2, Um0=None,
-                     M0=None, Y=None, q=None, Ym=None, sma=None):
+                     M0=None, Y=None, q=None, Ym=None, sma=None, partial=False):
     """gala_gat_fwd_continue_f32: the REF forward (Um0 None) or the row-statistics forward of
     rows whose first column range already gave the partials (U0, S0[, Um0, M0]); the outputs
-    default to those buffers (in place).  Returns (Y, q) or (Y, q, Ym, sma)."""
+    default to those buffers (in place).  partial: left unnormalised for a further range.
+    Returns (Y, q) or (Y, q, Ym, sma)."""
     F = X.shape[1]
     Y = U0 if Y is None else Y
     q = S0 if q is None else q
@@ -409,7 +410,8 @@ def gat_fwd_continue(g: DeviceGraph, aL, X, U0, S0, aR=None, wR=None, bR=None, h
         sma = M0 if sma is None else sma
     w = (F + 3) // 4 * 4
     _abi.call("gala_gat_fwd_continue_f32", g.csr(2 * w + 3 * heads if Um0 is not None else w + 2 * heads),
-              _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X), X.stride(0), F, heads, slope, _dp(U0), U0.stride(0),
+              _dp(aL), _dp(aR), _dp(wR), _dp(bR), _dp(X), X.stride(0), F, heads, slope,
+              _abi.GALA_GAT_PARTIAL if partial else 0, _dp(U0), U0.stride(0),
               _dp(S0), _dp(Um0), Um0.stride(0) if Um0 is not None else 0, _dp(M0), _dp(Y), Y.stride(0), _dp(q),
               _dp(Ym), Ym.stride(0) if Ym is not None else 0, _dp(sma), _stream())
     return (Y, q) if Um0 is None else (Y, q, Ym, sma)

@@ -426,14 +426,16 @@ int gala_gat_fwd_partial_stats_ex_f32(const gala_csr_t *A, const float *aL, cons
  * GALA_GAT_PARTIAL): each row's state starts at U0 = sum p X, S0 = sum p (and Um0 = sum m p X,
  * M0 = sum m p) and takes this pattern's edges, then Y = q (U0 + ...), q = 1/(S0 + ... + 1e-12),
  * Ym, sma as gala_gat_fwd_stats_f32.  The inputs may alias the outputs (Y = U0, q_out = S0,
- * Ym = Um0, sma = M0).  Used by a row partition whose own-column edges run while the halo
+ * Ym = Um0, sma = M0).  flags GALA_GAT_PARTIAL (else 0): the sums are continued but left
+ * unnormalised (Y = U0 + sum p X, q_out = the raw sum, ...), for one more range after this
+ * one (a halo that lands in row chunks).  Used by a row partition whose own-column edges run while the halo
  * rows are in flight (gala/dist.py HaloGatOverlap); no reference counterpart (the split of
  * the sums is this framework's, common.h:760-773 has the REF sums).  The sums are grouped
  * per range, so the results match the one-pass forward to fp32 rounding.
  */
 int gala_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *wR,
                               const float *bR, const float *X, int64_t ldx, int32_t F, int32_t heads,
-                              float slope, const float *U0, int64_t ldu0, const float *S0, const float *Um0,
+                              float slope, int32_t flags, const float *U0, int64_t ldu0, const float *S0, const float *Um0,
                               int64_t ldum0, const float *M0, float *Y, int64_t ldy, float *q_out, float *Ym,
                               int64_t ldym, float *sma, void *stream);
 

@@ -48,7 +48,7 @@ def test_bench_self_launches_ranks():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
     gat = d["gat"]                                    # the GAT layer: halo and vertex-cut layouts timed
-    assert gat["value"] > 0 and set(gat["candidates_ms_per_step"]) == {"halo", "halo-overlap", "vcut"}
+    assert gat["value"] > 0 and set(gat["candidates_ms_per_step"]) >= {"halo", "halo-overlap", "vcut"}
     assert gat["layout"].split()[0] in gat["candidates_ms_per_step"]
     assert d["unit"] == "edges/s" and d["steps"] == 2 and d["warmup"] == 1
     c = d["comm"]

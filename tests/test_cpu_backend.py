@@ -458,7 +458,14 @@ def test_gat_continue_matches_one_pass(rc, which):
     Y, q = be.gat_continue(g1, aL, Ar, X, H, 0.2, Y, s)
     np.testing.assert_allclose(Y.numpy(), want[0].numpy(), rtol=2e-5, atol=1e-6)
     np.testing.assert_allclose(q.numpy(), want[1].numpy().reshape(-1), rtol=2e-5, atol=0)
+    # three ranges: the middle one continued unnormalised (GALA_GAT_PARTIAL), the last normalises
+    g3 = [be.graph(_split_by_column(g, lambda c, r=r: c % 3 == r)) for r in range(3)]
+    U, S, Um, M = be.gat_partial_stats(g3[0], aL, aR, X, H, 0.2, U, S, Um, M, **kw)
+    be.gat_continue(g3[1], aL, aR, X, H, 0.2, U, S, Um, M, partial=True, **kw)
+    got = be.gat_continue(g3[2], aL, aR, X, H, 0.2, U, S, Um, M, **kw)
+    for a, b in zip(got, want):
+        np.testing.assert_allclose(a.numpy().reshape(-1), b.numpy().reshape(-1), rtol=2e-5, atol=1e-6)
     with pytest.raises(_abi.GalaError):
         _abi.call_cpu("gala_gat_fwd_continue_f32", g1.csr(), aL.data_ptr(), Ar.data_ptr(), None, None,
-                      X.data_ptr(), F, F, H, 0.2, U.data_ptr(), F, S.data_ptr(), None, 0, None, U.data_ptr(), F,
+                      X.data_ptr(), F, F, H, 0.2, 0, U.data_ptr(), F, S.data_ptr(), None, 0, None, U.data_ptr(), F,
                       S.data_ptr(), Um.data_ptr(), F, M.data_ptr(), None)

@@ -486,22 +486,23 @@ def test_auto_halo_mode_is_one_choice_for_all_ranks():
 
 
 # ---- halo GAT: the one-GPU statistics kernels over a gathered table ----------------------------
-def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q, cls="HaloGat"):
+def _halo_gat_worker(rank, world, port, name, rc, halo_mode, q, cls="HaloGat", chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         g = GRAPHS[name]()
         aL, aR, X = _gat_inputs(g)
         dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
-        pt = gdist.partition_graph(g, rank, world, halo_mode=halo_mode)
+        pt = gdist.partition_graph(g, rank, world, halo_mode=halo_mode, chunks=chunks)
         own = slice(pt.r0, pt.r0 + pt.n)
         gat = getattr(gdist, cls)(pt, F_GAT, H_GAT, CpuBackend(), Comm())
         t = lambda a: torch.from_numpy(a[own].copy())  # noqa: E731
         grads = []
         if rc:
             wR, bR = _gat_attn_weights()
-            gat.own_rows("X").copy_(t(X))               # written in place: no copy in forward_train
-            Y = gat.forward_train(t(aL), None, gat.own_rows("X"), torch.from_numpy(wR), torch.from_numpy(bR))
+            Xo = gat.own_rows("X") if chunks == 1 else t(X)
+            Xo.copy_(t(X))                              # written in place: no copy in forward_train
+            Y = gat.forward_train(t(aL), None, Xo, torch.from_numpy(wR), torch.from_numpy(bR))
             dX, d_aL, dW, db = gat.backward(t(dY))
             for G in (dW, db):
                 dist.all_reduce(G)
@@ -555,16 +556,22 @@ def test_halo_gat_bit_identical_to_one_process(world, name, rc, halo_mode):
         np.testing.assert_array_equal(got[1], ref[1])
 
 
-@pytest.mark.parametrize("world,name,rc,halo_mode", [(2, "powerlaw", False, "p2p"), (3, "cora", True, "dense"),
-                                                     (3, "banded", True, "p2p"), (2, "empty_rows", False, "dense")])
-def test_halo_gat_overlap_matches_one_process(world, name, rc, halo_mode):
+@pytest.mark.parametrize("world,name,rc,halo_mode,chunks", [(2, "powerlaw", False, "p2p", 1),
+                                                            (3, "cora", True, "dense", 1),
+                                                            (3, "banded", True, "p2p", 1),
+                                                            (2, "empty_rows", False, "dense", 1),
+                                                            (3, "cora", True, "dense", 3),
+                                                            (2, "powerlaw", False, "dense", 2)])
+def test_halo_gat_overlap_matches_one_process(world, name, rc, halo_mode, chunks):
     """HaloGatOverlap (gala/dist.py): the own-column partial statistics overlap the exchange and
-    the halo columns' partials are added after it -- each row's sums regrouped, so Y, dX and
-    d_aL agree with the one-process pair to fp32 rounding (not bit for bit)."""
+    every halo chunk continues them as it lands (a dense table gathered in 1-3 row chunks) --
+    each row's sums grouped per range, so Y, dX and d_aL agree with the one-process pair to
+    fp32 rounding (not bit for bit)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_halo_gat_worker, args=(r, world, port, name, rc, halo_mode, q, "HaloGatOverlap"))
+    procs = [ctx.Process(target=_halo_gat_worker, args=(r, world, port, name, rc, halo_mode, q, "HaloGatOverlap",
+                                                        chunks))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -1022,6 +1022,13 @@ def test_gat_continue_matches_one_pass(F, heads, rc):
     assert got[0].data_ptr() == U.data_ptr() and got[3].data_ptr() == M.data_ptr()   # in place
     for a, b in zip(got, want):
         torch.testing.assert_close(a.reshape(-1), b.reshape(-1), rtol=2e-5, atol=1e-6)
+    # three ranges, the middle one continued unnormalised (GALA_GAT_PARTIAL)
+    thirds = [ops.DeviceGraph.from_host(_split_by_column(g, lambda c, r=r: c % 3 == r)) for r in range(3)]
+    U, S, Um, M = ops.gat_fwd_partial_stats(thirds[0], aL, X, aR=aR, heads=heads, **kw)
+    ops.gat_fwd_continue(thirds[1], aL, X, U, S, aR=aR, heads=heads, Um0=Um, M0=M, partial=True, **kw)
+    got = ops.gat_fwd_continue(thirds[2], aL, X, U, S, aR=aR, heads=heads, Um0=Um, M0=M, **kw)
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a.reshape(-1), b.reshape(-1), rtol=2e-5, atol=1e-6)
     Ar = aR if aR is not None else ops.head_attn(X, wR, bR, heads=heads)
     Y, s = ops.gat_fwd_partial(halves[0], aL, X, aR=Ar, heads=heads)
     Y, q = ops.gat_fwd_continue(halves[1], aL, X, Y, s, aR=Ar, heads=heads)
