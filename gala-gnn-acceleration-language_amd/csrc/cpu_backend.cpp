@@ -952,6 +952,24 @@ extern "C" int gala_cpu_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *a
                              d_aL);
 }
 
+// gala_gat_bwd_stats_linear_f32 (gala_hip.h): then dX[r, f] += d_aL[r, head(f)] * wR[f]
+extern "C" int gala_cpu_gat_bwd_stats_linear_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                                 const float *pe, const float *dY, int64_t lddy,
+                                                 const float *dY_rows, int32_t F, int32_t heads, float slope,
+                                                 const float *q, const float *Y, int64_t ldy, const float *Ym,
+                                                 int64_t ldym, const float *sma, const float *wR, float *dX,
+                                                 int64_t lddx, float *d_aL, void *) {
+    if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    const int st = cpu_gat_bwd_stats(A, aL, aR, pe, dY, lddy, dY_rows, F, heads, slope, q, Y, ldy, Ym, ldym, sma,
+                                     dX, lddx, d_aL);
+    if (st || A->n_rows == 0) return st;
+    const int32_t D = F / heads;
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int32_t f = 0; f < F; ++f) dX[r * lddx + f] = dX[r * lddx + f] + d_aL[r * heads + f / D] * wR[f];
+    return GALA_OK;
+}
+
 extern "C" int gala_cpu_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X, int64_t ldx,
                                       const float *w, const float *b, float *out, void *) {
     if (n_rows < 0 || F < 1 || heads < 1 || F % heads != 0 || ldx < F) return GALA_ERR_INVALID_ARG;

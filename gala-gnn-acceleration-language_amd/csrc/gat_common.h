@@ -106,6 +106,9 @@ struct GatDev {
     // before it writes them)
     const float *init_acc, *init_sum, *init_accm, *init_sma;
     int64_t ld_init, ld_initm;
+    // statistics backward, nullable: the source logit's per-head Linear weights [F] (aR = X wR
+    // + bR); dX[r, f] += d_aL[r, head(f)] * attn_w[f] at the store (REF: d_aR = d_aL)
+    const float *attn_w;
 };
 
 // Internal forward MODE: REF softmax that also accumulates the row statistics.

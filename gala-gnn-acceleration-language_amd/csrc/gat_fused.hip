@@ -141,10 +141,23 @@ __device__ __forceinline__ void store_dx(const GatDev &d, const Lanes<G, VEC, CH
     }
 }
 
-// d_aL of one row from the forward's row statistics: <dY, Y> and <dY, Ym> per head
+// The attention Linear's backward folded into the dX store: dX[r, f] += d_aL[r, head(f)] *
+// w[f], with the roundings of gala_head_attn_bwd_f32 (a product, then a sum)
+template <int G, int VEC, int CH>
+__device__ __forceinline__ void add_attn_linear(const GatDev &d, const Lanes<G, VEC, CH> &ln, float dal,
+                                                float (&dxa)[CH][VEC]) {
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i)
+            if (ln.in(ch, i)) dxa[ch][i] = __fadd_rn(dxa[ch][i], __fmul_rn(dal, d.attn_w[ln.off[ch] + i]));
+}
+
+// d_aL of one row from the forward's row statistics: <dY, Y> and <dY, Ym> per head; every
+// lane of the head returns the value its leader stores
 template <int G, int VEC, int HW, int CH, bool RC>
-__device__ __forceinline__ void stats_d_al(const EdgeParams &p, const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
-                                           int64_t row, const float (&dy)[CH][VEC]) {
+__device__ __forceinline__ float stats_d_al(const EdgeParams &p, const GatDev &d, const GatLane<G, VEC, CH, RC> &gl_,
+                                            int64_t row, const float (&dy)[CH][VEC]) {
     typedef typename GVec<VEC>::T V;
     float syy = 0.0f, sym = 0.0f;
 #pragma unroll
@@ -162,10 +175,11 @@ __device__ __forceinline__ void stats_d_al(const EdgeParams &p, const GatDev &d,
     const float eps = (float)p.seg.n * 1e-12f;
     const float acc = group_sum<HW>(syy) + eps;  // K7 on sds (common.h:793-794)
     const float s1 = group_sum<HW>(sym);
-    if (gl_.leader) {
-        const int64_t o = row * gl_.H + gl_.hh;
-        d.d_aL[o] = (s1 - acc * d.smas[o]) + eps;   // common.h:662-667
-    }
+    if (!gl_.cv) return 0.0f;
+    const int64_t o = row * gl_.H + gl_.hh;
+    const float dal = (s1 - acc * d.smas[o]) + eps;   // common.h:662-667
+    if (gl_.leader) d.d_aL[o] = dal;
+    return dal;
 }
 
 template <int G, int VEC, int U, int HW, int CH, bool RC, bool ST>
@@ -174,9 +188,10 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d
     if (!row_ok) return;
     const GatLane<G, VEC, CH, RC> gl_(p, d, gl, row);
     float dy[CH][VEC], dxa[CH][VEC];
+    float dal = 0.0f;
     if constexpr (ST) {  // row-local: every row, hub rows included
         load_dy<G, VEC, CH, RC>(d, gl_, row, dy);
-        stats_d_al<G, VEC, HW, CH, RC>(p, d, gl_, row, dy);
+        dal = stats_d_al<G, VEC, HW, CH, RC>(p, d, gl_, row, dy);
     }
     if (split_threshold > 0 && p.rowptr[row + 1] - p.rowptr[row] > split_threshold)
         return;  // hub row: k_gat_bwd_fused_chunk / _fixup
@@ -191,6 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused(EdgeParams p, GatDev d
         row_range(p, s, row, e0, e1);
         gat_bwd_fused_range<G, VEC, U, HW, CH, RC, ST>(p, d, gl_, dy, e0, e1, st, dxa);
     }
+    if constexpr (ST)
+        if (d.attn_w) add_attn_linear<G, VEC, CH>(d, gl_.ln, dal, dxa);
     store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
     if constexpr (ST) return;
     const float eps = (float)p.seg.n * 1e-12f;
@@ -254,6 +271,8 @@ __global__ __launch_bounds__(kBlock) void k_gat_bwd_fused_fixup(EdgeParams p, Ga
             s2 = __fadd_rn(s2, w[F + 2 * H + hh]);
         }
     }
+    if constexpr (ST)  // the row's d_aL was stored by k_gat_bwd_fused
+        if (d.attn_w && gl_.cv) add_attn_linear<G, VEC, CH>(d, gl_.ln, d.d_aL[row * H + hh], dxa);
     store_dx<G, VEC, CH>(d, gl_.ln, d.dX + row * d.lddx, dxa);
     if (!ST && gl_.leader) {
         acc = __fadd_rn(acc, 1e-12f);
@@ -351,7 +370,8 @@ static int fused_dispatch(FusedArgs &a, int F, int heads, int vec, bool rc) {
 static int bwd_stats_impl(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
                           const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
                           float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
-                          int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream) {
+                          int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL, void *stream,
+                          const float *wR = nullptr) {
     FusedArgs a{};
     int st = edge_setup(A, heads, &a.p);
     if (st) return st;
@@ -376,6 +396,7 @@ static int bwd_stats_impl(const gala_csr_t *A, const float *aL, const float *aR,
     a.d.dY = dY, a.d.lddy = lddy, a.d.q = q, a.d.dX = dX, a.d.lddx = lddx, a.d.d_aL = d_aL;
     a.d.ys = Y, a.d.ldy = ldy, a.d.yms = Ym, a.d.ldym = ldym, a.d.smas = sma, a.d.alpha = pe;
     a.d.dy_rows = dY_rows;
+    a.d.attn_w = wR;
     a.hs = (hipStream_t)stream;
     a.split = hub_split(A, pad_to(F, 4), &a.sp);  // hub rows: dX[F] chunk partials
     return fused_dispatch(a, F, heads, vec, false);
@@ -396,6 +417,19 @@ extern "C" int gala_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, c
                                          float *d_aL, void *stream) {
     return bwd_stats_impl(A, aL, aR, pe, dY, lddy, dY_rows, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
                           d_aL, stream);
+}
+
+// The same with the source logit's per-head Linear (aR = X wR + bR) folded in: dX also
+// takes d_aR * wR (REF: d_aR = d_aL), bit-identical to gala_head_attn_bwd_f32 accumulating
+// into the statistics backward's dX.
+extern "C" int gala_gat_bwd_stats_linear_f32(const gala_csr_t *A, const float *aL, const float *aR,
+                                             const float *pe, const float *dY, int64_t lddy, const float *dY_rows,
+                                             int32_t F, int32_t heads, float slope, const float *q, const float *Y,
+                                             int64_t ldy, const float *Ym, int64_t ldym, const float *sma,
+                                             const float *wR, float *dX, int64_t lddx, float *d_aL, void *stream) {
+    if (!wR && A && A->n_rows > 0) return GALA_ERR_INVALID_ARG;
+    return bwd_stats_impl(A, aL, aR, pe, dY, lddy, dY_rows, F, heads, slope, q, Y, ldy, Ym, ldym, sma, dX, lddx,
+                          d_aL, stream, wR);
 }
 
 extern "C" int gala_gat_bwd_fused_f32(const gala_csr_t *A, const float *aL, const float *aR,

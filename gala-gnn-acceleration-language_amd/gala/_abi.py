@@ -104,6 +104,8 @@ SIGNATURES = {
                                                  _P, _I64, _P, _P, _P, _P, _P]),
     "gala_gat_bwd_stats_ex_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _I64, _P, _I32, _I32, _F, _P, _P, _I64,
                                                  _P, _I64, _P, _P, _I64, _P, _P]),
+    "gala_gat_bwd_stats_linear_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _I64, _P, _I32, _I32, _F, _P, _P,
+                                                     _I64, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "gala_gat_fwd_partial_stats_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P, _I64,
                                                       _P, _P, _I64, _P, _P]),
     "gala_gat_fwd_partial_stats_ex_f32": (ctypes.c_int, [_CSR, _P, _P, _P, _P, _P, _I64, _I32, _I32, _F, _P,
@@ -183,7 +185,7 @@ CPU_OPS = ("gala_spmm_f32", "gala_degree_f32", "gala_row_broadcast_f32", "gala_r
            "gala_gat_fwd_ex_f32", "gala_gat_bwd_ex_f32", "gala_gat_bwd_fused_f32",
            "gala_gat_fwd_stats_f32", "gala_gat_bwd_stats_f32", "gala_gat_fwd_partial_stats_f32",
            "gala_gat_fwd_stats_ex_f32", "gala_gat_bwd_stats_ex_f32", "gala_gat_fwd_partial_stats_ex_f32",
-           "gala_gat_fwd_continue_f32", "gala_head_attn_f32",
+           "gala_gat_fwd_continue_f32", "gala_gat_bwd_stats_linear_f32", "gala_head_attn_f32",
            "gala_head_attn_bwd_f32", "gala_edge_permute_f32", "gala_dense_grad_workspace",
            "gala_dense_grad_f32")
 

@@ -75,9 +75,10 @@ class HipBackend:
         return self.ops.gat_fwd_stats(g, aL, X, aR=aR, wR=wR, bR=bR, heads=heads, slope=slope, self_col=self_col,
                                       aR_out=aR_out)
 
-    def gat_bwd_stats_table(self, g, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope):
-        """(dX, d_aL) over a gathered table (gala_gat_bwd_stats_ex_f32)."""
-        return self.ops.gat_bwd_stats(g, aL, aR, dY, q, Y, Ym, sma, heads=heads, slope=slope, dY_rows=dY_rows)
+    def gat_bwd_stats_table(self, g, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope, wR=None):
+        """(dX, d_aL) over a gathered table (gala_gat_bwd_stats_ex_f32); wR: dX also takes the
+        source logit's per-head Linear (gala_gat_bwd_stats_linear_f32)."""
+        return self.ops.gat_bwd_stats(g, aL, aR, dY, q, Y, Ym, sma, heads=heads, slope=slope, dY_rows=dY_rows, wR=wR)
 
     def row_scale_relu(self, act, pre, X, out):
         """out = pre * relu(act * X) (gala_row_scale_relu_f32: the ReLU prologue)."""
@@ -206,10 +207,15 @@ class CpuBackend:
                       F, heads, slope, _hp(Y), F, _hp(q), _hp(Ym), F, _hp(sma), _hp(self_col), _hp(aR_out), None, None)
         return Y, q, Ym, sma
 
-    def gat_bwd_stats_table(self, g: CpuGraph, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope):
+    def gat_bwd_stats_table(self, g: CpuGraph, aL, aR, dY, dY_rows, q, Y, Ym, sma, heads, slope, wR=None):
         F = dY.shape[1]
         dX = torch.empty((g.n_rows, F), dtype=torch.float32)
         d_aL = torch.empty(g.n_rows * heads, dtype=torch.float32)
+        if wR is not None:
+            _abi.call_cpu("gala_gat_bwd_stats_linear_f32", g.csr(), _hp(aL), _hp(aR), None, _hp(dY), dY.stride(0),
+                          _hp(dY_rows), F, heads, slope, _hp(q), _hp(Y), Y.stride(0), _hp(Ym), Ym.stride(0),
+                          _hp(sma), _hp(wR), _hp(dX), dX.stride(0), _hp(d_aL), None)
+            return dX, d_aL
         _abi.call_cpu("gala_gat_bwd_stats_ex_f32", g.csr(), _hp(aL), _hp(aR), None, _hp(dY), dY.stride(0),
                       _hp(dY_rows), F, heads, slope, _hp(q), _hp(Y), Y.stride(0), _hp(Ym), Ym.stride(0), _hp(sma),
                       _hp(dX), dX.stride(0), _hp(d_aL), None)

@@ -609,13 +609,14 @@ class HaloGat:
         works = self._gather(self.dYs, dY)
         self._wait(ar_works)
         self._wait(works)
+        linear = linear and wR is not None
+        # with the Linear: dX += d_aR wR in the kernel's store (REF: d_aR = d_aL)
         dX, d_aL = self.be.gat_bwd_stats_table(self.graph, aL, self.As, self.dYs, self.own_rows("dY"), q, Y, Ym,
-                                               sma, H, self.slope)
+                                               sma, H, self.slope, wR=wR if linear else None)
         d_aL = d_aL.view(n, H)
-        if not (linear and wR is not None):
+        if not linear:
             return dX, d_aL
-        dW, db = self.be.head_linear_grads(self.own_rows("X"), d_aL, H)   # REF: d_aR = d_aL
-        self.be.head_attn_bwd(d_aL, wR, H, dX)
+        dW, db = self.be.head_linear_grads(self.own_rows("X"), d_aL, H)
         return dX, d_aL, dW, db
 
     def halo_bytes(self) -> int:

@@ -417,13 +417,19 @@ def gat_fwd_continue(g: DeviceGraph, aL, X, U0, S0, aR=None, wR=None, bR=None, h
     return (Y, q) if Um0 is None else (Y, q, Ym, sma)
 
 
-def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None, dY_rows=None):
+def gat_bwd_stats(g: DeviceGraph, aL, aR, dY, q, Y, Ym, sma, heads=1, slope=0.2, p=None, dY_rows=None, wR=None):
     """gala_gat_bwd_stats_f32 (REF): (dX, d_aL) from the forward's row statistics; gathers
     dY[col] only (alpha from aR, or from the forward's p when given).  dY_rows: dY is a
-    gathered table and dY_rows the rows' own dY (gala_gat_bwd_stats_ex_f32)."""
+    gathered table and dY_rows the rows' own dY (gala_gat_bwd_stats_ex_f32).  wR: dX also
+    takes the source logit's per-head Linear, d_aL * wR (gala_gat_bwd_stats_linear_f32)."""
     F = dY.shape[1]
     dX = _rows_like(dY, g.n_rows)
     d_aL = torch.empty(g.n_rows * heads, device=dY.device, dtype=torch.float32)
+    if wR is not None:
+        _abi.call("gala_gat_bwd_stats_linear_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(p), _dp(dY),
+                  dY.stride(0), _dp(dY_rows), F, heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0),
+                  _dp(sma), _dp(wR), _dp(dX), dX.stride(0), _dp(d_aL), _stream())
+        return dX, d_aL
     if dY_rows is not None:
         _abi.call("gala_gat_bwd_stats_ex_f32", g.csr((F + 3) // 4 * 4), _dp(aL), _dp(aR), _dp(p), _dp(dY),
                   dY.stride(0), _dp(dY_rows), F, heads, slope, _dp(q), _dp(Y), Y.stride(0), _dp(Ym), Ym.stride(0),

@@ -39,6 +39,7 @@ struct Backend {
     decltype(&gala_gat_bwd_fused_f32) gat_bwd_fused;
     decltype(&gala_gat_fwd_stats_f32) gat_fwd_stats;
     decltype(&gala_gat_bwd_stats_f32) gat_bwd_stats;
+    decltype(&gala_gat_bwd_stats_linear_f32) gat_bwd_stats_linear;
     decltype(&gala_head_attn_f32) head_attn;
     decltype(&gala_head_attn_bwd_f32) head_attn_bwd;
     decltype(&gala_edge_permute_f32) permute;
@@ -52,8 +53,8 @@ const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_edge_softmax_fwd_f32, gala_edge_softmax_bwd_f32, gala_gat_fwd_f32,
                    gala_gat_bwd_f32, gala_gat_fwd_attn_f32, gala_gat_bwd_attn_f32,
                    gala_gat_fwd_ex_f32, gala_gat_bwd_ex_f32, gala_gat_bwd_fused_f32,
-                   gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_head_attn_f32,
-                   gala_head_attn_bwd_f32,
+                   gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_gat_bwd_stats_linear_f32,
+                   gala_head_attn_f32, gala_head_attn_bwd_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
 const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
@@ -62,8 +63,8 @@ const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcas
                    gala_cpu_edge_softmax_bwd_f32, gala_cpu_gat_fwd_f32, gala_cpu_gat_bwd_f32,
                    gala_cpu_gat_fwd_attn_f32, gala_cpu_gat_bwd_attn_f32,
                    gala_cpu_gat_fwd_ex_f32, gala_cpu_gat_bwd_ex_f32, gala_cpu_gat_bwd_fused_f32,
-                   gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32, gala_cpu_head_attn_f32,
-                   gala_cpu_head_attn_bwd_f32,
+                   gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32, gala_cpu_gat_bwd_stats_linear_f32,
+                   gala_cpu_head_attn_f32, gala_cpu_head_attn_bwd_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32};
 
@@ -894,9 +895,10 @@ bool gat_forward_stats(const Slot &s, const torch::Tensor &l, const torch::Tenso
 }
 
 // REF backward from the row statistics: dX and d_aL (= d_aR) in one kernel that gathers
-// dY[col] only.
+// dY[col] only.  wR (defined): dX also takes the source logit's per-head Linear, d_aR * wR
+// (gala_gat_bwd_stats_linear_f32, bit-identical to a gala_head_attn_bwd_f32 pass after it).
 bool gat_backward_stats(const torch::Tensor &l, const GatStats &o, const torch::Tensor &dY_in, int64_t li,
-                        double slope, int heads, GatGrads &g) {
+                        double slope, int heads, GatGrads &g, const torch::Tensor &wR = torch::Tensor()) {
     Slot fw = slot(2 * li);
     const torch::Tensor dY = heads == 1 ? pad_rows4(dY_in) : dY_in.contiguous();
     const int64_t F = o.Y.size(1), nrows = fw.off.numel() / fw.segs - 1;
@@ -906,13 +908,20 @@ bool gat_backward_stats(const torch::Tensor &l, const GatStats &o, const torch::
     check_on(dY, fw.off, "grad");
     auto dX = rows_like(dY, nrows);
     auto daL = torch::empty_like(l);
-    const int st = be(fw.off).gat_bwd_stats(&cf.c, l.data_ptr<float>(), o.aR.data_ptr<float>(),
-                                            o.p.numel() > 0 ? o.p.data_ptr<float>() : nullptr,
-                                            dY.data_ptr<float>(), dY.stride(0), (int32_t)F, heads, (float)slope,
-                                            o.q.data_ptr<float>(), o.Y.data_ptr<float>(), o.Y.stride(0),
-                                            o.Ym.data_ptr<float>(), o.Ym.stride(0), o.sma.data_ptr<float>(),
-                                            dX.data_ptr<float>(), dX.stride(0), daL.data_ptr<float>(),
-                                            stream_of(fw.off));
+    const float *pp = o.p.numel() > 0 ? o.p.data_ptr<float>() : nullptr;
+    const int st = wR.defined()
+        ? be(fw.off).gat_bwd_stats_linear(&cf.c, l.data_ptr<float>(), o.aR.data_ptr<float>(), pp,
+                                          dY.data_ptr<float>(), dY.stride(0), nullptr, (int32_t)F, heads,
+                                          (float)slope, o.q.data_ptr<float>(), o.Y.data_ptr<float>(), o.Y.stride(0),
+                                          o.Ym.data_ptr<float>(), o.Ym.stride(0), o.sma.data_ptr<float>(),
+                                          wR.data_ptr<float>(), dX.data_ptr<float>(), dX.stride(0),
+                                          daL.data_ptr<float>(), stream_of(fw.off))
+        : be(fw.off).gat_bwd_stats(&cf.c, l.data_ptr<float>(), o.aR.data_ptr<float>(), pp,
+                                   dY.data_ptr<float>(), dY.stride(0), (int32_t)F, heads, (float)slope,
+                                   o.q.data_ptr<float>(), o.Y.data_ptr<float>(), o.Y.stride(0),
+                                   o.Ym.data_ptr<float>(), o.Ym.stride(0), o.sma.data_ptr<float>(),
+                                   dX.data_ptr<float>(), dX.stride(0), daL.data_ptr<float>(),
+                                   stream_of(fw.off));
     if (st == GALA_ERR_UNSUPPORTED) return false;
     check(st, "gala_gat_bwd_stats_f32");
     g = {daL, daL, dX};
@@ -1058,10 +1067,14 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         const double slope = ctx->saved_data["slope"].toDouble();
         torch::Tensor b = has_bias ? sv[3] : torch::Tensor();
         GatGrads g;
-        bool done = false;
+        bool done = false, fused_linear = false;
         if (stats) {
             const GatStats o{sv[6], q, sv[7], sv[8], sv[4], sv[9]};
-            done = gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g);
+            // several heads: the Linear's dX term goes into the kernel's dX store
+            fused_linear = heads > 1;
+            done = gat_backward_stats(l, o, grad_outputs[0], li, slope, heads, g,
+                                      fused_linear ? w.contiguous() : torch::Tensor());
+            fused_linear = fused_linear && done;
             alpha = torch::empty({0}, fopts(x));  // otherwise: the recomputed path below
         }
         if (!done && alpha.numel() == 0 && !gat_backward_recompute(l, {}, x, q, grad_outputs[0], li, slope, heads, w, b, g)) {
@@ -1090,9 +1103,10 @@ struct GatAggregateFfn : public torch::autograd::Function<GatAggregateFfn> {
         } else {  // per head: the block-diagonal Linear
             auto daR = g.daR.reshape({N, heads}).contiguous();
             head_linear_grads(x, daR, w, heads, dW, db);
-            check(be(x).head_attn_bwd(N, F, heads, daR.data_ptr<float>(), w.data_ptr<float>(),
-                                      g.dX.data_ptr<float>(), g.dX.stride(0), 1, stream_of(x)),
-                  "gala_head_attn_bwd_f32");  // dX[:, head h] += d_aR[:, h] wR[head h]
+            if (!fused_linear)
+                check(be(x).head_attn_bwd(N, F, heads, daR.data_ptr<float>(), w.data_ptr<float>(),
+                                          g.dX.data_ptr<float>(), g.dX.stride(0), 1, stream_of(x)),
+                      "gala_head_attn_bwd_f32");  // dX[:, head h] += d_aR[:, h] wR[head h]
         }
         return {g.daL.view_as(l), g.dX, dW.view_as(w), has_bias ? db.view_as(b) : torch::Tensor(),
                 torch::Tensor(), torch::Tensor(), torch::Tensor()};

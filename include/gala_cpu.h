@@ -100,6 +100,11 @@ int gala_cpu_gat_fwd_continue_f32(const gala_csr_t *A, const float *aL, const fl
                                   float slope, int32_t flags, const float *U0, int64_t ldu0, const float *S0, const float *Um0,
                                   int64_t ldum0, const float *M0, float *Y, int64_t ldy, float *q_out, float *Ym,
                                   int64_t ldym, float *sma, void *stream);
+int gala_cpu_gat_bwd_stats_linear_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *pe,
+                                      const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
+                                      float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
+                                      int64_t ldym, const float *sma, const float *wR, float *dX, int64_t lddx,
+                                      float *d_aL, void *stream);
 int gala_cpu_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *p,
                                   const float *dY, int64_t lddy, const float *dY_rows, int32_t F,
                                   int32_t heads, float slope, const float *q, const float *Y, int64_t ldy,

@@ -391,6 +391,19 @@ int gala_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float 
                               int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
                               void *stream);
 /*
+ * gala_gat_bwd_stats_linear_f32: gala_gat_bwd_stats_ex_f32 (dY_rows NULL: a square pattern)
+ * with the source logit's per-head Linear (aR = X wR + bR, the DSL's attnR = ffn(res, out=1),
+ * gala_head_attn_f32) folded into the dX store: dX[r, f] += d_aL[r, head(f)] * wR[f], REF's
+ * d_aR = d_aL (common.h:835-894 on the undirected pattern), with the product-then-sum
+ * roundings of gala_head_attn_bwd_f32 -- bit-identical to that pass after the statistics
+ * backward, without re-reading and re-writing dX.
+ */
+int gala_gat_bwd_stats_linear_f32(const gala_csr_t *A, const float *aL, const float *aR, const float *p,
+                                  const float *dY, int64_t lddy, const float *dY_rows, int32_t F, int32_t heads,
+                                  float slope, const float *q, const float *Y, int64_t ldy, const float *Ym,
+                                  int64_t ldym, const float *sma, const float *wR, float *dX, int64_t lddx,
+                                  float *d_aL, void *stream);
+/*
  * gala_gat_fwd_partial_stats_f32: gala_gat_fwd_stats_f32 over the columns one rank of a
  * vertex cut holds, every output unnormalised so that the rows' owners add the ranks'
  * partials before they divide (GALA_GAT_PARTIAL of gala_gat_fwd_ex_f32, plus the row

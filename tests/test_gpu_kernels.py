@@ -1034,3 +1034,27 @@ def test_gat_continue_matches_one_pass(F, heads, rc):
     Y, q = ops.gat_fwd_continue(halves[1], aL, X, Y, s, aR=Ar, heads=heads)
     torch.testing.assert_close(Y, want[0], rtol=2e-5, atol=1e-6)
     torch.testing.assert_close(q.reshape(-1), want[1].reshape(-1), rtol=2e-5, atol=0.0)
+
+
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4)])
+@pytest.mark.parametrize("split", [False, True])
+def test_gat_bwd_stats_linear_bitexact(F, heads, split):
+    """gala_gat_bwd_stats_linear_f32: the attention Linear's dX term folded into the statistics
+    backward's store equals gala_gat_bwd_stats_f32 followed by gala_head_attn_bwd_f32
+    accumulating into dX, bit for bit -- hub rows included (the fixup adds it), d_aL
+    unchanged."""
+    g = powerlaw()
+    aL = dev(features(g.n_rows, heads, seed=81))
+    X = dev(features(g.n_cols, F, seed=82))
+    dY = dev(features(g.n_rows, F, seed=83))
+    wR = dev(features(1, F, seed=84).ravel() * 0.5)
+    bR = dev(features(1, heads, seed=85).ravel())
+    dg = ops.DeviceGraph.from_host(g, split=False)
+    if split:
+        dg.set_split_plan(g.rowptr, 64, chunk=32, row_order=True)
+    Y, q, Ym, sma, aR = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=heads, want_aR=True)
+    dX0, daL0 = ops.gat_bwd_stats(dg, aL, aR, dY, q, Y, Ym, sma, heads=heads)
+    ops.head_attn_bwd(daL0.view(-1, heads), wR, heads=heads, dX=dX0, n_rows=g.n_rows)
+    dX1, daL1 = ops.gat_bwd_stats(dg, aL, aR, dY, q, Y, Ym, sma, heads=heads, wR=wR)
+    assert torch.equal(daL1, daL0)
+    assert torch.equal(dX1, dX0)
