@@ -469,3 +469,31 @@ def test_gat_continue_matches_one_pass(rc, which):
         _abi.call_cpu("gala_gat_fwd_continue_f32", g1.csr(), aL.data_ptr(), Ar.data_ptr(), None, None,
                       X.data_ptr(), F, F, H, 0.2, 0, U.data_ptr(), F, S.data_ptr(), None, 0, None, U.data_ptr(), F,
                       S.data_ptr(), Um.data_ptr(), F, M.data_ptr(), None)
+
+
+def test_gat_bwd_stats_linear_matches_two_passes():
+    """gala_cpu_gat_bwd_stats_linear_f32: the statistics backward with the attention Linear's
+    dX term folded in equals gala_cpu_gat_bwd_stats_ex_f32 followed by
+    gala_cpu_head_attn_bwd_f32 (d_aL identical, dX to one rounding); a missing wR is refused."""
+    import torch
+    from gala.backend import CpuBackend
+    g = powerlaw(n=1500, m=9000)
+    H, F = 4, 32
+    rng = np.random.default_rng(12)
+    t = lambda a: torch.from_numpy(a.astype(np.float32))  # noqa: E731
+    X, aL, dY = t(rng.uniform(-1, 1, (g.n_rows, F))), t(rng.uniform(-1, 1, (g.n_rows, H))), \
+        t(rng.uniform(-1, 1, (g.n_rows, F)))
+    wR, bR = t(rng.uniform(-0.5, 0.5, F)), t(rng.uniform(-0.5, 0.5, H))
+    be = CpuBackend()
+    cg = be.graph(g)
+    aR = be.head_attn(X, wR, bR, H)
+    Y, q, Ym, sma = be.gat_stats_table(cg, aL, aR, X, H, 0.2, None, None)
+    dX0, daL0 = be.gat_bwd_stats_table(cg, aL, aR, dY, None, q, Y, Ym, sma, H, 0.2)
+    be.head_attn_bwd(daL0.view(-1, H), wR, H, dX0)
+    dX1, daL1 = be.gat_bwd_stats_table(cg, aL, aR, dY, None, q, Y, Ym, sma, H, 0.2, wR=wR)
+    np.testing.assert_array_equal(daL1.numpy(), daL0.numpy())
+    np.testing.assert_allclose(dX1.numpy(), dX0.numpy(), rtol=1e-6, atol=1e-7)
+    with pytest.raises(_abi.GalaError):
+        _abi.call_cpu("gala_gat_bwd_stats_linear_f32", cg.csr(), aL.data_ptr(), aR.data_ptr(), None, dY.data_ptr(),
+                      F, None, F, H, 0.2, q.data_ptr(), Y.data_ptr(), F, Ym.data_ptr(), F, sma.data_ptr(), None,
+                      dX1.data_ptr(), F, daL1.data_ptr(), None)
