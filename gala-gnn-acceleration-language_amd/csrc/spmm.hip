@@ -334,6 +334,152 @@ __global__ __launch_bounds__(kBlock) void k_spmm_fixup(SpmmParams p, SplitParams
     store_row<VEC, G, CH, W>(p, cl, row, acc);
 }
 
+// ---- hub rows in the reference's order ----------------------------------------------
+// A hub row (deg > plan threshold) summed sequentially in CSR order, like every other row,
+// so the result is bit-identical to the reference's serial row loop (cuda.h:286-358) --
+// the REF parity mode.  One row group of G lanes would walk such a row one U-edge batch at
+// a time, a dependent col -> X load chain per batch (a 388 K-edge R-MAT hub: ~100 ms).
+// Instead one workgroup of kHubThreads lanes owns (row, slice of kHubSlice features): every
+// lane gathers X rows of a tile of T edges into registers (kHubTile floats in flight per
+// workgroup, the next tile's column indices already loaded), the tile goes to LDS, and wave 0
+// -- one lane per feature of the slice -- runs the row's add chain over the tile from LDS
+// while the next tile's gathers are in flight.  The chain keeps the per-feature operation
+// order and rounding of accumulate<> exactly.
+constexpr int kHubThreads = 512;
+constexpr int kHubSlice = 64;      // features per workgroup (one chain lane each)
+constexpr int kHubTile = 16384;    // floats of X per tile (64 KB of LDS)
+constexpr int kHubMaxT = 4096;     // edges per tile at most (the src-scale array)
+
+struct HubParams {
+    const int32_t *rows;           // hub row ids
+    const int32_t *order;          // nullable: the plan's descending-degree row order
+    int64_t n_hub;
+    int32_t n_slices;              // ceil(F / kHubSlice)
+};
+
+template <int VEC, bool W, bool SRCS>
+__global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, HubParams hp) {
+    typedef typename VecT<VEC>::T V;
+    constexpr int R = kHubTile / (VEC * kHubThreads);  // vector loads per lane per tile
+    extern __shared__ float hub_lds[];
+    const int64_t ri = blockIdx.x / hp.n_slices;
+    const int slice = blockIdx.x % hp.n_slices;
+    // the plan's descending-degree row order starts with exactly the hub rows: the longest
+    // serial chains are dispatched first
+    const int64_t row = hp.order ? hp.order[ri] : hp.rows[ri];
+    const int f0 = slice * kHubSlice;
+    const int fs = (p.F - f0) < kHubSlice ? (p.F - f0) : kHubSlice;  // features of the slice
+    const int lpe = (fs + VEC - 1) / VEC;                             // vectors per edge
+    const int fsp = lpe * VEC;                                        // LDS row width
+    int T = R * kHubThreads / lpe;
+    if (T > kHubMaxT) T = kHubMaxT;
+    float *tile = hub_lds;
+    float *scl = hub_lds + (int64_t)T * fsp;
+    const int64_t e0 = p.rowptr[row], n = (int64_t)p.rowptr[row + 1] - e0;
+    const int ntiles = (int)((n + T - 1) / T);
+    // this lane's load slots: (edge in tile, vector of the slice); fixed for every tile
+    int s_edge[R], s_off[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int i = k * kHubThreads + threadIdx.x;
+        s_edge[k] = i / lpe < T ? i / lpe : -1;
+        s_off[k] = (i % lpe) * VEC;
+    }
+    auto load_cols = [&](int t, int32_t (&c)[R]) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            int64_t j = (int64_t)t * T + (s_edge[k] < 0 ? 0 : s_edge[k]);
+            if (j >= n) j = n - 1;  // clamped: a valid address, never used
+            c[k] = p.col[e0 + j];
+        }
+    };
+    int32_t cc[R];
+    V xr[R];
+    float sr[R];
+    auto load_x = [&]() {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            xr[k] = ldv<VEC>(p.X + (int64_t)cc[k] * p.ldx + f0 + s_off[k]);
+            if (SRCS) sr[k] = p.src_scale[cc[k]];
+        }
+    };
+    // chain state (wave 0, lane f < fs owns feature f0 + f)
+    const int lane = threadIdx.x;
+    const bool chain = lane < fs;
+    const int f = f0 + (chain ? lane : 0);
+    const int head = W ? f / p.head_dim : 0;
+    const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + head] : 1.0f;
+    float acc = 0.0f;
+    if (chain && p.accum && p.dst_scale == nullptr) acc = p.Y[row * p.ldy + f];
+
+    if (ntiles > 0) {
+        load_cols(0, cc);
+        load_x();
+        if (ntiles > 1) load_cols(1, cc);
+    }
+    for (int t = 0; t < ntiles; ++t) {
+        __syncthreads();  // the chain is done with the previous tile
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (s_edge[k] < 0) continue;
+            stv<VEC>(tile + (int64_t)s_edge[k] * fsp + s_off[k], xr[k]);
+            if (SRCS && s_off[k] == 0) scl[s_edge[k]] = sr[k];
+        }
+        __syncthreads();
+        if (t + 1 < ntiles) {
+            load_x();                           // tile t+1's rows, in flight during the chain
+            if (t + 2 < ntiles) load_cols(t + 2, cc);
+        }
+        if (threadIdx.x < kWave) {
+            // the add chain, 8 edges per group, the next group's LDS reads (and weights) in
+            // flight while the current group is added (software-pipelined: the dependent
+            // adds, not LDS latency, set the pace)
+            const int64_t base = (int64_t)t * T;
+            const int cnt = (int)((n - base) < T ? (n - base) : T);
+            const int cl = chain ? lane : 0;
+            constexpr int GS = 8;
+            float xa[GS], wa[GS], sa[GS], xb[GS], wb[GS], sb[GS];
+            auto fetch = [&](int j, float (&x)[GS], float (&w)[GS], float (&s)[GS]) {
+#pragma unroll
+                for (int u = 0; u < GS; ++u) {
+                    const int jj = (j + u < cnt) ? j + u : cnt - 1;
+                    x[u] = tile[jj * fsp + cl];
+                    if (SRCS) s[u] = scl[jj];
+                    if (W) w[u] = p.val[(e0 + base + jj) * p.val_heads + head];
+                }
+            };
+            auto add = [&](const float &x, const float &w, const float &s) {
+                const float v = SRCS ? __fmul_rn(s, x) : x;
+                if (W) acc = fmaf(p.val_rs ? __fmul_rn(w, rs) : w, v, acc);
+                else acc = __fadd_rn(acc, v);
+            };
+            int j = 0;
+            if (cnt >= 2 * GS) {
+                fetch(0, xa, wa, sa);
+                for (; j + 2 * GS <= cnt; j += 2 * GS) {
+                    fetch(j + GS, xb, wb, sb);
+#pragma unroll
+                    for (int u = 0; u < GS; ++u) add(xa[u], wa[u], sa[u]);
+                    if (j + 2 * GS < cnt) fetch(j + 2 * GS, xa, wa, sa);
+#pragma unroll
+                    for (int u = 0; u < GS; ++u) add(xb[u], wb[u], sb[u]);
+                }
+            }
+            for (; j < cnt; ++j) {
+                const float ww = W ? p.val[(e0 + base + j) * p.val_heads + head] : 1.0f;
+                add(tile[j * fsp + cl], ww, SRCS ? scl[j] : 1.0f);
+            }
+        }
+    }
+    if (!chain) return;
+    float out = acc;
+    if (p.dst_scale) {
+        out = __fmul_rn(p.dst_scale[row], out);
+        if (p.accum) out = __fadd_rn(p.Y[row * p.ldy + f], out);
+    }
+    p.Y[row * p.ldy + f] = out;
+}
+
 // ---- degree: deg[r] = sum_e (val_e | 1), optionally ^power --------------------------
 struct DegParams {
     const int32_t *rowptr;
@@ -397,6 +543,32 @@ static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t 
         hipLaunchKernelGGL((k_spmm_fixup<VEC, G, CH, W>), dim3((unsigned)fb), dim3(kBlock), 0, st, p,
                            *sp);
     }
+}
+
+template <int VEC, bool W, bool SRCS>
+static void launch_hub_t(const SpmmParams &p, const HubParams &hp, hipStream_t st) {
+    constexpr size_t lds = (size_t)(kHubTile + (SRCS ? kHubMaxT : 0)) * sizeof(float);
+    // more than the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once
+    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, W, SRCS>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)opted;
+    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, W, SRCS>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
+                       dim3(kHubThreads), lds, st, p, hp);
+}
+
+static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w, bool srcs, hipStream_t st) {
+#define GALA_HUB(V)                                                    \
+    if (w) {                                                           \
+        if (srcs) launch_hub_t<V, true, true>(p, hp, st);              \
+        else launch_hub_t<V, true, false>(p, hp, st);                  \
+    } else {                                                           \
+        if (srcs) launch_hub_t<V, false, true>(p, hp, st);             \
+        else launch_hub_t<V, false, false>(p, hp, st);                 \
+    }
+    if (vec == 4) { GALA_HUB(4) }
+    else if (vec == 2) { GALA_HUB(2) }
+    else { GALA_HUB(1) }
+#undef GALA_HUB
 }
 
 template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
@@ -471,7 +643,8 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     int st = check_csr(A);
     if (st) return st;
     if (F < 0 || ldx < F || ldy < F ||
-        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT)))
+        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT | GALA_SPMM_HUB_CHUNKED)) ||
+        ((flags & GALA_SPMM_EXACT) && (flags & GALA_SPMM_HUB_CHUNKED)))
         return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
@@ -490,8 +663,11 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     int vec = 4;
     const bool one_head = !w || A->val_heads == 1;
     const gala_split_plan_t *plan = A->split;
-    const bool use_split =
-        plan && plan->n_chunks > 0 && A->n_seg == 1 && !samp && !(flags & GALA_SPMM_EXACT);
+    // hub rows: by default (REF order) summed sequentially by k_spmm_hub_exact; with
+    // GALA_SPMM_HUB_CHUNKED as chunk partials + an ordered fix-up (the fast, reordered mode)
+    const bool has_hubs = plan && plan->n_rows_split > 0 && A->n_seg == 1 && !samp;
+    const bool use_split = has_hubs && plan->n_chunks > 0 && (flags & GALA_SPMM_HUB_CHUNKED);
+    const bool use_hub = has_hubs && !use_split;
     auto ok = [&](int v) {
         const int64_t Fv = ((int64_t)F + v - 1) / v * v;
         const bool fits = (F % v == 0 && head_dim % v == 0) || (one_head && ldx >= Fv && ldy >= Fv);
@@ -547,6 +723,17 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
         p.split_threshold = plan->threshold;
         sp = &spl;
     }
+    HubParams hp{};
+    hipStream_t hub_st = hs;
+    if (use_hub) {
+        if (plan->threshold < 1 || !plan->rows) return GALA_ERR_INVALID_ARG;
+        p.split_threshold = plan->threshold;  // the row kernel leaves hub rows to k_spmm_hub_exact
+        hp.rows = plan->rows;
+        hp.order = plan->row_order;
+        hp.n_hub = plan->n_rows_split;
+        // the hub rows run beside the row kernel on the plan's side stream when it has one
+        if (plan->aux_stream && plan->aux_events[0] && plan->aux_events[1]) hub_st = (hipStream_t)plan->aux_stream;
+    }
 
     // feature chunks wider than 512 vectors per lane-group are split over launches
     const int64_t max_cols = 512LL * vec;
@@ -567,12 +754,28 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
             q.accum = accum;
             const int L = (int)((Fc + vec - 1) / vec);
             int r;
+            if (use_hub) {  // the long serial rows first, so their workgroups are dispatched first
+                hp.n_slices = (Fc + kHubSlice - 1) / kHubSlice;
+                if (hub_st != hs) {
+                    if (hipEventRecord((hipEvent_t)plan->aux_events[0], hs) != hipSuccess ||
+                        hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)
+                        return launch_status();
+                }
+                launch_hub(q, hp, vec, w, src_scale != nullptr, hub_st);
+                r = launch_status();
+                if (r) return r;
+            }
             if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs);
             else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
             else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
             if (r) return r;
             r = launch_status();
             if (r) return r;
+            if (use_hub && hub_st != hs) {  // join: the caller's stream waits for the hub rows
+                if (hipEventRecord((hipEvent_t)plan->aux_events[1], hub_st) != hipSuccess ||
+                    hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events[1], 0) != hipSuccess)
+                    return launch_status();
+            }
         }
     }
     return GALA_OK;

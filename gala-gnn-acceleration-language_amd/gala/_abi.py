@@ -24,6 +24,7 @@ GALA_ERR_GRAPH = -4
 GALA_SPMM_ACCUM = 0x1
 GALA_SPMM_SAMPLE = 0x2
 GALA_SPMM_EXACT = 0x4
+GALA_SPMM_HUB_CHUNKED = 0x8
 GALA_SDDVV_ADD = 0
 GALA_SDDVV_MUL = 1
 GALA_SDDVV_ADD_LRELU = 2
@@ -44,6 +45,8 @@ class gala_split_plan_t(ctypes.Structure):
         ("workspace", ctypes.c_void_p),
         ("ws_cols", ctypes.c_int64),
         ("row_order", ctypes.c_void_p),
+        ("aux_stream", ctypes.c_void_p),
+        ("aux_events", ctypes.c_void_p * 2),
     ]
 
 

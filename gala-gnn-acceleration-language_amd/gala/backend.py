@@ -24,10 +24,13 @@ from .layout import HostGraph
 class HipBackend:
     name = "hip"
 
-    def __init__(self, device="cuda"):
+    def __init__(self, device="cuda", hub="exact"):
         from . import ops
         self.ops = ops
         self.device = torch.device(device)
+        # hub rows of a split plan: "exact" (the reference's order, bit-identical) or
+        # "chunked" (GALA_SPMM_HUB_CHUNKED, the fast mode)
+        self.hub = hub
 
     def graph(self, hg: HostGraph, split="auto"):
         return self.ops.DeviceGraph.from_host(hg, self.device, split=split)
@@ -35,7 +38,7 @@ class HipBackend:
     def spmm(self, g, X, out, dst_scale=None, accum=False, samp=None):
         """samp (nsamp, ra, rb): the kernel-sampled aggregation (GALA_SPMM_SAMPLE)."""
         if samp is None:
-            return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum)
+            return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum, hub=self.hub)
         return self.ops.spmm(g, X, out=out, dst_scale=dst_scale, accum=accum, nsamp=samp[0], ra=samp[1], rb=samp[2])
 
     def row_broadcast(self, scale, X, out):
@@ -148,6 +151,7 @@ def _hp(t: torch.Tensor):
 class CpuBackend:
     name = "cpu"
     device = torch.device("cpu")
+    hub = "exact"   # the host rows are always one sequential pass
 
     def graph(self, hg: HostGraph, split="auto"):
         return CpuGraph(hg)

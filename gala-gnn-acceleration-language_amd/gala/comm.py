@@ -15,6 +15,29 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+# RCCL 2.26.6 (the torch 2.10 ROCm wheel's librccl) returns wrong rows from an
+# all_to_all_single whose payload exceeds 2 GiB: from about 1 GiB on, half the rows are
+# wrong (tools/a2a_probe.py on MI355X, profiles/r04_rccl_a2a_probe.jsonl; reduce_scatter is
+# exact at the same sizes).  That was the round-3 divergence of the sparse vertex-cut
+# exchange at config 5's 11.1 M-row shape (5.7 GB per all-to-all).  Every all-to-all and
+# point-to-point message is therefore cut into rounds of at most MAX_MSG_BYTES in all.
+MAX_MSG_BYTES = 1 << 30
+
+
+class _Works:
+    """Several async collectives waited on as one (a chunked all-to-all)."""
+
+    def __init__(self, works):
+        self.works = [w for w in works if w is not None]
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def _row_bytes(t: torch.Tensor) -> int:
+    return max(t[0].numel() if t.dim() > 1 else 1, 1) * t.element_size()
+
 
 class Comm:
     def __init__(self, group=None):
@@ -75,12 +98,34 @@ class Comm:
         dist.all_to_all_single(ho, self._host(inp), group=self.group)
         self._back(out, ho)
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, max_rows=None):
         """Uneven all-to-all of rows: inp's blocks of in_splits[q] rows go to rank q, out
-        receives out_splits[q] rows from rank q (in rank order).  Async on RCCL."""
+        receives out_splits[q] rows from rank q (in rank order).  Async on RCCL.
+        max_rows: a bound on every block's rows that ALL ranks pass alike (it fixes the
+        number of rounds when the exchange is cut at MAX_MSG_BYTES); default: this rank's
+        largest block, which is only safe when no rank's exchange needs cutting."""
         if self.rccl:
-            return dist.all_to_all_single(out, inp, output_split_sizes=list(out_splits),
-                                          input_split_sizes=list(in_splits), group=self.group, async_op=True)
+            in_splits, out_splits = [int(v) for v in in_splits], [int(v) for v in out_splits]
+            rb = _row_bytes(inp if inp.numel() else out)
+            r = max(MAX_MSG_BYTES // (self.world * rb), 1)
+            m = max(in_splits + out_splits + [0]) if max_rows is None else int(max_rows)
+            rounds = -(-m // r)
+            if rounds <= 1:
+                return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                                              input_split_sizes=in_splits, group=self.group, async_op=True)
+            io = [0] * self.world
+            oo = [0] * self.world
+            for q in range(1, self.world):
+                io[q] = io[q - 1] + in_splits[q - 1]
+                oo[q] = oo[q - 1] + out_splits[q - 1]
+            works = []
+            for j in range(rounds):
+                ins = [inp[io[q] + min(j * r, in_splits[q]):io[q] + min((j + 1) * r, in_splits[q])]
+                       for q in range(self.world)]
+                outs = [out[oo[q] + min(j * r, out_splits[q]):oo[q] + min((j + 1) * r, out_splits[q])]
+                        for q in range(self.world)]
+                works.append(dist.all_to_all(outs, ins, group=self.group, async_op=True))
+            return _Works(works)
         ho = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(ho, self._host(inp), output_split_sizes=list(out_splits),
                                input_split_sizes=list(in_splits), group=self.group)
@@ -90,8 +135,12 @@ class Comm:
     def exchange(self, sends, recvs):
         """Grouped point-to-point: sends = [(tensor, peer)], recvs = [(tensor, peer)]."""
         if self.rccl:
-            ops = [dist.P2POp(dist.isend, t, q, self.group) for t, q in sends]
-            ops += [dist.P2POp(dist.irecv, t, q, self.group) for t, q in recvs]
+            # messages past MAX_MSG_BYTES go as row pieces, in order (both ends cut alike)
+            def pieces(t):
+                r = max(MAX_MSG_BYTES // _row_bytes(t), 1)
+                return [t] if t.shape[0] <= r else [t[i:i + r] for i in range(0, t.shape[0], r)]
+            ops = [dist.P2POp(dist.isend, p, q, self.group) for t, q in sends for p in pieces(t)]
+            ops += [dist.P2POp(dist.irecv, p, q, self.group) for t, q in recvs for p in pieces(t)]
             return dist.batch_isend_irecv(ops) if ops else []
         hs = [(self._host(t), q) for t, q in sends]
         hr = [(torch.empty(t.shape, dtype=t.dtype), t, q) for t, q in recvs]

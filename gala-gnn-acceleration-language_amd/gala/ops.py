@@ -90,7 +90,16 @@ class DeviceGraph:
         plan.rows, plan.row_chunk0, plan.chunk_row = (a.data_ptr() for a in arrays)
         plan.workspace, plan.ws_cols = None, 0
         plan.row_order = None if order_t is None else order_t.data_ptr()
-        self._split = {"plan": plan, "arrays": arrays + (order_t,), "ws": None}
+        aux = None
+        if nr.value > 0 and dev.type == "cuda":
+            # the REF-order hub rows run beside the row kernel on a side stream (fork / join
+            # events recorded by the library on the caller's stream)
+            aux = (torch.cuda.Stream(device=dev), torch.cuda.Event(), torch.cuda.Event())
+            for ev in aux[1:]:
+                ev.record(aux[0])   # creates the event handles
+            plan.aux_stream = aux[0].cuda_stream
+            plan.aux_events[0], plan.aux_events[1] = aux[1].cuda_event, aux[2].cuda_event
+        self._split = {"plan": plan, "arrays": arrays + (order_t,), "ws": None, "aux": aux}
         self._csr = None
 
     @property
@@ -160,12 +169,19 @@ def _rows_like(X: torch.Tensor, n_rows: int, zero: bool = False) -> torch.Tensor
 
 
 def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=None,
-         accum=False, nsamp=None, ra=5, rb=7, exact=False) -> torch.Tensor:
+         accum=False, nsamp=None, ra=5, rb=7, exact=False, hub="exact") -> torch.Tensor:
+    """Y (+)= dst_scale * A (src_scale * X) (gala_spmm_f32).  hub: how the rows of the
+    graph's hub-row plan are summed -- "exact" (default, the reference's sequential CSR
+    order, bit-identical) or "chunked" (GALA_SPMM_HUB_CHUNKED: 512-edge chunk partials and
+    an ordered fix-up, the fast mode within fp32 summation rounding)."""
     F = X.shape[1]
     if out is None:
         out = _rows_like(X, g.n_rows, zero=accum)
+    if hub not in ("exact", "chunked"):
+        raise ValueError(f"spmm: hub {hub!r} (exact | chunked)")
+    chunked = hub == "chunked" and not exact
     flags = ((_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
-             | (_abi.GALA_SPMM_EXACT if exact else 0))
+             | (_abi.GALA_SPMM_EXACT if exact else 0) | (_abi.GALA_SPMM_HUB_CHUNKED if chunked else 0))
     _abi.call("gala_spmm_f32", g.csr(F), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
               _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, _stream())
     return out

@@ -284,8 +284,8 @@ class _PartialRows:
         if self.comm is None:       # one rank without collectives
             recv[c:d].copy_(send[a:b])
             return None
-        if self.sparse:
-            return self.comm.all_to_all(recv[c:d], send[a:b], self._rs[k], self._ss[k])
+        if self.sparse:   # every (chunk, owner) block has at most `block` rows, on every rank
+            return self.comm.all_to_all(recv[c:d], send[a:b], self._rs[k], self._ss[k], max_rows=self.part.block)
         return self.comm.reduce_scatter(recv[c:d], send[a:b])
 
     @staticmethod

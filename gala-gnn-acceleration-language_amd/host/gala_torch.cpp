@@ -273,7 +273,7 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
         check_dev(dsc, torch::kFloat, "dst_scale");
         ds = dsc.data_ptr<float>();
     }
-    const int32_t flags = nsamples > 0 ? GALA_SPMM_SAMPLE : 0;
+    const int32_t flags = nsamples > 0 ? GALA_SPMM_SAMPLE : spmm_hub_flag();
     check_on(x, offsets, "input_dense");
     if (ss) check_on(ssc, offsets, "src_scale");
     if (ds) check_on(dsc, offsets, "dst_scale");
@@ -287,6 +287,16 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
 }  // namespace
 
 // ---- split plans ----------------------------------------------------------------------
+int32_t spmm_hub_flag() {
+    static const int32_t f = [] {
+        const char *v = std::getenv("GALA_SPMM_HUB");
+        if (!v || !*v || std::string(v) == "exact") return 0;
+        TORCH_CHECK(std::string(v) == "chunked", "GALA_SPMM_HUB: exact | chunked, got ", v);
+        return (int32_t)GALA_SPMM_HUB_CHUNKED;
+    }();
+    return f;
+}
+
 void SplitState::ensure_workspace(int64_t F) {
     F = (F + 3) / 4 * 4;  // chunk rows hold whole float4 vectors (padded rows included)
     if (plan.ws_cols >= F) return;
@@ -330,6 +340,16 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
         auto order = torch::empty({n}, io);
         check(gala_host_row_order(n, r, order.data_ptr<int32_t>()), "gala_host_row_order");
         st->row_order = order.to(offsets.device());
+    }
+    if (nr > 0 && offsets.is_cuda()) {
+        // the REF-order hub rows run on a side stream beside the row kernel
+        auto aux = c10::hip::getStreamFromPool(false, offsets.device().index());
+        st->plan.aux_stream = (void *)aux.stream();
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t ev = nullptr;
+            TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+            st->aux_events[i] = st->plan.aux_events[i] = (void *)ev;
+        }
     }
     st->plan.threshold = thr;
     st->plan.chunk = chunk;

@@ -34,8 +34,14 @@ namespace gala {
 struct SplitState {
     gala_split_plan_t plan{};
     torch::Tensor rows, row_chunk0, chunk_row, row_order, ws;
+    // the side stream (torch's pool) and fork / join events of the REF-order hub rows; the
+    // events are never destroyed (a plan may outlive the HIP runtime at process exit)
+    void *aux_events[2] = {nullptr, nullptr};
     void ensure_workspace(int64_t F);
 };
+// GALA_SPMM_HUB=chunked selects the fast, reordered hub-row mode (GALA_SPMM_HUB_CHUNKED)
+// for every SpMM of the mirror; unset or "exact": the reference's order (the default).
+int32_t spmm_hub_flag();
 // Builds the plan from the device rowptr (one D2H copy) when some row is longer than
 // max(1024, 8 * mean degree) (hub-row split) or the graph is skewed (max degree > 4 x
 // mean: descending-degree row order); returns nullptr otherwise or for tiled graphs.

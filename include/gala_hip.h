@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GALA_ABI_VERSION 2
+#define GALA_ABI_VERSION 3
 
 typedef enum gala_status {
     GALA_OK = 0,
@@ -58,19 +58,26 @@ typedef enum gala_status {
  *             cuda.h:472-499; here segment 0 is accumulated first, then 1, ...).
  * ---------------------------------------------------------------------------------- */
 /*
- * Optional split plan for power-law graphs: rows longer than `threshold` edges are cut
- * into chunks of `chunk` edges that run in parallel; each chunk writes a partial sum to
- * `workspace` and a fix-up pass adds the partials of a row in chunk order.  Built once per
- * graph on the host with gala_host_split_plan; only used for n_seg == 1.  Rows that are
- * split are summed per chunk (not in one sequential pass), so their results match the
- * reference within fp32 rounding instead of bit for bit; GALA_SPMM_EXACT disables it.
+ * Optional split plan for power-law graphs, built once per graph on the host with
+ * gala_host_split_plan (only used for n_seg == 1).  Rows longer than `threshold` edges are
+ * hub rows.  By default (REF order, the reference's serial row loop, cuda.h:286-358) the
+ * SpMM sums a hub row sequentially in CSR order like every other row -- bit-identical to
+ * the reference -- in a dedicated kernel whose workgroup gathers a tile of the row's
+ * neighbour rows while one wave runs the row's add chain (k_spmm_hub_exact); with
+ * `aux_stream` and `aux_events` set it runs on that stream beside the row kernel (an
+ * event fork / join on the caller's stream: stream-ordered, hipGraph-capturable).  With
+ * GALA_SPMM_HUB_CHUNKED (the fast, reordered mode) a hub row is instead cut into chunks of
+ * `chunk` edges that run in parallel; each chunk writes a partial sum to `workspace` and a
+ * fix-up pass adds the partials of a row in chunk order, so those rows match the reference
+ * within fp32 summation rounding instead of bit for bit.  The GAT and edge kernels always
+ * use the chunks (their row sums are reductions the GPU regroups anyway).
  */
 typedef struct gala_split_plan {
-    int32_t threshold;         /* rows with deg > threshold are split                    */
+    int32_t threshold;         /* rows with deg > threshold are hub rows                 */
     int32_t chunk;             /* edges per chunk                                        */
     int64_t n_rows_split;
     int64_t n_chunks;
-    const int32_t *rows;       /* device [n_rows_split]: split row ids (ascending)       */
+    const int32_t *rows;       /* device [n_rows_split]: hub row ids (ascending)         */
     const int32_t *row_chunk0; /* device [n_rows_split+1]: first chunk of each split row  */
     const int32_t *chunk_row;  /* device [n_chunks]: index into rows[] of every chunk    */
     float *workspace;          /* device [n_chunks * ws_cols] partial results            */
@@ -80,7 +87,12 @@ typedef struct gala_split_plan {
                                   rows sharing a wavefront have similar lengths on skewed
                                   graphs; results are unchanged (every row is still one
                                   sequential pass).  A plan may carry only a row order
-                                  (n_chunks == 0).                                       */
+                                  (n_chunks == 0).  With hub rows it must be that order
+                                  of the same rowptr: its first n_rows_split entries are
+                                  then the hub rows, longest first, the order in which
+                                  the REF-order hub kernel takes them.                   */
+    void *aux_stream;          /* hipStream_t or NULL: where the REF-order hub rows run   */
+    void *aux_events[2];       /* hipEvent_t fork / join pair for aux_stream (both or none) */
 } gala_split_plan_t;
 
 typedef struct gala_csr {
@@ -114,7 +126,10 @@ int gala_last_hip_error(void);                 /* hipError_t of the last GALA_ER
                                  cuda.h:463 + 309-310); without it Y is overwritten       */
 #define GALA_SPMM_SAMPLE 0x2  /* kernel sampling: per row with deg>0, nsamp edges
                                  j = (ra*ji + rb) mod deg (cuda.h:313-321)                */
-#define GALA_SPMM_EXACT 0x4   /* ignore A->split: every row in one sequential pass       */
+#define GALA_SPMM_EXACT 0x4   /* every row in one sequential pass (the default since ABI 3;
+                                 kept as an explicit request; excludes HUB_CHUNKED)       */
+#define GALA_SPMM_HUB_CHUNKED 0x8 /* hub rows of A->split as chunk partials + ordered fix-up:
+                                 the fast mode, within fp32 summation rounding of REF     */
 
 /*
  * Y[r, 0:F] (+)= dst_scale[r] * sum_{e in row r} w_e * (src_scale[col_e] * X[col_e, 0:F])

@@ -42,7 +42,7 @@ def test_nm_exports():
 
 def test_version_and_status_strings():
     L = _abi.lib()
-    assert L.gala_abi_version() == 2
+    assert L.gala_abi_version() == 3
     assert L.gala_status_string(0) == b"GALA_OK"
     assert L.gala_status_string(-4) == b"GALA_ERR_GRAPH"
 

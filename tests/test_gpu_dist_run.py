@@ -114,7 +114,8 @@ def _khop_induced(rowptr, col, seeds, hops):
 def test_dist_run_config5_shape_at_size(tmp_path):
     """Config 5's program (bench/dsl/gcn3_papers10.txt, GCN-3 hidden 128, 172 classes) at
     1.1 M rows (--scale 0.1 of the 10 % papers100M shape) through the multi-rank runtime on
-    the one GPU: the vertex cut over RCCL at world 1 (--dist: its reduce-scatters run)
+    the one GPU: the vertex cut over RCCL at world 1 (--dist: its reduce-scatters, or with
+    --exchange sparse its uneven all-to-alls and receive-CSR sums, run)
     against the halo layout's exact mode (sampled rows' predictions and the loss curve
     within fp32 rounding), and the halo run's first forward against the float64 IR executor
     on sampled rows (their 3-hop induced subgraph, true degrees)."""
@@ -128,13 +129,14 @@ def test_dist_run_config5_shape_at_size(tmp_path):
     assert r.returncode == 0, r.stderr
     common = ("--scale", "0.1", "--dump-stride", "997")
     dh = _run_gpu(ir_path, tmp_path, 1, "halo", iters=3, extra=common)
-    dv = _run_gpu(ir_path, tmp_path, 1, "vcut", iters=3, extra=common + ("--layout", "vcut", "--dist"),
-                  backend="nccl")
     n = len(dh["rowptr"]) - 1
     assert n >= 1_000_000
-    np.testing.assert_array_equal(dv["rows"], dh["rows"])
-    np.testing.assert_allclose(dv["prediction"], dh["prediction"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(dv["losses"], dh["losses"], rtol=1e-4, atol=1e-6)
+    for exch in ("dense", "sparse"):
+        dv = _run_gpu(ir_path, tmp_path, 1, "vcut_" + exch, iters=3,
+                      extra=common + ("--layout", "vcut", "--dist", "--exchange", exch), backend="nccl")
+        np.testing.assert_array_equal(dv["rows"], dh["rows"])
+        np.testing.assert_allclose(dv["prediction"], dh["prediction"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(dv["losses"], dh["losses"], rtol=1e-4, atol=1e-6)
     ir = ref.load_ir(str(ir_path))["post"]
     seeds = dh["rows"][:: max(len(dh["rows"]) // 6, 1)][:6]
     rowptr, col = dh["rowptr"].astype(np.int64), dh["col"]

@@ -6,7 +6,8 @@ a head count, row padding, edge weights, a hub-row split plan with small chunks 
 tiling, then checks the HIP path against the oracle:
 
 * bit-exact: degree, SpMM without hub chunks, row-scale / row-broadcast;
-* reordered sums (hub chunks): within the worst-case fp32 summation bound of the row,
+* reordered sums (hub chunks, the GALA_SPMM_HUB_CHUNKED fast mode; the default REF order
+  is bit-exact): within the worst-case fp32 summation bound of the row,
   |err| <= (deg + 1) 2^-24 sum|a x| + 1e-6 per entry;
 * TOL (1e-4 abs + rel): SDDMM, edge softmax fwd / bwd, fused GAT forward / backward, the
   REF row-statistics backward's d_aL (its Y / q / dX bit-equal to the fused path's).
@@ -96,11 +97,10 @@ def test_random_case(seed):
     val = rng.uniform(0, 1, g.nnz).astype(np.float32)
     for w in (None, val):
         gd = dg if w is None else dg.with_values(_dev(w))
-        Y = _host(ops.spmm(gd, Xd))
-        if chunked:
-            _reordered_ok(Y, g, X, w)
-        else:
-            np.testing.assert_array_equal(Y, orc.spmm(og if w is None else to_oracle(g, w), X))
+        # REF order (default): bit-exact, hub rows included
+        np.testing.assert_array_equal(_host(ops.spmm(gd, Xd)), orc.spmm(og if w is None else to_oracle(g, w), X))
+        if chunked:   # the fast mode: hub rows as chunk partials
+            _reordered_ok(_host(ops.spmm(gd, Xd, hub="chunked")), g, X, w)
     # column-tiled layout (no split plan): segments summed in order, bit-exact
     if g.n_cols > 1 and not chunked:
         tg = layout.col_tile(g, int(rng.integers(1, g.n_cols)))

@@ -406,7 +406,8 @@ def assert_reordered_sum(Y, g, X, val=None, dst_scale=None, Y0=None):
     so the bound scales with the row's L1 mass: |Y - exact| <= 1e-6 * sum|A_e X_j| + 1e-6.
     (The reference's own sequential fp32 sum is no fixed point to compare with at 1e-4: on
     these hub rows it is itself up to 8e-4 from the exact sum, measured on MI355X; both sums
-    are within the L1 bound of it.  GALA_SPMM_EXACT keeps the sequential order, bit for bit.)
+    are within the L1 bound of it.)  This is the GALA_SPMM_HUB_CHUNKED fast mode only: the
+    default REF order sums every hub row sequentially, bit for bit.
     """
     import scipy.sparse as sp
     v = np.ones(g.nnz) if val is None else np.asarray(val, np.float64)
@@ -436,13 +437,17 @@ def test_spmm_split_hub_rows(F, weighted):
     assert dg.split_rows >= 2
     X = features(g.n_cols, F)
     ref = orc.spmm(to_oracle(hg), X)
+    # REF order (the default): hub rows summed sequentially by k_spmm_hub_exact -- within
+    # north_star's 1e-4 of the reference's sequential sum, in fact bit-identical
     Y = host(ops.spmm(dg, dev(X)))
-    assert_reordered_sum(Y, g, X, val)                         # split rows: chunked order
-    deg = np.diff(g.rowptr)
-    light = deg <= 1024
-    np.testing.assert_array_equal(Y[light], ref[light])       # other rows: still bit-exact
-    Ye = host(ops.spmm(dg, dev(X), exact=True))                # GALA_SPMM_EXACT: no split
-    np.testing.assert_array_equal(Ye, ref)
+    np.testing.assert_allclose(Y, ref, rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(Y, ref)
+    np.testing.assert_array_equal(host(ops.spmm(dg, dev(X), exact=True)), ref)   # GALA_SPMM_EXACT
+    # the fast mode: hub rows as chunk partials (reordered sum)
+    Yc = host(ops.spmm(dg, dev(X), hub="chunked"))
+    assert_reordered_sum(Yc, g, X, val)
+    light = np.diff(g.rowptr) <= 1024
+    np.testing.assert_array_equal(Yc[light], ref[light])     # other rows: still bit-exact
 
 
 @pytest.mark.parametrize("F", [1, 32, 47, 256])
@@ -458,13 +463,12 @@ def test_spmm_row_order_bitexact(F, weighted, hubs):
     dg = ops.DeviceGraph.from_host(layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, g.col, val), split=False)
     dg.set_split_plan(g.rowptr, 64 if hubs else 0, chunk=32, row_order=True)
     ref = orc.spmm(to_oracle(g, val), X)
-    got = host(ops.spmm(dg, dev(X)))
+    np.testing.assert_array_equal(host(ops.spmm(dg, dev(X))), ref)   # REF order: hub rows too
     if hubs:
+        got = host(ops.spmm(dg, dev(X), hub="chunked"))
         assert_reordered_sum(got, g, X, val)                     # split rows: chunked order
         light = np.diff(g.rowptr) <= 64
         np.testing.assert_array_equal(got[light], ref[light])  # the others: bit-exact
-    else:
-        np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(host(ops.spmm(dg, dev(X), nsamp=20)),
                                   orc.spmm(to_oracle(g, val), X, sample=True, nsamp=20))
 
@@ -475,12 +479,19 @@ def test_spmm_split_with_norms_and_accum():
     norm = (1.0 / np.sqrt(g.degrees().astype(np.float32))).astype(np.float32)
     X = features(g.n_cols, 32)
     Y0 = features(g.n_rows, 32, seed=3)
+    ref = orc.spmm(to_oracle(g), X, dst_scale=norm, Y=Y0.copy(), accum=True)
     Yt = dev(Y0)
     ops.spmm(dg, dev(X), dst_scale=dev(norm), out=Yt, accum=True)
-    ref = orc.spmm(to_oracle(g), X, dst_scale=norm, Y=Y0.copy(), accum=True)
+    np.testing.assert_array_equal(host(Yt), ref)                # REF order, hub rows included
+    Yt = dev(Y0)
+    ops.spmm(dg, dev(X), dst_scale=dev(norm), out=Yt, accum=True, hub="chunked")
     light = np.diff(g.rowptr) <= 1024
     np.testing.assert_allclose(host(Yt)[light], ref[light], **TOL)
     assert_reordered_sum(host(Yt), g, X, dst_scale=norm.astype(np.float64), Y0=Y0)
+    # accumulate without a dst scale starts from Y (the hub kernel too)
+    Yt = dev(Y0)
+    ops.spmm(dg, dev(X), out=Yt, accum=True)
+    np.testing.assert_array_equal(host(Yt), orc.spmm(to_oracle(g), X, Y=Y0.copy(), accum=True))
 
 
 @pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8)])
@@ -570,13 +581,10 @@ def test_padded_rows_float4_path(F, hubs):
     X = features(g.n_cols, F, seed=71)
     _, Xp = _padded(X, F, float("nan"))
     ybuf, Yp = _padded(np.zeros((g.n_rows, F), np.float32), F, 7.0)
-    # bit-identical to the unpadded (narrower-vector) launch on the same plan; that one is
-    # bit-exact vs the oracle without hub chunks, a reordered sum with them
+    # bit-identical to the unpadded (narrower-vector) launch on the same plan, and bit-exact
+    # vs the oracle (hub rows in REF order too)
     def check(Y, val=None):
-        if hubs:
-            assert_reordered_sum(Y, g, X, val)
-        else:
-            np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g, val), X))
+        np.testing.assert_array_equal(Y, orc.spmm(to_oracle(g, val), X))
     ops.spmm(dg, Xp, out=Yp)
     np.testing.assert_array_equal(host(Yp), host(ops.spmm(dg, dev(X))))
     check(host(Yp))
@@ -844,7 +852,8 @@ def test_gat_bwd_fused_recompute(F, heads, layout_, rc):
     else:
         assert torch.equal(Y, Y2) and torch.equal(q, q2)
     dX, daL = ops.gat_bwd_fused(dg, dev(aL), dev(X), dev(dY), q, heads=heads, **kw)
-    dX_ref = ops.spmm(dg.with_values(p, val_heads=heads, row_scale=q), dev(dY))
+    # the GAT kernels sum hub rows as chunk partials: the SpMM in the same (fast) mode
+    dX_ref = ops.spmm(dg.with_values(p, val_heads=heads, row_scale=q), dev(dY), hub="chunked")
     assert torch.equal(dX, dX_ref)
     og = to_oracle(g)
     _, al_ref = orc.gat_fwd(og, aL, aR, X, heads=heads, slope=0.2, mode=_abi.GALA_SOFTMAX_REF)

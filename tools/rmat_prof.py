@@ -30,8 +30,21 @@ def main():
     Y = torch.empty_like(X)
     dg = ops.DeviceGraph.from_host(hg)
     t = timer(lambda: ops.spmm(dg, X, out=Y), 10)
+    Ye = Y.clone()
+    tch = timer(lambda: ops.spmm(dg, X, out=Y, hub="chunked"), 10)
+    diff = float((Y - Ye).abs().max())
+    # the REF-order hub rows on the caller's stream (no side stream): serial cost
+    aux = dg._split["plan"].aux_stream
+    dg._split["plan"].aux_stream = None
+    dg._csr = None
+    tser = timer(lambda: ops.spmm(dg, X, out=Y), 10)
+    dg._split["plan"].aux_stream = aux
+    dg._csr = None
+    same = bool(torch.equal(Y, Ye))
     tc = bench.gather_ceiling(dg.col, X, timer)
-    print(json.dumps({"spmm_ms": t * 1e3, "split_rows": dg.split_rows,
+    print(json.dumps({"F": F, "spmm_exact_ms": t * 1e3, "spmm_chunked_ms": tch * 1e3,
+                      "spmm_exact_one_stream_ms": tser * 1e3, "one_stream_equal": same,
+                      "max_abs_exact_vs_chunked": diff, "split_rows": dg.split_rows,
                       "gather_ms": None if tc is None else tc * 1e3}), flush=True)
 
 
