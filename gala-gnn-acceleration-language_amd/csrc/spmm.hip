@@ -339,45 +339,56 @@ __global__ __launch_bounds__(kBlock) void k_spmm_fixup(SpmmParams p, SplitParams
 // so the result is bit-identical to the reference's serial row loop (cuda.h:286-358) --
 // the REF parity mode.  One row group of G lanes would walk such a row one U-edge batch at
 // a time, a dependent col -> X load chain per batch (a 388 K-edge R-MAT hub: ~100 ms).
-// Instead one workgroup of kHubThreads lanes owns (row, slice of kHubSlice features): every
+// Instead one workgroup of kHubThreads lanes owns (row, slice of FSP features): every
 // lane gathers X rows of a tile of T edges into registers (kHubTile floats in flight per
 // workgroup, the next tile's column indices already loaded), the tile goes to LDS, and wave 0
 // -- one lane per feature of the slice -- runs the row's add chain over the tile from LDS
 // while the next tile's gathers are in flight.  The chain keeps the per-feature operation
 // order and rounding of accumulate<> exactly.
 constexpr int kHubThreads = 512;
-constexpr int kHubSlice = 64;      // features per workgroup (one chain lane each)
 constexpr int kHubTile = 16384;    // floats of X per tile (64 KB of LDS)
-constexpr int kHubMaxT = 4096;     // edges per tile at most (the src-scale array)
 
 struct HubParams {
     const int32_t *rows;           // hub row ids
     const int32_t *order;          // nullable: the plan's descending-degree row order
     int64_t n_hub;
-    int32_t n_slices;              // ceil(F / kHubSlice)
+    int32_t n_slices;              // ceil(F / FSP)
 };
 
-template <int VEC, bool W, bool SRCS>
+// FSP: features per workgroup (32 or 64) = the LDS row stride, compile-time so the chain's
+// LDS addresses are immediate offsets; T = kHubTile / FSP edges per tile.  Everything the
+// chain reads comes from LDS (X rows, src scales, edge weights, the accumulate start value):
+// vmcnt counts in order, so a global load in the chain would wait for the next tile's gathers.
+constexpr int kHubMaxHeads = 4;    // edge-weight heads per slice staged in LDS
+template <int FSP, int TL>
+constexpr size_t hub_lds_floats() {
+    return (size_t)TL + (size_t)(TL / FSP) * (1 + kHubMaxHeads) + kWave;
+}
+
+template <int VEC, int FSP, bool W, bool SRCS, int TL = kHubTile>
 __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, HubParams hp) {
     typedef typename VecT<VEC>::T V;
-    constexpr int R = kHubTile / (VEC * kHubThreads);  // vector loads per lane per tile
+    constexpr int T = TL / FSP;                       // edges per tile
+    constexpr int R = TL / (VEC * kHubThreads);       // vector loads per lane per tile
+    constexpr int RW = T * kHubMaxHeads / kHubThreads;  // weight loads per lane per tile
     extern __shared__ float hub_lds[];
+    float *tile = hub_lds;                            // [T][FSP]
+    float *scl = tile + TL;                           // [T] src scales (SRCS)
+    float *wts = scl + T;                             // [T][hs] edge weights (W)
+    float *yinit = wts + T * kHubMaxHeads;            // [64] accumulate start values
     const int64_t ri = blockIdx.x / hp.n_slices;
     const int slice = blockIdx.x % hp.n_slices;
     // the plan's descending-degree row order starts with exactly the hub rows: the longest
     // serial chains are dispatched first
     const int64_t row = hp.order ? hp.order[ri] : hp.rows[ri];
-    const int f0 = slice * kHubSlice;
-    const int fs = (p.F - f0) < kHubSlice ? (p.F - f0) : kHubSlice;  // features of the slice
-    const int lpe = (fs + VEC - 1) / VEC;                             // vectors per edge
-    const int fsp = lpe * VEC;                                        // LDS row width
-    int T = R * kHubThreads / lpe;
-    if (T > kHubMaxT) T = kHubMaxT;
-    float *tile = hub_lds;
-    float *scl = hub_lds + (int64_t)T * fsp;
+    const int f0 = slice * FSP;
+    const int fs = (p.F - f0) < FSP ? (p.F - f0) : FSP;  // features of the slice
+    const int lpe = (fs + VEC - 1) / VEC;                // vectors per edge
+    const int h0 = W ? f0 / p.head_dim : 0;               // edge-weight heads of the slice
+    const int hs = W ? (f0 + fs - 1) / p.head_dim - h0 + 1 : 0;  // <= kHubMaxHeads (host)
     const int64_t e0 = p.rowptr[row], n = (int64_t)p.rowptr[row + 1] - e0;
     const int ntiles = (int)((n + T - 1) / T);
-    // this lane's load slots: (edge in tile, vector of the slice); fixed for every tile
+    // this lane's load slots (edge in tile, column in the slice), the same every tile
     int s_edge[R], s_off[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -385,93 +396,120 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
         s_edge[k] = i / lpe < T ? i / lpe : -1;
         s_off[k] = (i % lpe) * VEC;
     }
-    auto load_cols = [&](int t, int32_t (&c)[R]) {
+    int32_t cc[R];
+    V xr[R];
+    float sr[R], wr[RW > 0 ? RW : 1];
+    auto load_cols = [&](int t) {
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             int64_t j = (int64_t)t * T + (s_edge[k] < 0 ? 0 : s_edge[k]);
             if (j >= n) j = n - 1;  // clamped: a valid address, never used
-            c[k] = p.col[e0 + j];
+            cc[k] = p.col[e0 + j];
         }
     };
-    int32_t cc[R];
-    V xr[R];
-    float sr[R];
-    auto load_x = [&]() {
+    auto load_x = [&](int t) {
 #pragma unroll
         for (int k = 0; k < R; ++k) {
+            // unconditional (an unused slot's column is a valid one): branches around the
+            // loads would make the compiler wait for each load before issuing the next
             xr[k] = ldv<VEC>(p.X + (int64_t)cc[k] * p.ldx + f0 + s_off[k]);
             if (SRCS) sr[k] = p.src_scale[cc[k]];
         }
+        if (W) {  // weights (edge j, head h0 + k) at [j * hs + k], coalesced along the edges
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const int i = k * kHubThreads + threadIdx.x;
+                int64_t j = (int64_t)t * T + i / hs;
+                if (j >= n) j = n - 1;
+                wr[k] = i < T * hs ? p.val[(e0 + j) * p.val_heads + h0 + i % hs] : 0.0f;
+            }
+        }
     };
-    // chain state (wave 0, lane f < fs owns feature f0 + f)
+    // chain state: wave 0, lane f < fs owns feature f0 + f
     const int lane = threadIdx.x;
     const bool chain = lane < fs;
-    const int f = f0 + (chain ? lane : 0);
-    const int head = W ? f / p.head_dim : 0;
-    const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + head] : 1.0f;
+    const int cl = chain ? lane : 0;
+    const int f = f0 + cl;
+    const int hl = W ? f / p.head_dim - h0 : 0;
+    const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + h0 + hl] : 1.0f;
+    if (chain && p.accum && p.dst_scale == nullptr) yinit[lane] = p.Y[row * p.ldy + f];
     float acc = 0.0f;
-    if (chain && p.accum && p.dst_scale == nullptr) acc = p.Y[row * p.ldy + f];
+    auto add = [&](float x, float w, float s) {
+        const float v = SRCS ? __fmul_rn(s, x) : x;
+        if (W) acc = fmaf(p.val_rs ? __fmul_rn(w, rs) : w, v, acc);
+        else acc = __fadd_rn(acc, v);
+    };
 
     if (ntiles > 0) {
-        load_cols(0, cc);
-        load_x();
-        if (ntiles > 1) load_cols(1, cc);
+        load_cols(0);
+        load_x(0);
+        if (ntiles > 1) load_cols(1);
     }
     for (int t = 0; t < ntiles; ++t) {
         __syncthreads();  // the chain is done with the previous tile
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             if (s_edge[k] < 0) continue;
-            stv<VEC>(tile + (int64_t)s_edge[k] * fsp + s_off[k], xr[k]);
+            stv<VEC>(tile + s_edge[k] * FSP + s_off[k], xr[k]);
             if (SRCS && s_off[k] == 0) scl[s_edge[k]] = sr[k];
         }
+        if (W) {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const int i = k * kHubThreads + threadIdx.x;
+                if (i < T * hs) wts[i] = wr[k];
+            }
+        }
         __syncthreads();
+        if (t == 0 && chain && p.accum && p.dst_scale == nullptr) acc = yinit[lane];
         if (t + 1 < ntiles) {
-            load_x();                           // tile t+1's rows, in flight during the chain
-            if (t + 2 < ntiles) load_cols(t + 2, cc);
+            load_x(t + 1);              // tile t+1's rows, in flight during the chain
+            if (t + 2 < ntiles) load_cols(t + 2);
         }
         if (threadIdx.x < kWave) {
-            // the add chain, 8 edges per group, the next group's LDS reads (and weights) in
-            // flight while the current group is added (software-pipelined: the dependent
-            // adds, not LDS latency, set the pace)
-            const int64_t base = (int64_t)t * T;
-            const int cnt = (int)((n - base) < T ? (n - base) : T);
-            const int cl = chain ? lane : 0;
-            constexpr int GS = 8;
+            // the add chain over the tile, 16 edges per group, ping-pong: the next group's
+            // LDS reads are in flight while a group's dependent adds run.  The prefetch past
+            // the last full group is unconditional (no register copies at the loop edge): it
+            // reads at most GS rows past the tile, inside this kernel's LDS (scl, wts, yinit
+            // follow the tile), and is never consumed
+            const int cnt = (int)((n - (int64_t)t * T) < T ? (n - (int64_t)t * T) : T);
+            const float *xs = tile + cl;
+            const float *ws = wts + hl;
+            constexpr int GS = 16;
+            static_assert(GS * FSP <= T * (1 + kHubMaxHeads) + kWave, "prefetch stays in LDS");
             float xa[GS], wa[GS], sa[GS], xb[GS], wb[GS], sb[GS];
-            auto fetch = [&](int j, float (&x)[GS], float (&w)[GS], float (&s)[GS]) {
+            auto fetch = [&](int j, float (&x)[GS], float (&w)[GS], float (&sv)[GS]) {
 #pragma unroll
                 for (int u = 0; u < GS; ++u) {
-                    const int jj = (j + u < cnt) ? j + u : cnt - 1;
-                    x[u] = tile[jj * fsp + cl];
-                    if (SRCS) s[u] = scl[jj];
-                    if (W) w[u] = p.val[(e0 + base + jj) * p.val_heads + head];
+                    x[u] = xs[(j + u) * FSP];
+                    if (SRCS) sv[u] = scl[j + u];
+                    if (W) w[u] = ws[(j + u) * hs];
                 }
-            };
-            auto add = [&](const float &x, const float &w, const float &s) {
-                const float v = SRCS ? __fmul_rn(s, x) : x;
-                if (W) acc = fmaf(p.val_rs ? __fmul_rn(w, rs) : w, v, acc);
-                else acc = __fadd_rn(acc, v);
             };
             int j = 0;
-            if (cnt >= 2 * GS) {
+            const int full = cnt / (2 * GS) * (2 * GS);
+            if (full > 0) {
                 fetch(0, xa, wa, sa);
-                for (; j + 2 * GS <= cnt; j += 2 * GS) {
+                for (; j < full; j += 2 * GS) {
+                    // sched_barrier: keep each group's reads ahead of the other group's adds
+                    // (the scheduler otherwise sinks them to their first use)
                     fetch(j + GS, xb, wb, sb);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int u = 0; u < GS; ++u) add(xa[u], wa[u], sa[u]);
-                    if (j + 2 * GS < cnt) fetch(j + 2 * GS, xa, wa, sa);
+                    __builtin_amdgcn_sched_barrier(0);
+                    fetch(j + 2 * GS, xa, wa, sa);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int u = 0; u < GS; ++u) add(xb[u], wb[u], sb[u]);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
-            for (; j < cnt; ++j) {
-                const float ww = W ? p.val[(e0 + base + j) * p.val_heads + head] : 1.0f;
-                add(tile[j * fsp + cl], ww, SRCS ? scl[j] : 1.0f);
-            }
+            for (; j < cnt; ++j) add(xs[j * FSP], W ? ws[j * hs] : 1.0f, SRCS ? scl[j] : 1.0f);
         }
     }
     if (!chain) return;
+    if (ntiles == 0 && p.accum && p.dst_scale == nullptr) acc = yinit[lane];  // (own write)
     float out = acc;
     if (p.dst_scale) {
         out = __fmul_rn(p.dst_scale[row], out);
@@ -545,29 +583,42 @@ static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t 
     }
 }
 
-template <int VEC, bool W, bool SRCS>
-static void launch_hub_t(const SpmmParams &p, const HubParams &hp, hipStream_t st) {
-    constexpr size_t lds = (size_t)(kHubTile + (SRCS ? kHubMaxT : 0)) * sizeof(float);
+template <int VEC, int FSP, bool W, bool SRCS, int TL>
+static void launch_hub_tl(const SpmmParams &p, HubParams hp, hipStream_t st) {
+    constexpr size_t lds = hub_lds_floats<FSP, TL>() * sizeof(float);
     // more than the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once
-    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, W, SRCS>,
+    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS, TL>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)opted;
-    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, W, SRCS>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
+    hp.n_slices = (p.F + FSP - 1) / FSP;
+    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS, TL>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
                        dim3(kHubThreads), lds, st, p, hp);
 }
 
+template <int VEC, int FSP, bool W, bool SRCS>
+static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st) {
+    launch_hub_tl<VEC, FSP, W, SRCS, kHubTile>(p, hp, st);
+}
+
+// slices of 32 features when F <= 32 (F = 32: one 128-B row per edge, 512 edges a tile),
+// else of 64 (one chain lane per feature of a wave)
 static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w, bool srcs, hipStream_t st) {
-#define GALA_HUB(V)                                                    \
-    if (w) {                                                           \
-        if (srcs) launch_hub_t<V, true, true>(p, hp, st);              \
-        else launch_hub_t<V, true, false>(p, hp, st);                  \
-    } else {                                                           \
-        if (srcs) launch_hub_t<V, false, true>(p, hp, st);             \
-        else launch_hub_t<V, false, false>(p, hp, st);                 \
+#define GALA_HUB(V, S)                                                    \
+    if (w) {                                                              \
+        if (srcs) launch_hub_t<V, S, true, true>(p, hp, st);              \
+        else launch_hub_t<V, S, true, false>(p, hp, st);                  \
+    } else {                                                              \
+        if (srcs) launch_hub_t<V, S, false, true>(p, hp, st);             \
+        else launch_hub_t<V, S, false, false>(p, hp, st);                 \
     }
-    if (vec == 4) { GALA_HUB(4) }
-    else if (vec == 2) { GALA_HUB(2) }
-    else { GALA_HUB(1) }
+    const bool narrow = p.F <= 32;
+    if (vec == 4) {
+        if (narrow) { GALA_HUB(4, 32) } else { GALA_HUB(4, 64) }
+    } else if (vec == 2) {
+        if (narrow) { GALA_HUB(2, 32) } else { GALA_HUB(2, 64) }
+    } else {
+        if (narrow) { GALA_HUB(1, 32) } else { GALA_HUB(1, 64) }
+    }
 #undef GALA_HUB
 }
 
@@ -667,7 +718,17 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     // GALA_SPMM_HUB_CHUNKED as chunk partials + an ordered fix-up (the fast, reordered mode)
     const bool has_hubs = plan && plan->n_rows_split > 0 && A->n_seg == 1 && !samp;
     const bool use_split = has_hubs && plan->n_chunks > 0 && (flags & GALA_SPMM_HUB_CHUNKED);
-    const bool use_hub = has_hubs && !use_split;
+    // the hub kernel stages at most kHubMaxHeads edge-weight heads per feature slice in LDS;
+    // narrower heads keep the hub rows in the row kernel (one sequential pass: exact, slow)
+    bool heads_ok = true;
+    if (A->val && A->val_heads > 1) {
+        const int hd = F / A->val_heads, fsp = F <= 32 ? 32 : 64;
+        for (int f0 = 0; f0 < F && hd > 0; f0 += fsp) {
+            const int f1 = (f0 + fsp < F ? f0 + fsp : F) - 1;
+            if (f1 / hd - f0 / hd + 1 > kHubMaxHeads) heads_ok = false;
+        }
+    }
+    const bool use_hub = has_hubs && !use_split && heads_ok;
     auto ok = [&](int v) {
         const int64_t Fv = ((int64_t)F + v - 1) / v * v;
         const bool fits = (F % v == 0 && head_dim % v == 0) || (one_head && ldx >= Fv && ldy >= Fv);
@@ -755,7 +816,6 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
             const int L = (int)((Fc + vec - 1) / vec);
             int r;
             if (use_hub) {  // the long serial rows first, so their workgroups are dispatched first
-                hp.n_slices = (Fc + kHubSlice - 1) / kHubSlice;
                 if (hub_st != hs) {
                     if (hipEventRecord((hipEvent_t)plan->aux_events[0], hs) != hipSuccess ||
                         hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)
