@@ -47,6 +47,10 @@ import subprocess
 import sys
 import time
 
+# the wall clock the N > 1 budget counts from: the launching process's start (a self-launch
+# hands it to its ranks)
+START = float(os.environ.get("GALA_BENCH_T0", "0")) or time.time()
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gala-gnn-acceleration-language_amd"))
 
@@ -76,6 +80,7 @@ def self_launch(n: int) -> int:
     cmd += sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", str(max(1, min(16, (os.cpu_count() or 8) // n))))
+    env["GALA_BENCH_T0"] = repr(START)
     log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
     return subprocess.run(cmd, env=env).returncode
 
@@ -399,7 +404,38 @@ def _recoverable(e: Exception) -> bool:
     return not any(k in text for k in ("HIP", "hip", "CUDA", "cuda", "NCCL", "nccl", "RCCL"))
 
 
-def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max):
+class Budget:
+    """The N > 1 run's wall-clock budget (--budget-s from the process start), so the driver's
+    run always gets its headline line.  Every decision is agreed over the ranks (one MAX
+    all-reduce of "out of time"): a rank that skips a phase its peers run would leave them
+    waiting in a collective.  `phases` holds each phase's wall seconds, `skipped` what was left
+    out and why."""
+
+    def __init__(self, limit_s: float, reduce_max=None):
+        self.t0 = START
+        self.limit = float(limit_s)
+        self.reduce_max = reduce_max
+        self.phases, self.skipped = {}, []
+
+    def elapsed(self) -> float:
+        return time.time() - self.t0
+
+    def ok(self, need_s: float, what: str) -> bool:
+        """Whether `what`, estimated at need_s seconds, still fits (the same answer on every rank)."""
+        over = 1.0 if self.elapsed() + need_s > self.limit else 0.0
+        if self.reduce_max is not None:
+            over = self.reduce_max(over)
+        if over > 0:
+            self.skipped.append(f"{what} (needs ~{need_s:.0f} s, {self.elapsed():.0f} of {self.limit:.0f} s used)")
+            log(f"[bench] budget: skipping {what}")
+        return over == 0
+
+    def note(self):
+        return {"budget_s": self.limit, "elapsed_s": round(self.elapsed(), 1),
+                "phase_s": {k: round(v, 1) for k, v in self.phases.items()}, "skipped_for_time": self.skipped}
+
+
+def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max, budget=None):
     """Strong scaling of one Products-shaped graph of family `kind` over the ranks: every
     candidate layout timed for a few steps, the timed steps on the fastest.  Returns
     (result fields, graph, bounds)."""
@@ -411,27 +447,27 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
     log(f"[rank {rank}/{world}] {kind} graph N={g.n_rows} E={g.nnz} built in {time.time() - t0:.1f}s")
     bounds = gdist.row_bounds(g.rowptr, world)
     t0 = time.time()
-    modes = []
+    # candidates are built when they are timed (a candidate the budget skips costs nothing)
     pt1 = gdist.partition_graph(g, rank, world, bounds=bounds)
-    modes.append(HaloMode("halo-exact", pt1, F, be, comm, exact=True))
-    modes.append(HaloMode("halo-overlap", pt1, F, be, comm, exact=False))
+    modes = [("halo-exact", lambda: HaloMode("halo-exact", pt1, F, be, comm, exact=True)),
+             ("halo-overlap", lambda: HaloMode("halo-overlap", pt1, F, be, comm, exact=False))]
     if pt1.halo_mode == "dense":
-        ptk = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
-        modes.append(HaloMode("halo-pipe", ptk, F, be, comm, exact=False))
         # finer chunks leave less of the first chunk's transfer and the last chunk's SpMM
         # outside the overlap, at more (smaller) collectives: both are timed
-        pt8 = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=2 * PIPE_CHUNKS)
-        modes.append(HaloMode(f"halo-pipe{2 * PIPE_CHUNKS}", pt8, F, be, comm, exact=False))
-    modes.append(VcutMode("vcut", vc.vertex_cut_partition(g, rank, world, 1, bounds), F, be, comm))
-    modes.append(VcutMode("vcut-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds), F, be, comm))
+        for ck, nm in ((PIPE_CHUNKS, "halo-pipe"), (2 * PIPE_CHUNKS, f"halo-pipe{2 * PIPE_CHUNKS}")):
+            modes.append((nm, lambda ck=ck, nm=nm: HaloMode(nm, gdist.partition_graph(
+                g, rank, world, bounds=bounds, halo_mode="dense", chunks=ck), F, be, comm, exact=False)))
+    modes.append(("vcut", lambda: VcutMode("vcut", vc.vertex_cut_partition(g, rank, world, 1, bounds), F, be, comm)))
+    modes.append(("vcut-pipe", lambda: VcutMode("vcut-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS,
+                                                                                    bounds), F, be, comm)))
     frac = vc.touched_fraction(g, bounds) if world > 1 else 0.0
     if frac < 0.9:      # the DCSR exchange can only win when some partial rows are empty
-        modes.append(VcutMode("vcut-sparse", vc.vertex_cut_partition(g, rank, world, 1, bounds, "sparse"), F, be,
-                              comm))
-        modes.append(VcutMode("vcut-sparse-pipe", vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds,
-                                                                         "sparse"), F, be, comm))
-    log(f"[rank {rank}] {kind} partitions ({[m.name for m in modes]}, halo {pt1.halo_mode}, "
-        f"{pt1.n_halo_rows} halo rows, touched fraction {frac:.3f}) in {time.time() - t0:.1f}s")
+        modes.append(("vcut-sparse", lambda: VcutMode("vcut-sparse", vc.vertex_cut_partition(
+            g, rank, world, 1, bounds, "sparse"), F, be, comm)))
+        modes.append(("vcut-sparse-pipe", lambda: VcutMode("vcut-sparse-pipe", vc.vertex_cut_partition(
+            g, rank, world, PIPE_CHUNKS, bounds, "sparse"), F, be, comm)))
+    log(f"[rank {rank}] {kind} candidates {[m[0] for m in modes]}, halo {pt1.halo_mode}, "
+        f"{pt1.n_halo_rows} halo rows, touched fraction {frac:.3f}; row partition in {time.time() - t0:.1f}s")
     n, r0 = pt1.n, pt1.r0
     gen = torch.Generator(device=dev).manual_seed(1234)
     # every rank draws the whole X so row r is the same on any number of ranks
@@ -440,24 +476,34 @@ def strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, 
     dY = (torch.rand((g.n_rows, F), device=dev, generator=gen) * 2 - 1)[r0:r0 + n].clone()
     del Xall
     bufs = [be.empty(n, F) for _ in range(4)]
-    cand, failed = {}, {}
-    for m in modes:
+    cand, failed, best, longest = {}, {}, None, 0.0
+    forced = os.environ.get("GALA_DIST_MODE")
+    for name, make in modes:
+        # after the first candidate, one more is timed only while the budget holds (the
+        # estimate: the slowest candidate so far, build included)
+        if cand and budget is not None and not budget.ok(longest, f"{kind} candidate {name}"):
+            continue
         # a layout that raises (on every rank alike: the same code on the same graph) is
         # skipped and reported; the others are still timed
+        tc = time.time()
         try:
+            m = make()
             st = make_step(m.agg, X, dY, bufs)
-            cand[m.name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
-            log(f"[rank {rank}] {kind} candidate {m.name}: {cand[m.name] * 1e3:.3f} ms/step")
+            cand[name] = timed_steps(st, args.calib_steps, 2, sync, barrier, reduce_max)
+            log(f"[rank {rank}] {kind} candidate {name}: {cand[name] * 1e3:.3f} ms/step")
+            keep = name == forced or (forced not in dict(modes) and (best is None or cand[name] < cand[best.name]))
+            if keep:
+                best = m
+            del m, st
         except Exception as e:  # noqa: BLE001
             if not _recoverable(e):
                 raise
-            failed[m.name] = repr(e)[:300]
-            log(f"[rank {rank}] {kind} candidate {m.name} failed: {failed[m.name]}")
-    if not cand:
+            failed[name] = repr(e)[:300]
+            log(f"[rank {rank}] {kind} candidate {name} failed: {failed[name]}")
+        longest = max(longest, time.time() - tc)
+    if best is None:
         raise RuntimeError(f"bench.py: every {kind} layout failed: {failed}")
-    forced = os.environ.get("GALA_DIST_MODE")
-    name = forced if forced in cand else min(cand, key=cand.get)
-    best = next(m for m in modes if m.name == name)
+    name = best.name
     t_step = timed_steps(make_step(best.agg, X, dY, bufs), args.steps if kind == "uniform" else max(args.steps // 2, 2),
                          args.warmup if kind == "uniform" else 2, sync, barrier, reduce_max)
     t_kernel, alg = best.kernel(timer)
@@ -511,7 +557,11 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    fam, g, bounds = strong_family(args, "uniform", rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+    budget = Budget(args.budget_s, reduce_max)
+    t0 = time.time()
+    fam, g, bounds = strong_family(args, "uniform", rank, world, dev, be, comm, timer, sync, barrier, reduce_max,
+                                   budget)
+    budget.phases["uniform"] = t_uniform = time.time() - t0
     out = {
         "metric": "aggregated edges/sec, GCN-2 ogbn-products (4 F=32 aggregations per step)",
         "value": fam["value"],
@@ -534,37 +584,48 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         "roofline": fam["roofline"],
         "comm": fam["comm"],
     }
-    if not args.no_gat:
+    # secondary fields, each only while the budget holds; estimates from the uniform family's
+    # own wall time (a family of the same shape: graph, partitions, candidates)
+    if not args.no_gat and budget.ok(t_uniform, "gat field"):
+        t0 = time.time()
         try:
             out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
         except Exception as e:  # noqa: BLE001  (reported; the headline line stays)
             if not _recoverable(e):
                 raise
             out["gat"] = {"error": repr(e)[:500]}
+        budget.phases["gat"] = time.time() - t0
     del g
     for kind in ("rmat", "banded"):   # the skewed family, and one that shards naturally
-        if getattr(args, f"no_{kind}"):
+        if getattr(args, f"no_{kind}") or not budget.ok(1.2 * t_uniform, f"{kind} family"):
             continue
+        t0 = time.time()
         try:    # a secondary family that fails on every rank is reported; the headline line stays
-            rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max)
+            rm, gr, _ = strong_family(args, kind, rank, world, dev, be, comm, timer, sync, barrier, reduce_max,
+                                      budget)
         except Exception as e:  # noqa: BLE001
             if not _recoverable(e):
                 raise
             out[kind] = {"error": repr(e)[:500]}
             continue
+        finally:
+            budget.phases[kind] = time.time() - t0
         rm.pop("real_data")
         rm["graph"] = (f"{FAMILY_GRAPH[kind]}, N={gr.n_rows}, E={gr.nnz}, "
                        f"max degree {int((gr.rowptr[1:] - gr.rowptr[:-1]).max())}")
         rm["unit"] = "edges/s"
         out[kind] = rm
         del gr
-    if not args.no_weak:
+    if not args.no_weak and budget.ok(0.5 * t_uniform, "weak field"):
+        t0 = time.time()
         try:
             out["weak"] = weak_scaling(args, rank, world, dev, be, comm, sync, barrier, reduce_max)
         except Exception as e:  # noqa: BLE001
             if not _recoverable(e):
                 raise
             out["weak"] = {"error": repr(e)[:500]}
+        budget.phases["weak"] = time.time() - t0
+    out["budget"] = budget.note()
     return out
 
 
@@ -882,6 +943,9 @@ def main():
     ap.add_argument("--banded", action="store_true", help="N = 1: add the banded family line")
     ap.add_argument("--no-gat", action="store_true")
     ap.add_argument("--no-weak", action="store_true")
+    ap.add_argument("--budget-s", type=float, default=float(os.environ.get("GALA_BENCH_BUDGET_S", "420")),
+                    help="N > 1: wall-clock budget from the process start; secondary fields and candidates "
+                         "that would not fit are skipped (noted in the line's 'budget'); the headline always runs")
     ap.add_argument("--data", help="dataset directory in the reference's npy format (Adj_src.npy, Adj_dst.npy) "
                                    "or a Matrix Market .mtx graph; default: Data/Products/ when present, else "
                                    "the synthetic graph")

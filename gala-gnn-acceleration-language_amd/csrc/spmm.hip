@@ -339,14 +339,19 @@ __global__ __launch_bounds__(kBlock) void k_spmm_fixup(SpmmParams p, SplitParams
 // so the result is bit-identical to the reference's serial row loop (cuda.h:286-358) --
 // the REF parity mode.  One row group of G lanes would walk such a row one U-edge batch at
 // a time, a dependent col -> X load chain per batch (a 388 K-edge R-MAT hub: ~100 ms).
-// Instead one workgroup of kHubThreads lanes owns (row, slice of FSP features): every
-// lane gathers X rows of a tile of T edges into registers (kHubTile floats in flight per
-// workgroup, the next tile's column indices already loaded), the tile goes to LDS, and wave 0
-// -- one lane per feature of the slice -- runs the row's add chain over the tile from LDS
-// while the next tile's gathers are in flight.  The chain keeps the per-feature operation
-// order and rounding of accumulate<> exactly.
+// Instead one workgroup owns (row, slice of FSP features), split by role:
+//   waves 1-7 (gatherers) fetch the X rows of tile t+1 (T edges, the next tiles' column
+//        indices already loaded) and store them into one of two LDS buffers;
+//   wave 0 (the chain) -- one lane per feature of the slice -- adds tile t from the other
+//        buffer, in CSR order, with the per-feature operations and rounding of accumulate<>.
+// One barrier per tile swaps the buffers, so the chain never waits for a gather or a store
+// unless the gatherers fall behind.  Everything the chain reads is in LDS (X rows, src
+// scales, edge weights, the accumulate start value): vmcnt counts in order, so one global
+// load in the chain would wait for every gather issued before it.
 constexpr int kHubThreads = 512;
-constexpr int kHubTile = 16384;    // floats of X per tile (64 KB of LDS)
+constexpr int kHubGather = kHubThreads - kWave;  // gatherer lanes
+constexpr int kHubBuf = 8192;      // floats of X per LDS buffer (32 KB; two buffers)
+constexpr int kHubMaxHeads = 4;    // edge-weight heads per slice staged in LDS
 
 struct HubParams {
     const int32_t *rows;           // hub row ids
@@ -355,27 +360,26 @@ struct HubParams {
     int32_t n_slices;              // ceil(F / FSP)
 };
 
-// FSP: features per workgroup (32 or 64) = the LDS row stride, compile-time so the chain's
-// LDS addresses are immediate offsets; T = kHubTile / FSP edges per tile.  Everything the
-// chain reads comes from LDS (X rows, src scales, edge weights, the accumulate start value):
-// vmcnt counts in order, so a global load in the chain would wait for the next tile's gathers.
-constexpr int kHubMaxHeads = 4;    // edge-weight heads per slice staged in LDS
-template <int FSP, int TL>
-constexpr size_t hub_lds_floats() {
-    return (size_t)TL + (size_t)(TL / FSP) * (1 + kHubMaxHeads) + kWave;
-}
+// LDS: buf[2][T/4][FSP][4] (X; an edge quad of one feature is one 16-B read), scl[2][T]
+// (SRCS), wts[2][kHubMaxHeads][T] (W), yinit[64], then slack the chain's prefetch may read
+// past a buffer (never consumed).  Unweighted: 68 KB, two workgroups per CU.
+template <int FSP, bool W, bool SRCS>
+struct HubLds {
+    static constexpr int T = kHubBuf / FSP;          // edges per tile
+    static constexpr int kGroup = 16;                 // edges per chain group
+    static constexpr size_t buf = 0, scl = 2 * (size_t)kHubBuf, wts = scl + (SRCS ? 2 * T : 0),
+                            yinit = wts + (W ? 2 * (size_t)kHubMaxHeads * T : 0), slack = yinit + kWave,
+                            floats = slack + 2 * kGroup * FSP;
+};
 
-template <int VEC, int FSP, bool W, bool SRCS, int TL = kHubTile>
+template <int VEC, int FSP, bool W, bool SRCS>
 __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, HubParams hp) {
     typedef typename VecT<VEC>::T V;
-    constexpr int T = TL / FSP;                       // edges per tile
-    constexpr int R = TL / (VEC * kHubThreads);       // vector loads per lane per tile
-    constexpr int RW = T * kHubMaxHeads / kHubThreads;  // weight loads per lane per tile
+    typedef HubLds<FSP, W, SRCS> L;
+    constexpr int T = L::T;
+    constexpr int RG = (T * (FSP / VEC) + kHubGather - 1) / kHubGather;  // loads per gatherer
+    constexpr int RW = (T * kHubMaxHeads + kHubGather - 1) / kHubGather;
     extern __shared__ float hub_lds[];
-    float *tile = hub_lds;                            // [T][FSP]
-    float *scl = tile + TL;                           // [T] src scales (SRCS)
-    float *wts = scl + T;                             // [T][hs] edge weights (W)
-    float *yinit = wts + T * kHubMaxHeads;            // [64] accumulate start values
     const int64_t ri = blockIdx.x / hp.n_slices;
     const int slice = blockIdx.x % hp.n_slices;
     // the plan's descending-degree row order starts with exactly the hub rows: the longest
@@ -388,128 +392,168 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     const int hs = W ? (f0 + fs - 1) / p.head_dim - h0 + 1 : 0;  // <= kHubMaxHeads (host)
     const int64_t e0 = p.rowptr[row], n = (int64_t)p.rowptr[row + 1] - e0;
     const int ntiles = (int)((n + T - 1) / T);
-    // this lane's load slots (edge in tile, column in the slice), the same every tile
-    int s_edge[R], s_off[R];
+    const bool gatherer = threadIdx.x >= kWave;
+    const int g = threadIdx.x - kWave;
+
+    // ---- gatherers: slot k = (edge, column) of a tile, fixed for every tile ----
+    int s_edge[RG], s_off[RG];
+    int32_t cc[RG];
+    V xr[RG];
+    float sr[RG], wr[RW];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const int i = k * kHubThreads + threadIdx.x;
-        s_edge[k] = i / lpe < T ? i / lpe : -1;
+    for (int k = 0; k < RG; ++k) {
+        const int i = k * kHubGather + g;
+        s_edge[k] = (gatherer && i / lpe < T) ? i / lpe : -1;
         s_off[k] = (i % lpe) * VEC;
     }
-    int32_t cc[R];
-    V xr[R];
-    float sr[R], wr[RW > 0 ? RW : 1];
     auto load_cols = [&](int t) {
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
+        for (int k = 0; k < RG; ++k) {
             int64_t j = (int64_t)t * T + (s_edge[k] < 0 ? 0 : s_edge[k]);
             if (j >= n) j = n - 1;  // clamped: a valid address, never used
             cc[k] = p.col[e0 + j];
         }
     };
     auto load_x = [&](int t) {
+        // unconditional (an unused slot's column is a valid one): branches around the
+        // loads would make the compiler wait for each load before issuing the next
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            // unconditional (an unused slot's column is a valid one): branches around the
-            // loads would make the compiler wait for each load before issuing the next
+        for (int k = 0; k < RG; ++k) {
             xr[k] = ldv<VEC>(p.X + (int64_t)cc[k] * p.ldx + f0 + s_off[k]);
             if (SRCS) sr[k] = p.src_scale[cc[k]];
         }
-        if (W) {  // weights (edge j, head h0 + k) at [j * hs + k], coalesced along the edges
+        if (W) {  // weight (edge j, head h0 + k) for i = j * hs + k, coalesced along the edges
 #pragma unroll
             for (int k = 0; k < RW; ++k) {
-                const int i = k * kHubThreads + threadIdx.x;
-                int64_t j = (int64_t)t * T + i / hs;
+                const int i = k * kHubGather + g;
+                int64_t j = (int64_t)t * T + (hs > 0 ? i / hs : 0);
                 if (j >= n) j = n - 1;
-                wr[k] = i < T * hs ? p.val[(e0 + j) * p.val_heads + h0 + i % hs] : 0.0f;
+                wr[k] = p.val[(e0 + j) * p.val_heads + h0 + (hs > 0 ? i % hs : 0)];
             }
         }
     };
-    // chain state: wave 0, lane f < fs owns feature f0 + f
+    auto store = [&](int b) {
+        float *xb = hub_lds + L::buf + (size_t)b * kHubBuf;
+#pragma unroll
+        for (int k = 0; k < RG; ++k) {
+            const int e = s_edge[k];
+            if (e < 0) continue;
+            float *q = xb + ((e >> 2) * FSP + s_off[k]) * 4 + (e & 3);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) q[4 * v] = el<VEC>(xr[k], v);
+            if (SRCS && s_off[k] == 0) hub_lds[L::scl + b * T + e] = sr[k];
+        }
+        if (W) {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const int i = k * kHubGather + g;
+                if (i < T * hs) hub_lds[L::wts + (size_t)b * kHubMaxHeads * T + (i % hs) * T + i / hs] = wr[k];
+            }
+        }
+    };
+
+    // ---- chain: wave 0, lane f < fs owns feature f0 + f ----
     const int lane = threadIdx.x;
     const bool chain = lane < fs;
     const int cl = chain ? lane : 0;
     const int f = f0 + cl;
     const int hl = W ? f / p.head_dim - h0 : 0;
     const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + h0 + hl] : 1.0f;
-    if (chain && p.accum && p.dst_scale == nullptr) yinit[lane] = p.Y[row * p.ldy + f];
+    if (chain && p.accum && p.dst_scale == nullptr) hub_lds[L::yinit + lane] = p.Y[row * p.ldy + f];
     float acc = 0.0f;
-    auto add = [&](float x, float w, float s) {
-        const float v = SRCS ? __fmul_rn(s, x) : x;
+    auto add = [&](float x, float w, float sv) {
+        const float v = SRCS ? __fmul_rn(sv, x) : x;
         if (W) acc = fmaf(p.val_rs ? __fmul_rn(w, rs) : w, v, acc);
         else acc = __fadd_rn(acc, v);
     };
+    typedef float F4 __attribute__((ext_vector_type(4)));
+    constexpr int GS = L::kGroup;
+    struct Grp {
+        F4 x[GS / 4], w[GS / 4], s[GS / 4];
+    };
+    auto run_chain = [&](int t) {
+        const int b = t & 1;
+        const float *xb = hub_lds + L::buf + (size_t)b * kHubBuf + cl * 4;
+        const float *sb = hub_lds + L::scl + b * T;
+        const float *wb = hub_lds + L::wts + (size_t)b * kHubMaxHeads * T + hl * T;
+        const int cnt = (int)((n - (int64_t)t * T) < T ? (n - (int64_t)t * T) : T);
+        auto fetch = [&](int j, Grp &q) {  // edges j .. j+GS-1 (j % 4 == 0): 16-B reads
+#pragma unroll
+            for (int u = 0; u < GS / 4; ++u) {
+                q.x[u] = *reinterpret_cast<const F4 *>(xb + ((j >> 2) + u) * FSP * 4);
+                if (SRCS) q.s[u] = *reinterpret_cast<const F4 *>(sb + j + 4 * u);
+                if (W) q.w[u] = *reinterpret_cast<const F4 *>(wb + j + 4 * u);
+            }
+        };
+        auto consume = [&](const Grp &q) {
+#pragma unroll
+            for (int u = 0; u < GS / 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) add(q.x[u][v], W ? q.w[u][v] : 1.0f, SRCS ? q.s[u][v] : 1.0f);
+        };
+        // three groups in rotation: a group's 16-B reads are issued two groups ahead of its
+        // adds (sched_barrier keeps that order; the scheduler would sink them to their use).
+        // The prefetch past the last full round reads at most two groups past the buffer
+        // (the other buffer or the slack) and is never consumed.
+        int j = 0;
+        const int full = cnt / (3 * GS) * (3 * GS);
+        if (full > 0) {
+            Grp A, B, C;
+            fetch(0, A);
+            fetch(GS, B);
+            for (; j < full; j += 3 * GS) {
+                fetch(j + 2 * GS, C);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(A);
+                __builtin_amdgcn_sched_barrier(0);
+                fetch(j + 3 * GS, A);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(B);
+                __builtin_amdgcn_sched_barrier(0);
+                fetch(j + 4 * GS, B);
+                __builtin_amdgcn_sched_barrier(0);
+                consume(C);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        for (; j + GS <= cnt; j += GS) {  // the remaining whole groups, one at a time
+            Grp A;
+            fetch(j, A);
+            consume(A);
+        }
+        const float *xs = hub_lds + L::buf + (size_t)b * kHubBuf + cl * 4;
+        for (; j < cnt; ++j)
+            add(xs[(j >> 2) * FSP * 4 + (j & 3)], W ? wb[j] : 1.0f, SRCS ? sb[j] : 1.0f);
+    };
 
-    if (ntiles > 0) {
+    // ---- pipeline: tile t in buffer t&1 is added while tile t+1 is gathered into the other ----
+    if (gatherer && ntiles > 0) {
         load_cols(0);
         load_x(0);
         if (ntiles > 1) load_cols(1);
-    }
-    for (int t = 0; t < ntiles; ++t) {
-        __syncthreads();  // the chain is done with the previous tile
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            if (s_edge[k] < 0) continue;
-            stv<VEC>(tile + s_edge[k] * FSP + s_off[k], xr[k]);
-            if (SRCS && s_off[k] == 0) scl[s_edge[k]] = sr[k];
+        store(0);
+        if (ntiles > 1) {
+            load_x(1);
+            if (ntiles > 2) load_cols(2);
         }
-        if (W) {
-#pragma unroll
-            for (int k = 0; k < RW; ++k) {
-                const int i = k * kHubThreads + threadIdx.x;
-                if (i < T * hs) wts[i] = wr[k];
+    }
+    __syncthreads();
+    if (chain && p.accum && p.dst_scale == nullptr) acc = hub_lds[L::yinit + lane];
+    for (int t = 0; t < ntiles; ++t) {
+        if (gatherer) {
+            if (t + 1 < ntiles) {
+                store((t + 1) & 1);
+                if (t + 2 < ntiles) {
+                    load_x(t + 2);
+                    if (t + 3 < ntiles) load_cols(t + 3);
+                }
             }
+        } else {
+            run_chain(t);
         }
         __syncthreads();
-        if (t == 0 && chain && p.accum && p.dst_scale == nullptr) acc = yinit[lane];
-        if (t + 1 < ntiles) {
-            load_x(t + 1);              // tile t+1's rows, in flight during the chain
-            if (t + 2 < ntiles) load_cols(t + 2);
-        }
-        if (threadIdx.x < kWave) {
-            // the add chain over the tile, 16 edges per group, ping-pong: the next group's
-            // LDS reads are in flight while a group's dependent adds run.  The prefetch past
-            // the last full group is unconditional (no register copies at the loop edge): it
-            // reads at most GS rows past the tile, inside this kernel's LDS (scl, wts, yinit
-            // follow the tile), and is never consumed
-            const int cnt = (int)((n - (int64_t)t * T) < T ? (n - (int64_t)t * T) : T);
-            const float *xs = tile + cl;
-            const float *ws = wts + hl;
-            constexpr int GS = 16;
-            static_assert(GS * FSP <= T * (1 + kHubMaxHeads) + kWave, "prefetch stays in LDS");
-            float xa[GS], wa[GS], sa[GS], xb[GS], wb[GS], sb[GS];
-            auto fetch = [&](int j, float (&x)[GS], float (&w)[GS], float (&sv)[GS]) {
-#pragma unroll
-                for (int u = 0; u < GS; ++u) {
-                    x[u] = xs[(j + u) * FSP];
-                    if (SRCS) sv[u] = scl[j + u];
-                    if (W) w[u] = ws[(j + u) * hs];
-                }
-            };
-            int j = 0;
-            const int full = cnt / (2 * GS) * (2 * GS);
-            if (full > 0) {
-                fetch(0, xa, wa, sa);
-                for (; j < full; j += 2 * GS) {
-                    // sched_barrier: keep each group's reads ahead of the other group's adds
-                    // (the scheduler otherwise sinks them to their first use)
-                    fetch(j + GS, xb, wb, sb);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < GS; ++u) add(xa[u], wa[u], sa[u]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    fetch(j + 2 * GS, xa, wa, sa);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < GS; ++u) add(xb[u], wb[u], sb[u]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            for (; j < cnt; ++j) add(xs[j * FSP], W ? ws[j * hs] : 1.0f, SRCS ? scl[j] : 1.0f);
-        }
     }
     if (!chain) return;
-    if (ntiles == 0 && p.accum && p.dst_scale == nullptr) acc = yinit[lane];  // (own write)
     float out = acc;
     if (p.dst_scale) {
         out = __fmul_rn(p.dst_scale[row], out);
@@ -583,21 +627,16 @@ static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t 
     }
 }
 
-template <int VEC, int FSP, bool W, bool SRCS, int TL>
-static void launch_hub_tl(const SpmmParams &p, HubParams hp, hipStream_t st) {
-    constexpr size_t lds = hub_lds_floats<FSP, TL>() * sizeof(float);
+template <int VEC, int FSP, bool W, bool SRCS>
+static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st) {
+    constexpr size_t lds = HubLds<FSP, W, SRCS>::floats * sizeof(float);
     // more than the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once
-    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS, TL>,
+    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)opted;
     hp.n_slices = (p.F + FSP - 1) / FSP;
-    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS, TL>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
+    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
                        dim3(kHubThreads), lds, st, p, hp);
-}
-
-template <int VEC, int FSP, bool W, bool SRCS>
-static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st) {
-    launch_hub_tl<VEC, FSP, W, SRCS, kHubTile>(p, hp, st);
 }
 
 // slices of 32 features when F <= 32 (F = 32: one 128-B row per edge, 512 edges a tile),

@@ -636,7 +636,14 @@ class HaloGatOverlap(HaloGat):
     chunks' edges.  The backward likewise: sum_e p_e dY[c] over the own columns and the
     row-local d_aL overlap the dY exchange, each halo chunk continues it, dX = q (P_own +
     P_halo).  Each row's sums are grouped per column range, so results agree with one GPU to
-    fp32 rounding, not bit for bit."""
+    fp32 rounding, not bit for bit.
+
+    Unlike HaloGat, this backward keeps the two-pass attention-Linear backward (a separate
+    gala_head_attn_bwd_f32 pass adds d_aL wR to dX after the last chunk), and its row-local
+    d_aL comes from gala_gat_bwd_stats_f32 over an edgeless own-row graph, which also writes
+    an [n, F] dX of zeros that is dropped: two dX-sized passes per step that HaloGat does not
+    pay.  It is a layout for links slower than its own-column passes; bench.py
+    times it as a candidate and at one rank it is never chosen."""
     _chunked = True
 
     def __init__(self, part: GraphPartition, F: int, heads: int, backend, comm=None, slope: float = 0.2):

@@ -127,13 +127,19 @@ def touched_fraction(g: layout.HostGraph, bounds: np.ndarray) -> float:
     N = g.n_rows
     if P == 1 or g.nnz == 0:
         return 0.0
-    ow = (np.searchsorted(bounds, g.col, side="right") - 1).astype(np.int32)
-    rows = np.repeat(np.arange(N, dtype=np.int32), np.diff(g.rowptr.astype(np.int64)))
-    # columns ascend within a row, so owners do: count changes of (row, owner)
-    new = np.ones(g.nnz, bool)
-    new[1:] = (ow[1:] != ow[:-1]) | (rows[1:] != rows[:-1])
-    row_owner = (np.searchsorted(bounds, rows, side="right") - 1).astype(np.int32)
-    remote = int(np.count_nonzero(new & (ow != row_owner)))
+    rp = g.rowptr.astype(np.int64)
+    if P > 64:   # distinct (row, owner) pairs by sorting
+        rows = np.repeat(np.arange(N, dtype=np.int64), np.diff(rp))
+        ow = np.searchsorted(bounds, g.col, side="right") - 1
+        far = ow != np.searchsorted(bounds, rows, side="right") - 1
+        return np.unique(rows[far] * P + ow[far]).shape[0] / float(N * (P - 1))
+    # distinct remote (row, owner) pairs, whatever the column order inside a row: an owner
+    # bit mask per row (OR over the row's edges), the row's own owner cleared, popcount
+    bit = np.left_shift(np.uint64(1), (np.searchsorted(bounds, g.col, side="right") - 1).astype(np.uint64))
+    full = np.flatnonzero(np.diff(rp) > 0)
+    mask = np.bitwise_or.reduceat(bit, rp[full]) if full.size else np.zeros(0, np.uint64)
+    own = np.left_shift(np.uint64(1), (np.searchsorted(bounds, full, side="right") - 1).astype(np.uint64))
+    remote = int(np.bitwise_count(mask & ~own).sum())
     return remote / float(N * (P - 1))
 
 

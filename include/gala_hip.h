@@ -406,7 +406,8 @@ int gala_gat_bwd_stats_ex_f32(const gala_csr_t *A, const float *aL, const float 
                               int64_t ldym, const float *sma, float *dX, int64_t lddx, float *d_aL,
                               void *stream);
 /*
- * gala_gat_bwd_stats_linear_f32: gala_gat_bwd_stats_ex_f32 (dY_rows NULL: a square pattern)
+ * gala_gat_bwd_stats_linear_f32: gala_gat_bwd_stats_ex_f32 (a square pattern with dY_rows
+ * NULL, or a gathered dY table with the rows' own dY_rows, as HaloGat.backward runs it)
  * with the source logit's per-head Linear (aR = X wR + bR, the DSL's attnR = ffn(res, out=1),
  * gala_head_attn_f32) folded into the dX store: dX[r, f] += d_aL[r, head(f)] * wR[f], REF's
  * d_aR = d_aL (common.h:835-894 on the undirected pattern), with the product-then-sum

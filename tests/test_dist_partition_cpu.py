@@ -209,6 +209,26 @@ def test_vertex_cut_sparse_layout(name, world, chunks):
             assert srcs == sorted(set(srcs))                          # source-rank order, once each
 
 
+def test_touched_fraction_counts_pairs_whatever_the_column_order():
+    """touched_fraction counts distinct remote (row, owner) pairs: the same on a graph whose
+    rows hold their columns in any order, and equal to a direct count."""
+    g = layout.gen_graph("rmat", 5000, 40000)
+    rng = np.random.default_rng(1)
+    col = g.col.copy()
+    for r in range(0, g.n_rows, 3):
+        a, b = int(g.rowptr[r]), int(g.rowptr[r + 1])
+        col[a:b] = rng.permutation(col[a:b])
+    shuffled = layout.HostGraph(g.n_rows, g.n_cols, g.rowptr, col)
+    for P in (2, 3, 5):
+        bnd = gdist.row_bounds(g.rowptr, P)
+        rows = np.repeat(np.arange(g.n_rows), np.diff(g.rowptr.astype(np.int64)))
+        ow = np.searchsorted(bnd, g.col, side="right") - 1
+        far = ow != np.searchsorted(bnd, rows, side="right") - 1
+        want = np.unique(rows[far] * P + ow[far]).shape[0] / (g.n_rows * (P - 1))
+        assert vc.touched_fraction(g, bnd) == want
+        assert vc.touched_fraction(shuffled, bnd) == want
+
+
 def test_touched_fraction_and_auto_exchange():
     g = banded()
     b = gdist.row_bounds(g.rowptr, 4)

@@ -483,6 +483,7 @@ def test_halo_gat_bit_identical_to_one_gpu(world, halo, kind, heads, F):
     dg = ops.DeviceGraph.from_host(g)                    # the whole graph's hub plan
     Y1, q1, Ym1, sma1, aR1 = ops.gat_fwd_stats(dg, cu(aL), cu(X), wR=wR, bR=bR, heads=heads, want_aR=True)
     dX1, daL1 = ops.gat_bwd_stats(dg, cu(aL), aR1, cu(dY), q1, Y1, Ym1, sma1, heads=heads)
+    dXl1, _ = ops.gat_bwd_stats(dg, cu(aL), aR1, cu(dY), q1, Y1, Ym1, sma1, heads=heads, wR=wR)
     for p in range(world):
         pt = gdist.partition_graph(g, p, world, halo_mode=halo)
         own = slice(pt.r0, pt.r0 + pt.n)
@@ -501,12 +502,23 @@ def test_halo_gat_bit_identical_to_one_gpu(world, halo, kind, heads, F):
         dX, daL = ops.gat_bwd_stats(gp, cu(aL[own]), Aall, dYs, q, Y, Ym, sma, heads=heads,
                                     dY_rows=dYs[x0:x0 + pt.n])
         assert torch.equal(dX, dX1[own]) and torch.equal(daL.view(-1, heads), daL1.view(-1, heads)[own])
+        # the attention Linear folded into the dX store over the gathered table + dY_rows
+        # (gala_gat_bwd_stats_linear_f32 as HaloGat.backward runs it)
+        dXl, daLl = ops.gat_bwd_stats(gp, cu(aL[own]), Aall, dYs, q, Y, Ym, sma, heads=heads,
+                                      dY_rows=dYs[x0:x0 + pt.n], wR=wR)
+        assert torch.equal(dXl, dXl1[own]) and torch.equal(daLl, daL)
         if world == 1:
             from gala.backend import HipBackend
-            hg = gdist.HaloGat(pt, F, heads, HipBackend("cuda"), None)
+            be = HipBackend("cuda")
+            hg = gdist.HaloGat(pt, F, heads, be, None)
             Yc = hg.forward_train(cu(aL), None, cu(X), wR, bR)
             dXc, daLc = hg.backward(cu(dY), linear=False)
             assert torch.equal(Yc, Y1) and torch.equal(dXc, dX1) and torch.equal(daLc.reshape(-1), daL1)
+            Yc = hg.forward_train(cu(aL), None, cu(X), wR, bR)
+            dXc, daLc, dW, db = hg.backward(cu(dY), linear=True)
+            dW1, db1 = be.head_linear_grads(cu(X), daL1.view(-1, heads), heads)
+            assert torch.equal(dXc, dXl1) and torch.equal(daLc.reshape(-1), daL1)
+            assert torch.equal(dW, dW1) and torch.equal(db, db1)
 
 
 @pytest.mark.parametrize("world,halo,chunks", [(1, "p2p", 1), (2, "dense", 1), (3, "p2p", 1), (4, "dense", 1),
