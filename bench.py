@@ -318,6 +318,7 @@ class OneGpuGCN:
         self.g = be.graph(hg)
         self.norm = be.degree(self.g)
         self.Xs = be.empty(hg.n_cols, F)
+        self.Xs2 = None
         self.n = hg.n_rows
         self.nnz = hg.nnz
 
@@ -338,6 +339,28 @@ def make_step(agg, X, dY, bufs):
         agg(H1, H2)
         agg(dY, G1)
         agg(G1, G0)
+    return step
+
+
+def make_fused_step(agg, X, dY, bufs):
+    """The same step with the degree pass and the ROW_BROADCASTs folded (gala_spmm_ex_f32,
+    gala_row_broadcast_deg_f32): the input's `norm * X` pass forms the norm from the rowptr,
+    each SpMM forms its dst norm the same way, and the first aggregation of each direction
+    also writes the second one's pre-scaled input, norm * H (codegen/gala.cu:433-456: the
+    degree, two forward and two backward aggregations).  Outputs bit-identical to make_step."""
+    H1, H2, G1, G0 = bufs
+    be, g, Xs = agg.be, agg.g, agg.Xs
+    if agg.Xs2 is None:
+        agg.Xs2 = be.empty(agg.n, agg.F)
+    Xs2 = agg.Xs2
+
+    def step():
+        be.row_broadcast_deg(g, X, Xs)
+        be.spmm_deg(g, Xs, H1, out2=Xs2)
+        be.spmm_deg(g, Xs2, H2)
+        be.row_broadcast_deg(g, dY, Xs)
+        be.spmm_deg(g, Xs, G1, out2=Xs2)
+        be.spmm_deg(g, Xs2, G0)
     return step
 
 
@@ -732,7 +755,15 @@ def run_single(args, dev, be, timer, sync):
     dY = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
     bufs = [be.empty(hg.n_rows, F) for _ in range(4)]
     ident = lambda x: x  # noqa: E731
-    t_step = timed_steps(make_step(agg, X, dY, bufs), args.steps, args.warmup, sync, lambda: None, ident)
+    # the fused step's outputs against the unfused chain's, once, outside the timed region
+    make_step(agg, X, dY, bufs)()
+    want = [b.clone() for b in bufs]
+    make_fused_step(agg, X, dY, bufs)()
+    fused_same = all(bool(torch.equal(a, b)) for a, b in zip(want, bufs))
+    del want
+    if not fused_same:
+        raise RuntimeError("bench.py: the fused step's outputs differ from the degree + ROW_BROADCAST + SpMM chain")
+    t_step = timed_steps(make_fused_step(agg, X, dY, bufs), args.steps, args.warmup, sync, lambda: None, ident)
     value = 4 * hg.nnz / t_step
     Y = bufs[0]
     t_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, Y, agg.norm, False), 10)
@@ -755,6 +786,10 @@ def run_single(args, dev, be, timer, sync):
                         "X~U[-1,1) fp32",
         "config": {"workload": "GCN-2 ogbn-products-shaped hot path: degree + 2 fwd + 2 bwd norm-scaled "
                                "SpMM aggregations, F=32",
+                   "step": "degree norm and the next aggregation's ROW_BROADCAST folded into the SpMM "
+                           "epilogues (gala_spmm_ex_f32 / gala_row_broadcast_deg_f32); outputs checked "
+                           "bit-identical to the unfused chain in this run",
+                   "fused_step_bit_identical": fused_same,
                    "n_vertices": hg.n_rows, "edges": hg.nnz, "F": F, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
@@ -903,22 +938,42 @@ def rmat_family(args, dev, be, timer, sync, kind="rmat"):
     dY = torch.rand((hg.n_rows, F), device=dev, generator=gen) * 2 - 1
     bufs = [be.empty(hg.n_rows, F) for _ in range(4)]
     steps = max(args.steps // 2, 2)
-    t_step = timed_steps(make_step(agg, X, dY, bufs), steps, 2, sync, lambda: None, lambda x: x)
+    step = make_fused_step(agg, X, dY, bufs)
+    t_step = timed_steps(step, steps, 2, sync, lambda: None, lambda x: x)
     t_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, bufs[0], agg.norm, False), 10)
     alg = spmm_alg_bytes(hg.n_rows, hg.n_rows, hg.nnz, F)
+    hubs = getattr(agg.g, "split_rows", 0)
     out = {"value": 4 * hg.nnz / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
            "graph": f"{FAMILY_GRAPH[kind]}, N={hg.n_rows}, E={hg.nnz}, "
                     f"max degree {int((hg.rowptr[1:] - hg.rowptr[:-1]).max())}",
-           "split_rows": getattr(agg.g, "split_rows", 0),
+           "split_rows": hubs,
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
                         "alg_bytes_per_launch": alg,
-                        "traffic": (None if be.name != "hip" else rmat_traffic() if kind == "rmat" else
+                        "traffic": (None if be.name != "hip" or kind == "rmat" else
                                     load_traffic("banded|void gala::k_spmm_rowgroup<4, 8, 1, 4, false, false, false>")),
-                        "kernel": "gala_spmm_f32 (k_spmm_rows_chunks: degree-ordered rows + hub-row chunks in one "
-                                  "grid, then k_spmm_fixup)" if kind == "rmat" else
+                        "kernel": "gala_spmm_f32 (degree-ordered k_spmm_rowgroup + k_spmm_hub_exact on a side "
+                                  "stream: the hub rows in the reference's order)" if kind == "rmat" else
                                   "gala_spmm_f32 (k_spmm_rowgroup, XCD-ordered row blocks)"}}
     with_traffic_rate(out["roofline"])
+    if hubs and be.name == "hip":
+        # REF order is the default (bit-identical to the reference's serial row loop); the fast
+        # mode sums hub rows as chunk partials (GALA_SPMM_HUB_CHUNKED, within fp32 rounding)
+        out["hub_order"] = "exact: hub rows summed sequentially in CSR order (REF, bit-identical)"
+        be.hub = "chunked"
+        try:
+            tc_step = timed_steps(step, steps, 2, sync, lambda: None, lambda x: x)
+            tc_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, bufs[0], agg.norm, False), 10)
+        finally:
+            be.hub = "exact"
+        tr = rmat_traffic() if kind == "rmat" else None
+        out["chunked"] = {"hub_order": "chunked: 512-edge partials + ordered fix-up (GALA_SPMM_HUB_CHUNKED; fp32 "
+                                       "summation rounding of REF)",
+                          "value": 4 * hg.nnz / tc_step, "ms_per_step": tc_step * 1e3,
+                          "kernel_ms": tc_kernel * 1e3, "frac": alg / tc_kernel / HBM_PEAK, "traffic": tr,
+                          "kernel": "k_spmm_rows_chunks + k_spmm_fixup"}
+        if tr:
+            out["chunked"]["traffic_GBps"] = tr / tc_kernel / 1e9
     if be.name == "hip":
         t_ceil = gather_ceiling(agg.g.col, agg.Xs, timer)
         if t_ceil:

@@ -57,12 +57,28 @@ constexpr int64_t kRowChunk = 256;  // rows per OpenMP work item
 extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
                                  int64_t ldy, int32_t F, const float *src_scale,
                                  const float *dst_scale, int32_t flags, int32_t nsamp,
-                                 int32_t ra, int32_t rb, void *) {
+                                 int32_t ra, int32_t rb, void *stream) {
+    return gala_cpu_spmm_ex_f32(A, X, ldx, Y, ldy, F, src_scale, dst_scale, flags, nsamp, ra, rb, nullptr, stream);
+}
+
+// (every row is one sequential pass here: GALA_SPMM_HUB_CHUNKED is accepted and gives the
+// REF-order result, which is within that mode's tolerance)
+extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
+                                    int64_t ldy, int32_t F, const float *src_scale,
+                                    const float *dst_scale, int32_t flags, int32_t nsamp,
+                                    int32_t ra, int32_t rb, const gala_spmm_epilogue_t *epi, void *) {
     int st = check_csr(A);
     if (st) return st;
     if (F < 0 || ldx < F || ldy < F ||
-        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT)))
+        (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT | GALA_SPMM_HUB_CHUNKED)) ||
+        ((flags & GALA_SPMM_EXACT) && (flags & GALA_SPMM_HUB_CHUNKED)))
         return GALA_ERR_INVALID_ARG;
+    const bool dst_deg = epi && epi->dst_deg_rsqrt;
+    float *Y2 = epi ? epi->Y2 : nullptr;
+    const int64_t ldy2 = Y2 ? epi->ldy2 : 0;
+    const float *y2s = Y2 ? epi->y2_scale : nullptr;
+    if (dst_deg && (dst_scale || A->n_seg != 1 || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
+    if (Y2 && ldy2 < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const bool samp = (flags & GALA_SPMM_SAMPLE) != 0;
@@ -80,7 +96,7 @@ extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ld
         for (int64_t r = 0; r < A->n_rows; ++r) {
             float *a = acc.data();
             float *yr = Y + r * ldy;
-            if (accum && !dst_scale)
+            if (accum && !dst_scale && !dst_deg)
                 memcpy(a, yr, sizeof(float) * (size_t)F);
             else
                 std::fill(a, a + F, 0.0f);
@@ -110,14 +126,19 @@ extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ld
                     }
                 }
             }
-            if (dst_scale) {
-                const float ds = dst_scale[r];
+            const float ds = dst_deg ? 1.0f / sqrtf((float)(A->rowptr[r + 1] - A->rowptr[r]))
+                                     : (dst_scale ? dst_scale[r] : 1.0f);
+            if (dst_scale || dst_deg) {
                 if (accum)
                     for (int32_t f = 0; f < F; ++f) yr[f] = yr[f] + ds * a[f];
                 else
                     for (int32_t f = 0; f < F; ++f) yr[f] = ds * a[f];
             } else {
                 memcpy(yr, a, sizeof(float) * (size_t)F);
+            }
+            if (Y2) {  // the next aggregation's pre-scaled input
+                const float s2 = y2s ? y2s[r] : ds;
+                for (int32_t f = 0; f < F; ++f) Y2[r * ldy2 + f] = s2 * yr[f];
             }
         }
     }
@@ -166,6 +187,22 @@ extern "C" int gala_cpu_row_broadcast_f32(int64_t n_rows, int32_t F, const float
 #pragma omp parallel for schedule(static, 1024)
     for (int64_t r = 0; r < n_rows; ++r) {
         const float s = scale[r];
+        for (int32_t f = 0; f < F; ++f) Y[r * ldy + f] = s * X[r * ldx + f];
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const float *X, int64_t ldx,
+                                              float *Y, int64_t ldy, void *) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_seg != 1) return GALA_ERR_UNSUPPORTED;
+    if (A->n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !Y) return GALA_ERR_INVALID_ARG;
+#pragma omp parallel for schedule(static, 1024)
+    for (int64_t r = 0; r < A->n_rows; ++r) {
+        const float s = 1.0f / sqrtf((float)(A->rowptr[r + 1] - A->rowptr[r]));
         for (int32_t f = 0; f < F; ++f) Y[r * ldy + f] = s * X[r * ldx + f];
     }
     return GALA_OK;

@@ -54,8 +54,23 @@ struct SpmmParams {
     int32_t split_threshold;  // > 0: rows longer than this are left to the split kernels
     const int32_t *row_order; // nullable: row group i handles row row_order[i]
     int32_t xcd_order;        // 1: XCD-aware block order (logical_block_runs)
+    int32_t dst_deg;          // 1: the dst factor is 1/sqrt(deg) of the row (one segment)
+    float *Y2;                // nullable epilogue output: Y2[r] = s2[r] * Y[r]
+    int64_t ldy2;
+    const float *y2_scale;    // s2 (NULL: the dst factor)
     SegTable seg;
 };
+
+// GCN norm deg^-0.5 of a row count: the expression of k_degree_count (power -0.5), so an
+// in-kernel norm is bit-identical to the degree pass's
+__device__ __forceinline__ float deg_rsqrt(float d) { return 1.0f / sqrtf(d); }
+
+// the dst factor of `row` (has: whether there is one)
+__device__ __forceinline__ float dst_factor(const SpmmParams &p, int64_t row, bool &has) {
+    has = p.dst_deg || p.dst_scale;
+    if (p.dst_deg) return deg_rsqrt((float)(p.rowptr[row + 1] - p.rowptr[row]));
+    return p.dst_scale ? p.dst_scale[row] : 1.0f;
+}
 
 template <int VEC>
 __device__ __forceinline__ typename VecT<VEC>::T ldv(const float *p) {
@@ -188,7 +203,7 @@ template <int VEC, int G, int CH, bool W>
 __device__ __forceinline__ void init_acc(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
                                          int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
     typedef typename VecT<VEC>::T V;
-    const bool start_from_y = p.accum && p.dst_scale == nullptr;
+    const bool start_from_y = p.accum && p.dst_scale == nullptr && !p.dst_deg;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch)
         acc[ch] = (start_from_y && cl.valid[ch]) ? ldv<VEC>(p.Y + row * p.ldy + cl.off[ch]) : V(0.0f);
@@ -198,13 +213,15 @@ template <int VEC, int G, int CH, bool W>
 __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
                                           int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
     typedef typename VecT<VEC>::T V;
-    const float ds = p.dst_scale ? p.dst_scale[row] : 1.0f;
+    bool has_ds;
+    const float ds = dst_factor(p, row, has_ds);
+    const float s2 = p.y2_scale ? p.y2_scale[row] : ds;
 #pragma unroll
     for (int ch = 0; ch < CH; ++ch) {
         if (!cl.valid[ch]) continue;
         float *yp = p.Y + row * p.ldy + cl.off[ch];
         V out = acc[ch];
-        if (p.dst_scale) {
+        if (has_ds) {
 #pragma unroll
             for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fmul_rn(ds, el<VEC>(out, i));
             if (p.accum) {
@@ -214,6 +231,11 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
             }
         }
         stv_n<VEC>(yp, out, cl.nv[ch]);
+        if (p.Y2) {  // the next aggregation's pre-scaled input, s2 * Y (its ROW_BROADCAST rounding)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fmul_rn(s2, el<VEC>(out, i));
+            stv_n<VEC>(p.Y2 + row * p.ldy2 + cl.off[ch], out, cl.nv[ch]);
+        }
     }
 }
 
@@ -459,7 +481,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     const int f = f0 + cl;
     const int hl = W ? f / p.head_dim - h0 : 0;
     const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + h0 + hl] : 1.0f;
-    if (chain && p.accum && p.dst_scale == nullptr) hub_lds[L::yinit + lane] = p.Y[row * p.ldy + f];
+    if (chain && p.accum && p.dst_scale == nullptr && !p.dst_deg) hub_lds[L::yinit + lane] = p.Y[row * p.ldy + f];
     float acc = 0.0f;
     auto add = [&](float x, float w, float sv) {
         const float v = SRCS ? __fmul_rn(sv, x) : x;
@@ -538,7 +560,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
         }
     }
     __syncthreads();
-    if (chain && p.accum && p.dst_scale == nullptr) acc = hub_lds[L::yinit + lane];
+    if (chain && p.accum && p.dst_scale == nullptr && !p.dst_deg) acc = hub_lds[L::yinit + lane];
     for (int t = 0; t < ntiles; ++t) {
         if (gatherer) {
             if (t + 1 < ntiles) {
@@ -555,11 +577,14 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     }
     if (!chain) return;
     float out = acc;
-    if (p.dst_scale) {
-        out = __fmul_rn(p.dst_scale[row], out);
+    bool has_ds;
+    const float ds = dst_factor(p, row, has_ds);
+    if (has_ds) {
+        out = __fmul_rn(ds, out);
         if (p.accum) out = __fadd_rn(p.Y[row * p.ldy + f], out);
     }
     p.Y[row * p.ldy + f] = out;
+    if (p.Y2) p.Y2[row * p.ldy2 + f] = __fmul_rn(p.y2_scale ? p.y2_scale[row] : ds, out);
 }
 
 // ---- degree: deg[r] = sum_e (val_e | 1), optionally ^power --------------------------
@@ -589,7 +614,7 @@ __global__ __launch_bounds__(kBlock) void k_degree_count(DegParams p) {
         }
         d = (float)cnt;  // exact: sequential sum of 1.0f is exact below 2^24
     }
-    if (p.power != 1.0f) d = (p.power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, p.power);
+    if (p.power != 1.0f) d = (p.power == -0.5f) ? deg_rsqrt(d) : powf(d, p.power);
     p.deg[row] = d;
 }
 
@@ -604,7 +629,7 @@ __global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
         const int64_t e0 = seg->base[s] + (int64_t)rp[row], e1 = seg->base[s] + (int64_t)rp[row + 1];
         for (int64_t e = e0; e < e1; ++e) d = __fadd_rn(d, p.val[e]);
     }
-    if (p.power != 1.0f) d = (p.power == -0.5f) ? 1.0f / sqrtf(d) : powf(d, p.power);
+    if (p.power != 1.0f) d = (p.power == -0.5f) ? deg_rsqrt(d) : powf(d, p.power);
     p.deg[row] = d;
 }
 
@@ -730,8 +755,20 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
                              int64_t ldy, int32_t F, const float *src_scale,
                              const float *dst_scale, int32_t flags, int32_t nsamp, int32_t ra,
                              int32_t rb, void *stream) {
+    return gala_spmm_ex_f32(A, X, ldx, Y, ldy, F, src_scale, dst_scale, flags, nsamp, ra, rb, nullptr, stream);
+}
+
+extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
+                                int64_t ldy, int32_t F, const float *src_scale,
+                                const float *dst_scale, int32_t flags, int32_t nsamp, int32_t ra,
+                                int32_t rb, const gala_spmm_epilogue_t *epi, void *stream) {
     int st = check_csr(A);
     if (st) return st;
+    const bool dst_deg = epi && epi->dst_deg_rsqrt;
+    float *Y2 = epi ? epi->Y2 : nullptr;
+    const int64_t ldy2 = Y2 ? epi->ldy2 : 0;
+    if (dst_deg && (dst_scale || A->n_seg != 1 || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
+    if (Y2 && ldy2 < F) return GALA_ERR_INVALID_ARG;
     if (F < 0 || ldx < F || ldy < F ||
         (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT | GALA_SPMM_HUB_CHUNKED)) ||
         ((flags & GALA_SPMM_EXACT) && (flags & GALA_SPMM_HUB_CHUNKED)))
@@ -773,7 +810,8 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
         const bool fits = (F % v == 0 && head_dim % v == 0) || (one_head && ldx >= Fv && ldy >= Fv);
         const int64_t wcols = Fv < 512LL * v ? Fv : 512LL * v;
         const bool ws_ok = !use_split || (plan->ws_cols % v == 0 && plan->ws_cols >= wcols);
-        return fits && ws_ok && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
+        const bool y2_ok = !Y2 || (ldy2 % v == 0 && ((uintptr_t)Y2 % (4 * v)) == 0 && (F % v == 0 || ldy2 >= Fv));
+        return fits && ws_ok && y2_ok && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
                ((uintptr_t)Y % (4 * v)) == 0;
     };
     while (vec > 1 && !ok(vec)) vec >>= 1;
@@ -797,6 +835,10 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
     p.ra = ra;
     p.rb = rb;
     p.split_threshold = 0;
+    p.dst_deg = dst_deg ? 1 : 0;
+    p.Y2 = Y2;
+    p.ldy2 = ldy2;
+    p.y2_scale = Y2 ? epi->y2_scale : nullptr;
     p.row_order = nullptr;
     p.xcd_order = 1;  // off below when a degree-ordered row schedule is used (heavy rows first)
     hipStream_t hs = (hipStream_t)stream;
@@ -844,12 +886,13 @@ extern "C" int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, f
         if (st) return st;
         // segments after the first launch always accumulate onto the previous ones
         const bool accum = (flags & GALA_SPMM_ACCUM) || seg0 > 0;
-        if (seg0 > 0 && dst_scale) return GALA_ERR_UNSUPPORTED;
+        if (seg0 > 0 && (dst_scale || Y2)) return GALA_ERR_UNSUPPORTED;
         for (int64_t c0 = 0; c0 < F; c0 += max_cols) {
             const int32_t Fc = (int32_t)((F - c0) < max_cols ? (F - c0) : max_cols);
             SpmmParams q = p;
             q.X = X ? X + c0 : nullptr;
             q.Y = Y + c0;
+            q.Y2 = Y2 ? Y2 + c0 : nullptr;
             q.F = Fc;
             q.accum = accum;
             const int L = (int)((Fc + vec - 1) / vec);
@@ -1034,6 +1077,37 @@ extern "C" int gala_row_broadcast_f32(int64_t n_rows, int32_t F, const float *sc
     if (!scale || !X || !Y) return GALA_ERR_INVALID_ARG;
     return gala::launch_rows(n_rows, F, gala::rows_vec(F, {ldx, ldy}, {X, Y}),
                              gala::RowBroadcastOp{scale, X, Y, ldx, ldy}, stream);
+}
+
+namespace gala {
+// ROW_BROADCAST of the GCN norm computed from the graph: Y[r,:] = deg(r)^-0.5 * X[r,:]
+// (one segment), the degree pass and the `norm * res` product in one elementwise pass
+struct DegBroadcastOp {
+    const int32_t *rowptr;
+    const float *X;
+    float *Y;
+    int64_t ldx, ldy;
+    template <int VEC>
+    __device__ __forceinline__ void apply(int64_t r, int64_t c, int nv) const {
+        const float s = deg_rsqrt((float)(rowptr[r + 1] - rowptr[r]));
+        typename VecT<VEC>::T v = ldv<VEC>(X + r * ldx + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) el<VEC>(v, i) = __fmul_rn(s, el<VEC>(v, i));
+        store_cols<VEC>(Y + r * ldy + c, v, nv);
+    }
+};
+}  // namespace gala
+
+extern "C" int gala_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const float *X, int64_t ldx,
+                                          float *Y, int64_t ldy, void *stream) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
+    if (A->n_seg != 1) return GALA_ERR_UNSUPPORTED;
+    if (A->n_rows == 0 || F == 0) return GALA_OK;
+    if (!X || !Y) return GALA_ERR_INVALID_ARG;
+    return gala::launch_rows(A->n_rows, F, gala::rows_vec(F, {ldx, ldy}, {X, Y}),
+                             gala::DegBroadcastOp{A->rowptr, X, Y, ldx, ldy}, stream);
 }
 
 extern "C" int gala_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act,

@@ -50,6 +50,15 @@ class gala_split_plan_t(ctypes.Structure):
     ]
 
 
+class gala_spmm_epilogue_t(ctypes.Structure):
+    _fields_ = [
+        ("dst_deg_rsqrt", ctypes.c_int32),
+        ("Y2", ctypes.c_void_p),
+        ("ldy2", ctypes.c_int64),
+        ("y2_scale", ctypes.c_void_p),
+    ]
+
+
 class gala_csr_t(ctypes.Structure):
     _fields_ = [
         ("n_rows", ctypes.c_int64),
@@ -78,6 +87,9 @@ SIGNATURES = {
     "gala_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "gala_last_hip_error": (ctypes.c_int, []),
     "gala_spmm_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32, _P]),
+    "gala_spmm_ex_f32": (ctypes.c_int, [_CSR, _P, _I64, _P, _I64, _I32, _P, _P, _I32, _I32, _I32, _I32,
+                                        ctypes.POINTER(gala_spmm_epilogue_t), _P]),
+    "gala_row_broadcast_deg_f32": (ctypes.c_int, [_CSR, _I32, _P, _I64, _P, _I64, _P]),
     "gala_degree_f32": (ctypes.c_int, [_CSR, _P, _F, _I32, _I32, _P]),
     "gala_row_broadcast_f32": (ctypes.c_int, [_I64, _I32, _P, _P, _I64, _P, _I64, _P]),
     "gala_ffn_fwd_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P]),
@@ -180,7 +192,7 @@ def call(fn: str, *args) -> int:
 
 
 # operators with a host-CPU counterpart gala_cpu_X in libgala_cpu.so (include/gala_cpu.h)
-CPU_OPS = ("gala_spmm_f32", "gala_degree_f32", "gala_row_broadcast_f32", "gala_row_scale_relu_f32",
+CPU_OPS = ("gala_spmm_f32", "gala_spmm_ex_f32", "gala_row_broadcast_deg_f32", "gala_degree_f32", "gala_row_broadcast_f32", "gala_row_scale_relu_f32",
            "gala_relu_scale_backward_f32", "gala_ffn_fwd_f32", "gala_sddvv_f32",
            "gala_row_sum_f32", "gala_row_scale_f32", "gala_sddmm_dot_f32",
            "gala_edge_softmax_fwd_f32", "gala_edge_softmax_bwd_f32", "gala_gat_fwd_f32",

@@ -44,6 +44,15 @@ class HipBackend:
     def row_broadcast(self, scale, X, out):
         return self.ops.row_broadcast(scale, X, out=out)
 
+    def spmm_deg(self, g, X, out, out2=None):
+        """out = deg^-0.5 * A X with the norm formed from the rowptr inside the SpMM, and
+        optionally out2 = deg^-0.5 * out (gala_spmm_ex_f32's epilogue)."""
+        return self.ops.spmm(g, X, out=out, dst_deg=True, out2=out2, hub=self.hub)
+
+    def row_broadcast_deg(self, g, X, out):
+        """out = deg^-0.5 * X, the norm from g's rowptr (gala_row_broadcast_deg_f32)."""
+        return self.ops.row_broadcast_deg(g, X, out=out)
+
     def degree(self, g, power=-0.5):
         return self.ops.degree(g, power=power)
 
@@ -166,6 +175,19 @@ class CpuBackend:
     def row_broadcast(self, scale, X, out):
         _abi.call_cpu("gala_row_broadcast_f32", X.shape[0], X.shape[1], _hp(scale), _hp(X), X.stride(0),
                       _hp(out), out.stride(0), None)
+        return out
+
+    def spmm_deg(self, g: CpuGraph, X, out, out2=None):
+        epi = _abi.gala_spmm_epilogue_t()
+        epi.dst_deg_rsqrt = 1
+        epi.Y2, epi.ldy2, epi.y2_scale = _hp(out2), (out2.stride(0) if out2 is not None else 0), None
+        _abi.call_cpu("gala_spmm_ex_f32", g.csr(), _hp(X), X.stride(0), _hp(out), out.stride(0), X.shape[1], None,
+                      None, 0, 0, 5, 7, ctypes.byref(epi), None)
+        return out
+
+    def row_broadcast_deg(self, g: CpuGraph, X, out):
+        _abi.call_cpu("gala_row_broadcast_deg_f32", g.csr(), X.shape[1], _hp(X), X.stride(0), _hp(out),
+                      out.stride(0), None)
         return out
 
     def degree(self, g: CpuGraph, power=-0.5):

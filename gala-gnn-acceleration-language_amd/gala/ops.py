@@ -169,11 +169,14 @@ def _rows_like(X: torch.Tensor, n_rows: int, zero: bool = False) -> torch.Tensor
 
 
 def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=None,
-         accum=False, nsamp=None, ra=5, rb=7, exact=False, hub="exact") -> torch.Tensor:
+         accum=False, nsamp=None, ra=5, rb=7, exact=False, hub="exact", dst_deg=False, out2=None,
+         out2_scale=None) -> torch.Tensor:
     """Y (+)= dst_scale * A (src_scale * X) (gala_spmm_f32).  hub: how the rows of the
     graph's hub-row plan are summed -- "exact" (default, the reference's sequential CSR
     order, bit-identical) or "chunked" (GALA_SPMM_HUB_CHUNKED: 512-edge chunk partials and
-    an ordered fix-up, the fast mode within fp32 summation rounding)."""
+    an ordered fix-up, the fast mode within fp32 summation rounding).  Epilogue
+    (gala_spmm_ex_f32): dst_deg -- the dst factor is deg(r)^-0.5 from the rowptr; out2 --
+    also out2 = out2_scale (or the dst factor) * Y, the next aggregation's pre-scaled input."""
     F = X.shape[1]
     if out is None:
         out = _rows_like(X, g.n_rows, zero=accum)
@@ -182,8 +185,26 @@ def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=No
     chunked = hub == "chunked" and not exact
     flags = ((_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
              | (_abi.GALA_SPMM_EXACT if exact else 0) | (_abi.GALA_SPMM_HUB_CHUNKED if chunked else 0))
+    if dst_deg or out2 is not None:
+        epi = _abi.gala_spmm_epilogue_t()
+        epi.dst_deg_rsqrt = int(bool(dst_deg))
+        epi.Y2, epi.ldy2 = _dp(out2), (out2.stride(0) if out2 is not None else 0)
+        epi.y2_scale = _dp(out2_scale)
+        _abi.call("gala_spmm_ex_f32", g.csr(F), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
+                  _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, ctypes.byref(epi), _stream())
+        return out
     _abi.call("gala_spmm_f32", g.csr(F), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
               _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, _stream())
+    return out
+
+
+def row_broadcast_deg(g: DeviceGraph, X, out=None) -> torch.Tensor:
+    """out[r, :] = deg(r)^-0.5 * X[r, :], deg from g's rowptr (gala_row_broadcast_deg_f32: the
+    degree pass, pow(-0.5) and ROW_BROADCAST in one pass)."""
+    if out is None:
+        out = _rows_like(X, g.n_rows)
+    _abi.call("gala_row_broadcast_deg_f32", g.csr(), X.shape[1], _dp(X), X.stride(0), _dp(out), out.stride(0),
+              _stream())
     return out
 
 

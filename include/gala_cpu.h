@@ -29,6 +29,12 @@ extern "C" {
 int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
                       int32_t F, const float *src_scale, const float *dst_scale, int32_t flags,
                       int32_t nsamp, int32_t ra, int32_t rb, void *stream);
+int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, int64_t ldy,
+                         int32_t F, const float *src_scale, const float *dst_scale, int32_t flags,
+                         int32_t nsamp, int32_t ra, int32_t rb, const gala_spmm_epilogue_t *epi,
+                         void *stream);
+int gala_cpu_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const float *X, int64_t ldx, float *Y,
+                                   int64_t ldy, void *stream);
 int gala_cpu_degree_f32(const gala_csr_t *A, float *deg, float power, int32_t flags,
                         int32_t nsamp, void *stream);
 int gala_cpu_row_broadcast_f32(int64_t n_rows, int32_t F, const float *scale, const float *X,

@@ -153,6 +153,31 @@ int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, in
                   int32_t nsamp, int32_t ra, int32_t rb, void *stream);
 
 /*
+ * gala_spmm_ex_f32: gala_spmm_f32 with an epilogue (NULL: none), for the GCN step
+ * `norm * A (norm * H)` of codegen/gala.cu:433-456 without the separate degree and
+ * ROW_BROADCAST passes:
+ *   dst_deg_rsqrt = 1: the dst factor of row r is deg(r)^-0.5 computed from A's rowptr --
+ *                   the exact values gala_degree_f32(power -0.5) gives (dst_scale must be
+ *                   NULL; one segment; not with GALA_SPMM_SAMPLE);
+ *   Y2 != NULL:     also Y2[r, 0:F] = s2[r] * Y[r, 0:F] (s2 = y2_scale, or the dst factor
+ *                   when NULL), rounded as the ROW_BROADCAST the next aggregation's input
+ *                   would be -- bit-identical to that pass over Y.
+ */
+typedef struct gala_spmm_epilogue {
+    int32_t dst_deg_rsqrt;
+    float *Y2;
+    int64_t ldy2;
+    const float *y2_scale;
+} gala_spmm_epilogue_t;
+int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int32_t F,
+                     const float *src_scale, const float *dst_scale, int32_t flags, int32_t nsamp,
+                     int32_t ra, int32_t rb, const gala_spmm_epilogue_t *epi, void *stream);
+/* Y[r, :] = deg(r)^-0.5 * X[r, :] with deg from A's rowptr (one segment): the degree pass,
+ * pow(-0.5) and the `norm * X` ROW_BROADCAST in one elementwise pass, bit-identical to them. */
+int gala_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const float *X, int64_t ldx, float *Y,
+                               int64_t ldy, void *stream);
+
+/*
  * deg[r] = sum_{e in row r} (val ? val[e] : 1)  (exact integer counts for unweighted
  * graphs), then deg[r] = deg[r]^power when power != 1 (fuses torch::pow(degrees,-0.5),
  * codegen/gala.cu:437-440).  With GALA_SPMM_SAMPLE the degree of the kernel-sampled

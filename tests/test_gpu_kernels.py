@@ -388,6 +388,67 @@ def test_spmm_matches_reference_gspmm_fixtures(path):
         np.testing.assert_array_equal(host(ops.spmm(ops.DeviceGraph.from_host(t, split=False), X)), fx[f"Y_F{F}"])
 
 
+# ---- the GCN step's epilogues (gala_spmm_ex_f32, gala_row_broadcast_deg_f32) ---------
+@pytest.mark.parametrize("F", [1, 7, 32, 47, 128, 2100])
+@pytest.mark.parametrize("kind", ["cora", "hubs", "empty"])
+def test_spmm_epilogue_deg_norm_and_next_input(F, kind):
+    """The degree norm formed from the rowptr and the next aggregation's pre-scaled input
+    written by the SpMM equal the degree pass + pow(-0.5) + ROW_BROADCAST chain bit for bit
+    (codegen/gala.cu:433-456), hub rows (both orders), empty rows and F past one launch's
+    column block (2100 > 512 float4) included; the oracle pins the chain."""
+    g = {"cora": cora_like, "hubs": hub_graph, "empty": with_empty_rows}[kind]()
+    # bit patterns: an empty row's norm is inf (as pow(0, -0.5) is), its sums NaN on both paths
+    _same = lambda a, b: torch.equal(a.contiguous().view(torch.int32), b.contiguous().view(torch.int32))  # noqa: E731
+    dg = ops.DeviceGraph.from_host(g)
+    X = dev(features(g.n_cols, F, seed=5))
+    norm = ops.degree(dg, power=-0.5)
+    np.testing.assert_array_equal(host(norm), orc.degree(to_oracle(g), power=-0.5))
+    Xs = ops.row_broadcast(norm, X)
+    assert _same(ops.row_broadcast_deg(dg, X), Xs)
+    for hub in ("exact", "chunked"):
+        Y = ops.spmm(dg, Xs, dst_scale=norm, hub=hub)
+        Yn = ops.row_broadcast(norm, Y)
+        Y1, Y2 = torch.empty_like(Y), torch.empty_like(Y)
+        ops.spmm(dg, Xs, out=Y1, dst_deg=True, out2=Y2, hub=hub)
+        assert _same(Y1, Y) and _same(Y2, Yn)
+        # a given second scale, and the deg norm without the second output
+        s2 = dev(features(g.n_rows, 1, seed=6).ravel())
+        ops.spmm(dg, Xs, out=Y1, dst_deg=True, out2=Y2, out2_scale=s2, hub=hub)
+        assert _same(Y1, Y) and _same(Y2, ops.row_broadcast(s2, Y))
+        assert _same(ops.spmm(dg, Xs, dst_deg=True, hub=hub), Y)
+    if kind != "hubs":
+        np.testing.assert_array_equal(host(Y1), orc.spmm(to_oracle(g), host(Xs), dst_scale=host(norm)))
+    # accumulate with the deg norm: Y += norm * A X
+    Y0 = dev(features(g.n_rows, F, seed=8))
+    want = ops.spmm(dg, Xs, dst_scale=norm, out=Y0.clone(), accum=True)
+    got = ops.spmm(dg, Xs, dst_deg=True, out=Y0.clone(), accum=True)
+    assert _same(got, want)
+    # refused: the deg norm with a given dst scale, or with kernel sampling
+    with pytest.raises(_abi.GalaError):
+        ops.spmm(dg, Xs, dst_scale=norm, dst_deg=True)
+    with pytest.raises(_abi.GalaError):
+        ops.spmm(dg, Xs, dst_deg=True, nsamp=4)
+
+
+def test_fused_gcn_step_matches_the_chain():
+    """bench.py's fused step (the headline workload) against its unfused chain on a graph
+    with hub rows and one without: all four outputs bit-identical."""
+    import sys
+    sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+    import bench
+    from gala.backend import HipBackend
+    be = HipBackend("cuda")
+    for g in (cora_like(), hub_graph()):
+        agg = bench.OneGpuGCN(g, 32, be)
+        X, dY = dev(features(g.n_rows, 32, seed=1)), dev(features(g.n_rows, 32, seed=2))
+        bufs = [be.empty(g.n_rows, 32) for _ in range(4)]
+        bench.make_step(agg, X, dY, bufs)()
+        want = [b.clone() for b in bufs]
+        bench.make_fused_step(agg, X, dY, bufs)()
+        for a, b in zip(want, bufs):
+            assert torch.equal(a, b)
+
+
 # ---- hub rows (power-law): split plan ----------------------------------------------------
 def hub_graph():
     """R-MAT graph plus a star row of 20k edges and a few mid-size rows."""
