@@ -21,7 +21,8 @@
 //   writeCode   the base's sections, with its two device-specific spellings (a tensor
 //               option `.device(torch::kCUDA, 0)` and `cudaDeviceSynchronize()`, common.h
 //               :686-1557) retargeted to the program's device, and an optional dump of the
-//               first epoch's prediction and the initial weights (GALA_DUMP=<file>).
+//               first epoch's prediction, the initial weights, the loss and the weight
+//               gradients (GALA_DUMP=<file>).
 // The device is GALA_DEVICE (default "cuda", the HIP device of PyTorch-ROCm; "cpu" runs
 // the same program on the host backend).
 #ifndef GALA_HIP_CODEGEN_H
@@ -105,6 +106,24 @@ public:
             "  };\n"
             "  put(\"prediction\", prediction);\n"
             "  for (auto &p : net->named_parameters()) put(p.key(), p.value());\n"
+            "}\n"
+            "// ... and, appended after the first backward, the loss and every weight gradient\n"
+            "template <class Net>\n"
+            "static void gala_program_dump_grads(size_t epoch, const torch::Tensor &loss,\n"
+            "                                    const std::shared_ptr<Net> &net) {\n"
+            "  const char *path = std::getenv(\"GALA_DUMP\");\n"
+            "  if (!path || !*path || epoch != 1) return;\n"
+            "  std::ofstream f(path, std::ios::binary | std::ios::app);\n"
+            "  auto put = [&](const std::string &name, torch::Tensor t) {\n"
+            "    t = t.detach().to(torch::kCPU, torch::kFloat).contiguous();\n"
+            "    f << name << '\\n' << t.dim();\n"
+            "    for (auto s : t.sizes()) f << ' ' << s;\n"
+            "    f << '\\n';\n"
+            "    f.write(reinterpret_cast<const char *>(t.data_ptr<float>()), t.numel() * sizeof(float));\n"
+            "  };\n"
+            "  put(\"loss\", loss.reshape({1}));\n"
+            "  for (auto &p : net->named_parameters())\n"
+            "    if (p.value().grad().defined()) put(p.key() + \".grad\", p.value().grad());\n"
             "}\n"
             "// the reference runtime's names for the operator mirror's free functions\n"
             "using gala::edge_sddvv;\n"
@@ -315,15 +334,22 @@ private:
         }
     }
 
-    // after the loop's `prediction = net->forward(...)[0];` (common.h:1506-1560)
+    // after the loop's `prediction = net->forward(...)[0];`, and before its first
+    // `optimizer.step();` (common.h:1506-1560)
     static void addDumpHook(Code &post) {
+        bool fwd = false, grads = false;
         for (int i = 0; i < post.getNum(); ++i) {
             std::string *l = post.atLine(i);
-            const std::string key = "mod_v)[0];\n";
-            const size_t p = l->find(key);
-            if (p != std::string::npos) {
+            const std::string key = "mod_v)[0];\n", step = "    optimizer.step();";
+            size_t p = l->find(key);
+            if (!fwd && p != std::string::npos) {
                 l->insert(p + key.size(), "    gala_program_dump(epoch, prediction, net);\n");
-                return;
+                fwd = true;
+            }
+            p = l->find(step);
+            if (!grads && p != std::string::npos) {
+                l->insert(p, "    gala_program_dump_grads(epoch, d_loss, net);\n");
+                grads = true;
             }
         }
     }

@@ -1,19 +1,23 @@
 """The reference compiler's HIP code generator (gala-gnn-acceleration-language_amd/refgen/hip.h),
 end to end on the host, where the reference's sources are:
 
-1. refgen/gcn_driver.cpp -- the reference driver's steps (tests/gala_inference.cpp) with
+1. refgen/ir_driver.cpp -- the reference driver's steps (tests/gala_inference.cpp) with
    HIPGenerator in place of CUDAGenerator -- is compiled against the reference's own headers
    (src/codegen/common.h, src/ir, src/frontend/context.h, src/middle-end) and run on a
-   hand-built GCN-2 IR (the front-end's nodes and edges for the GCN layer template; bison
-   is absent, so the parser cannot run);
+   hand-built two-layer IR (the front-end's nodes and edges for the GCN layer template, or
+   for the GAT one of tests/GALA-DSL/gat over the column-tiled graph; bison is absent, so
+   the parser cannot run);
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
    over `<kernel>_call` functions that forward to the operator mirror -- is compiled against
    the reference's host headers (formats, tiling, npy reader) and libgala_torch.so, with no
    CUDA name left in it;
 3. it runs on the host backend (GALA_DEVICE=cpu) over an npy dataset in the reference's
    format, and its first-epoch prediction equals, within 1e-4, galac's program of the same
-   DSL (tests/dsl/gcn_ref_codegen.txt, the same schedule: operator reordering, no code
-   motion) evaluated by the float64 IR executor on the weights the program dumped.
+   DSL (tests/dsl/{gcn,gat}_ref_codegen.txt, the same schedule: operator reordering, no code
+   motion) evaluated by the float64 IR executor on the weights the program dumped, and so
+   do the first epoch's loss and weight gradients.  For GAT
+   that runs the base generator's own autograd classes (edge sum, softmax, the attention-
+   weighted aggregation, common.h:622-894) over the mirror's edge operators.
 """
 import json
 import os
@@ -75,27 +79,51 @@ def _dataset(root, n=600, feat=64, labels=7, seed=3):
     return d, X
 
 
-@pytest.mark.timeout(600)
-def test_hip_generator_emits_a_program_matching_galac(tmp_path):
-    # 1. the reference's driver with the HIP generator, on the hand-built GCN-2 IR
-    drv = tmp_path / "gcn_driver"
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    drv = tmp_path_factory.mktemp("refgen") / "ir_driver"
     r = subprocess.run(["g++", "-std=c++17", "-O1", "-w", f"-I{REF}", f"-I{REF}/src/codegen",
-                        f"-I{PKG}/refgen", f"{PKG}/refgen/gcn_driver.cpp", "-o", str(drv)],
+                        f"-I{PKG}/refgen", f"{PKG}/refgen/ir_driver.cpp", "-o", str(drv)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
+    return drv
+
+
+# model, driver arguments after the dataset (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]), DSL
+CASES = {
+    "gcn": (["64", "7", "32", "3", "2"], "gcn_ref_codegen.txt"),
+    "gat": (["64", "7", "32", "3", "2", "200"], "gat_ref_codegen.txt"),
+}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("model", sorted(CASES))
+def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
+    args, dsl = CASES[model]
+    # 1. the reference's driver with the HIP generator, on the hand-built IR
     out = tmp_path / "out"
     out.mkdir()
-    r = subprocess.run([str(drv), str(out) + "/", "Cora", "64", "7", "32", "3", "2"], capture_output=True,
-                       text=True, timeout=60)
+    r = subprocess.run([str(driver), str(out) + "/", model, "Cora", *args], capture_output=True, text=True,
+                       timeout=60)
     assert r.returncode == 0, r.stderr
     src = (out / "gala.cu").read_text()
     assert (out / "CMakeLists.txt").read_text().count("gala_torch")
-    for cuda_name in ("cudaMalloc", "cudaMemcpy", "cudaDeviceSynchronize", "torch::kCUDA", "__global__", "cusparse"):
+    for cuda_name in ("cudaMalloc", "cudaMemcpy", "cudaDeviceSynchronize", "torch::kCUDA", "__global__", "cusparse",
+                      "unsupported"):
         assert cuda_name not in src, cuda_name
     assert "gala::aggregate_node_mul_sum_call" in src and "aggregate_node_mul_sum_coarse2_AutoGrad" in src
-    # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
-    assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
+    if model == "gcn":
+        # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
+        assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
+    else:
+        # the edge chain of each layer: attention Linears, edge sum, LeakyReLU, softmax, aggregation
+        for a, b in (("efc0->forward", "aggregate_edge_sum_AutoGrad::apply"),
+                     ("aggregate_edge_sum_AutoGrad::apply", "leaky_relu->forward"),
+                     ("leaky_relu->forward", "non_lnr_op_softmax_AutoGrad::apply"),
+                     ("non_lnr_op_softmax_AutoGrad::apply", "aggregate_node_mul_sum_coarse2_AutoGrad::apply(res, attn")):
+            assert fwd.index(a) < fwd.index(b), (a, b)
+        assert "ord_col_tiling_torch" in src   # the column-tiled graph, built by the reference's host code
 
     # 2. the emitted program against the reference's host headers and the operator mirror
     T = _torch_dir()
@@ -117,18 +145,39 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path):
     r = subprocess.run([str(prog)], cwd=str(cwd), capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     dump = _read_dump(tmp_path / "dump.bin")
-    assert set(dump) >= {"prediction", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
+    want_params = {"prediction", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
+    if model == "gat":
+        want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
+    assert set(dump) >= want_params
 
     # galac's program of the same DSL, evaluated in float64 on the dumped weights
     ir_path = tmp_path / "ir.json"
-    r = subprocess.run([GALAC, os.path.join(HERE, "dsl", "gcn_ref_codegen.txt"), "--quiet", "--ir-json",
-                        str(ir_path)], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([GALAC, os.path.join(HERE, "dsl", dsl), "--quiet", "--ir-json", str(ir_path)],
+                       capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     ir = ref.load_ir(str(ir_path))["post"]
     ops = [nd["op"] for nd in ir["nodes"]]
-    assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same reordering
+    if model == "gcn":
+        assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same reordering
+    else:
+        assert ops.count("GAT_AGGREGATE") == 2
     g = layout.load_npy_dataset(d)
     graphs = ref.Graphs(ir, g.rowptr, g.col, np.ones(g.n_rows, np.int32))
-    params = {k: torch.as_tensor(v, dtype=torch.float64) for k, v in dump.items() if k != "prediction"}
-    want = ref.run(ir, graphs, torch.as_tensor(X, dtype=torch.float64), params).detach().numpy()
-    np.testing.assert_allclose(dump["prediction"], want, rtol=1e-4, atol=1e-4)
+    params = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in dump.items()
+              if k != "prediction" and k != "loss" and not k.endswith(".grad")}
+    pred = ref.run(ir, graphs, torch.as_tensor(X, dtype=torch.float64), params)
+    np.testing.assert_allclose(dump["prediction"], pred.detach().numpy(), rtol=1e-4, atol=1e-4)
+
+    # the first backward (the generator's autograd classes over the mirror): loss and every
+    # weight gradient, with _dsl_check's tolerance (1e-4 of the tensor's largest gradient plus
+    # 1e-6 of the model's: the REF GAT chain's attention gradients are a cancelling row sum)
+    mask = torch.as_tensor(np.load(os.path.join(d, "TnMsk.npy")).reshape(-1) != 0)
+    labels = torch.as_tensor(np.load(os.path.join(d, "Lab.npy")).reshape(-1))
+    loss = torch.nn.functional.cross_entropy(pred[mask], labels[mask])
+    np.testing.assert_allclose(float(dump["loss"][0]), loss.item(), rtol=1e-4, atol=1e-5)
+    loss.backward()
+    top = max(np.abs(p.grad.numpy()).max() for p in params.values())
+    for k, p in params.items():
+        want, got = p.grad.numpy(), dump[k + ".grad"]
+        tol = 1e-4 * np.abs(want).max() + 1e-6 * top
+        assert np.abs(got - want).max() <= tol, (k, np.abs(got - want).max(), tol)
