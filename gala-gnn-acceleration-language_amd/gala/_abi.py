@@ -163,6 +163,9 @@ class GalaError(RuntimeError):
 _lib = None
 
 
+ABI_VERSION = 3  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
+
+
 def lib() -> ctypes.CDLL:
     """Load libgala_hip.so (raises if it was not built: no fallback)."""
     global _lib
@@ -176,6 +179,8 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.gala_abi_version() != ABI_VERSION:  # the struct layouts below are ABI_VERSION's
+            raise ImportError(f"{LIB_PATH} has ABI {L.gala_abi_version()}, this module expects {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 
