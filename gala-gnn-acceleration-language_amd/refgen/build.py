@@ -1,0 +1,71 @@
+"""Build recipe of the reference-side HIP code generator's programs.
+
+The reference compiler's driver steps with HIPGenerator (refgen/ir_driver.cpp, compiled
+against the reference's own headers where they lie) emit a CMakeLists.txt + gala.cu; the
+gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here with g++
+against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
+only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
+
+    python refgen/build.py            # refgen/bin/gala_gcn and refgen/bin/gala_gat
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+REF = os.environ.get("GALA_REF_ROOT", "/root/reference")
+BIN = os.path.join(HERE, "bin")
+
+# the programs the GPU test runs: driver arguments after DATASET
+# (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]); the GAT one over 4 column tiles of 20 000 rows
+PROGRAMS = {
+    "gcn": ["64", "7", "32", "3", "2"],
+    "gat": ["64", "7", "32", "3", "2", "5000"],
+}
+
+
+def have_reference() -> bool:
+    return os.path.isfile(os.path.join(REF, "src", "codegen", "common.h"))
+
+
+def compile_driver(exe: str) -> None:
+    subprocess.run(["g++", "-std=c++17", "-O1", "-w", f"-I{REF}", f"-I{REF}/src/codegen", f"-I{HERE}",
+                    os.path.join(HERE, "ir_driver.cpp"), "-o", exe], check=True, capture_output=True, text=True,
+                   timeout=300)
+
+
+def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
+    os.makedirs(out_dir, exist_ok=True)
+    subprocess.run([driver, out_dir.rstrip("/") + "/", model, dataset, *args], check=True, capture_output=True,
+                   text=True, timeout=60)
+    return os.path.join(out_dir, "gala.cu")
+
+
+def compile_program(src: str, exe: str) -> None:
+    import torch
+    T = os.path.dirname(torch.__file__)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-w", "-fopenmp", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                    "-x", "c++", src, f"-I{REF}", f"-I{T}/include", f"-I{T}/include/torch/csrc/api/include",
+                    "-I/opt/rocm/include", f"-I{PKG}/host", f"-I{ROOT}/include", "-o", exe, f"-L{T}/lib",
+                    f"-Wl,-rpath,{T}/lib", "-Wl,--no-as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip",
+                    "-ltorch_hip", f"-L{PKG}/gala", f"-Wl,-rpath,{PKG}/gala", "-lgala_torch", "-Wl,--as-needed"],
+                   check=True, capture_output=True, text=True, timeout=600)
+
+
+def build_all() -> None:
+    os.makedirs(BIN, exist_ok=True)
+    driver = os.path.join(BIN, "ir_driver")
+    compile_driver(driver)
+    for model, args in PROGRAMS.items():
+        src = emit(driver, os.path.join(BIN, "src_" + model), model, "Cora", args)
+        compile_program(src, os.path.join(BIN, "gala_" + model))
+        print(f"refgen: built {os.path.join(BIN, 'gala_' + model)}")
+
+
+if __name__ == "__main__":
+    if not have_reference():
+        print(f"refgen: {REF} is absent, nothing built", file=sys.stderr)
+        sys.exit(0)
+    build_all()

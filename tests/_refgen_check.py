@@ -1,0 +1,107 @@
+"""Shared checks of programs emitted by the reference compiler's HIP generator
+(gala-gnn-acceleration-language_amd/refgen): the npy dataset they read, their GALA_DUMP
+output, and the comparison with galac's program of the same DSL in the float64 IR executor.
+Used by tests/test_ref_hip_emitter_cpu.py (host backend) and tests/test_gpu_refgen.py
+(MI355X); reads nothing of the reference."""
+import os
+import subprocess
+
+import numpy as np
+import torch
+
+import _ir_ref as ref
+from gala import layout
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
+GALAC = os.path.join(PKG, "gala", "galac")
+DSL = {"gcn": "gcn_ref_codegen.txt", "gat": "gat_ref_codegen.txt"}
+
+
+def read_dump(path):
+    """refgen/hip.h's GALA_DUMP format: per tensor a name line, a 'ndim dims...' line, then
+    the float32 values."""
+    out = {}
+    with open(path, "rb") as f:
+        data = f.read()
+    pos = 0
+    while pos < len(data):
+        e = data.index(b"\n", pos)
+        name = data[pos:e].decode()
+        e2 = data.index(b"\n", e + 1)
+        dims = [int(v) for v in data[e + 1:e2].split()]
+        shape = tuple(dims[1:1 + dims[0]])
+        n = int(np.prod(shape)) if shape else 1
+        out[name] = np.frombuffer(data[e2 + 1:e2 + 1 + 4 * n], np.float32).reshape(shape).copy()
+        pos = e2 + 1 + 4 * n
+    return out
+
+
+def dataset(root, n=600, nnz=2400, feat=64, labels=7, seed=3):
+    """An npy dataset in the reference's format (readSM_npy32 + readDM_npy) under
+    root/Data/Cora/; the emitted program reads ../../Data/<name>/ from its working directory."""
+    g = layout.gen_graph("uniform", n, nnz, seed=seed)
+    rows = np.repeat(np.arange(n), np.diff(g.rowptr)).astype(np.uint32)
+    d = os.path.join(root, "Data", "Cora")
+    os.makedirs(d)
+    np.save(os.path.join(d, "Adj_src.npy"), np.concatenate([[n, n], rows]).astype(np.uint32))
+    np.save(os.path.join(d, "Adj_dst.npy"), g.col.astype(np.uint32))
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-1, 1, (n, feat)).astype(np.float32)
+    np.save(os.path.join(d, "Feat.npy"), X)
+    np.save(os.path.join(d, "Lab.npy"), rng.integers(0, labels, (n, 1)).astype(np.int64))
+    for name, frac in (("TnMsk", 0.3), ("VlMsk", 0.2), ("TsMsk", 0.5)):
+        np.save(os.path.join(d, name + ".npy"), (rng.random((n, 1)) < frac).astype(np.int32))
+    return d, X
+
+
+def run_program(exe, root, device, timeout=300):
+    """Run an emitted program from root/run/b on `device` ("cpu" or "cuda"); its dump."""
+    cwd = os.path.join(root, "run", "b")
+    os.makedirs(cwd)
+    dump = os.path.join(root, "dump.bin")
+    env = dict(os.environ, GALA_DEVICE=device, GALA_DUMP=dump, OMP_NUM_THREADS="2")
+    r = subprocess.run([exe], cwd=cwd, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return read_dump(dump)
+
+
+def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
+    """The dump's first-epoch prediction, loss and weight gradients against galac's program
+    of the same DSL (tests/dsl/<model>_ref_codegen.txt) in the float64 IR executor.
+    noise_floor: the gradient tolerance's share of the model's largest gradient. The REF GAT
+    chain's attention-bias gradient is N * 1e-12 plus per-row softmax-gradient sums that cancel
+    exactly, so its fp32 value is rounding noise that grows with the row count N."""
+    want_params = {"prediction", "loss", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
+    if model == "gat":
+        want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
+    assert set(dump) >= want_params, sorted(dump)
+    r = subprocess.run([GALAC, os.path.join(HERE, "dsl", DSL[model]), "--quiet", "--ir-json", str(ir_path)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    ir = ref.load_ir(str(ir_path))["post"]
+    ops = [nd["op"] for nd in ir["nodes"]]
+    if model == "gcn":
+        assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same operator reordering
+    else:
+        assert ops.count("GAT_AGGREGATE") == 2
+    g = layout.load_npy_dataset(d)
+    graphs = ref.Graphs(ir, g.rowptr, g.col, np.ones(g.n_rows, np.int32))
+    params = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in dump.items()
+              if k != "prediction" and k != "loss" and not k.endswith(".grad")}
+    pred = ref.run(ir, graphs, torch.as_tensor(X, dtype=torch.float64), params)
+    np.testing.assert_allclose(dump["prediction"], pred.detach().numpy(), rtol=1e-4, atol=1e-4)
+    # the first backward (the generator's autograd classes over the mirror): loss and every
+    # weight gradient, with _dsl_check's tolerance (1e-4 of the tensor's largest gradient plus
+    # noise_floor of the model's)
+    mask = torch.as_tensor(np.load(os.path.join(d, "TnMsk.npy")).reshape(-1) != 0)
+    labels = torch.as_tensor(np.load(os.path.join(d, "Lab.npy")).reshape(-1))
+    loss = torch.nn.functional.cross_entropy(pred[mask], labels[mask])
+    np.testing.assert_allclose(float(dump["loss"][0]), loss.item(), rtol=1e-4, atol=1e-5)
+    loss.backward()
+    top = max(np.abs(p.grad.numpy()).max() for p in params.values())
+    for k, p in params.items():
+        want, got = p.grad.numpy(), dump[k + ".grad"]
+        tol = 1e-4 * np.abs(want).max() + noise_floor * top
+        assert np.abs(got - want).max() <= tol, (k, np.abs(got - want).max(), tol)

@@ -10,103 +10,50 @@ end to end on the host, where the reference's sources are:
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
    over `<kernel>_call` functions that forward to the operator mirror -- is compiled against
    the reference's host headers (formats, tiling, npy reader) and libgala_torch.so, with no
-   CUDA name left in it;
+   CUDA name left in it (refgen/build.py's recipe);
 3. it runs on the host backend (GALA_DEVICE=cpu) over an npy dataset in the reference's
-   format, and its first-epoch prediction equals, within 1e-4, galac's program of the same
-   DSL (tests/dsl/{gcn,gat}_ref_codegen.txt, the same schedule: operator reordering, no code
-   motion) evaluated by the float64 IR executor on the weights the program dumped, and so
-   do the first epoch's loss and weight gradients.  For GAT
-   that runs the base generator's own autograd classes (edge sum, softmax, the attention-
-   weighted aggregation, common.h:622-894) over the mirror's edge operators.
+   format, and its first-epoch prediction, loss and weight gradients equal, within 1e-4,
+   galac's program of the same DSL (tests/dsl/{gcn,gat}_ref_codegen.txt, the same schedule:
+   operator reordering, no code motion) evaluated by the float64 IR executor on the weights
+   the program dumped.  For GAT that runs the base generator's own autograd classes (edge
+   sum, softmax, the attention-weighted aggregation, common.h:622-894) over the mirror's
+   edge operators.
+tests/test_gpu_refgen.py runs the programs refgen/build.py builds on the MI355X.
 """
-import json
+import importlib.util
 import os
-import subprocess
 
-import numpy as np
 import pytest
-import torch
 
-import _ir_ref as ref
-from gala import layout
+import _refgen_check as rc
 
-HERE = os.path.dirname(os.path.abspath(__file__))
-ROOT = os.path.dirname(HERE)
-PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
-REF = os.environ.get("GALA_REF_ROOT", "/root/reference")
-GALAC = os.path.join(PKG, "gala", "galac")
+_spec = importlib.util.spec_from_file_location("gala_refgen_build", os.path.join(rc.PKG, "refgen", "build.py"))
+refgen = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(refgen)
 
-pytestmark = pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "src", "codegen", "common.h")),
-                                reason="the reference's sources are not present")
+pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the reference's sources are not present")
 
-
-def _torch_dir():
-    return os.path.dirname(torch.__file__)
-
-
-def _read_dump(path):
-    """refgen/hip.h's GALA_DUMP format: per tensor a name line, a 'ndim dims...' line, then
-    the float32 values."""
-    out = {}
-    with open(path, "rb") as f:
-        data = f.read()
-    pos = 0
-    while pos < len(data):
-        e = data.index(b"\n", pos)
-        name = data[pos:e].decode()
-        e2 = data.index(b"\n", e + 1)
-        dims = [int(v) for v in data[e + 1:e2].split()]
-        shape = tuple(dims[1:1 + dims[0]])
-        n = int(np.prod(shape)) if shape else 1
-        out[name] = np.frombuffer(data[e2 + 1:e2 + 1 + 4 * n], np.float32).reshape(shape).copy()
-        pos = e2 + 1 + 4 * n
-    return out
-
-
-def _dataset(root, n=600, feat=64, labels=7, seed=3):
-    g = layout.gen_graph("uniform", n, 2400, seed=seed)
-    rows = np.repeat(np.arange(n), np.diff(g.rowptr)).astype(np.uint32)
-    d = os.path.join(root, "Data", "Cora")
-    os.makedirs(d)
-    np.save(os.path.join(d, "Adj_src.npy"), np.concatenate([[n, n], rows]).astype(np.uint32))
-    np.save(os.path.join(d, "Adj_dst.npy"), g.col.astype(np.uint32))
-    rng = np.random.default_rng(seed)
-    X = rng.uniform(-1, 1, (n, feat)).astype(np.float32)
-    np.save(os.path.join(d, "Feat.npy"), X)
-    np.save(os.path.join(d, "Lab.npy"), rng.integers(0, labels, (n, 1)).astype(np.int64))
-    for name, frac in (("TnMsk", 0.3), ("VlMsk", 0.2), ("TsMsk", 0.5)):
-        np.save(os.path.join(d, name + ".npy"), (rng.random((n, 1)) < frac).astype(np.int32))
-    return d, X
+# model, driver arguments after the dataset (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]):
+# the GAT graph of 600 rows in 3 column tiles
+CASES = {
+    "gcn": ["64", "7", "32", "3", "2"],
+    "gat": ["64", "7", "32", "3", "2", "200"],
+}
 
 
 @pytest.fixture(scope="module")
 def driver(tmp_path_factory):
-    drv = tmp_path_factory.mktemp("refgen") / "ir_driver"
-    r = subprocess.run(["g++", "-std=c++17", "-O1", "-w", f"-I{REF}", f"-I{REF}/src/codegen",
-                        f"-I{PKG}/refgen", f"{PKG}/refgen/ir_driver.cpp", "-o", str(drv)],
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    return drv
-
-
-# model, driver arguments after the dataset (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]), DSL
-CASES = {
-    "gcn": (["64", "7", "32", "3", "2"], "gcn_ref_codegen.txt"),
-    "gat": (["64", "7", "32", "3", "2", "200"], "gat_ref_codegen.txt"),
-}
+    exe = str(tmp_path_factory.mktemp("refgen") / "ir_driver")
+    refgen.compile_driver(exe)
+    return exe
 
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("model", sorted(CASES))
 def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
-    args, dsl = CASES[model]
     # 1. the reference's driver with the HIP generator, on the hand-built IR
     out = tmp_path / "out"
-    out.mkdir()
-    r = subprocess.run([str(driver), str(out) + "/", model, "Cora", *args], capture_output=True, text=True,
-                       timeout=60)
-    assert r.returncode == 0, r.stderr
-    src = (out / "gala.cu").read_text()
+    src = open(refgen.emit(driver, str(out), model, "Cora", CASES[model])).read()
     assert (out / "CMakeLists.txt").read_text().count("gala_torch")
     for cuda_name in ("cudaMalloc", "cudaMemcpy", "cudaDeviceSynchronize", "torch::kCUDA", "__global__", "cusparse",
                       "unsupported"):
@@ -126,58 +73,10 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
         assert "ord_col_tiling_torch" in src   # the column-tiled graph, built by the reference's host code
 
     # 2. the emitted program against the reference's host headers and the operator mirror
-    T = _torch_dir()
-    prog = tmp_path / "gala_model"
-    r = subprocess.run(["g++", "-O2", "-std=c++17", "-w", "-fopenmp", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                        "-x", "c++", str(out / "gala.cu"), f"-I{REF}", f"-I{T}/include",
-                        f"-I{T}/include/torch/csrc/api/include", "-I/opt/rocm/include", f"-I{PKG}/host",
-                        f"-I{ROOT}/include", "-o", str(prog), f"-L{T}/lib", f"-Wl,-rpath,{T}/lib",
-                        "-Wl,--no-as-needed", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip",
-                        f"-L{PKG}/gala", f"-Wl,-rpath,{PKG}/gala", "-lgala_torch", "-Wl,--as-needed"],
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    prog = str(tmp_path / "gala_model")
+    refgen.compile_program(str(out / "gala.cu"), prog)
 
-    # 3. run on the host backend (the program reads ../../Data/<name>/, gala.cu's path)
-    d, X = _dataset(tmp_path)
-    cwd = tmp_path / "run" / "b"
-    cwd.mkdir(parents=True)
-    env = dict(os.environ, GALA_DEVICE="cpu", GALA_DUMP=str(tmp_path / "dump.bin"), OMP_NUM_THREADS="2")
-    r = subprocess.run([str(prog)], cwd=str(cwd), capture_output=True, text=True, timeout=120, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    dump = _read_dump(tmp_path / "dump.bin")
-    want_params = {"prediction", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
-    if model == "gat":
-        want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
-    assert set(dump) >= want_params
-
-    # galac's program of the same DSL, evaluated in float64 on the dumped weights
-    ir_path = tmp_path / "ir.json"
-    r = subprocess.run([GALAC, os.path.join(HERE, "dsl", dsl), "--quiet", "--ir-json", str(ir_path)],
-                       capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
-    ir = ref.load_ir(str(ir_path))["post"]
-    ops = [nd["op"] for nd in ir["nodes"]]
-    if model == "gcn":
-        assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same reordering
-    else:
-        assert ops.count("GAT_AGGREGATE") == 2
-    g = layout.load_npy_dataset(d)
-    graphs = ref.Graphs(ir, g.rowptr, g.col, np.ones(g.n_rows, np.int32))
-    params = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in dump.items()
-              if k != "prediction" and k != "loss" and not k.endswith(".grad")}
-    pred = ref.run(ir, graphs, torch.as_tensor(X, dtype=torch.float64), params)
-    np.testing.assert_allclose(dump["prediction"], pred.detach().numpy(), rtol=1e-4, atol=1e-4)
-
-    # the first backward (the generator's autograd classes over the mirror): loss and every
-    # weight gradient, with _dsl_check's tolerance (1e-4 of the tensor's largest gradient plus
-    # 1e-6 of the model's: the REF GAT chain's attention gradients are a cancelling row sum)
-    mask = torch.as_tensor(np.load(os.path.join(d, "TnMsk.npy")).reshape(-1) != 0)
-    labels = torch.as_tensor(np.load(os.path.join(d, "Lab.npy")).reshape(-1))
-    loss = torch.nn.functional.cross_entropy(pred[mask], labels[mask])
-    np.testing.assert_allclose(float(dump["loss"][0]), loss.item(), rtol=1e-4, atol=1e-5)
-    loss.backward()
-    top = max(np.abs(p.grad.numpy()).max() for p in params.values())
-    for k, p in params.items():
-        want, got = p.grad.numpy(), dump[k + ".grad"]
-        tol = 1e-4 * np.abs(want).max() + 1e-6 * top
-        assert np.abs(got - want).max() <= tol, (k, np.abs(got - want).max(), tol)
+    # 3. run on the host backend, check against galac's program in the float64 executor
+    d, X = rc.dataset(tmp_path)
+    dump = rc.run_program(prog, str(tmp_path), "cpu", timeout=120)
+    rc.check_against_galac(model, dump, d, X, tmp_path / "ir.json")
