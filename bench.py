@@ -907,11 +907,14 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     return out
 
 
-def rmat_traffic():
-    """PMC bytes of one R-MAT SpMM call: the rows + hub chunks grid and the chunk fix-up
-    (tools/gpu_pmc_rmat.sh -> profiles/traffic.json), or None."""
-    a = load_traffic("k_spmm_rows_chunks<4, 8, 1, 4, false, false>")
-    b = load_traffic("k_spmm_fixup<4, 8, 1, false>")
+def rmat_traffic(hub: str):
+    """PMC bytes of one R-MAT SpMM call (profiles/traffic.json's "rmat|" entries: the PMC
+    passes of tools/rmat_prof.py, tools/gpu_job.sh pmccmd=rmat + tools/merge_traffic.py), or
+    None. exact: the degree-ordered row kernel + the REF-order hub kernel beside it; chunked:
+    the rows + hub chunks grid and the chunk fix-up."""
+    names = (("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>", "k_spmm_hub_exact<4, 32, false, false>")
+             if hub == "exact" else ("k_spmm_rows_chunks<4, 8, 1, 4, false, false>", "k_spmm_fixup<4, 8, 1, false>"))
+    a, b = (load_traffic("rmat|void gala::" + n) for n in names)
     return a + b if a is not None and b is not None else None
 
 
@@ -950,7 +953,7 @@ def rmat_family(args, dev, be, timer, sync, kind="rmat"):
            "roofline": {"bound": "hbm", "achieved": alg / t_kernel / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
                         "alg_bytes_per_launch": alg,
-                        "traffic": (None if be.name != "hip" or kind == "rmat" else
+                        "traffic": (None if be.name != "hip" else rmat_traffic("exact") if kind == "rmat" else
                                     load_traffic("banded|void gala::k_spmm_rowgroup<4, 8, 1, 4, false, false, false>")),
                         "kernel": "gala_spmm_f32 (degree-ordered k_spmm_rowgroup + k_spmm_hub_exact on a side "
                                   "stream: the hub rows in the reference's order)" if kind == "rmat" else
@@ -966,7 +969,7 @@ def rmat_family(args, dev, be, timer, sync, kind="rmat"):
             tc_kernel = timer(lambda: be.spmm(agg.g, agg.Xs, bufs[0], agg.norm, False), 10)
         finally:
             be.hub = "exact"
-        tr = rmat_traffic() if kind == "rmat" else None
+        tr = rmat_traffic("chunked") if kind == "rmat" else None
         out["chunked"] = {"hub_order": "chunked: 512-edge partials + ordered fix-up (GALA_SPMM_HUB_CHUNKED; fp32 "
                                        "summation rounding of REF)",
                           "value": 4 * hg.nnz / tc_step, "ms_per_step": tc_step * 1e3,

@@ -26,11 +26,13 @@ OUT="$GRAFT_REPO_ROOT/gpurun_out"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export PYTHONPATH="$GRAFT_REPO_ROOT/gala-gnn-acceleration-language_amd${PYTHONPATH:+:$PYTHONPATH}"
-BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-banded"
-# the banded family's SpMM has the uniform one's kernel name: rocprof and PMC runs of
-# bench.py leave it out, so a kernel's average / bytes are the headline graph's (the banded
-# graph's own: pmccmd=banded,python3,<repo>/tools/banded_spmm.py,banded)
-BENCH_PMC_ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-banded"
+BENCH_PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-banded --no-rmat"
+# the banded and R-MAT families' SpMMs run the uniform one's row kernel: rocprof and PMC runs
+# of bench.py leave them out, so a kernel's average / bytes are the headline graph's (the
+# families' own: pmccmd=banded,python3,<repo>/tools/banded_spmm.py,banded and
+# pmccmd=rmat,python3,<repo>/tools/rmat_prof.py, merged into profiles/traffic.json under a
+# "banded|" / "rmat|" prefix by tools/merge_traffic.py)
+BENCH_PMC_ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-banded --no-rmat"
 
 step() {  # name, limit, command...
     local name=$1 lim=$2
