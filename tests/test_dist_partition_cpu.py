@@ -396,6 +396,22 @@ def _gat_attn_weights():
     return rng.uniform(-0.5, 0.5, F_GAT).astype(np.float32), rng.uniform(-0.5, 0.5, H_GAT).astype(np.float32)
 
 
+def _check_gat_against_oracle(g, got):
+    """A distributed REF layer with the attention Linear (Y, dX, d_aL gathered over the
+    ranks) against the oracle's pass-by-pass REF layer (orc_gat_ref_layer: edge sum,
+    LeakyReLU, REF softmax, aggregation, and the REF backward chain), whose dX gets the
+    attention Linear's term d_aL * wR, at 1e-4."""
+    import oracle as orc
+    aL, _, X = _gat_inputs(g)
+    wR, bR = _gat_attn_weights()
+    dY = np.random.default_rng(22).uniform(-1, 1, (g.n_rows, F_GAT)).astype(np.float32)
+    lay = orc.GatRefLayer(g.rowptr, g.col, g.n_rows, X, dY, aL, wR, bR, H_GAT).run()
+    D = F_GAT // H_GAT
+    dX = lay.dX.astype(np.float64) + np.repeat(lay.daL.astype(np.float64), D, 1) * wR.astype(np.float64)
+    for a, b, what in ((got[0], lay.Y, "Y"), (got[1], dX, "dX"), (got[2], lay.daL, "d_aL")):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4, err_msg=what)
+
+
 def _gat_train_one_process(g, rc=False):
     """Y, dX, d_aL of the REF layer on one process (gala_cpu_gat_{fwd,bwd}_stats_f32); rc:
     the source logits recomputed from X (wR, bR), dX then including the path through aR
@@ -477,7 +493,8 @@ def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc, ex
     """VertexCutGat.forward_train / backward (gala_gat_fwd_partial_stats_f32 partials, one
     exchange per direction, d_aL from the owner's row statistics) against the one-process
     row-statistics pair: Y, dX and d_aL within fp32 rounding; with the source logits
-    recomputed, dX includes the path through aR and the Linear's gradients match."""
+    recomputed, dX includes the path through aR and the Linear's gradients match, and Y, dX,
+    d_aL are within 1e-4 of the oracle's REF layer."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -492,6 +509,8 @@ def test_vertex_cut_gat_training_matches_one_process(world, name, chunks, rc, ex
     ref = _gat_train_one_process(GRAPHS[name](), rc)
     for a, b, what in zip(got, ref, ("Y", "dX", "d_aL", "dwR", "dbR")):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4, err_msg=what)
+    if rc:
+        _check_gat_against_oracle(GRAPHS[name](), got)
 
 
 def test_auto_halo_mode_is_one_choice_for_all_ranks():
@@ -554,7 +573,8 @@ def test_halo_gat_bit_identical_to_one_process(world, name, rc, halo_mode):
     """HaloGat (gala/dist.py): each rank runs the one-process statistics kernels over its rows
     with the pattern's columns in the gathered table (gala_cpu_gat_{fwd,bwd}_stats_ex_f32):
     Y, dX and d_aL are bit-identical to the one-process pair, the Linear's gradients within
-    fp32 rounding (summed over ranks)."""
+    fp32 rounding (summed over ranks); with the attention Linear, Y, dX and d_aL are also
+    within 1e-4 of the oracle's REF layer (the reference's pass sequence)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -565,13 +585,15 @@ def test_halo_gat_bit_identical_to_one_process(world, name, rc, halo_mode):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = _gat_train_one_process(GRAPHS[name](), rc)
+    g = GRAPHS[name]()
+    ref = _gat_train_one_process(g, rc)
     np.testing.assert_array_equal(got[0], ref[0])
     np.testing.assert_array_equal(got[2], ref[2])
     if rc:     # the one-process reference adds the Linear path in float64
         np.testing.assert_allclose(got[1], ref[1], rtol=1e-5, atol=1e-6)
         for a, b in zip(got[3:], ref[3:]):
             np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+        _check_gat_against_oracle(g, got)
     else:
         np.testing.assert_array_equal(got[1], ref[1])
 
