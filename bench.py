@@ -204,7 +204,8 @@ def load_traffic(kernel_substr: str):
     try:
         d = json.load(open(path))
         for k, v in d.get("kernels", {}).items():
-            if kernel_substr in k:
+            # "banded|" / "rmat|" entries are another graph's launches of the same kernel
+            if kernel_substr in k and ("|" in kernel_substr or "|" not in k):
                 return float(v["hbm_bytes_per_launch"])
     except Exception:
         return None
