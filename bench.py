@@ -61,7 +61,21 @@ PIPE_CHUNKS = 4
 
 
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    print(f"[+{time.time() - START:.1f}s]", *a, file=sys.stderr, flush=True)
+
+
+def start_heartbeat(rank: int, period_s: float = 60.0):
+    """N > 1: rank 0 logs that it is alive every period_s (a phase of host-staged gloo
+    collectives, or a slow rank, can run for minutes without a log line)."""
+    import threading
+    if rank != 0:
+        return
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(period_s):
+            log("[bench] alive")
+    threading.Thread(target=beat, daemon=True).start()
 
 
 def _free_port() -> int:
@@ -582,6 +596,7 @@ def run_multi(args, rank, world, dev, be, timer, sync):
         return float(t.item())
 
     budget = Budget(args.budget_s, reduce_max)
+    start_heartbeat(rank)
     t0 = time.time()
     fam, g, bounds = strong_family(args, "uniform", rank, world, dev, be, comm, timer, sync, barrier, reduce_max,
                                    budget)
@@ -613,7 +628,7 @@ def run_multi(args, rank, world, dev, be, timer, sync):
     if not args.no_gat and budget.ok(t_uniform, "gat field"):
         t0 = time.time()
         try:
-            out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max)
+            out["gat"] = gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max, budget)
         except Exception as e:  # noqa: BLE001  (reported; the headline line stays)
             if not _recoverable(e):
                 raise
@@ -653,7 +668,7 @@ def run_multi(args, rank, world, dev, be, timer, sync):
     return out
 
 
-def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max):
+def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce_max, budget=None):
     """The "gat" field at N > 1: the same 8-head GAT layer as at N = 1 (forward + backward,
     REF, the source logit formed from X), strong-scaled over the one graph.  The layouts are
     timed for a few steps and the faster runs the timed steps:
@@ -678,35 +693,52 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
     aL = torch.rand((n, H), device=dev, generator=gen) - 0.5
     wR = (torch.rand(F, device=dev, generator=gen) - 0.5) * 0.2
     bR = torch.zeros(H, device=dev)
-    layers = {}
     hpart = gdist.partition_graph(g, rank, world, bounds=bounds)
-    layers["halo"] = gdist.HaloGat(hpart, F, H, be, comm)
-    layers["halo-overlap"] = gdist.HaloGatOverlap(hpart, F, H, be, comm)
-    ppart = None
-    if world > 1 and hpart.halo_mode == "dense":    # the all-gather in row chunks, pipelined
-        ppart = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
-        layers["halo-overlap-pipe"] = gdist.HaloGatOverlap(ppart, F, H, be, comm)
-    vpart = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
-    layers["vcut"] = vc.VertexCutGat(vpart, F, H, be, comm)
-    X = layers["halo"].own_rows("X")              # the layer input, written into the table
+    halo = gdist.HaloGat(hpart, F, H, be, comm)
+    X = halo.own_rows("X")              # the layer input, written into the table
     X.copy_(torch.rand((n, F), device=dev, generator=gen) * 2 - 1)
-    dY = layers["halo"].own_rows("dY")
+    dY = halo.own_rows("dY")
     dY.copy_(torch.rand((n, F), device=dev, generator=gen) * 2 - 1)
+    comm_bytes = {"halo": hpart.halo_bytes(2 * F + H) if world > 1 else 0}
+    comm_bytes["halo-overlap"] = comm_bytes["halo"]
+
+    def pipe_layer():       # the all-gather in row chunks, pipelined
+        ppart = gdist.partition_graph(g, rank, world, bounds=bounds, halo_mode="dense", chunks=PIPE_CHUNKS)
+        comm_bytes["halo-overlap-pipe"] = ppart.halo_bytes(2 * F + H)
+        return gdist.HaloGatOverlap(ppart, F, H, be, comm)
+
+    def vcut_layer():
+        vpart = vc.vertex_cut_partition(g, rank, world, PIPE_CHUNKS, bounds)
+        comm_bytes["vcut"] = vpart.comm_bytes(2 * F + 2 * H) + vpart.comm_bytes(F)
+        return vc.VertexCutGat(vpart, F, H, be, comm)
+
+    # candidates are built when they are timed; after the first, one more is timed only while
+    # the budget holds (the estimate: the slowest candidate so far, build included)
+    makers = [("halo", lambda: halo), ("halo-overlap", lambda: gdist.HaloGatOverlap(hpart, F, H, be, comm))]
+    if world > 1 and hpart.halo_mode == "dense":
+        makers.append(("halo-overlap-pipe", pipe_layer))
+    makers.append(("vcut", vcut_layer))
 
     def step_of(layer):
         def step():
             layer.forward_train(aL, None, X, wR, bR)   # source logits recomputed from X, as at N = 1
             layer.backward(dY, linear=False)           # the aggregation's backward, as gala_gat_bwd_stats_f32
         return step
-    cand = {k: timed_steps(step_of(v), args.calib_steps, 2, sync, barrier, reduce_max) for k, v in layers.items()}
+    cand, kept, longest = {}, {}, 0.0
+    for name, make in makers:
+        if cand and budget is not None and not budget.ok(longest, f"gat candidate {name}"):
+            continue
+        tc = time.time()
+        layer = make()
+        cand[name] = timed_steps(step_of(layer), args.calib_steps, 2, sync, barrier, reduce_max)
+        log(f"[rank {rank}] gat candidate {name}: {cand[name] * 1e3:.3f} ms/step")
+        if cand[name] == min(cand.values()):
+            kept = {name: layer}
+        del layer
+        longest = max(longest, time.time() - tc)
     best = min(cand, key=cand.get)
     steps = max(args.steps // 2, 2)
-    t_step = timed_steps(step_of(layers[best]), steps, 2, sync, barrier, reduce_max)
-    comm_bytes = {"halo": hpart.halo_bytes(2 * F + H) if world > 1 else 0,
-                  "vcut": vpart.comm_bytes(2 * F + 2 * H) + vpart.comm_bytes(F)}
-    comm_bytes["halo-overlap"] = comm_bytes["halo"]
-    if ppart is not None:
-        comm_bytes["halo-overlap-pipe"] = ppart.halo_bytes(2 * F + H)
+    t_step = timed_steps(step_of(kept[best]), steps, 2, sync, barrier, reduce_max)
     desc = {"halo": "row partition, gathered X / logits / dY rows, the one-GPU kernels (bit-identical)",
             "halo-overlap": "row partition, gathered X / logits / dY rows; own-column partial statistics "
                             "overlap the exchange (fp32 rounding of one GPU)",
@@ -720,7 +752,7 @@ def gat_multi(args, g, rank, world, dev, be, comm, bounds, sync, barrier, reduce
            "candidates_ms_per_step": {k: v * 1e3 for k, v in cand.items()},
            "comm_bytes_per_step_per_rank": comm_bytes[best],
            "comm_bytes_per_step_per_rank_candidates": comm_bytes}
-    del layers, X, dY, ppart
+    del kept, halo, X, dY
     return out
 
 

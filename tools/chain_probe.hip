@@ -1,0 +1,102 @@
+// chain_probe.hip -- what one dependent fp32 add chain costs per element on gfx950, the
+// bound of the REF-order hub kernel (k_spmm_hub_exact's chain wave).
+//   reg : acc = acc + r[k] over values held in registers (the latency floor)
+//   lds : the hub chain's loop: 16-B LDS reads of an edge quad, issued two 16-edge groups
+//         ahead of the adds (as in spmm.hip's run_chain)
+//   lds1: the same with one group ahead
+// One workgroup of 64 lanes (one wave), n adds per lane; cycles from s_memtime around the
+// loop (shader clock), time from HIP events.  Measurement only.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/chain_probe tools/chain_probe.hip && tools/chain_probe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef float F4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_chain(const float *seed, float *out, long long *cycles, int n) {
+    __shared__ F4 buf[1024];  // 16 KB: [256 quads][4 lanes-groups]: lane l reads buf[(q*16 + l%16)]
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 1024; i += 64) {
+        const float s = seed[i % 64];
+        buf[i] = F4{s, s * 0.5f, s * 0.25f, s * 0.125f};
+    }
+    __syncthreads();
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = seed[(lane + k) % 64] * 1e-3f;
+    float acc = 0.0f;
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    if constexpr (MODE == 0) {
+        for (int i = 0; i < n; i += 16) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc = __fadd_rn(acc, r[k]);
+        }
+    } else {
+        // quads of 4 edges: 4 reads per 16-edge group, AHEAD groups in flight
+        constexpr int AHEAD = MODE == 1 ? 2 : 1;
+        const F4 *b = buf + (lane & 15);
+        F4 g[AHEAD + 1][4];
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < AHEAD; ++a) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[a][u] = b[((q + u) & 63) * 16];
+            q += 4;
+        }
+        for (int i = 0; i < n; i += 16 * (AHEAD + 1)) {
+#pragma unroll
+            for (int s = 0; s <= AHEAD; ++s) {
+                const int nx = (s + AHEAD) % (AHEAD + 1);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) g[nx][u] = b[((q + u) & 63) * 16];
+                q += 4;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc = __fadd_rn(acc, g[s][u][v]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    out[lane] = acc;
+    if (lane == 0) cycles[0] = t1 - t0;
+}
+
+template <int MODE>
+static void run(const char *name, const float *seed, float *out, long long *cyc, int n) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(k_chain<MODE>, dim3(1), dim3(64), 0, 0, seed, out, cyc, n);  // warm
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k_chain<MODE>, dim3(1), dim3(64), 0, 0, seed, out, cyc, n);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    long long c = 0;
+    (void)hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("{\"mode\": \"%s\", \"adds\": %d, \"ms\": %.4f, \"ns_per_add\": %.3f, \"memtime_ticks_per_add\": %.3f}\n",
+           name, n, ms, ms * 1e6 / n, (double)c / n);
+}
+
+int main(int argc, char **argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 388128;  // a multiple of 48
+    float *seed, *out;
+    long long *cyc;
+    (void)hipMalloc(&seed, 64 * sizeof(float));
+    (void)hipMalloc(&out, 64 * sizeof(float));
+    (void)hipMalloc(&cyc, sizeof(long long));
+    float h[64];
+    for (int i = 0; i < 64; ++i) h[i] = 0.001f * (i + 1);
+    (void)hipMemcpy(seed, h, sizeof(h), hipMemcpyHostToDevice);
+    run<0>("reg", seed, out, cyc, n);
+    run<1>("lds_ahead2", seed, out, cyc, n);
+    run<2>("lds_ahead1", seed, out, cyc, n);
+    return 0;
+}

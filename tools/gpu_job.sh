@@ -15,6 +15,7 @@
 #                    tools/pmc_traffic.py                   -> gpurun_out/traffic.json
 #   py=SCRIPT,ARGS   python SCRIPT ARGS                      -> gpurun_out/<script>.log
 #   sh=CMD           a preparation command, no GPU (commas as spaces)
+#   bin=TAG,CMD      a GPU program (commas as spaces)        -> gpurun_out/TAG.log
 #   env=NAME=VALUE   export a variable for the following steps
 #   profcmd=TAG,CMD  rocprofv3 --kernel-trace --stats of CMD (commas as spaces; the program
 #                    itself right after --)                  -> gpurun_out/prof_TAG/
@@ -99,6 +100,13 @@ for s in "$@"; do
             -d "$OUT/pmc_${tag}_write" -o run -- ${rest//,/ } > "$OUT/pmc_${tag}_write.log" 2>&1) || exit 1
         python3 tools/pmc_traffic.py "$OUT/pmc_${tag}_fetch" "$OUT/pmc_${tag}_write" "$OUT/traffic_$tag.json" \
             > "$OUT/traffic_$tag.log" 2>&1 ;;
+    bin=*)
+        # bin=TAG,prog,args...: a GPU program (commas = spaces)  -> gpurun_out/TAG.log
+        a="${s#bin=}"
+        tag="${a%%,*}"
+        rest="${a#*,}"
+        step "$tag" 300 ${rest//,/ } > "$OUT/$tag.log" 2>&1 || { tail -20 "$OUT/$tag.log"; exit 1; }
+        tail -5 "$OUT/$tag.log" ;;
     env=*)
         # env=NAME=VALUE: exported for the steps after it
         export "${s#env=}" ;;
