@@ -6,7 +6,7 @@ gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here w
 against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
 only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
 
-    python refgen/build.py            # refgen/bin/gala_gcn and refgen/bin/gala_gat
+    python refgen/build.py            # refgen/bin/gala_{gcn,gat,gin,sage}
 """
 import os
 import subprocess
@@ -23,6 +23,8 @@ BIN = os.path.join(HERE, "bin")
 PROGRAMS = {
     "gcn": ["64", "7", "32", "3", "2"],
     "gat": ["64", "7", "32", "3", "2", "5000"],
+    "gin": ["64", "7", "32", "3", "2"],
+    "sage": ["64", "7", "32", "3", "2"],
 }
 
 
@@ -36,10 +38,19 @@ def compile_driver(exe: str) -> None:
                    timeout=300)
 
 
+# gala_train's training-invariant code motion (tests/gala_train.cpp:136-140) for SAGE: without
+# it the reference generator's first SAGE FFN reads t_iden_n, which only the hoisted mean
+# aggregation defines (common.h:1210-1213)
+CODE_MOTION = {"sage"}
+
+
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
     os.makedirs(out_dir, exist_ok=True)
+    env = dict(os.environ)
+    if model in CODE_MOTION:
+        env["GALA_REFGEN_CODE_MOTION"] = "1"
     subprocess.run([driver, out_dir.rstrip("/") + "/", model, dataset, *args], check=True, capture_output=True,
-                   text=True, timeout=60)
+                   text=True, timeout=60, env=env)
     return os.path.join(out_dir, "gala.cu")
 
 

@@ -1,5 +1,6 @@
 // ir_driver.cpp -- the reference compiler's driver (tests/gala_inference.cpp:100-190) with
-// the HIP code generator (refgen/hip.h), fed a hand-built IR of a GCN or a GAT program.
+// the HIP code generator (refgen/hip.h), fed a hand-built IR of a GCN, GAT, GIN or
+// GraphSAGE program (the four model families of tests/GALA-DSL).
 //
 // The reference's parser is bison/flex (src/frontend/frontend.{y,l}), absent from this image,
 // so the IR a program parses into is built here directly, node for node and edge for edge as
@@ -21,12 +22,13 @@
 //        asks for (generate_ir's transformed graph).
 // frontend.y:471-802 for the ops, 940-1030 for the layer walk, 1031-1108 for the program.
 // Then, as gala_inference does, the middle-end's operator reordering and sparse rewrites run
-// and the generator writes CMakeLists.txt and gala.cu into the output directory.
+// (with GALA_REFGEN_CODE_MOTION set, also gala_train's training-invariant code motion) and the
+// generator writes CMakeLists.txt and gala.cu into the output directory.
 //
 // Compiled against the reference's own headers where they lie (-I <reference>,
 // -I <reference>/src/codegen); nothing of the reference is copied.
 //
-// usage: ir_driver OUT_DIR/ gcn|gat DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]
+// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -250,11 +252,113 @@ void buildGat(const Spec &s) {
     GALAFEContext::program.push_back(loop);
 }
 
+// The program the front-end builds for the GIN layer template of tests/GALA-DSL/gin/*
+//     res_n = aggregate_fn(G.graphs, feats); res = dsl.nn.scalar(1) * feats;
+//     res = res + res_n; res = dsl.nn.ffn(res, out=hs); feats = nonln_fn(res)
+// (MESSAGE_PASSING_AGGREGATE, MULT_SCALAR_FEATS, ADD_SCALAR_AGGR, FEED_FORWARD_NN,
+// NON_LINEARITY: frontend.y:562-589, 803-835, 965-1019).
+void buildGin(const Spec &s) {
+    DataNode *feat = nullptr;
+    DataNode *graph = loadProgram(s, feat);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    DataNode *prev = feat;
+    for (int l = 0; l < s.layers; ++l) {
+        const int in = l == 0 ? s.feat : s.hidden;
+        // MESSAGE_PASSING_AGGREGATE before MULT_SCALAR_FEATS: the output is "res_n"
+        DataNode *aggr = tensorNode("res_n", -1, in);
+        ForwardNode *a = op(loop, AGGREGATE_NODE, AGGREGATE_MUL_SUM_OP, {prev, graph}, aggr);
+        if (s.coarsen) a->addOpt(COARSE_COPT, (float)s.coarsen);
+        depend(prev, ALL_RELATION, aggr, ALL_RELATION);
+        depend(graph, ALL_RELATION, aggr, ALL_RELATION);
+        // MULT_SCALAR_FEATS: (1 + eps) * (the features | the previous layer's ReLU output)
+        DataNode *scaled = tensorNode("res", -1, in);
+        ForwardNode *e = op(loop, POINTWISE, SCALAR_ADD_EPS_MULTIPLY_OP, {prev}, scaled);
+        e->addParam("1");
+        depend(prev, ALL_RELATION, scaled, ALL_RELATION);
+        // ADD_SCALAR_AGGR
+        DataNode *sum = tensorNode("res", -1, in);
+        op(loop, UPDATE_NODE, ADD_OP, {scaled, aggr}, sum);
+        depend(scaled, ALL_RELATION, sum, ALL_RELATION);
+        depend(aggr, ALL_RELATION, sum, ALL_RELATION);
+        associate(scaled, ALL_RELATION, aggr, ALL_RELATION);
+        DataNode *ffn = ffnNode(loop, s, l, sum);
+        prev = s.relu(l) ? reluNode(loop, s.width(l), ffn) : ffn;
+    }
+    GALAFEContext::program.push_back(loop);
+}
+
+// The program the front-end builds for the GraphSAGE-mean layer template of
+// tests/GALA-DSL/sage/*
+//     res_n = aggregate_fn(G.graphs, feats);            (fn = dsl.fn.mul_mean)
+//     res = dsl.nn.ffn(res_n, out=hs) + dsl.nn.ffn(res, out=hs); feats = nonln_fn(res)
+// (the SAGE_OPS statement makes the layer GET_DEGREES, GET_NORMALIZATION (power -1),
+// MESSAGE_PASSING_AGGREGATE, MULT_NORM_RES, ADD_TWO_FFN, NON_LINEARITY: frontend.y:161-168,
+// 471-561, 836-928, 949-1022).
+void buildSage(const Spec &s) {
+    DataNode *feat = nullptr;
+    DataNode *graph = loadProgram(s, feat);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    DataNode *norm = nullptr, *prev = feat;
+    for (int l = 0; l < s.layers; ++l) {
+        const int in = l == 0 ? s.feat : s.hidden;
+        if (l == 0) {  // GET_DEGREES, GET_NORMALIZATION (the mean: deg ^ -1)
+            DataNode *ones = tensorNode("ones", -1, 1);
+            op(loop, POINTWISE, ONES_OP, {}, ones);
+            associate(graph, ALL_RELATION, ones, ROWS_RELATION);
+            DataNode *deg = tensorNode("degrees", -1, 1);
+            ForwardNode *d = op(loop, AGGREGATE_NODE, AGGREGATE_MUL_SUM_DIRECT, {ones, graph}, deg);
+            if (s.coarsen) d->addOpt(COARSE_COPT, (float)s.coarsen);
+            depend(ones, ALL_RELATION, deg, ALL_RELATION);
+            depend(graph, ALL_RELATION, deg, ROWS_RELATION);
+            norm = tensorNode("norm", -1, 1);
+            ForwardNode *p = op(loop, POINTWISE, POWER_OP, {deg}, norm);
+            p->addParam(std::to_string(-1.0f));
+            depend(deg, ALL_RELATION, norm, ALL_RELATION);
+        }
+        // MESSAGE_PASSING_AGGREGATE before MULT_NORM_RES: "res_n"
+        DataNode *aggr = tensorNode("res_n", -1, in);
+        ForwardNode *a = op(loop, AGGREGATE_NODE, AGGREGATE_MUL_SUM_OP, {prev, graph}, aggr);
+        if (s.coarsen) a->addOpt(COARSE_COPT, (float)s.coarsen);
+        depend(prev, ALL_RELATION, aggr, ALL_RELATION);
+        depend(graph, ALL_RELATION, aggr, ALL_RELATION);
+        // MULT_NORM_RES after the aggregation: res_n = norm * res_n
+        DataNode *mean = tensorNode("res_n", -1, s.hidden);
+        op(loop, UPDATE_NODE, ROW_BROADCAST_OP, {norm, aggr}, mean);
+        depend(norm, ALL_RELATION, mean, ROWS_RELATION);
+        depend(aggr, ALL_RELATION, mean, ALL_RELATION);
+        associate(norm, ALL_RELATION, aggr, ROWS_RELATION);
+        // ADD_TWO_FFN: res_n = W1(res_n) (FFN_OP), res = W2(res) (FFN_OP_SELF), res = res_n + res
+        auto weight = [&](const char *name) {
+            auto *info = new DataInfo(CM_DTYPE);
+            info->setDims(in, s.width(l));
+            return new DataNode(name, INT32, INT32, F32, new DataLevel(info, true));
+        };
+        DataNode *w1 = weight("weight1"), *w2 = weight("weight2");
+        DataNode *nbr = tensorNode("res_n", -1, s.width(l));
+        op(loop, UPDATE_NODE, FFN_OP, {mean, w1}, nbr);
+        depend(mean, ALL_RELATION, nbr, ALL_RELATION);
+        depend(w1, COLS_RELATION, nbr, ROWS_RELATION);
+        associate(mean, ROWS_RELATION, w1, COLS_RELATION);
+        DataNode *self = tensorNode("res", -1, s.width(l));
+        op(loop, UPDATE_NODE, FFN_OP_SELF, {mean, w2}, self);
+        depend(feat, ALL_RELATION, self, ALL_RELATION);
+        depend(w2, COLS_RELATION, self, ROWS_RELATION);
+        associate(mean, ROWS_RELATION, w2, COLS_RELATION);
+        DataNode *sum = tensorNode("res", -1, s.width(l));
+        op(loop, UPDATE_NODE, ADD_OP, {nbr, self}, sum);
+        depend(nbr, ALL_RELATION, sum, ALL_RELATION);
+        depend(self, ALL_RELATION, sum, ALL_RELATION);
+        associate(nbr, ALL_RELATION, self, ALL_RELATION);
+        prev = s.relu(l) ? reluNode(loop, s.width(l), sum) : sum;
+    }
+    GALAFEContext::program.push_back(loop);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
     if (argc < 8) {
-        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]\n";
+        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]\n";
         return 2;
     }
     std::string out = argv[1];
@@ -267,6 +371,7 @@ int main(int argc, char **argv) {
     s.iterations = std::atoi(argv[7]);
     s.coarsen = argc > 8 ? std::atoi(argv[8]) : 0;
     s.col_tile = argc > 9 ? std::atoi(argv[9]) : 0;
+    const bool motion = std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
     if (s.model == "gcn") {
         buildGcn(s);
     } else if (s.model == "gat") {
@@ -275,6 +380,10 @@ int main(int argc, char **argv) {
             return 2;
         }
         buildGat(s);
+    } else if (s.model == "gin") {
+        buildGin(s);
+    } else if (s.model == "sage") {
+        buildSage(s);
     } else {
         std::cerr << "unknown model " << s.model << "\n";
         return 2;
@@ -287,6 +396,9 @@ int main(int argc, char **argv) {
     if (GALAFEContext::sparse_rewrites)
         GALATransformations::sparsityAwareRewrites(GALAFEContext::program, GALAFEContext::dependencies,
                                                    GALAFEContext::associations, GALAFEContext::transforms);
+    if (motion)  // gala_train's third pass (tests/gala_train.cpp:136-140)
+        GALATransformations::trainingInvariantCodeMotion(GALAFEContext::program, GALAFEContext::dependencies,
+                                                         GALAFEContext::associations, GALAFEContext::transforms);
     gen.writeCode(GALAFEContext::program, GALAFEContext::dependencies, GALAFEContext::associations,
                   GALAFEContext::transforms);
     std::cout << "wrote " << out << "gala.cu and " << out << "CMakeLists.txt" << std::endl;

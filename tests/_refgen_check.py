@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
 GALAC = os.path.join(PKG, "gala", "galac")
-DSL = {"gcn": "gcn_ref_codegen.txt", "gat": "gat_ref_codegen.txt"}
+DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gat", "gin", "sage")}
 
 
 def read_dump(path):
@@ -76,6 +76,10 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     want_params = {"prediction", "loss", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
     if model == "gat":
         want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
+    elif model == "gin":
+        want_params |= {"eps0", "eps1"}
+    elif model == "sage":
+        want_params |= {f"sfc{i}.{k}" for i in range(2) for k in ("weight", "bias")}
     assert set(dump) >= want_params, sorted(dump)
     r = subprocess.run([GALAC, os.path.join(HERE, "dsl", DSL[model]), "--quiet", "--ir-json", str(ir_path)],
                        capture_output=True, text=True, timeout=60)
@@ -84,8 +88,12 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     ops = [nd["op"] for nd in ir["nodes"]]
     if model == "gcn":
         assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same operator reordering
-    else:
+    elif model == "gat":
         assert ops.count("GAT_AGGREGATE") == 2
+    elif model == "gin":
+        assert ops.count("SCALAR_ADD_EPS_MULTIPLY") == 2 and ops.index("FFN") < ops.index("GCN_AGGREGATE")
+    else:
+        assert [w["name"] for w in ir["weights"]] == ["fc0", "sfc0", "fc1", "sfc1"]
     g = layout.load_npy_dataset(d)
     graphs = ref.Graphs(ir, g.rowptr, g.col, np.ones(g.n_rows, np.int32))
     params = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in dump.items()

@@ -4,18 +4,17 @@ end to end on the host, where the reference's sources are:
 1. refgen/ir_driver.cpp -- the reference driver's steps (tests/gala_inference.cpp) with
    HIPGenerator in place of CUDAGenerator -- is compiled against the reference's own headers
    (src/codegen/common.h, src/ir, src/frontend/context.h, src/middle-end) and run on a
-   hand-built two-layer IR (the front-end's nodes and edges for the GCN layer template, or
-   for the GAT one of tests/GALA-DSL/gat over the column-tiled graph; bison is absent, so
-   the parser cannot run);
+   hand-built two-layer IR (the front-end's nodes and edges for the layer templates of the
+   four families of tests/GALA-DSL: GCN, GAT over the column-tiled graph, GIN, GraphSAGE;
+   bison is absent, so the parser cannot run);
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
    over `<kernel>_call` functions that forward to the operator mirror -- is compiled against
    the reference's host headers (formats, tiling, npy reader) and libgala_torch.so, with no
    CUDA name left in it (refgen/build.py's recipe);
 3. it runs on the host backend (GALA_DEVICE=cpu) over an npy dataset in the reference's
    format, and its first-epoch prediction, loss and weight gradients equal, within 1e-4,
-   galac's program of the same DSL (tests/dsl/{gcn,gat}_ref_codegen.txt, the same schedule:
-   operator reordering, no code motion) evaluated by the float64 IR executor on the weights
-   the program dumped.  For GAT that runs the base generator's own autograd classes (edge
+   galac's program of the same DSL (tests/dsl/<model>_ref_codegen.txt, the same passes)
+   evaluated by the float64 IR executor on the weights the program dumped.  For GAT that runs the base generator's own autograd classes (edge
    sum, softmax, the attention-weighted aggregation, common.h:622-894) over the mirror's
    edge operators.
 tests/test_gpu_refgen.py runs the programs refgen/build.py builds on the MI355X.
@@ -38,6 +37,8 @@ pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the referen
 CASES = {
     "gcn": ["64", "7", "32", "3", "2"],
     "gat": ["64", "7", "32", "3", "2", "200"],
+    "gin": ["64", "7", "32", "3", "2"],
+    "sage": ["64", "7", "32", "3", "2"],
 }
 
 
@@ -60,9 +61,13 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
         assert cuda_name not in src, cuda_name
     assert "gala::aggregate_node_mul_sum_call" in src and "aggregate_node_mul_sum_coarse2_AutoGrad" in src
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
-    if model == "gcn":
+    if model in ("gcn", "gin"):
         # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
         assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
+    elif model == "sage":
+        # code motion ran: the first layer's mean aggregation is hoisted out of the training loop
+        assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
+        assert fwd.index("fc0->forward(t_iden_n)") < fwd.index("sfc0->forward")
     else:
         # the edge chain of each layer: attention Linears, edge sum, LeakyReLU, softmax, aggregation
         for a, b in (("efc0->forward", "aggregate_edge_sum_AutoGrad::apply"),
