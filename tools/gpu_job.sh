@@ -48,12 +48,12 @@ step() {  # name, limit, command...
 for s in "$@"; do
     case "$s" in
     tests)
-        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread \
+        step tests 900 python -u -m pytest tests -m gpu -q -rs -x --timeout 120 --timeout-method thread \
             > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
         tail -3 "$OUT/pytest_gpu.log" ;;
     tests=*)
         k="${s#tests=}"
-        step tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -k "${k//_or_/ or }" \
+        step tests 900 python -u -m pytest tests -m gpu -q -rs -x --timeout 120 --timeout-method thread -k "${k//_or_/ or }" \
             > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
         tail -3 "$OUT/pytest_gpu.log" ;;
     smoke)
