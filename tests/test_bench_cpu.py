@@ -64,6 +64,23 @@ def test_bench_self_launches_ranks():
     assert bd["comm"]["halo_bytes_per_aggregation_per_rank"] < c["halo_bytes_per_aggregation_per_rank"]
 
 
+def test_bench_eight_ranks():
+    """The driver's N = 8 launch shape (8 self-launched ranks, here gloo on the host): one line
+    with n_gpus 8, every family and field present, every partition of the 8-way split built."""
+    env = _env()
+    env["OMP_NUM_THREADS"] = "1"
+    r = _run_ranks(["--gpus", "8", "--device", "cpu", "--scale", "0.002", "--steps", "2", "--warmup", "1",
+                    "--calib-steps", "1"], env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 8 and d["value"] > 0 and d["config"]["parallelism"].endswith("x8 (gloo)")
+    assert all(k in d and d[k]["value"] > 0 for k in ("gat", "rmat", "banded", "weak"))
+    assert not d["budget"]["skipped_for_time"] and set(d["budget"]["phase_s"]) == {"uniform", "gat", "rmat",
+                                                                                     "banded", "weak"}
+
+
 def test_bench_budget_keeps_the_headline():
     """--budget-s far below what the run needs: the N = 2 line still carries the headline
     (its first candidate timed, the others and every secondary field skipped, agreed over
