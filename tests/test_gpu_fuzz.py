@@ -5,7 +5,8 @@ R-MAT graph, a block of empty rows, a hub row longer than the split threshold), 
 a head count, row padding, edge weights, a hub-row split plan with small chunks and column
 tiling, then checks the HIP path against the oracle:
 
-* bit-exact: degree, SpMM without hub chunks, row-scale / row-broadcast;
+* bit-exact: degree, SpMM without hub chunks, the SpMM's GCN epilogue (deg norm from the
+  rowptr, the next input beside the output), row-scale / row-broadcast;
 * reordered sums (hub chunks, the GALA_SPMM_HUB_CHUNKED fast mode; the default REF order
   is bit-exact): within the worst-case fp32 summation bound of the row,
   |err| <= (deg + 1) 2^-24 sum|a x| + 1e-6 per entry;
@@ -101,6 +102,16 @@ def test_random_case(seed):
         np.testing.assert_array_equal(_host(ops.spmm(gd, Xd)), orc.spmm(og if w is None else to_oracle(g, w), X))
         if chunked:   # the fast mode: hub rows as chunk partials
             _reordered_ok(_host(ops.spmm(gd, Xd, hub="chunked")), g, X, w)
+    # the GCN epilogue (gala_spmm_ex_f32): the dst norm deg^-0.5 formed from the rowptr, the next
+    # aggregation's input Y2 = fl(norm * Y) beside Y -- the degree pass + ROW_BROADCAST chain
+    # of the oracle bit for bit (an empty row: inf norm, NaN row on both sides)
+    norm = orc.degree(og, power=-0.5)
+    want = orc.spmm(og, X, dst_scale=norm)
+    Y1 = torch.empty((g.n_rows, F), device="cuda")
+    Y2 = torch.empty((g.n_rows, F), device="cuda")
+    ops.spmm(dg, Xd, out=Y1, dst_deg=True, out2=Y2)
+    np.testing.assert_array_equal(_host(Y1), want)
+    np.testing.assert_array_equal(_host(Y2), (norm[:, None] * want).astype(np.float32))
     # column-tiled layout (no split plan): segments summed in order, bit-exact
     if g.n_cols > 1 and not chunked:
         tg = layout.col_tile(g, int(rng.integers(1, g.n_cols)))
