@@ -12,6 +12,8 @@ line per run:
                  (HaloGat layers)
   sage_reddit_sampled  config 4 (kernel-sampled SAGE on the Reddit shape): the generated
                  binary, then gala.dist_run on the row partition, alone and over RCCL
+  gcn3_papers10  gala.dist_run on 4 ranks of this one GPU over gloo (halo, vertex cut sparse):
+                 the 4-way partitions and exchanges at the full shape
 Epoch times are the programs' own means (first epochs dropped, as gala.cu:613-637).
 """
 import json
@@ -26,17 +28,34 @@ GALAC = os.path.join(PKG, "gala", "galac")
 
 
 def run(tag, cmd, env, limit=600):
+    """One run as a child process; a heartbeat line every 60 s while it runs (a long
+    host-staged multi-rank run would otherwise print nothing for minutes)."""
+    import tempfile
     t0 = time.time()
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=limit, env=env, cwd=ROOT)
-    rec = {"run": tag, "rc": r.returncode, "wall_s": time.time() - t0}
-    js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    with tempfile.TemporaryFile("w+") as out, tempfile.TemporaryFile("w+") as err:
+        p = subprocess.Popen(cmd, stdout=out, stderr=err, text=True, env=env, cwd=ROOT)
+        while True:
+            try:
+                p.wait(timeout=60)
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() - t0 > limit:
+                    p.kill()
+                    p.wait()
+                    break
+                print(f"[config5_run] {tag}: running, {time.time() - t0:.0f} s", flush=True)
+        out.seek(0)
+        err.seek(0)
+        stdout, stderr = out.read(), err.read()
+    rec = {"run": tag, "rc": p.returncode, "wall_s": time.time() - t0}
+    js = [ln for ln in stdout.splitlines() if ln.startswith("{")]
     if js:
         rec["summary"] = json.loads(js[-1])
-    rec["result_line"] = (r.stdout.strip().splitlines() or [""])[-1]
-    if r.returncode != 0:
-        rec["stderr"] = r.stderr[-2000:]
+    rec["result_line"] = (stdout.strip().splitlines() or [""])[-1]
+    if p.returncode != 0:
+        rec["stderr"] = stderr[-2000:]
     print(json.dumps(rec), flush=True)
-    return r.returncode
+    return p.returncode
 
 
 def main():
@@ -73,10 +92,22 @@ def main():
         ("sage_reddit_sampled dist_run halo RCCL world1",
          dr + [irs["sage_reddit_sampled"], "--synthetic", "--iters", iters, "--dist"]),
     ]
+    # config 5's program split over 4 ranks on this one GPU (gloo: host-staged collectives, the
+    # layouts' partitions and exchanges at the full 11.1 M-row shape)
+    tr = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4", "--master-addr",
+          "127.0.0.1", "--master-port=29533", "-m", "gala.dist_run"]
+    steps += [
+        ("gcn3_papers10 dist_run halo gloo world4", tr + [irs["gcn3_papers10"], "--synthetic", "--iters", iters,
+                                                          "--dist"]),
+        ("gcn3_papers10 dist_run vcut sparse gloo world4",
+         tr + [irs["gcn3_papers10"], "--synthetic", "--iters", iters, "--layout", "vcut", "--dist",
+               "--exchange", "sparse"]),
+    ]
     only = sys.argv[2:]
-    steps = [s for s in steps if not only or any(s[0].startswith(o) for o in only)]
+    steps = [s for s in steps if not only or any(o in s[0] for o in only)]
     for tag, cmd in steps:
-        if run(tag, cmd, env) != 0:
+        e = dict(env, GALA_DIST_BACKEND="gloo") if "gloo" in tag else env
+        if run(tag, cmd, e, limit=900 if "gloo" in tag else 600) != 0:
             return 1
     return 0
 
