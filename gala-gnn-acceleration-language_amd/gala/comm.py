@@ -35,8 +35,43 @@ class _Works:
             w.wait()
 
 
+def a2a_rounds(in_splits, out_splits, world: int, row_bytes: int, max_rows=None):
+    """The rounds of an all-to-all cut at MAX_MSG_BYTES: a list of (ins, outs), ins[q] the
+    (start, stop) rows of the input sent to rank q in that round, outs[q] the rows of the output
+    received from rank q.  Round j carries rows [j*r, (j+1)*r) of every block, r =
+    MAX_MSG_BYTES // (world * row_bytes), so one round's message is at most MAX_MSG_BYTES; the
+    round count comes from max_rows, a bound on every rank's blocks that all ranks pass alike
+    (they must issue the same collectives), or from this rank's largest block.  One round when
+    nothing needs cutting."""
+    in_splits, out_splits = [int(v) for v in in_splits], [int(v) for v in out_splits]
+    r = max(MAX_MSG_BYTES // (world * row_bytes), 1)
+    m = max(in_splits + out_splits + [0]) if max_rows is None else int(max_rows)
+    rounds = max(-(-m // r), 1)
+    io, oo = [0] * world, [0] * world
+    for q in range(1, world):
+        io[q] = io[q - 1] + in_splits[q - 1]
+        oo[q] = oo[q - 1] + out_splits[q - 1]
+    out = []
+    for j in range(rounds):
+        ins = [(io[q] + min(j * r, in_splits[q]), io[q] + min((j + 1) * r, in_splits[q])) for q in range(world)]
+        outs = [(oo[q] + min(j * r, out_splits[q]), oo[q] + min((j + 1) * r, out_splits[q])) for q in range(world)]
+        out.append((ins, outs))
+    return out
+
+
+def p2p_pieces(rows: int, row_bytes: int):
+    """The (start, stop) row pieces of a point-to-point message cut at MAX_MSG_BYTES (both
+    ends cut a message of the same shape alike)."""
+    r = max(MAX_MSG_BYTES // row_bytes, 1)
+    return [(0, rows)] if rows <= r else [(i, min(i + r, rows)) for i in range(0, rows, r)]
+
+
 def _row_bytes(t: torch.Tensor) -> int:
-    return max(t[0].numel() if t.dim() > 1 else 1, 1) * t.element_size()
+    """Bytes of one row (dim 0) of t, also for a tensor with no rows."""
+    n = 1
+    for d in t.shape[1:]:
+        n *= int(d)
+    return max(n, 1) * t.element_size()
 
 
 class Comm:
@@ -105,26 +140,13 @@ class Comm:
         number of rounds when the exchange is cut at MAX_MSG_BYTES); default: this rank's
         largest block, which is only safe when no rank's exchange needs cutting."""
         if self.rccl:
-            in_splits, out_splits = [int(v) for v in in_splits], [int(v) for v in out_splits]
-            rb = _row_bytes(inp if inp.numel() else out)
-            r = max(MAX_MSG_BYTES // (self.world * rb), 1)
-            m = max(in_splits + out_splits + [0]) if max_rows is None else int(max_rows)
-            rounds = -(-m // r)
-            if rounds <= 1:
-                return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
-                                              input_split_sizes=in_splits, group=self.group, async_op=True)
-            io = [0] * self.world
-            oo = [0] * self.world
-            for q in range(1, self.world):
-                io[q] = io[q - 1] + in_splits[q - 1]
-                oo[q] = oo[q - 1] + out_splits[q - 1]
-            works = []
-            for j in range(rounds):
-                ins = [inp[io[q] + min(j * r, in_splits[q]):io[q] + min((j + 1) * r, in_splits[q])]
-                       for q in range(self.world)]
-                outs = [out[oo[q] + min(j * r, out_splits[q]):oo[q] + min((j + 1) * r, out_splits[q])]
-                        for q in range(self.world)]
-                works.append(dist.all_to_all(outs, ins, group=self.group, async_op=True))
+            rounds = a2a_rounds(in_splits, out_splits, self.world, _row_bytes(inp), max_rows)
+            if len(rounds) == 1:
+                return dist.all_to_all_single(out, inp, output_split_sizes=[int(v) for v in out_splits],
+                                              input_split_sizes=[int(v) for v in in_splits], group=self.group,
+                                              async_op=True)
+            works = [dist.all_to_all([out[a:b] for a, b in outs], [inp[a:b] for a, b in ins], group=self.group,
+                                     async_op=True) for ins, outs in rounds]
             return _Works(works)
         ho = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(ho, self._host(inp), output_split_sizes=list(out_splits),
@@ -137,8 +159,7 @@ class Comm:
         if self.rccl:
             # messages past MAX_MSG_BYTES go as row pieces, in order (both ends cut alike)
             def pieces(t):
-                r = max(MAX_MSG_BYTES // _row_bytes(t), 1)
-                return [t] if t.shape[0] <= r else [t[i:i + r] for i in range(0, t.shape[0], r)]
+                return [t[a:b] for a, b in p2p_pieces(t.shape[0], _row_bytes(t))]
             ops = [dist.P2POp(dist.isend, p, q, self.group) for t, q in sends for p in pieces(t)]
             ops += [dist.P2POp(dist.irecv, p, q, self.group) for t, q in recvs for p in pieces(t)]
             return dist.batch_isend_irecv(ops) if ops else []
