@@ -15,13 +15,14 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-# RCCL 2.26.6 (the torch 2.10 ROCm wheel's librccl) returns wrong rows from an
-# all_to_all_single whose payload exceeds 2 GiB: from about 1 GiB on, half the rows are
-# wrong (tools/a2a_probe.py on MI355X, profiles/r04_rccl_a2a_probe.jsonl; reduce_scatter is
-# exact at the same sizes).  That was the round-3 divergence of the sparse vertex-cut
-# exchange at config 5's 11.1 M-row shape (5.7 GB per all-to-all).  Every all-to-all and
-# point-to-point message is therefore cut into rounds of at most MAX_MSG_BYTES in all.
-MAX_MSG_BYTES = 1 << 30
+# RCCL 2.26.6 (the torch 2.10 ROCm wheel's librccl) returns wrong rows from all_to_all_single
+# and from batched point-to-point once the payload passes 1 GiB: at 2^30 + 512 B (and at 2, 5.7
+# GiB) every row past the first half is wrong (tools/a2a_probe.py on MI355X,
+# profiles/r04_rccl_a2a_probe.jsonl; 568 MB is exact, and reduce_scatter / all_gather are exact
+# at every size).  That was the round-3 divergence of the sparse vertex-cut exchange at config
+# 5's 11.1 M-row shape (5.7 GB per all-to-all).  Every all-to-all and point-to-point message is
+# therefore cut into rounds of at most MAX_MSG_BYTES (512 MiB: half the smallest failing size).
+MAX_MSG_BYTES = 1 << 29
 
 
 class _Works:

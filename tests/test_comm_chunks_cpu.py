@@ -1,5 +1,5 @@
 """CPU: gala.comm's message cutting.  RCCL 2.26.6 corrupts all-to-all and point-to-point
-payloads past 2 GiB (profiles/r04_rccl_a2a_probe.jsonl), so every RCCL all-to-all is cut
+payloads past 1 GiB (profiles/r04_rccl_a2a_probe.jsonl), so every RCCL all-to-all is cut
 into rounds and every p2p message into row pieces of at most MAX_MSG_BYTES.
 
 The cutting plans (gala.comm.a2a_rounds / p2p_pieces, what Comm.all_to_all and Comm.exchange
