@@ -133,6 +133,7 @@ extern "C" int gala_host_col_tile(int64_t n_rows, const int32_t *rowptr, const i
         for (int64_t r = 0; r < n_rows; ++r) {
             const int64_t o = seg_start + orp[r];
             const int64_t n = hi[r] - lo[r];
+            if (n == 0) continue;  // (an empty graph may pass NULL col / val)
             memcpy(out_col + o, col + lo[r], n * sizeof(int32_t));
             if (val) memcpy(out_val + o, val + lo[r], n * sizeof(float));
         }
