@@ -6,7 +6,7 @@ gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here w
 against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
 only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
 
-    python refgen/build.py            # refgen/bin/gala_{gcn,gat,gin,sage}
+    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gat,gin,sage}
 """
 import os
 import subprocess
@@ -22,6 +22,8 @@ BIN = os.path.join(HERE, "bin")
 # (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]); the GAT one over 4 column tiles of 20 000 rows
 PROGRAMS = {
     "gcn": ["64", "7", "32", "3", "2"],
+    # the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel: sample(5), one tile
+    "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     "gat": ["64", "7", "32", "3", "2", "5000"],
     "gin": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
@@ -45,11 +47,13 @@ CODE_MOTION = {"sage"}
 
 
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
+    """Emit the program of `model` (a program name: gcn, gcn_ksample, gat, gin, sage)."""
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ)
     if model in CODE_MOTION:
         env["GALA_REFGEN_CODE_MOTION"] = "1"
-    subprocess.run([driver, out_dir.rstrip("/") + "/", model, dataset, *args], check=True, capture_output=True,
+    family = model.split("_")[0]          # the driver's layer template
+    subprocess.run([driver, out_dir.rstrip("/") + "/", family, dataset, *args], check=True, capture_output=True,
                    text=True, timeout=60, env=env)
     return os.path.join(out_dir, "gala.cu")
 

@@ -28,7 +28,9 @@
 // Compiled against the reference's own headers where they lie (-I <reference>,
 // -I <reference>/src/codegen); nothing of the reference is copied.
 //
-// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]
+// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE [NSAMP]]]
+// (NSAMP: GCN with aggrFn.sample(NSAMP), the kernel-sampled GCN of
+// tests/GALA-DSL/ablations/sampling/kernel)
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -55,6 +57,8 @@ namespace {
 struct Spec {
     std::string model, dataset;
     int feat = 0, labels = 0, hidden = 0, iterations = 1, coarsen = 0, col_tile = 0;
+    int nsamp = 0;        // aggrFn.sample(n): kernel sampling (compute transformation SAMP_CPT)
+    bool sparse = false;  // G.is_sparser(true)
     float power = -0.5f;
     int layers = 2;
     bool relu(int l) const { return l + 1 < layers; }  // nonln_fn on every layer but the output
@@ -103,9 +107,9 @@ DataNode *loadProgram(const Spec &s, DataNode *&feat) {
         ginfo->setIndex(0);
         return graph;
     }
-    // undirected, unweighted, is_sparser(true) (the tests/GALA-DSL/gat schedule)
+    // undirected, unweighted, the schedule's is_sparser
     auto *tinfo = new DataInfo(CSR_STYPE, false, false);
-    tinfo->setSparse(true);
+    tinfo->setSparse(s.sparse);
     tinfo->addOpt(COL_TILE_DOPT, std::to_string(s.col_tile));
     auto *tile = new DataNode("graph_tile", graph->getIType(), graph->getNType(), graph->getVType(),
                               new DataLevel(new DataLevel(tinfo, false), true));
@@ -145,7 +149,16 @@ void buildGcn(const Spec &s) {
     auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
     DataNode *norm = nullptr, *prev = feat;
     for (int l = 0; l < s.layers; ++l) {
-        if (l == 0) {  // GET_DEGREES: ones, then the direct (no-autograd) aggregation of them
+        if (l == 0 && s.nsamp) {  // GET_DEGREES of a kernel-sampled program: nsamp per row
+            DataNode *deg = tensorNode("degrees", -1, 1);
+            ForwardNode *d = op(loop, UPDATE_NODE, FULL_OP, {graph}, deg);
+            d->addParam(std::to_string((float)s.nsamp));
+            depend(graph, ALL_RELATION, deg, ROWS_RELATION);
+            norm = tensorNode("norm", -1, 1);
+            ForwardNode *p = op(loop, POINTWISE, POWER_OP, {deg}, norm);
+            p->addParam(std::to_string(s.power));
+            depend(deg, ALL_RELATION, norm, ALL_RELATION);
+        } else if (l == 0) {  // GET_DEGREES: ones, then the direct (no-autograd) aggregation of them
             DataNode *ones = tensorNode("ones", -1, 1);
             op(loop, POINTWISE, ONES_OP, {}, ones);
             associate(graph, ALL_RELATION, ones, ROWS_RELATION);
@@ -170,6 +183,7 @@ void buildGcn(const Spec &s) {
         DataNode *aggr = tensorNode("res", -1, l == 0 ? s.feat : s.hidden);
         ForwardNode *a = op(loop, AGGREGATE_NODE, AGGREGATE_MUL_SUM_OP, {scaled, graph}, aggr);
         if (s.coarsen) a->addOpt(COARSE_COPT, (float)s.coarsen);
+        if (s.nsamp) a->addOpt(SAMPLE_COPT, (float)s.nsamp);
         depend(scaled, ALL_RELATION, aggr, ALL_RELATION);
         depend(graph, ALL_RELATION, aggr, ALL_RELATION);
         // FEED_FORWARD_NN
@@ -358,7 +372,7 @@ void buildSage(const Spec &s) {
 
 int main(int argc, char **argv) {
     if (argc < 8) {
-        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE]]\n";
+        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE [NSAMP]]]\n";
         return 2;
     }
     std::string out = argv[1];
@@ -371,6 +385,8 @@ int main(int argc, char **argv) {
     s.iterations = std::atoi(argv[7]);
     s.coarsen = argc > 8 ? std::atoi(argv[8]) : 0;
     s.col_tile = argc > 9 ? std::atoi(argv[9]) : 0;
+    s.nsamp = argc > 10 ? std::atoi(argv[10]) : 0;
+    s.sparse = s.model == "gat";  // the tests/GALA-DSL/gat schedule's is_sparser(true)
     const bool motion = std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
     if (s.model == "gcn") {
         buildGcn(s);

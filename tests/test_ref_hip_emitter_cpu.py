@@ -5,8 +5,9 @@ end to end on the host, where the reference's sources are:
    HIPGenerator in place of CUDAGenerator -- is compiled against the reference's own headers
    (src/codegen/common.h, src/ir, src/frontend/context.h, src/middle-end) and run on a
    hand-built two-layer IR (the front-end's nodes and edges for the layer templates of the
-   four families of tests/GALA-DSL: GCN, GAT over the column-tiled graph, GIN, GraphSAGE;
-   bison is absent, so the parser cannot run);
+   four families of tests/GALA-DSL: GCN (also kernel-sampled, as in
+   tests/GALA-DSL/ablations/sampling/kernel), GAT over the column-tiled graph, GIN,
+   GraphSAGE; bison is absent, so the parser cannot run);
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
    over `<kernel>_call` functions that forward to the operator mirror -- is compiled against
    the reference's host headers (formats, tiling, npy reader) and libgala_torch.so, with no
@@ -36,6 +37,7 @@ pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the referen
 # the GAT graph of 600 rows in 3 column tiles
 CASES = {
     "gcn": ["64", "7", "32", "3", "2"],
+    "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     "gat": ["64", "7", "32", "3", "2", "200"],
     "gin": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
@@ -61,9 +63,14 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
         assert cuda_name not in src, cuda_name
     assert "gala::aggregate_node_mul_sum_call" in src and "aggregate_node_mul_sum_coarse2_AutoGrad" in src
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
-    if model in ("gcn", "gin"):
+    if model in ("gcn", "gcn_ksample", "gin"):
         # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
         assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
+        if model == "gcn_ksample":
+            # kernel sampling: the degree is nsamp per segment, the aggregation visits the
+            # (ra*j + rb) mod deg edges with the reference's fixed (5, 7) (common.h:813-821,1342-1360)
+            assert "5.000000 * global_segments[0]" in src and "global_ra = 5;" in src
+            assert "segments, false, 5, global_ra, global_rb" in src
     elif model == "sage":
         # code motion ran: the first layer's mean aggregation is hoisted out of the training loop
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
