@@ -6,7 +6,7 @@ gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here w
 against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
 only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
 
-    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gat,gin,sage}
+    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gcn_dsample,gat,gin,sage}
 """
 import os
 import subprocess
@@ -24,6 +24,8 @@ PROGRAMS = {
     "gcn": ["64", "7", "32", "3", "2"],
     # the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel: sample(5), one tile
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
+    # the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data: G.sample(3), one tile
+    "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "5000"],
     "gin": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
@@ -47,7 +49,7 @@ CODE_MOTION = {"sage"}
 
 
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
-    """Emit the program of `model` (a program name: gcn, gcn_ksample, gat, gin, sage)."""
+    """Emit the program of `model` (a program name: gcn, gcn_ksample, gcn_dsample, gat, gin, sage)."""
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ)
     if model in CODE_MOTION:

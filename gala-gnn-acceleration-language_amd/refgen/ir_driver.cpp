@@ -28,9 +28,10 @@
 // Compiled against the reference's own headers where they lie (-I <reference>,
 // -I <reference>/src/codegen); nothing of the reference is copied.
 //
-// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE [NSAMP]]]
-// (NSAMP: GCN with aggrFn.sample(NSAMP), the kernel-sampled GCN of
-// tests/GALA-DSL/ablations/sampling/kernel)
+// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS
+//                  [COARSEN [COL_TILE [NSAMP [DATA_SAMPLE]]]]
+// (NSAMP: aggrFn.sample(NSAMP), the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel;
+// DATA_SAMPLE: G.sample(n), the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data)
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -58,6 +59,7 @@ struct Spec {
     std::string model, dataset;
     int feat = 0, labels = 0, hidden = 0, iterations = 1, coarsen = 0, col_tile = 0;
     int nsamp = 0;        // aggrFn.sample(n): kernel sampling (compute transformation SAMP_CPT)
+    int data_samp = 0;    // G.sample(n): data sampling (graph transformation SAMP, SAMPLE_DOPT)
     bool sparse = false;  // G.is_sparser(true)
     float power = -0.5f;
     int layers = 2;
@@ -110,11 +112,17 @@ DataNode *loadProgram(const Spec &s, DataNode *&feat) {
     // undirected, unweighted, the schedule's is_sparser
     auto *tinfo = new DataInfo(CSR_STYPE, false, false);
     tinfo->setSparse(s.sparse);
+    if (s.data_samp) tinfo->addOpt(SAMPLE_DOPT, std::to_string(s.data_samp));
     tinfo->addOpt(COL_TILE_DOPT, std::to_string(s.col_tile));
     auto *tile = new DataNode("graph_tile", graph->getIType(), graph->getNType(), graph->getVType(),
                               new DataLevel(new DataLevel(tinfo, false), true));
     associate(tile, ALL_RELATION, feat, ROWS_RELATION);
     auto *edge = new TransformEdge(graph, tile);
+    if (s.data_samp) {  // the sampled rows first, then the column tiles of them
+        auto *samp = new TransformData(SAMPLE_DOPT);
+        samp->addParam(std::to_string(s.data_samp));
+        edge->addTransformation(samp);
+    }
     auto *tr = new TransformData(COL_TILE_DOPT);
     tr->addParam(std::to_string(s.col_tile));
     edge->addTransformation(tr);
@@ -372,7 +380,8 @@ void buildSage(const Spec &s) {
 
 int main(int argc, char **argv) {
     if (argc < 8) {
-        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS [COARSEN [COL_TILE [NSAMP]]]\n";
+        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS "
+                     "[COARSEN [COL_TILE [NSAMP [DATA_SAMPLE]]]]\n";
         return 2;
     }
     std::string out = argv[1];
@@ -386,6 +395,11 @@ int main(int argc, char **argv) {
     s.coarsen = argc > 8 ? std::atoi(argv[8]) : 0;
     s.col_tile = argc > 9 ? std::atoi(argv[9]) : 0;
     s.nsamp = argc > 10 ? std::atoi(argv[10]) : 0;
+    s.data_samp = argc > 11 ? std::atoi(argv[11]) : 0;
+    if (s.data_samp && !s.col_tile) {  // generate_ir makes the transformed graph only with a data transformation
+        std::cerr << "data sampling needs COL_TILE (the reference's transformed graph)\n";
+        return 2;
+    }
     s.sparse = s.model == "gat";  // the tests/GALA-DSL/gat schedule's is_sparser(true)
     const bool motion = std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
     if (s.model == "gcn") {

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
 GALAC = os.path.join(PKG, "gala", "galac")
-DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn_ksample", "gat", "gin", "sage")}
+DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn_ksample", "gcn_dsample", "gat", "gin", "sage")}
 
 
 def read_dump(path):
@@ -86,7 +86,7 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     assert r.returncode == 0, r.stderr
     ir = ref.load_ir(str(ir_path))["post"]
     ops = [nd["op"] for nd in ir["nodes"]]
-    if model in ("gcn", "gcn_ksample"):
+    if model in ("gcn", "gcn_ksample", "gcn_dsample"):
         assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same operator reordering
     elif model == "gat":
         assert ops.count("GAT_AGGREGATE") == 2

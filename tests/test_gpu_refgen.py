@@ -1,7 +1,7 @@
 """Programs emitted by the reference compiler's HIP generator, run on the MI355X.
 
 refgen/build.py (run in the build container, where the reference's sources are) emits the
-two-layer GCN (also kernel-sampled), GAT, GIN and GraphSAGE programs of
+two-layer GCN (also kernel- and data-sampled), GAT, GIN and GraphSAGE programs of
 tests/dsl/<model>_ref_codegen.txt through
 the reference's driver steps with HIPGenerator and compiles them over libgala_torch.so into
 refgen/bin/.
@@ -22,7 +22,7 @@ BIN = os.path.join(rc.PKG, "refgen", "bin")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["gcn", "gcn_ksample", "gat", "gin", "sage"])
+@pytest.mark.parametrize("model", ["gcn", "gcn_ksample", "gcn_dsample", "gat", "gin", "sage"])
 def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     exe = os.path.join(BIN, "gala_" + model)
     if not os.path.exists(exe):

@@ -5,8 +5,8 @@ end to end on the host, where the reference's sources are:
    HIPGenerator in place of CUDAGenerator -- is compiled against the reference's own headers
    (src/codegen/common.h, src/ir, src/frontend/context.h, src/middle-end) and run on a
    hand-built two-layer IR (the front-end's nodes and edges for the layer templates of the
-   four families of tests/GALA-DSL: GCN (also kernel-sampled, as in
-   tests/GALA-DSL/ablations/sampling/kernel), GAT over the column-tiled graph, GIN,
+   four families of tests/GALA-DSL: GCN (also kernel- and data-sampled, as in
+   tests/GALA-DSL/ablations/sampling/{kernel,data}), GAT over the column-tiled graph, GIN,
    GraphSAGE; bison is absent, so the parser cannot run);
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
    over `<kernel>_call` functions that forward to the operator mirror -- is compiled against
@@ -38,6 +38,7 @@ pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the referen
 CASES = {
     "gcn": ["64", "7", "32", "3", "2"],
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
+    "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "200"],
     "gin": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
@@ -63,7 +64,7 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
         assert cuda_name not in src, cuda_name
     assert "gala::aggregate_node_mul_sum_call" in src and "aggregate_node_mul_sum_coarse2_AutoGrad" in src
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
-    if model in ("gcn", "gcn_ksample", "gin"):
+    if model in ("gcn", "gcn_ksample", "gcn_dsample", "gin"):
         # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
         assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
         if model == "gcn_ksample":
@@ -71,6 +72,9 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
             # (ra*j + rb) mod deg edges with the reference's fixed (5, 7) (common.h:813-821,1342-1360)
             assert "5.000000 * global_segments[0]" in src and "global_ra = 5;" in src
             assert "segments, false, 5, global_ra, global_rb" in src
+        if model == "gcn_dsample":
+            # data sampling: the reference's host code samples the loaded graph before tiling it
+            assert src.index("inplace_sample_graph_ab(&adj0, 3, 5, 7);") < src.index("ord_col_tiling_torch(")
     elif model == "sage":
         # code motion ran: the first layer's mean aggregation is hoisted out of the training loop
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
