@@ -73,12 +73,13 @@ def compile_program(src: str, exe: str) -> None:
 
 def build_all() -> None:
     os.makedirs(BIN, exist_ok=True)
+    from concurrent.futures import ThreadPoolExecutor
     driver = os.path.join(BIN, "ir_driver")
     compile_driver(driver)
-    for model, args in PROGRAMS.items():
-        src = emit(driver, os.path.join(BIN, "src_" + model), model, "Cora", args)
-        compile_program(src, os.path.join(BIN, "gala_" + model))
-        print(f"refgen: built {os.path.join(BIN, 'gala_' + model)}")
+    srcs = {m: emit(driver, os.path.join(BIN, "src_" + m), m, "Cora", a) for m, a in PROGRAMS.items()}
+    with ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:   # g++ per program
+        for m in ex.map(lambda m: (compile_program(srcs[m], os.path.join(BIN, "gala_" + m)), m)[1], srcs):
+            print(f"refgen: built {os.path.join(BIN, 'gala_' + m)}")
 
 
 if __name__ == "__main__":
