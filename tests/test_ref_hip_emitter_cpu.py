@@ -46,18 +46,32 @@ CASES = {
 
 
 @pytest.fixture(scope="module")
-def driver(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("refgen") / "ir_driver")
+def programs(tmp_path_factory):
+    """The driver, then every case's emitted source and its compiled program (the g++ runs
+    in parallel): model -> (out dir, source text, program path)."""
+    from concurrent.futures import ThreadPoolExecutor
+    root = tmp_path_factory.mktemp("refgen")
+    exe = str(root / "ir_driver")
     refgen.compile_driver(exe)
-    return exe
+    built = {}
+    for model, args in CASES.items():
+        out = root / model
+        src = refgen.emit(exe, str(out), model, "Cora", args)
+        built[model] = (out, open(src).read(), str(out / "gala_model"))
+
+    def compile_one(model):
+        out, _, prog = built[model]
+        refgen.compile_program(str(out / "gala.cu"), prog)
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        list(ex.map(compile_one, built))
+    return built
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("model", sorted(CASES))
-def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
+def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model):
     # 1. the reference's driver with the HIP generator, on the hand-built IR
-    out = tmp_path / "out"
-    src = open(refgen.emit(driver, str(out), model, "Cora", CASES[model])).read()
+    out, src, prog = programs[model]
     assert (out / "CMakeLists.txt").read_text().count("gala_torch")
     for cuda_name in ("cudaMalloc", "cudaMemcpy", "cudaDeviceSynchronize", "torch::kCUDA", "__global__", "cusparse",
                       "unsupported"):
@@ -88,9 +102,8 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, driver, model):
             assert fwd.index(a) < fwd.index(b), (a, b)
         assert "ord_col_tiling_torch" in src   # the column-tiled graph, built by the reference's host code
 
-    # 2. the emitted program against the reference's host headers and the operator mirror
-    prog = str(tmp_path / "gala_model")
-    refgen.compile_program(str(out / "gala.cu"), prog)
+    # 2. the emitted program, compiled against the reference's host headers and the operator
+    # mirror (the fixture)
 
     # 3. run on the host backend, check against galac's program in the float64 executor
     d, X = rc.dataset(tmp_path)
