@@ -6,7 +6,7 @@ gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here w
 against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
 only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
 
-    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gcn_dsample,gat,gin,sage}
+    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gcn_dsample,gat,gin,gin_motion,sage}
 """
 import os
 import subprocess
@@ -28,6 +28,7 @@ PROGRAMS = {
     "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "5000"],
     "gin": ["64", "7", "32", "3", "2"],
+    "gin_motion": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
 }
 
@@ -42,14 +43,15 @@ def compile_driver(exe: str) -> None:
                    timeout=300)
 
 
-# gala_train's training-invariant code motion (tests/gala_train.cpp:136-140) for SAGE: without
+# gala_train's training-invariant code motion (tests/gala_train.cpp:136-140): for SAGE (without
 # it the reference generator's first SAGE FFN reads t_iden_n, which only the hoisted mean
-# aggregation defines (common.h:1210-1213)
-CODE_MOTION = {"sage"}
+# aggregation defines, common.h:1210-1213) and for the GIN under gala_train's passes
+CODE_MOTION = {"sage", "gin_motion"}
 
 
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
-    """Emit the program of `model` (a program name: gcn, gcn_ksample, gcn_dsample, gat, gin, sage)."""
+    """Emit the program of `model` (a program name: gcn, gcn_ksample, gcn_dsample, gat, gin, gin_motion,
+    sage)."""
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ)
     if model in CODE_MOTION:

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
 GALAC = os.path.join(PKG, "gala", "galac")
-DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn_ksample", "gcn_dsample", "gat", "gin", "sage")}
+DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage")}
 
 
 def read_dump(path):
@@ -76,7 +76,7 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     want_params = {"prediction", "loss", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
     if model == "gat":
         want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
-    elif model == "gin":
+    elif model in ("gin", "gin_motion"):
         want_params |= {"eps0", "eps1"}
     elif model == "sage":
         want_params |= {f"sfc{i}.{k}" for i in range(2) for k in ("weight", "bias")}
@@ -92,6 +92,8 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
         assert ops.count("GAT_AGGREGATE") == 2
     elif model == "gin":
         assert ops.count("SCALAR_ADD_EPS_MULTIPLY") == 2 and ops.index("FFN") < ops.index("GCN_AGGREGATE")
+    elif model == "gin_motion":
+        assert ops.count("SCALAR_ADD_EPS_MULTIPLY") == 2 and ops.index("GCN_AGGREGATE") < ops.index("FFN")
     else:
         assert [w["name"] for w in ir["weights"]] == ["fc0", "sfc0", "fc1", "sfc1"]
     g = layout.load_npy_dataset(d)

@@ -41,6 +41,7 @@ CASES = {
     "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "200"],
     "gin": ["64", "7", "32", "3", "2"],
+    "gin_motion": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
 }
 
@@ -89,6 +90,10 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         if model == "gcn_dsample":
             # data sampling: the reference's host code samples the loaded graph before tiling it
             assert src.index("inplace_sample_graph_ab(&adj0, 3, 5, 7);") < src.index("ord_col_tiling_torch(")
+    elif model == "gin_motion":
+        # gala_train's code motion: A x of the features hoisted, the FFNs back after the ADD
+        assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
+        assert fwd.index("res = res + t_iden_n;") < fwd.index("fc0->forward(res)")
     elif model == "sage":
         # code motion ran: the first layer's mean aggregation is hoisted out of the training loop
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
