@@ -6,7 +6,7 @@ gala.cu is host C++ over the operator mirror (libgala_torch.so), compiled here w
 against the reference's host headers. Needs /root/reference (or GALA_REF_ROOT); the GPU box
 only runs the programs built here (refgen/bin/, git-ignored, shipped with the tree).
 
-    python refgen/build.py            # refgen/bin/gala_{gcn,gcn_ksample,gcn_dsample,gat,gin,gin_motion,sage}
+    python refgen/build.py            # refgen/bin/gala_{gcn,gcn3,gcn_ksample,gcn_dsample,gat,gin,gin_motion,sage}
 """
 import os
 import subprocess
@@ -22,6 +22,8 @@ BIN = os.path.join(HERE, "bin")
 # (FEAT LABELS HIDDEN ITERS COARSEN [COL_TILE]); the GAT one over 4 column tiles of 20 000 rows
 PROGRAMS = {
     "gcn": ["64", "7", "32", "3", "2"],
+    # three layers (config 5's GCN-3) over 4 column tiles of 20 000 rows
+    "gcn3": ["64", "7", "32", "3", "2", "5000"],
     # the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel: sample(5), one tile
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     # the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data: G.sample(3), one tile
@@ -50,7 +52,7 @@ CODE_MOTION = {"sage", "gin_motion"}
 
 
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
-    """Emit the program of `model` (a program name: gcn, gcn_ksample, gcn_dsample, gat, gin, gin_motion,
+    """Emit the program of `model` (a program name: gcn, gcn3, gcn_ksample, gcn_dsample, gat, gin, gin_motion,
     sage)."""
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ)

@@ -28,7 +28,7 @@
 // Compiled against the reference's own headers where they lie (-I <reference>,
 // -I <reference>/src/codegen); nothing of the reference is copied.
 //
-// usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS
+// usage: ir_driver OUT_DIR/ gcn|gcn3|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS
 //                  [COARSEN [COL_TILE [NSAMP [DATA_SAMPLE]]]]
 // (NSAMP: aggrFn.sample(NSAMP), the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel;
 // DATA_SAMPLE: G.sample(n), the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data)
@@ -380,7 +380,7 @@ void buildSage(const Spec &s) {
 
 int main(int argc, char **argv) {
     if (argc < 8) {
-        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS "
+        std::cerr << "usage: ir_driver OUT_DIR/ gcn|gcn3|gat|gin|sage DATASET FEAT LABELS HIDDEN ITERS "
                      "[COARSEN [COL_TILE [NSAMP [DATA_SAMPLE]]]]\n";
         return 2;
     }
@@ -402,7 +402,8 @@ int main(int argc, char **argv) {
     }
     s.sparse = s.model == "gat";  // the tests/GALA-DSL/gat schedule's is_sparser(true)
     const bool motion = std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
-    if (s.model == "gcn") {
+    if (s.model == "gcn" || s.model == "gcn3") {  // gcn3: three layers (config 5's GCN-3, the
+        s.layers = s.model == "gcn3" ? 3 : 2;        // tests/GALA-DSL/ablations/scalability shape)
         buildGcn(s);
     } else if (s.model == "gat") {
         if (!s.col_tile) {  // the generator's edge operators need the tiled graph (common.h:641-650)

@@ -22,7 +22,7 @@ BIN = os.path.join(rc.PKG, "refgen", "bin")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["gcn", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage"])
+@pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage"])
 def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     exe = os.path.join(BIN, "gala_" + model)
     if not os.path.exists(exe):

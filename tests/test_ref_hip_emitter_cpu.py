@@ -5,7 +5,7 @@ end to end on the host, where the reference's sources are:
    HIPGenerator in place of CUDAGenerator -- is compiled against the reference's own headers
    (src/codegen/common.h, src/ir, src/frontend/context.h, src/middle-end) and run on a
    hand-built two-layer IR (the front-end's nodes and edges for the layer templates of the
-   four families of tests/GALA-DSL: GCN (also kernel- and data-sampled, as in
+   four families of tests/GALA-DSL: GCN (also three-layer, kernel- and data-sampled, as in
    tests/GALA-DSL/ablations/sampling/{kernel,data}), GAT over the column-tiled graph, GIN,
    GraphSAGE; bison is absent, so the parser cannot run);
 2. the gala.cu it writes -- the base generator's model, autograd classes and training loop
@@ -37,6 +37,7 @@ pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the referen
 # the GAT graph of 600 rows in 3 column tiles
 CASES = {
     "gcn": ["64", "7", "32", "3", "2"],
+    "gcn3": ["64", "7", "32", "3", "2", "300"],
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "200"],
@@ -79,7 +80,7 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         assert cuda_name not in src, cuda_name
     assert "gala::aggregate_node_mul_sum_call" in src and "aggregate_node_mul_sum_coarse2_AutoGrad" in src
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
-    if model in ("gcn", "gcn_ksample", "gcn_dsample", "gin"):
+    if model in ("gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gin"):
         # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
         assert fwd.index("fc0->forward") < fwd.index("_AutoGrad::apply")
         if model == "gcn_ksample":
