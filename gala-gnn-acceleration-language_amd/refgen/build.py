@@ -24,6 +24,9 @@ PROGRAMS = {
     "gcn": ["64", "7", "32", "3", "2"],
     # three layers (config 5's GCN-3) over 4 column tiles of 20 000 rows
     "gcn3": ["64", "7", "32", "3", "2", "5000"],
+    # config 5's GCN-3 at its own sizes (F 128, hidden 128, 172 labels, col_tile(1000000),
+    # 10 epochs: bench/dsl/gcn3_papers10.txt), for tools/refgen_config5.py
+    "gcn3_papers": ["128", "172", "128", "10", "2", "1000000"],
     # the kernel-sampled GCN of tests/GALA-DSL/ablations/sampling/kernel: sample(5), one tile
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     # the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data: G.sample(3), one tile
@@ -58,7 +61,7 @@ def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
     env = dict(os.environ)
     if model in CODE_MOTION:
         env["GALA_REFGEN_CODE_MOTION"] = "1"
-    family = model.split("_")[0]          # the driver's layer template
+    family = model.split("_")[0]          # the driver's layer template (gcn3_papers: gcn3)
     subprocess.run([driver, out_dir.rstrip("/") + "/", family, dataset, *args], check=True, capture_output=True,
                    text=True, timeout=60, env=env)
     return os.path.join(out_dir, "gala.cu")

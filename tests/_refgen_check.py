@@ -16,8 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 PKG = os.path.join(ROOT, "gala-gnn-acceleration-language_amd")
 GALAC = os.path.join(PKG, "gala", "galac")
-DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion",
-                                             "sage")}
+DSL = {m: f"{m}_ref_codegen.txt" for m in ("gcn", "gcn3", "gcn3_papers", "gcn_ksample", "gcn_dsample", "gat",
+                                             "gin", "gin_motion", "sage")}
 
 
 def read_dump(path):
@@ -75,7 +75,7 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     chain's attention-bias gradient is N * 1e-12 plus per-row softmax-gradient sums that cancel
     exactly, so its fp32 value is rounding noise that grows with the row count N."""
     want_params = {"prediction", "loss", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
-    if model == "gcn3":
+    if model in ("gcn3", "gcn3_papers"):
         want_params |= {"fc2.weight", "fc2.bias"}
     if model == "gat":
         want_params |= {f"efc{i}.{k}" for i in range(4) for k in ("weight", "bias")}
@@ -91,6 +91,8 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     ops = [nd["op"] for nd in ir["nodes"]]
     if model in ("gcn", "gcn3", "gcn_ksample", "gcn_dsample"):
         assert ops.index("FFN") < ops.index("GCN_AGGREGATE")   # the same operator reordering
+    elif model == "gcn3_papers":                                # no narrowing layer: nothing moves
+        assert [o for o in ops if o in ("FFN", "GCN_AGGREGATE")] == ["GCN_AGGREGATE", "FFN"] * 3
     elif model == "gat":
         assert ops.count("GAT_AGGREGATE") == 2
     elif model == "gin":

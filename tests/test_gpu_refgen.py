@@ -1,7 +1,8 @@
 """Programs emitted by the reference compiler's HIP generator, run on the MI355X.
 
 refgen/build.py (run in the build container, where the reference's sources are) emits the
-two-layer GCN (also kernel- and data-sampled), GAT, GIN and GraphSAGE programs of
+two-layer GCN (also kernel- and data-sampled), the three-layer GCN (also at config 5's layer
+widths), GAT, GIN and GraphSAGE programs of
 tests/dsl/<model>_ref_codegen.txt through
 the reference's driver steps with HIPGenerator and compiles them over libgala_torch.so into
 refgen/bin/.
@@ -22,12 +23,13 @@ BIN = os.path.join(rc.PKG, "refgen", "bin")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage"])
+@pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn3_papers", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage"])
 def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     exe = os.path.join(BIN, "gala_" + model)
     if not os.path.exists(exe):
         pytest.skip(f"{exe} is not built (refgen/build.py needs the reference's sources)")
-    d, X = rc.dataset(tmp_path, n=20000, nnz=240000, seed=11)
+    feat, labels = (128, 172) if model == "gcn3_papers" else (64, 7)    # refgen/build.py's PROGRAMS
+    d, X = rc.dataset(tmp_path, n=20000, nnz=240000, feat=feat, labels=labels, seed=11)
     dump = rc.run_program(exe, str(tmp_path), "cuda")
     # 20 000 rows: the GAT attention-bias gradients' cancellation noise is ~5e-8 against a
     # 1.5e-2 largest gradient (the same on the host backend), hence the 1e-5 floor

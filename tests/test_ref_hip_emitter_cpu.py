@@ -38,6 +38,7 @@ pytestmark = pytest.mark.skipif(not refgen.have_reference(), reason="the referen
 CASES = {
     "gcn": ["64", "7", "32", "3", "2"],
     "gcn3": ["64", "7", "32", "3", "2", "300"],
+    "gcn3_papers": ["128", "172", "128", "3", "2", "1000000"],   # config 5's layer widths
     "gcn_ksample": ["64", "7", "32", "3", "2", "10000000", "5"],
     "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "200"],
@@ -91,6 +92,11 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         if model == "gcn_dsample":
             # data sampling: the reference's host code samples the loaded graph before tiling it
             assert src.index("inplace_sample_graph_ab(&adj0, 3, 5, 7);") < src.index("ord_col_tiling_torch(")
+    elif model == "gcn3_papers":
+        # no layer narrows (128 -> 128 -> 128 -> 172): every aggregation stays before its FFN
+        for i in range(3):
+            assert fwd.index(f"fc{i}->forward") > fwd.index("_AutoGrad::apply")
+        assert fwd.count("_AutoGrad::apply") >= 3
     elif model == "gin_motion":
         # gala_train's code motion: A x of the features hoisted, the FFNs back after the ADD
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
@@ -112,6 +118,6 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
     # mirror (the fixture)
 
     # 3. run on the host backend, check against galac's program in the float64 executor
-    d, X = rc.dataset(tmp_path)
+    d, X = rc.dataset(tmp_path, feat=int(CASES[model][0]), labels=int(CASES[model][1]))
     dump = rc.run_program(prog, str(tmp_path), "cpu", timeout=120)
     rc.check_against_galac(model, dump, d, X, tmp_path / "ir.json")
