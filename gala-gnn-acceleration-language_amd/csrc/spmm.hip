@@ -14,6 +14,7 @@
 // bit-identical to the reference kernel while each lane keeps U*CH vector loads in
 // flight.  All address arithmetic is 64-bit.
 #include <stddef.h>
+#include <cstdlib>
 
 #include "gala_internal.h"
 
@@ -199,6 +200,75 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
     }
 }
 
+// A column-tiled row (several segments, no sampling): the rowptr pairs of kSegGroup segments
+// are loaded together and their edges walked as one list, segment order first, CSR order
+// inside a segment (the per-segment loop's order, so the sums are bit-identical).  With
+// col_tile(1000000) on an 11 M-row graph a row has ~0.2 edges per segment; the per-segment
+// loop paid rowptr -> col -> X as three dependent misses per segment (12 segments: 11 ms
+// per F = 128 call), here it is one of each per batch of U edges.
+constexpr int kSegGroup = 8;
+template <int VEC, int G, int CH, int U, bool W, bool SRCS>
+__device__ __forceinline__ void accumulate_segments(const SpmmParams &p, KernargSegPtr seg, const Cols<VEC, G, CH, W> &cl,
+                                                    int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
+    typedef typename VecT<VEC>::T V;
+    const int64_t rp_stride = p.n_rows + 1;
+    float rs[CH];
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) rs[ch] = (W && p.val_rs) ? p.val_rs[row * p.val_heads + cl.head[ch]] : 1.0f;
+    for (int s0 = 0; s0 < p.seg.n; s0 += kSegGroup) {
+        int64_t lo[kSegGroup];
+        int32_t pre[kSegGroup + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int i = 0; i < kSegGroup; ++i) {
+            const bool in = s0 + i < p.seg.n;
+            const int s = in ? s0 + i : s0;
+            const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
+            const int32_t a = rp[row], b = rp[row + 1];
+            lo[i] = (int64_t)seg->base[s] + a;
+            pre[i + 1] = pre[i] + (in ? b - a : 0);
+        }
+        const int32_t n = pre[kSegGroup];
+        for (int32_t j0 = 0; j0 < n; j0 += U) {
+            int32_t c[U];
+            V x[U][CH];
+            float w[U][CH];
+            float sc[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int32_t j = (j0 + k < n) ? j0 + k : n - 1;  // clamped: valid address
+                // the last segment starting at or before j holds it (an empty one is passed)
+                int64_t e = lo[0] + j;
+#pragma unroll
+                for (int i = 1; i < kSegGroup; ++i) e = (j >= pre[i]) ? lo[i] + (j - pre[i]) : e;
+                c[k] = p.col[e];
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch) w[k][ch] = W ? p.val[e * p.val_heads + cl.head[ch]] : 1.0f;
+            }
+            if (W && p.val_rs) {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+#pragma unroll
+                    for (int ch = 0; ch < CH; ++ch) w[k][ch] = __fmul_rn(w[k][ch], rs[ch]);
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const float *xr = p.X + (int64_t)c[k] * p.ldx;
+#pragma unroll
+                for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + cl.off[ch]);
+                sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                if (j0 + k < n) {
+#pragma unroll
+                    for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
+                }
+            }
+        }
+    }
+}
+
 template <int VEC, int G, int CH, bool W>
 __device__ __forceinline__ void init_acc(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
                                          int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
@@ -259,6 +329,11 @@ __device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid,
     init_acc<VEC, G, CH, W>(p, cl, row, acc);
     const int64_t rp_stride = p.n_rows + 1;
     const int nseg = p.seg.n;
+    if (!SAMP && nseg > 1) {
+        accumulate_segments<VEC, G, CH, U, W, SRCS>(p, seg, cl, row, acc);
+        store_row<VEC, G, CH, W>(p, cl, row, acc);
+        return;
+    }
     for (int s = 0; s < nseg; ++s) {
         const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
         const int64_t base = seg->base[s];
@@ -718,9 +793,29 @@ static void launch_flags(const SpmmParams &p, const SplitParams *sp, bool w, boo
     }
 }
 
+// Short rows (fewer than kSparseRowDeg edges on average: config 5's 11 M-row graph has
+// 2.45) leave a row's U-edge batch mostly empty, and the kernel waits out rowptr -> col -> X
+// once per row: its rate is rows in flight.  Rows of 17..64 float4 vectors then take half
+// the lanes with two vectors each (G/2, CH = 2, U = 4: the same x registers per lane), i.e.
+// twice the rows per wave.  The sums are unchanged (each lane still adds its features'
+// edges in CSR order).  GALA_SPMM_SPARSE_ROWS=0 keeps the wide groups (measurement).
+constexpr int64_t kSparseRowDeg = 8;
+static bool sparse_rows_enabled() {
+    static const bool on = [] {
+        const char *v = std::getenv("GALA_SPMM_SPARSE_ROWS");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 template <int VEC>
 static int launch_vec(const SpmmParams &p, const SplitParams *sp, int L, bool w, bool samp,
-                      bool srcs, hipStream_t st) {
+                      bool srcs, hipStream_t st, bool sparse_rows = false) {
+    if (VEC == 4 && sparse_rows && L > 16 && L <= 64) {
+        if (L <= 32) launch_flags<VEC, 16, 2>(p, sp, w, samp, srcs, st);
+        else launch_flags<VEC, 32, 2>(p, sp, w, samp, srcs, st);
+        return GALA_OK;
+    }
     // L = vector elements per row (ceil(F/VEC)).  Rows that are not a multiple of 4 floats
     // (VEC < 4) and span 17..64 vectors (F = 47, the Products class count) take 16 lanes
     // with ceil(L/16) chunks each rather than 64 lanes with one: 4 rows per wave.
@@ -907,7 +1002,9 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
                 r = launch_status();
                 if (r) return r;
             }
-            if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs);
+            const bool sparse_rows =
+                sparse_rows_enabled() && A->n_rows > 0 && A->nnz < kSparseRowDeg * (int64_t)A->n_rows;
+            if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs, sparse_rows);
             else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
             else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
             if (r) return r;

@@ -1,5 +1,7 @@
 // C++/libtorch mirror of GALA's emitted operator API over the C ABI (see gala_torch.h).
 #include "gala_torch.h"
+#include <climits>
+#include <cstring>
 
 #include "gala_cpu.h"
 
@@ -105,12 +107,26 @@ struct CsrView {
     torch::Tensor bounds_host;  // keeps the host bounds alive
 };
 
-// the split plan registered for this offsets tensor (same TensorImpl as a slot's)
+// the split plan registered for this offsets tensor (same TensorImpl as a slot's, or as a
+// slot's merged rowptr)
 SplitState *find_split(const torch::Tensor &offsets) {
     auto &S = global_slots();
-    for (size_t i = 0; i < S.offset_graph.size(); ++i)
+    for (size_t i = 0; i < S.offset_graph.size(); ++i) {
         if (S.split[i] && S.offset_graph[i].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
             return S.split[i].get();
+        if (S.merged[i] && S.merged[i]->split &&
+            S.merged[i]->rowptr.unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
+            return S.merged[i]->split.get();
+    }
+    return nullptr;
+}
+
+// the merged rows registered for this tiled offsets tensor
+const MergedCsr *find_merged(const torch::Tensor &offsets) {
+    auto &S = global_slots();
+    for (size_t i = 0; i < S.offset_graph.size(); ++i)
+        if (S.merged[i] && S.offset_graph[i].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
+            return S.merged[i].get();
     return nullptr;
 }
 
@@ -241,6 +257,11 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
                         const torch::Tensor *src_scale, const torch::Tensor *dst_scale,
                         int64_t nsamples, int64_t ra, int64_t rb,
                         const torch::Tensor *val_row_scale = nullptr) {
+    if (!vals && nsamples == 0 && segments > 1 && offsets.is_cuda()) {
+        if (const MergedCsr *m = find_merged(offsets))  // the same sums over one segment
+            return spmm_impl(X, m->rowptr, m->col, nullptr, torch::Tensor(), 1, val_heads, src_scale, dst_scale, 0,
+                             ra, rb, nullptr);
+    }
     CsrView cv = view(offsets, cols, vals, bounds, segments, val_heads);
     if (val_row_scale) {  // factored edge values (GAT p with its per-row q)
         check_dev(*val_row_scale, torch::kFloat, "val_row_scale");
@@ -364,6 +385,50 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
     return st;
 }
 
+std::shared_ptr<MergedCsr> make_merged_csr(const torch::Tensor &offsets, const torch::Tensor &cols,
+                                           const torch::Tensor &bounds_host, int segments) {
+    if (segments <= 1 || !offsets.defined() || !cols.defined() || !bounds_host.defined() ||
+        offsets.scalar_type() != torch::kInt || cols.scalar_type() != torch::kInt ||
+        offsets.numel() % segments != 0 || bounds_host.numel() < 2 * segments)
+        return nullptr;
+    auto rp = offsets.to(torch::kCPU).contiguous();
+    auto cl = cols.to(torch::kCPU).contiguous();
+    auto bd = bounds_host.to(torch::kCPU, torch::kInt).contiguous();
+    const int64_t n = offsets.numel() / segments - 1, nnz = cl.numel();
+    const int32_t *r = rp.data_ptr<int32_t>(), *c = cl.data_ptr<int32_t>(), *b = bd.data_ptr<int32_t>();
+    // the kernels' own checks (fill_segments, the rowptr contract): anything else stays tiled
+    int64_t total = 0;
+    for (int s = 0; s < segments; ++s) {
+        const int32_t *q = r + (int64_t)s * (n + 1);
+        if (b[2 * s] < 0 || b[2 * s + 1] < b[2 * s] || b[2 * s + 1] > nnz || q[0] < 0 ||
+            (int64_t)b[2 * s] + q[n] > nnz)
+            return nullptr;
+        for (int64_t i = 0; i < n; ++i)
+            if (q[i + 1] < q[i]) return nullptr;
+        total += q[n] - q[0];
+    }
+    if (total > INT32_MAX) return nullptr;
+    auto io = torch::TensorOptions().dtype(torch::kInt);
+    auto mrp = torch::empty({n + 1}, io), mcol = torch::empty({std::max<int64_t>(total, 1)}, io);
+    int32_t *o = mrp.data_ptr<int32_t>(), *oc = mcol.data_ptr<int32_t>();
+    int64_t k = 0;
+    o[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        for (int s = 0; s < segments; ++s) {
+            const int32_t *q = r + (int64_t)s * (n + 1);
+            const int64_t e0 = (int64_t)b[2 * s] + q[i], e1 = (int64_t)b[2 * s] + q[i + 1];
+            std::memcpy(oc + k, c + e0, (size_t)(e1 - e0) * sizeof(int32_t));
+            k += e1 - e0;
+        }
+        o[i + 1] = (int32_t)k;
+    }
+    auto m = std::make_shared<MergedCsr>();
+    m->rowptr = mrp.to(offsets.device());
+    m->col = mcol.to(offsets.device());
+    m->split = make_split_plan(m->rowptr, 1);
+    return m;
+}
+
 // ---- slots ----------------------------------------------------------------------------
 int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor vals,
                      torch::Tensor b, int segs, bool w) {
@@ -382,6 +447,13 @@ int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor va
     else if (offsets.is_cuda())  // the CPU backend runs every row in one sequential pass
         sp = make_split_plan(offsets, segs);
     split.push_back(sp);
+    std::shared_ptr<MergedCsr> mg;
+    if (!merged.empty() && offset_graph.size() >= 2 &&
+        offset_graph[offset_graph.size() - 2].unsafeGetTensorImpl() == offsets.unsafeGetTensorImpl())
+        mg = merged.back();
+    else if (offsets.is_cuda() && segs > 1 && !w)
+        mg = make_merged_csr(offsets, cols, bounds.back(), segs);
+    merged.push_back(mg);
     if (offset_graph.size() == 1) nrows = offsets.numel() / segs - 1;
     return (int)offset_graph.size() - 1;
 }

@@ -47,6 +47,18 @@ int32_t spmm_hub_flag();
 // mean: descending-degree row order); returns nullptr otherwise or for tiled graphs.
 std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int segments);
 
+// A column-tiled graph's rows with their segments concatenated (segment 0's edges first,
+// each segment's in CSR order: the order every tiled kernel sums in), built once per
+// unweighted tiled GPU graph.  The unweighted, unsampled SpMMs of the graph run on it as one
+// segment -- bit-identical sums, one rowptr pair per row instead of one per segment, and the
+// hub-row / degree-order plan of `split`.  nullptr for untiled, host or malformed graphs.
+struct MergedCsr {
+    torch::Tensor rowptr, col;
+    std::shared_ptr<SplitState> split;
+};
+std::shared_ptr<MergedCsr> make_merged_csr(const torch::Tensor &offsets, const torch::Tensor &cols,
+                                           const torch::Tensor &bounds_host, int segments);
+
 // The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's
 // forward graph, slot 2*li+1 its backward graph (the same tensors for undirected graphs,
 // cuda.h:1253-1257).  `bounds` stay on the host like the reference's total_bounds.
@@ -56,6 +68,7 @@ struct GraphSlots {
     std::vector<bool> weighted;
     std::vector<torch::Tensor> transpose_perm;  // optional: edge k of slot == edge perm[k] of forward
     std::vector<std::shared_ptr<SplitState>> split;  // hub-row plans (nullptr: none)
+    std::vector<std::shared_ptr<MergedCsr>> merged;  // tiled graphs' merged rows (nullptr: none)
     int64_t nrows = 0;
     int ra = 5, rb = 7;    // kernel-sampling coefficients (common.h:813-833)
     int nsamples = 0;      // 0 = no kernel sampling

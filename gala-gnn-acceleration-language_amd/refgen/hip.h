@@ -22,7 +22,8 @@
 //               option `.device(torch::kCUDA, 0)` and `cudaDeviceSynchronize()`, common.h
 //               :686-1557) retargeted to the program's device, and an optional dump of the
 //               first epoch's prediction, the initial weights, the loss and the weight
-//               gradients (GALA_DUMP=<file>).
+//               gradients (GALA_DUMP=<file>); the hidden Linears' calls go to the
+//               mirror's FFN op (row-split weight gradients, see denseOnMatrixCores).
 // The device is GALA_DEVICE (default "cuda", the HIP device of PyTorch-ROCm; "cpu" runs
 // the same program on the host backend).
 #ifndef GALA_HIP_CODEGEN_H
@@ -191,6 +192,8 @@ public:
         for (Code *c : {&kernelCallCode, model.getDef(), model.getInit(), model.getForward(), &preCode,
                         model.getInv(), model.getPreCall(), model.getCall(), model.getPostCall(), &postCode})
             retarget(*c);
+        denseOnMatrixCores(*model.getForward());
+        denseOnMatrixCores(*model.getInv());
         addDumpHook(*model.getPostCall());
         CodeGenerator::writeCode(cmakeCode, outStreamCMake);
         CodeGenerator::writeCode(importCode, outStreamModel);
@@ -266,14 +269,17 @@ private:
         s += "  global_offset_graph.push_back(t_offsets" + t + ");\n"
              "  global_columns_graph.push_back(t_cols" + t + ");\n"
              "  global_value_graph.push_back(t_vals" + t + ");\n";
-        s += register_(t, tiled, weighted);
+        s += register_(t, tiled, weighted, host, seg);
         return s;
     }
 
-    // the mirror's slot registry (its hub-row plans; one-segment graphs only have them)
-    static std::string register_(const std::string &t, bool tiled, bool weighted) {
-        if (tiled) return "";
-        return "  gala::global_slots().push(t_offsets" + t + ", t_cols" + t + ", t_vals" + t + ", torch::Tensor(), 1, " +
+    // the mirror's slot registry: a one-segment graph's hub-row plan; a column-tiled graph
+    // (the base's total_bounds_<name> / segments_<name>, common.h:1365-1402) gets its merged
+    // rows, on which its unweighted SpMMs run as one segment
+    static std::string register_(const std::string &t, bool tiled, bool weighted, const std::string &host,
+                                 const std::string &seg) {
+        const std::string b = tiled ? "total_bounds_" + host + ", " + seg : "torch::Tensor(), 1";
+        return "  gala::global_slots().push(t_offsets" + t + ", t_cols" + t + ", t_vals" + t + ", " + b + ", " +
                (weighted ? "true" : "false") + ");\n";
     }
 
@@ -285,7 +291,7 @@ private:
             s += "  global_offset_graph.push_back(t_offsets" + idx + ");\n"
                  "  global_columns_graph.push_back(t_cols" + idx + ");\n"
                  "  global_value_graph.push_back(t_vals" + idx + ");\n";
-            s += register_(idx, tiled, weighted);
+            s += register_(idx, tiled, weighted, tiled ? name : "adj" + idx, "segments_" + name);
         } else {          // directed: the transposed graph the host code built (adj<g>_b)
             s += slotCode(idx + "_b", idx, tiled ? name + "_b" : "adj" + idx + "_b", "segments_" + name + "_b", tiled,
                           weighted);
@@ -331,6 +337,38 @@ private:
             std::string *l = code.atLine(i);
             replaceAll(*l, ".device(torch::kCUDA, 0)", ".device(gala_program_device())");
             replaceAll(*l, "cudaDeviceSynchronize();", "gala_program_synchronize();");
+        }
+    }
+
+    // The model's hidden Linear layers (`fcN->forward(x)`, SAGE's `sfcN->forward(x)`,
+    // common.h:1205-1280) as the mirror's FFN op over the same parameters: the forward is
+    // at::linear's (at::addmm, or the matrix-core kernel for 33..64 outputs) and the weight /
+    // bias gradients run on gala_dense_grad_f32, split over rows.  torch::nn::Linear's
+    // backward takes dW = dYᵀX as one library GEMM whose only parallelism is the 128x128
+    // output (K = the 11 M rows of config 5: 12.0 ms per call on MI355X, 5.0 ms here;
+    // profiles/r04_refgen_config5_kernels.txt).
+    // The attention Linears (efcN, one output per head) stay as they are.
+    static void denseOnMatrixCores(Code &code) {
+        for (int i = 0; i < code.getNum(); ++i) {
+            std::string *l = code.atLine(i);
+            for (const std::string pre : {"sfc", "fc"}) {
+                for (size_t p = l->find(pre); p != std::string::npos; p = l->find(pre, p + 1)) {
+                    if (p > 0 && (std::isalnum((unsigned char)(*l)[p - 1]) || (*l)[p - 1] == '_')) continue;
+                    size_t q = p + pre.size();
+                    while (q < l->size() && std::isdigit((unsigned char)(*l)[q])) ++q;
+                    const std::string call = "->forward(";
+                    if (q == p + pre.size() || l->compare(q, call.size(), call) != 0) continue;
+                    const std::string mod = l->substr(p, q - p);
+                    size_t a = q + call.size(), e = a;
+                    for (int depth = 1; e < l->size(); ++e) {
+                        if ((*l)[e] == '(') ++depth;
+                        if ((*l)[e] == ')' && --depth == 0) break;
+                    }
+                    if (e >= l->size()) continue;
+                    const std::string arg = l->substr(a, e - a);
+                    l->replace(p, e + 1 - p, "gala::ffn_apply(" + arg + ", " + mod + "->weight, " + mod + "->bias)");
+                }
+            }
         }
     }
 

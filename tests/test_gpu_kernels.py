@@ -571,7 +571,11 @@ def test_sddmm_split_hub_rows(F, heads):
                                    (20000, 602, 256), (33, 7, 1), (1, 1, 1), (0, 16, 8),
                                    # narrow outputs (k_tn_skinny): every KL / CH class
                                    (100000, 32, 1), (100000, 47, 1), (70001, 5, 2), (3000, 16, 3),
-                                   (65537, 100, 4), (4099, 256, 1), (50, 129, 4), (0, 47, 1)])
+                                   (65537, 100, 4), (4099, 256, 1), (50, 129, 4), (0, 47, 1),
+                                   # LDS-staged 128 x 128 tiles (k_tn_lds): config 5's layers,
+                                   # partial m / k tiles, fewer rows than one stage, a ragged stage
+                                   (100000, 128, 128), (40000, 128, 172), (20003, 256, 68),
+                                   (5000, 132, 260), (31, 128, 128), (70, 68, 68)])
 def test_dense_grad_matches_float64(N, K, M):
     """dW = dY^T X, db = sum_n dY: |err| <= 1e-5 * sum_n |dY||X| (fp32 accumulation bound)."""
     rng = np.random.default_rng(N + K + M)

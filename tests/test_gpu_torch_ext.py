@@ -72,6 +72,25 @@ def test_emitted_functions_tiled(E):
     np.testing.assert_allclose(d.cpu().numpy(), orc.sddmm(to_oracle(g), A2, B2), **TOL)
 
 
+@pytest.mark.parametrize("tile", [300, 1000])
+def test_tiled_spmm_on_merged_rows_equals_segment_walk(E, tile):
+    """A registered tiled graph's unweighted SpMM runs on the slot's merged rows (segments
+    concatenated per row, with the merged graph's hub-row plan); an unregistered copy of the
+    same tensors takes the kernel's segment walk.  Both equal the oracle bit for bit."""
+    g = layout.col_tile(powerlaw(), tile)
+    assert g.n_seg > 1
+    off, cols, vals, bounds = push_graph(E, g)
+    X = dev(features(g.n_cols, 32))
+    want = orc.spmm(to_oracle(g), X.cpu().numpy())
+    merged = E.aggregate_node_mul_sum_call(X, off, cols, vals, bounds, g.n_seg)
+    walked = E.aggregate_node_mul_sum_call(X, off.clone(), cols.clone(), vals, bounds, g.n_seg)
+    np.testing.assert_array_equal(merged.cpu().numpy(), want)
+    np.testing.assert_array_equal(walked.cpu().numpy(), want)
+    ones = torch.ones(g.n_rows, 1, device="cuda")
+    deg = E.aggregate_node_mul_sum_direct_call(ones, off, cols, vals, bounds, g.n_seg)
+    np.testing.assert_array_equal(deg.cpu().numpy().ravel(), np.diff(powerlaw().rowptr).astype(np.float32))
+
+
 def test_gcn2_generated_forward_backward(E):
     """codegen/gala.cu:423-459 step through the mirror vs float64 torch.sparse."""
     g = powerlaw()

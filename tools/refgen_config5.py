@@ -65,7 +65,11 @@ def main():
     dump_path = os.path.join(root, "dump.bin")
     env = dict(os.environ, GALA_DEVICE=device, GALA_DUMP=dump_path)
     t0 = time.time()
-    p = subprocess.Popen([exe], cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cmd = [exe]
+    if os.environ.get("REFGEN_PROF"):          # kernel trace of the program: REFGEN_PROF=out_dir
+        cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.abspath(os.environ["REFGEN_PROF"]),
+               "-o", "run", "--"] + cmd
+    p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     while True:
         try:
             out, err = p.communicate(timeout=60)
@@ -75,7 +79,8 @@ def main():
     if p.returncode != 0:
         say(stage="program", rc=p.returncode, stderr=err[-2000:])
         return 1
-    last = (out.strip().splitlines() or [""])[-1]
+    import re
+    last = [ln for ln in out.splitlines() if re.fullmatch(r"[0-9.e+-]+,[0-9.e+-]+", ln.strip())][-1].strip()
     fwd_s, total_s = (float(v) for v in last.split(","))
     dump = rc.read_dump(dump_path)
     say(stage="program", epochs=10, wall_s=round(time.time() - t0, 1), fwd_mean_s=fwd_s,
