@@ -12,7 +12,7 @@
 //    rows, operands straight from global memory -- lane l reads dY[n][m0 + l%32] and
 //    X[n][k0 + l%32] of row n = 2s + l/32, both 128-B coalesced -- no LDS); consecutive
 //    waves share a chunk, so a row's bytes are fetched once and re-read from cache;
-//  * k_tn_lds: M and K > 64 with float4 rows, 128 x 128 block tiles whose row stages come
+//  * k_tn_lds: M and K > 64 with float4 rows, 128 (or 192) x 128 block tiles whose row stages come
 //    through LDS, double-buffered (see below);
 //  * k_tn_skinny: M <= 4 (the attention Linears, out = 1), lanes over K, see below.
 // Deterministic: the same shapes always use the same chunking and summation order (an
@@ -132,82 +132,101 @@ __global__ __launch_bounds__(kBlock) void k_tn_mfma(int64_t N, int32_t K, int32_
 }
 
 // Wide tiles (M > 64 and K > 64, every row a whole number of float4: config 5's 128 x 128
-// and 128 x 172 layers): a block owns a 128 (m) x 128 (k) tile of dW for one row chunk, and
-// its 32-row stages of dY and X come through LDS -- one float4 load per lane and row piece,
+// and 128 x 172 layers): a block owns a BM (m) x 128 (k) tile of dW for one row chunk, and
+// its 32-row (16 at BM = 192) stages of dY and X come through LDS -- one float4 load per lane and row piece,
 // double-buffered, the next stage's loads in flight while the matrix cores work on this one.
 // k_tn_mfma fed every MFMA operand by its own 4-B global load and waited out each batch
 // (5.0 ms for 11 M x 128 x 128, 0.46 of the f32 matrix peak).  Wave w of the block owns the
-// 64 x 64 quarter (m: w / 2, k: w % 2) as 2 x 2 32x32x2 tiles; a staged row is 128 floats
-// at a stride of 160, so the two row halves of an operand read (lanes 0-31 row n, 32-63 row
-// n + 1) fall in different banks.  Same partial layout and reduction as the other kernels.
-constexpr int kLdsRows = 32;                 // rows per stage
-constexpr int kLdsTile = 128;                // m and k extent of a block tile
-constexpr int kLdsStride = kLdsTile + 32;    // floats per staged row
-constexpr int kLdsStage = 2 * kLdsRows * kLdsStride;  // dY then X, floats
-constexpr size_t kLdsBytes = 2 * kLdsStage * sizeof(float);  // double-buffered: 80 KB
+// (BM / 2) x 64 quarter (m: w / 2, k: w % 2) as WT x 2 32x32x2 tiles; BM = 64 WT is 128, or
+// 192 when that pads M less (M = 172: one 192 tile instead of two of 128, the second 44
+// rows live).  A staged row of E floats sits at a stride of E + 32, so the two row halves of
+// an operand read (lanes 0-31 row n, 32-63 row n + 1) fall in different banks.  Same partial
+// layout and reduction as the other kernels.
+constexpr int kLdsK = 128;    // k extent of a block tile
+template <int WT>
+struct LdsTile {
+    static constexpr int R = WT == 2 ? 32 : 16;                // rows per stage
+    static constexpr int BM = 64 * WT;                         // m extent of a block tile
+    static constexpr int SY = BM + 32, SX = kLdsK + 32;        // staged row strides
+    static constexpr int stage = R * (SY + SX);                // dY then X, floats
+    static constexpr size_t bytes = 2 * stage * sizeof(float);  // double-buffered: 80 / 48 KB
+    static constexpr int NY = R * BM / 4 / kBlock;             // float4 loads per thread and stage
+    static constexpr int NX = R * kLdsK / 4 / kBlock;
+};
 
+template <int WT>
 __global__ __launch_bounds__(kBlock) void k_tn_lds(int64_t N, int32_t K, int32_t M,
                                                    const float *__restrict__ X, int64_t ldx,
                                                    const float *__restrict__ dY, int64_t ldy,
                                                    int64_t rows_per_chunk, int32_t tiles_m, int32_t tiles_k,
                                                    float *__restrict__ part, float *__restrict__ bpart) {
+    typedef LdsTile<WT> T;
     extern __shared__ float lds[];
     const int64_t chunk = blockIdx.x / (tiles_m * tiles_k);
     const int tg = (int)(blockIdx.x % (tiles_m * tiles_k));
-    const int mB = (tg / tiles_k) * kLdsTile, kB = (tg % tiles_k) * kLdsTile;
+    const int mB = (tg / tiles_k) * T::BM, kB = (tg % tiles_k) * kLdsK;
     const int64_t r0 = chunk * rows_per_chunk;
     const int64_t r1 = r0 + rows_per_chunk < N ? r0 + rows_per_chunk : N;
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     const int li = lane & 31, lh = lane >> 5;
-    const int mw = (wv >> 1) * 64, kw = (wv & 1) * 64;  // this wave's quarter of the tile
-    // stage loads: thread t moves float4 column c4 = t % 32 of rows t / 32 + 8 i (i < 4)
-    const int c4 = (threadIdx.x & 31) * 4, rt = threadIdx.x >> 5;
-    const bool my = mB + c4 < M, kx = kB + c4 < K;  // M, K multiples of 4: whole vectors
-    float4 ry[4], rx[4];
+    const int mw = (wv >> 1) * 32 * WT, kw = (wv & 1) * 64;  // this wave's quarter of the tile
+    // stage loads: float4 q = threadIdx.x + kBlock i of the stage's row-major image
+    float4 ry[T::NY], rx[T::NX];
     auto gload = [&](int64_t rb) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t n = rb + rt + 8 * i;
-            const bool ok = n < r1;
-            ry[i] = (ok && my) ? *reinterpret_cast<const float4 *>(dY + n * ldy + mB + c4) : make_float4(0, 0, 0, 0);
-            rx[i] = (ok && kx) ? *reinterpret_cast<const float4 *>(X + n * ldx + kB + c4) : make_float4(0, 0, 0, 0);
+        for (int i = 0; i < T::NY; ++i) {
+            const int q = threadIdx.x + kBlock * i, r = q / (T::BM / 4), c = (q % (T::BM / 4)) * 4;
+            const int64_t n = rb + r;
+            ry[i] = (n < r1 && mB + c < M) ? *reinterpret_cast<const float4 *>(dY + n * ldy + mB + c)
+                                          : make_float4(0, 0, 0, 0);  // M a multiple of 4: whole vectors
+        }
+#pragma unroll
+        for (int i = 0; i < T::NX; ++i) {
+            const int q = threadIdx.x + kBlock * i, r = q / (kLdsK / 4), c = (q % (kLdsK / 4)) * 4;
+            const int64_t n = rb + r;
+            rx[i] = (n < r1 && kB + c < K) ? *reinterpret_cast<const float4 *>(X + n * ldx + kB + c)
+                                          : make_float4(0, 0, 0, 0);
         }
     };
     auto swrite = [&](float *st) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = rt + 8 * i;
-            *reinterpret_cast<float4 *>(st + r * kLdsStride + c4) = ry[i];
-            *reinterpret_cast<float4 *>(st + (kLdsRows + r) * kLdsStride + c4) = rx[i];
+        for (int i = 0; i < T::NY; ++i) {
+            const int q = threadIdx.x + kBlock * i, r = q / (T::BM / 4), c = (q % (T::BM / 4)) * 4;
+            *reinterpret_cast<float4 *>(st + r * T::SY + c) = ry[i];
+        }
+#pragma unroll
+        for (int i = 0; i < T::NX; ++i) {
+            const int q = threadIdx.x + kBlock * i, r = q / (kLdsK / 4), c = (q % (kLdsK / 4)) * 4;
+            *reinterpret_cast<float4 *>(st + T::R * T::SY + r * T::SX + c) = rx[i];
         }
     };
-    f32x16 acc[2][2];
+    f32x16 acc[WT][2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = f32x16(0.0f);
-    float bacc[2] = {0.0f, 0.0f};
+    float bacc[WT] = {};
     const bool live = mB + mw < M && kB + kw < K;  // wave-uniform
     if (r0 < r1) gload(r0);
     int buf = 0;
-    for (int64_t rb = r0; rb < r1; rb += kLdsRows) {
-        float *st = lds + buf * kLdsStage;
+    for (int64_t rb = r0; rb < r1; rb += T::R) {
+        float *st = lds + buf * T::stage;
         swrite(st);
         __syncthreads();
-        if (rb + kLdsRows < r1) gload(rb + kLdsRows);
+        if (rb + T::R < r1) gload(rb + T::R);
         buf ^= 1;
-        if (!live) continue;  // a quarter past M or K (M = 172: the second m tile's upper half)
-        const float *ys = st + lh * kLdsStride + mw + li;
-        const float *xs = st + (kLdsRows + lh) * kLdsStride + kw + li;
+        if (!live) continue;  // a quarter wholly past M or K
+        const float *ys = st + lh * T::SY + mw + li;
+        const float *xs = st + T::R * T::SY + lh * T::SX + kw + li;
 #pragma unroll 4
-        for (int s2 = 0; s2 < kLdsRows; s2 += 2) {
-            float av[2], bv[2];
+        for (int s2 = 0; s2 < T::R; s2 += 2) {
+            float av[WT], bv[2];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) av[a] = ys[s2 * kLdsStride + a * 32];
+            for (int a = 0; a < WT; ++a) av[a] = ys[s2 * T::SY + a * 32];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) bv[b] = xs[s2 * kLdsStride + b * 32];
+            for (int b = 0; b < 2; ++b) bv[b] = xs[s2 * T::SX + b * 32];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) {
+            for (int a = 0; a < WT; ++a) {
                 bacc[a] += av[a];
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
@@ -218,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_tn_lds(int64_t N, int32_t K, int32_t
     // C/D layout: column (k) = lane % 32, row (m) = (r & 3) + 8 (r >> 2) + 4 (lane / 32)
     float *out = part + chunk * (int64_t)M * K;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < WT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             const int k = kB + kw + b * 32 + li;
@@ -230,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_tn_lds(int64_t N, int32_t K, int32_t
         }
     if (bpart && kB == 0 && kw == 0) {  // db: the two row parities (lane halves)
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
+        for (int a = 0; a < WT; ++a) {
             const float s2 = bacc[a] + __shfl_xor(bacc[a], 32, kWave);
             const int m = mB + mw + a * 32 + li;
             if (lh == 0 && m < M) bpart[chunk * M + m] = s2;
@@ -434,7 +453,8 @@ __global__ __launch_bounds__(kBlock) void k_tn_reduce_b(int64_t count, int64_t Q
 
 struct Plan {
     bool skinny;      // M <= 4 and K <= 256: k_tn_skinny; else k_tn_mfma
-    bool staged;      // M, K > 64, float4 rows: k_tn_lds (tiles_k / n_tg: its 128 x 128 tiles)
+    bool staged;      // M, K > 64, float4 rows: k_tn_lds (tiles_k / n_tg: its BM x 128 tiles)
+    int wt;           // k_tn_lds: BM = 64 wt (2 or 3)
     int wm, wk;       // MFMA wave tile: (32 wm) x (32 wk)
     int tiles_k, n_tg;  // wave tiles along K, per chunk
     int64_t P, rows_per_chunk;
@@ -448,11 +468,14 @@ Plan plan_for(int64_t N, int32_t K, int32_t M, bool vec4) {
     pl.staged = !pl.skinny && vec4 && M > 64 && K > 64;
     int64_t target;  // chunks
     int64_t align;   // rows per chunk: a multiple of the kernel's row step
-    if (pl.staged) {  // ~2 blocks (80 KB of LDS each) per CU
-        pl.tiles_k = (K + kLdsTile - 1) / kLdsTile;
-        pl.n_tg = pl.tiles_k * ((M + kLdsTile - 1) / kLdsTile);
+    if (pl.staged) {  // the m extent that pads M least; ~2 blocks per CU
+        const int64_t m128 = (M + 127) / 128 * 128, m192 = (M + 191) / 192 * 192;
+        pl.wt = m192 < m128 ? 3 : 2;
+        const int bm = 64 * pl.wt;
+        pl.tiles_k = (K + kLdsK - 1) / kLdsK;
+        pl.n_tg = pl.tiles_k * ((M + bm - 1) / bm);
         target = (512 + pl.n_tg - 1) / pl.n_tg;
-        align = kLdsRows;
+        align = 32;  // whole stages of either tile
     } else if (pl.skinny) {  // ~4 blocks per CU, chunks of whole block steps (4 x 4 waves x rows)
         pl.tiles_k = pl.n_tg = 1;
         target = 1024;
@@ -551,13 +574,19 @@ extern "C" int gala_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, const f
         else GALA_SK(64, 4);
 #undef GALA_SK
     } else if (pl.staged) {
-        static const hipError_t opted = hipFuncSetAttribute((const void *)k_tn_lds,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                            (int)kLdsBytes);
-        (void)opted;
-        hipLaunchKernelGGL(k_tn_lds, dim3((unsigned)(pl.P * pl.n_tg)), dim3(kBlock), kLdsBytes, hs, n_rows, K, M, X,
-                           ldx, dY, ldy, pl.rows_per_chunk, pl.n_tg / pl.tiles_k, pl.tiles_k, part,
-                           db ? bpart : nullptr);
+#define GALA_LDS(WT)                                                                                        \
+    do {                                                                                                    \
+        static const hipError_t opted = hipFuncSetAttribute((const void *)k_tn_lds<WT>,                     \
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                                            (int)LdsTile<WT>::bytes);                       \
+        (void)opted;                                                                                        \
+        hipLaunchKernelGGL(k_tn_lds<WT>, dim3((unsigned)(pl.P * pl.n_tg)), dim3(kBlock), LdsTile<WT>::bytes, hs, \
+                           n_rows, K, M, X, ldx, dY, ldy, pl.rows_per_chunk, pl.n_tg / pl.tiles_k, pl.tiles_k, \
+                           part, db ? bpart : nullptr);                                                     \
+    } while (0)
+        if (pl.wt == 3) GALA_LDS(3);
+        else GALA_LDS(2);
+#undef GALA_LDS
     } else {
         const int64_t n_work = pl.P * pl.n_tg;
         const dim3 g((unsigned)((n_work + kBlock / kWave - 1) / (kBlock / kWave)));

@@ -1296,9 +1296,15 @@ struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
         auto x = ctx->get_saved_variables()[0];
         auto &S = global_slots();
         Slot b = slot(2 * li + 1);
-        torch::Tensor dys = post.numel() > 0 ? row_broadcast(post, grad_outputs[0]) : grad_outputs[0];
+        // post * dY: on short rows (< 8 edges per row on average, config 5) as the SpMM's
+        // source scale -- fl(post[c] * dY[c]) per gathered element, the ROW_BROADCAST pass's
+        // roundings without its pass over [N, F]; on long rows the pass is cheaper than a
+        // scale load per edge
+        const bool has_post = post.numel() > 0;
+        const bool fold = has_post && b.cols.numel() < 8 * (x.size(0) > 0 ? x.size(0) : 1);
+        torch::Tensor dys = has_post && !fold ? row_broadcast(post, grad_outputs[0]) : grad_outputs[0].contiguous();
         auto G = spmm_impl(dys, b.off, b.cols, b.weighted ? &b.vals : nullptr, b.bounds, b.segs, 1,
-                           nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb);
+                           fold ? &post : nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb);
         return {relu_scale_backward(act.numel() > 0 ? act : torch::Tensor(), x, G), torch::Tensor(),
                 torch::Tensor(), torch::Tensor(), torch::Tensor()};
     }

@@ -575,7 +575,9 @@ def test_sddmm_split_hub_rows(F, heads):
                                    # LDS-staged 128 x 128 tiles (k_tn_lds): config 5's layers,
                                    # partial m / k tiles, fewer rows than one stage, a ragged stage
                                    (100000, 128, 128), (40000, 128, 172), (20003, 256, 68),
-                                   (5000, 132, 260), (31, 128, 128), (70, 68, 68)])
+                                   (5000, 132, 260), (31, 128, 128), (70, 68, 68),
+                                   # 192-row m tiles (they pad M less): one, and three with a partial last
+                                   (3000, 100, 180), (2000, 72, 540)])
 def test_dense_grad_matches_float64(N, K, M):
     """dW = dY^T X, db = sum_n dY: |err| <= 1e-5 * sum_n |dY||X| (fp32 accumulation bound)."""
     rng = np.random.default_rng(N + K + M)
