@@ -264,7 +264,8 @@ __global__ __launch_bounds__(kBlock) void k_tn_lds(int64_t N, int32_t K, int32_t
 // at an odd row stride, so the MFMA operand reads (lane l: row l%32, k = 2s + l/32) are
 // bank-conflict free.  One wave owns all M columns (WM tiles of 32); accumulators start at
 // the bias, and each 32x32 C tile is stored with 32 lanes on 32 consecutive columns of a row.
-constexpr int kFwdMaxKM = 16384;  // W^T floats in LDS (64 KB)
+constexpr int kFwdMaxKM = 24576;  // W^T floats in LDS (96 KB; past 64 KB the launch opts in)
+constexpr size_t kFwdMaxLds = 160 * 1024;  // gfx950's LDS per CU
 
 template <int WM, int V>
 __global__ __launch_bounds__(kBlock) void k_ffn_fwd(int64_t N, int32_t K, int32_t M,
@@ -619,11 +620,19 @@ extern "C" int gala_ffn_fwd_f32(int64_t n_rows, int32_t K, int32_t M, const floa
     if (blocks > 256 * 4) blocks = 256 * 4;  // blocks then walk 4-tile groups grid-stride
     const int Kp = (K + 1) & ~1;
     const size_t lds = sizeof(float) * ((size_t)Kp * 32 * wm + 4 * 32 * (size_t)(Kp + 1));
-    if (lds > 64 * 1024) return GALA_ERR_UNSUPPORTED;
+    if (lds > kFwdMaxLds) return GALA_ERR_UNSUPPORTED;
     const bool v4 = K % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X % 16) == 0;
     hipStream_t hs = (hipStream_t)stream;
 #define GALA_FF(WMV)                                                                                          \
     do {                                                                                                  \
+        static const hipError_t o4 = hipFuncSetAttribute((const void *)k_ffn_fwd<WMV, 4>,                 \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                                         (int)kFwdMaxLds);                                \
+        static const hipError_t o1 = hipFuncSetAttribute((const void *)k_ffn_fwd<WMV, 1>,                 \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                                         (int)kFwdMaxLds);                                \
+        (void)o4;                                                                                         \
+        (void)o1;                                                                                         \
         if (v4)                                                                                           \
             hipLaunchKernelGGL((k_ffn_fwd<WMV, 4>), dim3((unsigned)blocks), dim3(kBlock), lds, hs, n_rows, K, M, \
                                X, ldx, W, b, Y, ldy);                                                     \

@@ -506,7 +506,7 @@ def edge_permute(perm, src, heads=1):
 
 
 def ffn_fwd(X, W, b=None, out=None):
-    """Y = X W^T + b on the matrix cores (gala_ffn_fwd_f32; W^T must fit 16K floats)."""
+    """Y = X W^T + b on the matrix cores (gala_ffn_fwd_f32; W^T must fit 24K floats)."""
     X = X if X.stride(1) == 1 else X.contiguous()
     W = W.contiguous()
     N, K = X.shape

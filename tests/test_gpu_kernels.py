@@ -771,7 +771,9 @@ def test_row_scale_relu_matches_torch_chain(F, padded):
 
 @pytest.mark.parametrize("N,K,M", [(100000, 100, 32), (50000, 32, 47), (50000, 47, 32), (20000, 48, 128),
                                    (7000, 32, 172), (3000, 32, 256), (33, 7, 3), (1, 1, 1), (0, 16, 8),
-                                   (4097, 5, 40)])
+                                   (4097, 5, 40),
+                                   # W^T past 64 KB of LDS (the launch opts in to 160 KB)
+                                   (20000, 128, 128), (5000, 100, 160)])
 def test_ffn_fwd_matches_float64(N, K, M):
     """Y = X W^T + b on the matrix cores: |err| <= 1e-5 * sum_k |x w| + 1e-6 (fp32 chain)."""
     rng = np.random.default_rng(N + 7 * K + M)

@@ -27,7 +27,7 @@ def timed(fn, reps=20):
 
 def main():
     shapes = [(2449029, 100, 32), (2449029, 32, 47), (2449029, 32, 1), (2449029, 47, 1), (232965, 602, 256),
-              (232965, 256, 41), (169343, 128, 128), (11105995, 128, 128)]
+              (232965, 256, 41), (169343, 128, 128), (11105995, 128, 128), (11105995, 128, 172)]
     for N, K, M in shapes:
         X = torch.rand(N, K, device="cuda")
         dY = torch.rand(N, M, device="cuda")
