@@ -795,7 +795,7 @@ static void launch_flags(const SpmmParams &p, const SplitParams *sp, bool w, boo
 
 // Short rows (fewer than kSparseRowDeg edges on average: config 5's 11 M-row graph has
 // 2.45) leave a row's U-edge batch mostly empty, and the kernel waits out rowptr -> col -> X
-// once per row: its rate is rows in flight.  Rows of 17..64 float4 vectors then take half
+// once per row: its rate is rows in flight.  Rows of 5..64 float4 vectors then take half
 // the lanes with two vectors each (G/2, CH = 2, U = 4: the same x registers per lane), i.e.
 // twice the rows per wave.  The sums are unchanged (each lane still adds its features'
 // edges in CSR order).  GALA_SPMM_SPARSE_ROWS=0 keeps the wide groups (measurement).
@@ -811,8 +811,10 @@ static bool sparse_rows_enabled() {
 template <int VEC>
 static int launch_vec(const SpmmParams &p, const SplitParams *sp, int L, bool w, bool samp,
                       bool srcs, hipStream_t st, bool sparse_rows = false) {
-    if (VEC == 4 && sparse_rows && L > 16 && L <= 64) {
-        if (L <= 32) launch_flags<VEC, 16, 2>(p, sp, w, samp, srcs, st);
+    if (VEC == 4 && sparse_rows && L > 4 && L <= 64) {
+        if (L <= 8) launch_flags<VEC, 4, 2>(p, sp, w, samp, srcs, st);
+        else if (L <= 16) launch_flags<VEC, 8, 2>(p, sp, w, samp, srcs, st);
+        else if (L <= 32) launch_flags<VEC, 16, 2>(p, sp, w, samp, srcs, st);
         else launch_flags<VEC, 32, 2>(p, sp, w, samp, srcs, st);
         return GALA_OK;
     }
