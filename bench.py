@@ -665,6 +665,10 @@ def run_multi(args, rank, world, dev, be, timer, sync):
             out["weak"] = {"error": repr(e)[:500]}
         budget.phases["weak"] = time.time() - t0
     out["budget"] = budget.note()
+    # the largest message each collective kind sent (max over ranks) and its rounds: whether
+    # the all-to-all / p2p cut at MAX_MSG_BYTES held (RCCL corrupts payloads past 1 GiB, gala/comm.py)
+    from gala.comm import message_stats
+    out["comm"]["messages"] = message_stats(reduce_max)
     return out
 
 

@@ -77,7 +77,7 @@ extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t
     float *Y2 = epi ? epi->Y2 : nullptr;
     const int64_t ldy2 = Y2 ? epi->ldy2 : 0;
     const float *y2s = Y2 ? epi->y2_scale : nullptr;
-    if (dst_deg && (dst_scale || A->n_seg != 1 || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
+    if (dst_deg && (dst_scale || A->n_seg != 1 || A->val || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
     if (Y2 && ldy2 < F) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
@@ -197,7 +197,7 @@ extern "C" int gala_cpu_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, co
     int st = check_csr(A);
     if (st) return st;
     if (F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
-    if (A->n_seg != 1) return GALA_ERR_UNSUPPORTED;
+    if (A->n_seg != 1 || A->val) return GALA_ERR_UNSUPPORTED;  // rowptr counts: unweighted degree only
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!X || !Y) return GALA_ERR_INVALID_ARG;
 #pragma omp parallel for schedule(static, 1024)
@@ -308,7 +308,9 @@ extern "C" int gala_cpu_row_sum_f32(const gala_csr_t *A, const float *v_e, int32
                                     float eps, float *out_row, int32_t flags, void *) {
     int st = check_csr(A);
     if (st) return st;
-    if (heads < 1 || (flags & ~GALA_SPMM_ACCUM)) return GALA_ERR_INVALID_ARG;
+    // GALA_SPMM_HUB_CHUNKED is accepted (the HIP library's fast mode); every row here is
+    // one sequential pass, the reference's order
+    if (heads < 1 || (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_HUB_CHUNKED))) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!out_row || (!v_e && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const bool accum = (flags & GALA_SPMM_ACCUM) != 0;

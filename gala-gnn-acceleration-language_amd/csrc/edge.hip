@@ -92,26 +92,123 @@ __device__ __forceinline__ float sum_range(const float *v, int64_t e0, int64_t e
     return part;
 }
 
+// The reference's K7 sum in its own order (cuda.h:505-524: one thread per row, local = eps,
+// then local + v[e] for every edge in CSR order): the row group loads a register tile of G*K
+// values coalesced (value t of the row slice at lane t mod G, slot t div G), and lane h < HP
+// adds its head's values in edge order, fetched from their lanes with a shuffle.  Values of
+// the slice are vr[t * stride], t < n (stride > 1: one head of an [E, H] array).  Returns the
+// chain in lanes gl < HP (the head of lane gl); the other lanes' value is meaningless.
+template <int G, int HP>
+__device__ __forceinline__ float chain_range(const float *vr, int64_t n, int64_t stride, int gl, float local) {
+    constexpr int K = kTileK;
+    const int hb = gl & (HP - 1);
+    for (int64_t t0 = 0; t0 < n; t0 += G * K) {
+        float x[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int64_t t = t0 + gl + (int64_t)k * G;
+            x[k] = t < n ? vr[t * stride] : 0.0f;
+        }
+        const int64_t rem = n - t0;
+        // value j*HP + h of the tile: slot (j*HP) / G, lane (j*HP) % G + h (HP divides G)
+#pragma unroll
+        for (int j = 0; j < G * K / HP; ++j) {
+            const float xv = __shfl(x[(j * HP) / G], (j * HP) % G + hb, G);
+            if ((int64_t)j * HP < rem) local = __fadd_rn(local, xv);
+        }
+    }
+    return local;
+}
+
+// K7 for every row in the reference's order: per segment local = eps + the segment's values
+// in CSR order, added to the row's running value (segment 0 first; cuda.h:505-524,659-678,
+// whose per-segment launches each add one segment's local to C) -- bit-identical.
 template <int G, int HP>
 __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
                                                     int accum, float *out, int32_t thr) {
     GALA_ROW_PROLOGUE(G);
-    const bool mine = row_ok && !hub_row(p, thr, row);
-    float part = 0.0f;
-    if (mine) {
-        for (int s = 0; s < p.seg.n; ++s) {
-            int64_t e0, e1;
-            row_range(p, s, row, e0, e1);
-            part += sum_range<G, HP>(v, e0, e1, gl);
+    constexpr int LH = __builtin_ctz(HP);
+    if (!row_ok || hub_row(p, thr, row)) return;   // hub rows: k_row_sum_hub / the chunks
+    float c = (accum && gl < HP) ? out[row * HP + gl] : 0.0f;
+    for (int s = 0; s < p.seg.n; ++s) {
+        int64_t e0, e1;
+        row_range(p, s, row, e0, e1);
+        c = __fadd_rn(c, chain_range<G, HP>(v + (e0 << LH), (e1 - e0) << LH, 1, gl, eps));
+    }
+    if (gl < HP) out[row * HP + gl] = c;
+}
+
+// Hub rows of K7 in the reference's order (the default; GALA_SPMM_HUB_CHUNKED selects the
+// chunk partials below): one workgroup per (hub row, slice of <= 64 heads).  Waves 1-3 stage
+// tile t+1 of the row's values head-major in LDS ([head][edge], double-buffered) while lane h
+// of wave 0 adds tile t of its head in edge order -- the serial chain of the reference's
+// thread per row, fed from LDS so no global load latency sits in it.
+constexpr int kChainBuf = 6144;  // floats of values per LDS buffer
+constexpr int kChainPad = 4;     // per-head row padding: heads land on different banks
+
+__global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const float *v, float eps, int accum,
+                                                        float *out, HubSplit sp, int32_t n_slices) {
+    extern __shared__ float chain_lds[];
+    const int64_t ri = blockIdx.x / n_slices;
+    const int h0 = (int)(blockIdx.x % n_slices) * kWave;
+    const int H = p.heads;
+    const int hs = (H - h0) < kWave ? (H - h0) : kWave;       // heads of this slice
+    const int TE = (kChainBuf / hs) & ~3;                      // edges per tile
+    const int ld = TE + kChainPad;                             // LDS row of one head
+    const int buf_floats = hs * ld;
+    const int64_t row = sp.rows[ri];
+    const int64_t e0 = p.rowptr[row], n = (int64_t)p.rowptr[row + 1] - e0;
+    const int ntiles = (int)((n + TE - 1) / TE);
+    const bool chain = threadIdx.x < kWave;
+    const int g = threadIdx.x - kWave;
+    constexpr int kLoaders = kBlock - kWave;
+    auto fill = [&](int t) {
+        float *b = chain_lds + (t & 1) * buf_floats;
+        const int64_t es = e0 + (int64_t)t * TE;
+        const int ne = (int)((n - (int64_t)t * TE) < TE ? (n - (int64_t)t * TE) : TE);
+        const int total = ne * hs;
+        for (int i = g; i < total; i += kLoaders) {
+            const int e = i / hs, h = i - e * hs;
+            b[h * ld + e] = v[(es + e) * H + h0 + h];
         }
+    };
+    if (!chain) fill(0);
+    __syncthreads();
+    float local = eps;
+    const int lane = threadIdx.x;
+    for (int t = 0; t < ntiles; ++t) {
+        if (!chain) {
+            if (t + 1 < ntiles) fill(t + 1);
+        } else if (lane < hs) {
+            const float *b = chain_lds + (t & 1) * buf_floats + lane * ld;
+            const int ne = (int)((n - (int64_t)t * TE) < TE ? (n - (int64_t)t * TE) : TE);
+            int e = 0;
+            for (; e + 16 <= ne; e += 16) {
+                float4 q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const float4 *>(b + e + 4 * k);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    local = __fadd_rn(local, q[k].x);
+                    local = __fadd_rn(local, q[k].y);
+                    local = __fadd_rn(local, q[k].z);
+                    local = __fadd_rn(local, q[k].w);
+                }
+            }
+            for (; e < ne; ++e) local = __fadd_rn(local, b[e]);
+        }
+        __syncthreads();
     }
-    part = head_sum<G, HP>(part);
-    if (mine && gl < HP) {
-        // reference: each segment's sum starts at 1e-12 (cuda.h:512,666)
-        float r = part + (float)p.seg.n * eps;
-        if (accum) r = out[row * HP + gl] + r;
-        out[row * HP + gl] = r;
+    if (chain && lane < hs) {
+        const int64_t o = row * H + h0 + lane;
+        out[o] = __fadd_rn(accum ? out[o] : 0.0f, local);
     }
+}
+
+static inline size_t row_sum_hub_lds(int heads) {
+    const int hs = heads < kWave ? heads : kWave;
+    const int TE = (kChainBuf / hs) & ~3;
+    return 2 * (size_t)hs * (TE + kChainPad) * sizeof(float);
 }
 
 // hub rows: per-chunk head sums of v -> ws[c][h]
@@ -459,27 +556,22 @@ __global__ __launch_bounds__(kBlock) void k_sddvv_generic(EdgeParams p, const fl
 }
 
 // ---- edge -> row sum (K7) ----------------------------------------------------------
+// any head count: one head at a time, each in the reference's order (k_row_sum's chain over
+// the head's strided values)
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_row_sum_generic(EdgeParams p, const float *v, float eps,
                                                     int accum, float *out) {
     GALA_ROW_PROLOGUE(G);
+    if (!row_ok) return;
     const int H = p.heads;
     for (int h = 0; h < H; ++h) {
-        float part = 0.0f;
-        if (row_ok) {
-            for (int s = 0; s < p.seg.n; ++s) {
-                int64_t e0, e1;
-                row_range(p, s, row, e0, e1);
-                for (int64_t e = e0 + gl; e < e1; e += G) part += v[e * H + h];
-            }
+        float c = (accum && gl == 0) ? out[row * H + h] : 0.0f;
+        for (int s = 0; s < p.seg.n; ++s) {
+            int64_t e0, e1;
+            row_range(p, s, row, e0, e1);
+            c = __fadd_rn(c, chain_range<G, 1>(v + e0 * H + h, e1 - e0, H, gl, eps));
         }
-        part = group_sum<G>(part);
-        if (row_ok && gl == 0) {
-            // reference: each segment's sum starts at 1e-12 (cuda.h:512,666)
-            float r = part + (float)p.seg.n * eps;
-            if (accum) r = out[row * H + h] + r;
-            out[row * H + h] = r;
-        }
+        if (gl == 0) out[row * H + h] = c;
     }
 }
 
@@ -755,7 +847,7 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
     EdgeParams p;
     int st = edge_setup(A, heads, &p);
     if (st) return st;
-    if (flags & ~GALA_SPMM_ACCUM) return GALA_ERR_INVALID_ARG;
+    if (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_HUB_CHUNKED)) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!out_row || (!v_e && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const int accum = (flags & GALA_SPMM_ACCUM) ? 1 : 0;
@@ -765,8 +857,25 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
         const int G = std::max(pick_group_tiled(A, heads), hp);
         const dim3 grid(blocks_for(A->n_rows, G));
         HubSplit sp{};
-        const bool split = hub_split(A, 2 * (int64_t)hp, &sp);
+        const bool chunked = (flags & GALA_SPMM_HUB_CHUNKED) != 0;
+        // REF order (default): the hub rows' serial chains; chunked: partials + ordered fix-up
+        const bool split = hub_split(A, chunked ? 2 * (int64_t)hp : 0, &sp);
         const int32_t thr = split ? sp.threshold : 0;
+        if (split && !chunked) {   // the long chains first, beside the row kernel when the plan has a side stream
+            const int ns = (heads + kWave - 1) / kWave;
+            HubFork fk(A->split, hs);
+            st = fk.fork();
+            if (st) return st;
+            hipLaunchKernelGGL(k_row_sum_hub, dim3((unsigned)(sp.n_rows_split * ns)), dim3(kBlock),
+                               row_sum_hub_lds(heads), fk.side, p, v_e, eps, accum, out_row, sp, ns);
+            st = launch_status();
+            if (!st) {
+                GALA_DISPATCH_GH(G, hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps,
+                                                       accum, out_row, thr));
+                st = launch_status();
+            }
+            return fk.join(st);
+        }
         GALA_DISPATCH_GH(G, {
             hipLaunchKernelGGL((k_row_sum<GG, HH>), grid, dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row, thr);
             if (split) {
@@ -778,6 +887,7 @@ extern "C" int gala_row_sum_f32(const gala_csr_t *A, const float *v_e, int32_t h
         });
         return launch_status();
     }
+    // any other head count: every row (hub rows too) in one sequential pass per head
     const int G = pick_group(A, 1);
     GALA_DISPATCH_G(G, hipLaunchKernelGGL((k_row_sum_generic<GG>), dim3(blocks_for(A->n_rows, GG)),
                                           dim3(kBlock), 0, hs, p, v_e, eps, accum, out_row));

@@ -258,4 +258,38 @@ static inline bool hub_split(const gala_csr_t *A, int64_t need, HubSplit *sp) {
     return true;
 }
 
+// REF-order hub kernels run beside the row kernel on the plan's side stream when it has one
+// (gala_split_plan_t.aux_stream / aux_events): fork() makes the side stream wait for the
+// caller's, join(status) makes the caller's wait for the side stream -- also after a failed
+// launch, so a fork never stays open (that would invalidate a hipGraph capture).  Without
+// a side stream both are no-ops and `side` is the caller's stream.
+struct HubFork {
+    hipStream_t main, side;
+    hipEvent_t ev[2];
+    bool forked = false;
+    HubFork(const gala_split_plan_t *plan, hipStream_t hs) : main(hs), side(hs) {
+        if (plan && plan->aux_stream && plan->aux_events[0] && plan->aux_events[1]) {
+            side = (hipStream_t)plan->aux_stream;
+            ev[0] = (hipEvent_t)plan->aux_events[0];
+            ev[1] = (hipEvent_t)plan->aux_events[1];
+        }
+    }
+    int fork() {
+        if (side == main) return GALA_OK;
+        if (hipEventRecord(ev[0], main) != hipSuccess || hipStreamWaitEvent(side, ev[0], 0) != hipSuccess)
+            return launch_status();
+        forked = true;
+        return GALA_OK;
+    }
+    int join(int st) {
+        if (!forked) return st;
+        forked = false;
+        if (hipEventRecord(ev[1], side) != hipSuccess || hipStreamWaitEvent(main, ev[1], 0) != hipSuccess) {
+            const int j = launch_status();
+            return st ? st : (j ? j : GALA_ERR_HIP);
+        }
+        return st;
+    }
+};
+
 }  // namespace gala

@@ -289,10 +289,17 @@ extern "C" int gala_host_row_order(int64_t n_rows, const int32_t *rowptr, int32_
         start[kCap - std::min(deg, kCap) + 1]++;  // bucket 0 = the longest rows
     }
     for (int64_t b = 1; b <= kCap + 1; ++b) start[b] += start[b - 1];
+    const int64_t n_capped = start[1];  // rows with deg >= kCap: bucket 0
     for (int64_t r = 0; r < n_rows; ++r) {
         const int64_t deg = (int64_t)rowptr[r + 1] - rowptr[r];
         order[start[kCap - std::min(deg, kCap)]++] = (int32_t)r;
     }
+    // bucket 0 in exact descending degree (ties by row id): the whole order is then
+    // non-increasing in degree, so its first n entries are exactly the n longest rows -- the
+    // hub rows of any threshold (k_spmm_hub_exact takes them from there)
+    std::stable_sort(order, order + n_capped, [&](int32_t a, int32_t b) {
+        return rowptr[a + 1] - rowptr[a] > rowptr[b + 1] - rowptr[b];
+    });
     return GALA_OK;
 }
 

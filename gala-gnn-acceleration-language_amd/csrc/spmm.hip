@@ -864,7 +864,9 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
     const bool dst_deg = epi && epi->dst_deg_rsqrt;
     float *Y2 = epi ? epi->Y2 : nullptr;
     const int64_t ldy2 = Y2 ? epi->ldy2 : 0;
-    if (dst_deg && (dst_scale || A->n_seg != 1 || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
+    // the deg norm is the unweighted degree (rowptr counts): refused on weighted graphs, whose
+    // degree pass sums the values (k_degree_weighted)
+    if (dst_deg && (dst_scale || A->n_seg != 1 || A->val || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
     if (Y2 && ldy2 < F) return GALA_ERR_INVALID_ARG;
     if (F < 0 || ldx < F || ldy < F ||
         (flags & ~(GALA_SPMM_ACCUM | GALA_SPMM_SAMPLE | GALA_SPMM_EXACT | GALA_SPMM_HUB_CHUNKED)) ||
@@ -993,30 +995,36 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             q.F = Fc;
             q.accum = accum;
             const int L = (int)((Fc + vec - 1) / vec);
-            int r;
+            int r = 0;
+            const bool forked = use_hub && hub_st != hs;
             if (use_hub) {  // the long serial rows first, so their workgroups are dispatched first
-                if (hub_st != hs) {
+                if (forked) {
                     if (hipEventRecord((hipEvent_t)plan->aux_events[0], hs) != hipSuccess ||
                         hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)
                         return launch_status();
                 }
                 launch_hub(q, hp, vec, w, src_scale != nullptr, hub_st);
                 r = launch_status();
-                if (r) return r;
             }
-            const bool sparse_rows =
-                sparse_rows_enabled() && A->n_rows > 0 && A->nnz < kSparseRowDeg * (int64_t)A->n_rows;
-            if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs, sparse_rows);
-            else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
-            else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
-            if (r) return r;
-            r = launch_status();
-            if (r) return r;
-            if (use_hub && hub_st != hs) {  // join: the caller's stream waits for the hub rows
+            if (!r) {
+                const bool sparse_rows =
+                    sparse_rows_enabled() && A->n_rows > 0 && A->nnz < kSparseRowDeg * (int64_t)A->n_rows;
+                if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs, sparse_rows);
+                else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
+                else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
+                if (!r) r = launch_status();
+            }
+            // join (also after a failed launch, so a fork never stays open -- an unjoined fork
+            // would invalidate a hipGraph capture on the caller's stream): the caller's stream
+            // waits for the hub rows
+            if (forked) {
                 if (hipEventRecord((hipEvent_t)plan->aux_events[1], hub_st) != hipSuccess ||
-                    hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events[1], 0) != hipSuccess)
-                    return launch_status();
+                    hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events[1], 0) != hipSuccess) {
+                    const int j = launch_status();
+                    if (!r) r = j ? j : GALA_ERR_HIP;
+                }
             }
+            if (r) return r;
         }
     }
     return GALA_OK;
@@ -1202,7 +1210,7 @@ extern "C" int gala_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const 
     int st = check_csr(A);
     if (st) return st;
     if (F < 0 || ldx < F || ldy < F) return GALA_ERR_INVALID_ARG;
-    if (A->n_seg != 1) return GALA_ERR_UNSUPPORTED;
+    if (A->n_seg != 1 || A->val) return GALA_ERR_UNSUPPORTED;  // rowptr counts: unweighted degree only
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!X || !Y) return GALA_ERR_INVALID_ARG;
     return gala::launch_rows(A->n_rows, F, gala::rows_vec(F, {ldx, ldy}, {X, Y}),

@@ -25,6 +25,42 @@ import torch.distributed as dist
 MAX_MSG_BYTES = 1 << 29
 
 
+# Message sizes every collective kind sent in this process (for the first multi-GPU run to
+# show whether the MAX_MSG_BYTES cut held): per kind the calls, the largest tensor one RCCL
+# call was handed (an all-to-all round's send payload, one point-to-point piece), the largest
+# payload before cutting, and the most rounds / pieces one exchange took.  The host-staged
+# (gloo) path records the plan RCCL would have run.
+MSG_KINDS = ("all_gather", "reduce_scatter", "all_reduce", "all_to_all", "p2p")
+_MSG = {}
+
+
+def _note(kind: str, call_bytes: int, payload_bytes: int, rounds: int = 1) -> None:
+    s = _MSG.setdefault(kind, {"calls": 0, "max_call_bytes": 0, "max_payload_bytes": 0, "max_rounds": 0})
+    s["calls"] += 1
+    s["max_call_bytes"] = max(s["max_call_bytes"], int(call_bytes))
+    s["max_payload_bytes"] = max(s["max_payload_bytes"], int(payload_bytes))
+    s["max_rounds"] = max(s["max_rounds"], int(rounds))
+
+
+def reset_message_stats() -> None:
+    _MSG.clear()
+
+
+def message_stats(reduce_max=None) -> dict:
+    """{kind: {calls, max_call_bytes, max_payload_bytes, max_rounds}} for the kinds sent, plus
+    cut_at_bytes.  reduce_max (a collective every rank calls alike, e.g. a MAX all-reduce of
+    one number): the maxima over all ranks (every rank must call this together)."""
+    out = {}
+    for kind in MSG_KINDS:
+        s = dict(_MSG.get(kind, {"calls": 0, "max_call_bytes": 0, "max_payload_bytes": 0, "max_rounds": 0}))
+        if reduce_max is not None:
+            s = {k: int(reduce_max(float(v))) for k, v in s.items()}
+        if s["calls"]:
+            out[kind] = s
+    out["cut_at_bytes"] = MAX_MSG_BYTES
+    return out
+
+
 class _Works:
     """Several async collectives waited on as one (a chunked all-to-all)."""
 
@@ -46,7 +82,11 @@ def a2a_rounds(in_splits, out_splits, world: int, row_bytes: int, max_rows=None)
     nothing needs cutting."""
     in_splits, out_splits = [int(v) for v in in_splits], [int(v) for v in out_splits]
     r = max(MAX_MSG_BYTES // (world * row_bytes), 1)
-    m = max(in_splits + out_splits + [0]) if max_rows is None else int(max_rows)
+    biggest = max(in_splits + out_splits + [0])
+    if max_rows is not None and biggest > int(max_rows):
+        # rows past rounds * r would never be sent, and the output would keep stale rows
+        raise ValueError(f"a2a_rounds: a block of {biggest} rows exceeds max_rows={int(max_rows)}")
+    m = biggest if max_rows is None else int(max_rows)
     rounds = max(-(-m // r), 1)
     io, oo = [0] * world, [0] * world
     for q in range(1, world):
@@ -65,6 +105,10 @@ def p2p_pieces(rows: int, row_bytes: int):
     ends cut a message of the same shape alike)."""
     r = max(MAX_MSG_BYTES // row_bytes, 1)
     return [(0, rows)] if rows <= r else [(i, min(i + r, rows)) for i in range(0, rows, r)]
+
+
+def _bytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
 
 
 def _row_bytes(t: torch.Tensor) -> int:
@@ -101,6 +145,7 @@ class Comm:
     # -- collectives ----------------------------------------------------------------------
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         """out = concat over ranks of inp (out may contain inp: in-place all-gather)."""
+        _note("all_gather", _bytes(out), _bytes(out))
         if self.rccl:
             return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
         ho = torch.empty(out.shape, dtype=out.dtype)
@@ -110,6 +155,7 @@ class Comm:
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor):
         """out = sum over ranks of inp's block `rank` (blocks of out.shape[0] rows)."""
+        _note("reduce_scatter", _bytes(inp), _bytes(inp))
         if self.rccl:
             return dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group,
                                               async_op=True)
@@ -119,6 +165,7 @@ class Comm:
         return None
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM):
+        _note("all_reduce", _bytes(t), _bytes(t))
         if self.rccl:
             return dist.all_reduce(t, op=op, group=self.group, async_op=True)
         h = self._host(t).clone()
@@ -127,6 +174,7 @@ class Comm:
         return None
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        _note("all_to_all", _bytes(inp), _bytes(inp))
         if self.rccl:
             dist.all_to_all_single(out, inp, group=self.group)
             return
@@ -140,8 +188,11 @@ class Comm:
         max_rows: a bound on every block's rows that ALL ranks pass alike (it fixes the
         number of rounds when the exchange is cut at MAX_MSG_BYTES); default: this rank's
         largest block, which is only safe when no rank's exchange needs cutting."""
+        rb = _row_bytes(inp)
+        rounds = a2a_rounds(in_splits, out_splits, self.world, rb, max_rows)
+        _note("all_to_all", max(sum(b - a for a, b in ins) for ins, _ in rounds) * rb,
+              sum(int(v) for v in in_splits) * rb, len(rounds))
         if self.rccl:
-            rounds = a2a_rounds(in_splits, out_splits, self.world, _row_bytes(inp), max_rows)
             if len(rounds) == 1:
                 return dist.all_to_all_single(out, inp, output_split_sizes=[int(v) for v in out_splits],
                                               input_split_sizes=[int(v) for v in in_splits], group=self.group,
@@ -157,6 +208,9 @@ class Comm:
 
     def exchange(self, sends, recvs):
         """Grouped point-to-point: sends = [(tensor, peer)], recvs = [(tensor, peer)]."""
+        for t, _ in sends:
+            pc = p2p_pieces(t.shape[0], _row_bytes(t))
+            _note("p2p", max((b - a) for a, b in pc) * _row_bytes(t), _bytes(t), len(pc))
         if self.rccl:
             # messages past MAX_MSG_BYTES go as row pieces, in order (both ends cut alike)
             def pieces(t):

@@ -557,8 +557,18 @@ def main(argv=None):
                      rowptr=g_in.rowptr, col=g_in.col, weights=np.array(json.dumps(init_weights)),
                      samples=np.array(prog.samples, np.int64).reshape(-1, 2),
                      **{"grad:" + k: v for k, v in first_grads.items()})
+    messages = None
+    if distributed:   # every rank: the maxima over ranks are collectives
+        from .comm import message_stats
+
+        def reduce_max(x):
+            t = torch.tensor([x], dtype=torch.float64, device=dev if prog.comm.rccl else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+        messages = message_stats(reduce_max)
     if rank == 0:
         print(json.dumps({"ranks": world, "backend": dist.get_backend() if distributed else None,
+                          "messages": messages,
                           "vertices": g.n_rows, "edges": g.nnz, "layout": args.layout,
                           "halo": prog.part.halo_mode if args.layout == "halo" else None,
                           "exchange": prog.part.exchange if args.layout == "vcut" else None,

@@ -248,11 +248,14 @@ def sddvv(g: DeviceGraph, a, b, op=_abi.GALA_SDDVV_ADD, heads=1, slope=0.2) -> t
     return out
 
 
-def row_sum(g: DeviceGraph, v, heads=1, eps=1e-12, out=None, accum=False) -> torch.Tensor:
+def row_sum(g: DeviceGraph, v, heads=1, eps=1e-12, out=None, accum=False, hub="exact") -> torch.Tensor:
+    """out[r, h] (+)= eps + sum_{e in row r} v[e, h] (K7, gala_row_sum_f32) in the reference's
+    order, bit-identical; hub="chunked": the plan's hub rows as chunk partials (fast mode)."""
     if out is None:
         out = torch.zeros(g.n_rows * heads, device=v.device, dtype=torch.float32)
-    _abi.call("gala_row_sum_f32", g.csr(2 * heads), _dp(v), heads, eps, _dp(out),
-              _abi.GALA_SPMM_ACCUM if accum else 0, _stream())
+    flags = (_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_HUB_CHUNKED if hub == "chunked" else 0)
+    _abi.call("gala_row_sum_f32", g.csr(2 * heads if hub == "chunked" else 0), _dp(v), heads, eps, _dp(out),
+              flags, _stream())
     return out
 
 

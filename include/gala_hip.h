@@ -157,8 +157,10 @@ int gala_spmm_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, in
  * `norm * A (norm * H)` of codegen/gala.cu:433-456 without the separate degree and
  * ROW_BROADCAST passes:
  *   dst_deg_rsqrt = 1: the dst factor of row r is deg(r)^-0.5 computed from A's rowptr --
- *                   the exact values gala_degree_f32(power -0.5) gives (dst_scale must be
- *                   NULL; one segment; not with GALA_SPMM_SAMPLE);
+ *                   the exact values gala_degree_f32(power -0.5) gives on an unweighted
+ *                   graph (dst_scale must be NULL; one segment; A->val NULL -- a weighted
+ *                   graph's degree sums its values: GALA_ERR_UNSUPPORTED; not with
+ *                   GALA_SPMM_SAMPLE);
  *   Y2 != NULL:     also Y2[r, 0:F] = s2[r] * Y[r, 0:F] (s2 = y2_scale, or the dst factor
  *                   when NULL), rounded as the ROW_BROADCAST the next aggregation's input
  *                   would be -- bit-identical to that pass over Y.
@@ -172,8 +174,9 @@ typedef struct gala_spmm_epilogue {
 int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y, int64_t ldy, int32_t F,
                      const float *src_scale, const float *dst_scale, int32_t flags, int32_t nsamp,
                      int32_t ra, int32_t rb, const gala_spmm_epilogue_t *epi, void *stream);
-/* Y[r, :] = deg(r)^-0.5 * X[r, :] with deg from A's rowptr (one segment): the degree pass,
- * pow(-0.5) and the `norm * X` ROW_BROADCAST in one elementwise pass, bit-identical to them. */
+/* Y[r, :] = deg(r)^-0.5 * X[r, :] with deg from A's rowptr (one segment, unweighted: A->val
+ * set gives GALA_ERR_UNSUPPORTED): the degree pass, pow(-0.5) and the `norm * X`
+ * ROW_BROADCAST in one elementwise pass, bit-identical to them. */
 int gala_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, const float *X, int64_t ldx, float *Y,
                                int64_t ldy, void *stream);
 
@@ -573,9 +576,11 @@ int gala_host_split_plan(int64_t n_rows, const int32_t *rowptr, int32_t threshol
 int32_t gala_host_split_threshold(int64_t n_rows, int64_t nnz);
 
 /*
- * Row schedule for skewed graphs: order[] = the rows sorted by descending degree (stable
- * counting sort; degrees above 4096 share one bucket).  Degree-aware row binning
- * (SURVEY §7): rows that share a wavefront then have similar lengths.
+ * Row schedule for skewed graphs: order[] = the rows sorted by descending degree, ties by
+ * row id (a counting sort up to degree 4096, the rows above it sorted exactly).  Degree-aware
+ * row binning: rows that share a wavefront then have similar lengths; and for
+ * any threshold the rows longer than it are exactly the order's first entries (the REF-order
+ * hub kernel's contract, gala_split_plan_t.row_order).
  */
 int gala_host_row_order(int64_t n_rows, const int32_t *rowptr, int32_t *order);
 

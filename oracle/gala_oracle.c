@@ -280,14 +280,18 @@ void orc_head_attn(int64_t r0, int64_t r1, const float *X, int64_t ldx, int32_t 
 #define ROWS_OMP _Pragma("omp parallel for schedule(dynamic, 256)") for (int64_t r = 0; r < n_rows; ++r)
 #define EDGES for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e)
 
-void orc_gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col, int32_t H,
-                       int32_t D, const float *aL, const float *X, const float *wR,
-                       const float *bR, const float *dY, float slope, float *aR, float *s,
-                       float *pa, float *da, float *res, float *q, float *Y, float *dX,
-                       float *daL) {
+/* rid (nullable): row r of the CSR given is the layer's row rid[r] (a row sample of a larger
+ * graph: aL and the row side of dY are read at rid[r], columns stay global, outputs at r);
+ * aR must then hold every row already (no recompute). */
+static void gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col, int32_t H,
+                          int32_t D, const float *aL, const float *X, const float *wR,
+                          const float *bR, const float *dY, float slope, float *aR, float *s,
+                          float *pa, float *da, float *res, float *q, float *Y, float *dX,
+                          float *daL, const int64_t *rid) {
     const int32_t F = H * D;
-    orc_head_attn(0, n_rows, X, F, H, D, wR, bR, aR);
-    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) s[e * H + h] = aL[r * H + h] + aR[(int64_t)col[e] * H + h];
+    if (!rid) orc_head_attn(0, n_rows, X, F, H, D, wR, bR, aR);
+#define RID (rid ? rid[r] : r)
+    ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) s[e * H + h] = aL[RID * H + h] + aR[(int64_t)col[e] * H + h];
     ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) {
         const float v = s[e * H + h];
         pa[e * H + h] = v > 0.0f ? v : v * slope;
@@ -315,7 +319,7 @@ void orc_gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col
     ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) {
         float local = 0.0f;
         for (int32_t k = h * D; k < (h + 1) * D; ++k)
-            local = fmaf(dY[r * F + k], X[(int64_t)col[e] * F + k], local);
+            local = fmaf(dY[RID * F + k], X[(int64_t)col[e] * F + k], local);
         da[e * H + h] = local;
     }
     ROWS_OMP EDGES for (int32_t h = 0; h < H; ++h) da[e * H + h] = pa[e * H + h] * da[e * H + h];
@@ -335,6 +339,25 @@ void orc_gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col
         EDGES local = local + da[e * H + h];
         daL[r * H + h] = 0.0f + local;
     }
+#undef RID
+}
+
+void orc_gat_ref_layer(int64_t n_rows, const int32_t *rowptr, const int32_t *col, int32_t H,
+                       int32_t D, const float *aL, const float *X, const float *wR,
+                       const float *bR, const float *dY, float slope, float *aR, float *s,
+                       float *pa, float *da, float *res, float *q, float *Y, float *dX,
+                       float *daL) {
+    gat_ref_layer(n_rows, rowptr, col, H, D, aL, X, wR, bR, dY, slope, aR, s, pa, da, res, q, Y, dX,
+                  daL, NULL);
+}
+
+void orc_gat_ref_layer_rows(int64_t n_rows, const int32_t *rowptr, const int32_t *col, int32_t H,
+                            int32_t D, const float *aL, const float *X, const float *wR,
+                            const float *bR, const float *dY, float slope, float *aR, float *s,
+                            float *pa, float *da, float *res, float *q, float *Y, float *dX,
+                            float *daL, const int64_t *rid) {
+    gat_ref_layer(n_rows, rowptr, col, H, D, aL, X, wR, bR, dY, slope, aR, s, pa, da, res, q, Y, dX,
+                  daL, rid);
 }
 #undef ROWS_OMP
 #undef EDGES

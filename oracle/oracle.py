@@ -205,7 +205,11 @@ class GatRefLayer:
     [0, n_rows) of a CSR graph (a row sample of it when n_rows < the graph's).  Buffers are
     allocated (and prefaulted) once here; run() touches only them."""
 
-    def __init__(self, rowptr, col, n_rows, X, dY, aL, wR, bR, heads, slope=0.2):
+    def __init__(self, rowptr, col, n_rows, X, dY, aL, wR, bR, heads, slope=0.2, row_ids=None, aR=None):
+        """row_ids: row r of (rowptr, col) is the layer's row row_ids[r] of a larger graph
+        (aL and the row side of dY are read there; columns stay global; outputs at r).
+        aR: the source logits [rows, heads] to use (with row_ids; otherwise head_attn's)."""
+        self.rid = None if row_ids is None else np.ascontiguousarray(row_ids, np.int64)
         self.rowptr = np.ascontiguousarray(rowptr, np.int32)
         self.col = np.ascontiguousarray(col, np.int32)
         self.n_rows, self.H = int(n_rows), int(heads)
@@ -219,7 +223,10 @@ class GatRefLayer:
         ne = int(self.rowptr[self.n_rows]) * self.H
         self.nnz = int(self.rowptr[self.n_rows])
         # attention logits of every source row; run() recomputes rows [0, n_rows) itself
-        self.aR = head_attn(self.X, self.wR, self.bR, self.H)
+        # (unless row_ids is given)
+        self.aR = (head_attn(self.X, self.wR, self.bR, self.H) if aR is None
+                   else np.ascontiguousarray(aR, np.float32).reshape(-1, self.H))
+        assert aR is None or self.rid is not None, "aR is used as given only with row_ids"
         self.s, self.pa, self.da, self.res = (np.ones(ne, np.float32) for _ in range(4))
         self.q = np.ones((self.n_rows, self.H), np.float32)
         self.daL = np.ones((self.n_rows, self.H), np.float32)
@@ -227,11 +234,15 @@ class GatRefLayer:
         self.dX = np.ones((self.n_rows, self.F), np.float32)
 
     def run(self):
-        lib().orc_gat_ref_layer(_i64(self.n_rows), _ptr(self.rowptr), _ptr(self.col), _i32(self.H),
-                                _i32(self.F // self.H), _ptr(self.aL), _ptr(self.X), _ptr(self.wR),
-                                _ptr(self.bR), _ptr(self.dY), ctypes.c_float(self.slope), _ptr(self.aR),
-                                _ptr(self.s), _ptr(self.pa), _ptr(self.da), _ptr(self.res), _ptr(self.q),
-                                _ptr(self.Y), _ptr(self.dX), _ptr(self.daL))
+        args = (_i64(self.n_rows), _ptr(self.rowptr), _ptr(self.col), _i32(self.H),
+                _i32(self.F // self.H), _ptr(self.aL), _ptr(self.X), _ptr(self.wR),
+                _ptr(self.bR), _ptr(self.dY), ctypes.c_float(self.slope), _ptr(self.aR),
+                _ptr(self.s), _ptr(self.pa), _ptr(self.da), _ptr(self.res), _ptr(self.q),
+                _ptr(self.Y), _ptr(self.dX), _ptr(self.daL))
+        if self.rid is None:
+            lib().orc_gat_ref_layer(*args)
+        else:
+            lib().orc_gat_ref_layer_rows(*args, _ptr(self.rid))
         return self
 
 

@@ -43,6 +43,19 @@ def with_empty_rows(n=700, m=3000, seed=3) -> layout.HostGraph:
     return layout.csr_build(n, n, src, dst)
 
 
+def long_row_graph(seed=3) -> layout.HostGraph:
+    """Mean degree ~600 (hub threshold 8 * 600 > 4096): rows of 4 500 edges (above the row
+    order's counting-sort cap, below the threshold) beside real hub rows of 9 000-12 000."""
+    rng = np.random.default_rng(seed)
+    n = 2000
+    deg = rng.integers(450, 750, n)
+    deg[[5, 700, 1500, 1999]] = 4500
+    deg[[3, 900, 1200]] = [9000, 12000, 9000]
+    src = np.repeat(np.arange(n), deg).astype(np.int32)
+    dst = rng.integers(0, n, src.shape[0]).astype(np.int32)
+    return layout.csr_build(n, n, src, dst)
+
+
 def features(n, F, seed=1234, integer=False):
     rng = np.random.default_rng(seed)
     if integer:

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from gala import _abi, layout
+from _graphs import long_row_graph
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "gala_hip.h")
@@ -117,3 +118,18 @@ def test_col_tile_large_segment_count_and_breakpoints():
     assert t.n_seg == 16 and t.bounds[-1] == g.nnz
     rp = t.rowptr.reshape(t.n_seg, g.n_rows + 1)
     np.testing.assert_array_equal((rp[:, 1:] - rp[:, :-1]).sum(0), g.degrees())
+
+
+def test_row_order_exact_above_the_counting_cap():
+    """gala_host_row_order: non-increasing degree over the whole order (rows past the 4096
+    counting-sort cap sorted exactly, ties by row id), so the rows above any hub threshold
+    are exactly its first entries (the REF-order hub kernel's contract)."""
+    g = long_row_graph()
+    order = np.empty(g.n_rows, np.int32)
+    _abi.call("gala_host_row_order", g.n_rows, g.rowptr.ctypes.data, order.ctypes.data)
+    deg = np.diff(g.rowptr)
+    assert sorted(order.tolist()) == list(range(g.n_rows))
+    np.testing.assert_array_equal(order, np.lexsort((np.arange(g.n_rows), -deg)))
+    thr = layout.split_threshold(g.n_rows, g.nnz)
+    assert thr > 4500 and (deg > thr).sum() == 3
+    assert set(order[:3].tolist()) == set(np.flatnonzero(deg > thr).tolist())

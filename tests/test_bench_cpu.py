@@ -62,6 +62,16 @@ def test_bench_self_launches_ranks():
     bd = d["banded"]
     assert bd["value"] > 0 and bd["comm"]["halo_layout"] == "p2p" and "banded" in bd["graph"]
     assert bd["comm"]["halo_bytes_per_aggregation_per_rank"] < c["halo_bytes_per_aggregation_per_rank"]
+    # the largest message each collective kind sent (max over ranks) and its rounds
+    m = c["messages"]
+    assert m["cut_at_bytes"] == 1 << 29
+    assert {"all_gather", "reduce_scatter"} <= set(m)
+    for kind, st in m.items():
+        if kind == "cut_at_bytes":
+            continue
+        assert st["calls"] > 0 and st["max_rounds"] >= 1 and st["max_payload_bytes"] >= st["max_call_bytes"] > 0
+        if kind in ("all_to_all", "p2p"):
+            assert st["max_call_bytes"] <= m["cut_at_bytes"]
 
 
 def test_bench_eight_ranks():

@@ -299,6 +299,14 @@ def test_status_codes_match_the_hip_abi():
     bad = HostCsr(layout.col_tile(g, 1000))
     bad.g.bounds[1] = g.nnz + 5
     assert L.gala_cpu_spmm_f32(bad.ref, P(X), 4, P(Y), 4, 4, None, None, 0, 0, 5, 7, None) == _abi.GALA_ERR_GRAPH
+    # the rowptr-count degree norm is refused on a weighted graph (its degree sums the values)
+    W = HostCsr(g, val=edge_values(g.nnz))
+    epi = _abi.gala_spmm_epilogue_t()
+    epi.dst_deg_rsqrt = 1
+    assert L.gala_cpu_spmm_ex_f32(W.ref, P(X), 4, P(Y), 4, 4, None, None, 0, 0, 5, 7, ctypes.byref(epi),
+                                  None) == _abi.GALA_ERR_UNSUPPORTED
+    assert L.gala_cpu_row_broadcast_deg_f32(W.ref, 4, P(X), 4, P(Y), 4, None) == _abi.GALA_ERR_UNSUPPORTED
+    assert L.gala_cpu_row_broadcast_deg_f32(A.ref, 4, P(X), 4, P(Y), 4, None) == _abi.GALA_OK
 
 
 def test_row_scale_relu_and_backward_match_numpy():

@@ -175,6 +175,13 @@ def test_dist_run_vertex_cut_matches_one_rank(world, tmp_path):
     d1, _ = _run(ir_path, tmp_path, 1, "w1")
     dn, sn = _run(ir_path, tmp_path, world, f"v{world}", extra=("--layout", "vcut"))
     assert sn["layout"] == "vcut"
+    if world > 1:   # the summary's largest message per collective kind (max over ranks)
+        m = sn["messages"]
+        assert m["cut_at_bytes"] == 1 << 29 and m["all_reduce"]["calls"] > 0
+        assert ("reduce_scatter" in m) or ("all_to_all" in m)
+        for kind in ("reduce_scatter", "all_to_all"):
+            if kind in m:
+                assert m[kind]["max_rounds"] >= 1 and m[kind]["max_call_bytes"] > 0
     np.testing.assert_allclose(dn["prediction"], d1["prediction"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(dn["losses"], d1["losses"], rtol=1e-4, atol=1e-6)
     assert sn["loss_last"] < sn["loss_first"]

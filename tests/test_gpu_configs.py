@@ -88,8 +88,11 @@ def test_config3_products_gat8_rows_against_ref_layer():
     dX, daL = ops.gat_bwd_stats(dg, aL, aR, dY, q, Y, Ym, sma, heads=H)
     torch.cuda.synchronize()
     k = int(np.searchsorted(g.rowptr, 600_000))          # rows [0, k): ~600 K edges
-    ref = orc.GatRefLayer(g.rowptr, g.col, k, X.cpu().numpy(), dY.cpu().numpy(), aL.cpu().numpy(),
-                          wR.cpu().numpy(), bR.cpu().numpy(), H).run()
+    # on the kernels' own source logits (the reference's torch Linear order is unpinned; see
+    # tests/test_gpu_hub_rows.py)
+    ref = orc.GatRefLayer(g.rowptr[:k + 1], g.col[:g.rowptr[k]], k, X.cpu().numpy(), dY.cpu().numpy(),
+                          aL.cpu().numpy(), wR.cpu().numpy(), bR.cpu().numpy(), H, row_ids=np.arange(k),
+                          aR=aR.view(-1, H).cpu().numpy()).run()
     np.testing.assert_allclose(Y[:k].cpu().numpy(), ref.Y, **TOL)
     np.testing.assert_allclose(dX[:k].cpu().numpy(), ref.dX, **TOL)
     np.testing.assert_allclose(daL.view(-1, H)[:k].cpu().numpy(), ref.daL, **TOL)

@@ -173,7 +173,13 @@ def test_row_sum_and_scale(graph, tiled, heads):
     v = edge_values(g.nnz, heads=heads, seed=5)
     dg = ops.DeviceGraph.from_host(g, split=False)
     got = host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12))
-    np.testing.assert_allclose(got, orc.row_sum(to_oracle(g), v, heads=heads, eps=1e-12), **TOL)
+    # K7 in the reference's order (cuda.h:505-524): bit-identical, segments and empty rows too
+    np.testing.assert_array_equal(got, orc.row_sum(to_oracle(g), v, heads=heads, eps=1e-12))
+    out0 = features(g.n_rows, heads, seed=7).ravel()
+    acc = dev(out0)
+    ops.row_sum(dg, dev(v), heads=heads, eps=1e-12, out=acc, accum=True)
+    np.testing.assert_array_equal(host(acc), orc.row_sum(to_oracle(g), v, heads=heads, eps=1e-12,
+                                                         out=out0.copy(), accum=True))
     q = features(g.n_rows, heads, seed=6).ravel()
     vv = dev(v)
     ops.row_scale_(dg, dev(q), vv, heads=heads)
@@ -321,7 +327,10 @@ def test_edge_ops_hub_rows_split(heads, mode):
     np.testing.assert_array_equal(host(ops.sddvv(dg, dev(a), dev(b), op=2, heads=heads, slope=0.2)),
                                   orc.sddvv(og, a, b, heads=heads, op=2, slope=0.2))
     v = edge_values(g.nnz, heads=heads, seed=73)
-    np.testing.assert_allclose(host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12)),
+    # REF order (default): hub rows by k_row_sum_hub's chains, bit-identical; chunked: tolerance
+    np.testing.assert_array_equal(host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12)),
+                                  orc.row_sum(og, v, heads=heads, eps=1e-12))
+    np.testing.assert_allclose(host(ops.row_sum(dg, dev(v), heads=heads, eps=1e-12, hub="chunked")),
                                orc.row_sum(og, v, heads=heads, eps=1e-12), **TOL)
     vv = dev(v)
     ops.row_scale_(dg, dev(a), vv, heads=heads)
@@ -428,6 +437,12 @@ def test_spmm_epilogue_deg_norm_and_next_input(F, kind):
         ops.spmm(dg, Xs, dst_scale=norm, dst_deg=True)
     with pytest.raises(_abi.GalaError):
         ops.spmm(dg, Xs, dst_deg=True, nsamp=4)
+    # refused on a weighted graph (its degree pass sums the values, not the rowptr counts)
+    gw = dg.with_values(dev(edge_values(g.nnz)))
+    with pytest.raises(_abi.GalaError):
+        ops.spmm(gw, Xs, dst_deg=True)
+    with pytest.raises(_abi.GalaError):
+        ops.row_broadcast_deg(gw, X)
 
 
 def test_fused_gcn_step_matches_the_chain():
