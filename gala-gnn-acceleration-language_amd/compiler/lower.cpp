@@ -16,14 +16,104 @@
 //   - a name read in a layer before it is assigned (SAGE's `dsl.nn.ffn(res, out=hs)`)
 //     denotes the layer's input features, which is what ADD_TWO_FFN's self FFN reads
 //     (frontend.y:163-167, add_addTwoFFN_CIR).
+#include <algorithm>
+#include <cstring>
+#include <fstream>
 #include <functional>
 #include <map>
 #include <sstream>
+#include <vector>
 
 #include "../host/gala_datasets.h"
 #include "ir.h"
 
 namespace galac {
+
+namespace {
+// .npy header: dtype descr and shape; `data` at the first element (little-endian, C order)
+struct NpyHead {
+    std::string descr;
+    std::vector<int64_t> shape;
+    std::streamoff data = 0;
+};
+
+bool npy_head(const std::string &path, NpyHead *out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    char magic[8];
+    if (!f.read(magic, 8) || std::memcmp(magic, "\x93NUMPY", 6) != 0) return false;
+    uint32_t hlen = 0;
+    if (magic[6] == 1) {
+        uint16_t h16 = 0;
+        f.read((char *)&h16, 2);
+        hlen = h16;
+    } else {
+        f.read((char *)&hlen, 4);
+    }
+    std::string h(hlen, ' ');
+    if (!f.read(&h[0], hlen)) return false;
+    auto field = [&](const char *key) {
+        const size_t k = h.find(std::string("'") + key + "'");
+        if (k == std::string::npos) return std::string();
+        size_t a = h.find(':', k) + 1;
+        while (a < h.size() && h[a] == ' ') ++a;
+        const char close = h[a] == '(' ? ')' : (h[a] == '\'' ? '\'' : ',');
+        const size_t b = h.find(close, a + 1);
+        return h.substr(a, b == std::string::npos ? std::string::npos : b - a + 1);
+    };
+    out->descr = field("descr");
+    if (out->descr.size() < 4 || out->descr[1] == '>' || field("fortran_order").find("True") != std::string::npos)
+        return false;
+    out->descr = out->descr.substr(2, out->descr.size() - 3);   // '<u4' -> u4
+    const std::string shp = field("shape");
+    for (size_t q = 0; q < shp.size();) {
+        if (!std::isdigit((unsigned char)shp[q])) { ++q; continue; }
+        size_t e = q;
+        while (e < shp.size() && std::isdigit((unsigned char)shp[e])) ++e;
+        out->shape.push_back(std::stoll(shp.substr(q, e - q)));
+        q = e;
+    }
+    out->data = (std::streamoff)(magic[6] == 1 ? 10 : 12) + hlen;
+    return true;
+}
+
+// The dataset facts gala_inference reads at compile time (tests/gala_inference.cpp:98-120):
+// readSM_npy32's rows (Adj_src[0]) and stored edges (Adj_dst's length, tests/common.h:
+// 331-366), Feat.npy's columns and max(Lab) + 1.  false when a file is missing or unreadable.
+bool read_dataset_facts(const std::string &dir, int64_t *nrows, int64_t *nvals, int64_t *feat, int64_t *classes) {
+    NpyHead src, dst, ft, lab;
+    if (!npy_head(dir + "Adj_src.npy", &src) || !npy_head(dir + "Adj_dst.npy", &dst) ||
+        !npy_head(dir + "Feat.npy", &ft) || !npy_head(dir + "Lab.npy", &lab))
+        return false;
+    if (src.descr != "u4" || src.shape.empty() || src.shape[0] < 2 || dst.shape.empty() || ft.shape.size() != 2)
+        return false;
+    std::ifstream fs(dir + "Adj_src.npy", std::ios::binary);
+    uint32_t head[2];
+    fs.seekg(src.data);
+    if (!fs.read((char *)head, sizeof(head))) return false;
+    *nrows = head[0];
+    *nvals = dst.shape[0];
+    *feat = ft.shape[1];
+    int64_t n = 1;
+    for (int64_t d : lab.shape) n *= d;
+    std::ifstream fl(dir + "Lab.npy", std::ios::binary);
+    fl.seekg(lab.data);
+    int64_t mx = -1;
+    if (lab.descr == "i8") {
+        std::vector<int64_t> v((size_t)n);
+        if (!fl.read((char *)v.data(), (std::streamsize)(n * 8))) return false;
+        for (int64_t x : v) mx = std::max(mx, x);
+    } else if (lab.descr == "i4") {
+        std::vector<int32_t> v((size_t)n);
+        if (!fl.read((char *)v.data(), (std::streamsize)(n * 4))) return false;
+        for (int32_t x : v) mx = std::max<int64_t>(mx, x);
+    } else {
+        return false;
+    }
+    *classes = mx + 1;
+    return true;
+}
+}  // namespace
 
 const char *op_name(Op op) {
     switch (op) {
@@ -118,7 +208,8 @@ std::string Module::to_json() const {
     const Schedule &s = sched;
     o << "{\"source\": " << str(source) << ", \"output\": " << output
       << ", \"num_graphs\": " << num_graphs << ", \"num_layers\": " << num_layers
-      << ",\n \"sched\": {\"dataset\": " << str(s.dataset) << ", \"undirected\": " << s.undirected
+      << ",\n \"sched\": {\"dataset\": " << str(s.dataset) << ", \"opt_input\": " << str(s.opt_input)
+      << ", \"unweighted\": " << s.unweighted << ", \"coarsen\": " << s.coarsen << ", \"undirected\": " << s.undirected
       << ", \"sparse\": " << s.sparse << ", \"feat_size\": " << s.feat_size
       << ", \"label_size\": " << s.label_size << ", \"col_tile\": " << s.col_tile
       << ", \"data_sample\": " << s.data_sample << ", \"kernel_sample\": " << s.kernel_sample
@@ -369,7 +460,55 @@ class Lowering {
         return m_.sched.label_size;
     }
 
+    // G.opt_input(path): the input-aware schedule gala_inference fixes after parsing
+    // (tests/gala_inference.cpp:84-131) -- undirected, unweighted, coarsen(2), the feature and
+    // label sizes of the dataset, and COL_TILE nrows / 5 when nnz / nrows^2 > 0.001.  The
+    // facts come from the dataset's files (the path as written, from the working directory as
+    // the reference opens it, else from the DSL file's directory); when neither holds them,
+    // from the dataset's published shape (nnz = 2 * undirected edges + N self loops, the
+    // export's normalisation), noted.  The reference would stop there instead.
+    void auto_schedule() {
+        Schedule &s = m_.sched;
+        int64_t nrows = 0, nvals = 0, feat = 0, classes = 0;
+        std::string dir = s.opt_input;
+        if (!dir.empty() && dir.back() != '/') dir += '/';
+        std::string from;
+        const std::string src_dir = m_.source.find('/') == std::string::npos
+                                        ? std::string()
+                                        : m_.source.substr(0, m_.source.rfind('/') + 1);
+        if (read_dataset_facts(dir, &nrows, &nvals, &feat, &classes)) {
+            from = "the files in " + dir;
+        } else if (!src_dir.empty() && dir[0] != '/' &&
+                   read_dataset_facts(src_dir + dir, &nrows, &nvals, &feat, &classes)) {
+            from = "the files in " + src_dir + dir;
+        } else {
+            gala::DatasetShape shape{};
+            if (!gala::dataset_shape(s.dataset, &shape))
+                throw DslError({1, 1}, "opt_input(\"" + s.opt_input + "\"): no dataset files there and no published "
+                                       "shape for '" + s.dataset + "'");
+            nrows = shape.n;
+            nvals = 2 * shape.undirected + shape.n;
+            feat = shape.feat;
+            classes = shape.classes;
+            from = "the published " + s.dataset + " shape (no dataset files at " + s.opt_input + ")";
+        }
+        s.undirected = true;
+        s.unweighted = true;
+        s.coarsen = 2;
+        s.feat_size = feat;
+        s.label_size = classes;
+        // ((float)nvals / ((long)nrows * nrows)) > 0.001, as the reference evaluates it
+        const float density = (float)nvals / (float)(nrows * nrows);
+        if ((double)density > 0.001) s.col_tile = nrows / 5;
+        std::ostringstream o;
+        o << "opt_input schedule from " << from << ": N=" << nrows << " nnz=" << nvals << " density=" << density
+          << " -> undirected, unweighted, coarsen(2), feature_size " << feat << ", label_size " << classes
+          << (s.col_tile ? ", col_tile(" + std::to_string(s.col_tile) + ")" : std::string(", no column tiling"));
+        m_.notes.push_back(o.str());
+    }
+
     void build_model() {
+        if (!m_.sched.opt_input.empty()) auto_schedule();
         // sizes not given in the schedule: the dataset's published shape (the reference's
         // gala_inference reads them from the files at compile time, gala_inference.cpp:84-130)
         gala::DatasetShape shape{};

@@ -94,28 +94,59 @@ __device__ __forceinline__ float sum_range(const float *v, int64_t e0, int64_t e
 
 // The reference's K7 sum in its own order (cuda.h:505-524: one thread per row, local = eps,
 // then local + v[e] for every edge in CSR order): the row group loads a register tile of G*K
-// values coalesced (value t of the row slice at lane t mod G, slot t div G), and lane h < HP
-// adds its head's values in edge order, fetched from their lanes with a shuffle.  Values of
-// the slice are vr[t * stride], t < n (stride > 1: one head of an [E, H] array).  Returns the
-// chain in lanes gl < HP (the head of lane gl); the other lanes' value is meaningless.
+// values coalesced (value t of the row slice at lane t mod G, slot t div G), parks it in the
+// group's LDS region head-major ([head][value / HP], value t at head t mod HP), and lane
+// h < HP adds its head's values in edge order from there with 16-B reads -- the chain waits
+// on nothing but its own adds.  Values of the slice are vr[t * stride], t < n (stride > 1:
+// one head of an [E, H] array).  Returns the chain in lanes gl < HP (the head of lane gl);
+// the other lanes' value is meaningless.  The tile's tail holds +0.0f: adding it is exact
+// (local is never -0.0f: it starts at eps >= +0 and x + (-x) rounds to +0).
+constexpr int kChainRow = kTileK * kWave;  // floats of one wave's tile
 template <int G, int HP>
-__device__ __forceinline__ float chain_range(const float *vr, int64_t n, int64_t stride, int gl, float local) {
+struct ChainLds {
+    static constexpr int per_head = G * kTileK / HP + 4;   // padded: heads on other banks
+    static constexpr int per_group = HP * per_head;
+    static constexpr int per_wave = (kWave / G) * per_group;
+};
+
+template <int G, int HP>
+__device__ __forceinline__ float chain_range(const float *vr, int64_t n, int64_t stride, int gl, float local,
+                                             float *lg) {
     constexpr int K = kTileK;
-    const int hb = gl & (HP - 1);
+    typedef ChainLds<G, HP> L;
+    float *mine = lg + (gl & (HP - 1)) * L::per_head;   // this lane's head row (lanes gl < HP chain)
     for (int64_t t0 = 0; t0 < n; t0 += G * K) {
         float x[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
+        for (int k = 0; k < K; ++k) {   // clamped: every load is unconditional (n > t0 >= 0)
             const int64_t t = t0 + gl + (int64_t)k * G;
-            x[k] = t < n ? vr[t * stride] : 0.0f;
+            const float xv = vr[(t < n ? t : n - 1) * stride];
+            x[k] = t < n ? xv : 0.0f;
         }
-        const int64_t rem = n - t0;
-        // value j*HP + h of the tile: slot (j*HP) / G, lane (j*HP) % G + h (HP divides G)
+        // value t = k*G + gl -> head t mod HP = gl mod HP, position t div HP
 #pragma unroll
-        for (int j = 0; j < G * K / HP; ++j) {
-            const float xv = __shfl(x[(j * HP) / G], (j * HP) % G + hb, G);
-            if ((int64_t)j * HP < rem) local = __fadd_rn(local, xv);
+        for (int k = 0; k < K; ++k) lg[(gl & (HP - 1)) * L::per_head + k * (G / HP) + gl / HP] = x[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (gl < HP) {
+            const int64_t rem = n - t0;
+            const int cnt = (int)(((rem < G * K ? rem : G * K) + HP - 1) / HP);   // this head's values
+            const float4 *q = reinterpret_cast<const float4 *>(mine);
+            for (int j = 0; j < cnt; j += 16) {
+                float4 a[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = (j + 4 * i < cnt) ? q[j / 4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    local = __fadd_rn(local, a[i].x);
+                    local = __fadd_rn(local, a[i].y);
+                    local = __fadd_rn(local, a[i].z);
+                    local = __fadd_rn(local, a[i].w);
+                }
+            }
         }
+        __builtin_amdgcn_wave_barrier();   // the chain lanes' reads before the next tile's writes
     }
     return local;
 }
@@ -126,14 +157,17 @@ __device__ __forceinline__ float chain_range(const float *vr, int64_t n, int64_t
 template <int G, int HP>
 __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v, float eps,
                                                     int accum, float *out, int32_t thr) {
+    typedef ChainLds<G, HP> L;
+    __shared__ __attribute__((aligned(16))) float chain_tile[(kBlock / kWave) * L::per_wave];
     GALA_ROW_PROLOGUE(G);
     constexpr int LH = __builtin_ctz(HP);
     if (!row_ok || hub_row(p, thr, row)) return;   // hub rows: k_row_sum_hub / the chunks
+    float *lg = chain_tile + (threadIdx.x / kWave) * L::per_wave + (lane / G) * L::per_group;
     float c = (accum && gl < HP) ? out[row * HP + gl] : 0.0f;
     for (int s = 0; s < p.seg.n; ++s) {
         int64_t e0, e1;
         row_range(p, s, row, e0, e1);
-        c = __fadd_rn(c, chain_range<G, HP>(v + (e0 << LH), (e1 - e0) << LH, 1, gl, eps));
+        c = __fadd_rn(c, chain_range<G, HP>(v + (e0 << LH), (e1 - e0) << LH, 1, gl, eps, lg));
     }
     if (gl < HP) out[row * HP + gl] = c;
 }
@@ -145,32 +179,35 @@ __global__ __launch_bounds__(kBlock) void k_row_sum(EdgeParams p, const float *v
 // thread per row, fed from LDS so no global load latency sits in it.
 constexpr int kChainBuf = 6144;  // floats of values per LDS buffer
 constexpr int kChainPad = 4;     // per-head row padding: heads land on different banks
+static_assert(kChainBuf / kWave >= 16, "a tile holds at least 16 edges of every head");
 
 __global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const float *v, float eps, int accum,
                                                         float *out, HubSplit sp, int32_t n_slices) {
-    extern __shared__ float chain_lds[];
+    extern __shared__ __attribute__((aligned(16))) float chain_lds[];
     const int64_t ri = blockIdx.x / n_slices;
     const int h0 = (int)(blockIdx.x % n_slices) * kWave;
     const int H = p.heads;
-    const int hs = (H - h0) < kWave ? (H - h0) : kWave;       // heads of this slice
-    const int TE = (kChainBuf / hs) & ~3;                      // edges per tile
-    const int ld = TE + kChainPad;                             // LDS row of one head
+    const int hs = (H - h0) < kWave ? (H - h0) : kWave;        // heads of this slice (a power of two)
+    const int lhs = __builtin_ctz(hs);
+    const int TE = (kChainBuf >> lhs) & ~15;                    // edges per tile, a multiple of 16
+    const int ld = TE + kChainPad;                              // LDS row of one head
     const int buf_floats = hs * ld;
     const int64_t row = sp.rows[ri];
     const int64_t e0 = p.rowptr[row], n = (int64_t)p.rowptr[row + 1] - e0;
     const int ntiles = (int)((n + TE - 1) / TE);
     const bool chain = threadIdx.x < kWave;
     const int g = threadIdx.x - kWave;
-    constexpr int kLoaders = kBlock - kWave;
+    constexpr int kLoaders = kBlock - kWave;                    // 192: a multiple of every hs
+    const int lh = g & (hs - 1), estep = kLoaders >> lhs;
+    auto tile_edges = [&](int t) { return (int)((n - (int64_t)t * TE) < TE ? (n - (int64_t)t * TE) : TE); };
+    // loader thread g: head g mod hs, edges g / hs + k * (192 / hs) of the tile; the last
+    // tile's row tail up to a multiple of 16 is zero-filled (+0.0f adds are exact: local is
+    // never -0.0f)
     auto fill = [&](int t) {
-        float *b = chain_lds + (t & 1) * buf_floats;
+        float *b = chain_lds + (t & 1) * buf_floats + lh * ld;
         const int64_t es = e0 + (int64_t)t * TE;
-        const int ne = (int)((n - (int64_t)t * TE) < TE ? (n - (int64_t)t * TE) : TE);
-        const int total = ne * hs;
-        for (int i = g; i < total; i += kLoaders) {
-            const int e = i / hs, h = i - e * hs;
-            b[h * ld + e] = v[(es + e) * H + h0 + h];
-        }
+        const int ne = tile_edges(t), ne16 = (ne + 15) & ~15;
+        for (int e = g >> lhs; e < ne16; e += estep) b[e] = e < ne ? v[(es + e) * H + h0 + lh] : 0.0f;
     };
     if (!chain) fill(0);
     __syncthreads();
@@ -180,22 +217,27 @@ __global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const floa
         if (!chain) {
             if (t + 1 < ntiles) fill(t + 1);
         } else if (lane < hs) {
-            const float *b = chain_lds + (t & 1) * buf_floats + lane * ld;
-            const int ne = (int)((n - (int64_t)t * TE) < TE ? (n - (int64_t)t * TE) : TE);
-            int e = 0;
-            for (; e + 16 <= ne; e += 16) {
-                float4 q[4];
+            const float4 *b = reinterpret_cast<const float4 *>(chain_lds + (t & 1) * buf_floats + lane * ld);
+            const int n16 = (tile_edges(t) + 15) >> 4;
+            float4 cur[4], nxt[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const float4 *>(b + e + 4 * k);
+            for (int k = 0; k < 4; ++k) cur[k] = b[k];
+            for (int i = 0; i < n16; ++i) {
+                // the next group's reads are issued before this group's adds (the chain never
+                // waits on LDS latency); past the tile they read the padding, never used
+#pragma unroll
+                for (int k = 0; k < 4; ++k) nxt[k] = b[4 * (i + 1 < n16 ? i + 1 : i) + k];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    local = __fadd_rn(local, q[k].x);
-                    local = __fadd_rn(local, q[k].y);
-                    local = __fadd_rn(local, q[k].z);
-                    local = __fadd_rn(local, q[k].w);
+                    local = __fadd_rn(local, cur[k].x);
+                    local = __fadd_rn(local, cur[k].y);
+                    local = __fadd_rn(local, cur[k].z);
+                    local = __fadd_rn(local, cur[k].w);
                 }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
             }
-            for (; e < ne; ++e) local = __fadd_rn(local, b[e]);
         }
         __syncthreads();
     }
@@ -205,9 +247,9 @@ __global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const floa
     }
 }
 
-static inline size_t row_sum_hub_lds(int heads) {
+static inline size_t row_sum_hub_lds(int heads) {   // heads: a power of two
     const int hs = heads < kWave ? heads : kWave;
-    const int TE = (kChainBuf / hs) & ~3;
+    const int TE = (kChainBuf / hs) & ~15;
     return 2 * (size_t)hs * (TE + kChainPad) * sizeof(float);
 }
 
@@ -561,15 +603,18 @@ __global__ __launch_bounds__(kBlock) void k_sddvv_generic(EdgeParams p, const fl
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_row_sum_generic(EdgeParams p, const float *v, float eps,
                                                     int accum, float *out) {
+    typedef ChainLds<G, 1> L;
+    __shared__ __attribute__((aligned(16))) float chain_tile[(kBlock / kWave) * L::per_wave];
     GALA_ROW_PROLOGUE(G);
     if (!row_ok) return;
+    float *lg = chain_tile + (threadIdx.x / kWave) * L::per_wave + (lane / G) * L::per_group;
     const int H = p.heads;
     for (int h = 0; h < H; ++h) {
         float c = (accum && gl == 0) ? out[row * H + h] : 0.0f;
         for (int s = 0; s < p.seg.n; ++s) {
             int64_t e0, e1;
             row_range(p, s, row, e0, e1);
-            c = __fadd_rn(c, chain_range<G, 1>(v + e0 * H + h, e1 - e0, H, gl, eps));
+            c = __fadd_rn(c, chain_range<G, 1>(v + e0 * H + h, e1 - e0, H, gl, eps, lg));
         }
         if (gl == 0) out[row * H + h] = c;
     }

@@ -189,3 +189,55 @@ def test_emitted_program_compiles(tmp_path):
     r = subprocess.run(["make", "-C", str(out)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert os.access(out / "gala_prog", os.X_OK)
+
+
+def _opt_input_dsl(data_dir):
+    """The GCN-2 program of tests/GALA-DSL/ablations/input-optimize (structure), scheduled
+    only by opt_input."""
+    body = open(os.path.join(HERE, "dsl", "gcn.txt")).read().split("# schedule")[0]
+    return body.replace('load_dataset("Cora")', 'load_dataset("Mine")') + f'# schedule\nG = G.opt_input("{data_dir}");\n'
+
+
+def _write_dataset(d, n, m, feat, classes, seed=0):
+    rng = np.random.default_rng(seed)
+    d.mkdir(parents=True, exist_ok=True)
+    np.save(d / "Adj_src.npy", np.concatenate([[n, n], rng.integers(0, n, m)]).astype(np.uint32))
+    np.save(d / "Adj_dst.npy", rng.integers(0, n, m).astype(np.uint32))
+    np.save(d / "Feat.npy", rng.random((n, feat)).astype(np.float32))
+    lab = rng.integers(0, classes, n).astype(np.int64)
+    lab[0] = classes - 1
+    np.save(d / "Lab.npy", lab)
+
+
+@pytest.mark.parametrize("n,m,tiled", [(100, 200, True), (2000, 1000, False)])
+def test_opt_input_schedule_from_dataset_files(n, m, tiled, tmp_path):
+    """G.opt_input(path) fixes the schedule as gala_inference does after parsing
+    (tests/gala_inference.cpp:84-131): undirected, unweighted, coarsen(2), feature_size =
+    Feat.npy's columns, label_size = max(Lab) + 1, and COL_TILE nrows / 5 when the stored
+    edges over nrows^2 exceed 0.001 (200 / 100^2 = 0.02: tiled; 1000 / 2000^2: not)."""
+    _write_dataset(tmp_path / "data", n, m, feat=13, classes=6)
+    prog = tmp_path / "prog.txt"
+    prog.write_text(_opt_input_dsl(str(tmp_path / "data")))
+    s = galac(str(prog), tmp_path)["post"]["sched"]
+    assert (s["undirected"], s["unweighted"], s["coarsen"]) == (1, 1, 2)
+    assert (s["feat_size"], s["label_size"]) == (13, 6)
+    assert s["col_tile"] == (n // 5 if tiled else 0)
+    # a relative path is looked up from the working directory (the reference's) and then
+    # from the DSL file's directory
+    prog.write_text(_opt_input_dsl("data/"))
+    assert galac(str(prog), tmp_path)["post"]["sched"]["feat_size"] == 13
+
+
+@pytest.mark.skipif(not REF_DSL, reason="the reference's DSL corpus is not in this container")
+def test_opt_input_reference_programs(tmp_path):
+    """tests/GALA-DSL/ablations/input-optimize: Products lowers untiled (density 2e-5, the
+    schedule of the shipped codegen/gala.cu), Reddit into 5 column segments (density
+    0.0021 > 0.001: COL_TILE 232965 / 5); no dataset files here, so the facts come from the
+    datasets' published shapes."""
+    d = "/root/reference/tests/GALA-DSL/ablations/input-optimize/"
+    p = galac(d + "Products.txt", tmp_path)["post"]["sched"]
+    assert (p["unweighted"], p["coarsen"], p["feat_size"], p["label_size"], p["col_tile"]) == (1, 2, 100, 47, 0)
+    r = galac(d + "Reddit.txt", tmp_path)["post"]["sched"]
+    assert (r["unweighted"], r["coarsen"], r["feat_size"], r["label_size"]) == (1, 2, 602, 41)
+    assert r["col_tile"] == 232965 // 5
+    assert len(layout.col_breakpoints(232965, r["col_tile"])) - 1 == 5

@@ -10,7 +10,7 @@ import numpy as np
 
 import pytest
 
-from _dsl_check import PKG, PROGS, RESULT, check_against_ir, run_prog
+from _dsl_check import PKG, PROGS, RESULT, check_against_ir, check_against_ir_file, run_prog
 
 BENCH_PROG = os.path.join(PKG, "progs", "gcn_cora_cpu", "gala_prog")
 
@@ -23,12 +23,22 @@ def test_program_on_cpu_matches_ir_semantics(name, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists(BENCH_PROG), reason="bench/dsl programs not built")
-def test_cora_gcn_inference_config1():
-    r = subprocess.run([BENCH_PROG, "--synthetic", "--device", "cpu", "--iters", "10"],
-                       capture_output=True, text=True, timeout=300)
+def test_cora_gcn_inference_config1(tmp_path):
+    """Config 1 (bench/dsl/gcn_cora_cpu.txt: Cora GCN-2, hidden 16, col_tile(100000), the
+    gala_inference schedule) on the host backend: the run prints its timing / accuracy line,
+    and its first epoch -- prediction, loss and weight gradients -- matches the float64
+    executor of its own post-pass IR (tests/_dsl_check.py's tolerances), like every
+    tests/dsl program."""
+    from _ir_ref import read_dump
+    dump = tmp_path / "cora.dump"
+    r = subprocess.run([BENCH_PROG, "--synthetic", "--seed", "3", "--device", "cpu", "--iters", "10",
+                        "--dump", str(dump)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     fwd, acc = map(float, r.stdout.strip().splitlines()[-1].split(","))
     assert fwd > 0 and 0.0 <= acc <= 100.0
+    d = read_dump(str(dump))
+    assert d["t_iden"].shape == (2708, 1433) and d["prediction"].shape == (2708, 7)
+    check_against_ir_file(os.path.join(os.path.dirname(BENCH_PROG), "ir.json"), d)
 
 
 def test_gpu_device_without_gpu_fails_loudly(tmp_path):
