@@ -203,11 +203,25 @@ __global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const floa
     // loader thread g: head g mod hs, edges g / hs + k * (192 / hs) of the tile; the last
     // tile's row tail up to a multiple of 16 is zero-filled (+0.0f adds are exact: local is
     // never -0.0f)
+    // (32 loads in flight per thread -- a whole tile in one round trip for every slice width
+    // -- clamped to the tile: unconditional)
     auto fill = [&](int t) {
+        constexpr int U = 32;
         float *b = chain_lds + (t & 1) * buf_floats + lh * ld;
-        const int64_t es = e0 + (int64_t)t * TE;
+        const float *src = v + (e0 + (int64_t)t * TE) * H + h0 + lh;
         const int ne = tile_edges(t), ne16 = (ne + 15) & ~15;
-        for (int e = g >> lhs; e < ne16; e += estep) b[e] = e < ne ? v[(es + e) * H + h0 + lh] : 0.0f;
+        for (int ea = g >> lhs; ea < ne16; ea += U * estep) {
+            float x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = ea + u * estep;
+                const float xv = src[(int64_t)(e < ne ? e : ne - 1) * H];
+                x[u] = e < ne ? xv : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ea + u * estep < ne16) b[ea + u * estep] = x[u];
+        }
     };
     if (!chain) fill(0);
     __syncthreads();
@@ -217,26 +231,22 @@ __global__ __launch_bounds__(kBlock) void k_row_sum_hub(EdgeParams p, const floa
         if (!chain) {
             if (t + 1 < ntiles) fill(t + 1);
         } else if (lane < hs) {
-            const float4 *b = reinterpret_cast<const float4 *>(chain_lds + (t & 1) * buf_floats + lane * ld);
+            // groups of 16 values: 4 16-B reads, then 16 dependent adds (8.3 cycles per add
+            // measured on the 388 K-edge row; explicit read-ahead, 32- or 64-value groups and
+            // s_setprio measured no better, tools/row_sum_probe.py)
+            const float *bb = chain_lds + (t & 1) * buf_floats + lane * ld;
             const int n16 = (tile_edges(t) + 15) >> 4;
-            float4 cur[4], nxt[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = b[k];
             for (int i = 0; i < n16; ++i) {
-                // the next group's reads are issued before this group's adds (the chain never
-                // waits on LDS latency); past the tile they read the padding, never used
+                float4 q[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) nxt[k] = b[4 * (i + 1 < n16 ? i + 1 : i) + k];
-                __builtin_amdgcn_sched_barrier(0);
+                for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const float4 *>(bb + 16 * i + 4 * k);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    local = __fadd_rn(local, cur[k].x);
-                    local = __fadd_rn(local, cur[k].y);
-                    local = __fadd_rn(local, cur[k].z);
-                    local = __fadd_rn(local, cur[k].w);
+                    local = __fadd_rn(local, q[k].x);
+                    local = __fadd_rn(local, q[k].y);
+                    local = __fadd_rn(local, q[k].z);
+                    local = __fadd_rn(local, q[k].w);
                 }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
             }
         }
         __syncthreads();
