@@ -111,14 +111,18 @@ def _khop_induced(rowptr, col, seeds, hops):
 
 
 @pytest.mark.timeout(500)
-def test_dist_run_config5_shape_at_size(tmp_path):
+@pytest.mark.parametrize("scale,iters", [(0.1, 3), (1.0, 2)])
+def test_dist_run_config5_shape_at_size(scale, iters, tmp_path):
     """Config 5's program (bench/dsl/gcn3_papers10.txt, GCN-3 hidden 128, 172 classes) at
-    1.1 M rows (--scale 0.1 of the 10 % papers100M shape) through the multi-rank runtime on
-    the one GPU: the vertex cut over RCCL at world 1 (--dist: its reduce-scatters, or with
-    --exchange sparse its uneven all-to-alls and receive-CSR sums, run)
-    against the halo layout's exact mode (sampled rows' predictions and the loss curve
-    within fp32 rounding), and the halo run's first forward against the float64 IR executor
-    on sampled rows (their 3-hop induced subgraph, true degrees)."""
+    its own shape -- 11.1 M rows, the 10 % papers100M subset of
+    tests/GALA-DSL/ablations/scalability/graph_10.txt (scale 1.0) -- and at 1.1 M rows
+    (--scale 0.1), through the multi-rank runtime on the one GPU: the vertex cut over RCCL
+    at world 1 (--dist: its reduce-scatters, or with --exchange sparse its uneven all-to-alls
+    -- 5.7 GB per exchange at 11.1 M rows, cut into 512 MiB rounds -- and receive-CSR sums,
+    run) against the halo layout's exact mode (sampled rows' predictions within 1e-5, the
+    first loss within 1e-6, the curve within fp32 rounding), and the halo run's first forward
+    against the float64 IR executor on sampled rows (their 3-hop induced subgraph, true
+    degrees)."""
     from gala import dist_run
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ir_path = tmp_path / "p10.json"
@@ -127,15 +131,16 @@ def test_dist_run_config5_shape_at_size(tmp_path):
     r = subprocess.run([GALAC, os.path.join(root, "bench", "dsl", "gcn3_papers10.txt"), "--quiet", "--ir-json",
                         str(ir_path)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
-    common = ("--scale", "0.1", "--dump-stride", "997")
-    dh = _run_gpu(ir_path, tmp_path, 1, "halo", iters=3, extra=common)
+    common = ("--scale", str(scale), "--dump-stride", "997")
+    dh = _run_gpu(ir_path, tmp_path, 1, "halo", iters=iters, extra=common)
     n = len(dh["rowptr"]) - 1
-    assert n >= 1_000_000
+    assert n >= 11_000_000 * scale
     for exch in ("dense", "sparse"):
-        dv = _run_gpu(ir_path, tmp_path, 1, "vcut_" + exch, iters=3,
+        dv = _run_gpu(ir_path, tmp_path, 1, "vcut_" + exch, iters=iters,
                       extra=common + ("--layout", "vcut", "--dist", "--exchange", exch), backend="nccl")
         np.testing.assert_array_equal(dv["rows"], dh["rows"])
         np.testing.assert_allclose(dv["prediction"], dh["prediction"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(dv["losses"][0], dh["losses"][0], rtol=1e-6, atol=0)
         np.testing.assert_allclose(dv["losses"], dh["losses"], rtol=1e-4, atol=1e-6)
     ir = ref.load_ir(str(ir_path))["post"]
     seeds = dh["rows"][:: max(len(dh["rows"]) // 6, 1)][:6]
