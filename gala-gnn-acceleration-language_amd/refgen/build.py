@@ -35,6 +35,10 @@ PROGRAMS = {
     "gin": ["64", "7", "32", "3", "2"],
     "gin_motion": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
+    # the GCN-3 programs without HIPGenerator's fused GCN chains and loss (GALA_REFGEN_UNFUSED):
+    # the fused ones must give the same prediction and gradients bit for bit
+    "gcn3_unfused": ["64", "7", "32", "3", "2", "5000"],
+    "gcn3_papers_unfused": ["128", "172", "128", "10", "2", "1000000"],
 }
 
 
@@ -61,6 +65,8 @@ def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
     env = dict(os.environ)
     if model in CODE_MOTION:
         env["GALA_REFGEN_CODE_MOTION"] = "1"
+    if model.endswith("_unfused"):
+        env["GALA_REFGEN_UNFUSED"] = "1"
     family = model.split("_")[0]          # the driver's layer template (gcn3_papers: gcn3)
     subprocess.run([driver, out_dir.rstrip("/") + "/", family, dataset, *args], check=True, capture_output=True,
                    text=True, timeout=60, env=env)

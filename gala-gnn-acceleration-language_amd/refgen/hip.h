@@ -29,6 +29,8 @@
 #ifndef GALA_HIP_CODEGEN_H
 #define GALA_HIP_CODEGEN_H
 
+#include <cstdlib>
+#include <regex>
 #include <unordered_set>
 
 #include "common.h"
@@ -153,8 +155,17 @@ public:
         }
     }
 
+    // The features leave the program without requires_grad: CUDAGenerator creates them with
+    // options_cu_float_grad (cuda.h:1381-1382), so every backward also formed and accumulated
+    // d t_iden -- an [N, F] gradient nothing reads (5.7 GB per epoch at config 5's 11 M rows:
+    // the first aggregation's backward, its ROW_BROADCAST and the accumulation, 7.7 ms).  The
+    // weights' gradients are unchanged (checked bit for bit against the base spelling,
+    // GALA_REFGEN_UNFUSED, which keeps it).
     void dataPrep(std::vector<CIRNode *> &program) override {
         std::string s =
+            "  // GALA_SEED=<n>: torch's generators seeded before the model's weights are drawn (the\n"
+            "  // reference seeds nothing: every run starts from other weights)\n"
+            "  if (const char *seed = std::getenv(\"GALA_SEED\")) torch::manual_seed(std::atoll(seed));\n"
             "  torch::Device device = gala_program_device();\n"
             "  auto options_cu_int = torch::TensorOptions().dtype(torch::kInt).requires_grad(false).device(device);\n"
             "  auto options_cu_float_grad = torch::TensorOptions().dtype(torch::kFloat).requires_grad(true).device(device);\n"
@@ -163,7 +174,8 @@ public:
             "  auto options_cu_long = torch::TensorOptions().dtype(torch::kLong).device(device);\n"
             "  // features, labels and masks: host matrices copied into torch-owned device tensors\n"
             "  torch::Tensor t_iden = torch::from_blob(input_emb.vals_ptr(), {(int64_t)nrows, (int64_t)emb_size},\n"
-            "                                         torch::kFloat).to(device).clone().requires_grad_(true);\n"
+            "                                         torch::kFloat).to(device).clone()" +
+            std::string(std::getenv("GALA_REFGEN_UNFUSED") ? ".requires_grad_(true)" : "") + ";\n"
             "  torch::Tensor t_labs = torch::from_blob(labels.vals_ptr(), {(int64_t)nrows}, torch::kLong).to(device).clone();\n"
             "  torch::Tensor t_train_mask = torch::from_blob(train_mask.vals_ptr(), {(int64_t)nrows}, torch::kBool).to(device).clone();\n"
             "  torch::Tensor t_valid_mask = torch::from_blob(valid_mask.vals_ptr(), {(int64_t)nrows}, torch::kBool).to(device).clone();\n"
@@ -194,6 +206,10 @@ public:
             retarget(*c);
         denseOnMatrixCores(*model.getForward());
         denseOnMatrixCores(*model.getInv());
+        if (!std::getenv("GALA_REFGEN_UNFUSED")) {   // (the unfused spelling: a bit-identity check)
+            fuseGcnChains(*model.getForward());
+            trainRowsAndLoss(preCode, *model.getPostCall());
+        }
         addDumpHook(*model.getPostCall());
         CodeGenerator::writeCode(cmakeCode, outStreamCMake);
         CodeGenerator::writeCode(importCode, outStreamModel);
@@ -229,6 +245,7 @@ private:
         int nsamp = 0;
         for (auto &o : *c->getOpts())
             if (o.first == SAMPLE_COPT || o.first == SAMPLE_DYNAMIC_COPT) nsamp = (int)o.second;
+        if (op == AGGREGATE_MUL_SUM_OP && nsamp == 0) plainAgg_.insert(name + "_AutoGrad");
         std::string fn = "torch::Tensor " + name +
                          "_call(torch::Tensor input_dense, torch::Tensor offset_graph, torch::Tensor columns_graph,\n"
                          "                     torch::Tensor value_graph";
@@ -371,6 +388,163 @@ private:
             }
         }
     }
+
+    // The base emits a GCN layer as torch ops around the aggregation's autograd class:
+    // `res = norm * x;` (ROW_BROADCAST), `res = torch::relu(res);`, the aggregation (an
+    // `if (ep % mod_v == 0)` pair of identical apply calls), `res = norm * res;`
+    // (common.h:928-978, 1150-1184).  On config 5's 11 M rows each such torch op is a 5.7 GB
+    // pass (a ROW_BROADCAST 1.8 ms, a ReLU 2.9 ms, forward and backward alike).  A chain
+    //     [res = act * X;] [res = torch::relu(res);] [res = pre * res;] AGG [res = post * res;]
+    // around an unsampled aggregation becomes the mirror's fused op over the same slot,
+    //     res = gala::gcn_aggregate_relu_apply(X, act, pre, post, li);   (or gcn_aggregate_apply)
+    // whose forward and backward are the unfused chain's roundings bit for bit (the ROW_
+    // BROADCASTs in the aggregation's prologue / epilogue, relu as torch's GPU kernel).
+    // Statements of any other shape are left as they are.
+    struct FwdStmt {
+        enum Kind { Other, Mul, Relu, Agg } kind = Other;
+        std::string text, a, b;  // Mul: a = scale, b = source; Agg: a = class, b = slot index
+    };
+
+    static std::vector<FwdStmt> splitForward(const std::string &t) {
+        static const std::regex mul("^res = (\\w+) \\* (\\w+);$"), relu("^res = torch::relu\\(res\\);$"),
+            app("^res = (\\w+)::apply\\(res, (\\d+)\\);$");
+        std::vector<FwdStmt> out;
+        size_t p = 0;
+        auto trim = [](std::string x) {
+            const size_t a = x.find_first_not_of(" \t\n"), b = x.find_last_not_of(" \t\n");
+            return a == std::string::npos ? std::string() : x.substr(a, b - a + 1);
+        };
+        auto block = [&](size_t open, size_t &close) {  // body of the {...} opening at `open`
+            int depth = 0;
+            for (size_t i = open; i < t.size(); ++i) {
+                if (t[i] == '{') ++depth;
+                if (t[i] == '}' && --depth == 0) {
+                    close = i;
+                    return trim(t.substr(open + 1, i - open - 1));
+                }
+            }
+            close = std::string::npos;
+            return std::string();
+        };
+        const std::string ifkey = "if (ep % mod_v == 0)";
+        while (p < t.size()) {
+            const size_t q = t.find_first_not_of(" \t\n", p);
+            if (q == std::string::npos) {
+                out.push_back({FwdStmt::Other, t.substr(p), "", ""});
+                break;
+            }
+            FwdStmt st;
+            if (t.compare(q, ifkey.size(), ifkey) == 0) {
+                size_t c1 = std::string::npos, c2 = std::string::npos;
+                const size_t o1 = t.find('{', q);
+                const std::string b1 = o1 == std::string::npos ? "" : block(o1, c1);
+                const size_t e = c1 == std::string::npos ? c1 : t.find_first_not_of(" \t\n", c1 + 1);
+                const bool has_else = e != std::string::npos && t.compare(e, 4, "else") == 0;
+                const size_t o2 = has_else ? t.find('{', e) : std::string::npos;
+                const std::string b2 = o2 == std::string::npos ? "" : block(o2, c2);
+                std::smatch m1, m2;
+                if (c2 != std::string::npos && std::regex_match(b1, m1, app) && std::regex_match(b2, m2, app) &&
+                    m1[0] == m2[0]) {
+                    st = {FwdStmt::Agg, t.substr(p, c2 + 1 - p), m1[1], m1[2]};
+                    out.push_back(st);
+                    p = c2 + 1;
+                    continue;
+                }
+            }
+            const size_t semi = t.find(';', q);
+            const size_t end = semi == std::string::npos ? t.size() : semi + 1;
+            st.text = t.substr(p, end - p);
+            const std::string body = trim(st.text);
+            std::smatch m;
+            if (std::regex_match(body, m, mul)) st = {FwdStmt::Mul, st.text, m[1], m[2]};
+            else if (std::regex_match(body, relu)) st = {FwdStmt::Relu, st.text, "", ""};
+            out.push_back(st);
+            p = end;
+        }
+        return out;
+    }
+
+    void fuseGcnChains(Code &fwd) {
+        std::string t;
+        for (int i = 0; i < fwd.getNum(); ++i) t += *fwd.atLine(i) + "\n";
+        std::vector<FwdStmt> st = splitForward(t);
+        std::string out;
+        size_t done = 0;  // statements [0, done) are emitted
+        for (size_t k = 0; k < st.size(); ++k) {
+            if (st[k].kind != FwdStmt::Agg || !plainAgg_.count(st[k].a)) continue;
+            // prologue, walking back: [Mul(act, X)] [Relu] [Mul(pre, res | X)]
+            size_t j = k;
+            std::string X = "res", act, pre, post;
+            bool relu = false;
+            if (j > done && st[j - 1].kind == FwdStmt::Mul) {
+                pre = st[j - 1].a;
+                X = st[j - 1].b;
+                --j;
+            }
+            if (X == "res" && j > done && st[j - 1].kind == FwdStmt::Relu) {
+                relu = true;
+                --j;
+                if (j > done && st[j - 1].kind == FwdStmt::Mul) {
+                    act = st[j - 1].a;
+                    X = st[j - 1].b;
+                    --j;
+                }
+            }
+            size_t last = k;   // epilogue: Mul(post, res)
+            if (k + 1 < st.size() && st[k + 1].kind == FwdStmt::Mul && st[k + 1].b == "res") {
+                post = st[k + 1].a;
+                last = k + 1;
+            }
+            if (!relu && pre.empty() && post.empty()) continue;   // nothing to fuse: as emitted
+            for (size_t i = done; i < j; ++i) out += st[i].text;
+            const std::string none = "torch::Tensor()";
+            auto arg = [&](const std::string &v) { return v.empty() ? none : v; };
+            out += "\n        // ROW_BROADCAST / RELU / AGGREGATE / ROW_BROADCAST fused (HIPGenerator)\n";
+            if (relu)
+                out += "        res = gala::gcn_aggregate_relu_apply(" + X + ", " + arg(act) + ", " + arg(pre) + ", " +
+                       arg(post) + ", " + st[k].b + ");";
+            else
+                out += "        res = gala::gcn_aggregate_apply(" + X + ", " + arg(pre) + ", " + arg(post) + ", " +
+                       st[k].b + ");";
+            done = last + 1;
+            k = last;
+        }
+        for (size_t i = done; i < st.size(); ++i) out += st[i].text;
+        *fwd.atLine(0) = out;
+        for (int i = 1; i < fwd.getNum(); ++i) fwd.atLine(i)->clear();
+    }
+
+    // The training loop's loss (common.h:1506-1560): the training rows by index_select over
+    // the mask's row list (computed once) instead of boolean indexing -- the same rows in the
+    // same order, and the backward scatters one gradient per row either way -- and the
+    // CrossEntropyLoss (mean) as log_softmax + gather + mean: the same prediction and
+    // gradients bit for bit (d loss / d pred = -1/n at the label, then log_softmax's
+    // backward); the loss value is the same sum taken in another order.  torch's
+    // nll_loss_forward_reduce kernel reduces in one workgroup: 7.9 ms per epoch at config 5's
+    // 3.3 M training rows (profiles/r04_refgen_config5_kernels.txt), its backward 5.4 ms.
+    void trainRowsAndLoss(Code &pre, Code &post) {
+        bool used = false;
+        for (int i = 0; i < post.getNum(); ++i) {
+            std::string *l = post.atLine(i);
+            const size_t n0 = l->size();
+            replaceAll(*l, "prediction.index({t_train_mask})", "prediction.index_select(0, gala_train_rows)");
+            replaceAll(*l, "t_labs.index({t_train_mask})", "t_labs.index_select(0, gala_train_rows)");
+            replaceAll(*l, "auto criterion = torch::nn::CrossEntropyLoss();", "");
+            replaceAll(*l, "criterion(prediction_train, labels_train)", "gala_cross_entropy(prediction_train, labels_train)");
+            used = used || l->size() != n0 || l->find("gala_train_rows") != std::string::npos;
+        }
+        if (!used) return;
+        std::string rows = "  // the training rows, once (the loop's index_select)\n"
+                           "  torch::Tensor gala_train_rows = t_train_mask.nonzero().reshape({-1});\n";
+        pre.addCode(rows);
+        std::string ce = "// CrossEntropyLoss (mean) as log_softmax + gather + mean\n"
+                         "static torch::Tensor gala_cross_entropy(const torch::Tensor &pred, const torch::Tensor &labels) {\n"
+                         "  return -torch::log_softmax(pred, 1).gather(1, labels.reshape({-1, 1})).mean();\n"
+                         "}";
+        kernelCode.addCode(ce);
+    }
+
+    std::unordered_set<std::string> plainAgg_;   // autograd classes of unsampled aggregations
 
     // after the loop's `prediction = net->forward(...)[0];`, and before its first
     // `optimizer.step();` (common.h:1506-1560)

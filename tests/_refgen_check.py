@@ -57,12 +57,15 @@ def dataset(root, n=600, nnz=2400, feat=64, labels=7, seed=3):
     return d, X
 
 
-def run_program(exe, root, device, timeout=300):
-    """Run an emitted program from root/run/b on `device` ("cpu" or "cuda"); its dump."""
+def run_program(exe, root, device, timeout=300, seed=None):
+    """Run an emitted program from root/run/b on `device` ("cpu" or "cuda"); its dump.
+    seed: GALA_SEED (the same initial weights in every run)."""
     cwd = os.path.join(root, "run", "b")
-    os.makedirs(cwd)
+    os.makedirs(cwd, exist_ok=True)
     dump = os.path.join(root, "dump.bin")
     env = dict(os.environ, GALA_DEVICE=device, GALA_DUMP=dump, OMP_NUM_THREADS="2")
+    if seed is not None:
+        env["GALA_SEED"] = str(seed)
     r = subprocess.run([exe], cwd=cwd, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return read_dump(dump)

@@ -34,3 +34,29 @@ def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     # 20 000 rows: the GAT attention-bias gradients' cancellation noise is ~5e-8 against a
     # 1.5e-2 largest gradient (the same on the host backend), hence the 1e-5 floor
     rc.check_against_galac(model, dump, d, X, tmp_path / "ir.json", noise_floor=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("model", ["gcn3", "gcn3_papers"])
+def test_fused_gcn_chains_bit_identical_to_the_base_spelling(tmp_path, model):
+    """HIPGenerator's fused GCN chains (gcn_aggregate[_relu]_apply in place of the base's torch
+    ROW_BROADCAST / ReLU ops around the aggregation, common.h:928-978,1150-1184) and its loss
+    spelling (index_select + log_softmax / gather / mean for boolean indexing +
+    CrossEntropyLoss): the first epoch's prediction and every weight gradient equal the
+    unfused program's (GALA_REFGEN_UNFUSED) bit for bit; the loss is the same sum in another
+    order."""
+    import numpy as np
+    exe, exe0 = (os.path.join(BIN, "gala_" + m) for m in (model, model + "_unfused"))
+    if not (os.path.exists(exe) and os.path.exists(exe0)):
+        pytest.skip("refgen programs not built (refgen/build.py needs the reference's sources)")
+    feat, labels = (128, 172) if model == "gcn3_papers" else (64, 7)
+    rc.dataset(tmp_path, n=20000, nnz=240000, feat=feat, labels=labels, seed=11)
+    d1 = rc.run_program(exe, str(tmp_path), "cuda", seed=7)
+    d0 = rc.run_program(exe0, str(tmp_path), "cuda", seed=7)
+    assert set(d1) == set(d0)
+    for k in d0:
+        if k == "loss":
+            np.testing.assert_allclose(d1[k], d0[k], rtol=1e-6, atol=0)
+        else:
+            np.testing.assert_array_equal(d1[k], d0[k], err_msg=k)

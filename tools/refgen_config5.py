@@ -12,6 +12,7 @@ executor on the weights the program dumped.  Measurement; prints one JSON line p
 """
 import json
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -79,12 +80,28 @@ def main():
     if p.returncode != 0:
         say(stage="program", rc=p.returncode, stderr=err[-2000:])
         return 1
-    import re
     last = [ln for ln in out.splitlines() if re.fullmatch(r"[0-9.e+-]+,[0-9.e+-]+", ln.strip())][-1].strip()
     fwd_s, total_s = (float(v) for v in last.split(","))
     dump = rc.read_dump(dump_path)
     say(stage="program", epochs=10, wall_s=round(time.time() - t0, 1), fwd_mean_s=fwd_s,
         epoch_mean_s=total_s, timing_line=last, loss_first=float(dump["loss"][0]))
+
+    # galac's programs on the same dataset: the same DSL and passes (tests/dsl/
+    # gcn3_papers_ref_codegen.txt: gala_inference's operator reordering, no code motion, no
+    # training subgraph) and galac's defaults (bench/dsl/gcn3_papers10.txt: code motion hoists
+    # the first aggregation out of the loop)
+    for prog in ("gcn3_papers_ref_codegen", "gcn3_papers10"):
+        pexe = os.path.join(PKG, "progs", prog, "gala_prog")
+        if not os.path.exists(pexe) or device != "cuda":
+            continue
+        r = subprocess.run([pexe, "--data", d + "/", "--iters", "10"], capture_output=True, text=True, timeout=600)
+        line = (r.stdout.strip().splitlines() or [""])[-1].strip()
+        rec = {"stage": "galac", "program": prog, "rc": r.returncode, "timing_line": line}
+        if r.returncode == 0 and re.fullmatch(r"[0-9.e+-]+,[0-9.e+-]+", line):
+            rec["fwd_mean_s"], rec["epoch_mean_s"] = (float(v) for v in line.split(","))
+        else:
+            rec["stderr"] = r.stderr[-1500:]
+        say(**rec)
 
     # galac's program of the same DSL, forward in float64 on the dumped weights
     t0 = time.time()
