@@ -12,7 +12,9 @@
 // Forward layout: HW = D / VEC lanes per (row, head) pair (a power of two up to 64), each
 // lane one VEC-wide slice, so a wave reads 64 consecutive vectors (contiguous rows);
 // the pair's dot is each lane's fma chain over its slice, then an xor butterfly over the
-// HW lanes (deterministic).  Other head widths: one thread per pair, a sequential chain.
+// HW lanes (deterministic); a head width that is no power of two of vectors (D = 47) takes
+// the next power of two of lanes, the ones past D idle.  Wider heads: one thread per pair, a
+// sequential chain.
 // Backward: one thread per VEC-wide vector of dX, consecutive threads on consecutive
 // vectors (full-line stores).
 #include "gala_internal.h"
@@ -37,14 +39,16 @@ __global__ __launch_bounds__(kBlock) void k_head_attn_group(int64_t n_rows, int3
     if (pair >= n_rows * H) return;  // whole groups leave together
     const int64_t r = pair / H;
     const int h = (int)(pair - r * H);
-    const int64_t c = (int64_t)h * D + gl * VEC;
+    // lanes past the head's D / VEC vectors (HW rounded up to a power of two) add nothing
+    const bool live = gl * VEC < D;
+    const int64_t c = (int64_t)h * D + (live ? gl * VEC : 0);
     const V x = *reinterpret_cast<const V *>(X + r * ldx + c);
     const V v = *reinterpret_cast<const V *>(w + c);
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < VEC; ++i)
         acc = fmaf(reinterpret_cast<const float *>(&x)[i], reinterpret_cast<const float *>(&v)[i], acc);
-    acc = group_sum<HW>(acc);
+    acc = group_sum<HW>(live ? acc : 0.0f);
     if (gl == 0) out[pair] = b ? __fadd_rn(acc, b[h]) : acc;
 }
 
@@ -115,8 +119,9 @@ extern "C" int gala_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, cons
     const int vec = attn_vec(D, {ldx}, {X, w});
     const int64_t total = n_rows * heads;
     hipStream_t hs = (hipStream_t)stream;
-    const int hw = D / vec;
-    if (hw <= 64 && (hw & (hw - 1)) == 0) {  // lanes per head: a power of two
+    int hw = 1;   // lanes per head: D / vec rounded up to a power of two (D = 47: 64 lanes, 47 live)
+    while (hw < D / vec) hw <<= 1;
+    if (hw <= 64) {
         const unsigned gb = (unsigned)((total * hw + kBlock - 1) / kBlock);
 #define GALA_ATTN_GROUP(V, W) hipLaunchKernelGGL((k_head_attn_group<V, W>), dim3(gb), dim3(kBlock), 0, hs, n_rows, heads, D, X, ldx, w, b, out)
 #define GALA_ATTN_HW(V)                                      \

@@ -32,6 +32,9 @@ PROGRAMS = {
     # the data-sampled GCN of tests/GALA-DSL/ablations/sampling/data: G.sample(3), one tile
     "gcn_dsample": ["64", "7", "32", "3", "2", "10000000", "0", "3"],
     "gat": ["64", "7", "32", "3", "2", "5000"],
+    # config 3's single-head drop-in shape (tests/GALA-DSL/gat/Products/h100.txt: F 100, hidden 32,
+    # 47 labels, col_tile(10000000)), 10 epochs, for tools/refgen_gat_products.py
+    "gat_products": ["100", "47", "32", "10", "2", "10000000"],
     "gin": ["64", "7", "32", "3", "2"],
     "gin_motion": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],

@@ -364,11 +364,18 @@ private:
     // backward takes dW = dYᵀX as one library GEMM whose only parallelism is the 128x128
     // output (K = the 11 M rows of config 5: 12.0 ms per call on MI355X, 5.0 ms here;
     // profiles/r04_refgen_config5_kernels.txt).
-    // The attention Linears (efcN, one output per head) stay as they are.
+    // The attention Linears (`efcN->forward(x)`, Linear(hs, 1): attnL / attnR of the GAT
+    // layer, common.h:1248-1260) run as the mirror's head-attention op with one head over the
+    // same parameters (gala_head_attn_f32 / _bwd_f32, the weight gradient on
+    // gala_dense_grad_f32): torch's Linear(32, 1) forward is a hipBLASLt GEMM with a 32 x 1
+    // tile, 2.2 ms per call at 2.4 M rows for 313 MB read (profiles/
+    // r05_refgen_gat_products_kernels.csv), and its backward three more such GEMMs.  The
+    // attention logits are the same dot products summed in another order (the reference's
+    // BLAS order is not pinned either).
     static void denseOnMatrixCores(Code &code) {
         for (int i = 0; i < code.getNum(); ++i) {
             std::string *l = code.atLine(i);
-            for (const std::string pre : {"sfc", "fc"}) {
+            for (const std::string pre : {"efc", "sfc", "fc"}) {
                 for (size_t p = l->find(pre); p != std::string::npos; p = l->find(pre, p + 1)) {
                     if (p > 0 && (std::isalnum((unsigned char)(*l)[p - 1]) || (*l)[p - 1] == '_')) continue;
                     size_t q = p + pre.size();
@@ -383,7 +390,8 @@ private:
                     }
                     if (e >= l->size()) continue;
                     const std::string arg = l->substr(a, e - a);
-                    l->replace(p, e + 1 - p, "gala::ffn_apply(" + arg + ", " + mod + "->weight, " + mod + "->bias)");
+                    const std::string fn = pre == "efc" ? "gala::head_attn_apply(" : "gala::ffn_apply(";
+                    l->replace(p, e + 1 - p, fn + arg + ", " + mod + "->weight, " + mod + "->bias)");
                 }
             }
         }

@@ -1029,8 +1029,8 @@ def test_gat_row_stats_rejects_bad_arguments():
 @pytest.mark.parametrize("F,heads", [(256, 8), (47, 1), (64, 4), (24, 3), (100, 1)])
 def test_head_attn(F, heads):
     """gala_head_attn_f32 within fp32 rounding of the CPU twin's sequential chain (lane
-    chains + a butterfly; F = 47 and 100 take the one-thread-per-head kernel, bit-equal);
-    its backward bit-exact against float32 numpy (one product, one sum)."""
+    chains + a butterfly; F = 47 and 100 on a power of two of lanes with the ones past D
+    idle); its backward bit-exact against float32 numpy (one product, one sum)."""
     N = 3001
     X = features(N, F, seed=71)
     w = features(1, F, seed=72).ravel()
@@ -1040,8 +1040,6 @@ def test_head_attn(F, heads):
     ref = np.empty((N, heads), np.float32)
     _abi.call_cpu("gala_head_attn_f32", N, F, heads, X.ctypes.data, F, w.ctypes.data, b.ctypes.data,
                   ref.ctypes.data, None)
-    if F in (47, 100):  # head widths without a power-of-two lane count: the sequential chain
-        assert np.array_equal(host(out), ref)
     np.testing.assert_allclose(host(out), ref, rtol=1e-5, atol=1e-5)
     g = features(N, heads, seed=74)
     m = np.repeat(g, D, axis=1) * w[None, :]

@@ -117,7 +117,9 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         assert fwd.index("gala::ffn_apply(t_iden_n, fc0->weight, fc0->bias)") < fwd.index("sfc0->weight")
     else:
         # the edge chain of each layer: attention Linears, edge sum, LeakyReLU, softmax, aggregation
-        for a, b in (("efc0->forward", "aggregate_edge_sum_AutoGrad::apply"),
+        # (the attention Linears as the mirror's head-attention op)
+        assert "efc0->forward" not in src and "gala::head_attn_apply(" in fwd
+        for a, b in (("head_attn_apply(", "aggregate_edge_sum_AutoGrad::apply"),
                      ("aggregate_edge_sum_AutoGrad::apply", "leaky_relu->forward"),
                      ("leaky_relu->forward", "non_lnr_op_softmax_AutoGrad::apply"),
                      ("non_lnr_op_softmax_AutoGrad::apply", "aggregate_node_mul_sum_coarse2_AutoGrad::apply(res, attn")):
