@@ -61,6 +61,9 @@ extern "C" int gala_cpu_spmm_f32(const gala_csr_t *A, const float *X, int64_t ld
     return gala_cpu_spmm_ex_f32(A, X, ldx, Y, ldy, F, src_scale, dst_scale, flags, nsamp, ra, rb, nullptr, stream);
 }
 
+// torch.relu as its GPU kernel computes it (the HIP backend's relu_t): t > 0 ? t : +0, NaN passes
+static inline float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
+
 // (every row is one sequential pass here: GALA_SPMM_HUB_CHUNKED is accepted and gives the
 // REF-order result, which is within that mode's tolerance)
 extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx, float *Y,
@@ -79,6 +82,16 @@ extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t
     const float *y2s = Y2 ? epi->y2_scale : nullptr;
     if (dst_deg && (dst_scale || A->n_seg != 1 || A->val || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
     if (Y2 && ldy2 < F) return GALA_ERR_INVALID_ARG;
+    const bool relu_pro = epi && epi->src_relu;
+    const float *src_act = relu_pro ? epi->src_act : nullptr;
+    const float *relu_x = epi ? epi->relu_x : nullptr;
+    const int64_t ldrx = relu_x ? epi->ldrx : 0;
+    const float *relu_act = relu_x ? epi->relu_act : nullptr;
+    if (epi && epi->src_act && !relu_pro) return GALA_ERR_INVALID_ARG;
+    if (relu_x && ldrx < F) return GALA_ERR_INVALID_ARG;
+    if ((relu_pro || relu_x) &&
+        (A->val || (flags & GALA_SPMM_SAMPLE) || Y2 || (A->split && A->split->n_rows_split > 0)))
+        return GALA_ERR_UNSUPPORTED;
     if (A->n_rows == 0 || F == 0) return GALA_OK;
     if (!Y || (!X && A->nnz > 0)) return GALA_ERR_INVALID_ARG;
     const bool samp = (flags & GALA_SPMM_SAMPLE) != 0;
@@ -119,6 +132,15 @@ extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t
                             else
                                 for (int32_t f = h * D; f < (h + 1) * D; ++f) a[f] = fmaf(wv, xr[f], a[f]);
                         }
+                    } else if (relu_pro) {  // the next layer's prologue: sc * relu(act * x)
+                        const float ac = src_act ? src_act[c] : 1.0f;
+                        for (int32_t f = 0; f < F; ++f) {
+                            float t = xr[f];
+                            if (src_act) t = ac * t;
+                            t = relu_t(t);
+                            if (src_scale) t = sc * t;
+                            a[f] = a[f] + t;
+                        }
                     } else if (src_scale) {
                         for (int32_t f = 0; f < F; ++f) a[f] = a[f] + sc * xr[f];
                     } else {
@@ -135,6 +157,16 @@ extern "C" int gala_cpu_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t
                     for (int32_t f = 0; f < F; ++f) yr[f] = ds * a[f];
             } else {
                 memcpy(yr, a, sizeof(float) * (size_t)F);
+            }
+            if (relu_x) {  // the ReLU backward of the layer's input (gala_cpu_relu_scale_backward_f32)
+                const float ra_ = relu_act ? relu_act[r] : 1.0f;
+                for (int32_t f = 0; f < F; ++f) {
+                    float t = relu_x[r * ldrx + f];
+                    if (relu_act) t = ra_ * t;
+                    float d = relu_t(t) <= 0.0f ? 0.0f : yr[f];
+                    if (relu_act) d = d * ra_;
+                    yr[f] = d;
+                }
             }
             if (Y2) {  // the next aggregation's pre-scaled input
                 const float s2 = y2s ? y2s[r] : ds;
@@ -207,9 +239,6 @@ extern "C" int gala_cpu_row_broadcast_deg_f32(const gala_csr_t *A, int32_t F, co
     }
     return GALA_OK;
 }
-
-// torch.relu as its GPU kernel computes it (the HIP backend's relu_t): t > 0 ? t : +0, NaN passes
-static inline float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
 
 extern "C" int gala_cpu_row_scale_relu_f32(int64_t n_rows, int32_t F, const float *act,
                                            const float *pre, const float *X, int64_t ldx,

@@ -59,8 +59,19 @@ struct SpmmParams {
     float *Y2;                // nullable epilogue output: Y2[r] = s2[r] * Y[r]
     int64_t ldy2;
     const float *y2_scale;    // s2 (NULL: the dst factor)
+    // ABI 4 epilogue fields (gala_spmm_epilogue_t): the ReLU prologue's act (RELU kernels:
+    // the gathered source is src_scale[c] * relu(src_act[c] * X[c])), and the ReLU-backward
+    // epilogue (relu_x != NULL: Y[r] = relu_act[r] * (relu(relu_act[r] * relu_x[r]) <= 0 ? 0 : Y[r]))
+    int32_t relu_prologue;
+    const float *src_act;
+    const float *relu_x;
+    int64_t ldrx;
+    const float *relu_act;
     SegTable seg;
 };
+
+// torch.relu as its GPU kernel computes it: t > 0 ? t : +0, NaN passes
+__device__ __forceinline__ float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
 
 // GCN norm deg^-0.5 of a row count: the expression of k_degree_count (power -0.5), so an
 // in-kernel norm is bit-identical to the degree pass's
@@ -90,18 +101,22 @@ __device__ __forceinline__ float &el(typename VecT<VEC>::T &v, int i) {
 
 // acc (+)= w * (s * x), reference rounding:  s*x is the torch `norm * res` product
 // (rounded), `local + A*B` is contracted to fma by nvcc (cuda.h:335-342).
-template <int VEC, bool W, bool SRCS>
+// RELU: the next layer's ReLU prologue on the gathered element, v = s * relu(a * x) with the
+// roundings of gala_row_scale_relu_f32 (a, s = 1.0f when absent: exact)
+template <int VEC, bool W, bool SRCS, bool RELU = false>
 __device__ __forceinline__ void accumulate(typename VecT<VEC>::T &acc,
-                                           const typename VecT<VEC>::T &x, float w, float s) {
+                                           const typename VecT<VEC>::T &x, float w, float s,
+                                           float a = 1.0f) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
         float v = reinterpret_cast<const float *>(&x)[i];
+        if (RELU) v = relu_t(__fmul_rn(a, v));
         if (SRCS) v = __fmul_rn(s, v);
-        float &a = el<VEC>(acc, i);
+        float &r = el<VEC>(acc, i);
         if (W)
-            a = fmaf(w, v, a);
+            r = fmaf(w, v, r);
         else
-            a = __fadd_rn(a, v);
+            r = __fadd_rn(r, v);
     }
 }
 
@@ -140,7 +155,7 @@ __device__ __forceinline__ void stv_n(float *p, const typename VecT<VEC>::T &v, 
 
 // acc += the edges [e0, e1) of one row (or nsamp kernel samples), sequentially in CSR
 // order; the loads of U edges are issued before the first add of the batch.
-template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols<VEC, G, CH, W> &cl,
                                                  int64_t row, int64_t e0, int64_t e1,
                                                  typename VecT<VEC>::T (&acc)[CH]) {
@@ -156,7 +171,7 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
         int32_t c[U];
         V x[U][CH];
         float w[U][CH];
-        float sc[U];
+        float sc[U], sa[U];
         // one row per wave (G = 64): a batch's columns are wave-uniform, so one coalesced
         // load of U columns is spread to scalar registers (v_readlane) and the X row
         // addresses are formed on the scalar unit instead of per lane
@@ -189,12 +204,14 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
 #pragma unroll
             for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + cl.off[ch]);
             sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
+            sa[k] = (RELU && p.src_act) ? p.src_act[c[k]] : 1.0f;
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
             if (j0 + k < n) {
 #pragma unroll
-                for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
+                for (int ch = 0; ch < CH; ++ch)
+                    accumulate<VEC, W, SRCS, RELU>(acc[ch], x[k][ch], w[k][ch], sc[k], sa[k]);
             }
         }
     }
@@ -207,7 +224,7 @@ __device__ __forceinline__ void accumulate_range(const SpmmParams &p, const Cols
 // loop paid rowptr -> col -> X as three dependent misses per segment (12 segments: 11 ms
 // per F = 128 call), here it is one of each per batch of U edges.
 constexpr int kSegGroup = 8;
-template <int VEC, int G, int CH, int U, bool W, bool SRCS>
+template <int VEC, int G, int CH, int U, bool W, bool SRCS, bool RELU = false>
 __device__ __forceinline__ void accumulate_segments(const SpmmParams &p, KernargSegPtr seg, const Cols<VEC, G, CH, W> &cl,
                                                     int64_t row, typename VecT<VEC>::T (&acc)[CH]) {
     typedef typename VecT<VEC>::T V;
@@ -233,7 +250,7 @@ __device__ __forceinline__ void accumulate_segments(const SpmmParams &p, Kernarg
             int32_t c[U];
             V x[U][CH];
             float w[U][CH];
-            float sc[U];
+            float sc[U], sa[U];
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const int32_t j = (j0 + k < n) ? j0 + k : n - 1;  // clamped: valid address
@@ -257,12 +274,14 @@ __device__ __forceinline__ void accumulate_segments(const SpmmParams &p, Kernarg
 #pragma unroll
                 for (int ch = 0; ch < CH; ++ch) x[k][ch] = ldv<VEC>(xr + cl.off[ch]);
                 sc[k] = SRCS ? p.src_scale[c[k]] : 1.0f;
+                sa[k] = (RELU && p.src_act) ? p.src_act[c[k]] : 1.0f;
             }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 if (j0 + k < n) {
 #pragma unroll
-                    for (int ch = 0; ch < CH; ++ch) accumulate<VEC, W, SRCS>(acc[ch], x[k][ch], w[k][ch], sc[k]);
+                    for (int ch = 0; ch < CH; ++ch)
+                        accumulate<VEC, W, SRCS, RELU>(acc[ch], x[k][ch], w[k][ch], sc[k], sa[k]);
                 }
             }
         }
@@ -300,6 +319,18 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
                 for (int i = 0; i < VEC; ++i) el<VEC>(out, i) = __fadd_rn(el<VEC>(y, i), el<VEC>(out, i));
             }
         }
+        if (p.relu_x) {  // the ReLU backward of the layer's input: gala_relu_scale_backward_f32's roundings
+            const float a = p.relu_act ? p.relu_act[row] : 1.0f;
+            V xv = ldv<VEC>(p.relu_x + row * p.ldrx + cl.off[ch]);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+                float t = el<VEC>(xv, i);
+                if (p.relu_act) t = __fmul_rn(a, t);
+                float d = relu_t(t) <= 0.0f ? 0.0f : el<VEC>(out, i);
+                if (p.relu_act) d = __fmul_rn(d, a);
+                el<VEC>(out, i) = d;
+            }
+        }
         stv_n<VEC>(yp, out, cl.nv[ch]);
         if (p.Y2) {  // the next aggregation's pre-scaled input, s2 * Y (its ROW_BROADCAST rounding)
 #pragma unroll
@@ -310,7 +341,7 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
 }
 
 // the rows of row block `bid` of `nb` (skipping hub rows)
-template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 __device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid, int64_t nb) {
     typedef typename VecT<VEC>::T V;
     constexpr int RPW = kWave / G;
@@ -330,21 +361,21 @@ __device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid,
     const int64_t rp_stride = p.n_rows + 1;
     const int nseg = p.seg.n;
     if (!SAMP && nseg > 1) {
-        accumulate_segments<VEC, G, CH, U, W, SRCS>(p, seg, cl, row, acc);
+        accumulate_segments<VEC, G, CH, U, W, SRCS, RELU>(p, seg, cl, row, acc);
         store_row<VEC, G, CH, W>(p, cl, row, acc);
         return;
     }
     for (int s = 0; s < nseg; ++s) {
         const int32_t *rp = p.rowptr + (int64_t)seg->rp[s] * rp_stride;
         const int64_t base = seg->base[s];
-        accumulate_range<VEC, G, CH, U, W, SAMP, SRCS>(p, cl, row, base + rp[row], base + rp[row + 1], acc);
+        accumulate_range<VEC, G, CH, U, W, SAMP, SRCS, RELU>(p, cl, row, base + rp[row], base + rp[row + 1], acc);
     }
     store_row<VEC, G, CH, W>(p, cl, row, acc);
 }
 
-template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
-    spmm_row_block<VEC, G, CH, U, W, SAMP, SRCS>(p, blockIdx.x, gridDim.x);
+    spmm_row_block<VEC, G, CH, U, W, SAMP, SRCS, RELU>(p, blockIdx.x, gridDim.x);
 }
 
 // ---- split rows: chunk partials + ordered fix-up ---------------------------------------
@@ -709,14 +740,15 @@ __global__ __launch_bounds__(kBlock) void k_degree_weighted(DegParams p) {
 }
 
 // ---- dispatch ---------------------------------------------------------------------------
-template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS>
+template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
     constexpr int rows_per_block = (kBlock / kWave) * (kWave / G);
     const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
-    if (SAMP || !sp || sp->n_chunks <= 0) {
-        hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS>), dim3((unsigned)blocks),
+    if (RELU || SAMP || !sp || sp->n_chunks <= 0) {   // (the ReLU prologue: no hub split, host-checked)
+        hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS, RELU>), dim3((unsigned)blocks),
                            dim3(kBlock), 0, st, p);
     }
+    if constexpr (!RELU)
     if (!SAMP && sp && sp->n_chunks > 0) {
         const int64_t cb = (sp->n_chunks + rows_per_block - 1) / rows_per_block;
         hipLaunchKernelGGL((k_spmm_rows_chunks<VEC, G, CH, U, W, SRCS>), dim3((unsigned)(cb + blocks)),
@@ -761,19 +793,24 @@ static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w
 #undef GALA_HUB
 }
 
-template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS>
+template <int VEC, int G, int CH, bool W, bool SAMP, bool SRCS, bool RELU = false>
 static void launch_rg(const SpmmParams &p, const SplitParams *sp, hipStream_t st) {
     // U: edges whose loads are in flight before the first add (per lane: U*CH vectors).
     // Measured on the Products shape (tools/spmm_sweep.py, uniform and R-MAT graphs):
     // 8 or 16 lanes per row (F = 32, 64) are fastest with 4 edges in flight (F = 32: 2.44
     // vs 2.60 ms at 8); narrower and wider rows keep 8.
     constexpr int U = (CH * VEC >= 16) ? 2 : (CH * VEC >= 8) ? 4 : (VEC == 4 && (G == 8 || G == 16)) ? 4 : 8;
-    launch_rg_u<VEC, G, CH, U, W, SAMP, SRCS>(p, sp, st);
+    launch_rg_u<VEC, G, CH, U, W, SAMP, SRCS, RELU>(p, sp, st);
 }
 
 template <int VEC, int G, int CH>
 static void launch_flags(const SpmmParams &p, const SplitParams *sp, bool w, bool samp, bool srcs,
                          hipStream_t st) {
+    if (p.src_act || p.relu_prologue) {   // the ReLU prologue: unweighted, unsampled (host-checked)
+        if (srcs) launch_rg<VEC, G, CH, false, false, true, true>(p, sp, st);
+        else launch_rg<VEC, G, CH, false, false, false, true>(p, sp, st);
+        return;
+    }
     if (w) {
         if (samp) {
             if (srcs) launch_rg<VEC, G, CH, true, true, true>(p, sp, st);
@@ -864,6 +901,14 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
     const bool dst_deg = epi && epi->dst_deg_rsqrt;
     float *Y2 = epi ? epi->Y2 : nullptr;
     const int64_t ldy2 = Y2 ? epi->ldy2 : 0;
+    const bool relu_pro = epi && epi->src_relu;
+    const float *relu_x = epi ? epi->relu_x : nullptr;
+    const int64_t ldrx = relu_x ? epi->ldrx : 0;
+    if (epi && epi->src_act && !relu_pro) return GALA_ERR_INVALID_ARG;
+    if (relu_x && ldrx < F) return GALA_ERR_INVALID_ARG;
+    if ((relu_pro || relu_x) &&
+        (A->val || (flags & GALA_SPMM_SAMPLE) || Y2 || (A->split && A->split->n_rows_split > 0)))
+        return GALA_ERR_UNSUPPORTED;
     // the deg norm is the unweighted degree (rowptr counts): refused on weighted graphs, whose
     // degree pass sums the values (k_degree_weighted)
     if (dst_deg && (dst_scale || A->n_seg != 1 || A->val || (flags & GALA_SPMM_SAMPLE))) return GALA_ERR_UNSUPPORTED;
@@ -910,7 +955,8 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         const int64_t wcols = Fv < 512LL * v ? Fv : 512LL * v;
         const bool ws_ok = !use_split || (plan->ws_cols % v == 0 && plan->ws_cols >= wcols);
         const bool y2_ok = !Y2 || (ldy2 % v == 0 && ((uintptr_t)Y2 % (4 * v)) == 0 && (F % v == 0 || ldy2 >= Fv));
-        return fits && ws_ok && y2_ok && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
+        const bool rx_ok = !relu_x || (ldrx % v == 0 && ((uintptr_t)relu_x % (4 * v)) == 0 && (F % v == 0 || ldrx >= Fv));
+        return fits && ws_ok && y2_ok && rx_ok && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)X % (4 * v)) == 0 &&
                ((uintptr_t)Y % (4 * v)) == 0;
     };
     while (vec > 1 && !ok(vec)) vec >>= 1;
@@ -938,6 +984,11 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
     p.Y2 = Y2;
     p.ldy2 = ldy2;
     p.y2_scale = Y2 ? epi->y2_scale : nullptr;
+    p.relu_prologue = relu_pro ? 1 : 0;
+    p.src_act = relu_pro ? epi->src_act : nullptr;
+    p.relu_x = relu_x;
+    p.ldrx = ldrx;
+    p.relu_act = relu_x ? epi->relu_act : nullptr;
     p.row_order = nullptr;
     p.xcd_order = 1;  // off below when a degree-ordered row schedule is used (heavy rows first)
     hipStream_t hs = (hipStream_t)stream;
@@ -992,6 +1043,7 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             q.X = X ? X + c0 : nullptr;
             q.Y = Y + c0;
             q.Y2 = Y2 ? Y2 + c0 : nullptr;
+            q.relu_x = relu_x ? relu_x + c0 : nullptr;
             q.F = Fc;
             q.accum = accum;
             const int L = (int)((Fc + vec - 1) / vec);
@@ -1084,7 +1136,7 @@ struct RowBroadcastOp {
 };
 
 // torch.relu as its GPU kernel computes it: t > 0 ? t : +0, NaN passes through
-__device__ __forceinline__ float relu_t(float t) { return (t > 0.0f || t != t) ? t : 0.0f; }
+
 
 // Y[r,:] = pre[r] * relu(act[r] * X[r,:]), each factor optional (absent: no rounding step)
 struct ScaleReluOp {

@@ -56,6 +56,11 @@ class gala_spmm_epilogue_t(ctypes.Structure):
         ("Y2", ctypes.c_void_p),
         ("ldy2", ctypes.c_int64),
         ("y2_scale", ctypes.c_void_p),
+        ("src_relu", ctypes.c_int32),
+        ("src_act", ctypes.c_void_p),
+        ("relu_x", ctypes.c_void_p),
+        ("ldrx", ctypes.c_int64),
+        ("relu_act", ctypes.c_void_p),
     ]
 
 
@@ -163,7 +168,7 @@ class GalaError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 3  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
+ABI_VERSION = 4  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
 
 
 def lib() -> ctypes.CDLL:

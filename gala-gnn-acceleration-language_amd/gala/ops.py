@@ -170,13 +170,18 @@ def _rows_like(X: torch.Tensor, n_rows: int, zero: bool = False) -> torch.Tensor
 
 def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=None,
          accum=False, nsamp=None, ra=5, rb=7, exact=False, hub="exact", dst_deg=False, out2=None,
-         out2_scale=None) -> torch.Tensor:
+         out2_scale=None, src_relu=False, src_act=None, relu_x=None, relu_act=None) -> torch.Tensor:
     """Y (+)= dst_scale * A (src_scale * X) (gala_spmm_f32).  hub: how the rows of the
     graph's hub-row plan are summed -- "exact" (default, the reference's sequential CSR
     order, bit-identical) or "chunked" (GALA_SPMM_HUB_CHUNKED: 512-edge chunk partials and
     an ordered fix-up, the fast mode within fp32 summation rounding).  Epilogue
     (gala_spmm_ex_f32): dst_deg -- the dst factor is deg(r)^-0.5 from the rowptr; out2 --
-    also out2 = out2_scale (or the dst factor) * Y, the next aggregation's pre-scaled input."""
+    also out2 = out2_scale (or the dst factor) * Y, the next aggregation's pre-scaled input;
+    src_relu -- the gathered source is src_scale * relu(src_act * X) (the next layer's ReLU
+    prologue, gala_row_scale_relu_f32's roundings); relu_x -- the ReLU backward of the layer's
+    input on the result, Y = relu_act * (relu(relu_act * relu_x) <= 0 ? 0 : Y)
+    (gala_relu_scale_backward_f32's roundings).  The ReLU fields need an unweighted, unsampled
+    graph without hub rows (else GalaError UNSUPPORTED)."""
     F = X.shape[1]
     if out is None:
         out = _rows_like(X, g.n_rows, zero=accum)
@@ -185,11 +190,14 @@ def spmm(g: DeviceGraph, X: torch.Tensor, src_scale=None, dst_scale=None, out=No
     chunked = hub == "chunked" and not exact
     flags = ((_abi.GALA_SPMM_ACCUM if accum else 0) | (_abi.GALA_SPMM_SAMPLE if nsamp is not None else 0)
              | (_abi.GALA_SPMM_EXACT if exact else 0) | (_abi.GALA_SPMM_HUB_CHUNKED if chunked else 0))
-    if dst_deg or out2 is not None:
+    if dst_deg or out2 is not None or src_relu or relu_x is not None:
         epi = _abi.gala_spmm_epilogue_t()
         epi.dst_deg_rsqrt = int(bool(dst_deg))
         epi.Y2, epi.ldy2 = _dp(out2), (out2.stride(0) if out2 is not None else 0)
         epi.y2_scale = _dp(out2_scale)
+        epi.src_relu, epi.src_act = int(bool(src_relu)), _dp(src_act)
+        epi.relu_x, epi.ldrx = _dp(relu_x), (relu_x.stride(0) if relu_x is not None else 0)
+        epi.relu_act = _dp(relu_act)
         _abi.call("gala_spmm_ex_f32", g.csr(F), _dp(X), X.stride(0), _dp(out), out.stride(0), F,
                   _dp(src_scale), _dp(dst_scale), flags, nsamp or 0, ra, rb, ctypes.byref(epi), _stream())
         return out

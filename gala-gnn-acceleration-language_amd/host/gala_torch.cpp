@@ -20,7 +20,7 @@ void *stream() { return (void *)c10::hip::getCurrentHIPStream().stream(); }
 // that device (check_on), so nothing moves between devices behind the caller's back and a
 // GPU call never runs on the CPU.
 struct Backend {
-    decltype(&gala_spmm_f32) spmm;
+    decltype(&gala_spmm_ex_f32) spmm;
     decltype(&gala_degree_f32) degree;
     decltype(&gala_row_broadcast_f32) row_broadcast;
     decltype(&gala_row_scale_relu_f32) scale_relu;
@@ -48,7 +48,7 @@ struct Backend {
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
 };
-const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
+const Backend kHip{gala_spmm_ex_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_ffn_fwd_f32,
                    gala_sddvv_f32,
                    gala_row_sum_f32, gala_row_scale_f32, gala_sddmm_dot_f32,
@@ -58,7 +58,7 @@ const Backend kHip{gala_spmm_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_gat_bwd_stats_linear_f32,
                    gala_head_attn_f32, gala_head_attn_bwd_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
-const Backend kCpu{gala_cpu_spmm_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
+const Backend kCpu{gala_cpu_spmm_ex_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
                    gala_cpu_sddmm_dot_f32, gala_cpu_edge_softmax_fwd_f32,
@@ -256,13 +256,19 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
                         const torch::Tensor &bounds, int64_t segments, int val_heads,
                         const torch::Tensor *src_scale, const torch::Tensor *dst_scale,
                         int64_t nsamples, int64_t ra, int64_t rb,
-                        const torch::Tensor *val_row_scale = nullptr) {
+                        const torch::Tensor *val_row_scale = nullptr,
+                        const gala_spmm_epilogue_t *epi = nullptr) {
     if (!vals && nsamples == 0 && segments > 1 && offsets.is_cuda()) {
         if (const MergedCsr *m = find_merged(offsets))  // the same sums over one segment
             return spmm_impl(X, m->rowptr, m->col, nullptr, torch::Tensor(), 1, val_heads, src_scale, dst_scale, 0,
-                             ra, rb, nullptr);
+                             ra, rb, nullptr, epi);
     }
     CsrView cv = view(offsets, cols, vals, bounds, segments, val_heads);
+    // the ReLU prologue / epilogue (gcn_aggregate_relu_apply) run on unweighted, unsampled
+    // graphs without hub rows: otherwise an undefined result, and the caller runs the passes
+    if (epi && (epi->src_relu || epi->relu_x) &&
+        (vals || nsamples > 0 || (cv.c.split && cv.c.split->n_rows_split > 0)))
+        return torch::Tensor();
     if (val_row_scale) {  // factored edge values (GAT p with its per-row q)
         check_dev(*val_row_scale, torch::kFloat, "val_row_scale");
         check_on(*val_row_scale, offsets, "val_row_scale");
@@ -300,8 +306,8 @@ torch::Tensor spmm_impl(const torch::Tensor &X, const torch::Tensor &offsets,
     if (ds) check_on(dsc, offsets, "dst_scale");
     check(be(offsets).spmm(&cv.c, x.data_ptr<float>(), ldx, out.data_ptr<float>(), ldy,
                            (int32_t)dcols, ss, ds, flags, (int32_t)nsamples, (int32_t)ra,
-                           (int32_t)rb, stream_of(offsets)),
-          "gala_spmm_f32");
+                           (int32_t)rb, epi, stream_of(offsets)),
+          "gala_spmm_ex_f32");
     return out;
 }
 
@@ -1284,12 +1290,32 @@ struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
         Slot s = slot(2 * li);
         const bool has_act = act.numel() > 0, has_pre = pre.numel() > 0, has_post = post.numel() > 0;
         auto x = X.contiguous();
-        auto xs = scale_relu(x, has_act ? act : torch::Tensor(), has_pre ? pre : torch::Tensor());
         ctx->save_for_backward({x});
         ctx->saved_data["li"] = li;
         ctx->saved_data["act"] = act.detach();
         ctx->saved_data["pre"] = pre.detach();
         ctx->saved_data["post"] = post.detach();
+        // on short rows (< 8 edges per row on average, config 5) the SpMM forms
+        // pre[c] * relu(act[c] * X[c]) per gathered element (its ReLU prologue, the pass's
+        // roundings) instead of the pass over [N, F]; on long rows the pass is cheaper than two
+        // factor loads per edge
+        const int64_t n = x.size(0) > 0 ? x.size(0) : 1;
+        if (s.cols.numel() < 8 * n) {
+            torch::Tensor a = has_act ? act.contiguous() : torch::Tensor();
+            if (has_act) {
+                check_dev(a, torch::kFloat, "act");
+                check_on(a, x, "act");
+                TORCH_CHECK(a.numel() == x.size(0), "gala: act holds one factor per row");
+            }
+            gala_spmm_epilogue_t epi{};
+            epi.src_relu = 1;
+            epi.src_act = has_act ? a.data_ptr<float>() : nullptr;
+            auto y = spmm_impl(x, s.off, s.cols, s.weighted ? &s.vals : nullptr, s.bounds, s.segs, 1,
+                               has_pre ? &pre : nullptr, has_post ? &post : nullptr, S.nsamples, S.ra, S.rb,
+                               nullptr, &epi);
+            if (y.defined()) return y;
+        }
+        auto xs = scale_relu(x, has_act ? act : torch::Tensor(), has_pre ? pre : torch::Tensor());
         return spmm_impl(xs, s.off, s.cols, s.weighted ? &s.vals : nullptr, s.bounds, s.segs, 1,
                          nullptr, has_post ? &post : nullptr, S.nsamples, S.ra, S.rb);
     }
@@ -1308,10 +1334,22 @@ struct GcnAggregateRelu : public torch::autograd::Function<GcnAggregateRelu> {
         const bool has_post = post.numel() > 0;
         const bool fold = has_post && b.cols.numel() < 8 * (x.size(0) > 0 ? x.size(0) : 1);
         torch::Tensor dys = has_post && !fold ? row_broadcast(post, grad_outputs[0]) : grad_outputs[0].contiguous();
-        auto G = spmm_impl(dys, b.off, b.cols, b.weighted ? &b.vals : nullptr, b.bounds, b.segs, 1,
-                           fold ? &post : nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb);
-        return {relu_scale_backward(act.numel() > 0 ? act : torch::Tensor(), x, G), torch::Tensor(),
-                torch::Tensor(), torch::Tensor(), torch::Tensor()};
+        // the ReLU backward as the SpMM's epilogue: act * (relu(act * x) <= 0 ? 0 : G) on the
+        // row in registers, without G's round trip through HBM
+        torch::Tensor a = act.numel() > 0 ? act.contiguous() : torch::Tensor();
+        gala_spmm_epilogue_t epi{};
+        epi.relu_x = x.data_ptr<float>();
+        epi.ldrx = x.size(0) > 0 ? x.numel() / x.size(0) : 0;
+        epi.relu_act = a.defined() ? a.data_ptr<float>() : nullptr;
+        auto dx = spmm_impl(dys, b.off, b.cols, b.weighted ? &b.vals : nullptr, b.bounds, b.segs, 1,
+                            fold ? &post : nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb,
+                            nullptr, &epi);
+        if (!dx.defined()) {
+            auto G = spmm_impl(dys, b.off, b.cols, b.weighted ? &b.vals : nullptr, b.bounds, b.segs, 1,
+                               fold ? &post : nullptr, pre.numel() > 0 ? &pre : nullptr, S.nsamples, S.ra, S.rb);
+            dx = relu_scale_backward(act.numel() > 0 ? act : torch::Tensor(), x, G);
+        }
+        return {dx, torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor()};
     }
 };
 

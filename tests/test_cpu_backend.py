@@ -331,6 +331,58 @@ def test_row_scale_relu_and_backward_match_numpy():
     np.testing.assert_array_equal(dX, np.where(r <= 0, np.float32(0), G) * act[:, None])
 
 
+def test_spmm_relu_prologue_and_epilogue_match_the_passes():
+    """gala_spmm_ex_f32's ReLU fields against the passes they fold, bit for bit: the source
+    pre * relu(act * X) (gala_row_scale_relu_f32, then the SpMM) and the ReLU backward of the
+    result (the SpMM, then gala_relu_scale_backward_f32); refusals on weighted / sampled graphs
+    and for src_act without src_relu."""
+    g = cora_like()
+    A = HostCsr(g)
+    n, F = g.n_rows, 13
+    rng = np.random.default_rng(8)
+    X = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    X[::7, 0] = 0.0
+    act = rng.uniform(0.1, 2, n).astype(np.float32)
+    pre = rng.uniform(0.1, 2, n).astype(np.float32)
+    post = rng.uniform(0.1, 2, n).astype(np.float32)
+    Rx = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    L = _abi.cpu_lib()
+    for a, s in ((act, pre), (None, pre), (act, None), (None, None)):
+        H = np.empty_like(X)
+        _abi.call_cpu("gala_row_scale_relu_f32", n, F, P(a), P(s), P(X), F, P(H), F, None)
+        want = np.empty_like(X)
+        _abi.call_cpu("gala_spmm_f32", A.ref, P(H), F, P(want), F, F, None, P(post), 0, 0, 5, 7, None)
+        epi = _abi.gala_spmm_epilogue_t()
+        epi.src_relu, epi.src_act = 1, P(a)
+        got = np.empty_like(X)
+        _abi.call_cpu("gala_spmm_ex_f32", A.ref, P(X), F, P(got), F, F, P(s), P(post), 0, 0, 5, 7,
+                      ctypes.byref(epi), None)
+        np.testing.assert_array_equal(got, want)
+        G = np.empty_like(X)
+        _abi.call_cpu("gala_spmm_f32", A.ref, P(X), F, P(G), F, F, P(s), P(post), 0, 0, 5, 7, None)
+        _abi.call_cpu("gala_relu_scale_backward_f32", n, F, P(a), P(Rx), F, P(G), F, P(want), F, None)
+        epi = _abi.gala_spmm_epilogue_t()
+        epi.relu_x, epi.ldrx, epi.relu_act = P(Rx), F, P(a)
+        _abi.call_cpu("gala_spmm_ex_f32", A.ref, P(X), F, P(got), F, F, P(s), P(post), 0, 0, 5, 7,
+                      ctypes.byref(epi), None)
+        np.testing.assert_array_equal(got, want)
+    epi = _abi.gala_spmm_epilogue_t()
+    epi.src_relu = 1
+    W = HostCsr(g, val=edge_values(g.nnz))
+    assert L.gala_cpu_spmm_ex_f32(W.ref, P(X), F, P(got), F, F, None, None, 0, 0, 5, 7, ctypes.byref(epi),
+                                  None) == _abi.GALA_ERR_UNSUPPORTED
+    assert L.gala_cpu_spmm_ex_f32(A.ref, P(X), F, P(got), F, F, None, None, _abi.GALA_SPMM_SAMPLE, 3, 5, 7,
+                                  ctypes.byref(epi), None) == _abi.GALA_ERR_UNSUPPORTED
+    epi = _abi.gala_spmm_epilogue_t()
+    epi.src_act = P(act)
+    assert L.gala_cpu_spmm_ex_f32(A.ref, P(X), F, P(got), F, F, None, None, 0, 0, 5, 7, ctypes.byref(epi),
+                                  None) == _abi.GALA_ERR_INVALID_ARG
+    epi = _abi.gala_spmm_epilogue_t()
+    epi.relu_x, epi.ldrx = P(Rx), F - 1
+    assert L.gala_cpu_spmm_ex_f32(A.ref, P(X), F, P(got), F, F, None, None, 0, 0, 5, 7, ctypes.byref(epi),
+                                  None) == _abi.GALA_ERR_INVALID_ARG
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_random_case(seed):
     """Seeded random sweep of the host backend (the GPU suite runs the same generator through

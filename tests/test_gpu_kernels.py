@@ -445,6 +445,47 @@ def test_spmm_epilogue_deg_norm_and_next_input(F, kind):
         ops.row_broadcast_deg(gw, X)
 
 
+@pytest.mark.parametrize("F", [1, 7, 32, 47, 128, 2100])
+@pytest.mark.parametrize("kind", ["cora", "empty", "tiled", "padded"])
+def test_spmm_relu_prologue_and_epilogue_match_the_passes(F, kind):
+    """gala_spmm_ex_f32's ReLU fields (gcn_aggregate_relu_apply's fused forward and backward)
+    against the passes they fold, bit for bit: the source pre * relu(act * X) formed per
+    gathered element (gala_row_scale_relu_f32, then the SpMM), and the ReLU backward of the
+    result in the store (the SpMM, then gala_relu_scale_backward_f32); each factor absent or
+    present, -0 / exact zeros / NaN in X, column segments, row-padded operands, F past one
+    launch's column block.  Refused on weighted or sampled graphs and with hub rows."""
+    g = with_empty_rows() if kind == "empty" else cora_like()
+    dg = ops.DeviceGraph.from_host(layout.col_tile(g, 900) if kind == "tiled" else g, split=False)
+    _same = lambda a, b: torch.equal(a.contiguous().view(torch.int32), b.contiguous().view(torch.int32))  # noqa: E731
+    rng = np.random.default_rng(F)
+    X = rng.uniform(-1, 1, (g.n_cols, F)).astype(np.float32)
+    X[::7, 0] = 0.0
+    X[1::11, -1] = -0.0
+    X[5, 0] = np.nan
+    R = rng.uniform(-1, 1, (g.n_rows, F)).astype(np.float32)
+    if kind == "padded":
+        _, Xd = _padded(X, F, 5.0)
+        _, Rd = _padded(R, F, 7.0)
+    else:
+        Xd, Rd = dev(X), dev(R)
+    act, pre, post = (dev(rng.uniform(0.1, 2, g.n_rows).astype(np.float32)) for _ in range(3))
+    for a, s, d in ((act, pre, post), (None, pre, None), (act, None, post), (None, None, None)):
+        want = ops.spmm(dg, ops.row_scale_relu(Xd, a, s), dst_scale=d)
+        got = ops.spmm(dg, Xd, src_scale=s, dst_scale=d, src_relu=True, src_act=a)
+        assert _same(got, want), (a is None, s is None, d is None)
+        G = ops.spmm(dg, Xd, src_scale=s, dst_scale=d)
+        want = ops.relu_scale_backward(Rd, G, a)
+        got = ops.spmm(dg, Xd, src_scale=s, dst_scale=d, relu_x=Rd, relu_act=a)
+        assert _same(got, want), (a is None, s is None, d is None)
+    if kind == "cora":
+        with pytest.raises(_abi.GalaError):
+            ops.spmm(dg.with_values(dev(edge_values(g.nnz))), Xd, src_relu=True)
+        with pytest.raises(_abi.GalaError):
+            ops.spmm(dg, Xd, relu_x=Rd, nsamp=3)
+        with pytest.raises(_abi.GalaError):
+            ops.spmm(ops.DeviceGraph.from_host(hub_graph()), dev(features(hub_graph().n_cols, F)), src_relu=True)
+
+
 def test_fused_gcn_step_matches_the_chain():
     """bench.py's fused step (the headline workload) against its unfused chain on a graph
     with hub rows and one without: all four outputs bit-identical."""
