@@ -134,10 +134,11 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
     // batch wait out its write latency (8 heads: 3 ms over the no-alpha forward).
     float pend[NK];
     int32_t pend_j0 = -1;
+    int32_t win = 0;  // the row's next 64 column indices (load_batch_cols_win)
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         int64_t c[U];
         V x[U][CH];
-        load_batch_cols<G, U>(p, e0, n, j0, c);
+        load_batch_cols_win<G, U>(p, e0, n, j0, win, c);
         float ar[NK];
         if (!RC) {
 #pragma unroll

@@ -30,6 +30,24 @@ __device__ __forceinline__ void load_batch_cols(const EdgeParams &p, int64_t e0,
     }
 }
 
+// The same columns from a window of the row's next 64 column indices held one per lane
+// (G = 64, U | 64): one coalesced load per 64 edges instead of one per U-edge batch, so a
+// batch's gathers wait on one memory round trip (the X rows) rather than two (the column
+// indices, then the rows).  `win` carries the window between batches; j0 steps by U from 0.
+template <int G, int U>
+__device__ __forceinline__ void load_batch_cols_win(const EdgeParams &p, int64_t e0, int32_t n, int32_t j0,
+                                                    int32_t &win, int64_t (&c)[U]) {
+    if constexpr (G == 64 && (64 % U) == 0) {
+        const int lane = threadIdx.x & 63;
+        const int b = j0 & 63;
+        if (b == 0) win = p.col[e0 + ((j0 + lane < n) ? j0 + lane : n - 1)];
+#pragma unroll
+        for (int k = 0; k < U; ++k) c[k] = __builtin_amdgcn_readlane(win, b + k);
+    } else {
+        load_batch_cols<G, U>(p, e0, n, j0, c);
+    }
+}
+
 // Broadcast of lane SRC of each aligned group of HW lanes to the group, SRC a compile-time
 // constant: ds_swizzle in bitmask mode for HW <= 32 (no address VGPR, unlike ds_bpermute),
 // v_readlane for a whole wave (its value is wave-uniform).

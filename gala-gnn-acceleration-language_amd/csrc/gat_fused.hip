@@ -44,10 +44,11 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
     const int kl = hl % UH;
     const bool owner = hl < UH;
     const int32_t n = (int32_t)(e1 - e0);
+    int32_t win = 0;  // the row's next 64 column indices (load_batch_cols_win)
     for (int32_t j0 = 0; j0 < n; j0 += U) {
         int64_t c[U];
         V x[U][CH], yv[U][CH];
-        load_batch_cols<G, U>(p, e0, n, j0, c);
+        load_batch_cols_win<G, U>(p, e0, n, j0, win, c);
         float ar[NK];
         // ST with the forward's p (d.alpha): alpha = fl(p * q) from the edge-ordered p,
         // no aR[col] gather

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""The 8-head GAT statistics pair (bench.py's "gat" leg: gala_gat_fwd_stats_f32 /
+gala_gat_bwd_stats_f32, F = 256, the Products-shaped uniform graph) beside the same-process
+gather ceiling (tools/libgala_probe.so).  One JSON line per variant: fwd / bwd ms (HIP events,
+10 calls), frac of the ceiling, and whether the outputs are bit-identical to the first run's.
+Variants: the default pair, and p_stored -- the forward also writes the edge-ordered exp terms
+p and the backward rebuilds alpha = p * q from them instead of gathering aR[col].
+(profiles/r05_gat_tune.jsonl also holds a sweep of kernel variants this tool ran while they
+were selectable: 4 / 8 / 16 edges per batch, two batches in flight; none beat the default
+beyond box noise, and they were removed.)    python tools/gat_tune.py [scale]
+"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gala-gnn-acceleration-language_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from gala import ops  # noqa: E402
+
+
+def main():
+    scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+    H, D = 8, 32
+    F = H * D
+    hg = bench.products_graph("uniform", scale)
+    dg = ops.DeviceGraph.from_host(hg)
+    N = hg.n_rows
+    gen = torch.Generator(device="cuda").manual_seed(4321)
+    X = torch.rand((N, F), device="cuda", generator=gen) * 2 - 1
+    dY = torch.rand((N, F), device="cuda", generator=gen) * 2 - 1
+    aL = torch.rand((N, H), device="cuda", generator=gen) - 0.5
+    wR = (torch.rand(F, device="cuda", generator=gen) - 0.5) * 0.2
+    bR = torch.zeros(H, device="cuda")
+    timer = bench.Timer(True)
+    t_ceil = bench.gather_ceiling(dg.col, X, timer)
+    print(json.dumps({"graph": "uniform", "rows": N, "edges": int(hg.nnz), "F": F,
+                      "gather_ceiling_ms": t_ceil * 1e3 if t_ceil else None}), flush=True)
+    ref = None
+    samples = {}
+    for want_p in (False, True) * 4:   # alternated: box and allocation noise is about 1 ms
+        st = {}
+
+        def fwd():
+            st["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True, want_p=want_p)
+
+        def bwd():
+            Y, q, Ym, sma, aRo = st["f"][:5]
+            st["b"] = ops.gat_bwd_stats(dg, aL, aRo, dY, q, Y, Ym, sma, heads=H,
+                                        p=st["f"][5] if want_p else None)
+        fwd()
+        bwd()
+        torch.cuda.synchronize()
+        outs = [t.clone() for t in st["f"][:5]] + [t.clone() for t in st["b"]]
+        if ref is None:
+            ref = outs
+        same = all(torch.equal(a, b) for a, b in zip(outs, ref))
+        tf = timer(fwd, 10)
+        tb = timer(bwd, 10)
+        rec = {"p_stored": want_p, "fwd_ms": round(tf * 1e3, 3), "bwd_ms": round(tb * 1e3, 3), "bit_identical": same}
+        if t_ceil:
+            rec["fwd_frac_of_ceiling"] = round(t_ceil / tf, 4)
+            rec["bwd_frac_of_ceiling"] = round(t_ceil / tb, 4)
+        print(json.dumps(rec), flush=True)
+        samples.setdefault(want_p, []).append((tf * 1e3, tb * 1e3))
+        del st, outs
+    for want_p, v in samples.items():
+        fs, bs, ps = sorted(a for a, _ in v), sorted(b for _, b in v), sorted(a + b for a, b in v)
+        med = lambda xs: (xs[(len(xs) - 1) // 2] + xs[len(xs) // 2]) / 2  # noqa: E731
+        print(json.dumps({"p_stored": want_p, "samples": len(v), "fwd_ms_median": round(med(fs), 3),
+                          "bwd_ms_median": round(med(bs), 3), "pair_ms_median": round(med(ps), 3),
+                          "pair_ms_min": round(ps[0], 3), "pair_ms_max": round(ps[-1], 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
