@@ -208,6 +208,7 @@ public:
         denseOnMatrixCores(*model.getInv());
         if (!std::getenv("GALA_REFGEN_UNFUSED")) {   // (the unfused spelling: a bit-identity check)
             fuseGcnChains(*model.getForward());
+            fuseGatChains(*model.getForward());
             trainRowsAndLoss(preCode, *model.getPostCall());
         }
         addDumpHook(*model.getPostCall());
@@ -409,13 +410,22 @@ private:
     // BROADCASTs in the aggregation's prologue / epilogue, relu as torch's GPU kernel).
     // Statements of any other shape are left as they are.
     struct FwdStmt {
-        enum Kind { Other, Mul, Relu, Agg } kind = Other;
-        std::string text, a, b;  // Mul: a = scale, b = source; Agg: a = class, b = slot index
+        enum Kind { Other, Mul, Relu, Agg, AttnAgg, EdgeSum, LeakyDecl, Leaky, Softmax, HeadAttn } kind = Other;
+        // Mul: a = scale, b = source; Agg: a = class, b = slot index; AttnAgg: a = class,
+        // b = slot, c = source; EdgeSum: a = attn_l, b = attn_r, c = slot; LeakyDecl: a = slope;
+        // Softmax: b = slot; HeadAttn: lhs = gala::head_attn_apply(a, c->weight, c->bias), b = lhs
+        std::string text, a, b, c;
     };
 
     static std::vector<FwdStmt> splitForward(const std::string &t) {
         static const std::regex mul("^res = (\\w+) \\* (\\w+);$"), relu("^res = torch::relu\\(res\\);$"),
-            app("^res = (\\w+)::apply\\(res, (\\d+)\\);$");
+            app("^res = (\\w+)::apply\\(res, (\\d+)\\);$"),
+            app_attn("^res = (\\w+)::apply\\((\\w+), attn, (\\d+)\\);$"),
+            edge("^attn = aggregate_edge_sum_AutoGrad::apply\\((\\w+), (\\w+), (\\d+)\\);$"),
+            leaky_decl("^torch::nn::LeakyReLU leaky_relu\\(torch::nn::LeakyReLUOptions\\(\\)\\.negative_slope\\(([0-9.eE+-]+)\\)\\);$"),
+            leaky("^attn = leaky_relu->forward\\(attn\\);$"),
+            softmax("^attn = non_lnr_op_softmax_AutoGrad::apply\\(attn, (\\d+)\\);$"),
+            head_attn("^(\\w+) = gala::head_attn_apply\\((\\w+), (\\w+)->weight, \\3->bias\\);$");
         std::vector<FwdStmt> out;
         size_t p = 0;
         auto trim = [](std::string x) {
@@ -453,7 +463,14 @@ private:
                 std::smatch m1, m2;
                 if (c2 != std::string::npos && std::regex_match(b1, m1, app) && std::regex_match(b2, m2, app) &&
                     m1[0] == m2[0]) {
-                    st = {FwdStmt::Agg, t.substr(p, c2 + 1 - p), m1[1], m1[2]};
+                    st = {FwdStmt::Agg, t.substr(p, c2 + 1 - p), m1[1], m1[2], ""};
+                    out.push_back(st);
+                    p = c2 + 1;
+                    continue;
+                }
+                if (c2 != std::string::npos && std::regex_match(b1, m1, app_attn) &&
+                    std::regex_match(b2, m2, app_attn) && m1[0] == m2[0]) {
+                    st = {FwdStmt::AttnAgg, t.substr(p, c2 + 1 - p), m1[1], m1[3], m1[2]};
                     out.push_back(st);
                     p = c2 + 1;
                     continue;
@@ -464,8 +481,13 @@ private:
             st.text = t.substr(p, end - p);
             const std::string body = trim(st.text);
             std::smatch m;
-            if (std::regex_match(body, m, mul)) st = {FwdStmt::Mul, st.text, m[1], m[2]};
-            else if (std::regex_match(body, relu)) st = {FwdStmt::Relu, st.text, "", ""};
+            if (std::regex_match(body, m, mul)) st = {FwdStmt::Mul, st.text, m[1], m[2], ""};
+            else if (std::regex_match(body, relu)) st = {FwdStmt::Relu, st.text, "", "", ""};
+            else if (std::regex_match(body, m, edge)) st = {FwdStmt::EdgeSum, st.text, m[1], m[2], m[3]};
+            else if (std::regex_match(body, m, leaky_decl)) st = {FwdStmt::LeakyDecl, st.text, m[1], "", ""};
+            else if (std::regex_match(body, leaky)) st = {FwdStmt::Leaky, st.text, "", "", ""};
+            else if (std::regex_match(body, m, softmax)) st = {FwdStmt::Softmax, st.text, "", m[1], ""};
+            else if (std::regex_match(body, m, head_attn)) st = {FwdStmt::HeadAttn, st.text, m[2], m[1], m[3]};
             out.push_back(st);
             p = end;
         }
@@ -518,6 +540,95 @@ private:
             k = last;
         }
         for (size_t i = done; i < st.size(); ++i) out += st[i].text;
+        *fwd.atLine(0) = out;
+        for (int i = 1; i < fwd.getNum(); ++i) fwd.atLine(i)->clear();
+    }
+
+    // The base emits a GAT layer (common.h:622-894, 1175-1184) as four steps over E-long
+    // edge tensors: the edge sum's autograd class (K5), torch's LeakyReLU, the softmax class
+    // (torch exp / clamp / reciprocal around K7 and K8) and the attention-weighted aggregation
+    // class -- with their backwards (K9, the softmax backward's torch ops around K7 / K8, K7 for
+    // the logits' gradient): on the Products shape 30.8 ms per epoch where galac's fused layer
+    // takes 20.8 (profiles/r05_refgen_gat_products.jsonl).  The chain
+    //     attn = aggregate_edge_sum_AutoGrad::apply(L, R, li);  [LeakyReLU declaration]
+    //     attn = leaky_relu->forward(attn);  attn = non_lnr_op_softmax_AutoGrad::apply(attn, li);
+    //     AGG(X, attn, li)   (the `if (ep % mod_v == 0)` pair)
+    // becomes the mirror's fused layer over the same slot in REF mode,
+    //     res = gala::gat_aggregate_apply(L, R, X, li, slope, GALA_SOFTMAX_REF);
+    // (the same chain of operations per edge, one pass per row; alpha = p * q with the
+    // reference's clamp, 1e-12 and sequential row sums; gradients d aL = d aR = the row sums of
+    // the LeakyReLU'd softmax gradient, as the base's classes return them).  When R is
+    // `gala::head_attn_apply(X, W->weight, W->bias)` of the aggregated rows themselves, the
+    // layer recomputes it from the rows it gathers (gat_aggregate_ffn_apply, galac's spelling)
+    // and the statement goes when nothing else reads R.  The values are the chain's within
+    // fp32 rounding, not bit for bit: the fused kernels sum in the chain's order but round
+    // alpha = p * q once per edge where the chain stores it (tests/test_gpu_refgen.py checks
+    // the program against galac's IR in float64 at 1e-4; GALA_REFGEN_UNFUSED keeps the base's
+    // spelling).
+    void fuseGatChains(Code &fwd) {
+        std::string t;
+        for (int i = 0; i < fwd.getNum(); ++i) t += *fwd.atLine(i) + "\n";
+        std::vector<FwdStmt> st = splitForward(t);
+        static const std::regex word_attn("\\battn\\b");
+        auto mentions = [](const std::string &text, const std::string &name) {
+            return std::regex_search(text, std::regex("\\b" + name + "\\b"));
+        };
+        std::vector<bool> drop(st.size(), false);
+        std::vector<std::string> repl(st.size());
+        std::string slope = "0.2";
+        bool any = false;
+        for (size_t k = 0; k < st.size(); ++k) {
+            if (st[k].kind == FwdStmt::LeakyDecl) slope = st[k].a;
+            if (st[k].kind != FwdStmt::AttnAgg || !plainAgg_.count(st[k].a) || k < 3) continue;
+            const std::string li = st[k].b, X = st[k].c;
+            if (st[k - 1].kind != FwdStmt::Softmax || st[k - 1].b != li || st[k - 2].kind != FwdStmt::Leaky) continue;
+            size_t e = k - 3;
+            if (st[e].kind == FwdStmt::LeakyDecl) {   // kept: later layers use the variable
+                if (e == 0) continue;
+                --e;
+            }
+            if (st[e].kind != FwdStmt::EdgeSum || st[e].c != li) continue;
+            // `attn` must not be read after the chain before it is assigned again
+            bool attn_dead = true;
+            for (size_t i = k + 1; i < st.size(); ++i) {
+                if (!std::regex_search(st[i].text, word_attn)) continue;
+                attn_dead = st[i].kind == FwdStmt::EdgeSum;
+                break;
+            }
+            if (!attn_dead) continue;
+            const std::string L = st[e].a, R = st[e].b;
+            // R = head_attn_apply(X, W->weight, W->bias) just before, with only other attention
+            // Linears (not assigning X) in between
+            long h = -1;
+            for (long i = (long)e - 1; i >= 0; --i) {
+                if (st[i].kind != FwdStmt::HeadAttn || st[i].b == X) break;
+                if (st[i].b == R) {
+                    if (st[i].a == X) h = i;
+                    break;
+                }
+            }
+            std::string rest;
+            for (size_t i = k + 1; i < st.size(); ++i) rest += st[i].text;
+            std::string call;
+            if (h >= 0 && R != L) {
+                const std::string W = st[h].c;
+                call = "res = gala::gat_aggregate_ffn_apply(" + L + ", " + X + ", " + W + "->weight, " + W + "->bias, " +
+                       li + ", " + slope + ", GALA_SOFTMAX_REF);";
+                if (!mentions(rest, R)) drop[h] = true;
+            } else {
+                call = "res = gala::gat_aggregate_apply(" + L + ", " + R + ", " + X + ", " + li + ", " + slope +
+                       ", GALA_SOFTMAX_REF);";
+            }
+            repl[e] = "\n        // EDGE SUM / LEAKY RELU / SOFTMAX / AGGREGATE fused (HIPGenerator)\n        " + call;
+            drop[k - 2] = drop[k - 1] = drop[k] = true;
+            any = true;
+        }
+        if (!any) return;
+        std::string out;
+        for (size_t i = 0; i < st.size(); ++i) {
+            if (!repl[i].empty()) out += repl[i];
+            else if (!drop[i]) out += st[i].text;
+        }
         *fwd.atLine(0) = out;
         for (int i = 1; i < fwd.getNum(); ++i) fwd.atLine(i)->clear();
     }

@@ -15,9 +15,10 @@ end to end on the host, where the reference's sources are:
 3. it runs on the host backend (GALA_DEVICE=cpu) over an npy dataset in the reference's
    format, and its first-epoch prediction, loss and weight gradients equal, within 1e-4,
    galac's program of the same DSL (tests/dsl/<model>_ref_codegen.txt, the same passes)
-   evaluated by the float64 IR executor on the weights the program dumped.  For GAT that runs the base generator's own autograd classes (edge
-   sum, softmax, the attention-weighted aggregation, common.h:622-894) over the mirror's
-   edge operators.
+   evaluated by the float64 IR executor on the weights the program dumped.  For GAT the
+   base's edge chain (edge sum, LeakyReLU, softmax, the attention-weighted aggregation,
+   common.h:622-894) runs as the mirror's fused layer in REF mode (HIPGenerator's
+   fuseGatChains).
 tests/test_gpu_refgen.py runs the programs refgen/build.py builds on the MI355X.
 """
 import importlib.util
@@ -116,14 +117,14 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
         assert fwd.index("gala::ffn_apply(t_iden_n, fc0->weight, fc0->bias)") < fwd.index("sfc0->weight")
     else:
-        # the edge chain of each layer: attention Linears, edge sum, LeakyReLU, softmax, aggregation
-        # (the attention Linears as the mirror's head-attention op)
+        # the edge chain of each layer (edge sum, LeakyReLU, softmax, aggregation: the base's
+        # classes, which the program still defines) runs as the mirror's fused layer in REF
+        # mode; the source logits' Linear of the aggregated rows is recomputed inside it
+        # (gat_aggregate_ffn_apply), the other attention Linear runs as the head-attention op
         assert "efc0->forward" not in src and "gala::head_attn_apply(" in fwd
-        for a, b in (("head_attn_apply(", "aggregate_edge_sum_AutoGrad::apply"),
-                     ("aggregate_edge_sum_AutoGrad::apply", "leaky_relu->forward"),
-                     ("leaky_relu->forward", "non_lnr_op_softmax_AutoGrad::apply"),
-                     ("non_lnr_op_softmax_AutoGrad::apply", "aggregate_node_mul_sum_coarse2_AutoGrad::apply(res, attn")):
-            assert fwd.index(a) < fwd.index(b), (a, b)
+        assert "class non_lnr_op_softmax_AutoGrad" in src and "_AutoGrad::apply" not in fwd
+        assert fwd.count("gala::gat_aggregate_ffn_apply(") == 2 and "GALA_SOFTMAX_REF" in fwd
+        assert fwd.index("head_attn_apply(res, efc0->weight") < fwd.index("gat_aggregate_ffn_apply(attenL, res, efc1")
         assert "ord_col_tiling_torch" in src   # the column-tiled graph, built by the reference's host code
 
     # 2. the emitted program, compiled against the reference's host headers and the operator
