@@ -735,22 +735,23 @@ __global__ __launch_bounds__(kBlock) void k_softmax_bwd_generic(EdgeParams p, co
 // their loads in flight before the dot products.  For one head (HW == G) the U partial
 // dots are reduced with a reduce-scatter butterfly (U-1 + log2(G/U) shuffles per batch,
 // lane k*(G/U) ends with edge k); with heads each head reduces over its HW lanes.
+template <int M, int O, int U>
+__device__ __forceinline__ void reduce_scatter_step(float (&v)[U], int gl) {
+    if constexpr (M > 1) {
+        const bool up = (gl & O) != 0;
+#pragma unroll
+        for (int i = 0; i < M / 2; ++i) {
+            const float send = up ? v[i] : v[i + M / 2];
+            const float keep = up ? v[i + M / 2] : v[i];
+            v[i] = keep + lane_xor<O>(send);
+        }
+        reduce_scatter_step<M / 2, O / 2, U>(v, gl);
+    }
+}
 template <int G, int U>
 __device__ __forceinline__ float reduce_scatter(float (&v)[U], int gl) {
-#pragma unroll
-    for (int m = U, o = G / 2; m > 1; m >>= 1, o >>= 1) {
-        const bool up = (gl & o) != 0;
-#pragma unroll
-        for (int i = 0; i < m / 2; ++i) {
-            const float send = up ? v[i] : v[i + m / 2];
-            const float keep = up ? v[i + m / 2] : v[i];
-            v[i] = keep + __shfl_xor(send, o, 64);
-        }
-    }
-    float r = v[0];
-#pragma unroll
-    for (int o = G / (2 * U); o >= 1; o >>= 1) r += __shfl_xor(r, o, 64);
-    return r;
+    reduce_scatter_step<U, G / 2, U>(v, gl);
+    return group_sum<G / U>(v[0]);
 }
 
 

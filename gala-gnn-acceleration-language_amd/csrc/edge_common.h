@@ -68,17 +68,24 @@ struct HubSplit {
 // When a row fits one tile, the second pass of softmax fwd/bwd runs from the registers.
 constexpr int kTileK = 8;
 
+// over the lanes of one head: partners G/2, ..., HP (lane_xor: DPP below 16)
 template <int G, int HP>
 __device__ __forceinline__ float head_sum(float v) {
-#pragma unroll
-    for (int o = G / 2; o >= HP; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    if constexpr (G / 2 >= HP && G >= 2) {
+        v += lane_xor<G / 2>(v);
+        return head_sum<G / 2, HP>(v);
+    } else {
+        return v;
+    }
 }
 template <int G, int HP>
 __device__ __forceinline__ float head_max(float v) {
-#pragma unroll
-    for (int o = G / 2; o >= HP; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    if constexpr (G / 2 >= HP && G >= 2) {
+        v = fmaxf(v, lane_xor<G / 2>(v));
+        return head_max<G / 2, HP>(v);
+    } else {
+        return v;
+    }
 }
 
 // v[k] = base[t0 + gl + k*G] for indices < n, `fill` elsewhere

@@ -71,18 +71,46 @@ __device__ __forceinline__ int32_t ld_nt(const int32_t *p) { return __builtin_no
 // Wave-uniform value broadcast (keeps the row bounds in SGPRs).
 __device__ __forceinline__ int32_t uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Lane i's partner i ^ O.  O <= 8 stays inside a 16-lane DPP row: a VALU data-parallel move
+// (quad_perm for 1 and 2; for 4 and 8 a row shift each way, picked by the lane's bit), where
+// __shfl_xor is a ds_bpermute through the LDS crossbar whose result the next step must wait
+// for.  Every lane of the row must be active.  row_shl:n reads lane i + n, row_shr:n lane i - n.
+template <int O>
+__device__ __forceinline__ float lane_xor(float v) {
+    const int x = __float_as_int(v);
+    if constexpr (O == 1) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+    } else if constexpr (O == 2) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    } else if constexpr (O == 4 || O == 8) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x100 + O, 0xF, 0xF, false);    // row_shl:O
+        const int down = __builtin_amdgcn_update_dpp(0, x, 0x110 + O, 0xF, 0xF, false);  // row_shr:O
+        return __int_as_float((threadIdx.x & O) ? down : up);
+    } else {
+        return __shfl_xor(v, O, 64);
+    }
+}
+
+// xor-butterfly inside aligned groups of W lanes (W power of two <= 64): partners W/2, ..., 1,
+// each step v + partner (every lane ends with the same bits).  Partners below 16 are DPP moves
+// (lane_xor); all lanes of a group must be active.
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
-    // xor-butterfly inside aligned groups of W lanes (W power of two <= 64)
-#pragma unroll
-    for (int o = W / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    if constexpr (W >= 2) {
+        v += lane_xor<W / 2>(v);
+        return group_sum<W / 2>(v);
+    } else {
+        return v;
+    }
 }
 template <int W>
 __device__ __forceinline__ float group_max(float v) {
-#pragma unroll
-    for (int o = W / 2; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    if constexpr (W >= 2) {
+        v = fmaxf(v, lane_xor<W / 2>(v));
+        return group_max<W / 2>(v);
+    } else {
+        return v;
+    }
 }
 
 }  // namespace gala

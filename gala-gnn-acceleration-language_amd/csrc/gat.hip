@@ -196,8 +196,7 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
             float mb = -INFINITY;
 #pragma unroll
             for (int i = 0; i < NK; ++i) mb = (j0 + kl + i * UH < n) ? fmaxf(mb, z[i]) : mb;
-#pragma unroll
-            for (int o = HW / 2; o >= 1; o >>= 1) mb = fmaxf(mb, __shfl_xor(mb, o, 64));
+            mb = group_max<HW>(mb);
             if (mb > st.m) {
                 const float r = (st.m == -INFINITY) ? 0.0f : expf(st.m - mb);
                 st.sum = __fmul_rn(st.sum, r);

@@ -49,12 +49,30 @@ __device__ __forceinline__ void load_batch_cols_win(const EdgeParams &p, int64_t
 }
 
 // Broadcast of lane SRC of each aligned group of HW lanes to the group, SRC a compile-time
-// constant: ds_swizzle in bitmask mode for HW <= 32 (no address VGPR, unlike ds_bpermute),
-// v_readlane for a whole wave (its value is wave-uniform).
+// constant.  HW <= 16: DPP moves inside the 16-lane row (quad_perm picks lane SRC % 4 of each
+// quad; a row shift by 4, then 8, carries it to the group's other quads), VALU only; HW = 32:
+// ds_swizzle in bitmask mode (no address VGPR, unlike ds_bpermute); a whole wave: v_readlane.
 template <int HW, int SRC>
 __device__ __forceinline__ float group_bcast(float v) {
     if constexpr (HW == 1) {
         return v;
+    } else if constexpr (HW == 2) {
+        constexpr int c = SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6);
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), c, 0xF, 0xF, false));
+    } else if constexpr (HW <= 16) {
+        constexpr int s = SRC & 3;
+        int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), s | (s << 2) | (s << 4) | (s << 6), 0xF, 0xF, false);
+        if constexpr (HW >= 8) {   // quad SRC / 4 of each 8-lane group to the other quad
+            constexpr int q = (SRC >> 2) & 1;
+            const int u = __builtin_amdgcn_update_dpp(0, t, q ? 0x104 : 0x114, 0xF, 0xF, false);
+            t = (((threadIdx.x >> 2) & 1) == q) ? t : u;
+        }
+        if constexpr (HW == 16) {  // 8-lane half SRC / 8 to the other half
+            constexpr int h = (SRC >> 3) & 1;
+            const int u = __builtin_amdgcn_update_dpp(0, t, h ? 0x108 : 0x118, 0xF, 0xF, false);
+            t = (((threadIdx.x >> 3) & 1) == h) ? t : u;
+        }
+        return __int_as_float(t);
     } else if constexpr (HW <= 32) {
         constexpr int pattern = (0x1F & ~(HW - 1)) | (SRC << 5);  // lane' = (lane & and) | or
         return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), pattern));

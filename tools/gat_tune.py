@@ -36,12 +36,18 @@ def main():
     wR = (torch.rand(F, device="cuda", generator=gen) - 0.5) * 0.2
     bR = torch.zeros(H, device="cuda")
     timer = bench.Timer(True)
+    # a process's first timed work runs 1-3 ms slow at this size: warm the probe and the pair
+    # up first, and take the ceiling again at the end (the lower of the two is used)
+    bench.gather_ceiling(dg.col, X, timer, reps=3)
+    f = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+    ops.gat_bwd_stats(dg, aL, f[4], dY, f[1], f[0], f[2], f[3], heads=H)
+    del f
     t_ceil = bench.gather_ceiling(dg.col, X, timer)
     print(json.dumps({"graph": "uniform", "rows": N, "edges": int(hg.nnz), "F": F,
                       "gather_ceiling_ms": t_ceil * 1e3 if t_ceil else None}), flush=True)
     ref = None
     samples = {}
-    for want_p in (False, True) * 4:   # alternated: box and allocation noise is about 1 ms
+    for want_p in (False, True) * 3:   # alternated: box and allocation noise is about 1 ms
         st = {}
 
         def fwd():
@@ -67,12 +73,17 @@ def main():
         print(json.dumps(rec), flush=True)
         samples.setdefault(want_p, []).append((tf * 1e3, tb * 1e3))
         del st, outs
+    t_end = bench.gather_ceiling(dg.col, X, timer)
+    print(json.dumps({"gather_ceiling_ms_start": t_ceil * 1e3, "gather_ceiling_ms_end": t_end * 1e3}), flush=True)
+    t_ceil = min(t_ceil, t_end)
     for want_p, v in samples.items():
         fs, bs, ps = sorted(a for a, _ in v), sorted(b for _, b in v), sorted(a + b for a, b in v)
         med = lambda xs: (xs[(len(xs) - 1) // 2] + xs[len(xs) // 2]) / 2  # noqa: E731
         print(json.dumps({"p_stored": want_p, "samples": len(v), "fwd_ms_median": round(med(fs), 3),
                           "bwd_ms_median": round(med(bs), 3), "pair_ms_median": round(med(ps), 3),
-                          "pair_ms_min": round(ps[0], 3), "pair_ms_max": round(ps[-1], 3)}), flush=True)
+                          "pair_ms_min": round(ps[0], 3), "pair_ms_max": round(ps[-1], 3),
+                          "fwd_frac_of_ceiling": round(t_ceil * 1e3 / med(fs), 4),
+                          "bwd_frac_of_ceiling": round(t_ceil * 1e3 / med(bs), 4)}), flush=True)
 
 
 if __name__ == "__main__":
