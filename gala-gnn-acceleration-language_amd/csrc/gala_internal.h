@@ -79,12 +79,12 @@ template <int O>
 __device__ __forceinline__ float lane_xor(float v) {
     const int x = __float_as_int(v);
     if constexpr (O == 1) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true));  // quad_perm [1,0,3,2]
     } else if constexpr (O == 2) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+        return __int_as_float(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true));  // quad_perm [2,3,0,1]
     } else if constexpr (O == 4 || O == 8) {
-        const int up = __builtin_amdgcn_update_dpp(0, x, 0x100 + O, 0xF, 0xF, false);    // row_shl:O
-        const int down = __builtin_amdgcn_update_dpp(0, x, 0x110 + O, 0xF, 0xF, false);  // row_shr:O
+        const int up = __builtin_amdgcn_mov_dpp(x, 0x100 + O, 0xF, 0xF, true);    // row_shl:O
+        const int down = __builtin_amdgcn_mov_dpp(x, 0x110 + O, 0xF, 0xF, true);  // row_shr:O
         return __int_as_float((threadIdx.x & O) ? down : up);
     } else {
         return __shfl_xor(v, O, 64);

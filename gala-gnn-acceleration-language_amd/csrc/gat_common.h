@@ -58,18 +58,18 @@ __device__ __forceinline__ float group_bcast(float v) {
         return v;
     } else if constexpr (HW == 2) {
         constexpr int c = SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6);
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), c, 0xF, 0xF, false));
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), c, 0xF, 0xF, true));
     } else if constexpr (HW <= 16) {
         constexpr int s = SRC & 3;
-        int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), s | (s << 2) | (s << 4) | (s << 6), 0xF, 0xF, false);
+        int t = __builtin_amdgcn_mov_dpp(__float_as_int(v), s | (s << 2) | (s << 4) | (s << 6), 0xF, 0xF, true);
         if constexpr (HW >= 8) {   // quad SRC / 4 of each 8-lane group to the other quad
             constexpr int q = (SRC >> 2) & 1;
-            const int u = __builtin_amdgcn_update_dpp(0, t, q ? 0x104 : 0x114, 0xF, 0xF, false);
+            const int u = __builtin_amdgcn_mov_dpp(t, q ? 0x104 : 0x114, 0xF, 0xF, true);
             t = (((threadIdx.x >> 2) & 1) == q) ? t : u;
         }
         if constexpr (HW == 16) {  // 8-lane half SRC / 8 to the other half
             constexpr int h = (SRC >> 3) & 1;
-            const int u = __builtin_amdgcn_update_dpp(0, t, h ? 0x108 : 0x118, 0xF, 0xF, false);
+            const int u = __builtin_amdgcn_mov_dpp(t, h ? 0x108 : 0x118, 0xF, 0xF, true);
             t = (((threadIdx.x >> 3) & 1) == h) ? t : u;
         }
         return __int_as_float(t);
