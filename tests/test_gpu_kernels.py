@@ -860,14 +860,15 @@ def test_ffn_fwd_strided_and_unsupported():
 
 
 # ---- factored attention output (p, q) and the head-distributed forward ------------------
-@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (24, 3), (16, 8)])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (24, 3), (16, 8), (128, 2), (256, 2)])
 @pytest.mark.parametrize("split", [False, True])
 def test_gat_factored_alpha_bitexact(F, heads, split):
     """REF mode, gala_gat_fwd_ex_f32 with q_out: alpha_out = p, q_out = 1/(sum + 1e-12),
     and p * q (rounded) is BIT-identical to the materialised alpha of gala_gat_fwd_f32; Y
     is identical too.  The backward on (p, q) equals the backward on alpha bit for bit, and
     so does the dX SpMM over val = p with val_row_scale = q.  Against the oracle within the
-    tolerance (hub-row plan included)."""
+    tolerance (hub-row plan included).  The head widths give 1, 2, 4, 8, 16 and 32 lanes per
+    head: every DPP lane exchange (lane_xor, group_bcast) and the ds_swizzle / shuffle ones."""
     g = powerlaw()
     aL = features(g.n_rows, heads, seed=71)
     aR = features(g.n_cols, heads, seed=72)
@@ -895,7 +896,7 @@ def test_gat_factored_alpha_bitexact(F, heads, split):
 
 
 @pytest.mark.parametrize("mode", [_abi.GALA_SOFTMAX_REF, _abi.GALA_SOFTMAX_FIXED])
-@pytest.mark.parametrize("F,heads", [(256, 8), (64, 4), (32, 2), (48, 3)])
+@pytest.mark.parametrize("F,heads", [(256, 8), (64, 4), (32, 2), (48, 3), (128, 2), (256, 2), (16, 8)])
 def test_gat_multihead_attention_recompute(graph, mode, F, heads):
     """gala_gat_fwd_ex_f32 with aR recomputed per head, aR[j,h] = <X[j, head h], wR[head h]>
     + bR[h] (the multi-head GAT layer's source logit), against the oracle chain on that aR
@@ -989,7 +990,7 @@ def test_gat_bwd_fused_recompute(F, heads, layout_, rc):
         ops.gat_bwd_fused(rect, dev(aL), dev(np.vstack([X, X[:5]])), dev(dY), q, heads=heads, **kw)
 
 
-@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (100, 1)])
+@pytest.mark.parametrize("F,heads", [(32, 1), (47, 1), (256, 8), (64, 4), (100, 1), (128, 2), (256, 2)])
 @pytest.mark.parametrize("layout_", ["plain", "tiled", "split"])
 @pytest.mark.parametrize("rc", [False, True])
 def test_gat_row_stats(F, heads, layout_, rc):
