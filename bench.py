@@ -838,7 +838,7 @@ def run_single(args, dev, be, timer, sync):
                    "n_vertices": hg.n_rows, "edges": hg.nnz, "F": F, "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>") if be.name == "hip" else None,
+                     "traffic": load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>") if be.name == "hip" else None,
                      "kernel": "gala::k_spmm_rowgroup<VEC=4,G=8,CH=1,U=4,unweighted> (gala_spmm_f32, F=32, dst norm)",
                      "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg,
                      "gather_model_GBps": gather_bytes / t_kernel / 1e9,
@@ -968,7 +968,7 @@ def rmat_traffic(hub: str):
     passes of tools/rmat_prof.py, tools/gpu_job.sh pmccmd=rmat + tools/merge_traffic.py), or
     None. exact: the degree-ordered row kernel + the REF-order hub kernel beside it; chunked:
     the rows + hub chunks grid and the chunk fix-up."""
-    names = (("k_spmm_rowgroup<4, 8, 1, 4, false, false, false>", "k_spmm_hub_exact<4, 32, false, false>")
+    names = (("k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>", "k_spmm_hub_exact<4, 32, false, false>")
              if hub == "exact" else ("k_spmm_rows_chunks<4, 8, 1, 4, false, false>", "k_spmm_fixup<4, 8, 1, false>"))
     a, b = (load_traffic("rmat|void gala::" + n) for n in names)
     return a + b if a is not None and b is not None else None
@@ -1010,7 +1010,7 @@ def rmat_family(args, dev, be, timer, sync, kind="rmat"):
                         "frac": alg / t_kernel / HBM_PEAK, "kernel_ms": t_kernel * 1e3,
                         "alg_bytes_per_launch": alg,
                         "traffic": (None if be.name != "hip" else rmat_traffic("exact") if kind == "rmat" else
-                                    load_traffic("banded|void gala::k_spmm_rowgroup<4, 8, 1, 4, false, false, false>")),
+                                    load_traffic("banded|void gala::k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>")),
                         "kernel": "gala_spmm_f32 (degree-ordered k_spmm_rowgroup + k_spmm_hub_exact on a side "
                                   "stream: the hub rows in the reference's order)" if kind == "rmat" else
                                   "gala_spmm_f32 (k_spmm_rowgroup, XCD-ordered row blocks)"}}
