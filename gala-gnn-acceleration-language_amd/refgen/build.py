@@ -42,6 +42,9 @@ PROGRAMS = {
     # the fused ones must give the same prediction and gradients bit for bit
     "gcn3_unfused": ["64", "7", "32", "3", "2", "5000"],
     "gcn3_papers_unfused": ["128", "172", "128", "10", "2", "1000000"],
+    # the GAT program in the base's spelling: its own edge-sum / softmax / aggregation classes
+    # over the mirror's K5 / K7 / K8 / K9 and weighted SpMM (the operator-level drop-in path)
+    "gat_unfused": ["64", "7", "32", "3", "2", "5000"],
 }
 
 

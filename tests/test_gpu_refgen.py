@@ -23,8 +23,11 @@ BIN = os.path.join(rc.PKG, "refgen", "bin")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn3_papers", "gcn_ksample", "gcn_dsample", "gat", "gin", "gin_motion", "sage"])
+@pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn3_papers", "gcn_ksample", "gcn_dsample", "gat", "gat_unfused", "gin",
+                                   "gin_motion", "sage"])
 def test_reference_emitted_program_on_the_gpu(tmp_path, model):
+    """gat_unfused: the base's spelling of the GAT edge chain (its own autograd classes over the
+    mirror's edge operators), gat: HIPGenerator's fused layer; both against galac's IR."""
     exe = os.path.join(BIN, "gala_" + model)
     if not os.path.exists(exe):
         pytest.skip(f"{exe} is not built (refgen/build.py needs the reference's sources)")
@@ -37,7 +40,7 @@ def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     # (128 / 128 / 172) sums its FFN weight gradients over the 20 000 rows in fp32 and has
     # measured up to 6e-5 of the model's largest gradient off on a weight whose own largest
     # entry is small (fc1: 7.4e-8 against 4.3e-4), hence a 1e-4 floor there
-    rc.check_against_galac(model, dump, d, X, tmp_path / "ir.json",
+    rc.check_against_galac(model.replace("_unfused", ""), dump, d, X, tmp_path / "ir.json",
                            noise_floor=1e-4 if model == "gcn3_papers" else 1e-5)
 
 
