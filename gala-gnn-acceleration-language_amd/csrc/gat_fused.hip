@@ -66,7 +66,10 @@ __device__ __forceinline__ void gat_bwd_fused_range(const EdgeParams &p, const G
             for (int ch = 0; ch < CH; ++ch) {
                 if constexpr (!ST)
                     x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
-                yv[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.dY + c[k] * d.lddy + gl_.ln.off[ch]));
+                // nontemporal: the gathered dY rows (2.5 GB at the Products shape, each read ~51
+                // times at random) would otherwise evict the 78 MB aR table every edge also reads
+                // (measured in one process: backward 26.1 -> 24.4 ms, tools/ab_gat.py)
+                yv[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], __builtin_nontemporal_load(reinterpret_cast<const V *>(d.dY + c[k] * d.lddy + gl_.ln.off[ch])));
             }
         if constexpr (RC && !ST) {
             float all[U];

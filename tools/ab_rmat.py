@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""In-process A/B of builds of libgala_hip.so on the R-MAT Products-shape SpMM in the
-reference's hub order (bench.py's "rmat" family, F = 32): tools/ab/libgala_hip_<label>.so and
-"tree" (this tree's build), alternated on the same inputs; medians and bit-identity to the tree.
-Measurement only.    python tools/ab_rmat.py [rounds]
+"""In-process A/B of builds of libgala_hip.so on a Products-shape SpMM, F = 32: the R-MAT graph
+in the reference's hub order (bench.py's "rmat" family) or the uniform graph (the headline's):
+tools/ab/libgala_hip_<label>.so and "tree" (this tree's build), alternated on the same inputs;
+medians and bit-identity to the tree.  Measurement only.
+    python tools/ab_rmat.py [rounds] [rmat|uniform]
 """
 import glob
 import json
@@ -25,7 +26,8 @@ def main():
     libs = {os.path.basename(f)[len("libgala_hip_"):-3]: load(f)
             for f in sorted(glob.glob(os.path.join(ROOT, "tools", "ab", "libgala_hip_*.so")))}
     libs["tree"] = _abi.lib()
-    hg = bench.products_graph("rmat", 1.0)
+    kind = sys.argv[2] if len(sys.argv) > 2 else "rmat"
+    hg = bench.products_graph(kind, 1.0)
     dg = ops.DeviceGraph.from_host(hg)
     X = torch.rand((hg.n_rows, 32), device="cuda") * 2 - 1
     Y = torch.empty_like(X)
@@ -41,7 +43,7 @@ def main():
             if r:
                 samples[k].append(round(t * 1e3, 4))
     _abi._lib = libs["tree"]
-    print(json.dumps({"medians_ms": {k: sorted(v)[len(v) // 2] for k, v in samples.items()}, "samples": samples,
+    print(json.dumps({"graph": kind, "medians_ms": {k: sorted(v)[len(v) // 2] for k, v in samples.items()}, "samples": samples,
                       "bit_identical_to_tree": {k: bool(torch.equal(outs[k], outs["tree"])) for k in libs}}), flush=True)
 
 
