@@ -6,7 +6,9 @@ kernel changes, so the builds run alternately in one process on the same inputs:
 tools/ab/libgala_hip_<label>.so (builds of other commits: git worktree + make) and "tree", this
 tree's gala/libgala_hip.so.  Prints per round fwd / bwd ms of each, the medians, and whether
 each build's outputs are bit-identical to the tree's.  Measurement only.
-    python tools/ab_gat.py [rounds]
+    python tools/ab_gat.py [rounds] [h8|h1f32]
+h1f32: one head at F = 32 with the source logits given (aR, not recomputed: the
+reference-emitted GAT's first layer), the same statistics pair.
 """
 import ctypes
 import json
@@ -33,14 +35,15 @@ def load(path):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    kind = sys.argv[2] if len(sys.argv) > 2 else "h8"
     import glob
     libs = {os.path.basename(f)[len("libgala_hip_"):-3]: load(f)
             for f in sorted(glob.glob(os.path.join(ROOT, "tools", "ab", "libgala_hip_*.so")))}
     libs["tree"] = _abi.lib()
     fns = {k: ctypes.cast(L.gala_gat_fwd_stats_f32, ctypes.c_void_p).value for k, L in libs.items()}
     assert len(set(fns.values())) == len(fns), fns   # every build loaded as its own copy
-    print(json.dumps({"builds": list(libs)}), flush=True)
-    H, F = 8, 256
+    print(json.dumps({"builds": list(libs), "kind": kind}), flush=True)
+    H, F = (8, 256) if kind == "h8" else (1, 32)
     hg = bench.products_graph("uniform", 1.0)
     dg = ops.DeviceGraph.from_host(hg)
     N = hg.n_rows
@@ -50,6 +53,7 @@ def main():
     aL = torch.rand((N, H), device="cuda", generator=gen) - 0.5
     wR = (torch.rand(F, device="cuda", generator=gen) - 0.5) * 0.2
     bR = torch.zeros(H, device="cuda")
+    aR = torch.rand((N, H), device="cuda", generator=gen) - 0.5
     timer = bench.Timer(True)
     outs, samples = {}, {k: [] for k in libs}
     for r in range(rounds + 1):          # round 0: warm-up, not recorded
@@ -58,7 +62,10 @@ def main():
             st = {}
 
             def fwd():
-                st["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+                if kind == "h8":
+                    st["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+                else:
+                    st["f"] = ops.gat_fwd_stats(dg, aL, X, aR=aR, heads=H) + (aR,)
 
             def bwd():
                 Y, q, Ym, sma, aRo = st["f"]

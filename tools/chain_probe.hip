@@ -7,6 +7,10 @@
 //   lds_interleaved one 16-B read between every four adds, 8 quads ahead
 //   lanes < 64     the same loop with only that many lanes of the wave active (the others exit)
 //   lds_b64_ahead2 8-B reads of an edge pair, 8 reads per 16-edge group
+//   row4 / row2    a lane owns 4 (2) features: one 16-B (8-B) read per edge of the lane's
+//                  features, 4 (2) independent chains, reads two 8-edge groups ahead; per edge
+//                  the chains advance one add each (ns_per_add is then per edge)
+//   reg4           the floor of that: 4 chains over registers
 // One workgroup of 64 lanes (one wave), n adds per lane; cycles from s_memtime around the
 // loop (shader clock), time from HIP events.  Measurement only.
 //
@@ -19,7 +23,7 @@
 typedef float F4 __attribute__((ext_vector_type(4)));
 typedef float F2 __attribute__((ext_vector_type(2)));
 
-enum Mode { REG, AHEAD2, AHEAD1, INTERLEAVED, B64 };
+enum Mode { REG, AHEAD2, AHEAD1, INTERLEAVED, B64, ROW4, ROW2, REG4 };
 
 template <int MODE, int LANES>
 __global__ __launch_bounds__(64) void k_chain(const float *seed, float *out, long long *cycles, int n) {
@@ -57,6 +61,52 @@ __global__ __launch_bounds__(64) void k_chain(const float *seed, float *out, lon
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+    } else if constexpr (MODE == REG4) {
+        float a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        for (int i = 0; i < n; i += 16) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                acc = __fadd_rn(acc, r[k]);
+                a1 = __fadd_rn(a1, r[(k + 1) & 15]);
+                a2 = __fadd_rn(a2, r[(k + 2) & 15]);
+                a3 = __fadd_rn(a3, r[(k + 3) & 15]);
+            }
+        }
+        acc += a1 + a2 + a3;
+    } else if constexpr (MODE == ROW4 || MODE == ROW2) {
+        constexpr int NV = MODE == ROW4 ? 4 : 2;
+        typedef float VT __attribute__((ext_vector_type(NV)));
+        constexpr int GE = 8;  // edges per group
+        const VT *b = reinterpret_cast<const VT *>(buf) + (lane & 15);
+        constexpr int WRAP = 1024 * 4 / NV / 16;  // edges in the buffer
+        VT g[3][GE];
+        float a[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) a[v] = 0.0f;
+        int q = 0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int u = 0; u < GE; ++u) g[s][u] = b[((q + u) % WRAP) * 16];
+            q += GE;
+        }
+        for (int i = 0; i < n; i += 3 * GE) {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                const int nx = (s + 2) % 3;
+#pragma unroll
+                for (int u = 0; u < GE; ++u) g[nx][u] = b[((q + u) % WRAP) * 16];
+                q += GE;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < GE; ++u)
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) a[v] = __fadd_rn(a[v], g[s][u][v]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc += a[v];
     } else if constexpr (MODE == REG) {
         for (int i = 0; i < n; i += 16) {
 #pragma unroll
@@ -159,5 +209,10 @@ int main(int argc, char **argv) {
     run<AHEAD2, 4>("lds_ahead2", seed, out, cyc, n);
     run<B64>("lds_b64_ahead2", seed, out, cyc, n);
     run<REG, 16>("reg", seed, out, cyc, n);
+    run<REG4>("reg4", seed, out, cyc, n);
+    run<ROW4>("row4", seed, out, cyc, n);
+    run<ROW4, 8>("row4", seed, out, cyc, n);
+    run<ROW2>("row2", seed, out, cyc, n);
+    run<ROW2, 16>("row2", seed, out, cyc, n);
     return 0;
 }
