@@ -147,11 +147,17 @@ __device__ __forceinline__ void gat_fwd_range_dist(const EdgeParams &p, const Ga
                 ar[i] = d.aR[(int64_t)p.col[e0 + j] * H + hh];
             }
         }
+        // given source logits: the X rows are loaded nontemporal, so the gathered rows do not
+        // evict the aR table every edge also reads a line of (one head, F = 32, the Products
+        // graph: 4.31 -> 3.87 ms in one process, tools/ab_gat.py h1f32).  Recomputed logits
+        // read no such table, and there the hint only costs the rows' reuse.
 #pragma unroll
         for (int k = 0; k < U; ++k)
 #pragma unroll
-            for (int ch = 0; ch < CH; ++ch)
-                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], *reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]));
+            for (int ch = 0; ch < CH; ++ch) {
+                const V *xp = reinterpret_cast<const V *>(d.X + c[k] * d.ldx + gl_.ln.off[ch]);
+                x[k][ch] = mask_pad<VEC>(gl_.ln.nv[ch], RC ? *xp : __builtin_nontemporal_load(xp));
+            }
         if (store && pend_j0 >= 0) {
 #pragma unroll
             for (int i = 0; i < NK; ++i)  // a previous batch is always full

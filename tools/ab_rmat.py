@@ -3,7 +3,8 @@
 in the reference's hub order (bench.py's "rmat" family) or the uniform graph (the headline's):
 tools/ab/libgala_hip_<label>.so and "tree" (this tree's build), alternated on the same inputs;
 medians and bit-identity to the tree.  Measurement only.
-    python tools/ab_rmat.py [rounds] [rmat|uniform]
+    python tools/ab_rmat.py [rounds] [rmat|uniform] [spmm|sddvv|sddmm]
+sddvv: K5 (ADD, one head: a[row] + b[col] per edge); sddmm: K9 at F = 32.
 """
 import glob
 import json
@@ -29,21 +30,34 @@ def main():
     kind = sys.argv[2] if len(sys.argv) > 2 else "rmat"
     hg = bench.products_graph(kind, 1.0)
     dg = ops.DeviceGraph.from_host(hg)
+    op = sys.argv[3] if len(sys.argv) > 3 else "spmm"
     X = torch.rand((hg.n_rows, 32), device="cuda") * 2 - 1
+    a = torch.rand(hg.n_rows, device="cuda") - 0.5
+    b = torch.rand(hg.n_rows, device="cuda") - 0.5
     Y = torch.empty_like(X)
+    res = {}
+
+    def run():
+        if op == "spmm":
+            ops.spmm(dg, X, out=Y)
+            res["y"] = Y
+        elif op == "sddvv":
+            res["y"] = ops.sddvv(dg, a, b)
+        else:
+            res["y"] = ops.sddmm(dg, X, X)
     timer = bench.Timer(True)
     outs, samples = {}, {k: [] for k in libs}
     for r in range(rounds + 1):
         for k in libs:
             _abi._lib = libs[k]
-            ops.spmm(dg, X, out=Y)
+            run()
             torch.cuda.synchronize()
-            outs.setdefault(k, Y.clone())
-            t = timer(lambda: ops.spmm(dg, X, out=Y), 10)
+            outs.setdefault(k, res["y"].clone())
+            t = timer(run, 10)
             if r:
                 samples[k].append(round(t * 1e3, 4))
     _abi._lib = libs["tree"]
-    print(json.dumps({"graph": kind, "medians_ms": {k: sorted(v)[len(v) // 2] for k, v in samples.items()}, "samples": samples,
+    print(json.dumps({"graph": kind, "op": op, "medians_ms": {k: sorted(v)[len(v) // 2] for k, v in samples.items()}, "samples": samples,
                       "bit_identical_to_tree": {k: bool(torch.equal(outs[k], outs["tree"])) for k in libs}}), flush=True)
 
 
