@@ -3,8 +3,8 @@
 in the reference's hub order (bench.py's "rmat" family) or the uniform graph (the headline's):
 tools/ab/libgala_hip_<label>.so and "tree" (this tree's build), alternated on the same inputs;
 medians and bit-identity to the tree.  Measurement only.
-    python tools/ab_rmat.py [rounds] [rmat|uniform] [spmm|sddvv|sddmm]
-sddvv: K5 (ADD, one head: a[row] + b[col] per edge); sddmm: K9 at F = 32.
+    python tools/ab_rmat.py [rounds] [rmat|uniform] [spmm|wspmm|sddvv|sddmm]
+wspmm: the SpMM with one value per edge; sddvv: K5 (ADD, one head: a[row] + b[col] per edge); sddmm: K9 at F = 32.
 """
 import glob
 import json
@@ -35,11 +35,15 @@ def main():
     a = torch.rand(hg.n_rows, device="cuda") - 0.5
     b = torch.rand(hg.n_rows, device="cuda") - 0.5
     Y = torch.empty_like(X)
+    gw = dg.with_values(torch.rand(hg.nnz, device="cuda")) if op == "wspmm" else None
     res = {}
 
     def run():
         if op == "spmm":
             ops.spmm(dg, X, out=Y)
+            res["y"] = Y
+        elif op == "wspmm":
+            ops.spmm(gw, X, out=Y)
             res["y"] = Y
         elif op == "sddvv":
             res["y"] = ops.sddvv(dg, a, b)
