@@ -470,15 +470,24 @@ class Lowering {
     void auto_schedule() {
         Schedule &s = m_.sched;
         int64_t nrows = 0, nvals = 0, feat = 0, classes = 0;
-        std::string dir = s.opt_input;
+        // the reference joins the file names straight onto the path as written
+        // (gala_inference.cpp:102-117, common.h:342), so a prefix ("data/reddit_") is tried
+        // first as it stands, then as a directory ('/' added), then from the DSL file's directory
+        const std::string asis = s.opt_input;
+        std::string dir = asis;
         if (!dir.empty() && dir.back() != '/') dir += '/';
         std::string from;
         const std::string src_dir = m_.source.find('/') == std::string::npos
                                         ? std::string()
                                         : m_.source.substr(0, m_.source.rfind('/') + 1);
-        if (read_dataset_facts(dir, &nrows, &nvals, &feat, &classes)) {
+        const bool rel = !asis.empty() && asis[0] != '/';
+        if (!asis.empty() && read_dataset_facts(asis, &nrows, &nvals, &feat, &classes)) {
+            from = "the files at " + asis;
+        } else if (read_dataset_facts(dir, &nrows, &nvals, &feat, &classes)) {
             from = "the files in " + dir;
-        } else if (!src_dir.empty() && dir[0] != '/' &&
+        } else if (!src_dir.empty() && rel && read_dataset_facts(src_dir + asis, &nrows, &nvals, &feat, &classes)) {
+            from = "the files at " + src_dir + asis;
+        } else if (!src_dir.empty() && rel &&
                    read_dataset_facts(src_dir + dir, &nrows, &nvals, &feat, &classes)) {
             from = "the files in " + src_dir + dir;
         } else {

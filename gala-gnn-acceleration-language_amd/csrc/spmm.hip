@@ -1043,7 +1043,10 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             q.X = X ? X + c0 : nullptr;
             q.Y = Y + c0;
             q.Y2 = Y2 ? Y2 + c0 : nullptr;
-            q.relu_x = relu_x ? relu_x + c0 : nullptr;
+            // the ReLU backward belongs to the finished row: only the launch of the last segment
+            // group applies it (earlier launches leave the partial sums for it to accumulate)
+            q.relu_x = relu_x && seg0 + kMaxSegPerLaunch >= A->n_seg ? relu_x + c0 : nullptr;
+            if (!q.relu_x) q.relu_act = nullptr;
             q.F = Fc;
             q.accum = accum;
             const int L = (int)((Fc + vec - 1) / vec);

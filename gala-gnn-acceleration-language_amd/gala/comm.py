@@ -72,21 +72,24 @@ class _Works:
             w.wait()
 
 
-def a2a_rounds(in_splits, out_splits, world: int, row_bytes: int, max_rows=None):
+def a2a_rounds(in_splits, out_splits, world: int, row_bytes: int, max_rows=None, strict=True):
     """The rounds of an all-to-all cut at MAX_MSG_BYTES: a list of (ins, outs), ins[q] the
     (start, stop) rows of the input sent to rank q in that round, outs[q] the rows of the output
     received from rank q.  Round j carries rows [j*r, (j+1)*r) of every block, r =
     MAX_MSG_BYTES // (world * row_bytes), so one round's message is at most MAX_MSG_BYTES; the
     round count comes from max_rows, a bound on every rank's blocks that all ranks pass alike
     (they must issue the same collectives), or from this rank's largest block.  One round when
-    nothing needs cutting."""
+    nothing needs cutting.  strict=False (the uncut host-staged path, which only records the
+    plan) takes the larger of the two instead of refusing a block past max_rows; the ranks'
+    agreement on the bound is checked collectively once per exchange plan
+    (Comm.check_block_bound)."""
     in_splits, out_splits = [int(v) for v in in_splits], [int(v) for v in out_splits]
     r = max(MAX_MSG_BYTES // (world * row_bytes), 1)
     biggest = max(in_splits + out_splits + [0])
-    if max_rows is not None and biggest > int(max_rows):
+    if strict and max_rows is not None and biggest > int(max_rows):
         # rows past rounds * r would never be sent, and the output would keep stale rows
         raise ValueError(f"a2a_rounds: a block of {biggest} rows exceeds max_rows={int(max_rows)}")
-    m = biggest if max_rows is None else int(max_rows)
+    m = biggest if max_rows is None else max(int(max_rows), biggest)
     rounds = max(-(-m // r), 1)
     io, oo = [0] * world, [0] * world
     for q in range(1, world):
@@ -189,7 +192,10 @@ class Comm:
         number of rounds when the exchange is cut at MAX_MSG_BYTES); default: this rank's
         largest block, which is only safe when no rank's exchange needs cutting."""
         rb = _row_bytes(inp)
-        rounds = a2a_rounds(in_splits, out_splits, self.world, rb, max_rows)
+        # only the RCCL path cuts (and so depends on the agreed bound); a block past it raises
+        # here on the ranks that hold it -- check_block_bound, run when the plan is built, makes
+        # every rank raise together before any exchange is posted
+        rounds = a2a_rounds(in_splits, out_splits, self.world, rb, max_rows, strict=self.rccl)
         _note("all_to_all", max(sum(b - a for a, b in ins) for ins, _ in rounds) * rb,
               sum(int(v) for v in in_splits) * rb, len(rounds))
         if self.rccl:
@@ -205,6 +211,17 @@ class Comm:
                                input_split_sizes=list(in_splits), group=self.group)
         self._back(out, ho)
         return None
+
+    def check_block_bound(self, biggest: int, max_rows: int) -> None:
+        """Collective: raise ValueError on EVERY rank when any rank's largest all-to-all block
+        (biggest rows) exceeds the max_rows bound all ranks cut their exchanges by.  A rank
+        that raised alone would leave its peers waiting inside the next collective."""
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.rccl else torch.device("cpu")
+        t = torch.tensor([int(biggest)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        worst = int(t.item())
+        if worst > int(max_rows):
+            raise ValueError(f"all_to_all: a block of {worst} rows (some rank) exceeds max_rows={int(max_rows)}")
 
     def exchange(self, sends, recvs):
         """Grouped point-to-point: sends = [(tensor, peer)], recvs = [(tensor, peer)]."""

@@ -268,6 +268,9 @@ class _PartialRows:
             self._ss = [sp.send_counts[k].tolist() for k in range(K)]
             self._rs = [sp.recv_counts[k].tolist() for k in range(K)]
             self.n_send, self.n_recv = max(int(so[-1]), 1), max(int(ro[-1]), 1)
+            if comm is not None:  # every rank agrees that no block passes the cut's bound
+                biggest = max([int(v) for k in range(K) for v in self._ss[k] + self._rs[k]] + [0])
+                comm.check_block_bound(biggest, c)
         else:
             self.graphs = [backend.graph(h, split=thr) for h in part.chunk_graphs]
             self._send = [(k * P * c, (k + 1) * P * c) for k in range(K)]

@@ -93,7 +93,13 @@ typedef struct gala_split_plan {
                                   then the hub rows, longest first, the order in which
                                   the REF-order hub kernel takes them.                   */
     void *aux_stream;          /* hipStream_t or NULL: where the REF-order hub rows run   */
-    void *aux_events[2];       /* hipEvent_t fork / join pair for aux_stream (both or none) */
+    void *aux_events[2];       /* hipEvent_t fork / join pair for aux_stream (both or none).
+                                  Every hub fork of the plan (gala_spmm_ex_f32,
+                                  gala_row_sum_f32) records and waits on these two events,
+                                  so a plan serves ONE caller stream at a time: calls on one
+                                  graph from two host threads / streams must be ordered by
+                                  the caller (or use a plan each), else one call's join can
+                                  wait on the other's fork.                               */
 } gala_split_plan_t;
 
 typedef struct gala_csr {

@@ -71,12 +71,13 @@ def run_program(exe, root, device, timeout=300, seed=None):
     return read_dump(dump)
 
 
-def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
+def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6, floors=None):
     """The dump's first-epoch prediction, loss and weight gradients against galac's program
     of the same DSL (tests/dsl/<model>_ref_codegen.txt) in the float64 IR executor.
     noise_floor: the gradient tolerance's share of the model's largest gradient. The REF GAT
     chain's attention-bias gradient is N * 1e-12 plus per-row softmax-gradient sums that cancel
-    exactly, so its fp32 value is rounding noise that grows with the row count N."""
+    exactly, so its fp32 value is rounding noise that grows with the row count N.
+    floors: {weight name: noise floor} for the tensors that need a looser one than the rest."""
     want_params = {"prediction", "loss", "fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"}
     if model in ("gcn3", "gcn3_papers"):
         want_params |= {"fc2.weight", "fc2.bias"}
@@ -121,5 +122,5 @@ def check_against_galac(model, dump, d, X, ir_path, noise_floor=1e-6):
     top = max(np.abs(p.grad.numpy()).max() for p in params.values())
     for k, p in params.items():
         want, got = p.grad.numpy(), dump[k + ".grad"]
-        tol = 1e-4 * np.abs(want).max() + noise_floor * top
+        tol = 1e-4 * np.abs(want).max() + (floors or {}).get(k, noise_floor) * top
         assert np.abs(got - want).max() <= tol, (k, np.abs(got - want).max(), tol)

@@ -80,3 +80,53 @@ def test_p2p_pieces_cover_the_message_in_order():
         assert len(gcomm.p2p_pieces(3 << 20, 1024)) == 3     # 3 GiB of 1-KB rows: 3 pieces
     finally:
         gcomm.MAX_MSG_BYTES = old
+
+
+def _bound_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    from gala.comm import Comm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = Comm()
+        c.check_block_bound(5, 8)                       # every block within the bound: no error
+        try:                                            # only rank 1 holds a block past it
+            c.check_block_bound(12 if rank == 1 else 3, 8)
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, str(e)))
+        # the uncut (gloo) exchange records a plan past the bound instead of refusing it
+        rounds = gcomm.a2a_rounds([12, 3, 0], [3, 3, 3], world, 4, max_rows=8, strict=False)
+        assert len(rounds) == 1
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_block_bound_raises_on_every_rank():
+    """a2a_rounds refused an oversize block only on the ranks that held it, so its
+    peers went on into the all-to-all and hung.  Comm.check_block_bound (run when a sparse
+    vertex-cut plan is built) all-reduces the largest block: every rank raises together."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bound_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(got) == [0, 1, 2]
+    assert all("12 rows" in v and "max_rows=8" in v for v in got.values()), got
+    with pytest.raises(ValueError):
+        gcomm.a2a_rounds([12, 3], [3, 3], 2, 4, max_rows=8)

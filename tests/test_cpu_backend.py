@@ -331,14 +331,14 @@ def test_row_scale_relu_and_backward_match_numpy():
     np.testing.assert_array_equal(dX, np.where(r <= 0, np.float32(0), G) * act[:, None])
 
 
-@pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("tiled", [0, 900, 20])
 def test_spmm_relu_prologue_and_epilogue_match_the_passes(tiled):
     """gala_spmm_ex_f32's ReLU fields against the passes they fold, bit for bit: the source
     pre * relu(act * X) (gala_row_scale_relu_f32, then the SpMM) and the ReLU backward of the
     result (the SpMM, then gala_relu_scale_backward_f32), one segment and column-tiled;
     refusals on weighted / sampled graphs and for src_act without src_relu."""
     g = cora_like()
-    A = HostCsr(layout.col_tile(g, 900) if tiled else g)
+    A = HostCsr(layout.col_tile(g, tiled) if tiled else g)  # 20: 136 segments
     n, F = g.n_rows, 13
     rng = np.random.default_rng(8)
     X = rng.uniform(-1, 1, (n, F)).astype(np.float32)

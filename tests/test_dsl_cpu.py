@@ -226,6 +226,15 @@ def test_opt_input_schedule_from_dataset_files(n, m, tiled, tmp_path):
     # from the DSL file's directory
     prog.write_text(_opt_input_dsl("data/"))
     assert galac(str(prog), tmp_path)["post"]["sched"]["feat_size"] == 13
+    # the reference joins the file names straight onto the path (gala_inference.cpp:102-117):
+    # a prefix path finds files named <prefix>Adj_src.npy ...
+    pre = tmp_path / "pfx"
+    _write_dataset(pre, n, m, feat=9, classes=4)
+    for f in ("Adj_src", "Adj_dst", "Feat", "Lab"):
+        (pre / f"{f}.npy").rename(tmp_path / f"reddit_{f}.npy")
+    prog.write_text(_opt_input_dsl(str(tmp_path / "reddit_")))
+    s = galac(str(prog), tmp_path)["post"]["sched"]
+    assert (s["feat_size"], s["label_size"]) == (9, 4)
 
 
 @pytest.mark.skipif(not REF_DSL, reason="the reference's DSL corpus is not in this container")

@@ -39,9 +39,10 @@ def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     # 1.5e-2 largest gradient (the same on the host backend); the GCN-3 at config 5's widths
     # (128 / 128 / 172) sums its FFN weight gradients over the 20 000 rows in fp32 and has
     # measured up to 6e-5 of the model's largest gradient off on a weight whose own largest
-    # entry is small (fc1: 7.4e-8 against 4.3e-4), hence a 1e-4 floor there
-    rc.check_against_galac(model.replace("_unfused", ""), dump, d, X, tmp_path / "ir.json",
-                           noise_floor=1e-4 if model == "gcn3_papers" else 1e-5)
+    # entry is small (fc1: 7.4e-8 against 4.3e-4), hence a 1e-4 floor for that one tensor;
+    # every other gradient keeps the 1e-5 floor
+    rc.check_against_galac(model.replace("_unfused", ""), dump, d, X, tmp_path / "ir.json", noise_floor=1e-5,
+                           floors={"fc1.weight": 1e-4} if model == "gcn3_papers" else None)
 
 
 @pytest.mark.gpu
