@@ -71,6 +71,56 @@ def test_config2_arxiv_gcn2_step_bitexact():
 
 
 @pytest.mark.timeout(300)
+def test_headline_products_gcn2_fused_step_bitexact():
+    """The headline workload itself: bench.py's OneGpuGCN + make_fused_step on its uniform
+    Products graph (N = 2 449 029, E = 126 167 309, F = 32 -- the graph, width and step the
+    BENCH line times), all four outputs (H1, H2, G1, G0) on EVERY row bit-exact against the
+    oracle's degree-normed chain (codegen/gala.cu:433-456: norm = deg^-1/2 from the
+    degree pass, then norm * A (norm * H) per aggregation)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from gala.backend import HipBackend
+    _threads()
+    F = 32
+    g = bench.products_graph("uniform", 1.0)
+    assert (g.n_rows, g.nnz) == (bench.PRODUCTS_N, bench.PRODUCTS_E)
+    be = HipBackend("cuda")
+    agg = bench.OneGpuGCN(g, F, be)
+    gen = torch.Generator(device="cuda").manual_seed(2024)
+    X = torch.rand((g.n_rows, F), device="cuda", generator=gen) * 2 - 1
+    dY = torch.rand((g.n_rows, F), device="cuda", generator=gen) * 2 - 1
+    bufs = [be.empty(g.n_rows, F) for _ in range(4)]
+    step = bench.make_fused_step(agg, X, dY, bufs)
+    step()
+    step()                                   # a second step overwrites every output alike
+    torch.cuda.synchronize()
+    og = orc.Graph(g.n_rows, g.n_cols, g.rowptr, g.col)
+    norm = orc.degree(og, power=-0.5)
+    xh, dyh = X.cpu().numpy(), dY.cpu().numpy()
+    H1 = orc.spmm(og, xh, src_scale=norm, dst_scale=norm)
+    H2 = orc.spmm(og, H1, src_scale=norm, dst_scale=norm)
+    G1 = orc.spmm(og, dyh, src_scale=norm, dst_scale=norm)
+    G0 = orc.spmm(og, G1, src_scale=norm, dst_scale=norm)
+    for name, got, want in zip(("H1", "H2", "G1", "G0"), bufs, (H1, H2, G1, G0)):
+        np.testing.assert_array_equal(got.cpu().numpy(), want, err_msg=name)
+
+
+def _assert_source_logits(aR, X, wR, bR, H, cols):
+    """The kernels' recomputed source logits aR[c] = <X[c, head h], wR_h> + bR[h] against the
+    float64 per-head Linear (common.h:1248-1260) on the columns the oracle layer reads, 1e-5."""
+    D = X.shape[1] // H
+    w = wR.cpu().double().view(H, D)
+    b = bR.cpu().double()
+    got = aR.view(-1, H)
+    for i in range(0, len(cols), 65536):
+        c = torch.from_numpy(cols[i:i + 65536]).cuda()
+        xc = X[c].cpu().double().view(-1, H, D)
+        want = (xc * w[None]).sum(-1) + b[None]
+        np.testing.assert_allclose(got[c].cpu().double().numpy(), want.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.timeout(300)
 def test_config3_products_gat8_rows_against_ref_layer():
     _threads()
     H, D = 8, 32
@@ -96,6 +146,9 @@ def test_config3_products_gat8_rows_against_ref_layer():
     np.testing.assert_allclose(Y[:k].cpu().numpy(), ref.Y, **TOL)
     np.testing.assert_allclose(dX[:k].cpu().numpy(), ref.dX, **TOL)
     np.testing.assert_allclose(daL.view(-1, H)[:k].cpu().numpy(), ref.daL, **TOL)
+    # the aR handed to the oracle is itself checked: the float64 Linear on every column those
+    # rows read (and the rows themselves), at size
+    _assert_source_logits(aR, X, wR, bR, H, np.unique(np.concatenate([g.col[:g.rowptr[k]], np.arange(k)])))
 
 
 @pytest.mark.timeout(300)

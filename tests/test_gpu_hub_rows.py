@@ -218,6 +218,10 @@ def test_config3_rmat_hub_rows_against_ref_layer(rmat):
     check("rmat_stats_Y", Y[rt].cpu().numpy(), ref.Y, hr)
     check("rmat_stats_dX", dX[rt].cpu().numpy(), ref.dX, hr)
     check("rmat_stats_daL", daL.view(-1, H)[rt].cpu().numpy(), ref.daL, hr)
+    # the kernels' source logits themselves: the float64 per-head Linear on every column the
+    # checked rows read, at size (tests/test_gpu_configs.py)
+    from test_gpu_configs import _assert_source_logits
+    _assert_source_logits(aR, X, wR, bR, H, np.unique(np.concatenate([col, rows])).astype(np.int64))
 
 
 @pytest.mark.timeout(600)
