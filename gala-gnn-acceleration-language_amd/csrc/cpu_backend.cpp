@@ -1144,3 +1144,246 @@ extern "C" int gala_cpu_dense_grad_f32(int64_t n_rows, int32_t K, int32_t M, con
         }
     return GALA_OK;
 }
+
+// ---- the multi-head GAT layer in input space (gala_gat_in_*, gat_input.hip) -------------
+// The same extended rows and the same sums in the same order as the gfx950 kernels (the
+// matrix cores' k-ordered fmaf chains: the edges of a row in CSR order; the projection over
+// the feature tiles; the backward's column partials per persistent workgroup, summed in
+// workgroup order); exp is the host's, so values agree to fp32 rounding.
+namespace {
+
+constexpr int kInLd = 128, kInMaxFin = 100, kInMaxHeads = 8, kInTiles = 7, kInWaves = 8, kInGrid = 512;
+constexpr int kOnesSlot = 112;
+inline int aR_slot(int h) { return 67 + 4 * h; }
+inline int aL_slot(int h) { return 99 + 4 * h; }
+inline int q_slot(int h) { return 116 + 4 * (h / 3) + h % 3; }
+inline int tile_feature(int t, int m, int fin) {
+    int f;
+    if (t < 4) f = 4 * m + t;
+    else if (m < 12) f = 64 + 3 * m + (t - 4);
+    else return (m == 12 && t == 4) ? -2 : -1;
+    return f < fin ? f : -1;
+}
+// extended-row slot of tile t's row m (the kernels' lane / component layout)
+inline int tile_slot(int t, int m) { return t < 4 ? 4 * m + t : 64 + 4 * m + (t - 4); }
+
+int check_in_graph(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (fin < 1 || heads < 1 || D < 1) return GALA_ERR_INVALID_ARG;
+    if (fin > kInMaxFin || heads > kInMaxHeads || !(D == 4 || D == 8 || D == 16 || D == 32) || A->n_seg != 1 ||
+        A->n_rows != A->n_cols || (A->split && A->split->n_rows_split > 0))
+        return GALA_ERR_UNSUPPORTED;
+    return GALA_OK;
+}
+
+// the d_aL dots over D / 4 lanes of four features each, summed by the kernels' xor butterfly
+float butterfly_dot(const float *a, const float *b, int D) {
+    float v[8];
+    const int L = D / 4;
+    for (int l = 0; l < L; ++l) {
+        float s = 0.0f;
+        for (int i = 0; i < 4; ++i) s = fmaf(a[4 * l + i], b[4 * l + i], s);
+        v[l] = s;
+    }
+    for (int o = L / 2; o >= 1; o /= 2) {
+        float w[8];
+        for (int l = 0; l < L; ++l) w[l] = v[l] + v[l ^ o];
+        for (int l = 0; l < L; ++l) v[l] = w[l];
+    }
+    return v[0];
+}
+
+}  // namespace
+
+extern "C" int gala_cpu_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t ldxin, int32_t heads,
+                                        const float *u, const float *c, float *Xext, void *stream) {
+    (void)stream;
+    if (n < 0 || fin < 1 || heads < 1 || ldxin < fin) return GALA_ERR_INVALID_ARG;
+    if (fin > kInMaxFin || heads > kInMaxHeads) return GALA_ERR_UNSUPPORTED;
+    if (n == 0) return GALA_OK;
+    if (!Xin || !u || !c || !Xext) return GALA_ERR_INVALID_ARG;
+    const int H = heads;
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < n; ++r) {
+        const float *x = Xin + r * ldxin;
+        float *o = Xext + r * kInLd;
+        float lg[2 * kInMaxHeads] = {0.0f};
+        for (int f = 0; f < fin; ++f)
+            for (int k = 0; k < 2 * H; ++k) lg[k] = fmaf(x[f], u[k * fin + f], lg[k]);
+        for (int s = 0; s < kInLd; ++s) {
+            float v = 0.0f;
+            if (s < 64) {
+                v = s < fin ? x[s] : 0.0f;
+            } else {
+                const int nn = (s - 64) >> 2, cc = (s - 64) & 3;
+                if (cc < 3 && nn < 12) {
+                    const int f = 64 + 3 * nn + cc;
+                    v = f < fin ? x[f] : 0.0f;
+                } else if (s == kOnesSlot) {
+                    v = 1.0f;
+                } else if (cc == 3 && nn < kInMaxHeads) {
+                    v = nn < H ? lg[H + nn] + c[H + nn] : 0.0f;
+                } else if (cc == 3) {
+                    v = nn - 8 < H ? lg[nn - 8] + c[nn - 8] : 0.0f;
+                }
+            }
+            o[s] = v;
+        }
+    }
+    return GALA_OK;
+}
+
+extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+                                       float *Xext, const float *W, int64_t ldw, const float *b, float *Y,
+                                       float *Ym, int64_t ldy, float *q, float *sma, void *stream) {
+    (void)stream;
+    int st = check_in_graph(A, fin, heads, D);
+    if (st) return st;
+    if (ldw < fin || ldy < (int64_t)heads * D) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!Xext || !W || !Y || !Ym || !q || !sma) return GALA_ERR_INVALID_ARG;
+    const int H = heads;
+    const int32_t *order = A->split ? A->split->row_order : nullptr;
+    std::vector<float> qv((size_t)A->n_rows * H);
+#pragma omp parallel
+    {
+        std::vector<float> Z((size_t)16 * kInTiles * 16);   // [variant][tile][m]
+#pragma omp for schedule(dynamic, kRowChunk)
+        for (int64_t ri = 0; ri < A->n_rows; ++ri) {
+            const int64_t r = order ? order[ri] : ri;
+            std::fill(Z.begin(), Z.end(), 0.0f);
+            const float *xr = Xext + r * kInLd;
+            for (int64_t e = A->rowptr[r]; e < A->rowptr[r + 1]; ++e) {
+                const float *xc = Xext + (int64_t)A->col[e] * kInLd;
+                float pv[8], mp[8];
+                for (int h = 0; h < 8; ++h) {
+                    pv[h] = mp[h] = 0.0f;
+                    if (h >= H) continue;
+                    const float t = xr[aL_slot(h)] + xc[aR_slot(h)];
+                    const bool pos = t > 0.0f;
+                    pv[h] = ref_exp(pos ? t : t * slope);
+                    mp[h] = pos ? pv[h] : pv[h] * slope;
+                }
+                for (int v = 0; v < 16; ++v) {
+                    const float bv = v < 8 ? pv[v] : mp[v - 8];
+                    for (int t = 0; t < kInTiles; ++t)
+                        for (int m = 0; m < 16; ++m) {
+                            const float a = (t >= 4 && m >= 13) ? 0.0f : xc[tile_slot(t, m)];
+                            float &z = Z[((size_t)v * kInTiles + t) * 16 + m];
+                            z = fmaf(a, bv, z);
+                        }
+                }
+            }
+            for (int h = 0; h < H; ++h) {
+                const float S = Z[((size_t)h * kInTiles + 4) * 16 + 12];
+                const float Sm = Z[((size_t)(h + 8) * kInTiles + 4) * 16 + 12];
+                const float qq = 1.0f / (S + 1e-12f);
+                for (int j = 0; j < D; ++j) {
+                    float y0 = 0.0f, y1 = 0.0f;
+                    const int64_t o = (int64_t)h * D + j;
+                    for (int t = 0; t < kInTiles; ++t)
+                        for (int q4 = 0; q4 < 4; ++q4)
+                            for (int kq = 0; kq < 4; ++kq) {
+                                const int m = 4 * kq + q4, f = tile_feature(t, m, fin);
+                                const float w = f >= 0 ? W[o * ldw + f] : (f == -2 && b ? b[o] : 0.0f);
+                                y0 = fmaf(Z[((size_t)h * kInTiles + t) * 16 + m], w, y0);
+                                y1 = fmaf(Z[((size_t)(h + 8) * kInTiles + t) * 16 + m], w, y1);
+                            }
+                    Y[r * ldy + o] = qq * y0;
+                    Ym[r * ldy + o] = qq * y1;
+                }
+                q[r * H + h] = qq;
+                qv[(size_t)r * H + h] = qq;
+                sma[r * H + h] = qq * Sm;
+            }
+        }
+    }
+    // q into the extended rows after every row has read its neighbours' (as the kernels'
+    // slots, which no aggregation reads)
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < A->n_rows; ++r)
+        for (int h = 0; h < H; ++h) Xext[r * kInLd + q_slot(h)] = qv[(size_t)r * H + h];
+    return GALA_OK;
+}
+
+extern "C" int64_t gala_cpu_gat_in_bwd_workspace(int32_t heads) {
+    if (heads < 1 || heads > kInMaxHeads) return -1;
+    return (int64_t)kInGrid * heads * 2 * kInTiles * 64 * 4 * (int64_t)sizeof(float);
+}
+
+extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+                                       const float *Xext, const float *dY, const float *Y, const float *Ym,
+                                       int64_t ldy, const float *sma, float *daL, float *M, void *ws,
+                                       int64_t ws_bytes, void *stream) {
+    (void)stream;
+    int st = check_in_graph(AT, fin, heads, D);
+    if (st) return st;
+    if (ldy < (int64_t)heads * D || (ldy & 3)) return GALA_ERR_INVALID_ARG;
+    if (!M) return GALA_ERR_INVALID_ARG;
+    const int H = heads;
+    const int64_t outn = (int64_t)H * D * (fin + 1);
+    std::fill(M, M + outn, 0.0f);
+    if (AT->n_rows == 0) return GALA_OK;
+    if (!Xext || !dY || !Y || !Ym || !sma || !daL || !ws) return GALA_ERR_INVALID_ARG;
+    if (ws_bytes < gala_cpu_gat_in_bwd_workspace(heads)) return GALA_ERR_INVALID_ARG;
+    const int32_t *order = AT->split ? AT->split->row_order : nullptr;
+    const int64_t n = AT->n_rows, nblk = (n + kInWaves - 1) / kInWaves;
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
+    const int64_t per = (int64_t)H * D * (fin + 1);
+    float *part = (float *)ws;   // [grid][H][D][fin + 1]
+    const int F = H * D;
+#pragma omp parallel
+    {
+        std::vector<float> T((size_t)kInMaxHeads * kInTiles * 16);
+#pragma omp for schedule(dynamic, 1)
+        for (int g = 0; g < grid; ++g) {
+            float *Mg = part + (int64_t)g * per;
+            std::fill(Mg, Mg + per, 0.0f);
+            for (int64_t blk = g; blk < nblk; blk += grid)
+                for (int w = 0; w < kInWaves; ++w) {
+                    const int64_t ci = blk * kInWaves + w;
+                    if (ci >= n) break;
+                    const int64_t c = order ? order[ci] : ci;
+                    std::fill(T.begin(), T.end(), 0.0f);
+                    const float *xc = Xext + c * kInLd;
+                    for (int64_t e = AT->rowptr[c]; e < AT->rowptr[c + 1]; ++e) {
+                        const float *xr = Xext + (int64_t)AT->col[e] * kInLd;
+                        for (int h = 0; h < H; ++h) {
+                            const float t = xr[aL_slot(h)] + xc[aR_slot(h)];
+                            const float a = ref_exp(t > 0.0f ? t : t * slope) * xr[q_slot(h)];
+                            for (int tt = 0; tt < kInTiles; ++tt)
+                                for (int m = 0; m < 16; ++m) {
+                                    const float x = (tt >= 4 && m >= 13) ? 0.0f : xr[tile_slot(tt, m)];
+                                    float &z = T[((size_t)h * kInTiles + tt) * 16 + m];
+                                    z = fmaf(x, a, z);
+                                }
+                        }
+                    }
+                    for (int h = 0; h < H; ++h) {
+                        const float *dy = dY + c * ldy + (int64_t)h * D;
+                        const float sy = butterfly_dot(dy, Y + c * ldy + (int64_t)h * D, D);
+                        const float sm = butterfly_dot(dy, Ym + c * ldy + (int64_t)h * D, D);
+                        const float accv = sy + 1e-12f;
+                        daL[c * H + h] = (sm - accv * sma[c * H + h]) + 1e-12f;
+                        for (int j = 0; j < D; ++j)
+                            for (int tt = 0; tt < kInTiles; ++tt)
+                                for (int m = 0; m < 16; ++m) {
+                                    const int f = tile_feature(tt, m, fin);
+                                    if (f == -1) continue;
+                                    float &z = Mg[((int64_t)h * D + j) * (fin + 1) + (f == -2 ? fin : f)];
+                                    z = fmaf(dy[j], T[((size_t)h * kInTiles + tt) * 16 + m], z);
+                                }
+                    }
+                }
+        }
+    }
+    (void)F;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < per; ++i) {
+        float s = 0.0f;
+        for (int g = 0; g < grid; ++g) s += part[(int64_t)g * per + i];
+        M[i] = s;
+    }
+    return GALA_OK;
+}

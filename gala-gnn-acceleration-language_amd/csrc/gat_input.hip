@@ -1,0 +1,505 @@
+// gat_input.hip -- config 3's multi-head GAT layer in input space (round 6).
+//
+// The layer (tests/GALA-DSL/gat/*, galac gat_heads(H)) is
+//     v1 = Xin W^T + b                 FFN_OP, Xin [N, fin] -> H heads of D
+//     aL = head_attn(v1, wL, bL)       attnL = dsl.nn.ffn(res, out=1) per head
+//     aR = head_attn(v1, wR, bR)       attnR, recomputed from the aggregated rows
+//     Y  = REF GAT(aL, aR, v1)         K5 -> LeakyReLU -> softmax -> weighted aggregation
+// and the reference gathers v1[col] -- H*D floats, 1 KB per edge at config 3 -- for every
+// edge of the forward, and dY[col] for every edge of the backward.  Per head the aggregation
+// is linear in v1, so with alpha = p * q (p per edge, q per row):
+//     Y_h[r]  = q_h[r] * (sum_e p_e,h Xin_ext[c_e]) W_ext,h^T       (Xin_ext = [Xin, 1],
+//     Ym_h[r] = q_h[r] * (sum_e m_e p_e,h Xin_ext[c_e]) W_ext,h^T    W_ext = [W, b])
+//     aL / aR = Xin uL/uR^T + betaL/R, uL_h = W_h^T wL_h, betaL_h = b_h . wL_h + bL_h
+// so the forward gathers the 400-B input row instead (fin = 100), accumulates the per-head
+// aggregates of the input rows on the matrix cores (v_mfma_f32_16x16x4_f32, exact f32: edges
+// are the k dimension) and projects each row's aggregates with W_ext,h in the epilogue -- one
+// workgroup phase projects eight rows per head, so W's fragments stay in registers.  The
+// REF backward (common.h:835-894: dX[r] = sum_{e in row r} alpha_e dY[c_e] with the forward
+// alpha) only feeds the FFN's weight gradient, which regroups by column:
+//     sum_r dX[r]^T Xin_ext[r] = sum_c dY[c]^T T[c],   T_h[c] = sum_{e: c_e = c} alpha_e,h Xin_ext[r_e]
+// over the transposed pattern: the backward gathers the 512-B extended input row (with aL and
+// q riding in its padding) instead of 1 KB of dY plus an aR line, and never forms dX.
+//
+// Extended rows (kInLd = 128 floats, written by k_gat_in_prep every forward).  The
+// aggregation kernels read a row as two float4 per lane over 16 lanes: lane n holds slots
+// 4n..4n+3 and 64+4n..64+4n+3.
+//     slots 0..63            features 0..63
+//     64+4n+{0,1,2}, n < 12  features 64+3n .. 64+3n+2 (features 64..99)
+//     112 (lane 12 .x)       1.0: the ones column (sum p, and the bias through W_ext)
+//     64+4h+3, h < 8         aR[h]  (lane h's .w: the forward's source logit, no extra line)
+//     96+4h+3, h < 8         aL[h]  (lane 8+h's .w: read by the transposed backward)
+//     116+4(h/3)+h%3         q[h]   (lanes 13..15 .xyz: written by the forward's projection)
+// MFMA feature tile t (k order of the aggregation): t < 4 is the first float4's component t
+// (feature 4n + t), t = 4..6 the second float4's component t - 4.
+//
+// Numerics (north_star: fp32 within 1e-4 of the reference): the per-edge terms are the
+// reference's -- t = fl(aL + aR), LeakyReLU, clamp(exp(t), 1e12), alpha = fl(p * q) in the
+// backward -- and every sum is an f32 fmaf chain, regrouped (edge order inside an MFMA k-step,
+// the input-space association); the layer is checked against the oracle's pass-by-pass REF
+// layer at the Products shape (tests/test_gpu_gat_input.py).
+#include "edge_common.h"
+
+namespace gala {
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int kInLd = 128;
+constexpr int kInMaxFin = 100;
+constexpr int kInMaxHeads = 8;
+constexpr int kInWaves = 8;              // waves per workgroup = rows (columns) per phase
+constexpr int kInBlock = kInWaves * kWave;
+constexpr int kInTiles = 7;              // feature tiles of 16
+constexpr int kInGrid = 512;             // persistent workgroups (2 per CU)
+constexpr int kOnesSlot = 112;
+
+__host__ __device__ constexpr int ext_slot(int f) { return f < 64 ? f : 64 + 4 * ((f - 64) / 3) + (f - 64) % 3; }
+__host__ __device__ constexpr int aR_slot(int h) { return 67 + 4 * h; }
+__host__ __device__ constexpr int aL_slot(int h) { return 99 + 4 * h; }
+__host__ __device__ constexpr int q_slot(int h) { return 116 + 4 * (h / 3) + h % 3; }
+
+// input feature of row m of feature tile t: >= 0 a feature, -2 the ones column, -1 padding
+__device__ __forceinline__ int tile_feature(int t, int m, int fin) {
+    int f;
+    if (t < 4) f = 4 * m + t;
+    else if (m < 12) f = 64 + 3 * m + (t - 4);
+    else return (m == 12 && t == 4) ? -2 : -1;
+    return f < fin ? f : -1;
+}
+
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// lane i <- lane i +- 8 inside its 16-lane row (row_ror:8)
+__device__ __forceinline__ float ror8(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, true));
+}
+
+struct InPrepParams {
+    const float *X;
+    int64_t n, ldx;
+    int32_t fin, H;
+    const float *u;   // [2H][fin]: uL rows, then uR rows
+    const float *c;   // [2H]: betaL, betaR
+    float *xext;
+};
+
+// one thread per row: the 2H logit dots (u is wave-uniform: scalar loads) and the row's
+// extended image
+__global__ __launch_bounds__(kBlock) void k_gat_in_prep(InPrepParams p) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= p.n) return;
+    const float *x = p.X + r * p.ldx;
+    float *o = p.xext + r * kInLd;
+    float lg[2 * kInMaxHeads];
+#pragma unroll
+    for (int k = 0; k < 2 * kInMaxHeads; ++k) lg[k] = 0.0f;
+    f4v img[kInLd / 4];
+#pragma unroll
+    for (int i = 0; i < kInLd / 4; ++i) img[i] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int f = 0; f < p.fin; ++f) {
+        const float v = x[f];
+#pragma unroll
+        for (int k = 0; k < 2 * kInMaxHeads; ++k)
+            if (k < 2 * p.H) lg[k] = fmaf(v, p.u[k * p.fin + f], lg[k]);
+    }
+    // the image is assembled in registers (constant slots) and stored as 32 float4
+#pragma unroll
+    for (int s = 0; s < kInLd; ++s) {
+        float v = 0.0f;
+        if (s < 64) {
+            v = s < p.fin ? x[s] : 0.0f;
+        } else {
+            const int n = (s - 64) >> 2, cc = (s - 64) & 3;
+            if (cc < 3 && n < 12) {
+                const int f = 64 + 3 * n + cc;
+                v = f < p.fin ? x[f] : 0.0f;
+            } else if (s == kOnesSlot) {
+                v = 1.0f;
+            } else if (cc == 3 && n < kInMaxHeads) {
+                v = n < p.H ? __fadd_rn(lg[p.H + n], p.c[p.H + n]) : 0.0f;       // aR
+            } else if (cc == 3) {
+                v = n - 8 < p.H ? __fadd_rn(lg[n - 8], p.c[n - 8]) : 0.0f;       // aL
+            }
+        }
+        img[s >> 2][s & 3] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < kInLd / 4; ++i) *reinterpret_cast<f4v *>(o + 4 * i) = img[i];
+}
+
+struct InFwdParams {
+    const int32_t *rowptr, *col, *order;
+    int64_t n_rows;
+    float *xext;
+    const float *W, *b;
+    int64_t ldw;
+    int32_t fin, H, D;
+    float slope;
+    float *Y, *Ym, *q, *sma;
+    int64_t ldy;
+};
+
+// the gathered extended row of edge (4s + kq) of a 16-edge batch: column from the row's
+// 64-index window (lane i holds col[e0 + j0w + i])
+__device__ __forceinline__ int64_t batch_col(int32_t win, int j0, int s, int kq) {
+    const int src = (j0 & 63) + 4 * s + kq;
+    return (int64_t)__builtin_amdgcn_ds_bpermute(src * 4, win);
+}
+
+// a row's (or transposed column's) 7 feature tiles of sum_e B_e * Xext[nb_e], B from bfn
+template <typename BFn>
+__device__ __forceinline__ void gather_tiles(const int32_t *col, int64_t e0, int32_t deg, const float *xext,
+                                             int lane, BFn &&bfn, f4v (&acc)[kInTiles]) {
+    const int n16 = lane & 15, kq = lane >> 4;
+    int32_t win = 0;
+    for (int32_t j0 = 0; j0 < deg; j0 += 16) {
+        if ((j0 & 63) == 0) win = col[e0 + ((j0 + lane < deg) ? j0 + lane : deg - 1)];
+        f4v xa[4], xb[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int64_t c = batch_col(win, j0, s, kq);
+            xa[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 4 * n16);
+            xb[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 64 + 4 * n16);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const bool ok = j0 + 4 * s + kq < deg;
+            const float bv = bfn(xb[s], ok);
+            acc[0] = mfma4(xa[s][0], bv, acc[0]);
+            acc[1] = mfma4(xa[s][1], bv, acc[1]);
+            acc[2] = mfma4(xa[s][2], bv, acc[2]);
+            acc[3] = mfma4(xa[s][3], bv, acc[3]);
+            // lanes 13..15 of the second float4 hold q (and lane 12's .yz zeros): not features
+            const bool feat = n16 < 13;
+            acc[4] = mfma4(feat ? xb[s][0] : 0.0f, bv, acc[4]);
+            acc[5] = mfma4(feat ? xb[s][1] : 0.0f, bv, acc[5]);
+            acc[6] = mfma4(feat ? xb[s][2] : 0.0f, bv, acc[6]);
+        }
+    }
+}
+
+// Forward.  Workgroup phase: wave w aggregates row order[8 blk + w] (B = p of head v for
+// variant v < 8, m * p of head v - 8 for v >= 8), parks its tiles in LDS, then wave h
+// projects the eight rows' head-h aggregates (M = 8 rows x {p, m p}, K = the 112 tile rows,
+// N = D) with W_ext,h fragments held in registers.
+__global__ __launch_bounds__(kInBlock) void k_gat_in_fwd(InFwdParams p) {
+    __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // [slot][variant][tile][16 floats]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
+    const int h = wave;
+    // B fragments of the projection: W_ext,h[j = 16 nt + n16][feature(t, 4 kq + q4)]
+    float wf[kInTiles][4][2];
+#pragma unroll
+    for (int t = 0; t < kInTiles; ++t)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int j = 16 * nt + n16, f = tile_feature(t, 4 * kq + q4, p.fin);
+                float v = 0.0f;
+                if (h < p.H && j < p.D) {
+                    const int64_t o = (int64_t)h * p.D + j;
+                    if (f >= 0) v = p.W[o * p.ldw + f];
+                    else if (f == -2) v = p.b ? p.b[o] : 0.0f;
+                }
+                wf[t][q4][nt] = v;
+            }
+    const float *stf = reinterpret_cast<const float *>(stash);
+    const int64_t nblk = (p.n_rows + kInWaves - 1) / kInWaves;
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        f4v acc[kInTiles];
+#pragma unroll
+        for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        const int64_t ri = blk * kInWaves + wave;
+        if (ri < p.n_rows) {
+            const int64_t r = p.order ? (int64_t)p.order[ri] : ri;
+            const int64_t e0 = uniform(p.rowptr[r]);
+            const int32_t deg = uniform(p.rowptr[r + 1] - p.rowptr[r]);
+            const float al = n16 < p.H ? p.xext[r * kInLd + aL_slot(n16)] : 0.0f;
+            const int H = p.H;
+            const float slope = p.slope;
+            gather_tiles(p.col, e0, deg, p.xext, lane,
+                         [&](const f4v &xb, bool ok) {
+                             const float t = __fadd_rn(al, xb[3]);   // lanes v < 8: aR[col][v]
+                             const bool pos = t > 0.0f;
+                             float pv = ref_exp(pos ? t : __fmul_rn(t, slope));
+                             if (!(ok && n16 < H)) pv = 0.0f;
+                             const float mp = pos ? pv : __fmul_rn(pv, slope);
+                             const float mpo = ror8(mp);
+                             return n16 < 8 ? pv : mpo;
+                         },
+                         acc);
+        }
+#pragma unroll
+        for (int t = 0; t < kInTiles; ++t) stash[((wave * 16 + n16) * kInTiles + t) * 4 + kq] = acc[t];
+        __syncthreads();
+        if (h < p.H) {
+            f4v y[2] = {f4v{0.0f, 0.0f, 0.0f, 0.0f}, f4v{0.0f, 0.0f, 0.0f, 0.0f}};
+            const int s_a = n16 >> 1, v_a = h + 8 * (n16 & 1);
+#pragma unroll
+            for (int t = 0; t < kInTiles; ++t) {
+                const f4v a4 = stash[((s_a * 16 + v_a) * kInTiles + t) * 4 + kq];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    y[0] = mfma4(a4[q4], wf[t][q4][0], y[0]);
+                    y[1] = mfma4(a4[q4], wf[t][q4][1], y[1]);
+                }
+            }
+            // D[m = 4 kq + i][n16]: slot s = m / 2, variant class u = m % 2
+#pragma unroll
+            for (int hs = 0; hs < 2; ++hs) {
+                const int s = 2 * kq + hs;
+                const int64_t si = blk * kInWaves + s;
+                if (si >= p.n_rows) continue;
+                const int64_t row = p.order ? (int64_t)p.order[si] : si;
+                const float S = stf[((s * 16 + h) * kInTiles + 4) * 16 + 12];
+                const float Sm = stf[((s * 16 + h + 8) * kInTiles + 4) * 16 + 12];
+                const float qv = 1.0f / __fadd_rn(S, 1e-12f);   // REF: 1 / (1e-12 + sum p)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    const int j = 16 * nt + n16;
+                    if (j >= p.D) continue;
+                    const int64_t o = row * p.ldy + (int64_t)h * p.D + j;
+                    p.Y[o] = __fmul_rn(qv, y[nt][2 * hs]);
+                    p.Ym[o] = __fmul_rn(qv, y[nt][2 * hs + 1]);
+                }
+                if (n16 == 0) {
+                    p.q[row * p.H + h] = qv;
+                    p.sma[row * p.H + h] = __fmul_rn(qv, Sm);
+                    p.xext[row * kInLd + q_slot(h)] = qv;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct InBwdParams {
+    const int32_t *rowptr, *col, *order;   // the transposed pattern
+    int64_t n_rows;
+    const float *xext, *dY, *Y, *Ym, *sma;
+    int64_t ldy;
+    int32_t fin, H, D;
+    float slope;
+    float *daL;
+    float *part;    // [gridDim][H][2][kInTiles][64][4]
+};
+
+template <int DW>   // lanes per head in the row-local d_aL dots: D / 4
+__device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v); }
+
+// Backward.  Workgroup phase: wave w walks column c = order[8 blk + w] of the transposed
+// pattern (the rows r whose edge e = (r -> c) it holds), accumulates T_h[c] = sum alpha_e,h
+// Xin_ext[r] (alpha rebuilt from aL[r], q[r] in r's extended row and aR[c]) and c's d_aL from
+// the forward's row statistics; then wave h adds dY_h[c]^T T_h[c] of the eight columns into
+// its register accumulators M_h[D x 112] (K = the columns).  Partials per workgroup.
+template <int DW>
+__global__ __launch_bounds__(kInBlock) void k_gat_in_bwd(InBwdParams p) {
+    __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
+    const int h = wave;
+    const float *stf = reinterpret_cast<const float *>(stash);
+    f4v M[2][kInTiles];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int t = 0; t < kInTiles; ++t) M[mt][t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+    const int F = p.H * p.D;
+    const int64_t nblk = (p.n_rows + kInWaves - 1) / kInWaves;
+    // q[h] of a gathered row: lane 13 + h / 3 of its edge's 16 lanes, component h % 3
+    const int hq = n16 & 7;
+    const int qsrc = (16 * kq + 13 + hq / 3) * 4, qc = hq % 3;
+    for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        f4v acc[kInTiles];
+#pragma unroll
+        for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        const int64_t ci = blk * kInWaves + wave;
+        if (ci < p.n_rows) {
+            const int64_t c = p.order ? (int64_t)p.order[ci] : ci;
+            const int64_t e0 = uniform(p.rowptr[c]);
+            const int32_t deg = uniform(p.rowptr[c + 1] - p.rowptr[c]);
+            const float ar = n16 < p.H ? p.xext[c * kInLd + aR_slot(n16)] : 0.0f;
+            const int H = p.H;
+            const float slope = p.slope;
+            gather_tiles(p.col, e0, deg, p.xext, lane,
+                         [&](const f4v &xb, bool ok) {
+                             const float alr = ror8(xb[3]);            // aL[r][v] from lane v + 8
+                             const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
+                             const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
+                             const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
+                             const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
+                             const float t = __fadd_rn(alr, ar);
+                             const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
+                             const float a = __fmul_rn(pv, qr);       // K8: alpha = p * q[row]
+                             return (ok && n16 < H) ? a : 0.0f;
+                         },
+                         acc);
+            // d_aL[c] from the forward's row statistics (gala_gat_bwd_stats_f32's formula)
+            for (int f0 = 0; f0 < F; f0 += 4 * kWave) {
+                const int f = f0 + 4 * lane;
+                f4v dy = f4v{0.0f, 0.0f, 0.0f, 0.0f}, yy = dy, ym = dy;
+                if (f < F) {
+                    dy = *reinterpret_cast<const f4v *>(p.dY + c * p.ldy + f);
+                    yy = *reinterpret_cast<const f4v *>(p.Y + c * p.ldy + f);
+                    ym = *reinterpret_cast<const f4v *>(p.Ym + c * p.ldy + f);
+                }
+                float syy = 0.0f, sym = 0.0f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    syy = fmaf(dy[i], yy[i], syy);
+                    sym = fmaf(dy[i], ym[i], sym);
+                }
+                syy = head_dot_sum<DW>(syy);
+                sym = head_dot_sum<DW>(sym);
+                if (f < F && (f % p.D) == 0) {
+                    const int hh = f / p.D;
+                    const float accv = syy + 1e-12f;                       // K7 on sds (common.h:793-794)
+                    p.daL[c * p.H + hh] = (sym - accv * p.sma[c * p.H + hh]) + 1e-12f;   // common.h:662-667
+                }
+            }
+        }
+        if (n16 < kInMaxHeads) {
+#pragma unroll
+            for (int t = 0; t < kInTiles; ++t) stash[((wave * kInMaxHeads + n16) * kInTiles + t) * 4 + kq] = acc[t];
+        }
+        __syncthreads();
+        if (h < p.H) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int s = 4 * ks + kq;
+                const int64_t si = blk * kInWaves + s;
+                const bool ok = si < p.n_rows;
+                const int64_t cs = ok ? (p.order ? (int64_t)p.order[si] : si) : 0;
+                float a[2];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int j = 16 * mt + n16;
+                    a[mt] = (ok && j < p.D) ? p.dY[cs * p.ldy + (int64_t)h * p.D + j] : 0.0f;
+                }
+#pragma unroll
+                for (int t = 0; t < kInTiles; ++t) {
+                    const float bv = ok ? stf[((s * kInMaxHeads + h) * kInTiles + t) * 16 + n16] : 0.0f;
+                    M[0][t] = mfma4(a[0], bv, M[0][t]);
+                    M[1][t] = mfma4(a[1], bv, M[1][t]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (h < p.H) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int t = 0; t < kInTiles; ++t)
+                *reinterpret_cast<f4v *>(p.part + (((((int64_t)blockIdx.x * p.H + h) * 2 + mt) * kInTiles + t) * 64 +
+                                                   lane) * 4) = M[mt][t];
+    }
+}
+
+// M[h][j][k], k < fin a feature, k = fin the ones column: the workgroups' partials summed
+__global__ __launch_bounds__(kBlock) void k_gat_in_reduce(const float *part, int32_t nparts, int32_t H, int32_t D,
+                                                          int32_t fin, float *M) {
+    const int64_t id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t per = (int64_t)H * 2 * kInTiles * 64 * 4;
+    if (id >= per) return;
+    const int i = id & 3, lane = (int)((id >> 2) & 63);
+    const int64_t rest = id >> 8;
+    const int t = (int)(rest % kInTiles), mt = (int)((rest / kInTiles) % 2), h = (int)(rest / (kInTiles * 2));
+    const int j = 16 * mt + 4 * (lane >> 4) + i;
+    const int f = tile_feature(t, lane & 15, fin);
+    if (j >= D || f == -1) return;
+    float s = 0.0f;
+    for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * per + id];
+    M[((int64_t)h * D + j) * (fin + 1) + (f == -2 ? fin : f)] = s;
+}
+
+int grid_for(int64_t n_rows) {
+    const int64_t nblk = (n_rows + kInWaves - 1) / kInWaves;
+    return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
+}
+
+int check_in_graph(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D) {
+    int st = check_csr(A);
+    if (st) return st;
+    if (fin < 1 || heads < 1 || D < 1) return GALA_ERR_INVALID_ARG;
+    // the extended row holds at most 100 features and 8 heads; the projection's N = D <= 32
+    // with D / 4 lanes per head in the d_aL dots; one segment, a square pattern, no hub-row
+    // plan (a hub row is one wave's serial walk: those graphs stay on the statistics pair)
+    if (fin > kInMaxFin || heads > kInMaxHeads || !(D == 4 || D == 8 || D == 16 || D == 32) || A->n_seg != 1 ||
+        A->n_rows != A->n_cols || (A->split && A->split->n_rows_split > 0))
+        return GALA_ERR_UNSUPPORTED;
+    return GALA_OK;
+}
+
+}  // namespace
+
+extern "C" int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t ldxin, int32_t heads,
+                                    const float *u, const float *c, float *Xext, void *stream) {
+    if (n < 0 || fin < 1 || heads < 1 || ldxin < fin) return GALA_ERR_INVALID_ARG;
+    if (fin > kInMaxFin || heads > kInMaxHeads) return GALA_ERR_UNSUPPORTED;
+    if (n == 0) return GALA_OK;
+    if (!Xin || !u || !c || !Xext || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
+    InPrepParams p{Xin, n, ldxin, fin, heads, u, c, Xext};
+    hipLaunchKernelGGL(k_gat_in_prep, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, p);
+    return launch_status();
+}
+
+extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+                                   float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
+                                   int64_t ldy, float *q, float *sma, void *stream) {
+    int st = check_in_graph(A, fin, heads, D);
+    if (st) return st;
+    if (ldw < fin || ldy < (int64_t)heads * D) return GALA_ERR_INVALID_ARG;
+    if (A->n_rows == 0) return GALA_OK;
+    if (!Xext || !W || !Y || !Ym || !q || !sma || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
+    InFwdParams p{A->rowptr, A->col, A->split ? A->split->row_order : nullptr, A->n_rows, Xext, W, b, ldw,
+                  fin, heads, D, slope, Y, Ym, q, sma, ldy};
+    hipLaunchKernelGGL(k_gat_in_fwd, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
+    return launch_status();
+}
+
+extern "C" int64_t gala_gat_in_bwd_workspace(int32_t heads) {
+    if (heads < 1 || heads > kInMaxHeads) return -1;
+    return (int64_t)kInGrid * heads * 2 * kInTiles * 64 * 4 * (int64_t)sizeof(float);
+}
+
+extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+                                   const float *Xext, const float *dY, const float *Y, const float *Ym,
+                                   int64_t ldy, const float *sma, float *daL, float *M, void *ws_,
+                                   int64_t ws_bytes, void *stream) {
+    float *ws = (float *)ws_;
+    int st = check_in_graph(AT, fin, heads, D);
+    if (st) return st;
+    if (ldy < (int64_t)heads * D || (ldy & 3)) return GALA_ERR_INVALID_ARG;
+    if (!M) return GALA_ERR_INVALID_ARG;
+    hipStream_t hs = (hipStream_t)stream;
+    const int64_t outn = (int64_t)heads * D * (fin + 1);
+    if (AT->n_rows == 0) {
+        return hipMemsetAsync(M, 0, outn * sizeof(float), hs) == hipSuccess ? GALA_OK : GALA_ERR_HIP;
+    }
+    if (!Xext || !dY || !Y || !Ym || !sma || !daL || !ws || ((uintptr_t)Xext & 15) || ((uintptr_t)dY & 15) ||
+        ((uintptr_t)Y & 15) || ((uintptr_t)Ym & 15))
+        return GALA_ERR_INVALID_ARG;
+    if (ws_bytes < gala_gat_in_bwd_workspace(heads)) return GALA_ERR_INVALID_ARG;
+    const int grid = grid_for(AT->n_rows);
+    InBwdParams p{AT->rowptr, AT->col, AT->split ? AT->split->row_order : nullptr, AT->n_rows, Xext, dY, Y, Ym,
+                  sma, ldy, fin, heads, D, slope, daL, ws};
+    if (hipMemsetAsync(M, 0, outn * sizeof(float), hs) != hipSuccess) return GALA_ERR_HIP;
+    switch (D / 4) {
+    case 1: hipLaunchKernelGGL(k_gat_in_bwd<1>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 2: hipLaunchKernelGGL(k_gat_in_bwd<2>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 4: hipLaunchKernelGGL(k_gat_in_bwd<4>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    default: hipLaunchKernelGGL(k_gat_in_bwd<8>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    }
+    st = launch_status();
+    if (st) return st;
+    const int64_t per = (int64_t)heads * 2 * kInTiles * 64 * 4;
+    hipLaunchKernelGGL(k_gat_in_reduce, dim3((unsigned)((per + kBlock - 1) / kBlock)), dim3(kBlock), 0, hs,
+                       (const float *)ws, grid, heads, D, fin, M);
+    return launch_status();
+}
+
+}  // namespace gala

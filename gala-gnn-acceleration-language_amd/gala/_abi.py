@@ -151,6 +151,12 @@ SIGNATURES = {
     "gala_host_mtx_read_dense": (ctypes.c_int, [ctypes.c_char_p, _P, _I64, _I64, _P]),
     "gala_dense_grad_workspace": (ctypes.c_int64, [_I64, _I32, _I32]),
     "gala_dense_grad_f32": (ctypes.c_int, [_I64, _I32, _I32, _P, _I64, _P, _I64, _P, _P, _I32, _P, _I64, _P]),
+    "gala_gat_in_prep_f32": (ctypes.c_int, [_I64, _I32, _P, _I64, _I32, _P, _P, _P, _P]),
+    "gala_gat_in_fwd_f32": (ctypes.c_int, [_CSR, _I32, _I32, _I32, _F, _P, _P, _I64, _P, _P, _P, _I64, _P, _P,
+                                           _P]),
+    "gala_gat_in_bwd_workspace": (ctypes.c_int64, [_I32]),
+    "gala_gat_in_bwd_f32": (ctypes.c_int, [_CSR, _I32, _I32, _I32, _F, _P, _P, _P, _P, _I64, _P, _P, _P, _P,
+                                           _I64, _P]),
 }
 
 
@@ -168,7 +174,7 @@ class GalaError(RuntimeError):
 _lib = None
 
 
-ABI_VERSION = 4  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
+ABI_VERSION = 5  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
 
 
 def lib() -> ctypes.CDLL:
@@ -212,7 +218,8 @@ CPU_OPS = ("gala_spmm_f32", "gala_spmm_ex_f32", "gala_row_broadcast_deg_f32", "g
            "gala_gat_fwd_stats_ex_f32", "gala_gat_bwd_stats_ex_f32", "gala_gat_fwd_partial_stats_ex_f32",
            "gala_gat_fwd_continue_f32", "gala_gat_bwd_stats_linear_f32", "gala_head_attn_f32",
            "gala_head_attn_bwd_f32", "gala_edge_permute_f32", "gala_dense_grad_workspace",
-           "gala_dense_grad_f32")
+           "gala_dense_grad_f32", "gala_gat_in_prep_f32", "gala_gat_in_fwd_f32", "gala_gat_in_bwd_workspace",
+           "gala_gat_in_bwd_f32")
 
 
 def cpu_name(fn: str) -> str:

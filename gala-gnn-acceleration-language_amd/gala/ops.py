@@ -546,3 +546,74 @@ def dense_grad(X, dY, bias=True, dW=None, db=None, accumulate=False):
     _abi.call("gala_dense_grad_f32", N, K, M, _dp(X), ldx, _dp(dY), ldy, _dp(dW),
               _dp(db) if bias else None, int(accumulate), _dp(ws), wsb, _stream())
     return (dW, db) if bias else dW
+
+
+# ---- the multi-head GAT layer in input space (gala_gat_in_*) ------------------------------
+def gat_in_compose(W, b, wL, bL, wR, bR, heads):
+    """The attention vectors folded through the Linear: u [2H, fin] (uL_h = W_h^T wL_h, then
+    uR) and c [2H] (cL_h = b_h . wL_h + bL_h, then cR) -- the mirror's GatInputLayer spelling."""
+    F, fin = W.shape
+    H, D = heads, F // heads
+    w3 = W.reshape(H, D, fin)
+    bb = b.reshape(H, D) if b is not None else torch.zeros(H, D, device=W.device)
+    uL, uR = (w3 * wL.reshape(H, D, 1)).sum(1), (w3 * wR.reshape(H, D, 1)).sum(1)
+    cL, cR = (bb * wL.reshape(H, D)).sum(1) + bL.reshape(H), (bb * wR.reshape(H, D)).sum(1) + bR.reshape(H)
+    return torch.cat([uL, uR]).contiguous(), torch.cat([cL, cR]).contiguous()
+
+
+def gat_in_prep(X, u, c, heads, xext=None):
+    """gala_gat_in_prep_f32: the extended rows [N, 128] (features, ones, aR, aL)."""
+    N, fin = X.shape
+    xext = torch.empty(N, 128, device=X.device, dtype=torch.float32) if xext is None else xext
+    _abi.call("gala_gat_in_prep_f32", N, fin, _dp(X), X.stride(0), heads, _dp(u), _dp(c), _dp(xext), _stream())
+    return xext
+
+
+def gat_in_fwd(g: DeviceGraph, xext, W, b, heads, fin, slope=0.2):
+    """gala_gat_in_fwd_f32: (Y, Ym, q, sma); writes q into xext."""
+    F = W.shape[0]
+    D = F // heads
+    Y = torch.empty(g.n_rows, F, device=W.device, dtype=torch.float32)
+    Ym = torch.empty_like(Y)
+    q = torch.empty(g.n_rows, heads, device=W.device, dtype=torch.float32)
+    sma = torch.empty_like(q)
+    _abi.call("gala_gat_in_fwd_f32", g.csr(0), fin, heads, D, slope, _dp(xext), _dp(W), W.stride(0), _dp(b),
+              _dp(Y), _dp(Ym), F, _dp(q), _dp(sma), _stream())
+    return Y, Ym, q, sma
+
+
+def gat_in_bwd(gT: DeviceGraph, xext, dY, Y, Ym, sma, heads, fin, slope=0.2):
+    """gala_gat_in_bwd_f32 over the transposed pattern gT: (d_aL [N, H], M [H, D, fin + 1])."""
+    F = dY.shape[1]
+    D = F // heads
+    daL = torch.empty(gT.n_rows, heads, device=dY.device, dtype=torch.float32)
+    M = torch.empty(heads, D, fin + 1, device=dY.device, dtype=torch.float32)
+    wsb = _abi.lib().gala_gat_in_bwd_workspace(heads)
+    ws = torch.empty(max(wsb // 4, 1), device=dY.device, dtype=torch.float32)
+    _abi.call("gala_gat_in_bwd_f32", gT.csr(0), fin, heads, D, slope, _dp(xext), _dp(dY), _dp(Y), _dp(Ym), F,
+              _dp(sma), _dp(daL), _dp(M), _dp(ws), wsb, _stream())
+    return daL, M
+
+
+def gat_input_layer(g: DeviceGraph, X, W, b, wL, bL, wR, bR, heads, slope=0.2, dY=None, gT=None):
+    """Config 3's layer 1 in input space through the C ABI, the composition of the mirror's
+    GatInputLayer: forward (Y, q, sma, xext) and, with dY, the gradients
+    {W, b, wL, bL, wR, bR} (REF: d aR = d aL) and d_aL.  gT: the transposed pattern (default g,
+    the symmetric graph of an undirected program)."""
+    F, fin = W.shape
+    H, D = heads, F // heads
+    u, c = gat_in_compose(W, b, wL, bL, wR, bR, heads)
+    xext = gat_in_prep(X, u, c, heads)
+    Y, Ym, q, sma = gat_in_fwd(g, xext, W, b, heads, fin, slope)
+    out = {"Y": Y, "Ym": Ym, "q": q, "sma": sma, "xext": xext}
+    if dY is None:
+        return out
+    daL, M = gat_in_bwd(g if gT is None else gT, xext, dY, Y, Ym, sma, heads, fin, slope)
+    Gw, Gb = dense_grad(X, daL)
+    sLR = wL.reshape(H, D) + wR.reshape(H, D)
+    bb = b.reshape(H, D) if b is not None else torch.zeros(H, D, device=W.device)
+    dw = (W.reshape(H, D, fin) * Gw.unsqueeze(1)).sum(2) + bb * Gb.unsqueeze(1)
+    out.update(daL=daL, M=M, G=Gw, dW=(M[:, :, :fin] + sLR.unsqueeze(2) * Gw.unsqueeze(1)).reshape(F, fin),
+               db=(M[:, :, fin] + sLR * Gb.unsqueeze(1)).reshape(F), dwL=dw.reshape(-1), dwR=dw.reshape(-1),
+               dbL=Gb, dbR=Gb)
+    return out

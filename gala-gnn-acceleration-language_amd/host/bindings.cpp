@@ -109,4 +109,13 @@ PYBIND11_MODULE(_gala_torch, m) {
     m.def("gat_aggregate_ffn_apply", &gat_aggregate_ffn_apply, py::arg("attn_l"), py::arg("X"),
           py::arg("attn_r_weight"), py::arg("attn_r_bias"), py::arg("li"), py::arg("slope") = 0.2,
           py::arg("mode") = 0);
+    m.def("gat_input_layer_apply",
+          [opt](torch::Tensor x, torch::Tensor w, std::optional<torch::Tensor> b, torch::Tensor wl, torch::Tensor bl,
+                torch::Tensor wr, torch::Tensor br, int64_t li, double slope, int64_t mode) {
+              return gat_input_layer_apply(x, w, opt(b), wl, bl, wr, br, li, slope, mode);
+          },
+          py::arg("X"), py::arg("weight"), py::arg("bias"), py::arg("attn_l_weight"), py::arg("attn_l_bias"),
+          py::arg("attn_r_weight"), py::arg("attn_r_bias"), py::arg("li"), py::arg("slope") = 0.2,
+          py::arg("mode") = 0);
+    m.def("gat_input_layer_eligible", &gat_input_layer_eligible);
 }

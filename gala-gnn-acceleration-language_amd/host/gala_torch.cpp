@@ -47,6 +47,10 @@ struct Backend {
     decltype(&gala_edge_permute_f32) permute;
     decltype(&gala_dense_grad_workspace) dense_ws;
     decltype(&gala_dense_grad_f32) dense_grad;
+    decltype(&gala_gat_in_prep_f32) gat_in_prep;
+    decltype(&gala_gat_in_fwd_f32) gat_in_fwd;
+    decltype(&gala_gat_in_bwd_workspace) gat_in_ws;
+    decltype(&gala_gat_in_bwd_f32) gat_in_bwd;
 };
 const Backend kHip{gala_spmm_ex_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_ffn_fwd_f32,
@@ -57,7 +61,8 @@ const Backend kHip{gala_spmm_ex_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_gat_fwd_ex_f32, gala_gat_bwd_ex_f32, gala_gat_bwd_fused_f32,
                    gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_gat_bwd_stats_linear_f32,
                    gala_head_attn_f32, gala_head_attn_bwd_f32,
-                   gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32};
+                   gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32,
+                   gala_gat_in_prep_f32, gala_gat_in_fwd_f32, gala_gat_in_bwd_workspace, gala_gat_in_bwd_f32};
 const Backend kCpu{gala_cpu_spmm_ex_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
@@ -68,7 +73,8 @@ const Backend kCpu{gala_cpu_spmm_ex_f32, gala_cpu_degree_f32, gala_cpu_row_broad
                    gala_cpu_gat_fwd_stats_f32, gala_cpu_gat_bwd_stats_f32, gala_cpu_gat_bwd_stats_linear_f32,
                    gala_cpu_head_attn_f32, gala_cpu_head_attn_bwd_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
-                   gala_cpu_dense_grad_f32};
+                   gala_cpu_dense_grad_f32, gala_cpu_gat_in_prep_f32, gala_cpu_gat_in_fwd_f32,
+                   gala_cpu_gat_in_bwd_workspace, gala_cpu_gat_in_bwd_f32};
 
 const Backend &be(const torch::Tensor &t) {
     TORCH_CHECK(t.is_cuda() || t.is_cpu(), "gala: unsupported device ", t.device());
@@ -460,6 +466,7 @@ int GraphSlots::push(torch::Tensor offsets, torch::Tensor cols, torch::Tensor va
     else if (offsets.is_cuda() && segs > 1 && !w)
         mg = make_merged_csr(offsets, cols, bounds.back(), segs);
     merged.push_back(mg);
+    pattern_t.push_back(nullptr);
     if (offset_graph.size() == 1) nrows = offsets.numel() / segs - 1;
     return (int)offset_graph.size() - 1;
 }
@@ -1466,6 +1473,145 @@ torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, tor
     return GatAggregateFfn::apply(attn_l, X, attn_r_weight, attn_r_bias, li, slope, mode);
 }
 
+// The multi-head GAT layer in input space (gala_gat_in_*, include/gala_hip.h): the chain
+// ffn_apply(X, W, b) -> head_attn_apply(., wL, bL) -> gat_aggregate_ffn_apply(., ., wR, bR)
+// as one autograd op whose kernels gather X's fin-float rows instead of the H*D-float Linear
+// output.  Forward: the attention vectors folded through the Linear (uL_h = W_h^T wL_h, cL_h
+// = b_h . wL_h + bL_h; the same for R), the extended rows, the aggregation with the
+// projection in its epilogue.  Backward (REF, the reference's chain on the undirected
+// graph): d_aL and M = sum_r dX[r]^T X_ext[r] from the kernel, G = d_aL^T X_ext from the
+// dense gradient kernel, then
+//   dW_h = M_h[:, :fin] + (wL_h + wR_h) G_h,   db_h = M_h[:, fin] + (wL_h + wR_h) sum d_aL_h
+//   d wL_h = d wR_h = W_h G_h + b_h sum d_aL_h,  d bL = d bR = sum d_aL   (REF: d aR = d aL)
+// -- exactly the gradients autograd forms through the three ops (Ffn, HeadAttnFn,
+// GatAggregateFfn), regrouped.  X itself gets no gradient (the layer's input is the
+// dataset's features); the apply wrapper keeps the three-op chain whenever X needs one.
+const PatternT &transposed_pattern(int64_t idx);
+
+struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
+    static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor W, torch::Tensor b,
+                                 torch::Tensor wL, torch::Tensor bL, torch::Tensor wR, torch::Tensor bR,
+                                 int64_t li, double slope, int64_t heads) {
+        Slot s = slot(2 * li);
+        auto x = X.contiguous(), w = W.contiguous();
+        const bool has_b = b.defined() && b.numel() > 0;
+        check_dev(x, torch::kFloat, "X");
+        check_dev(w, torch::kFloat, "weight");
+        check_on(x, s.off, "X");
+        check_on(w, s.off, "weight");
+        const int64_t N = x.size(0), fin = x.size(1), F = w.size(0), H = heads, D = F / H;
+        TORCH_CHECK(w.size(1) == fin && F % H == 0 && wL.numel() == F && wR.numel() == F && bL.numel() == H &&
+                        bR.numel() == H && (!has_b || b.numel() == F),
+                    "gala: gat_input_layer: X [N, fin], W [H*D, fin], b [H*D], attention vectors [H*D] and biases [H]");
+        auto w3 = w.view({H, D, fin});
+        auto bb = has_b ? b.contiguous().view({H, D}) : torch::zeros({H, D}, fopts(x));
+        auto uL = (w3 * wL.reshape({H, D, 1})).sum(1), uR = (w3 * wR.reshape({H, D, 1})).sum(1);
+        auto cL = (bb * wL.reshape({H, D})).sum(1) + bL.reshape({H}), cR = (bb * wR.reshape({H, D})).sum(1) + bR.reshape({H});
+        auto u = torch::cat({uL, uR}).contiguous(), c = torch::cat({cL, cR}).contiguous();
+        auto xext = torch::empty({N, 128}, fopts(x));
+        const Backend &B = be(x);
+        check(B.gat_in_prep(N, (int32_t)fin, x.data_ptr<float>(), x.stride(0), (int32_t)H, u.data_ptr<float>(),
+                            c.data_ptr<float>(), xext.data_ptr<float>(), stream_of(x)),
+              "gala_gat_in_prep_f32");
+        CsrView cv = view(s.off, s.cols, nullptr, s.bounds, s.segs);
+        auto Y = torch::empty({N, F}, fopts(x)), Ym = torch::empty({N, F}, fopts(x));
+        auto q = torch::empty({N, H}, fopts(x)), sma = torch::empty({N, H}, fopts(x));
+        torch::Tensor bc = has_b ? b.contiguous() : torch::Tensor();
+        check(B.gat_in_fwd(&cv.c, (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+                           w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr, Y.data_ptr<float>(),
+                           Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(), stream_of(x)),
+              "gala_gat_in_fwd_f32");
+        ctx->saved_data["li"] = li;
+        ctx->saved_data["slope"] = slope;
+        ctx->saved_data["heads"] = heads;
+        ctx->saved_data["has_b"] = has_b;
+        ctx->save_for_backward({x, w, has_b ? bc : torch::empty({0}, fopts(x)), wL, wR, xext, Y, Ym, sma});
+        return Y;
+    }
+    static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
+        auto sv = ctx->get_saved_variables();
+        auto x = sv[0], w = sv[1], b = sv[2], wL = sv[3], wR = sv[4], xext = sv[5], Y = sv[6], Ym = sv[7], sma = sv[8];
+        const int64_t li = ctx->saved_data["li"].toInt(), H = ctx->saved_data["heads"].toInt();
+        const double slope = ctx->saved_data["slope"].toDouble();
+        const bool has_b = ctx->saved_data["has_b"].toBool();
+        const int64_t N = x.size(0), fin = x.size(1), F = w.size(0), D = F / H;
+        auto dY = grad_outputs[0].contiguous();
+        check_dev(dY, torch::kFloat, "grad");
+        check_on(dY, x, "grad");
+        // the reference's REF backward on the undirected graph is dX = A_alpha dY over A itself;
+        // regrouped by column it walks A's transposed pattern (A's own tensors when symmetric)
+        const PatternT &pt = transposed_pattern(2 * li);
+        CsrView cv = view(pt.rowptr, pt.col, nullptr, torch::Tensor(), 1);
+        const Backend &B = be(x);
+        auto daL = torch::empty({N, H}, fopts(x));
+        auto M = torch::empty({H, D, fin + 1}, fopts(x));
+        const int64_t wsb = B.gat_in_ws((int32_t)H);
+        TORCH_CHECK(wsb > 0, "gala: gala_gat_in_bwd_workspace failed");
+        auto ws = torch::empty({wsb / 4}, fopts(x));
+        check(B.gat_in_bwd(&cv.c, (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+                           dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F, sma.data_ptr<float>(),
+                           daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb, stream_of(x)),
+              "gala_gat_in_bwd_f32");
+        // G = d_aL^T X (and its column sums): the attention Linears' terms
+        auto Gw = torch::empty({H, fin}, fopts(x)), Gb = torch::empty({H}, fopts(x));
+        const int64_t gws = B.dense_ws(N, (int32_t)fin, (int32_t)H);
+        TORCH_CHECK(gws >= 0, "gala: gala_dense_grad_workspace failed");
+        auto gw = torch::empty({std::max<int64_t>(gws / 4, 1)}, fopts(x));
+        check(B.dense_grad(N, (int32_t)fin, (int32_t)H, x.data_ptr<float>(), x.stride(0), daL.data_ptr<float>(), H,
+                           Gw.data_ptr<float>(), Gb.data_ptr<float>(), 0, gw.data_ptr<float>(), gws, stream_of(x)),
+              "gala_dense_grad_f32");
+        auto sLR = (wL.reshape({H, D}) + wR.reshape({H, D}));
+        auto dW = (M.narrow(2, 0, fin) + sLR.unsqueeze(2) * Gw.unsqueeze(1)).reshape({F, fin});
+        torch::Tensor db = has_b ? (M.select(2, fin) + sLR * Gb.unsqueeze(1)).reshape({F}) : torch::Tensor();
+        auto bb = has_b ? b.view({H, D}) : torch::zeros({H, D}, fopts(x));
+        auto dw = ((w.view({H, D, fin}) * Gw.unsqueeze(1)).sum(2) + bb * Gb.unsqueeze(1));
+        return {torch::Tensor(), dW, db, dw.reshape(wL.sizes()), Gb.reshape({H}), dw.reshape(wR.sizes()),
+                Gb.reshape({H}), torch::Tensor(), torch::Tensor(), torch::Tensor()};
+    }
+};
+
+// slot idx's transposed pattern (one segment): a host transpose on first use
+// (gala_host_csr_transpose), compared with the pattern itself; kept on the graph's device
+const PatternT &transposed_pattern(int64_t idx) {
+    auto &S = global_slots();
+    auto &pt = S.pattern_t[idx];
+    if (pt) return *pt;
+    for (size_t i = 0; i < S.pattern_t.size(); ++i)
+        if (S.pattern_t[i] && S.offset_graph[i].unsafeGetTensorImpl() == S.offset_graph[idx].unsafeGetTensorImpl() &&
+            S.columns_graph[i].unsafeGetTensorImpl() == S.columns_graph[idx].unsafeGetTensorImpl()) {
+            pt = S.pattern_t[i];
+            return *pt;
+        }
+    TORCH_CHECK(S.segments[idx] == 1, "gala: transposed pattern of a column-tiled graph");
+    auto off = S.offset_graph[idx].to(torch::kCPU).contiguous(), col = S.columns_graph[idx].to(torch::kCPU).contiguous();
+    const int64_t n = off.numel() - 1, nnz = col.numel();
+    auto io = torch::TensorOptions().dtype(torch::kInt);
+    auto tr = torch::empty({n + 1}, io), tc = torch::empty({nnz}, io), perm = torch::empty({nnz}, io);
+    check(gala_host_csr_transpose(n, n, off.data_ptr<int32_t>(), col.data_ptr<int32_t>(), tr.data_ptr<int32_t>(),
+                                  tc.data_ptr<int32_t>(), perm.data_ptr<int32_t>()),
+          "gala_host_csr_transpose");
+    auto p = std::make_shared<PatternT>();
+    p->symmetric = torch::equal(tr, off) && torch::equal(tc, col);
+    if (p->symmetric) {
+        p->rowptr = S.offset_graph[idx];
+        p->col = S.columns_graph[idx];
+    } else {
+        p->rowptr = tr.to(S.offset_graph[idx].device());
+        p->col = tc.to(S.offset_graph[idx].device());
+    }
+    pt = p;
+    return *pt;
+}
+
+// GALA_GAT_INPUT=0 keeps the three-op chain (A/B runs, the tests' reference spelling)
+bool gat_input_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("GALA_GAT_INPUT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 HeadAttnImpl::HeadAttnImpl(int64_t in, int64_t heads) {
     TORCH_CHECK(heads >= 1 && in % heads == 0, "gala: HeadAttn(", in, ", ", heads, "): in is not a whole number of heads");
     const double bound = 1.0 / std::sqrt((double)(in / heads));  // torch Linear(D, 1) init range
@@ -1514,6 +1660,41 @@ torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tens
     TORCH_CHECK(X.dim() == 2 && X.size(-1) == F && F % H == 0, "gala: head_attn_apply: X has ", X.size(-1),
                 " columns, the attention vectors ", F);
     return HeadAttnFn::apply(X, weight, bias);
+}
+
+bool gat_input_layer_eligible(const torch::Tensor &X, const torch::Tensor &W, int64_t li, int64_t heads,
+                              int64_t mode) {
+    if (!gat_input_enabled() || mode != GALA_SOFTMAX_REF || X.requires_grad() || X.dim() != 2 || W.dim() != 2)
+        return false;
+    if (X.scalar_type() != torch::kFloat || W.scalar_type() != torch::kFloat || X.device() != W.device()) return false;
+    const int64_t fin = X.size(1), F = W.size(0);
+    if (heads < 1 || heads > 8 || F % heads != 0 || W.size(1) != fin || fin < 1 || fin > 100) return false;
+    const int64_t D = F / heads;
+    if (!(D == 4 || D == 8 || D == 16 || D == 32)) return false;
+    // the byte saving is the point: the input row narrower than the Linear's output
+    if (fin >= F) return false;
+    // REF on the undirected graph (slot 2li+1 = slot 2li, the reference's A-not-A^T backward
+    // then equals the transposed regrouping), one segment, no hub-row plan
+    Slot s = slot(2 * li);
+    if (!recompute_attention(li, mode) || s.segs != 1 || s.weighted || global_slots().nsamples > 0) return false;
+    if (s.off.device() != X.device()) return false;
+    if (s.off.is_cuda()) {
+        SplitState *sp = find_split(s.off);
+        if (sp && sp->plan.n_rows_split > 0) return false;
+    }
+    return true;
+}
+
+torch::Tensor gat_input_layer_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias, torch::Tensor attn_l_weight,
+                                    torch::Tensor attn_l_bias, torch::Tensor attn_r_weight, torch::Tensor attn_r_bias,
+                                    int64_t li, double slope, int64_t mode) {
+    const int64_t heads = attn_l_bias.numel();
+    if (gat_input_layer_eligible(X, weight, li, heads, mode))
+        return GatInputLayer::apply(X, weight, bias, attn_l_weight, attn_l_bias, attn_r_weight, attn_r_bias, li,
+                                    slope, heads);
+    auto v1 = ffn_apply(X, weight, bias);
+    auto aL = head_attn_apply(v1, attn_l_weight, attn_l_bias);
+    return gat_aggregate_ffn_apply(aL, v1, attn_r_weight, attn_r_bias, li, slope, mode);
 }
 
 }  // namespace gala

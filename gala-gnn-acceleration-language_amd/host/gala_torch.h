@@ -59,6 +59,13 @@ struct MergedCsr {
 std::shared_ptr<MergedCsr> make_merged_csr(const torch::Tensor &offsets, const torch::Tensor &cols,
                                            const torch::Tensor &bounds_host, int segments);
 
+// The transposed pattern of a one-segment slot graph, built on first use (the input-space
+// GAT backward walks it): the slot's own tensors when the pattern is symmetric.
+struct PatternT {
+    torch::Tensor rowptr, col;
+    bool symmetric = false;
+};
+
 // The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's
 // forward graph, slot 2*li+1 its backward graph (the same tensors for undirected graphs,
 // cuda.h:1253-1257).  `bounds` stay on the host like the reference's total_bounds.
@@ -69,6 +76,7 @@ struct GraphSlots {
     std::vector<torch::Tensor> transpose_perm;  // optional: edge k of slot == edge perm[k] of forward
     std::vector<std::shared_ptr<SplitState>> split;  // hub-row plans (nullptr: none)
     std::vector<std::shared_ptr<MergedCsr>> merged;  // tiled graphs' merged rows (nullptr: none)
+    std::vector<std::shared_ptr<PatternT>> pattern_t;  // transposed patterns (built on first use)
     int64_t nrows = 0;
     int ra = 5, rb = 7;    // kernel-sampling coefficients (common.h:813-833)
     int nsamples = 0;      // 0 = no kernel sampling
@@ -173,5 +181,18 @@ struct HeadAttnImpl : torch::nn::Module {
 TORCH_MODULE(HeadAttn);
 // [N, H]: out[:, h] = X[:, hD:(h+1)D] . weight[hD:(h+1)D] + bias[h] (torch ops, autograd)
 torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias);
+
+// The first layer of a multi-head GAT program in input space (include/gala_hip.h
+// gala_gat_in_*): the value and gradients of
+//   gat_aggregate_ffn_apply(head_attn_apply(v1, attn_l_weight, attn_l_bias), v1,
+//                           attn_r_weight, attn_r_bias, li, slope, mode),   v1 = ffn_apply(X, weight, bias)
+// with the edges gathering X's rows (fin floats) instead of v1's (H*D).  Used when X needs
+// no gradient (the dataset's features), fin < H*D <= 8*32, REF softmax on the undirected
+// graph without hub rows; otherwise it runs the three ops themselves (GALA_GAT_INPUT=0: always).
+bool gat_input_layer_eligible(const torch::Tensor &X, const torch::Tensor &W, int64_t li, int64_t heads, int64_t mode);
+torch::Tensor gat_input_layer_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias,
+                                    torch::Tensor attn_l_weight, torch::Tensor attn_l_bias,
+                                    torch::Tensor attn_r_weight, torch::Tensor attn_r_bias, int64_t li,
+                                    double slope, int64_t mode);
 
 }  // namespace gala

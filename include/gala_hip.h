@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GALA_ABI_VERSION 4
+#define GALA_ABI_VERSION 5
 
 typedef enum gala_status {
     GALA_OK = 0,
@@ -544,6 +544,48 @@ int gala_head_attn_f32(int64_t n_rows, int32_t F, int32_t heads, const float *X,
                        const float *w, const float *b, float *out, void *stream);
 int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float *g, const float *w,
                            float *dX, int64_t lddx, int32_t accumulate, void *stream);
+
+/*
+ * The multi-head GAT layer in INPUT space (ABI 5; config 3's layer 1).  Replaces, for a layer
+ * whose aggregated rows are a Linear of a narrower input (the tests/GALA-DSL/gat programs: res =
+ * dsl.nn.ffn(G.node.feats, out=hs); attnL / attnR = dsl.nn.ffn(res, out=1); softmax;
+ * res = aggregate_fn(G.graphs, res)), the chain FFN_OP (common.h:1188-1242) -> the two
+ * attention Linears (common.h:1248-1260) -> the REF edge chain K5-K8 + the weighted
+ * aggregation (cuda.h:286-358,505-562,679-698; common.h:735-810) and its REF backward
+ * (common.h:835-894: dX = A_alpha dY with the forward alpha, the K9 / softmax / K7 chain):
+ * per head h, with W_h the [D, fin] block of the Linear and Xin_ext = [Xin, 1], W_ext = [W, b],
+ *     aL = Xin uL^T + cL, aR = Xin uR^T + cR  (uL_h = W_h^T wL_h, cL_h = b_h . wL_h + bL_h)
+ *     Y_h[r]  = q_h[r] (sum_e p_e,h Xin_ext[c_e]) W_ext,h^T,   q = 1 / (1e-12 + sum_e p_e)
+ *     p = min(exp(LeakyReLU(aL[r] + aR[c])), 1e12)
+ * so the edges gather the fin-float input row instead of the H*D-float Linear output.
+ *   gala_gat_in_prep_f32: Xext [n][128] (16-B aligned) = the extended rows: Xin's fin <= 100
+ *     features, the ones column, aL / aR (u [2H][fin]: uL rows then uR rows; c [2H]).  Every
+ *     forward (aL / aR follow the weights).
+ *   gala_gat_in_fwd_f32: Y, Ym [n][ldy] (Ym = the m-weighted aggregate, m = 1 or slope by the
+ *     logit's sign), q, sma [n][H] (the row statistics of gala_gat_fwd_stats_f32); writes q
+ *     into Xext too (the backward reads it there).  W [H*D][ldw], b [H*D] nullable.
+ *   gala_gat_in_bwd_f32: AT = the TRANSPOSED pattern of A (A itself for the symmetric graphs
+ *     of undirected programs).  d_aL [n][H] (REF: d aR = d aL) and
+ *     M [H][D][fin+1] = sum_r dX[r]^T Xin_ext[r] with dX the REF aggregation backward -- the
+ *     FFN's weight gradient through the aggregation (column fin: its bias gradient); the
+ *     attention Linears' terms follow from G = d_aL^T Xin_ext (gala_dense_grad_f32):
+ *     dW_h += (wL_h + wR_h) G_h, d wL_h = d wR_h = W_ext,h G_h, d bL = d bR = sum d_aL.
+ *     ws: gala_gat_in_bwd_workspace(heads) bytes.
+ * Limits (else GALA_ERR_UNSUPPORTED, callers keep the statistics pair): fin <= 100, heads
+ * <= 8, D in {4, 8, 16, 32}, one segment, a square pattern, no hub rows in A->split (a hub
+ * row would be one wave's serial walk).  Sums are regrouped (the matrix cores sum four edges
+ * per step; the input-space association): fp32 rounding of the reference, checked at 1e-4.
+ */
+int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t ldxin, int32_t heads,
+                         const float *u, const float *c, float *Xext, void *stream);
+int gala_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+                        float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
+                        int64_t ldy, float *q, float *sma, void *stream);
+int64_t gala_gat_in_bwd_workspace(int32_t heads);
+int gala_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+                        const float *Xext, const float *dY, const float *Y, const float *Ym,
+                        int64_t ldy, const float *sma, float *daL, float *M, void *ws,
+                        int64_t ws_bytes, void *stream);
 
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,

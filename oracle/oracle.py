@@ -425,3 +425,39 @@ def ref_threads() -> int:
 
 def ref_set_threads(n: int) -> None:
     ref().ref_set_threads(ctypes.c_int(int(n)))
+
+
+def gat_input_layer_ref(rowptr, col, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, threads=None):
+    """TEST INFRASTRUCTURE: config 3's first GAT layer as the reference's generated program
+    composes it, with its REF backward -- the reference for the input-space layer
+    (gala_gat_in_*):
+      v1 = X W^T + b                          FFN_OP, torch::nn::Linear (common.h:1188-1242);
+                                              fp32 result of a float64 product (the library
+                                              GEMM's order is not pinned)
+      aL = head_attn(v1, wL, bL)              attnL = ffn(res, out=1) per head (common.h:1248-1260)
+      Y, dX_agg, d_aL = orc_gat_ref_layer     K5 ... K8 + aggregation, and its REF backward
+                                              (common.h:735-894; aR recomputed from v1, d aR = d aL)
+    and the parameter gradients autograd forms through those ops (float64 from the layer's
+    fp32 outputs):
+      dv1 = dX_agg + d_aL (x) (wL + wR) per head   (HeadAttn / the aR Linear's input gradient)
+      dW = dv1^T X, db = sum dv1, d wL = d wR = sum_r d_aL[r, h] v1[r, head h], d bL = d bR = sum d_aL.
+    Returns a dict of numpy arrays (Y, daL, aR, dW, db, dwL, dbL, dwR, dbR, v1)."""
+    X = np.ascontiguousarray(X, np.float32)
+    F, fin = W.shape
+    H, D = heads, F // heads
+    v1 = (X.astype(np.float64) @ np.asarray(W, np.float64).T + (0 if b is None else np.asarray(b, np.float64)))
+    v1 = v1.astype(np.float32)
+    aL = head_attn(v1, wL, bL, H)
+    n = len(rowptr) - 1
+    if threads:
+        set_threads(threads)
+    lay = GatRefLayer(rowptr, col, n, v1, dY, aL, wR, bR, H, slope=slope).run()
+    daL = lay.daL.astype(np.float64)
+    sLR = (np.asarray(wL, np.float64) + np.asarray(wR, np.float64)).reshape(H, D)
+    dv1 = lay.dX.astype(np.float64).reshape(n, H, D) + daL[:, :, None] * sLR[None]
+    dv1 = dv1.reshape(n, F)
+    dW = dv1.T @ X.astype(np.float64)
+    db = dv1.sum(0)
+    dw = np.einsum("rh,rhd->hd", daL, v1.astype(np.float64).reshape(n, H, D)).reshape(-1)
+    return dict(Y=lay.Y, daL=lay.daL, aR=lay.aR, q=lay.q, dW=dW, db=db, dwL=dw, dbL=daL.sum(0), dwR=dw,
+                dbR=daL.sum(0), v1=v1)
