@@ -427,7 +427,8 @@ def ref_set_threads(n: int) -> None:
     ref().ref_set_threads(ctypes.c_int(int(n)))
 
 
-def gat_input_layer_ref(rowptr, col, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, threads=None):
+def gat_input_layer_ref(rowptr, col, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, threads=None, aL=None,
+                        aR=None):
     """TEST INFRASTRUCTURE: config 3's first GAT layer as the reference's generated program
     composes it, with its REF backward -- the reference for the input-space layer
     (gala_gat_in_*):
@@ -441,17 +442,23 @@ def gat_input_layer_ref(rowptr, col, X, W, b, wL, bL, wR, bR, dY, heads, slope=0
     fp32 outputs):
       dv1 = dX_agg + d_aL (x) (wL + wR) per head   (HeadAttn / the aR Linear's input gradient)
       dW = dv1^T X, db = sum dv1, d wL = d wR = sum_r d_aL[r, h] v1[r, head h], d bL = d bR = sum d_aL.
+    aL / aR [n, heads] (optional): the attention logits to use instead of head_attn(v1) --
+    the kernels' own, whose summation order differs from the Linear's: an edge whose logit
+    sits at 0 may take the other LeakyReLU slope under a one-ulp change and move its row's
+    d_aL by ~ alpha * |d alpha|; the tests check the logits themselves
+    against the float64 Linear separately.
     Returns a dict of numpy arrays (Y, daL, aR, dW, db, dwL, dbL, dwR, dbR, v1)."""
     X = np.ascontiguousarray(X, np.float32)
     F, fin = W.shape
     H, D = heads, F // heads
     v1 = (X.astype(np.float64) @ np.asarray(W, np.float64).T + (0 if b is None else np.asarray(b, np.float64)))
     v1 = v1.astype(np.float32)
-    aL = head_attn(v1, wL, bL, H)
+    aL = head_attn(v1, wL, bL, H) if aL is None else np.ascontiguousarray(aL, np.float32)
     n = len(rowptr) - 1
     if threads:
         set_threads(threads)
-    lay = GatRefLayer(rowptr, col, n, v1, dY, aL, wR, bR, H, slope=slope).run()
+    rid = None if aR is None else np.arange(n, dtype=np.int64)
+    lay = GatRefLayer(rowptr, col, n, v1, dY, aL, wR, bR, H, slope=slope, row_ids=rid, aR=aR).run()
     daL = lay.daL.astype(np.float64)
     sLR = (np.asarray(wL, np.float64) + np.asarray(wR, np.float64)).reshape(H, D)
     dv1 = lay.dX.astype(np.float64).reshape(n, H, D) + daL[:, :, None] * sLR[None]
