@@ -1208,9 +1208,31 @@ extern "C" int gala_cpu_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin
     for (int64_t r = 0; r < n; ++r) {
         const float *x = Xin + r * ldxin;
         float *o = Xext + r * kInLd;
+        // the kernel's association: 16 lane partials (lane n: features 4n..4n+3, then
+        // 64+3n..64+3n+2), summed by the xor butterfly 8, 4, 2, 1
         float lg[2 * kInMaxHeads] = {0.0f};
-        for (int f = 0; f < fin; ++f)
-            for (int k = 0; k < 2 * H; ++k) lg[k] = fmaf(x[f], u[k * fin + f], lg[k]);
+        for (int k = 0; k < 2 * H; ++k) {
+            float v[16];
+            for (int nn = 0; nn < 16; ++nn) {
+                float d = 0.0f;
+                for (int i = 0; i < 4; ++i) {
+                    const int f = 4 * nn + i;
+                    d = fmaf(f < fin ? x[f] : 0.0f, f < fin ? u[k * fin + f] : 0.0f, d);
+                }
+                for (int i = 0; i < 3; ++i) {
+                    const int f = 64 + 3 * nn + i;
+                    const bool ok = nn < 12 && f < fin;
+                    d = fmaf(ok ? x[f] : 0.0f, ok ? u[k * fin + f] : 0.0f, d);
+                }
+                v[nn] = d;
+            }
+            for (int o = 8; o >= 1; o /= 2) {
+                float w[16];
+                for (int nn = 0; nn < 16; ++nn) w[nn] = v[nn] + v[nn ^ o];
+                for (int nn = 0; nn < 16; ++nn) v[nn] = w[nn];
+            }
+            lg[k] = v[0];
+        }
         for (int s = 0; s < kInLd; ++s) {
             float v = 0.0f;
             if (s < 64) {
@@ -1234,7 +1256,8 @@ extern "C" int gala_cpu_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin
     return GALA_OK;
 }
 
-extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order_in, int32_t fin, int32_t heads,
+                                       int32_t D, float slope,
                                        float *Xext, const float *W, int64_t ldw, const float *b, float *Y,
                                        float *Ym, int64_t ldy, float *q, float *sma, void *stream) {
     (void)stream;
@@ -1244,7 +1267,7 @@ extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t
     if (A->n_rows == 0) return GALA_OK;
     if (!Xext || !W || !Y || !Ym || !q || !sma) return GALA_ERR_INVALID_ARG;
     const int H = heads;
-    const int32_t *order = A->split ? A->split->row_order : nullptr;
+    const int32_t *order = order_in ? order_in : (A->split ? A->split->row_order : nullptr);
     std::vector<float> qv((size_t)A->n_rows * H);
 #pragma omp parallel
     {
@@ -1312,7 +1335,8 @@ extern "C" int64_t gala_cpu_gat_in_bwd_workspace(int32_t heads) {
     return (int64_t)kInGrid * heads * 2 * kInTiles * 64 * 4 * (int64_t)sizeof(float);
 }
 
-extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order_in, int32_t fin, int32_t heads,
+                                       int32_t D, float slope,
                                        const float *Xext, const float *dY, const float *Y, const float *Ym,
                                        int64_t ldy, const float *sma, float *daL, float *M, void *ws,
                                        int64_t ws_bytes, void *stream) {
@@ -1327,7 +1351,7 @@ extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_
     if (AT->n_rows == 0) return GALA_OK;
     if (!Xext || !dY || !Y || !Ym || !sma || !daL || !ws) return GALA_ERR_INVALID_ARG;
     if (ws_bytes < gala_cpu_gat_in_bwd_workspace(heads)) return GALA_ERR_INVALID_ARG;
-    const int32_t *order = AT->split ? AT->split->row_order : nullptr;
+    const int32_t *order = order_in ? order_in : (AT->split ? AT->split->row_order : nullptr);
     const int64_t n = AT->n_rows, nblk = (n + kInWaves - 1) / kInWaves;
     const int grid = (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
     const int64_t per = (int64_t)H * D * (fin + 1);

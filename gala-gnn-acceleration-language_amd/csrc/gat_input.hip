@@ -38,6 +38,8 @@
 // backward -- and every sum is an f32 fmaf chain, regrouped (edge order inside an MFMA k-step,
 // the input-space association); the layer is checked against the oracle's pass-by-pass REF
 // layer at the Products shape (tests/test_gpu_gat_input.py).
+#include <cstdlib>
+
 #include "edge_common.h"
 
 namespace gala {
@@ -86,48 +88,61 @@ struct InPrepParams {
     float *xext;
 };
 
-// one thread per row: the 2H logit dots (u is wave-uniform: scalar loads) and the row's
-// extended image
+// 16 lanes per row, each owning the two float4 slots the aggregation kernels read (lane n:
+// features 4n..4n+3, and 64+3n..64+3n+2 for n < 12): the row's 2H logits are per-lane partial
+// dots (u held in registers for the lane's seven features, the grid persistent) summed by a
+// 16-lane butterfly, then every lane stores its two float4 (the row's 512 B, coalesced).
 __global__ __launch_bounds__(kBlock) void k_gat_in_prep(InPrepParams p) {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= p.n) return;
-    const float *x = p.X + r * p.ldx;
-    float *o = p.xext + r * kInLd;
-    float lg[2 * kInMaxHeads];
+    const int lane = threadIdx.x & 63, n = lane & 15;
+    const int64_t g0 = (int64_t)blockIdx.x * (kBlock / 16) + threadIdx.x / 16, gstep = (int64_t)gridDim.x * (kBlock / 16);
+    const int K = 2 * p.H;
+    float ua[2 * kInMaxHeads][4], ub[2 * kInMaxHeads][3];
 #pragma unroll
-    for (int k = 0; k < 2 * kInMaxHeads; ++k) lg[k] = 0.0f;
-    f4v img[kInLd / 4];
+    for (int k = 0; k < 2 * kInMaxHeads; ++k) {
 #pragma unroll
-    for (int i = 0; i < kInLd / 4; ++i) img[i] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int f = 0; f < p.fin; ++f) {
-        const float v = x[f];
-#pragma unroll
-        for (int k = 0; k < 2 * kInMaxHeads; ++k)
-            if (k < 2 * p.H) lg[k] = fmaf(v, p.u[k * p.fin + f], lg[k]);
-    }
-    // the image is assembled in registers (constant slots) and stored as 32 float4
-#pragma unroll
-    for (int s = 0; s < kInLd; ++s) {
-        float v = 0.0f;
-        if (s < 64) {
-            v = s < p.fin ? x[s] : 0.0f;
-        } else {
-            const int n = (s - 64) >> 2, cc = (s - 64) & 3;
-            if (cc < 3 && n < 12) {
-                const int f = 64 + 3 * n + cc;
-                v = f < p.fin ? x[f] : 0.0f;
-            } else if (s == kOnesSlot) {
-                v = 1.0f;
-            } else if (cc == 3 && n < kInMaxHeads) {
-                v = n < p.H ? __fadd_rn(lg[p.H + n], p.c[p.H + n]) : 0.0f;       // aR
-            } else if (cc == 3) {
-                v = n - 8 < p.H ? __fadd_rn(lg[n - 8], p.c[n - 8]) : 0.0f;       // aL
-            }
+        for (int i = 0; i < 4; ++i) {
+            const int f = 4 * n + i;
+            ua[k][i] = (k < K && f < p.fin) ? p.u[k * p.fin + f] : 0.0f;
         }
-        img[s >> 2][s & 3] = v;
-    }
 #pragma unroll
-    for (int i = 0; i < kInLd / 4; ++i) *reinterpret_cast<f4v *>(o + 4 * i) = img[i];
+        for (int i = 0; i < 3; ++i) {
+            const int f = 64 + 3 * n + i;
+            ub[k][i] = (k < K && n < 12 && f < p.fin) ? p.u[k * p.fin + f] : 0.0f;
+        }
+    }
+    const float cl = n >= 8 && n - 8 < p.H ? p.c[n - 8] : 0.0f;     // lane 8+h: aL[h]'s constant
+    const float cr = n < 8 && n < p.H ? p.c[p.H + n] : 0.0f;       // lane h: aR[h]'s
+    for (int64_t r = g0; r < p.n; r += gstep) {
+        const float *x = p.X + r * p.ldx;
+        float xa[4], xb[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xa[i] = 4 * n + i < p.fin ? x[4 * n + i] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xb[i] = (n < 12 && 64 + 3 * n + i < p.fin) ? x[64 + 3 * n + i] : 0.0f;
+        float lg[2 * kInMaxHeads];
+#pragma unroll
+        for (int k = 0; k < 2 * kInMaxHeads; ++k) {
+            float d = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d = fmaf(xa[i], ua[k][i], d);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) d = fmaf(xb[i], ub[k][i], d);
+            lg[k] = group_sum<16>(d);
+        }
+        // lane h < 8: aR[h] = lg[H + h] + cR; lane 8 + h: aL[h] = lg[h] + cL
+        float w = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 2 * kInMaxHeads; ++k) {
+            if (n < 8 && k == p.H + n) w = lg[k];
+            if (n >= 8 && k == n - 8) w = lg[k];
+        }
+        w = (n < 8 ? (n < p.H) : (n - 8 < p.H)) ? __fadd_rn(w, n < 8 ? cr : cl) : 0.0f;
+        f4v A = f4v{xa[0], xa[1], xa[2], xa[3]};
+        f4v B = n < 12 ? f4v{xb[0], xb[1], xb[2], w} : f4v{n == 12 ? 1.0f : 0.0f, 0.0f, 0.0f, w};
+        float *o = p.xext + r * kInLd;
+        *reinterpret_cast<f4v *>(o + 4 * n) = A;
+        *reinterpret_cast<f4v *>(o + 64 + 4 * n) = B;
+    }
 }
 
 struct InFwdParams {
@@ -185,7 +200,8 @@ __device__ __forceinline__ void gather_tiles(const int32_t *col, int64_t e0, int
 // variant v < 8, m * p of head v - 8 for v >= 8), parks its tiles in LDS, then wave h
 // projects the eight rows' head-h aggregates (M = 8 rows x {p, m p}, K = the 112 tile rows,
 // N = D) with W_ext,h fragments held in registers.
-__global__ __launch_bounds__(kInBlock) void k_gat_in_fwd(InFwdParams p) {
+template <int WPE>
+__global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_fwd(InFwdParams p) {
     __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // [slot][variant][tile][16 floats]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
@@ -295,8 +311,8 @@ __device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v)
 // Xin_ext[r] (alpha rebuilt from aL[r], q[r] in r's extended row and aR[c]) and c's d_aL from
 // the forward's row statistics; then wave h adds dY_h[c]^T T_h[c] of the eight columns into
 // its register accumulators M_h[D x 112] (K = the columns).  Partials per workgroup.
-template <int DW>
-__global__ __launch_bounds__(kInBlock) void k_gat_in_bwd(InBwdParams p) {
+template <int DW, int WPE>
+__global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_bwd(InBwdParams p) {
     __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
@@ -415,9 +431,17 @@ __global__ __launch_bounds__(kBlock) void k_gat_in_reduce(const float *part, int
     M[((int64_t)h * D + j) * (fin + 1) + (f == -2 ? fin : f)] = s;
 }
 
+// the aggregation kernels' occupancy target: 2 waves per SIMD (one workgroup of 8 waves per
+// CU, no spills) or 4 (two workgroups, registers capped at 128: spills).  GALA_GIN_WPE=4|2
+// (measured in tools/gat_input_bench.py)
+int waves_per_simd() {
+    const char *e = std::getenv("GALA_GIN_WPE");
+    return (e && e[0] == '4') ? 4 : 2;
+}
+
 int grid_for(int64_t n_rows) {
     const int64_t nblk = (n_rows + kInWaves - 1) / kInWaves;
-    return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
+    return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), (int64_t)kInGrid * (waves_per_simd() == 4 ? 1 : 1));
 }
 
 int check_in_graph(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D) {
@@ -442,12 +466,14 @@ extern "C" int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, in
     if (n == 0) return GALA_OK;
     if (!Xin || !u || !c || !Xext || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
     InPrepParams p{Xin, n, ldxin, fin, heads, u, c, Xext};
-    hipLaunchKernelGGL(k_gat_in_prep, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+    const int64_t groups = (n + kBlock / 16 - 1) / (kBlock / 16);
+    hipLaunchKernelGGL(k_gat_in_prep, dim3((unsigned)std::min<int64_t>(groups, 4096)), dim3(kBlock), 0,
                        (hipStream_t)stream, p);
     return launch_status();
 }
 
-extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                   float slope,
                                    float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
                                    int64_t ldy, float *q, float *sma, void *stream) {
     int st = check_in_graph(A, fin, heads, D);
@@ -455,9 +481,13 @@ extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t hea
     if (ldw < fin || ldy < (int64_t)heads * D) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!Xext || !W || !Y || !Ym || !q || !sma || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
-    InFwdParams p{A->rowptr, A->col, A->split ? A->split->row_order : nullptr, A->n_rows, Xext, W, b, ldw,
+    InFwdParams p{A->rowptr, A->col, order ? order : (A->split ? A->split->row_order : nullptr), A->n_rows, Xext, W,
+                  b, ldw,
                   fin, heads, D, slope, Y, Ym, q, sma, ldy};
-    hipLaunchKernelGGL(k_gat_in_fwd, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
+    if (waves_per_simd() == 4)
+        hipLaunchKernelGGL(k_gat_in_fwd<4>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(k_gat_in_fwd<2>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
     return launch_status();
 }
 
@@ -466,7 +496,8 @@ extern "C" int64_t gala_gat_in_bwd_workspace(int32_t heads) {
     return (int64_t)kInGrid * heads * 2 * kInTiles * 64 * 4 * (int64_t)sizeof(float);
 }
 
-extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                   float slope,
                                    const float *Xext, const float *dY, const float *Y, const float *Ym,
                                    int64_t ldy, const float *sma, float *daL, float *M, void *ws_,
                                    int64_t ws_bytes, void *stream) {
@@ -485,14 +516,19 @@ extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t he
         return GALA_ERR_INVALID_ARG;
     if (ws_bytes < gala_gat_in_bwd_workspace(heads)) return GALA_ERR_INVALID_ARG;
     const int grid = grid_for(AT->n_rows);
-    InBwdParams p{AT->rowptr, AT->col, AT->split ? AT->split->row_order : nullptr, AT->n_rows, Xext, dY, Y, Ym,
+    InBwdParams p{AT->rowptr, AT->col, order ? order : (AT->split ? AT->split->row_order : nullptr), AT->n_rows, Xext,
+                  dY, Y, Ym,
                   sma, ldy, fin, heads, D, slope, daL, ws};
     if (hipMemsetAsync(M, 0, outn * sizeof(float), hs) != hipSuccess) return GALA_ERR_HIP;
+    const bool w4 = waves_per_simd() == 4;
     switch (D / 4) {
-    case 1: hipLaunchKernelGGL(k_gat_in_bwd<1>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 2: hipLaunchKernelGGL(k_gat_in_bwd<2>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 4: hipLaunchKernelGGL(k_gat_in_bwd<4>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    default: hipLaunchKernelGGL(k_gat_in_bwd<8>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 1: hipLaunchKernelGGL((k_gat_in_bwd<1, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 2: hipLaunchKernelGGL((k_gat_in_bwd<2, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 4: hipLaunchKernelGGL((k_gat_in_bwd<4, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    default:
+        if (w4) hipLaunchKernelGGL((k_gat_in_bwd<8, 4>), dim3(grid), dim3(kInBlock), 0, hs, p);
+        else hipLaunchKernelGGL((k_gat_in_bwd<8, 2>), dim3(grid), dim3(kInBlock), 0, hs, p);
+        break;
     }
     st = launch_status();
     if (st) return st;

@@ -1517,7 +1517,8 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         auto Y = torch::empty({N, F}, fopts(x)), Ym = torch::empty({N, F}, fopts(x));
         auto q = torch::empty({N, H}, fopts(x)), sma = torch::empty({N, H}, fopts(x));
         torch::Tensor bc = has_b ? b.contiguous() : torch::Tensor();
-        check(B.gat_in_fwd(&cv.c, (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+        const PatternT &pt = transposed_pattern(2 * li);
+        check(B.gat_in_fwd(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
                            w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr, Y.data_ptr<float>(),
                            Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(), stream_of(x)),
               "gala_gat_in_fwd_f32");
@@ -1548,7 +1549,7 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         const int64_t wsb = B.gat_in_ws((int32_t)H);
         TORCH_CHECK(wsb > 0, "gala: gala_gat_in_bwd_workspace failed");
         auto ws = torch::empty({wsb / 4}, fopts(x));
-        check(B.gat_in_bwd(&cv.c, (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+        check(B.gat_in_bwd(&cv.c, pt.order_t.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
                            dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F, sma.data_ptr<float>(),
                            daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb, stream_of(x)),
               "gala_gat_in_bwd_f32");
@@ -1592,12 +1593,20 @@ const PatternT &transposed_pattern(int64_t idx) {
           "gala_host_csr_transpose");
     auto p = std::make_shared<PatternT>();
     p->symmetric = torch::equal(tr, off) && torch::equal(tc, col);
+    const auto dev = S.offset_graph[idx].device();
+    auto ord = torch::empty({n}, io);
+    check(gala_host_row_order(n, off.data_ptr<int32_t>(), ord.data_ptr<int32_t>()), "gala_host_row_order");
+    p->order = ord.to(dev);
     if (p->symmetric) {
         p->rowptr = S.offset_graph[idx];
         p->col = S.columns_graph[idx];
+        p->order_t = p->order;
     } else {
-        p->rowptr = tr.to(S.offset_graph[idx].device());
-        p->col = tc.to(S.offset_graph[idx].device());
+        p->rowptr = tr.to(dev);
+        p->col = tc.to(dev);
+        auto ot = torch::empty({n}, io);
+        check(gala_host_row_order(n, tr.data_ptr<int32_t>(), ot.data_ptr<int32_t>()), "gala_host_row_order");
+        p->order_t = ot.to(dev);
     }
     pt = p;
     return *pt;

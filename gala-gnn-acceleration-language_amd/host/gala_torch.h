@@ -60,10 +60,12 @@ std::shared_ptr<MergedCsr> make_merged_csr(const torch::Tensor &offsets, const t
                                            const torch::Tensor &bounds_host, int segments);
 
 // The transposed pattern of a one-segment slot graph, built on first use (the input-space
-// GAT backward walks it): the slot's own tensors when the pattern is symmetric.
+// GAT backward walks it): the slot's own tensors when the pattern is symmetric; with the
+// descending-degree row orders of both (gala_host_row_order: equal-length rows per phase).
 struct PatternT {
     torch::Tensor rowptr, col;
     bool symmetric = false;
+    torch::Tensor order, order_t;   // rows of the pattern / of its transpose by descending degree
 };
 
 // The generated program's graph slots (codegen/gala.cu:32-43): slot 2*li is layer li's

@@ -561,6 +561,9 @@ int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float
  *   gala_gat_in_prep_f32: Xext [n][128] (16-B aligned) = the extended rows: Xin's fin <= 100
  *     features, the ones column, aL / aR (u [2H][fin]: uL rows then uR rows; c [2H]).  Every
  *     forward (aL / aR follow the weights).
+ *   order (nullable; else A->split->row_order, else row-id order): the order rows (columns) are
+ *     taken in, eight per workgroup phase -- a descending-degree order (gala_host_row_order)
+ *     gives the eight rows of a phase equal lengths.
  *   gala_gat_in_fwd_f32: Y, Ym [n][ldy] (Ym = the m-weighted aggregate, m = 1 or slope by the
  *     logit's sign), q, sma [n][H] (the row statistics of gala_gat_fwd_stats_f32); writes q
  *     into Xext too (the backward reads it there).  W [H*D][ldw], b [H*D] nullable.
@@ -578,11 +581,11 @@ int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float
  */
 int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t ldxin, int32_t heads,
                          const float *u, const float *c, float *Xext, void *stream);
-int gala_gat_in_fwd_f32(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D, float slope,
+int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                         float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
                         int64_t ldy, float *q, float *sma, void *stream);
 int64_t gala_gat_in_bwd_workspace(int32_t heads);
-int gala_gat_in_bwd_f32(const gala_csr_t *AT, int32_t fin, int32_t heads, int32_t D, float slope,
+int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                         const float *Xext, const float *dY, const float *Y, const float *Ym,
                         int64_t ldy, const float *sma, float *daL, float *M, void *ws,
                         int64_t ws_bytes, void *stream);

@@ -42,7 +42,7 @@ def compose(W, b, wL, bL, wR, bR, heads):
     return u.numpy(), c.numpy()
 
 
-def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2):
+def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, order=None, order_t=None):
     """The host twins composed as the mirror's GatInputLayer composes the GPU ops (the
     backward over the transposed pattern: g itself when it is symmetric)."""
     n, fin = X.shape
@@ -54,7 +54,7 @@ def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2):
     A = HostCsr(g)
     Y, Ym = np.empty((n, F), np.float32), np.empty((n, F), np.float32)
     q, sma = np.empty((n, heads), np.float32), np.empty((n, heads), np.float32)
-    _abi.call_cpu("gala_gat_in_fwd_f32", A.ref, fin, heads, D, slope, P(xext), P(W), fin, P(b), P(Y), P(Ym), F,
+    _abi.call_cpu("gala_gat_in_fwd_f32", A.ref, P(order), fin, heads, D, slope, P(xext), P(W), fin, P(b), P(Y), P(Ym), F,
                   P(q), P(sma), None)
     daL = np.empty((n, heads), np.float32)
     M = np.empty((heads, D, fin + 1), np.float32)
@@ -62,7 +62,7 @@ def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2):
     ws = np.empty(wsb // 4, np.float32)
     gT, _ = layout.transpose(g)
     AT = HostCsr(gT)
-    _abi.call_cpu("gala_gat_in_bwd_f32", AT.ref, fin, heads, D, slope, P(xext), P(dY), P(Y), P(Ym), F, P(sma),
+    _abi.call_cpu("gala_gat_in_bwd_f32", AT.ref, P(order_t), fin, heads, D, slope, P(xext), P(dY), P(Y), P(Ym), F, P(sma),
                   P(daL), P(M), P(ws), wsb, None)
     Gw, Gb = np.empty((heads, fin), np.float32), np.empty(heads, np.float32)
     gwb = _abi.cpu_lib().gala_cpu_dense_grad_workspace(n, fin, heads)
@@ -142,14 +142,14 @@ def test_input_space_refusals():
     q = np.zeros((100, 8), np.float32)
     L = _abi.cpu_lib()
     # fin > 100, D not in {4, 8, 16, 32}, more than 8 heads: unsupported (callers keep the chain)
-    assert L.gala_cpu_gat_in_fwd_f32(A.ref, 101, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
+    assert L.gala_cpu_gat_in_fwd_f32(A.ref, None, 101, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
                                      None) == _abi.GALA_ERR_UNSUPPORTED
-    assert L.gala_cpu_gat_in_fwd_f32(A.ref, 100, 8, 24, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
+    assert L.gala_cpu_gat_in_fwd_f32(A.ref, None, 100, 8, 24, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
                                      None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_prep_f32(100, 101, P(X), 128, 8, P(W), P(W), P(xext), None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_prep_f32(100, 100, P(X), 99, 8, P(W), P(W), P(xext), None) == _abi.GALA_ERR_INVALID_ARG
     t = HostCsr(layout.col_tile(g, 40))
-    assert L.gala_cpu_gat_in_fwd_f32(t.ref, 100, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
+    assert L.gala_cpu_gat_in_fwd_f32(t.ref, None, 100, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
                                      None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_bwd_workspace(9) < 0
 
