@@ -164,36 +164,114 @@ __device__ __forceinline__ int64_t batch_col(int32_t win, int j0, int s, int kq)
     return (int64_t)__builtin_amdgcn_ds_bpermute(src * 4, win);
 }
 
-// a row's (or transposed column's) 7 feature tiles of sum_e B_e * Xext[nb_e], B from bfn
+// the 16-edge batch j0 of a row: lane (16 kq + n) requests slots 4n.. and 64+4n.. of the
+// extended rows of edges j0 + 4s + kq (s = 0..3)
+__device__ __forceinline__ void load_batch(const float *xext, int32_t win, int32_t j0, int kq, int n16,
+                                           f4v (&xa)[4], f4v (&xb)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int64_t c = batch_col(win, j0, s, kq);
+        xa[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 4 * n16);
+        xb[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 64 + 4 * n16);
+    }
+}
+
+// the batch's four k-steps into the 7 feature tiles: B = bfn(the lane's second float4, edge valid)
 template <typename BFn>
-__device__ __forceinline__ void gather_tiles(const int32_t *col, int64_t e0, int32_t deg, const float *xext,
-                                             int lane, BFn &&bfn, f4v (&acc)[kInTiles]) {
+__device__ __forceinline__ void mfma_batch(const f4v (&xa)[4], const f4v (&xb)[4], int32_t j0, int32_t deg, int kq,
+                                           int n16, BFn &&bfn, f4v (&acc)[kInTiles]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const bool ok = j0 + 4 * s + kq < deg;
+        const float bv = bfn(xb[s], ok);
+        acc[0] = mfma4(xa[s][0], bv, acc[0]);
+        acc[1] = mfma4(xa[s][1], bv, acc[1]);
+        acc[2] = mfma4(xa[s][2], bv, acc[2]);
+        acc[3] = mfma4(xa[s][3], bv, acc[3]);
+        // lanes 13..15 of the second float4 hold q (and lane 12's .yz zeros): not features
+        const bool feat = n16 < 13;
+        acc[4] = mfma4(feat ? xb[s][0] : 0.0f, bv, acc[4]);
+        acc[5] = mfma4(feat ? xb[s][1] : 0.0f, bv, acc[5]);
+        acc[6] = mfma4(feat ? xb[s][2] : 0.0f, bv, acc[6]);
+    }
+}
+
+// One wave's walk over its rows (one per workgroup phase), software-pipelined so that a
+// phase's barriers and projection do not drain the wave's memory pipeline: a row's next
+// 16-edge batch is requested before the current one is summed, and the NEXT phase's row
+// bounds (scalar loads), column window, row-local slot (`side`) and first batch are requested
+// while this row is walked.  The cursor holds the current row; walk() advances it to `next`
+// (-1: none).
+struct RowCursor {
+    int64_t e0 = 0;
+    int32_t deg = 0, win = 0;
+    float side = 0.0f;     // xext[row * 128 + side_slot]: aL (forward) / aR (backward) of the lane's head
+    f4v xa[4], xb[4];      // the row's first batch (requested)
+};
+
+__device__ __forceinline__ void cursor_start(RowCursor &c, const int32_t *rowptr, const int32_t *col,
+                                             const float *xext, int64_t row, int side_slot, bool side_ok, int lane) {
     const int n16 = lane & 15, kq = lane >> 4;
-    int32_t win = 0;
-    for (int32_t j0 = 0; j0 < deg; j0 += 16) {
-        if ((j0 & 63) == 0) win = col[e0 + ((j0 + lane < deg) ? j0 + lane : deg - 1)];
-        f4v xa[4], xb[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int64_t c = batch_col(win, j0, s, kq);
-            xa[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 4 * n16);
-            xb[s] = *reinterpret_cast<const f4v *>(xext + c * kInLd + 64 + 4 * n16);
+    c.e0 = 0;
+    c.deg = 0;
+    c.side = 0.0f;
+    if (row < 0) return;
+    c.e0 = uniform(rowptr[row]);
+    c.deg = uniform(rowptr[row + 1]) - (int32_t)c.e0;
+    c.side = side_ok ? xext[row * kInLd + side_slot] : 0.0f;
+    if (c.deg > 0) {
+        c.win = col[c.e0 + (lane < c.deg ? lane : c.deg - 1)];
+        load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
+    }
+}
+
+template <typename BFn>
+__device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr, const int32_t *col,
+                                            const float *xext, int64_t next, int side_slot, bool side_ok, int lane,
+                                            BFn &&bfn, f4v (&acc)[kInTiles]) {
+    const int n16 = lane & 15, kq = lane >> 4;
+    // the next row's bounds: scalar loads (their own counter), waited for only below
+    int64_t ne0 = 0;
+    int32_t nend = 0;
+    if (next >= 0) {
+        const int64_t nx = __builtin_amdgcn_readfirstlane((int32_t)next);
+        ne0 = rowptr[nx];
+        nend = rowptr[nx + 1];
+    }
+    int32_t nwin = 0;
+    float nside = 0.0f;
+    bool next_issued = false;
+    auto issue_next = [&]() {
+        if (next < 0 || next_issued) return;
+        next_issued = true;
+        const int32_t nd = nend - (int32_t)ne0;
+        if (nd > 0) nwin = col[ne0 + (lane < nd ? lane : nd - 1)];
+        nside = side_ok ? xext[next * kInLd + side_slot] : 0.0f;
+    };
+    for (int32_t j0 = 0; j0 < c.deg; j0 += 16) {
+        const int32_t j1 = j0 + 16;
+        f4v ya[4], yb[4];
+        const bool more = j1 < c.deg;
+        if (more) {
+            if ((j1 & 63) == 0) c.win = col[c.e0 + ((j1 + lane < c.deg) ? j1 + lane : c.deg - 1)];
+            load_batch(xext, c.win, j1, kq, n16, ya, yb);
         }
+        if (j0 == 0) issue_next();
+        mfma_batch(c.xa, c.xb, j0, c.deg, kq, n16, bfn, acc);
+        if (more) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const bool ok = j0 + 4 * s + kq < deg;
-            const float bv = bfn(xb[s], ok);
-            acc[0] = mfma4(xa[s][0], bv, acc[0]);
-            acc[1] = mfma4(xa[s][1], bv, acc[1]);
-            acc[2] = mfma4(xa[s][2], bv, acc[2]);
-            acc[3] = mfma4(xa[s][3], bv, acc[3]);
-            // lanes 13..15 of the second float4 hold q (and lane 12's .yz zeros): not features
-            const bool feat = n16 < 13;
-            acc[4] = mfma4(feat ? xb[s][0] : 0.0f, bv, acc[4]);
-            acc[5] = mfma4(feat ? xb[s][1] : 0.0f, bv, acc[5]);
-            acc[6] = mfma4(feat ? xb[s][2] : 0.0f, bv, acc[6]);
+            for (int s = 0; s < 4; ++s) {
+                c.xa[s] = ya[s];
+                c.xb[s] = yb[s];
+            }
         }
     }
+    issue_next();   // (an empty row walked no batch)
+    c.e0 = uniform((int32_t)ne0);
+    c.deg = next >= 0 ? uniform(nend - (int32_t)ne0) : 0;
+    c.win = nwin;
+    c.side = nside;
+    if (c.deg > 0) load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
 }
 
 // Forward.  Workgroup phase: wave w aggregates row order[8 blk + w] (B = p of head v for
@@ -203,7 +281,7 @@ __device__ __forceinline__ void gather_tiles(const int32_t *col, int64_t e0, int
 template <int WPE>
 __global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_fwd(InFwdParams p) {
     __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // [slot][variant][tile][16 floats]
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
     // B fragments of the projection: W_ext,h[j = 16 nt + n16][feature(t, 4 kq + q4)]
     float wf[kInTiles][4][2];
@@ -224,29 +302,33 @@ __global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_fwd(InFwdParams p) {
             }
     const float *stf = reinterpret_cast<const float *>(stash);
     const int64_t nblk = (p.n_rows + kInWaves - 1) / kInWaves;
+    auto row_of = [&](int64_t b) -> int64_t {
+        const int64_t ri = b * kInWaves + wave;
+        if (b >= nblk || ri >= p.n_rows) return -1;
+        return p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[ri]) : ri;
+    };
+    const bool side_ok = n16 < p.H;
+    RowCursor cur;
+    cursor_start(cur, p.rowptr, p.col, p.xext, row_of(blockIdx.x), aL_slot(n16 & 7), side_ok, lane);
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         f4v acc[kInTiles];
 #pragma unroll
         for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        const int64_t ri = blk * kInWaves + wave;
-        if (ri < p.n_rows) {
-            const int64_t r = p.order ? (int64_t)p.order[ri] : ri;
-            const int64_t e0 = uniform(p.rowptr[r]);
-            const int32_t deg = uniform(p.rowptr[r + 1] - p.rowptr[r]);
-            const float al = n16 < p.H ? p.xext[r * kInLd + aL_slot(n16)] : 0.0f;
+        {
+            const float al = cur.side;
             const int H = p.H;
             const float slope = p.slope;
-            gather_tiles(p.col, e0, deg, p.xext, lane,
-                         [&](const f4v &xb, bool ok) {
-                             const float t = __fadd_rn(al, xb[3]);   // lanes v < 8: aR[col][v]
-                             const bool pos = t > 0.0f;
-                             float pv = ref_exp(pos ? t : __fmul_rn(t, slope));
-                             if (!(ok && n16 < H)) pv = 0.0f;
-                             const float mp = pos ? pv : __fmul_rn(pv, slope);
-                             const float mpo = ror8(mp);
-                             return n16 < 8 ? pv : mpo;
-                         },
-                         acc);
+            cursor_walk(cur, p.rowptr, p.col, p.xext, row_of(blk + gridDim.x), aL_slot(n16 & 7), side_ok, lane,
+                        [&](const f4v &xb, bool ok) {
+                            const float t = __fadd_rn(al, xb[3]);   // lanes v < 8: aR[col][v]
+                            const bool pos = t > 0.0f;
+                            float pv = ref_exp(pos ? t : __fmul_rn(t, slope));
+                            if (!(ok && n16 < H)) pv = 0.0f;
+                            const float mp = pos ? pv : __fmul_rn(pv, slope);
+                            const float mpo = ror8(mp);
+                            return n16 < 8 ? pv : mpo;
+                        },
+                        acc);
         }
 #pragma unroll
         for (int t = 0; t < kInTiles; ++t) stash[((wave * 16 + n16) * kInTiles + t) * 4 + kq] = acc[t];
@@ -314,7 +396,7 @@ __device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v)
 template <int DW, int WPE>
 __global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_bwd(InBwdParams p) {
     __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
     const float *stf = reinterpret_cast<const float *>(stash);
     f4v M[2][kInTiles];
@@ -327,53 +409,59 @@ __global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_bwd(InBwdParams p) {
     // q[h] of a gathered row: lane 13 + h / 3 of its edge's 16 lanes, component h % 3
     const int hq = n16 & 7;
     const int qsrc = (16 * kq + 13 + hq / 3) * 4, qc = hq % 3;
+    auto col_of = [&](int64_t b) -> int64_t {
+        const int64_t ci = b * kInWaves + wave;
+        if (b >= nblk || ci >= p.n_rows) return -1;
+        return p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[ci]) : ci;
+    };
+    const bool side_ok = n16 < p.H;
+    RowCursor cur;
+    cursor_start(cur, p.rowptr, p.col, p.xext, col_of(blockIdx.x), aR_slot(n16 & 7), side_ok, lane);
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         f4v acc[kInTiles];
 #pragma unroll
         for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
-        const int64_t ci = blk * kInWaves + wave;
-        if (ci < p.n_rows) {
-            const int64_t c = p.order ? (int64_t)p.order[ci] : ci;
-            const int64_t e0 = uniform(p.rowptr[c]);
-            const int32_t deg = uniform(p.rowptr[c + 1] - p.rowptr[c]);
-            const float ar = n16 < p.H ? p.xext[c * kInLd + aR_slot(n16)] : 0.0f;
+        const int64_t c = col_of(blk);
+        // the column's row statistics for d_aL, requested before the walk (F = H*D <= 256:
+        // one float4 per lane)
+        const int f = 4 * lane;
+        f4v dy = f4v{0.0f, 0.0f, 0.0f, 0.0f}, yy = dy, ym = dy;
+        if (c >= 0 && f < F) {
+            dy = *reinterpret_cast<const f4v *>(p.dY + c * p.ldy + f);
+            yy = *reinterpret_cast<const f4v *>(p.Y + c * p.ldy + f);
+            ym = *reinterpret_cast<const f4v *>(p.Ym + c * p.ldy + f);
+        }
+        {
+            const float ar = cur.side;
             const int H = p.H;
             const float slope = p.slope;
-            gather_tiles(p.col, e0, deg, p.xext, lane,
-                         [&](const f4v &xb, bool ok) {
-                             const float alr = ror8(xb[3]);            // aL[r][v] from lane v + 8
-                             const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
-                             const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
-                             const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
-                             const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
-                             const float t = __fadd_rn(alr, ar);
-                             const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
-                             const float a = __fmul_rn(pv, qr);       // K8: alpha = p * q[row]
-                             return (ok && n16 < H) ? a : 0.0f;
-                         },
-                         acc);
-            // d_aL[c] from the forward's row statistics (gala_gat_bwd_stats_f32's formula)
-            for (int f0 = 0; f0 < F; f0 += 4 * kWave) {
-                const int f = f0 + 4 * lane;
-                f4v dy = f4v{0.0f, 0.0f, 0.0f, 0.0f}, yy = dy, ym = dy;
-                if (f < F) {
-                    dy = *reinterpret_cast<const f4v *>(p.dY + c * p.ldy + f);
-                    yy = *reinterpret_cast<const f4v *>(p.Y + c * p.ldy + f);
-                    ym = *reinterpret_cast<const f4v *>(p.Ym + c * p.ldy + f);
-                }
-                float syy = 0.0f, sym = 0.0f;
+            cursor_walk(cur, p.rowptr, p.col, p.xext, col_of(blk + gridDim.x), aR_slot(n16 & 7), side_ok, lane,
+                        [&](const f4v &xb, bool ok) {
+                            const float alr = ror8(xb[3]);            // aL[r][v] from lane v + 8
+                            const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
+                            const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
+                            const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
+                            const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
+                            const float t = __fadd_rn(alr, ar);
+                            const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
+                            const float a = __fmul_rn(pv, qr);       // K8: alpha = p * q[row]
+                            return (ok && n16 < H) ? a : 0.0f;
+                        },
+                        acc);
+        }
+        if (c >= 0) {   // d_aL[c] from the forward's row statistics (gala_gat_bwd_stats_f32's formula)
+            float syy = 0.0f, sym = 0.0f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    syy = fmaf(dy[i], yy[i], syy);
-                    sym = fmaf(dy[i], ym[i], sym);
-                }
-                syy = head_dot_sum<DW>(syy);
-                sym = head_dot_sum<DW>(sym);
-                if (f < F && (f % p.D) == 0) {
-                    const int hh = f / p.D;
-                    const float accv = syy + 1e-12f;                       // K7 on sds (common.h:793-794)
-                    p.daL[c * p.H + hh] = (sym - accv * p.sma[c * p.H + hh]) + 1e-12f;   // common.h:662-667
-                }
+            for (int i = 0; i < 4; ++i) {
+                syy = fmaf(dy[i], yy[i], syy);
+                sym = fmaf(dy[i], ym[i], sym);
+            }
+            syy = head_dot_sum<DW>(syy);
+            sym = head_dot_sum<DW>(sym);
+            if (f < F && (f % p.D) == 0) {
+                const int hh = f / p.D;
+                const float accv = syy + 1e-12f;                       // K7 on sds (common.h:793-794)
+                p.daL[c * p.H + hh] = (sym - accv * p.sma[c * p.H + hh]) + 1e-12f;   // common.h:662-667
             }
         }
         if (n16 < kInMaxHeads) {
