@@ -874,89 +874,142 @@ def run_single(args, dev, be, timer, sync):
 
 
 GAT_HEADS, GAT_HEAD_F = 8, 32   # BASELINE configs[2]: ogbn-products GAT, 8 heads x 32 (galac gat_heads(8))
+GAT_IN_F = 100                  # ogbn-products node features (bench/dsl/gat_products_h8.txt feature_size)
 
 
 def gat_layer(args, dg, hg, dev, timer, sync):
-    """SDDMM + edge-softmax + aggregation throughput on the same graph: one 8-head GAT layer
-    of config 3 (bench/dsl/gat_products_h8.txt), forward + backward, as the generated
-    program runs it (REF undirected layer, source logit recomputed from X):
-        forward   gala_gat_fwd_stats_f32  per edge: logit aL[r] + <X[c], wR_h> + bR_h,
-                  LeakyReLU, exp, alpha * X[c] into Y and Ym; per row q = 1/sum, sum m*alpha
-        backward  gala_gat_bwd_stats_f32  per edge: alpha from aR[c], dX[r] += alpha*dY[c];
-                  per row d_aL from <dY[r], Y[r]>, <dY[r], Ym[r]>
-    (the edge chains of cuda.h:505-562,679-845 and common.h:622-894 fused).  value counts
-    2*E edges per step (the forward's and the backward's pass over every edge)."""
+    """SDDMM + edge-softmax + aggregation throughput on the same graph: config 3's first GAT
+    layer (bench/dsl/gat_products_h8.txt: 100 input features -> 8 heads x 32), forward +
+    backward, from the 100-d input with the Linear included, as the generated program runs it
+    (galac emits gala::gat_input_layer_apply for it):
+        forward   the attention vectors folded through the Linear (uL, uR), the extended input
+                  rows (gala_gat_in_prep_f32), then gala_gat_in_fwd_f32: per edge p =
+                  exp(LeakyReLU(aL[r] + aR[c])) and the 512-B extended row of c into the
+                  per-head input-space aggregates (matrix cores), projected per row by the
+                  Linear into Y and Ym, with q = 1/(1e-12 + sum p) and sum m*alpha
+        backward  gala_gat_in_bwd_f32 over the transposed pattern (the symmetric graph itself):
+                  T_h[c] = sum alpha X_ext[r], M_h += dY_h[c]^T T_h[c], d_aL from <dY, Y>,
+                  <dY, Ym>; then G = d_aL^T X (gala_dense_grad_f32) and the parameter
+                  gradients of W, b and both attention Linears
+    (the reference's FFN_OP + attention Linears + the edge chains of cuda.h:505-562,679-845 and
+    common.h:622-894, fused and regrouped in input space; tests/test_gpu_gat_input.py checks it
+    against the oracle's pass-by-pass chain at this size).  `gathering_linear_output` times the
+    previous formulation beside it: the Linear's 1-KB output rows gathered by the row-statistics
+    pair (gala_gat_{fwd,bwd}_stats_f32).  value counts 2*E edges per step (the forward's and the
+    backward's pass over every edge)."""
     import torch
     from gala import ops
-    H, F = GAT_HEADS, GAT_HEADS * GAT_HEAD_F
+    H, D = GAT_HEADS, GAT_HEAD_F
+    F, FIN = H * D, GAT_IN_F
     N, E = hg.n_rows, hg.nnz
     gen = torch.Generator(device=dev).manual_seed(4321)
-    X = torch.rand((N, F), device=dev, generator=gen) * 2 - 1
+    Xin = torch.rand((N, FIN), device=dev, generator=gen) * 2 - 1
     dY = torch.rand((N, F), device=dev, generator=gen) * 2 - 1
-    aL = torch.rand((N, H), device=dev, generator=gen) - 0.5
-    wR = (torch.rand(F, device=dev, generator=gen) - 0.5) * 0.2
-    bR = torch.zeros(H, device=dev)
+    W = (torch.rand((F, FIN), device=dev, generator=gen) * 2 - 1) / 10
+    b = (torch.rand(F, device=dev, generator=gen) - 0.5) * 0.2
+    wL, wR = ((torch.rand(F, device=dev, generator=gen) - 0.5) * 0.6 for _ in range(2))
+    bL, bR = ((torch.rand(H, device=dev, generator=gen) - 0.5) * 0.2 for _ in range(2))
+    order = torch.from_numpy(ops.degree_order(hg.rowptr)).to(dev)   # the mirror's phase order
     st = {}
 
     def fwd():
-        st["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+        st["f"] = ops.gat_input_layer(dg, Xin, W, b, wL, bL, wR, bR, H, order=order)
 
     def bwd():
-        Y, q, Ym, sma, aRo = st["f"]
-        st["b"] = ops.gat_bwd_stats(dg, aL, aRo, dY, q, Y, Ym, sma, heads=H)
+        f = st["f"]
+        daL, M = ops.gat_in_bwd(dg, f["xext"], dY, f["Y"], f["Ym"], f["sma"], H, FIN, order=order)
+        Gw, Gb = ops.dense_grad(Xin, daL)
+        sLR = (wL + wR).reshape(H, D)
+        dW = M[:, :, :FIN] + sLR.unsqueeze(2) * Gw.unsqueeze(1)
+        db = M[:, :, FIN] + sLR * Gb.unsqueeze(1)
+        dw = (W.reshape(H, D, FIN) * Gw.unsqueeze(1)).sum(2) + b.reshape(H, D) * Gb.unsqueeze(1)
+        st["b"] = (dW, db, dw, Gb)
 
     def step():
         fwd()
         bwd()
     steps = max(args.steps // 2, 2)
     t_step = timed_steps(step, steps, 2, sync, lambda: None, lambda x: x)
-    # the kernels and the same-process gather probe, interleaved over three rounds (medians):
-    # both move by up to 10 % with the GPU's load state, so a probe timed apart from the
-    # kernels gives an unstable ratio (DESIGN §4.4)
-    rounds = {"fwd": [], "bwd": [], "ceil": []}
+    f0 = st["f"]
+    xext, Y0, Ym0, sma0 = f0["xext"], f0["Y"], f0["Ym"], f0["sma"]
+
+    def k_fwd():   # the aggregation kernel alone (its extended rows prepared)
+        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order)
+
+    def k_bwd():
+        ops.gat_in_bwd(dg, xext, dY, Y0, Ym0, sma0, H, FIN, order=order)
+    # the layer, its two kernels and the same-process gather probe of the 512-B extended rows,
+    # interleaved over three rounds (medians: all move by up to 10 % with the GPU's load state,
+    # DESIGN §4.4)
+    rounds = {"fwd": [], "bwd": [], "k_fwd": [], "k_bwd": [], "ceil": []}
     for _ in range(3):
         rounds["fwd"].append(timer(fwd, 5))
         rounds["bwd"].append(timer(bwd, 5))
-        t_c = gather_ceiling(dg.col, X, timer, reps=5)
+        rounds["k_fwd"].append(timer(k_fwd, 5))
+        rounds["k_bwd"].append(timer(k_bwd, 5))
+        t_c = gather_ceiling(dg.col, xext, timer, reps=5)
         if t_c:
             rounds["ceil"].append(t_c)
     med = lambda xs: sorted(xs)[len(xs) // 2] if xs else None  # noqa: E731
-    t_fwd, t_bwd = med(rounds["fwd"]), med(rounds["bwd"])
-    # forward stats kernel, SURVEY §8(d) model (X read once, no per-edge outputs):
-    # rowptr + col + X + Y + Ym + aL, q, sum m*alpha, aR_out per row and head + wR
-    alg = 4 * (N + 1) + 4 * E + 3 * 4 * N * F + 4 * 4 * N * H + 4 * F
+    t_fwd, t_bwd, t_kf, t_kb = (med(rounds[k]) for k in ("fwd", "bwd", "k_fwd", "k_bwd"))
+    # algorithmic bytes per launch, SURVEY §8(d)'s model (every operand once, no per-edge
+    # outputs): forward rowptr + col + the extended rows + Y, Ym + q, sma (+ q into the rows)
+    # + W; backward rowptr + col + the extended rows + dY, Y, Ym + sma + d_aL
+    alg = 4 * (N + 1) + 4 * E + 512 * N + 2 * 4 * N * F + 3 * 4 * N * H + 4 * F * (FIN + 1)
+    alg_b = 4 * (N + 1) + 4 * E + 512 * N + 3 * 4 * N * F + 2 * 4 * N * H
     out = {"value": 2 * E / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
-           "layer": f"GAT {H} heads x {GAT_HEAD_F} (F={F}), REF softmax, source logit recomputed; forward + backward",
+           "layer": (f"GAT layer 1 of config 3: {FIN} input features -> {H} heads x {D} (F={F}), Linear + both "
+                     f"attention Linears + REF softmax aggregation, input space; forward + backward with every "
+                     f"parameter gradient"),
            "fwd_ms": t_fwd * 1e3, "bwd_ms": t_bwd * 1e3,
-           "roofline": {"bound": "hbm", "achieved": alg / t_fwd / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                        "frac": alg / t_fwd / HBM_PEAK, "kernel_ms": t_fwd * 1e3, "alg_bytes_per_launch": alg,
-                        "traffic": load_traffic("k_gat_fwd<64, 4, 8, 2, 1, true, 8>"),
-                        "kernel": "gala::k_gat_fwd<64,4,8,2,1,true,8> (gala_gat_fwd_stats_f32, 8 heads, F=256)",
+           "roofline": {"bound": "hbm", "achieved": alg / t_kf / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": alg / t_kf / HBM_PEAK, "kernel_ms": t_kf * 1e3, "alg_bytes_per_launch": alg,
+                        "traffic": load_traffic("k_gat_in_fwd"),
+                        "kernel": "gala::k_gat_in_fwd (gala_gat_in_fwd_f32, 8 heads x 32 from 100 inputs)",
                         "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json): 126 M "
-                                        "gathered 1-KB X rows; at the measured HBM copy rate"}}
-    # backward stats kernel: rowptr + col + dY, Y, Ym read once + dX written + aL, aR, q,
-    # sum m*alpha read + d_aL written per row and head (dY[c] gathered per edge: traffic)
-    alg_b = 4 * (N + 1) + 4 * E + 4 * 4 * N * F + 5 * 4 * N * H
-    out["bwd_roofline"] = {"bound": "hbm", "achieved": alg_b / t_bwd / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                           "frac": alg_b / t_bwd / HBM_PEAK, "kernel_ms": t_bwd * 1e3, "alg_bytes_per_launch": alg_b,
-                           "traffic": load_traffic("k_gat_bwd_fused<64, 4, 8, 8, 1, false, true>"),
-                           "kernel": "gala::k_gat_bwd_fused<64,4,8,8,1,false,true> (gala_gat_bwd_stats_f32, 8 heads, "
-                                     "F=256)"}
+                                        "gathered 512-B extended input rows"}}
+    out["bwd_roofline"] = {"bound": "hbm", "achieved": alg_b / t_kb / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                           "frac": alg_b / t_kb / HBM_PEAK, "kernel_ms": t_kb * 1e3, "alg_bytes_per_launch": alg_b,
+                           "traffic": load_traffic("k_gat_in_bwd<8>"),
+                           "kernel": "gala::k_gat_in_bwd<8> (gala_gat_in_bwd_f32, 8 heads x 32 from 100 inputs)"}
     with_traffic_rate(out["roofline"])
     with_traffic_rate(out["bwd_roofline"])
     t_ceil = med(rounds["ceil"])
     if t_ceil:
         out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
-        out["roofline"]["frac_of_gather_ceiling"] = med([c / f for c, f in zip(rounds["ceil"], rounds["fwd"])])
+        out["roofline"]["frac_of_gather_ceiling"] = med([c / f for c, f in zip(rounds["ceil"], rounds["k_fwd"])])
         out["bwd_roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
-        out["bwd_roofline"]["frac_of_gather_ceiling"] = med([c / b for c, b in zip(rounds["ceil"], rounds["bwd"])])
-        out["interleaved_ms"] = {k: [round(v * 1e3, 3) for v in vs] for k, vs in rounds.items()}
-    del st
+        out["bwd_roofline"]["frac_of_gather_ceiling"] = med([c / b for c, b in zip(rounds["ceil"], rounds["k_bwd"])])
+    out["interleaved_ms"] = {k: [round(v * 1e3, 3) for v in vs] for k, vs in rounds.items()}
+    del st, f0, xext, Y0, Ym0, sma0
+    torch.cuda.empty_cache()
+    # the previous formulation on the same layer: the Linear's output (1-KB rows) gathered by
+    # the row-statistics pair, timed from that output (kernels only)
+    X = torch.rand((N, F), device=dev, generator=gen) * 2 - 1
+    aL = torch.rand((N, H), device=dev, generator=gen) - 0.5
+    st2 = {}
+
+    def fwd2():
+        st2["f"] = ops.gat_fwd_stats(dg, aL, X, wR=wR, bR=bR, heads=H, want_aR=True)
+
+    def bwd2():
+        Yv, q, Ym, sma, aRo = st2["f"]
+        st2["b"] = ops.gat_bwd_stats(dg, aL, aRo, dY, q, Yv, Ym, sma, heads=H)
+    fwd2()
+    t2f, t2b = timer(fwd2, 5), timer(bwd2, 5)
+    out["gathering_linear_output"] = {
+        "fwd_ms": t2f * 1e3, "bwd_ms": t2b * 1e3,
+        "kernels": "gala::k_gat_fwd<64,4,8,2,1,true,8> / k_gat_bwd_fused<64,4,8,8,1,false,true> "
+                   "(gala_gat_{fwd,bwd}_stats_f32 over the 1-KB Linear output rows; Linear and weight "
+                   "gradients not included)"}
+    del st2
     torch.cuda.empty_cache()
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = gat_cpu_baseline(hg, X.cpu().numpy(), dY.cpu().numpy(), aL.cpu().numpy(),
                                                    wR.cpu().numpy(), bR.cpu().numpy(), H)
+            out["cpu_baseline"]["note"] = ("the reference's REF GAT pass sequence over the Linear's output "
+                                           "(the Linear and the weight gradients are not in the CPU sample)")
         except Exception as e:  # the baseline is reported, never the target
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
     del X, dY

@@ -278,8 +278,9 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
 // variant v < 8, m * p of head v - 8 for v >= 8), parks its tiles in LDS, then wave h
 // projects the eight rows' head-h aggregates (M = 8 rows x {p, m p}, K = the 112 tile rows,
 // N = D) with W_ext,h fragments held in registers.
-template <int WPE>
-__global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_fwd(InFwdParams p) {
+// one workgroup of 8 waves per CU (2 per SIMD: ~210 VGPRs, no spills; 4 per SIMD spilled
+// and ran 1.5x slower, tools/gat_input_bench.py)
+__global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
     __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // [slot][variant][tile][16 floats]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
@@ -393,8 +394,8 @@ __device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v)
 // Xin_ext[r] (alpha rebuilt from aL[r], q[r] in r's extended row and aR[c]) and c's d_aL from
 // the forward's row statistics; then wave h adds dY_h[c]^T T_h[c] of the eight columns into
 // its register accumulators M_h[D x 112] (K = the columns).  Partials per workgroup.
-template <int DW, int WPE>
-__global__ __launch_bounds__(kInBlock, WPE) void k_gat_in_bwd(InBwdParams p) {
+template <int DW>
+__global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
     __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
@@ -519,17 +520,9 @@ __global__ __launch_bounds__(kBlock) void k_gat_in_reduce(const float *part, int
     M[((int64_t)h * D + j) * (fin + 1) + (f == -2 ? fin : f)] = s;
 }
 
-// the aggregation kernels' occupancy target: 2 waves per SIMD (one workgroup of 8 waves per
-// CU, no spills) or 4 (two workgroups, registers capped at 128: spills).  GALA_GIN_WPE=4|2
-// (measured in tools/gat_input_bench.py)
-int waves_per_simd() {
-    const char *e = std::getenv("GALA_GIN_WPE");
-    return (e && e[0] == '4') ? 4 : 2;
-}
-
 int grid_for(int64_t n_rows) {
     const int64_t nblk = (n_rows + kInWaves - 1) / kInWaves;
-    return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), (int64_t)kInGrid * (waves_per_simd() == 4 ? 1 : 1));
+    return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
 }
 
 int check_in_graph(const gala_csr_t *A, int32_t fin, int32_t heads, int32_t D) {
@@ -572,10 +565,7 @@ extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, in
     InFwdParams p{A->rowptr, A->col, order ? order : (A->split ? A->split->row_order : nullptr), A->n_rows, Xext, W,
                   b, ldw,
                   fin, heads, D, slope, Y, Ym, q, sma, ldy};
-    if (waves_per_simd() == 4)
-        hipLaunchKernelGGL(k_gat_in_fwd<4>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
-    else
-        hipLaunchKernelGGL(k_gat_in_fwd<2>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(k_gat_in_fwd, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
     return launch_status();
 }
 
@@ -608,15 +598,11 @@ extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, i
                   dY, Y, Ym,
                   sma, ldy, fin, heads, D, slope, daL, ws};
     if (hipMemsetAsync(M, 0, outn * sizeof(float), hs) != hipSuccess) return GALA_ERR_HIP;
-    const bool w4 = waves_per_simd() == 4;
     switch (D / 4) {
-    case 1: hipLaunchKernelGGL((k_gat_in_bwd<1, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 2: hipLaunchKernelGGL((k_gat_in_bwd<2, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 4: hipLaunchKernelGGL((k_gat_in_bwd<4, 2>), dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    default:
-        if (w4) hipLaunchKernelGGL((k_gat_in_bwd<8, 4>), dim3(grid), dim3(kInBlock), 0, hs, p);
-        else hipLaunchKernelGGL((k_gat_in_bwd<8, 2>), dim3(grid), dim3(kInBlock), 0, hs, p);
-        break;
+    case 1: hipLaunchKernelGGL(k_gat_in_bwd<1>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 2: hipLaunchKernelGGL(k_gat_in_bwd<2>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 4: hipLaunchKernelGGL(k_gat_in_bwd<4>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    default: hipLaunchKernelGGL(k_gat_in_bwd<8>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
     }
     st = launch_status();
     if (st) return st;

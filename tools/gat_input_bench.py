@@ -49,15 +49,10 @@ def main():
         return E.gat_aggregate_ffn_apply(E.head_attn_apply(v1, wL, bL), v1, wR, bR, 0, 0.2, 0)
 
     def inspace():
-        os.environ["GALA_GIN_WPE"] = "2"
-        return E.gat_input_layer_apply(x, W, b, wL, bL, wR, bR, 0, 0.2, 0)
-
-    def inspace4():   # two workgroups per CU (registers capped at 128)
-        os.environ["GALA_GIN_WPE"] = "4"
         return E.gat_input_layer_apply(x, W, b, wL, bL, wR, bR, 0, 0.2, 0)
 
     assert E.gat_input_layer_eligible(x, W, 0, H, 0)
-    variants = {"input_space": inspace, "input_space_wpe4": inspace4, "chain": chain}
+    variants = {"input_space": inspace, "chain": chain}
     res = {k: {"fwd": [], "bwd": []} for k in variants}
     outs = {}
     for rep in range(a.reps + 1):
@@ -69,7 +64,7 @@ def main():
             e[0].record()
             Y = fn()
             e[1].record()
-            Y.backward(dY)   # (the WPE switch is read per launch: the backward runs as set above)
+            Y.backward(dY)
             e[2].record()
             torch.cuda.synchronize()
             if rep > 0:
