@@ -206,16 +206,8 @@ struct RowCursor {
     int64_t e0 = 0;
     int32_t deg = 0, win = 0;
     float side = 0.0f;     // xext[row * 128 + side_slot]: aL (forward) / aR (backward) of the lane's head
-    f4v xa[4], xb[4];      // the row's batch 0 (requested)
-    f4v ya[4], yb[4];      // batch 1 (requested when the row has more than 16 edges)
+    f4v xa[4], xb[4];      // the row's first batch (requested)
 };
-
-// the batches a cursor keeps in flight: the current one and the next (prefetch distance 2
-// with the one requested inside the walk)
-__device__ __forceinline__ void cursor_first_batches(RowCursor &c, const float *xext, int kq, int n16) {
-    if (c.deg > 0) load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
-    if (c.deg > 16) load_batch(xext, c.win, 16, kq, n16, c.ya, c.yb);
-}
 
 __device__ __forceinline__ void cursor_start(RowCursor &c, const int32_t *rowptr, const int32_t *col,
                                              const float *xext, int64_t row, int side_slot, bool side_ok, int lane) {
@@ -227,8 +219,10 @@ __device__ __forceinline__ void cursor_start(RowCursor &c, const int32_t *rowptr
     c.e0 = uniform(rowptr[row]);
     c.deg = uniform(rowptr[row + 1]) - (int32_t)c.e0;
     c.side = side_ok ? xext[row * kInLd + side_slot] : 0.0f;
-    if (c.deg > 0) c.win = col[c.e0 + (lane < c.deg ? lane : c.deg - 1)];
-    cursor_first_batches(c, xext, kq, n16);
+    if (c.deg > 0) {
+        c.win = col[c.e0 + (lane < c.deg ? lane : c.deg - 1)];
+        load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
+    }
 }
 
 template <typename BFn>
@@ -255,22 +249,20 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
         nside = side_ok ? xext[next * kInLd + side_slot] : 0.0f;
     };
     for (int32_t j0 = 0; j0 < c.deg; j0 += 16) {
-        const int32_t j2 = j0 + 32;
-        f4v za[4], zb[4];
-        const bool more2 = j2 < c.deg;
-        if (more2) {
-            if ((j2 & 63) == 0) c.win = col[c.e0 + ((j2 + lane < c.deg) ? j2 + lane : c.deg - 1)];
-            load_batch(xext, c.win, j2, kq, n16, za, zb);
+        const int32_t j1 = j0 + 16;
+        f4v ya[4], yb[4];
+        const bool more = j1 < c.deg;
+        if (more) {
+            if ((j1 & 63) == 0) c.win = col[c.e0 + ((j1 + lane < c.deg) ? j1 + lane : c.deg - 1)];
+            load_batch(xext, c.win, j1, kq, n16, ya, yb);
         }
         if (j0 == 0) issue_next();
         mfma_batch(c.xa, c.xb, j0, c.deg, kq, n16, bfn, acc);
+        if (more) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            c.xa[s] = c.ya[s];
-            c.xb[s] = c.yb[s];
-            if (more2) {
-                c.ya[s] = za[s];
-                c.yb[s] = zb[s];
+            for (int s = 0; s < 4; ++s) {
+                c.xa[s] = ya[s];
+                c.xb[s] = yb[s];
             }
         }
     }
@@ -279,7 +271,7 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
     c.deg = next >= 0 ? uniform(nend - (int32_t)ne0) : 0;
     c.win = nwin;
     c.side = nside;
-    cursor_first_batches(c, xext, kq, n16);
+    if (c.deg > 0) load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
 }
 
 // Forward.  Workgroup phase: wave w aggregates row order[8 blk + w] (B = p of head v for
