@@ -913,11 +913,11 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     st = {}
 
     def fwd():
-        st["f"] = ops.gat_input_layer(dg, Xin, W, b, wL, bL, wR, bR, H, order=order)
+        st["f"] = ops.gat_input_layer(dg, Xin, W, b, wL, bL, wR, bR, H, order=order, relu=True)
 
     def bwd():
         f = st["f"]
-        daL, M = ops.gat_in_bwd(dg, f["xext"], dY, f["Y"], f["Ym"], f["sma"], H, FIN, order=order)
+        daL, M = ops.gat_in_bwd(dg, f["xext"], dY, f["Y"], f["Ym"], f["sma"], H, FIN, order=order, relu=True)
         Gw, Gb = ops.dense_grad(Xin, daL)
         sLR = (wL + wR).reshape(H, D)
         dW = M[:, :, :FIN] + sLR.unsqueeze(2) * Gw.unsqueeze(1)
@@ -934,10 +934,10 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     xext, Y0, Ym0, sma0 = f0["xext"], f0["Y"], f0["Ym"], f0["sma"]
 
     def k_fwd():   # the aggregation kernel alone (its extended rows prepared)
-        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order)
+        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order, relu=True)
 
     def k_bwd():
-        ops.gat_in_bwd(dg, xext, dY, Y0, Ym0, sma0, H, FIN, order=order)
+        ops.gat_in_bwd(dg, xext, dY, Y0, Ym0, sma0, H, FIN, order=order, relu=True)
     # the layer, its two kernels and the same-process gather probe of the 512-B extended rows,
     # interleaved over three rounds (medians: all move by up to 10 % with the GPU's load state,
     # DESIGN §4.4)
@@ -959,8 +959,8 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     alg_b = 4 * (N + 1) + 4 * E + 512 * N + 3 * 4 * N * F + 2 * 4 * N * H
     out = {"value": 2 * E / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
            "layer": (f"GAT layer 1 of config 3: {FIN} input features -> {H} heads x {D} (F={F}), Linear + both "
-                     f"attention Linears + REF softmax aggregation, input space; forward + backward with every "
-                     f"parameter gradient"),
+                     f"attention Linears + REF softmax aggregation + the program's ReLU, input space; forward + "
+                     f"backward with every parameter gradient"),
            "fwd_ms": t_fwd * 1e3, "bwd_ms": t_bwd * 1e3,
            "roofline": {"bound": "hbm", "achieved": alg / t_kf / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kf / HBM_PEAK, "kernel_ms": t_kf * 1e3, "alg_bytes_per_launch": alg,

@@ -1259,13 +1259,14 @@ extern "C" int gala_cpu_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin
 extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order_in, int32_t fin, int32_t heads,
                                        int32_t D, float slope,
                                        float *Xext, const float *W, int64_t ldw, const float *b, float *Y,
-                                       float *Ym, int64_t ldy, float *q, float *sma, void *stream) {
+                                       float *Ym, int64_t ldy, float *q, float *sma, int32_t flags, void *stream) {
     (void)stream;
     int st = check_in_graph(A, fin, heads, D);
     if (st) return st;
-    if (ldw < fin || ldy < (int64_t)heads * D) return GALA_ERR_INVALID_ARG;
+    if (ldw < fin || ldy < (int64_t)heads * D || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!Xext || !W || !Y || !Ym || !q || !sma) return GALA_ERR_INVALID_ARG;
+    const bool relu = flags & GALA_GAT_IN_RELU;
     const int H = heads;
     const int32_t *order = order_in ? order_in : (A->split ? A->split->row_order : nullptr);
     std::vector<float> qv((size_t)A->n_rows * H);
@@ -1313,7 +1314,8 @@ extern "C" int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order
                                 y0 = fmaf(Z[((size_t)h * kInTiles + t) * 16 + m], w, y0);
                                 y1 = fmaf(Z[((size_t)(h + 8) * kInTiles + t) * 16 + m], w, y1);
                             }
-                    Y[r * ldy + o] = qq * y0;
+                    const float yv = qq * y0;
+                    Y[r * ldy + o] = (!relu || yv > 0.0f || yv != yv) ? yv : 0.0f;
                     Ym[r * ldy + o] = qq * y1;
                 }
                 q[r * H + h] = qq;
@@ -1339,13 +1341,14 @@ extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *orde
                                        int32_t D, float slope,
                                        const float *Xext, const float *dY, const float *Y, const float *Ym,
                                        int64_t ldy, const float *sma, float *daL, float *M, void *ws,
-                                       int64_t ws_bytes, void *stream) {
+                                       int64_t ws_bytes, int32_t flags, void *stream) {
     (void)stream;
     int st = check_in_graph(AT, fin, heads, D);
     if (st) return st;
-    if (ldy < (int64_t)heads * D || (ldy & 3)) return GALA_ERR_INVALID_ARG;
+    if (ldy < (int64_t)heads * D || (ldy & 3) || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (!M) return GALA_ERR_INVALID_ARG;
     const int H = heads;
+    const bool relu = flags & GALA_GAT_IN_RELU;
     const int64_t outn = (int64_t)H * D * (fin + 1);
     std::fill(M, M + outn, 0.0f);
     if (AT->n_rows == 0) return GALA_OK;
@@ -1385,7 +1388,10 @@ extern "C" int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *orde
                         }
                     }
                     for (int h = 0; h < H; ++h) {
-                        const float *dy = dY + c * ldy + (int64_t)h * D;
+                        float dym[32];   // dY, masked by relu(Y) > 0 with the fused ReLU
+                        const float *yh = Y + c * ldy + (int64_t)h * D;
+                        for (int j = 0; j < D; ++j) dym[j] = (!relu || yh[j] > 0.0f) ? dY[c * ldy + (int64_t)h * D + j] : 0.0f;
+                        const float *dy = dym;
                         const float sy = butterfly_dot(dy, Y + c * ldy + (int64_t)h * D, D);
                         const float sm = butterfly_dot(dy, Ym + c * ldy + (int64_t)h * D, D);
                         const float accv = sy + 1e-12f;

@@ -155,6 +155,7 @@ struct InFwdParams {
     float slope;
     float *Y, *Ym, *q, *sma;
     int64_t ldy;
+    int32_t relu;   // GALA_GAT_IN_RELU: Y = relu(the aggregation) (the layer's NON_LNR_OP_RELU)
 };
 
 // the gathered extended row of edge (4s + kq) of a 16-edge batch: column from the row's
@@ -361,7 +362,9 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
                     const int j = 16 * nt + n16;
                     if (j >= p.D) continue;
                     const int64_t o = row * p.ldy + (int64_t)h * p.D + j;
-                    p.Y[o] = __fmul_rn(qv, y[nt][2 * hs]);
+                    const float yv = __fmul_rn(qv, y[nt][2 * hs]);
+                    // torch::relu keeps NaN (clamp_min); its backward zeroes it (out > 0 fails)
+                    p.Y[o] = (!p.relu || yv > 0.0f || yv != yv) ? yv : 0.0f;
                     p.Ym[o] = __fmul_rn(qv, y[nt][2 * hs + 1]);
                 }
                 if (n16 == 0) {
@@ -383,7 +386,8 @@ struct InBwdParams {
     int32_t fin, H, D;
     float slope;
     float *daL;
-    float *part;    // [gridDim][H][2][kInTiles][64][4]
+    float *part;
+    int32_t relu;   // Y holds relu(the aggregation): dY is masked by Y > 0 (torch's threshold_backward)    // [gridDim][H][2][kInTiles][64][4]
 };
 
 template <int DW>   // lanes per head in the row-local d_aL dots: D / 4
@@ -431,6 +435,10 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
             dy = *reinterpret_cast<const f4v *>(p.dY + c * p.ldy + f);
             yy = *reinterpret_cast<const f4v *>(p.Y + c * p.ldy + f);
             ym = *reinterpret_cast<const f4v *>(p.Ym + c * p.ldy + f);
+            if (p.relu) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dy[i] = yy[i] > 0.0f ? dy[i] : 0.0f;
+            }
         }
         {
             const float ar = cur.side;
@@ -481,7 +489,9 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
                     const int j = 16 * mt + n16;
-                    a[mt] = (ok && j < p.D) ? p.dY[cs * p.ldy + (int64_t)h * p.D + j] : 0.0f;
+                    const int64_t o = cs * p.ldy + (int64_t)h * p.D + j;
+                    a[mt] = (ok && j < p.D) ? p.dY[o] : 0.0f;
+                    if (p.relu && ok && j < p.D && !(p.Y[o] > 0.0f)) a[mt] = 0.0f;
                 }
 #pragma unroll
                 for (int t = 0; t < kInTiles; ++t) {
@@ -556,15 +566,15 @@ extern "C" int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, in
 extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
                                    float slope,
                                    float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
-                                   int64_t ldy, float *q, float *sma, void *stream) {
+                                   int64_t ldy, float *q, float *sma, int32_t flags, void *stream) {
     int st = check_in_graph(A, fin, heads, D);
     if (st) return st;
-    if (ldw < fin || ldy < (int64_t)heads * D) return GALA_ERR_INVALID_ARG;
+    if (ldw < fin || ldy < (int64_t)heads * D || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
     if (!Xext || !W || !Y || !Ym || !q || !sma || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
     InFwdParams p{A->rowptr, A->col, order ? order : (A->split ? A->split->row_order : nullptr), A->n_rows, Xext, W,
                   b, ldw,
-                  fin, heads, D, slope, Y, Ym, q, sma, ldy};
+                  fin, heads, D, slope, Y, Ym, q, sma, ldy, (flags & GALA_GAT_IN_RELU) ? 1 : 0};
     hipLaunchKernelGGL(k_gat_in_fwd, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
     return launch_status();
 }
@@ -578,11 +588,11 @@ extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, i
                                    float slope,
                                    const float *Xext, const float *dY, const float *Y, const float *Ym,
                                    int64_t ldy, const float *sma, float *daL, float *M, void *ws_,
-                                   int64_t ws_bytes, void *stream) {
+                                   int64_t ws_bytes, int32_t flags, void *stream) {
     float *ws = (float *)ws_;
     int st = check_in_graph(AT, fin, heads, D);
     if (st) return st;
-    if (ldy < (int64_t)heads * D || (ldy & 3)) return GALA_ERR_INVALID_ARG;
+    if (ldy < (int64_t)heads * D || (ldy & 3) || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (!M) return GALA_ERR_INVALID_ARG;
     hipStream_t hs = (hipStream_t)stream;
     const int64_t outn = (int64_t)heads * D * (fin + 1);
@@ -596,7 +606,7 @@ extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, i
     const int grid = grid_for(AT->n_rows);
     InBwdParams p{AT->rowptr, AT->col, order ? order : (AT->split ? AT->split->row_order : nullptr), AT->n_rows, Xext,
                   dY, Y, Ym,
-                  sma, ldy, fin, heads, D, slope, daL, ws};
+                  sma, ldy, fin, heads, D, slope, daL, ws, (flags & GALA_GAT_IN_RELU) ? 1 : 0};
     if (hipMemsetAsync(M, 0, outn * sizeof(float), hs) != hipSuccess) return GALA_ERR_HIP;
     switch (D / 4) {
     case 1: hipLaunchKernelGGL(k_gat_in_bwd<1>, dim3(grid), dim3(kInBlock), 0, hs, p); break;

@@ -111,11 +111,11 @@ PYBIND11_MODULE(_gala_torch, m) {
           py::arg("mode") = 0);
     m.def("gat_input_layer_apply",
           [opt](torch::Tensor x, torch::Tensor w, std::optional<torch::Tensor> b, torch::Tensor wl, torch::Tensor bl,
-                torch::Tensor wr, torch::Tensor br, int64_t li, double slope, int64_t mode) {
-              return gat_input_layer_apply(x, w, opt(b), wl, bl, wr, br, li, slope, mode);
+                torch::Tensor wr, torch::Tensor br, int64_t li, double slope, int64_t mode, bool relu) {
+              return gat_input_layer_apply(x, w, opt(b), wl, bl, wr, br, li, slope, mode, relu);
           },
           py::arg("X"), py::arg("weight"), py::arg("bias"), py::arg("attn_l_weight"), py::arg("attn_l_bias"),
           py::arg("attn_r_weight"), py::arg("attn_r_bias"), py::arg("li"), py::arg("slope") = 0.2,
-          py::arg("mode") = 0);
+          py::arg("mode") = 0, py::arg("relu") = false);
     m.def("gat_input_layer_eligible", &gat_input_layer_eligible);
 }

@@ -1491,7 +1491,7 @@ const PatternT &transposed_pattern(int64_t idx);
 struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor W, torch::Tensor b,
                                  torch::Tensor wL, torch::Tensor bL, torch::Tensor wR, torch::Tensor bR,
-                                 int64_t li, double slope, int64_t heads) {
+                                 int64_t li, double slope, int64_t heads, bool relu) {
         Slot s = slot(2 * li);
         auto x = X.contiguous(), w = W.contiguous();
         const bool has_b = b.defined() && b.numel() > 0;
@@ -1520,12 +1520,14 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         const PatternT &pt = transposed_pattern(2 * li);
         check(B.gat_in_fwd(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
                            w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr, Y.data_ptr<float>(),
-                           Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(), stream_of(x)),
+                           Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(),
+                           relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
               "gala_gat_in_fwd_f32");
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
         ctx->saved_data["heads"] = heads;
         ctx->saved_data["has_b"] = has_b;
+        ctx->saved_data["relu"] = relu;
         ctx->save_for_backward({x, w, has_b ? bc : torch::empty({0}, fopts(x)), wL, wR, xext, Y, Ym, sma});
         return Y;
     }
@@ -1534,7 +1536,7 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         auto x = sv[0], w = sv[1], b = sv[2], wL = sv[3], wR = sv[4], xext = sv[5], Y = sv[6], Ym = sv[7], sma = sv[8];
         const int64_t li = ctx->saved_data["li"].toInt(), H = ctx->saved_data["heads"].toInt();
         const double slope = ctx->saved_data["slope"].toDouble();
-        const bool has_b = ctx->saved_data["has_b"].toBool();
+        const bool has_b = ctx->saved_data["has_b"].toBool(), relu = ctx->saved_data["relu"].toBool();
         const int64_t N = x.size(0), fin = x.size(1), F = w.size(0), D = F / H;
         auto dY = grad_outputs[0].contiguous();
         check_dev(dY, torch::kFloat, "grad");
@@ -1551,7 +1553,8 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         auto ws = torch::empty({wsb / 4}, fopts(x));
         check(B.gat_in_bwd(&cv.c, pt.order_t.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
                            dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F, sma.data_ptr<float>(),
-                           daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb, stream_of(x)),
+                           daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb,
+                           relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
               "gala_gat_in_bwd_f32");
         // G = d_aL^T X (and its column sums): the attention Linears' terms
         auto Gw = torch::empty({H, fin}, fopts(x)), Gb = torch::empty({H}, fopts(x));
@@ -1567,7 +1570,7 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         auto bb = has_b ? b.view({H, D}) : torch::zeros({H, D}, fopts(x));
         auto dw = ((w.view({H, D, fin}) * Gw.unsqueeze(1)).sum(2) + bb * Gb.unsqueeze(1));
         return {torch::Tensor(), dW, db, dw.reshape(wL.sizes()), Gb.reshape({H}), dw.reshape(wR.sizes()),
-                Gb.reshape({H}), torch::Tensor(), torch::Tensor(), torch::Tensor()};
+                Gb.reshape({H}), torch::Tensor(), torch::Tensor(), torch::Tensor(), torch::Tensor()};
     }
 };
 
@@ -1696,14 +1699,15 @@ bool gat_input_layer_eligible(const torch::Tensor &X, const torch::Tensor &W, in
 
 torch::Tensor gat_input_layer_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias, torch::Tensor attn_l_weight,
                                     torch::Tensor attn_l_bias, torch::Tensor attn_r_weight, torch::Tensor attn_r_bias,
-                                    int64_t li, double slope, int64_t mode) {
+                                    int64_t li, double slope, int64_t mode, bool relu) {
     const int64_t heads = attn_l_bias.numel();
     if (gat_input_layer_eligible(X, weight, li, heads, mode))
         return GatInputLayer::apply(X, weight, bias, attn_l_weight, attn_l_bias, attn_r_weight, attn_r_bias, li,
-                                    slope, heads);
+                                    slope, heads, relu);
     auto v1 = ffn_apply(X, weight, bias);
     auto aL = head_attn_apply(v1, attn_l_weight, attn_l_bias);
-    return gat_aggregate_ffn_apply(aL, v1, attn_r_weight, attn_r_bias, li, slope, mode);
+    auto y = gat_aggregate_ffn_apply(aL, v1, attn_r_weight, attn_r_bias, li, slope, mode);
+    return relu ? torch::relu(y) : y;
 }
 
 }  // namespace gala

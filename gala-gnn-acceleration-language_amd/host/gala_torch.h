@@ -191,10 +191,11 @@ torch::Tensor head_attn_apply(torch::Tensor X, torch::Tensor weight, torch::Tens
 // with the edges gathering X's rows (fin floats) instead of v1's (H*D).  Used when X needs
 // no gradient (the dataset's features), fin < H*D <= 8*32, REF softmax on the undirected
 // graph without hub rows; otherwise it runs the three ops themselves (GALA_GAT_INPUT=0: always).
+// relu: the program's torch::relu on the layer's output fused (forward store, backward mask).
 bool gat_input_layer_eligible(const torch::Tensor &X, const torch::Tensor &W, int64_t li, int64_t heads, int64_t mode);
 torch::Tensor gat_input_layer_apply(torch::Tensor X, torch::Tensor weight, torch::Tensor bias,
                                     torch::Tensor attn_l_weight, torch::Tensor attn_l_bias,
                                     torch::Tensor attn_r_weight, torch::Tensor attn_r_bias, int64_t li,
-                                    double slope, int64_t mode);
+                                    double slope, int64_t mode, bool relu = false);
 
 }  // namespace gala

@@ -143,12 +143,12 @@ int gala_cpu_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t l
                              const float *u, const float *c, float *Xext, void *stream);
 int gala_cpu_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                             float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
-                            int64_t ldy, float *q, float *sma, void *stream);
+                            int64_t ldy, float *q, float *sma, int32_t flags, void *stream);
 int64_t gala_cpu_gat_in_bwd_workspace(int32_t heads);
 int gala_cpu_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                             const float *Xext, const float *dY, const float *Y, const float *Ym,
                             int64_t ldy, const float *sma, float *daL, float *M, void *ws,
-                            int64_t ws_bytes, void *stream);
+                            int64_t ws_bytes, int32_t flags, void *stream);
 
 #ifdef __cplusplus
 }

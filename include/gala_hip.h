@@ -574,6 +574,10 @@ int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float
  *     attention Linears' terms follow from G = d_aL^T Xin_ext (gala_dense_grad_f32):
  *     dW_h += (wL_h + wR_h) G_h, d wL_h = d wR_h = W_ext,h G_h, d bL = d bR = sum d_aL.
  *     ws: gala_gat_in_bwd_workspace(heads) bytes.
+ *   flags GALA_GAT_IN_RELU (both calls): the program's NON_LNR_OP_RELU after the layer fused --
+ *     the forward stores relu(Y) (NaN kept, as torch::relu) and the backward takes the
+ *     gradient of relu(Y), masked by relu(Y) > 0 (torch's threshold_backward); the d_aL dots
+ *     <dY, Y> are then the same sums over relu(Y).
  * Limits (else GALA_ERR_UNSUPPORTED, callers keep the statistics pair): fin <= 100, heads
  * <= 8, D in {4, 8, 16, 32}, one segment, a square pattern, no hub rows in A->split (a hub
  * row would be one wave's serial walk).  Sums are regrouped (the matrix cores sum four edges
@@ -581,14 +585,15 @@ int gala_head_attn_bwd_f32(int64_t n_rows, int32_t F, int32_t heads, const float
  */
 int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, int64_t ldxin, int32_t heads,
                          const float *u, const float *c, float *Xext, void *stream);
+#define GALA_GAT_IN_RELU 1   /* the layer's ReLU fused: Y = relu(.) forward, dY masked by Y > 0 backward */
 int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                         float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
-                        int64_t ldy, float *q, float *sma, void *stream);
+                        int64_t ldy, float *q, float *sma, int32_t flags, void *stream);
 int64_t gala_gat_in_bwd_workspace(int32_t heads);
 int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
                         const float *Xext, const float *dY, const float *Y, const float *Ym,
                         int64_t ldy, const float *sma, float *daL, float *M, void *ws,
-                        int64_t ws_bytes, void *stream);
+                        int64_t ws_bytes, int32_t flags, void *stream);
 
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,

@@ -42,7 +42,7 @@ def compose(W, b, wL, bL, wR, bR, heads):
     return u.numpy(), c.numpy()
 
 
-def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, order=None, order_t=None):
+def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, order=None, order_t=None, relu=False):
     """The host twins composed as the mirror's GatInputLayer composes the GPU ops (the
     backward over the transposed pattern: g itself when it is symmetric)."""
     n, fin = X.shape
@@ -55,7 +55,7 @@ def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, order=None, orde
     Y, Ym = np.empty((n, F), np.float32), np.empty((n, F), np.float32)
     q, sma = np.empty((n, heads), np.float32), np.empty((n, heads), np.float32)
     _abi.call_cpu("gala_gat_in_fwd_f32", A.ref, P(order), fin, heads, D, slope, P(xext), P(W), fin, P(b), P(Y), P(Ym), F,
-                  P(q), P(sma), None)
+                  P(q), P(sma), _abi.GALA_GAT_IN_RELU if relu else 0, None)
     daL = np.empty((n, heads), np.float32)
     M = np.empty((heads, D, fin + 1), np.float32)
     wsb = _abi.cpu_lib().gala_cpu_gat_in_bwd_workspace(heads)
@@ -63,7 +63,7 @@ def cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, slope=0.2, order=None, orde
     gT, _ = layout.transpose(g)
     AT = HostCsr(gT)
     _abi.call_cpu("gala_gat_in_bwd_f32", AT.ref, P(order_t), fin, heads, D, slope, P(xext), P(dY), P(Y), P(Ym), F, P(sma),
-                  P(daL), P(M), P(ws), wsb, None)
+                  P(daL), P(M), P(ws), wsb, _abi.GALA_GAT_IN_RELU if relu else 0, None)
     Gw, Gb = np.empty((heads, fin), np.float32), np.empty(heads, np.float32)
     gwb = _abi.cpu_lib().gala_cpu_dense_grad_workspace(n, fin, heads)
     gws = np.empty(max(gwb // 4, 1), np.float32)
@@ -80,7 +80,7 @@ def own_logits(xext, heads):
     return (xext[:, [99 + 4 * h for h in range(heads)]], xext[:, [67 + 4 * h for h in range(heads)]])
 
 
-def ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, heads):
+def ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, heads, relu=False):
     """The oracle's layer on the kernels' own attention logits, after checking those against
     the float64 attention Linears of the float64 Linear output (1e-5): a logit at the
     LeakyReLU kink takes the other slope under a one-ulp change."""
@@ -91,7 +91,12 @@ def ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, heads):
     v1 = v1.reshape(-1, heads, D)
     np.testing.assert_allclose(aL, (v1 * wL.reshape(heads, D)).sum(-1) + bL, atol=1e-5, rtol=1e-5)
     np.testing.assert_allclose(aR, (v1 * wR.reshape(heads, D)).sum(-1) + bR, atol=1e-5, rtol=1e-5)
-    return orc.gat_input_layer_ref(g.rowptr, g.col, X, W, b, wL, bL, wR, bR, dY, heads, aL=aL, aR=aR)
+    if relu:   # torch's threshold_backward on the layer's output (the kernels' own relu(Y) > 0)
+        dY = np.where(got["Y"] > 0, dY, np.float32(0)).astype(np.float32)
+    ref = orc.gat_input_layer_ref(g.rowptr, g.col, X, W, b, wL, bL, wR, bR, dY, heads, aL=aL, aR=aR)
+    if relu:
+        ref["Y"] = np.maximum(ref["Y"], 0)
+    return ref
 
 
 def grad_close(got, want, name):
@@ -109,6 +114,13 @@ def test_input_space_layer_matches_the_reference_chain(fin, heads, D):
     ref = ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, heads)
     np.testing.assert_allclose(got["Y"], ref["Y"], **TOL)
     np.testing.assert_allclose(got["q"], ref["q"], rtol=1e-4)
+    # with the program's ReLU fused (forward store, backward mask)
+    gr = cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, relu=True)
+    rr = ref_on_own_logits(g, gr, X, W, b, wL, bL, wR, bR, dY, heads, relu=True)
+    np.testing.assert_allclose(gr["Y"], rr["Y"], **TOL)
+    np.testing.assert_allclose(gr["daL"], rr["daL"], **TOL)
+    for k in ("dW", "db", "dwL", "dbL"):
+        grad_close(gr[k], rr[k], k + "_relu")
     np.testing.assert_allclose(got["daL"], ref["daL"], **TOL)
     for k in ("dW", "db", "dwL", "dbL"):
         grad_close(got[k], ref[k], k)
@@ -143,14 +155,14 @@ def test_input_space_refusals():
     L = _abi.cpu_lib()
     # fin > 100, D not in {4, 8, 16, 32}, more than 8 heads: unsupported (callers keep the chain)
     assert L.gala_cpu_gat_in_fwd_f32(A.ref, None, 101, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
-                                     None) == _abi.GALA_ERR_UNSUPPORTED
+                                     0, None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_fwd_f32(A.ref, None, 100, 8, 24, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
-                                     None) == _abi.GALA_ERR_UNSUPPORTED
+                                     0, None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_prep_f32(100, 101, P(X), 128, 8, P(W), P(W), P(xext), None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_prep_f32(100, 100, P(X), 99, 8, P(W), P(W), P(xext), None) == _abi.GALA_ERR_INVALID_ARG
     t = HostCsr(layout.col_tile(g, 40))
     assert L.gala_cpu_gat_in_fwd_f32(t.ref, None, 100, 8, 32, 0.2, P(xext), P(W), 128, None, P(Y), P(Y), 256, P(q), P(q),
-                                     None) == _abi.GALA_ERR_UNSUPPORTED
+                                     0, None) == _abi.GALA_ERR_UNSUPPORTED
     assert L.gala_cpu_gat_in_bwd_workspace(9) < 0
 
 
@@ -171,17 +183,22 @@ def test_mirror_op_on_host_tensors_equals_the_three_op_chain():
         params = [torch.from_numpy(a).requires_grad_() for a in (W, b, wL.reshape(1, -1), bL, wR.reshape(1, -1), bR)]
         x = torch.from_numpy(X)
         assert E.gat_input_layer_eligible(x, params[0], 0, H, 0)
-        Y = E.gat_input_layer_apply(x, *params, 0, 0.2, 0)
-        Y.backward(torch.from_numpy(dY))
-        got = [Y.detach().numpy()] + [p.grad.numpy().copy() for p in params]
-        for p in params:
-            p.grad = None
-        v1 = E.ffn_apply(x, params[0], params[1])
-        aL = E.head_attn_apply(v1, params[2], params[3])
-        Y0 = E.gat_aggregate_ffn_apply(aL, v1, params[4], params[5], 0, 0.2, 0)
-        Y0.backward(torch.from_numpy(dY))
-        want = [Y0.detach().numpy()] + [p.grad.numpy() for p in params]
-        np.testing.assert_allclose(got[0], want[0], **TOL)
-        for name, a, w in zip(("W", "b", "wL", "bL", "wR", "bR"), got[1:], want[1:]):
-            grad_close(a, w, name)
+        for relu in (False, True):
+            for p in params:
+                p.grad = None
+            Y = E.gat_input_layer_apply(x, *params, 0, 0.2, 0, relu)
+            Y.backward(torch.from_numpy(dY))
+            got = [Y.detach().numpy()] + [p.grad.numpy().copy() for p in params]
+            for p in params:
+                p.grad = None
+            v1 = E.ffn_apply(x, params[0], params[1])
+            aL = E.head_attn_apply(v1, params[2], params[3])
+            Y0 = E.gat_aggregate_ffn_apply(aL, v1, params[4], params[5], 0, 0.2, 0)
+            if relu:
+                Y0 = torch.relu(Y0)
+            Y0.backward(torch.from_numpy(dY))
+            want = [Y0.detach().numpy()] + [p.grad.numpy() for p in params]
+            np.testing.assert_allclose(got[0], want[0], **TOL)
+            for name, a, w in zip(("W", "b", "wL", "bL", "wR", "bR"), got[1:], want[1:]):
+                grad_close(a, w, f"{name} relu={relu}")
     E.slots_clear()

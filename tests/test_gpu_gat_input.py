@@ -29,11 +29,12 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, gT=None):
+def gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, gT=None, relu=False, order=None):
     dg = ops.DeviceGraph.from_host(g, split=False)
     dgT = None if gT is None else ops.DeviceGraph.from_host(gT, split=False)
+    od = None if order is None else dev(order)
     out = ops.gat_input_layer(dg, dev(X), dev(W), dev(b), dev(wL), dev(bL), dev(wR), dev(bR), heads,
-                              dY=dev(dY), gT=dgT)
+                              dY=dev(dY), gT=dgT, relu=relu, order=od, order_t=od)
     torch.cuda.synchronize()
     return {k: v.cpu().numpy() for k, v in out.items()}
 
@@ -53,6 +54,10 @@ def test_input_space_kernels_against_the_reference_chain(fin, heads, D):
     got = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads)
     ref = ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, heads)
     check_against_ref(got, ref)
+    # the fused ReLU, rows taken in descending-degree order
+    gr = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, relu=True, order=ops.degree_order(g.rowptr))
+    rr = ref_on_own_logits(g, gr, X, W, b, wL, bL, wR, bR, dY, heads, relu=True)
+    check_against_ref(gr, rr)
     # the host twins run the same sums in the same order (exp aside)
     host = cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads)
     np.testing.assert_allclose(got["Y"], host["Y"], atol=2e-6, rtol=2e-6)
@@ -107,19 +112,24 @@ def test_mirror_op_equals_the_three_op_chain(E):
     params = [dev(a).requires_grad_() for a in (W, b, wL.reshape(1, -1), bL, wR.reshape(1, -1), bR)]
     x = dev(X)
     assert E.gat_input_layer_eligible(x, params[0], 0, H, 0)
-    Y = E.gat_input_layer_apply(x, *params, 0, 0.2, 0)
-    Y.backward(dev(dY))
-    got = [Y.detach().cpu().numpy()] + [p.grad.cpu().numpy() for p in params]
-    for p in params:
-        p.grad = None
-    v1 = E.ffn_apply(x, params[0], params[1])
-    aL = E.head_attn_apply(v1, params[2], params[3])
-    Y0 = E.gat_aggregate_ffn_apply(aL, v1, params[4], params[5], 0, 0.2, 0)
-    Y0.backward(dev(dY))
-    want = [Y0.detach().cpu().numpy()] + [p.grad.cpu().numpy() for p in params]
-    np.testing.assert_allclose(got[0], want[0], **TOL)
-    for name, a, w in zip(("W", "b", "wL", "bL", "wR", "bR"), got[1:], want[1:]):
-        grad_close(a, w, name)
+    for relu in (False, True):
+        for p in params:
+            p.grad = None
+        Y = E.gat_input_layer_apply(x, *params, 0, 0.2, 0, relu)
+        Y.backward(dev(dY))
+        got = [Y.detach().cpu().numpy()] + [p.grad.cpu().numpy() for p in params]
+        for p in params:
+            p.grad = None
+        v1 = E.ffn_apply(x, params[0], params[1])
+        aL = E.head_attn_apply(v1, params[2], params[3])
+        Y0 = E.gat_aggregate_ffn_apply(aL, v1, params[4], params[5], 0, 0.2, 0)
+        if relu:
+            Y0 = torch.relu(Y0)
+        Y0.backward(dev(dY))
+        want = [Y0.detach().cpu().numpy()] + [p.grad.cpu().numpy() for p in params]
+        np.testing.assert_allclose(got[0], want[0], **TOL)
+        for name, a, w in zip(("W", "b", "wL", "bL", "wR", "bR"), got[1:], want[1:]):
+            grad_close(a, w, f"{name} relu={relu}")
     # an input that needs a gradient keeps the chain
     assert not E.gat_input_layer_eligible(x.clone().requires_grad_(), params[0], 0, H, 0)
 
@@ -137,6 +147,7 @@ def test_config3_products_input_layer_against_the_reference_chain():
     assert (g.n_rows, g.nnz) == (bench.PRODUCTS_N, bench.PRODUCTS_E)
     fin, H, D = 100, 8, 32
     X, W, b, wL, bL, wR, bR, dY = layer_inputs(g.n_rows, fin, H, D, seed=2024)
-    got = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, H)
-    ref = ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, H)
+    # as the program runs it: the ReLU fused, rows in descending-degree order
+    got = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, H, relu=True, order=ops.degree_order(g.rowptr))
+    ref = ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, H, relu=True)
     check_against_ref(got, ref)
