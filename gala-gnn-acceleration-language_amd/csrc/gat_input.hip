@@ -316,6 +316,14 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
         f4v acc[kInTiles];
 #pragma unroll
         for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        // the rows this lane's projection outputs will go to (slots 2 kq, 2 kq + 1), requested
+        // before the walk so the stores after the barrier wait on nothing
+        int64_t prow[2];
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+            const int64_t si = blk * kInWaves + 2 * kq + hs;
+            prow[hs] = si < p.n_rows ? (p.order ? (int64_t)p.order[si] : si) : -1;
+        }
         {
             const float al = cur.side;
             const int H = p.H;
@@ -351,9 +359,8 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
 #pragma unroll
             for (int hs = 0; hs < 2; ++hs) {
                 const int s = 2 * kq + hs;
-                const int64_t si = blk * kInWaves + s;
-                if (si >= p.n_rows) continue;
-                const int64_t row = p.order ? (int64_t)p.order[si] : si;
+                const int64_t row = prow[hs];
+                if (row < 0) continue;
                 const float S = stf[((s * 16 + h) * kInTiles + 4) * 16 + 12];
                 const float Sm = stf[((s * 16 + h + 8) * kInTiles + 4) * 16 + 12];
                 const float qv = 1.0f / __fadd_rn(S, 1e-12f);   // REF: 1 / (1e-12 + sum p)
@@ -401,6 +408,7 @@ __device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v)
 template <int DW>
 __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
     __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
+    __shared__ f4v dstash[kInWaves * kWave];                        // [slot][256]: the columns' dY (masked)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
     const float *stf = reinterpret_cast<const float *>(stash);
@@ -473,6 +481,7 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 p.daL[c * p.H + hh] = (sym - accv * p.sma[c * p.H + hh]) + 1e-12f;   // common.h:662-667
             }
         }
+        dstash[wave * kWave + lane] = dy;   // the M phase's A operand, from LDS after the barrier
         if (n16 < kInMaxHeads) {
 #pragma unroll
             for (int t = 0; t < kInTiles; ++t) stash[((wave * kInMaxHeads + n16) * kInTiles + t) * 4 + kq] = acc[t];
@@ -484,14 +493,12 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 const int s = 4 * ks + kq;
                 const int64_t si = blk * kInWaves + s;
                 const bool ok = si < p.n_rows;
-                const int64_t cs = ok ? (p.order ? (int64_t)p.order[si] : si) : 0;
+                const float *dsf = reinterpret_cast<const float *>(dstash) + s * 4 * kWave;
                 float a[2];
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
                     const int j = 16 * mt + n16;
-                    const int64_t o = cs * p.ldy + (int64_t)h * p.D + j;
-                    a[mt] = (ok && j < p.D) ? p.dY[o] : 0.0f;
-                    if (p.relu && ok && j < p.D && !(p.Y[o] > 0.0f)) a[mt] = 0.0f;
+                    a[mt] = (ok && j < p.D) ? dsf[h * p.D + j] : 0.0f;
                 }
 #pragma unroll
                 for (int t = 0; t < kInTiles; ++t) {
