@@ -55,8 +55,6 @@ struct SpmmParams {
     int32_t split_threshold;  // > 0: rows longer than this are left to the split kernels
     const int32_t *row_order; // nullable: row group i handles row row_order[i]
     int32_t xcd_order;        // 1: XCD-aware block order (logical_block_runs)
-    int32_t lds_guard;        // host: launch the row kernel with a token of LDS, so it never shares a
-                              // CU with a whole-LDS hub workgroup (the longest chains)
     int32_t dst_deg;          // 1: the dst factor is 1/sqrt(deg) of the row (one segment)
     float *Y2;                // nullable epilogue output: Y2[r] = s2[r] * Y[r]
     int64_t ldy2;
@@ -750,7 +748,7 @@ static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t 
     const int64_t blocks = (p.n_rows + rows_per_block - 1) / rows_per_block;
     if (RELU || SAMP || !sp || sp->n_chunks <= 0) {   // (the ReLU prologue: no hub split, host-checked)
         hipLaunchKernelGGL((k_spmm_rowgroup<VEC, G, CH, U, W, SAMP, SRCS, RELU>), dim3((unsigned)blocks),
-                           dim3(kBlock), p.lds_guard ? 16 : 0, st, p);
+                           dim3(kBlock), 0, st, p);
     }
     if constexpr (!RELU)
     if (!SAMP && sp && sp->n_chunks > 0) {
@@ -781,11 +779,8 @@ static void launch_hub_hb(const SpmmParams &p, HubParams hp, hipStream_t st, siz
 
 template <int VEC, int FSP, bool W, bool SRCS>
 static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st, bool whole_cu) {
-    // whole_cu: a CU's whole LDS, so no other hub workgroup, and no row-kernel workgroup
-    // (launched with an LDS guard then), shares the CU with the chain.  (Double tiles for these
-    // rows measured slower: 2.39 vs 2.09 ms on R-MAT, tools/hub_long_ab.py)
-    if (whole_cu)
-        launch_hub_hb<VEC, FSP, W, SRCS, kHubBuf>(p, hp, st, kCuLds);
+    if (whole_cu)   // double tiles; the whole LDS, so no other hub workgroup shares the CU
+        launch_hub_hb<VEC, FSP, W, SRCS, 2 * kHubBuf>(p, hp, st, kCuLds);
     else
         launch_hub_hb<VEC, FSP, W, SRCS, kHubBuf>(p, hp, st, HubLds<FSP, W, SRCS>::floats * sizeof(float));
 }
@@ -1011,7 +1006,6 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
     p.ldrx = ldrx;
     p.relu_act = relu_x ? epi->relu_act : nullptr;
     p.row_order = nullptr;
-    p.lds_guard = 0;
     p.xcd_order = 1;  // off below when a degree-ordered row schedule is used (heavy rows first)
     hipStream_t hs = (hipStream_t)stream;
 
@@ -1051,7 +1045,6 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         if (hub_st != hs && plan->row_order && plan->n_long > 0 && plan->n_long <= plan->n_rows_split &&
             plan->aux_stream2 && plan->aux_events2[0] && plan->aux_events2[1]) {
             long_st = (hipStream_t)plan->aux_stream2;
-            p.lds_guard = 1;
             hp_long = hp;
             hp_long.n_hub = plan->n_long;
             hp.order = plan->row_order + plan->n_long;
