@@ -491,21 +491,19 @@ struct HubParams {
 // LDS: buf[2][T/4][FSP][4] (X; an edge quad of one feature is one 16-B read), scl[2][T]
 // (SRCS), wts[2][kHubMaxHeads][T] (W), yinit[64], then slack the chain's prefetch may read
 // past a buffer (never consumed).  Unweighted: 68 KB, two workgroups per CU.
-template <int FSP, bool W, bool SRCS, int HB = kHubBuf>
+template <int FSP, bool W, bool SRCS>
 struct HubLds {
-    static constexpr int T = HB / FSP;               // edges per tile
+    static constexpr int T = kHubBuf / FSP;          // edges per tile
     static constexpr int kGroup = 16;                 // edges per chain group
-    static constexpr size_t buf = 0, scl = 2 * (size_t)HB, wts = scl + (SRCS ? 2 * T : 0),
+    static constexpr size_t buf = 0, scl = 2 * (size_t)kHubBuf, wts = scl + (SRCS ? 2 * T : 0),
                             yinit = wts + (W ? 2 * (size_t)kHubMaxHeads * T : 0), slack = yinit + kWave,
                             floats = slack + 2 * kGroup * FSP;
 };
 
-// HB: floats of X per tile buffer -- kHubBuf, or twice that for the longest chains (a CU's
-// LDS each: a tile then outlasts the gathers' memory latency under load)
-template <int VEC, int FSP, bool W, bool SRCS, int HB = kHubBuf>
+template <int VEC, int FSP, bool W, bool SRCS>
 __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, HubParams hp) {
     typedef typename VecT<VEC>::T V;
-    typedef HubLds<FSP, W, SRCS, HB> L;
+    typedef HubLds<FSP, W, SRCS> L;
     constexpr int T = L::T;
     constexpr int RG = (T * (FSP / VEC) + kHubGather - 1) / kHubGather;  // loads per gatherer
     constexpr int RW = (T * kHubMaxHeads + kHubGather - 1) / kHubGather;
@@ -563,7 +561,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
         }
     };
     auto store = [&](int b) {
-        float *xb = hub_lds + L::buf + (size_t)b * HB;
+        float *xb = hub_lds + L::buf + (size_t)b * kHubBuf;
 #pragma unroll
         for (int k = 0; k < RG; ++k) {
             const int e = s_edge[k];
@@ -603,7 +601,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     };
     auto run_chain = [&](int t) {
         const int b = t & 1;
-        const float *xb = hub_lds + L::buf + (size_t)b * HB + cl * 4;
+        const float *xb = hub_lds + L::buf + (size_t)b * kHubBuf + cl * 4;
         const float *sb = hub_lds + L::scl + b * T;
         const float *wb = hub_lds + L::wts + (size_t)b * kHubMaxHeads * T + hl * T;
         const int cnt = (int)((n - (int64_t)t * T) < T ? (n - (int64_t)t * T) : T);
@@ -651,7 +649,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
             fetch(j, A);
             consume(A);
         }
-        const float *xs = hub_lds + L::buf + (size_t)b * HB + cl * 4;
+        const float *xs = hub_lds + L::buf + (size_t)b * kHubBuf + cl * 4;
         for (; j < cnt; ++j)
             add(xs[(j >> 2) * FSP * 4 + (j & 3)], W ? wb[j] : 1.0f, SRCS ? sb[j] : 1.0f);
     };
@@ -765,24 +763,17 @@ constexpr size_t kCuLds = 160 * 1024;   // gfx950: LDS per CU
 
 // whole_cu: each workgroup takes a CU's whole LDS (the longest chains: no other hub
 // workgroup may share the CU while they run)
-template <int VEC, int FSP, bool W, bool SRCS, int HB>
-static void launch_hub_hb(const SpmmParams &p, HubParams hp, hipStream_t st, size_t lds) {
-    static_assert(HubLds<FSP, W, SRCS, HB>::floats * sizeof(float) <= kCuLds, "hub LDS");
+template <int VEC, int FSP, bool W, bool SRCS>
+static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st, bool whole_cu) {
+    constexpr size_t need = HubLds<FSP, W, SRCS>::floats * sizeof(float);
+    static_assert(need <= kCuLds, "hub LDS");
     // more than the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once
-    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS, HB>,
+    static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
     (void)opted;
     hp.n_slices = (p.F + FSP - 1) / FSP;
-    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS, HB>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
-                       dim3(kHubThreads), lds, st, p, hp);
-}
-
-template <int VEC, int FSP, bool W, bool SRCS>
-static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st, bool whole_cu) {
-    if (whole_cu)   // double tiles; the whole LDS, so no other hub workgroup shares the CU
-        launch_hub_hb<VEC, FSP, W, SRCS, 2 * kHubBuf>(p, hp, st, kCuLds);
-    else
-        launch_hub_hb<VEC, FSP, W, SRCS, kHubBuf>(p, hp, st, HubLds<FSP, W, SRCS>::floats * sizeof(float));
+    hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
+                       dim3(kHubThreads), whole_cu ? kCuLds : need, st, p, hp);
 }
 
 // slices of 32 features when F <= 32 (F = 32: one 128-B row per edge, 512 edges a tile),
