@@ -759,35 +759,28 @@ static void launch_rg_u(const SpmmParams &p, const SplitParams *sp, hipStream_t 
     }
 }
 
-constexpr size_t kCuLds = 160 * 1024;   // gfx950: LDS per CU
-
-// whole_cu: each workgroup takes a CU's whole LDS (the longest chains: no other hub
-// workgroup may share the CU while they run)
 template <int VEC, int FSP, bool W, bool SRCS>
-static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st, bool whole_cu) {
-    constexpr size_t need = HubLds<FSP, W, SRCS>::floats * sizeof(float);
-    static_assert(need <= kCuLds, "hub LDS");
+static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st) {
+    constexpr size_t lds = HubLds<FSP, W, SRCS>::floats * sizeof(float);
     // more than the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once
     static const hipError_t opted = hipFuncSetAttribute((const void *)k_spmm_hub_exact<VEC, FSP, W, SRCS>,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)opted;
     hp.n_slices = (p.F + FSP - 1) / FSP;
     hipLaunchKernelGGL((k_spmm_hub_exact<VEC, FSP, W, SRCS>), dim3((unsigned)(hp.n_hub * hp.n_slices)),
-                       dim3(kHubThreads), whole_cu ? kCuLds : need, st, p, hp);
+                       dim3(kHubThreads), lds, st, p, hp);
 }
 
 // slices of 32 features when F <= 32 (F = 32: one 128-B row per edge, 512 edges a tile),
 // else of 64 (one chain lane per feature of a wave)
-static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w, bool srcs, hipStream_t st,
-                       bool whole_cu = false) {
-    if (hp.n_hub <= 0) return;
+static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w, bool srcs, hipStream_t st) {
 #define GALA_HUB(V, S)                                                    \
     if (w) {                                                              \
-        if (srcs) launch_hub_t<V, S, true, true>(p, hp, st, whole_cu);    \
-        else launch_hub_t<V, S, true, false>(p, hp, st, whole_cu);        \
+        if (srcs) launch_hub_t<V, S, true, true>(p, hp, st);              \
+        else launch_hub_t<V, S, true, false>(p, hp, st);                  \
     } else {                                                              \
-        if (srcs) launch_hub_t<V, S, false, true>(p, hp, st, whole_cu);   \
-        else launch_hub_t<V, S, false, false>(p, hp, st, whole_cu);       \
+        if (srcs) launch_hub_t<V, S, false, true>(p, hp, st);             \
+        else launch_hub_t<V, S, false, false>(p, hp, st);                 \
     }
     const bool narrow = p.F <= 32;
     if (vec == 4) {
@@ -1022,8 +1015,8 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         p.split_threshold = plan->threshold;
         sp = &spl;
     }
-    HubParams hp{}, hp_long{};
-    hipStream_t hub_st = hs, long_st = hs;
+    HubParams hp{};
+    hipStream_t hub_st = hs;
     if (use_hub) {
         if (plan->threshold < 1 || !plan->rows) return GALA_ERR_INVALID_ARG;
         p.split_threshold = plan->threshold;  // the row kernel leaves hub rows to k_spmm_hub_exact
@@ -1032,15 +1025,6 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         hp.n_hub = plan->n_rows_split;
         // the hub rows run beside the row kernel on the plan's side stream when it has one
         if (plan->aux_stream && plan->aux_events[0] && plan->aux_events[1]) hub_st = (hipStream_t)plan->aux_stream;
-        // the longest chains in a launch of their own, a CU each (the order's first n_long rows)
-        if (hub_st != hs && plan->row_order && plan->n_long > 0 && plan->n_long <= plan->n_rows_split &&
-            plan->aux_stream2 && plan->aux_events2[0] && plan->aux_events2[1]) {
-            long_st = (hipStream_t)plan->aux_stream2;
-            hp_long = hp;
-            hp_long.n_hub = plan->n_long;
-            hp.order = plan->row_order + plan->n_long;
-            hp.n_hub = plan->n_rows_split - plan->n_long;
-        }
     }
 
     // feature chunks wider than 512 vectors per lane-group are split over launches
@@ -1068,15 +1052,12 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             const int L = (int)((Fc + vec - 1) / vec);
             int r = 0;
             const bool forked = use_hub && hub_st != hs;
-            const bool forked2 = forked && long_st != hs;
             if (use_hub) {  // the long serial rows first, so their workgroups are dispatched first
                 if (forked) {
                     if (hipEventRecord((hipEvent_t)plan->aux_events[0], hs) != hipSuccess ||
-                        hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess ||
-                        (forked2 && hipStreamWaitEvent(long_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess))
+                        hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)
                         return launch_status();
                 }
-                if (forked2) launch_hub(q, hp_long, vec, w, src_scale != nullptr, long_st, true);
                 launch_hub(q, hp, vec, w, src_scale != nullptr, hub_st);
                 r = launch_status();
             }
@@ -1094,13 +1075,6 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             if (forked) {
                 if (hipEventRecord((hipEvent_t)plan->aux_events[1], hub_st) != hipSuccess ||
                     hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events[1], 0) != hipSuccess) {
-                    const int j = launch_status();
-                    if (!r) r = j ? j : GALA_ERR_HIP;
-                }
-            }
-            if (forked2) {
-                if (hipEventRecord((hipEvent_t)plan->aux_events2[1], long_st) != hipSuccess ||
-                    hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events2[1], 0) != hipSuccess) {
                     const int j = launch_status();
                     if (!r) r = j ? j : GALA_ERR_HIP;
                 }

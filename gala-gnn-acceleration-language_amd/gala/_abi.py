@@ -47,9 +47,6 @@ class gala_split_plan_t(ctypes.Structure):
         ("row_order", ctypes.c_void_p),
         ("aux_stream", ctypes.c_void_p),
         ("aux_events", ctypes.c_void_p * 2),
-        ("n_long", ctypes.c_int64),
-        ("aux_stream2", ctypes.c_void_p),
-        ("aux_events2", ctypes.c_void_p * 2),
     ]
 
 

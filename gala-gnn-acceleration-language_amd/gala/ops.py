@@ -8,7 +8,6 @@ wrappers and autograd Functions of codegen/gala.cu) lives in host/gala_torch.cpp
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -27,14 +26,6 @@ def _dp(t):
     if not t.is_cuda:
         raise ValueError("gala ops take device tensors (no CPU fallback)")
     return t.data_ptr()
-
-
-def long_chain_edges() -> int:
-    """Hub rows of at least this many edges run their REF-order chain on a CU of their own
-    (gala_split_plan_t.n_long): 131072 (a chain of ~0.6 ms, about the R-MAT row kernel's
-    time); GALA_HUB_LONG overrides it (0: one hub launch)."""
-    v = int(os.environ.get("GALA_HUB_LONG", "131072"))
-    return v if v > 0 else 1 << 62
 
 
 class DeviceGraph:
@@ -108,20 +99,6 @@ class DeviceGraph:
                 ev.record(aux[0])   # creates the event handles
             plan.aux_stream = aux[0].cuda_stream
             plan.aux_events[0], plan.aux_events[1] = aux[1].cuda_event, aux[2].cuda_event
-            # the longest chains (a whole CU each, on a second side stream): hub rows of at
-            # least long_chain_edges() edges, the order's first entries
-            n_long = 0
-            if order is not None:
-                deg = np.diff(rp.astype(np.int64))
-                n_long = int((deg[order[:nr.value]] >= long_chain_edges()).sum())
-            if n_long > 0:
-                aux2 = (torch.cuda.Stream(device=dev), torch.cuda.Event(), torch.cuda.Event())
-                for ev in aux2[1:]:
-                    ev.record(aux2[0])
-                plan.n_long = n_long
-                plan.aux_stream2 = aux2[0].cuda_stream
-                plan.aux_events2[0], plan.aux_events2[1] = aux2[1].cuda_event, aux2[2].cuda_event
-                aux = aux + aux2
         self._split = {"plan": plan, "arrays": arrays + (order_t,), "ws": None, "aux": aux}
         self._csr = None
 

@@ -369,11 +369,10 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
     st->rows = rows.to(offsets.device());
     st->row_chunk0 = rc0.to(offsets.device());
     st->chunk_row = crow.to(offsets.device());
-    torch::Tensor order_host;
     if (skewed) {
-        order_host = torch::empty({n}, io);
-        check(gala_host_row_order(n, r, order_host.data_ptr<int32_t>()), "gala_host_row_order");
-        st->row_order = order_host.to(offsets.device());
+        auto order = torch::empty({n}, io);
+        check(gala_host_row_order(n, r, order.data_ptr<int32_t>()), "gala_host_row_order");
+        st->row_order = order.to(offsets.device());
     }
     if (nr > 0 && offsets.is_cuda()) {
         // the REF-order hub rows run on a side stream beside the row kernel
@@ -383,25 +382,6 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
             hipEvent_t ev = nullptr;
             TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
             st->aux_events[i] = st->plan.aux_events[i] = (void *)ev;
-        }
-        // the longest chains (>= GALA_HUB_LONG edges, default 131072) in a launch of their own,
-        // a whole CU each, on a second side stream
-        int64_t long_edges = 131072;
-        if (const char *e = std::getenv("GALA_HUB_LONG")) long_edges = std::atoll(e) > 0 ? std::atoll(e) : INT64_MAX;
-        int64_t n_long = 0;
-        if (skewed) {
-            const int32_t *o = order_host.data_ptr<int32_t>();
-            while (n_long < nr && (int64_t)r[o[n_long] + 1] - r[o[n_long]] >= long_edges) ++n_long;
-        }
-        if (n_long > 0) {
-            auto aux2 = c10::hip::getStreamFromPool(false, offsets.device().index());
-            st->plan.aux_stream2 = (void *)aux2.stream();
-            for (int i = 0; i < 2; ++i) {
-                hipEvent_t ev = nullptr;
-                TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
-                st->plan.aux_events2[i] = (void *)ev;
-            }
-            st->plan.n_long = n_long;
         }
     }
     st->plan.threshold = thr;

@@ -100,14 +100,6 @@ typedef struct gala_split_plan {
                                   graph from two host threads / streams must be ordered by
                                   the caller (or use a plan each), else one call's join can
                                   wait on the other's fork.                               */
-    int64_t n_long;            /* ABI 5: the first n_long entries of row_order (the longest hub
-                                  rows' serial chains).  With aux_stream2 / aux_events2 set the
-                                  REF-order SpMM runs them in a launch of their own on
-                                  aux_stream2, each workgroup holding a whole CU's LDS, so no other
-                                  hub workgroup shares its CU for the chain's duration (the
-                                  others run beside it on aux_stream).  0: one hub launch.   */
-    void *aux_stream2;         /* hipStream_t or NULL                                      */
-    void *aux_events2[2];      /* hipEvent_t fork / join pair for aux_stream2               */
 } gala_split_plan_t;
 
 typedef struct gala_csr {
