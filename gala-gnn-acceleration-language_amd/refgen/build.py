@@ -45,6 +45,20 @@ PROGRAMS = {
     # the GAT program in the base's spelling: its own edge-sum / softmax / aggregation classes
     # over the mirror's K5 / K7 / K8 / K9 and weighted SpMM (the operator-level drop-in path)
     "gat_unfused": ["64", "7", "32", "3", "2", "5000"],
+    # gala_train's whole pass set (GALA_REFGEN_TRAIN: reordering, sparse rewrites, code motion and
+    # the training subgraph, tests/gala_train.cpp:124-146), the schedule of the paper's evaluation
+    # (scripts/Evaluations/Figures-16-17.py:82): the GCN untiled and the GCN-3 over 4 column tiles
+    # (the subgraphs' own tiled copies)
+    "gcn_train": ["64", "7", "32", "3", "2"],
+    "gcn3_train": ["64", "7", "32", "3", "2", "5000"],
+    "gat_train": ["64", "7", "32", "3", "2", "5000"],
+    "gin_train": ["64", "7", "32", "3", "2"],
+    "sage_train": ["64", "7", "32", "3", "2"],
+    # the base's spelling of the GIN, SAGE and gala_train GCN-3 programs (no fused chains, the
+    # base's loss): the fused ones give the same prediction and gradients bit for bit
+    "gin_unfused": ["64", "7", "32", "3", "2"],
+    "sage_unfused": ["64", "7", "32", "3", "2"],
+    "gcn3_train_unfused": ["64", "7", "32", "3", "2", "5000"],
 }
 
 
@@ -61,7 +75,7 @@ def compile_driver(exe: str) -> None:
 # gala_train's training-invariant code motion (tests/gala_train.cpp:136-140): for SAGE (without
 # it the reference generator's first SAGE FFN reads t_iden_n, which only the hoisted mean
 # aggregation defines, common.h:1210-1213) and for the GIN under gala_train's passes
-CODE_MOTION = {"sage", "gin_motion"}
+CODE_MOTION = {"sage", "gin_motion", "sage_unfused"}
 
 
 def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
@@ -73,6 +87,8 @@ def emit(driver: str, out_dir: str, model: str, dataset: str, args) -> str:
         env["GALA_REFGEN_CODE_MOTION"] = "1"
     if model.endswith("_unfused"):
         env["GALA_REFGEN_UNFUSED"] = "1"
+    if "_train" in model:
+        env["GALA_REFGEN_TRAIN"] = "1"
     family = model.split("_")[0]          # the driver's layer template (gcn3_papers: gcn3)
     subprocess.run([driver, out_dir.rstrip("/") + "/", family, dataset, *args], check=True, capture_output=True,
                    text=True, timeout=60, env=env)

@@ -30,7 +30,7 @@
 #define GALA_HIP_CODEGEN_H
 
 #include <cstdlib>
-#include <regex>
+#include <iostream>
 #include <unordered_set>
 
 #include "common.h"
@@ -182,12 +182,13 @@ public:
             "  torch::Tensor t_test_mask = torch::from_blob(test_mask.vals_ptr(), {(int64_t)nrows}, torch::kBool).to(device).clone();\n";
         preCode.addCode(s);
         std::unordered_set<std::string> seen;
+        std::unordered_set<int> slots;
         bool defaultLoaded = false;
         for (CIRNode *n : program) {
             if (auto *c = dynamic_cast<ComputeNode *>(n)) {
-                transferInputs(c, seen, defaultLoaded);
+                transferInputs(c, seen, slots, defaultLoaded);
             } else if (auto *loop = dynamic_cast<TrainingLoopNode *>(n)) {
-                for (int i = 0; i < loop->getLoopNodeNum(); ++i) transferInputs(loop->getNode(i), seen, defaultLoaded);
+                for (int i = 0; i < loop->getLoopNodeNum(); ++i) transferInputs(loop->getNode(i), seen, slots, defaultLoaded);
             }
         }
     }
@@ -200,15 +201,28 @@ public:
         initCMake();
         initKernels(program);
         commonPerCode();
+        const State before = save();
         generateCode(program, transforms);
+        const State after = save();
+        load(before);   // the dry run: which forward entries each in-loop node emitted
+        const std::vector<Span> spans = forwardSpans(program, transforms);
+        Code dry = *model.getForward();
+        load(after);
+        Code &fwd = *model.getForward();
+        bool same = dry.getNum() <= fwd.getNum();
+        for (int i = 0; same && i < dry.getNum(); ++i) same = *dry.atLine(i) == *fwd.atLine(i);
+        if (!same) {
+            std::cerr << "HIPGenerator: the dry run's forward differs from generateCode's; no fusion is safe\n";
+            std::exit(3);
+        }
         for (Code *c : {&kernelCallCode, model.getDef(), model.getInit(), model.getForward(), &preCode,
                         model.getInv(), model.getPreCall(), model.getCall(), model.getPostCall(), &postCode})
             retarget(*c);
         denseOnMatrixCores(*model.getForward());
         denseOnMatrixCores(*model.getInv());
         if (!std::getenv("GALA_REFGEN_UNFUSED")) {   // (the unfused spelling: a bit-identity check)
-            fuseGcnChains(*model.getForward());
-            fuseGatChains(*model.getForward());
+            fuseGcnChains(fwd, spans);
+            fuseGatChains(fwd, spans);
             trainRowsAndLoss(preCode, *model.getPostCall());
         }
         addDumpHook(*model.getPostCall());
@@ -318,8 +332,13 @@ private:
     }
 
     // The graph inputs of one compute node, each transferred once (the order and slot
-    // numbering of cuda.h:1051-1305: the default graph first, then every other CSR input)
-    void transferInputs(ComputeNode *c, std::unordered_set<std::string> &seen, bool &defaultLoaded) {
+    // numbering of cuda.h:1051-1305: the default graph first, then every other CSR input).
+    // Each graph index is transferred once: under gala_train's training subgraph
+    // (middle-end.h:39-210) an untiled program meets its loaded graph twice -- as the
+    // subgraphs' default graph "adj" (index 0) and by its own name adj0 -- and cuda.h emits
+    // dA_csrOffsets0 both times (a redeclaration nvcc would refuse); here the second is skipped.
+    void transferInputs(ComputeNode *c, std::unordered_set<std::string> &seen, std::unordered_set<int> &slots,
+                        bool &defaultLoaded) {
         if (!c) return;
         std::string code;
         for (int i = 0; i < c->getNumInputs(); ++i) {
@@ -330,7 +349,8 @@ private:
                 if (!seen.count(name) && info->getFormat() == CSR_STYPE) {
                     defaultLoaded = true;
                     seen.insert(name);
-                    code += graphPair(d, name, info->getDefaultIndex(), info->getDefaultDirected(), info->getWeighted());
+                    if (slots.insert(info->getDefaultIndex()).second)
+                        code += graphPair(d, name, info->getDefaultIndex(), info->getDefaultDirected(), info->getWeighted());
                 }
             }
             if (seen.count(d->getName())) continue;
@@ -340,7 +360,8 @@ private:
             seen.insert(d->getName());
             if (d->getName() == "attn" || d->getName() == "val") continue;  // edge values, not graphs
             info->setIndex(index);
-            code += graphPair(d, d->getName(), index, info->getDirected(), info->getWeighted());
+            if (slots.insert(index).second)
+                code += graphPair(d, d->getName(), index, info->getDirected(), info->getWeighted());
         }
         if (!code.empty()) preCode.addCode(code);
     }
@@ -398,150 +419,192 @@ private:
         }
     }
 
-    // The base emits a GCN layer as torch ops around the aggregation's autograd class:
-    // `res = norm * x;` (ROW_BROADCAST), `res = torch::relu(res);`, the aggregation (an
-    // `if (ep % mod_v == 0)` pair of identical apply calls), `res = norm * res;`
-    // (common.h:928-978, 1150-1184).  On config 5's 11 M rows each such torch op is a 5.7 GB
-    // pass (a ROW_BROADCAST 1.8 ms, a ReLU 2.9 ms, forward and backward alike).  A chain
-    //     [res = act * X;] [res = torch::relu(res);] [res = pre * res;] AGG [res = post * res;]
-    // around an unsampled aggregation becomes the mirror's fused op over the same slot,
-    //     res = gala::gcn_aggregate_relu_apply(X, act, pre, post, li);   (or gcn_aggregate_apply)
-    // whose forward and backward are the unfused chain's roundings bit for bit (the ROW_
-    // BROADCASTs in the aggregation's prologue / epilogue, relu as torch's GPU kernel).
-    // Statements of any other shape are left as they are.
-    struct FwdStmt {
-        enum Kind { Other, Mul, Relu, Agg, AttnAgg, EdgeSum, LeakyDecl, Leaky, Softmax, HeadAttn } kind = Other;
-        // Mul: a = scale, b = source; Agg: a = class, b = slot index; AttnAgg: a = class,
-        // b = slot, c = source; EdgeSum: a = attn_l, b = attn_r, c = slot; LeakyDecl: a = slope;
-        // Softmax: b = slot; HeadAttn: lhs = gala::head_attn_apply(a, c->weight, c->bias), b = lhs
-        std::string text, a, b, c;
-    };
+    // ---- fusions, recognised on the CIR -------------------------------------------------
+    // The base emits each in-loop node's statements into the forward (one Code entry per
+    // statement) from the node's op, operand names and slot indices (common.h:511-1377).  The
+    // fusions below recognise node chains on those same fields -- ops, names (the emitted
+    // program's data flow is by name), graph indices, compute options -- and replace exactly
+    // the forward entries the chain's nodes emitted.  Which entries a node emitted comes from a
+    // dry run of the base's own generateOpCode over the program (forwardSpans), checked entry
+    // for entry against the forward generateCode wrote; a mismatch stops the generator rather
+    // than leaving a fusion silently off.
 
-    static std::vector<FwdStmt> splitForward(const std::string &t) {
-        static const std::regex mul("^res = (\\w+) \\* (\\w+);$"), relu("^res = torch::relu\\(res\\);$"),
-            app("^res = (\\w+)::apply\\(res, (\\d+)\\);$"),
-            app_attn("^res = (\\w+)::apply\\((\\w+), attn, (\\d+)\\);$"),
-            edge("^attn = aggregate_edge_sum_AutoGrad::apply\\((\\w+), (\\w+), (\\d+)\\);$"),
-            leaky_decl("^torch::nn::LeakyReLU leaky_relu\\(torch::nn::LeakyReLUOptions\\(\\)\\.negative_slope\\(([0-9.eE+-]+)\\)\\);$"),
-            leaky("^attn = leaky_relu->forward\\(attn\\);$"),
-            softmax("^attn = non_lnr_op_softmax_AutoGrad::apply\\(attn, (\\d+)\\);$"),
-            head_attn("^(\\w+) = gala::head_attn_apply\\((\\w+), (\\w+)->weight, \\3->bias\\);$");
-        std::vector<FwdStmt> out;
-        size_t p = 0;
-        auto trim = [](std::string x) {
-            const size_t a = x.find_first_not_of(" \t\n"), b = x.find_last_not_of(" \t\n");
-            return a == std::string::npos ? std::string() : x.substr(a, b - a + 1);
-        };
-        auto block = [&](size_t open, size_t &close) {  // body of the {...} opening at `open`
-            int depth = 0;
-            for (size_t i = open; i < t.size(); ++i) {
-                if (t[i] == '{') ++depth;
-                if (t[i] == '}' && --depth == 0) {
-                    close = i;
-                    return trim(t.substr(open + 1, i - open - 1));
-                }
-            }
-            close = std::string::npos;
-            return std::string();
-        };
-        const std::string ifkey = "if (ep % mod_v == 0)";
-        while (p < t.size()) {
-            const size_t q = t.find_first_not_of(" \t\n", p);
-            if (q == std::string::npos) {
-                out.push_back({FwdStmt::Other, t.substr(p), "", ""});
-                break;
-            }
-            FwdStmt st;
-            if (t.compare(q, ifkey.size(), ifkey) == 0) {
-                size_t c1 = std::string::npos, c2 = std::string::npos;
-                const size_t o1 = t.find('{', q);
-                const std::string b1 = o1 == std::string::npos ? "" : block(o1, c1);
-                const size_t e = c1 == std::string::npos ? c1 : t.find_first_not_of(" \t\n", c1 + 1);
-                const bool has_else = e != std::string::npos && t.compare(e, 4, "else") == 0;
-                const size_t o2 = has_else ? t.find('{', e) : std::string::npos;
-                const std::string b2 = o2 == std::string::npos ? "" : block(o2, c2);
-                std::smatch m1, m2;
-                if (c2 != std::string::npos && std::regex_match(b1, m1, app) && std::regex_match(b2, m2, app) &&
-                    m1[0] == m2[0]) {
-                    st = {FwdStmt::Agg, t.substr(p, c2 + 1 - p), m1[1], m1[2], ""};
-                    out.push_back(st);
-                    p = c2 + 1;
-                    continue;
-                }
-                if (c2 != std::string::npos && std::regex_match(b1, m1, app_attn) &&
-                    std::regex_match(b2, m2, app_attn) && m1[0] == m2[0]) {
-                    st = {FwdStmt::AttnAgg, t.substr(p, c2 + 1 - p), m1[1], m1[3], m1[2]};
-                    out.push_back(st);
-                    p = c2 + 1;
-                    continue;
-                }
-            }
-            const size_t semi = t.find(';', q);
-            const size_t end = semi == std::string::npos ? t.size() : semi + 1;
-            st.text = t.substr(p, end - p);
-            const std::string body = trim(st.text);
-            std::smatch m;
-            if (std::regex_match(body, m, mul)) st = {FwdStmt::Mul, st.text, m[1], m[2], ""};
-            else if (std::regex_match(body, relu)) st = {FwdStmt::Relu, st.text, "", "", ""};
-            else if (std::regex_match(body, m, edge)) st = {FwdStmt::EdgeSum, st.text, m[1], m[2], m[3]};
-            else if (std::regex_match(body, m, leaky_decl)) st = {FwdStmt::LeakyDecl, st.text, m[1], "", ""};
-            else if (std::regex_match(body, leaky)) st = {FwdStmt::Leaky, st.text, "", "", ""};
-            else if (std::regex_match(body, m, softmax)) st = {FwdStmt::Softmax, st.text, "", m[1], ""};
-            else if (std::regex_match(body, m, head_attn)) st = {FwdStmt::HeadAttn, st.text, m[2], m[1], m[3]};
-            out.push_back(st);
-            p = end;
-        }
-        return out;
+    // The sections generateCode writes into, saved and restored around the dry run.
+    struct State {
+        Code cmake, imports, kernels, kernelCalls, autoGrad, pre, post;
+        Model model;
+        std::vector<std::string> functions;
+    };
+    State save() const {
+        State s;
+        s.cmake = cmakeCode;
+        s.imports = importCode;
+        s.kernels = kernelCode;
+        s.kernelCalls = kernelCallCode;
+        s.autoGrad = autoGradCode;
+        s.pre = preCode;
+        s.post = postCode;
+        s.model = model;
+        s.functions = generatedFunctions;
+        return s;
+    }
+    void load(const State &s) {
+        cmakeCode = s.cmake;
+        importCode = s.imports;
+        kernelCode = s.kernels;
+        kernelCallCode = s.kernelCalls;
+        autoGradCode = s.autoGrad;
+        preCode = s.pre;
+        postCode = s.post;
+        model = s.model;
+        generatedFunctions = s.functions;
     }
 
-    void fuseGcnChains(Code &fwd) {
-        std::string t;
-        for (int i = 0; i < fwd.getNum(); ++i) t += *fwd.atLine(i) + "\n";
-        std::vector<FwdStmt> st = splitForward(t);
-        std::string out;
-        size_t done = 0;  // statements [0, done) are emitted
-        for (size_t k = 0; k < st.size(); ++k) {
-            if (st[k].kind != FwdStmt::Agg || !plainAgg_.count(st[k].a)) continue;
-            // prologue, walking back: [Mul(act, X)] [Relu] [Mul(pre, res | X)]
-            size_t j = k;
-            std::string X = "res", act, pre, post;
-            bool relu = false;
-            if (j > done && st[j - 1].kind == FwdStmt::Mul) {
-                pre = st[j - 1].a;
-                X = st[j - 1].b;
-                --j;
+    // One in-loop node and the forward entries [first, last) it emitted.
+    struct Span {
+        ComputeNode *node;
+        int first, last;
+        bool edgeUpdate;   // the base's hasFFNEdgeUpdate when the node was emitted (attention aggregation form)
+        int fcEdge;        // its fcEdgeCount then (an FFN_OP_EDGE's module is efc<fcEdge>)
+    };
+
+    // generateCode's node walk (common.h:1378-1442) with the base's generateOpCode, recording
+    // each in-loop node's forward entries.  Run on the state generateCode started from.
+    std::vector<Span> forwardSpans(std::vector<CIRNode *> &program, std::vector<TransformEdge *> &transforms) {
+        std::vector<int> inputSizes;
+        int fcCount = 0, fcEdgeCount = 0, fcSelfCount = 0, epCount = 0;
+        bool hasFFNEdgeUpdate = false, hasEdgeMulAggr = false;
+        std::unordered_set<std::string> autograds;
+        std::vector<Span> spans;
+        for (CIRNode *n : program) {
+            if (auto *c = dynamic_cast<ComputeNode *>(n)) {
+                generateOpCode(c, fcCount, fcEdgeCount, fcSelfCount, epCount, true, hasFFNEdgeUpdate, hasEdgeMulAggr,
+                               autograds, inputSizes, transforms);
+                continue;
             }
-            if (X == "res" && j > done && st[j - 1].kind == FwdStmt::Relu) {
-                relu = true;
-                --j;
-                if (j > done && st[j - 1].kind == FwdStmt::Mul) {
-                    act = st[j - 1].a;
-                    X = st[j - 1].b;
+            auto *loop = dynamic_cast<TrainingLoopNode *>(n);
+            for (int i = 0; loop && i < loop->getLoopNodeNum(); ++i) {
+                auto *c = dynamic_cast<ComputeNode *>(loop->getNode(i));
+                Span s{c, model.getForward()->getNum(), 0, hasFFNEdgeUpdate, fcEdgeCount};
+                generateOpCode(c, fcCount, fcEdgeCount, fcSelfCount, epCount, false, hasFFNEdgeUpdate, hasEdgeMulAggr,
+                               autograds, inputSizes, transforms);
+                s.last = model.getForward()->getNum();
+                spans.push_back(s);
+            }
+        }
+        return spans;
+    }
+
+    // the value a node's statement assigns, and its operand names, as the base spells them
+    std::string out(const Span &s) { return generateOutputString(s.node, false); }
+    static std::string in(const Span &s, int i) { return s.node->getInput(i)->getName(); }
+    static ComputeOp opOf(const Span &s) { return s.node->getOp(); }
+    static bool sampled(ComputeNode *c) {
+        for (auto &o : *c->getOpts())
+            if (o.first == SAMPLE_COPT || o.first == SAMPLE_DYNAMIC_COPT) return true;
+        return false;
+    }
+    // the slot an in-loop aggregation's autograd call takes: 0 on validation epochs, its graph's
+    // index otherwise (common.h:1003-1010; the index is a training subgraph's under gala_train)
+    static std::string slotExpr(int idx) {
+        return idx == 0 ? std::string("0") : "ep % mod_v == 0 ? 0 : " + std::to_string(idx);
+    }
+    // Is `name` still read after span `upto`?  Judged on the statements the forward holds
+    // after it (the base spells some operands independently of the node's inputs, e.g.
+    // FFN_OP_SELF's `res`): the first later statement that mentions the name must assign it
+    // without reading it, otherwise the value is live.
+    static bool mentions(const std::string &t, const std::string &name) {
+        auto ident = [](char c) { return std::isalnum((unsigned char)c) || c == '_'; };
+        for (size_t p = t.find(name); p != std::string::npos; p = t.find(name, p + 1))
+            if ((p == 0 || !ident(t[p - 1])) && (p + name.size() >= t.size() || !ident(t[p + name.size()]))) return true;
+        return false;
+    }
+    static bool readLater(Code &fwd, const std::vector<Span> &sp, size_t upto, const std::string &name) {
+        for (int e = sp[upto].last; e < fwd.getNum(); ++e) {
+            const std::string &t = *fwd.atLine(e);
+            if (!mentions(t, name)) continue;
+            const size_t a = t.find_first_not_of(" \t\n");
+            const std::string lhs = name + " = ";
+            if (a == std::string::npos || t.compare(a, lhs.size(), lhs) != 0) return true;
+            return mentions(t.substr(a + lhs.size()), name) || t.find(';', a) + 1 < t.size();
+        }
+        return false;
+    }
+    // the forward entries of spans [a, b] replaced by one statement
+    static void replaceSpans(Code &fwd, const std::vector<Span> &sp, size_t a, size_t b, const std::string &stmt) {
+        for (size_t i = a; i <= b; ++i)
+            for (int e = sp[i].first; e < sp[i].last; ++e) fwd.atLine(e)->clear();
+        *fwd.atLine(sp[a].first) = stmt;
+    }
+
+    // The base emits a GCN layer as torch ops around the aggregation's autograd class: ROW_
+    // BROADCAST `res = norm * x;`, NON_LINEARITY `res = torch::relu(res);`, the aggregation (an
+    // `if (ep % mod_v == 0)` pair of apply calls) and the ROW_BROADCAST after it
+    // (common.h:1003-1010, 1150-1184).  On config 5's 11 M rows each such torch op is a 5.7 GB
+    // pass (a ROW_BROADCAST 1.8 ms, a ReLU 2.9 ms, forward and backward alike).  A node chain
+    //     [ROW_BROADCAST(act, X)] [RELU] [ROW_BROADCAST(pre, .)] AGGREGATE_MUL_SUM [ROW_BROADCAST(post, .)]
+    // around an unsampled, unweighted aggregation (each node reading the previous one's
+    // value, the intermediate values read by nothing after the chain) becomes the mirror's
+    // fused op over the same slot,
+    //     res = gala::gcn_aggregate_relu_apply(X, act, pre, post, li);   (or gcn_aggregate_apply)
+    // whose forward and backward are the unfused chain's roundings bit for bit (the ROW_
+    // BROADCASTs in the aggregation's prologue / epilogue, relu as torch's GPU kernel).  li
+    // keeps the base's choice of slot per epoch (a training subgraph's off validation epochs).
+    void fuseGcnChains(Code &fwd, const std::vector<Span> &sp) {
+        size_t done = 0;   // spans [0, done) are taken
+        for (size_t k = 0; k < sp.size(); ++k) {
+            const Span &ag = sp[k];
+            if (opOf(ag) != AGGREGATE_MUL_SUM_OP || ag.edgeUpdate || sampled(ag.node) || ag.last == ag.first) continue;
+            // the longest chain first; a ReLU whose output is still read later stays unfused
+            for (bool withRelu : {true, false}) {
+                size_t j = k;
+                std::string X = in(ag, 0), act, pre, post;
+                bool relu = false;
+                std::vector<std::string> inner;   // values the chain writes before its last node
+                if (j > done && opOf(sp[j - 1]) == ROW_BROADCAST_OP && out(sp[j - 1]) == X) {
+                    pre = in(sp[j - 1], 0);
+                    inner.push_back(X);
+                    X = in(sp[j - 1], 1);
                     --j;
                 }
+                if (withRelu && j > done && opOf(sp[j - 1]) == NON_LNR_OP_RELU && out(sp[j - 1]) == X) {
+                    relu = true;
+                    inner.push_back(X);
+                    X = in(sp[j - 1], 0);
+                    --j;
+                    if (j > done && opOf(sp[j - 1]) == ROW_BROADCAST_OP && out(sp[j - 1]) == X) {
+                        act = in(sp[j - 1], 0);
+                        inner.push_back(X);
+                        X = in(sp[j - 1], 1);
+                        --j;
+                    }
+                }
+                size_t last = k;
+                if (k + 1 < sp.size() && opOf(sp[k + 1]) == ROW_BROADCAST_OP && in(sp[k + 1], 1) == out(ag)) {
+                    post = in(sp[k + 1], 0);
+                    inner.push_back(out(ag));
+                    last = k + 1;
+                }
+                if (!relu && pre.empty() && post.empty()) break;   // nothing to fuse: as emitted
+                const std::string res = out(sp[last]);
+                bool dead = true;
+                for (const std::string &v : inner)
+                    dead = dead && (v == res || !readLater(fwd, sp, last, v));
+                if (!dead) continue;
+                const int idx = ag.node->getInput(1)->getDataInfo()->getIndex();
+                auto arg = [](const std::string &v) { return v.empty() ? std::string("torch::Tensor()") : v; };
+                std::string stmt = "\n        // ROW_BROADCAST / RELU / AGGREGATE / ROW_BROADCAST fused (HIPGenerator)\n        " + res;
+                if (relu)
+                    stmt += " = gala::gcn_aggregate_relu_apply(" + X + ", " + arg(act) + ", " + arg(pre) + ", " + arg(post) +
+                            ", " + slotExpr(idx) + ");";
+                else
+                    stmt += " = gala::gcn_aggregate_apply(" + X + ", " + arg(pre) + ", " + arg(post) + ", " + slotExpr(idx) + ");";
+                replaceSpans(fwd, sp, j, last, stmt);
+                done = last + 1;
+                k = last;
+                break;
             }
-            size_t last = k;   // epilogue: Mul(post, res)
-            if (k + 1 < st.size() && st[k + 1].kind == FwdStmt::Mul && st[k + 1].b == "res") {
-                post = st[k + 1].a;
-                last = k + 1;
-            }
-            if (!relu && pre.empty() && post.empty()) continue;   // nothing to fuse: as emitted
-            for (size_t i = done; i < j; ++i) out += st[i].text;
-            const std::string none = "torch::Tensor()";
-            auto arg = [&](const std::string &v) { return v.empty() ? none : v; };
-            out += "\n        // ROW_BROADCAST / RELU / AGGREGATE / ROW_BROADCAST fused (HIPGenerator)\n";
-            if (relu)
-                out += "        res = gala::gcn_aggregate_relu_apply(" + X + ", " + arg(act) + ", " + arg(pre) + ", " +
-                       arg(post) + ", " + st[k].b + ");";
-            else
-                out += "        res = gala::gcn_aggregate_apply(" + X + ", " + arg(pre) + ", " + arg(post) + ", " +
-                       st[k].b + ");";
-            done = last + 1;
-            k = last;
         }
-        for (size_t i = done; i < st.size(); ++i) out += st[i].text;
-        *fwd.atLine(0) = out;
-        for (int i = 1; i < fwd.getNum(); ++i) fwd.atLine(i)->clear();
     }
 
     // The base emits a GAT layer (common.h:622-894, 1175-1184) as four steps over E-long
@@ -549,88 +612,62 @@ private:
     // (torch exp / clamp / reciprocal around K7 and K8) and the attention-weighted aggregation
     // class -- with their backwards (K9, the softmax backward's torch ops around K7 / K8, K7 for
     // the logits' gradient): on the Products shape 30.8 ms per epoch where galac's fused layer
-    // takes 20.8 (profiles/r05_refgen_gat_products.jsonl).  The chain
-    //     attn = aggregate_edge_sum_AutoGrad::apply(L, R, li);  [LeakyReLU declaration]
-    //     attn = leaky_relu->forward(attn);  attn = non_lnr_op_softmax_AutoGrad::apply(attn, li);
-    //     AGG(X, attn, li)   (the `if (ep % mod_v == 0)` pair)
-    // becomes the mirror's fused layer over the same slot in REF mode,
-    //     res = gala::gat_aggregate_apply(L, R, X, li, slope, GALA_SOFTMAX_REF);
+    // takes 20.8 (profiles/r05_refgen_gat_products.jsonl).  The node chain
+    //     AGGREGATE_EDGE_SUM(L, R, graph) -> LEAKY_RELU -> SOFTMAX -> AGGREGATE_MUL_SUM(X, attn)
+    // (the aggregation in the base's attention form, every node on slot 0, `attn` read by
+    // nothing after the chain) becomes the mirror's fused layer over the same slot in REF mode,
+    //     res = gala::gat_aggregate_apply(L, R, X, li, 0.2, GALA_SOFTMAX_REF);
     // (the same chain of operations per edge, one pass per row; alpha = p * q with the
     // reference's clamp, 1e-12 and sequential row sums; gradients d aL = d aR = the row sums of
-    // the LeakyReLU'd softmax gradient, as the base's classes return them).  When R is
-    // `gala::head_attn_apply(X, W->weight, W->bias)` of the aggregated rows themselves, the
-    // layer recomputes it from the rows it gathers (gat_aggregate_ffn_apply, galac's spelling)
-    // and the statement goes when nothing else reads R.  The values are the chain's within
-    // fp32 rounding, not bit for bit: the fused kernels sum in the chain's order but round
-    // alpha = p * q once per edge where the chain stores it (tests/test_gpu_refgen.py checks
-    // the program against galac's IR in float64 at 1e-4; GALA_REFGEN_UNFUSED keeps the base's
-    // spelling).
-    void fuseGatChains(Code &fwd) {
-        std::string t;
-        for (int i = 0; i < fwd.getNum(); ++i) t += *fwd.atLine(i) + "\n";
-        std::vector<FwdStmt> st = splitForward(t);
-        static const std::regex word_attn("\\battn\\b");
-        auto mentions = [](const std::string &text, const std::string &name) {
-            return std::regex_search(text, std::regex("\\b" + name + "\\b"));
-        };
-        std::vector<bool> drop(st.size(), false);
-        std::vector<std::string> repl(st.size());
-        std::string slope = "0.2";
-        bool any = false;
-        for (size_t k = 0; k < st.size(); ++k) {
-            if (st[k].kind == FwdStmt::LeakyDecl) slope = st[k].a;
-            if (st[k].kind != FwdStmt::AttnAgg || !plainAgg_.count(st[k].a) || k < 3) continue;
-            const std::string li = st[k].b, X = st[k].c;
-            if (st[k - 1].kind != FwdStmt::Softmax || st[k - 1].b != li || st[k - 2].kind != FwdStmt::Leaky) continue;
-            size_t e = k - 3;
-            if (st[e].kind == FwdStmt::LeakyDecl) {   // kept: later layers use the variable
-                if (e == 0) continue;
-                --e;
-            }
-            if (st[e].kind != FwdStmt::EdgeSum || st[e].c != li) continue;
-            // `attn` must not be read after the chain before it is assigned again
-            bool attn_dead = true;
-            for (size_t i = k + 1; i < st.size(); ++i) {
-                if (!std::regex_search(st[i].text, word_attn)) continue;
-                attn_dead = st[i].kind == FwdStmt::EdgeSum;
-                break;
-            }
-            if (!attn_dead) continue;
-            const std::string L = st[e].a, R = st[e].b;
-            // R = head_attn_apply(X, W->weight, W->bias) just before, with only other attention
-            // Linears (not assigning X) in between
+    // the LeakyReLU'd softmax gradient, as the base's classes return them; the slope is the
+    // base's LeakyReLU module's, 0.2 whatever the node's parameter, common.h:1180).  When R is
+    // the FFN_OP_EDGE of the aggregated rows X themselves (efcN, emitted as the head-attention
+    // op), the layer recomputes it from the rows it gathers (gat_aggregate_ffn_apply, galac's
+    // spelling) and R's statement goes when nothing else reads R.  The values are the chain's
+    // within fp32 rounding, not bit for bit: the fused kernels sum in the chain's order but
+    // round alpha = p * q once per edge where the chain stores it (tests/test_gpu_refgen.py
+    // checks the program against galac's IR in float64 at 1e-4 and against the base's spelling,
+    // GALA_REFGEN_UNFUSED).
+    void fuseGatChains(Code &fwd, const std::vector<Span> &sp) {
+        for (size_t k = 3; k < sp.size(); ++k) {
+            const Span &ag = sp[k], &sm = sp[k - 1], &lr = sp[k - 2], &es = sp[k - 3];
+            if (opOf(ag) != AGGREGATE_MUL_SUM_OP || !ag.edgeUpdate || sampled(ag.node) || ag.last == ag.first) continue;
+            if (opOf(sm) != NON_LNR_OP_SOFTMAX || out(sm) != "attn") continue;   // the aggregation reads `attn`
+            if (opOf(lr) != NON_LNR_OP_LEAKY_RELU || out(lr) != in(sm, 0)) continue;
+            if (opOf(es) != AGGREGATE_EDGE_SUM_OP || out(es) != in(lr, 0)) continue;
+            if (ag.node->getInput(1)->getDataInfo()->getIndex() != 0 || es.node->getInput(2)->getDataInfo()->getIndex() != 0)
+                continue;   // a subgraph slot off validation epochs: the base's spelling
+            bool dead = !readLater(fwd, sp, k, "attn");
+            for (const std::string &v : {out(es), out(lr)})
+                dead = dead && (v == "attn" || !readLater(fwd, sp, k, v));
+            if (!dead) continue;
+            const std::string X = in(ag, 0), L = in(es, 0), R = in(es, 1);
+            // R = efcN(X) just before, with only other attention Linears (not assigning X) between
             long h = -1;
-            for (long i = (long)e - 1; i >= 0; --i) {
-                if (st[i].kind != FwdStmt::HeadAttn || st[i].b == X) break;
-                if (st[i].b == R) {
-                    if (st[i].a == X) h = i;
+            for (long i = (long)k - 4; i >= 0; --i) {
+                if (opOf(sp[i]) != FFN_OP_EDGE || out(sp[i]) == X) break;
+                if (out(sp[i]) == R) {
+                    if (in(sp[i], 0) == X) h = i;
                     break;
                 }
             }
-            std::string rest;
-            for (size_t i = k + 1; i < st.size(); ++i) rest += st[i].text;
+            const std::string res = out(ag), head = "\n        // EDGE SUM / LEAKY RELU / SOFTMAX / AGGREGATE fused (HIPGenerator)\n        ";
             std::string call;
             if (h >= 0 && R != L) {
-                const std::string W = st[h].c;
-                call = "res = gala::gat_aggregate_ffn_apply(" + L + ", " + X + ", " + W + "->weight, " + W + "->bias, " +
-                       li + ", " + slope + ", GALA_SOFTMAX_REF);";
-                if (!mentions(rest, R)) drop[h] = true;
+                const std::string W = "efc" + std::to_string(sp[h].fcEdge);
+                call = res + " = gala::gat_aggregate_ffn_apply(" + L + ", " + X + ", " + W + "->weight, " + W +
+                       "->bias, 0, 0.2, GALA_SOFTMAX_REF);";
+                if (!readLater(fwd, sp, k, R))
+                    for (int e = sp[h].first; e < sp[h].last; ++e) fwd.atLine(e)->clear();
             } else {
-                call = "res = gala::gat_aggregate_apply(" + L + ", " + R + ", " + X + ", " + li + ", " + slope +
-                       ", GALA_SOFTMAX_REF);";
+                call = res + " = gala::gat_aggregate_apply(" + L + ", " + R + ", " + X + ", 0, 0.2, GALA_SOFTMAX_REF);";
             }
-            repl[e] = "\n        // EDGE SUM / LEAKY RELU / SOFTMAX / AGGREGATE fused (HIPGenerator)\n        " + call;
-            drop[k - 2] = drop[k - 1] = drop[k] = true;
-            any = true;
+            // the LeakyReLU module's declaration (the span's first entry when it has two) stays:
+            // later layers' calls use the variable
+            const std::string decl = lr.last - lr.first == 2 ? *fwd.atLine(lr.first) : std::string();
+            replaceSpans(fwd, sp, k - 3, k, head + call);
+            if (!decl.empty()) *fwd.atLine(lr.first) = decl;
         }
-        if (!any) return;
-        std::string out;
-        for (size_t i = 0; i < st.size(); ++i) {
-            if (!repl[i].empty()) out += repl[i];
-            else if (!drop[i]) out += st[i].text;
-        }
-        *fwd.atLine(0) = out;
-        for (int i = 1; i < fwd.getNum(); ++i) fwd.atLine(i)->clear();
     }
 
     // The training loop's loss (common.h:1506-1560): the training rows by index_select over

@@ -63,6 +63,7 @@ struct Spec {
     bool sparse = false;  // G.is_sparser(true)
     float power = -0.5f;
     int layers = 2;
+    int validation = 1;   // m1.train(validation_step=): the loop's stepValid (frontend.y:1089)
     bool relu(int l) const { return l + 1 < layers; }  // nonln_fn on every layer but the output
     int width(int l) const { return l + 1 < layers ? hidden : labels; }
 };
@@ -154,7 +155,7 @@ DataNode *reluNode(TrainingLoopNode *loop, int width, DataNode *in) {
 void buildGcn(const Spec &s) {
     DataNode *feat = nullptr;
     DataNode *graph = loadProgram(s, feat);
-    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, s.validation);
     DataNode *norm = nullptr, *prev = feat;
     for (int l = 0; l < s.layers; ++l) {
         if (l == 0 && s.nsamp) {  // GET_DEGREES of a kernel-sampled program: nsamp per row
@@ -238,7 +239,7 @@ DataNode *edgeNode(const Spec &s, bool tiled_derived) {
 void buildGat(const Spec &s) {
     DataNode *feat = nullptr;
     DataNode *graph = loadProgram(s, feat);
-    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, s.validation);
     DataNode *prev = feat;
     for (int l = 0; l < s.layers; ++l) {
         // FEED_FORWARD_NN
@@ -282,7 +283,7 @@ void buildGat(const Spec &s) {
 void buildGin(const Spec &s) {
     DataNode *feat = nullptr;
     DataNode *graph = loadProgram(s, feat);
-    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, s.validation);
     DataNode *prev = feat;
     for (int l = 0; l < s.layers; ++l) {
         const int in = l == 0 ? s.feat : s.hidden;
@@ -319,7 +320,7 @@ void buildGin(const Spec &s) {
 void buildSage(const Spec &s) {
     DataNode *feat = nullptr;
     DataNode *graph = loadProgram(s, feat);
-    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, 1);
+    auto *loop = new TrainingLoopNode(s.iterations, CROSS_ENTROPY, ADAM, s.validation);
     DataNode *norm = nullptr, *prev = feat;
     for (int l = 0; l < s.layers; ++l) {
         const int in = l == 0 ? s.feat : s.hidden;
@@ -401,7 +402,11 @@ int main(int argc, char **argv) {
         return 2;
     }
     s.sparse = s.model == "gat";  // the tests/GALA-DSL/gat schedule's is_sparser(true)
-    const bool motion = std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
+    // GALA_REFGEN_TRAIN: gala_train's whole pass set (tests/gala_train.cpp:124-146): operator
+    // reordering, sparse rewrites, training-invariant code motion and the training subgraph
+    const bool train = std::getenv("GALA_REFGEN_TRAIN") != nullptr;
+    const bool motion = train || std::getenv("GALA_REFGEN_CODE_MOTION") != nullptr;
+    if (train) s.validation = 5;   // the corpus's validation_step=5 (tests/GALA-DSL/*)
     if (s.model == "gcn" || s.model == "gcn3") {  // gcn3: three layers (config 5's GCN-3, the
         s.layers = s.model == "gcn3" ? 3 : 2;        // tests/GALA-DSL/ablations/scalability shape)
         buildGcn(s);
@@ -430,6 +435,9 @@ int main(int argc, char **argv) {
     if (motion)  // gala_train's third pass (tests/gala_train.cpp:136-140)
         GALATransformations::trainingInvariantCodeMotion(GALAFEContext::program, GALAFEContext::dependencies,
                                                          GALAFEContext::associations, GALAFEContext::transforms);
+    if (train)  // gala_train's fourth pass (tests/gala_train.cpp:142-146)
+        GALATransformations::trainingSubGraph(GALAFEContext::program, GALAFEContext::dependencies,
+                                              GALAFEContext::associations, GALAFEContext::transforms);
     gen.writeCode(GALAFEContext::program, GALAFEContext::dependencies, GALAFEContext::associations,
                   GALAFEContext::transforms);
     std::cout << "wrote " << out << "gala.cu and " << out << "CMakeLists.txt" << std::endl;

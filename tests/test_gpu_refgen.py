@@ -24,7 +24,8 @@ BIN = os.path.join(rc.PKG, "refgen", "bin")
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("model", ["gcn", "gcn3", "gcn3_papers", "gcn_ksample", "gcn_dsample", "gat", "gat_unfused", "gin",
-                                   "gin_motion", "sage"])
+                                   "gin_motion", "sage", "gcn_train", "gcn3_train", "gat_train", "gin_train",
+                                   "sage_train"])
 def test_reference_emitted_program_on_the_gpu(tmp_path, model):
     """gat_unfused: the base's spelling of the GAT edge chain (its own autograd classes over the
     mirror's edge operators), gat: HIPGenerator's fused layer; both against galac's IR."""
@@ -47,7 +48,7 @@ def test_reference_emitted_program_on_the_gpu(tmp_path, model):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("model", ["gcn3", "gcn3_papers"])
+@pytest.mark.parametrize("model", ["gcn3", "gcn3_papers", "gin", "sage", "gcn3_train"])
 def test_fused_gcn_chains_bit_identical_to_the_base_spelling(tmp_path, model):
     """HIPGenerator's fused GCN chains (gcn_aggregate[_relu]_apply in place of the base's torch
     ROW_BROADCAST / ReLU ops around the aggregation, common.h:928-978,1150-1184) and its loss
@@ -69,3 +70,29 @@ def test_fused_gcn_chains_bit_identical_to_the_base_spelling(tmp_path, model):
             np.testing.assert_allclose(d1[k], d0[k], rtol=1e-6, atol=0)
         else:
             np.testing.assert_array_equal(d1[k], d0[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_fused_gat_chain_against_the_base_spelling(tmp_path):
+    """HIPGenerator's fused GAT layer (gat_aggregate[_ffn]_apply in place of the base's edge sum,
+    LeakyReLU, softmax and attention-weighted aggregation classes, common.h:622-894) beside the
+    base's spelling over the mirror's K5 / K7 / K8 / K9 operators (GALA_REFGEN_UNFUSED), same
+    seed: the fused kernels sum each row in the chain's order but round alpha = p * q once per
+    edge where the chain stores it, so the first epoch's prediction, loss and weight gradients
+    agree to fp32 rounding (1e-5 relative to each tensor's largest entry), not bit for bit."""
+    import numpy as np
+    exe, exe0 = (os.path.join(BIN, "gala_" + m) for m in ("gat", "gat_unfused"))
+    if not (os.path.exists(exe) and os.path.exists(exe0)):
+        pytest.skip("refgen programs not built (refgen/build.py needs the reference's sources)")
+    rc.dataset(tmp_path, n=20000, nnz=240000, feat=64, labels=7, seed=11)
+    d1 = rc.run_program(exe, str(tmp_path), "cuda", seed=7)
+    d0 = rc.run_program(exe0, str(tmp_path), "cuda", seed=7)
+    assert set(d1) == set(d0)
+    top = max(np.abs(v).max() for k, v in d0.items() if k.endswith(".grad"))
+    for k in d0:
+        scale = np.abs(d0[k]).max()
+        # gradients: 1e-5 of the tensor's largest entry plus 1e-6 of the model's (the attention
+        # biases' gradients are cancellation noise, see tests/_refgen_check.py)
+        tol = 1e-5 * scale + (1e-6 * top if k.endswith(".grad") else 0)
+        assert np.abs(d1[k] - d0[k]).max() <= tol, (k, np.abs(d1[k] - d0[k]).max(), tol)

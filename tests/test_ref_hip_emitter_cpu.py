@@ -46,6 +46,12 @@ CASES = {
     "gin": ["64", "7", "32", "3", "2"],
     "gin_motion": ["64", "7", "32", "3", "2"],
     "sage": ["64", "7", "32", "3", "2"],
+    # gala_train's whole pass set (refgen/build.py's *_train programs): the training subgraph
+    "gcn_train": ["64", "7", "32", "3", "2"],
+    "gcn3_train": ["64", "7", "32", "3", "2", "300"],
+    "gat_train": ["64", "7", "32", "3", "2", "200"],
+    "gin_train": ["64", "7", "32", "3", "2"],
+    "sage_train": ["64", "7", "32", "3", "2"],
 }
 
 
@@ -86,13 +92,35 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
     fwd = src[src.index("forward(torch::Tensor t_iden"):]
     # the GCN layers' ROW_BROADCAST / ReLU / aggregation chains run as the mirror's fused op
     # (the kernel-sampled program keeps the base's spelling), the loss as log_softmax + gather
-    fused = model in ("gcn", "gcn3", "gcn3_papers", "gcn_dsample")
+    fused = model in ("gcn", "gcn3", "gcn3_papers", "gcn_dsample", "gcn_train", "gcn3_train", "sage", "sage_train")
     assert ("gala::gcn_aggregate" in fwd) == fused
     assert "gala_cross_entropy(prediction_train, labels_train)" in src and "CrossEntropyLoss()" not in src
 
     def agg(s):   # the first aggregation of the forward, in either spelling
         return min(s.index(k) for k in ("_AutoGrad::apply", "gala::gcn_aggregate") if k in s)
-    if model in ("gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gin"):
+    if model.endswith("_train"):
+        # gala_train's training subgraph: the reference's host code builds the mask subgraphs
+        # (common.h:480-490) and HIPGenerator transfers each graph slot once
+        L = 3 if model == "gcn3_train" else 2
+        assert f"getMaskSubgraphs(&adj0, &train_mask, {L}, forward_adj, backward_adj);" in src
+        assert src.count("torch::Tensor t_offsets0 =") == 1
+        for g in range(1, L + 1):
+            assert src.count(f"torch::Tensor t_offsets{g} =") == 1 and src.count(f"torch::Tensor t_offsets{g}_b =") == 1
+        if model != "gat_train":   # code motion hoisted the first aggregation (on slot 0)
+            assert "_AutoGrad::apply(t_iden, 0);" in src
+        if model in ("gcn_train", "gcn3_train"):
+            # each in-loop layer's chain is one fused op whose slot is the base's per-epoch choice
+            # (a mask subgraph's off validation epochs)
+            for g in range(2, L + 1):
+                assert f"gala::gcn_aggregate_relu_apply(res, torch::Tensor(), norm, norm, ep % mod_v == 0 ? 0 : {g});" in fwd
+        elif model == "sage_train":
+            assert "res_n = gala::gcn_aggregate_apply(res, torch::Tensor(), norm, ep % mod_v == 0 ? 0 : 2);" in fwd
+        elif model == "gat_train":
+            # the reference's pass put the attention aggregation's edge values on a subgraph slot:
+            # the edge chain is not one slot's, so it keeps the base's spelling
+            assert "apply(res, attn, 1);" in fwd and "aggregate_edge_sum_AutoGrad::apply(attenL, attenR, 0);" in fwd
+            assert "gala::gat_aggregate" not in fwd
+    elif model in ("gcn", "gcn3", "gcn_ksample", "gcn_dsample", "gin"):
         # operator reordering ran (the reference's middle-end): both FFNs before their aggregation
         assert fwd.index("fc0->weight") < agg(fwd)
         if model == "gcn_ksample":
@@ -116,6 +144,9 @@ def test_hip_generator_emits_a_program_matching_galac(tmp_path, programs, model)
         # code motion ran: the first layer's mean aggregation is hoisted out of the training loop
         assert "torch::Tensor t_iden_n = aggregate_node_mul_sum_coarse2_AutoGrad::apply(t_iden, 0);" in src
         assert fwd.index("gala::ffn_apply(t_iden_n, fc0->weight, fc0->bias)") < fwd.index("sfc0->weight")
+        # the second layer's mean aggregation and its ROW_BROADCAST fused; its ReLU stays a torch
+        # op (the self FFN reads the ReLU's output)
+        assert "res_n = gala::gcn_aggregate_apply(res, torch::Tensor(), norm, 0);" in fwd and "torch::relu(res)" in fwd
     else:
         # the edge chain of each layer (edge sum, LeakyReLU, softmax, aggregation: the base's
         # classes, which the program still defines) runs as the mirror's fused layer in REF
