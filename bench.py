@@ -212,14 +212,45 @@ def gat_cpu_baseline(hg, X, dY, aL, wR, bR, heads, budget_s: float = 12.0):
                       "oracle orc_gat_ref_layer: the reference's GAT pass sequence restated, OpenMP"}
 
 
+# the sources a kernel's machine code comes from (its .hip file, the shared headers, the ABI)
+_KERNEL_SOURCES = (("k_gat_in_", "gat_input.hip"), ("k_gat_bwd_fused", "gat_fused.hip"), ("k_gat_", "gat.hip"),
+                   ("k_spmm_", "spmm.hip"), ("k_rows", "spmm.hip"), ("k_degree", "spmm.hip"))
+_COMMON_SOURCES = ("gala_internal.h", "edge_common.h", "gat_common.h")
+
+
+def _sources_fresh(kernel: str, recorded: dict) -> bool:
+    """Do the kernel's sources in this tree still have the digests its PMC pass recorded?"""
+    import hashlib
+    files = [f for key, f in _KERNEL_SOURCES if key in kernel][:1] + list(_COMMON_SOURCES)
+    if not recorded or len(files) == len(_COMMON_SOURCES):
+        return False
+    for f in files:
+        rel = os.path.join("gala-gnn-acceleration-language_amd", "csrc", f)
+        try:
+            now = hashlib.sha256(open(os.path.join(ROOT, rel), "rb").read()).hexdigest()
+        except OSError:
+            return False
+        if recorded.get(rel) != now:
+            return False
+    return True
+
+
+TRAFFIC_STALE = []   # kernels whose committed PMC bytes predate their current sources
+
+
 def load_traffic(kernel_substr: str):
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary
+    (profiles/traffic.json), or None when the kernel's sources changed since that PMC pass
+    (the summary records their sha256): a stale byte count is never reported."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(path))
         for k, v in d.get("kernels", {}).items():
             # "banded|" / "rmat|" entries are another graph's launches of the same kernel
             if kernel_substr in k and ("|" in kernel_substr or "|" not in k):
+                if not _sources_fresh(k, v.get("sources_sha256")):
+                    TRAFFIC_STALE.append(kernel_substr)
+                    return None
                 return float(v["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -842,7 +873,8 @@ def run_single(args, dev, be, timer, sync):
                      "kernel": "gala::k_spmm_rowgroup<VEC=4,G=8,CH=1,U=4,unweighted> (gala_spmm_f32, F=32, dst norm)",
                      "kernel_ms": t_kernel * 1e3, "alg_bytes_per_launch": alg,
                      "gather_model_GBps": gather_bytes / t_kernel / 1e9,
-                     "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json); "
+                     "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json, null when the kernel's "
+                                     "sources changed since that pass); "
                                      "uniform random columns: each edge's 128-B X row misses L2"},
     }
     with_traffic_rate(out["roofline"])
@@ -1161,6 +1193,8 @@ def main():
         out = run_single(args, dev, be, timer, sync)
     if dev.type == "cpu":
         out["device"] = "cpu (host-CPU backend plumbing run; not a GPU measurement)"
+    if TRAFFIC_STALE:   # PMC bytes withheld: the kernel changed since profiles/traffic.json's pass
+        out["traffic_withheld_stale"] = sorted(set(TRAFFIC_STALE))
     if rank == 0:
         os.write(result_fd, (json.dumps(out) + "\n").encode())
     if distributed:

@@ -10,10 +10,24 @@ for 128-B requests), so fetch bytes are reported raw and x2; WRITE_SIZE is exact
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "gala-gnn-acceleration-language_amd", "csrc")
+
+
+def source_digests():
+    """sha256 of every kernel source and header the PMC pass ran (bench.py reports a kernel's
+    traffic only while the digests of its sources still match)."""
+    out = {}
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h"))
+                    + [os.path.join(ROOT, "include", "gala_hip.h")]):
+        out[os.path.relpath(f, ROOT)] = hashlib.sha256(open(f, "rb").read()).hexdigest()
+    return out
 
 
 def read_counter(d, name):
@@ -31,6 +45,7 @@ def main():
     fdir, wdir, out = sys.argv[1:4]
     fetch = read_counter(fdir, "FETCH_SIZE")
     write = read_counter(wdir, "WRITE_SIZE")
+    digests = source_digests()
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB -> bytes",
            "correction": "hbm_bytes_per_launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
            "kernels": {}}
@@ -42,7 +57,7 @@ def main():
         fm = f[len(f) // 2] * 1024
         wm = w[len(w) // 2] * 1024
         res["kernels"][k] = {"launches": len(f), "fetch_bytes_raw": fm, "write_bytes": wm,
-                             "hbm_bytes_per_launch": 2 * fm + wm}
+                             "hbm_bytes_per_launch": 2 * fm + wm, "sources_sha256": digests}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
