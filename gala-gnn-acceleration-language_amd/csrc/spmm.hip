@@ -15,7 +15,6 @@
 // flight.  All address arithmetic is 64-bit.
 #include <stddef.h>
 #include <cstdlib>
-#include <type_traits>
 
 #include "gala_internal.h"
 
@@ -341,24 +340,6 @@ __device__ __forceinline__ void store_row(const SpmmParams &p, const Cols<VEC, G
     }
 }
 
-#ifdef GALA_HUB_TRACE
-// measurement build only (tools/hub_trace.py): wall-clock stamps (100 MHz) of the REF hub
-// kernel's first workgroups, its first start / last end, the row kernel's, and the longest
-// chain's progress
-__device__ unsigned long long g_hub_trace[64];
-extern "C" int gala_dbg_hub_trace(unsigned long long *out, int reset) {
-    if (reset) {
-        unsigned long long init[64];
-        for (int i = 0; i < 64; ++i) init[i] = (i == 16 || i == 18) ? ~0ULL : 0ULL;
-        return hipMemcpyToSymbol(HIP_SYMBOL(g_hub_trace), init, sizeof(init)) != hipSuccess;
-    }
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hub_trace), 64 * sizeof(unsigned long long)) != hipSuccess;
-}
-#define GALA_TRACE(...) __VA_ARGS__
-#else
-#define GALA_TRACE(...)
-#endif
-
 // the rows of row block `bid` of `nb` (skipping hub rows)
 template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 __device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid, int64_t nb) {
@@ -394,9 +375,7 @@ __device__ __forceinline__ void spmm_row_block(const SpmmParams &p, int64_t bid,
 
 template <int VEC, int G, int CH, int U, bool W, bool SAMP, bool SRCS, bool RELU = false>
 __global__ __launch_bounds__(kBlock) void k_spmm_rowgroup(SpmmParams p) {
-    GALA_TRACE(if (threadIdx.x == 0 && blockIdx.x == 0) g_hub_trace[18] = wall_clock64());
     spmm_row_block<VEC, G, CH, U, W, SAMP, SRCS, RELU>(p, blockIdx.x, gridDim.x);
-    GALA_TRACE(if (threadIdx.x == 0 && blockIdx.x + 1 == gridDim.x) g_hub_trace[19] = wall_clock64());
 }
 
 // ---- split rows: chunk partials + ordered fix-up ---------------------------------------
@@ -501,16 +480,6 @@ constexpr int kHubThreads = 512;
 constexpr int kHubGather = kHubThreads - kWave;  // gatherer lanes
 constexpr int kHubBuf = 8192;      // floats of X per LDS buffer (32 KB; two buffers)
 constexpr int kHubMaxHeads = 4;    // edge-weight heads per slice staged in LDS
-#ifndef GALA_HUB_AHEAD
-#define GALA_HUB_AHEAD 1
-#endif
-#ifndef GALA_HUB_PRIO_C
-#define GALA_HUB_PRIO_C 0
-#endif
-#ifndef GALA_HUB_PRIO_G
-#define GALA_HUB_PRIO_G 0
-#endif
-constexpr int kHubAhead = GALA_HUB_AHEAD;   // register stages of gathered tiles (1 or 2)
 
 struct HubParams {
     const int32_t *rows;           // hub row ids
@@ -519,7 +488,8 @@ struct HubParams {
     int32_t n_slices;              // ceil(F / FSP)
 };
 
-// LDS: buf[2][T/4][FSP][4] (X; an edge quad of one feature is one 16-B read), scl[2][T]
+// LDS: buf[2][T/4][FSP][4] (X; an edge quad of one feature is one 16-B read; feature f in
+// slot (f % VEC) * (FSP / VEC) + f / VEC of the quad's row), scl[2][T]
 // (SRCS), wts[2][kHubMaxHeads][T] (W), yinit[64], then slack the chain's prefetch may read
 // past a buffer (never consumed).  Unweighted: 68 KB, two workgroups per CU.
 template <int FSP, bool W, bool SRCS>
@@ -539,10 +509,6 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     constexpr int RG = (T * (FSP / VEC) + kHubGather - 1) / kHubGather;  // loads per gatherer
     constexpr int RW = (T * kHubMaxHeads + kHubGather - 1) / kHubGather;
     extern __shared__ float hub_lds[];
-    GALA_TRACE(const unsigned long long t_in = wall_clock64();
-               if (threadIdx.x == 0) atomicMin(&g_hub_trace[16], t_in);
-               if (threadIdx.x == 0 && blockIdx.x < 8) g_hub_trace[2 * blockIdx.x] = t_in;
-               if (threadIdx.x == 0 && blockIdx.x == 0) { g_hub_trace[40] = clock64(); g_hub_trace[56] = t_in; });
     const int64_t ri = blockIdx.x / hp.n_slices;
     const int slice = blockIdx.x % hp.n_slices;
     // the plan's descending-degree row order starts with exactly the hub rows: the longest
@@ -561,10 +527,8 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     // ---- gatherers: slot k = (edge, column) of a tile, fixed for every tile ----
     int s_edge[RG], s_off[RG];
     int32_t cc[RG];
-    // register stages of gathered tiles: the gatherers' loads run kHubAhead tiles ahead of the
-    // stores the chain waits for
-    V xr[kHubAhead][RG];
-    float sr[kHubAhead][RG], wr[kHubAhead][RW];
+    V xr[RG];
+    float sr[RG], wr[RW];
 #pragma unroll
     for (int k = 0; k < RG; ++k) {
         const int i = k * kHubGather + g;
@@ -579,43 +543,46 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
             cc[k] = p.col[e0 + j];
         }
     };
-    // stage q (compile-time after unrolling) holds the tile whose index is q mod kHubAhead
-    auto load_x = [&](int t, auto q) {
+    auto load_x = [&](int t) {
         // unconditional (an unused slot's column is a valid one): branches around the
         // loads would make the compiler wait for each load before issuing the next
 #pragma unroll
         for (int k = 0; k < RG; ++k) {
-            xr[q][k] = ldv<VEC>(p.X + (int64_t)cc[k] * p.ldx + f0 + s_off[k]);
-            if (SRCS) sr[q][k] = p.src_scale[cc[k]];
+            xr[k] = ldv<VEC>(p.X + (int64_t)cc[k] * p.ldx + f0 + s_off[k]);
+            if (SRCS) sr[k] = p.src_scale[cc[k]];
         }
-        if constexpr (W) {  // weight (edge j, head h0 + k) for i = j * hs + k, coalesced along the edges
+        if (W) {  // weight (edge j, head h0 + k) for i = j * hs + k, coalesced along the edges
 #pragma unroll
             for (int k = 0; k < RW; ++k) {
                 const int i = k * kHubGather + g;
                 int64_t j = (int64_t)t * T + (hs > 0 ? i / hs : 0);
                 if (j >= n) j = n - 1;
-                wr[q][k] = p.val[(e0 + j) * p.val_heads + h0 + (hs > 0 ? i % hs : 0)];
+                wr[k] = p.val[(e0 + j) * p.val_heads + h0 + (hs > 0 ? i % hs : 0)];
             }
         }
     };
-    auto store = [&](int b, auto q) {
+    auto store = [&](int b) {
         float *xb = hub_lds + L::buf + (size_t)b * kHubBuf;
 #pragma unroll
         for (int k = 0; k < RG; ++k) {
             const int e = s_edge[k];
             if (e < 0) continue;
             // feature f = s_off + v sits in slot v * (FSP / VEC) + s_off / VEC of its edge quad's
-            // row: one store instruction's lanes then hit distinct banks
-            float *dq = xb + ((e >> 2) * FSP + s_off[k] / VEC) * 4 + (e & 3);
+            // row (the chain lane of feature f reads that slot): the lanes of one store
+            // instruction -- FSP / VEC features of 64 * VEC / FSP edges -- then fall on distinct
+            // banks, where slot f put every fourth lane of a row on one bank (a 4-way conflict
+            // on every gatherer store, stalling the chain's own LDS reads: the 388 K-edge R-MAT
+            // chain 2.06 -> 1.80 ms, profiles/r06_hub_clock_swizzle.jsonl)
+            float *q = xb + ((e >> 2) * FSP + s_off[k] / VEC) * 4 + (e & 3);
 #pragma unroll
-            for (int v = 0; v < VEC; ++v) dq[4 * v * (FSP / VEC)] = el<VEC>(xr[q][k], v);
-            if (SRCS && s_off[k] == 0) hub_lds[L::scl + b * T + e] = sr[q][k];
+            for (int v = 0; v < VEC; ++v) q[4 * v * (FSP / VEC)] = el<VEC>(xr[k], v);
+            if (SRCS && s_off[k] == 0) hub_lds[L::scl + b * T + e] = sr[k];
         }
-        if constexpr (W) {
+        if (W) {
 #pragma unroll
             for (int k = 0; k < RW; ++k) {
                 const int i = k * kHubGather + g;
-                if (i < T * hs) hub_lds[L::wts + (size_t)b * kHubMaxHeads * T + (i % hs) * T + i / hs] = wr[q][k];
+                if (i < T * hs) hub_lds[L::wts + (size_t)b * kHubMaxHeads * T + (i % hs) * T + i / hs] = wr[k];
             }
         }
     };
@@ -625,7 +592,7 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
     const bool chain = lane < fs;
     const int cl = chain ? lane : 0;
     const int f = f0 + cl;
-    const int slot = (cl % VEC) * (FSP / VEC) + cl / VEC;   // the store's slot of feature cl
+    const int slot = (cl % VEC) * (FSP / VEC) + cl / VEC;   // where the gatherers store feature cl
     const int hl = W ? f / p.head_dim - h0 : 0;
     const float rs = (W && p.val_rs) ? p.val_rs[row * p.val_heads + h0 + hl] : 1.0f;
     if (chain && p.accum && p.dst_scale == nullptr && !p.dst_deg) hub_lds[L::yinit + lane] = p.Y[row * p.ldy + f];
@@ -695,58 +662,33 @@ __global__ __launch_bounds__(kHubThreads) void k_spmm_hub_exact(SpmmParams p, Hu
             add(xs[(j >> 2) * FSP * 4 + (j & 3)], W ? wb[j] : 1.0f, SRCS ? sb[j] : 1.0f);
     };
 
-    // ---- pipeline: tile t in LDS buffer t&1 is added while tile t+1 is stored into the other;
-    // the gatherers' loads of tile t+1+kHubAhead are issued right after that store ----
-    using Q0 = std::integral_constant<int, 0>;
-    using Q1 = std::integral_constant<int, kHubAhead - 1>;   // stage of odd tiles
+    // ---- pipeline: tile t in buffer t&1 is added while tile t+1 is gathered into the other ----
     if (gatherer && ntiles > 0) {
         load_cols(0);
-        load_x(0, Q0{});
+        load_x(0);
         if (ntiles > 1) load_cols(1);
-        store(0, Q0{});
+        store(0);
         if (ntiles > 1) {
-            load_x(1, Q1{});
+            load_x(1);
             if (ntiles > 2) load_cols(2);
-        }
-        if (kHubAhead == 2 && ntiles > 2) {
-            load_x(2, Q0{});
-            if (ntiles > 3) load_cols(3);
         }
     }
     __syncthreads();
-    if (GALA_HUB_PRIO_C && !gatherer) __builtin_amdgcn_s_setprio(GALA_HUB_PRIO_C);
-    if (GALA_HUB_PRIO_G && gatherer) __builtin_amdgcn_s_setprio(GALA_HUB_PRIO_G);
     if (chain && p.accum && p.dst_scale == nullptr && !p.dst_deg) acc = hub_lds[L::yinit + lane];
-    // one step: store tile t+1 from its register stage, then reload that stage with tile
-    // t+1+kHubAhead (kHubAhead 1: stage 0 always; 2: even tiles in stage 0, odd in stage 1)
-    auto step = [&](int t, auto qs) {
+    for (int t = 0; t < ntiles; ++t) {
         if (gatherer) {
             if (t + 1 < ntiles) {
-                store((t + 1) & 1, qs);
-                if (t + 1 + kHubAhead < ntiles) {
-                    load_x(t + 1 + kHubAhead, qs);
-                    if (t + 2 + kHubAhead < ntiles) load_cols(t + 2 + kHubAhead);
+                store((t + 1) & 1);
+                if (t + 2 < ntiles) {
+                    load_x(t + 2);
+                    if (t + 3 < ntiles) load_cols(t + 3);
                 }
             }
         } else {
             run_chain(t);
-            GALA_TRACE(if (blockIdx.x == 0 && threadIdx.x == 0 && ntiles >= 8 && (t + 1) % (ntiles / 8) == 0 &&
-                           (t + 1) / (ntiles / 8) <= 8)
-                       { g_hub_trace[24 + (t + 1) / (ntiles / 8)] = wall_clock64();
-                         g_hub_trace[40 + (t + 1) / (ntiles / 8)] = clock64(); });
         }
         __syncthreads();
-    };
-    for (int t = 0; t < ntiles; t += 2) {
-        step(t, Q1{});                        // tile t+1 is odd
-        if (t + 1 < ntiles) step(t + 1, Q0{});
     }
-    GALA_TRACE(if (threadIdx.x == 0) {
-        const unsigned long long t_out = wall_clock64();
-        atomicMax(&g_hub_trace[17], t_out);
-        if (blockIdx.x < 8) g_hub_trace[2 * blockIdx.x + 1] = t_out;
-        if (blockIdx.x == 0) g_hub_trace[24] = (unsigned long long)ntiles;
-    });
     if (!chain) return;
     float out = acc;
     bool has_ds;
@@ -840,7 +782,6 @@ static void launch_hub_t(const SpmmParams &p, HubParams hp, hipStream_t st) {
 // slices of 32 features when F <= 32 (F = 32: one 128-B row per edge, 512 edges a tile),
 // else of 64 (one chain lane per feature of a wave)
 static void launch_hub(const SpmmParams &p, const HubParams &hp, int vec, bool w, bool srcs, hipStream_t st) {
-    if (hp.n_hub <= 0) return;
 #define GALA_HUB(V, S)                                                    \
     if (w) {                                                              \
         if (srcs) launch_hub_t<V, S, true, true>(p, hp, st);              \
@@ -1082,8 +1023,8 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         p.split_threshold = plan->threshold;
         sp = &spl;
     }
-    HubParams hp{}, hp_long{};
-    hipStream_t hub_st = hs, long_st = hs, row_st = hs;
+    HubParams hp{};
+    hipStream_t hub_st = hs;
     if (use_hub) {
         if (plan->threshold < 1 || !plan->rows) return GALA_ERR_INVALID_ARG;
         p.split_threshold = plan->threshold;  // the row kernel leaves hub rows to k_spmm_hub_exact
@@ -1092,18 +1033,6 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
         hp.n_hub = plan->n_rows_split;
         // the hub rows run beside the row kernel on the plan's side stream when it has one
         if (plan->aux_stream && plan->aux_events[0] && plan->aux_events[1]) hub_st = (hipStream_t)plan->aux_stream;
-        // ABI 6: the longest chains (the order's first n_long rows) on long_stream's CUs, the
-        // row kernel on row_stream (the host keeps those off long_stream's CUs)
-        if (hub_st != hs && plan->row_order && plan->n_long > 0 && plan->long_stream && plan->row_stream &&
-            plan->join_events[0] && plan->join_events[1]) {
-            if (plan->n_long > plan->n_rows_split) return GALA_ERR_INVALID_ARG;
-            long_st = (hipStream_t)plan->long_stream;
-            row_st = (hipStream_t)plan->row_stream;
-            hp_long = hp;
-            hp_long.n_hub = plan->n_long;
-            hp.order = plan->row_order + plan->n_long;
-            hp.n_hub = plan->n_rows_split - plan->n_long;
-        }
     }
 
     // feature chunks wider than 512 vectors per lane-group are split over launches
@@ -1131,40 +1060,31 @@ extern "C" int gala_spmm_ex_f32(const gala_csr_t *A, const float *X, int64_t ldx
             const int L = (int)((Fc + vec - 1) / vec);
             int r = 0;
             const bool forked = use_hub && hub_st != hs;
-            const bool forked3 = forked && long_st != hs;   // + long_stream and row_stream
             if (use_hub) {  // the long serial rows first, so their workgroups are dispatched first
                 if (forked) {
                     if (hipEventRecord((hipEvent_t)plan->aux_events[0], hs) != hipSuccess ||
-                        hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess ||
-                        (forked3 && (hipStreamWaitEvent(long_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess ||
-                                     hipStreamWaitEvent(row_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)))
+                        hipStreamWaitEvent(hub_st, (hipEvent_t)plan->aux_events[0], 0) != hipSuccess)
                         return launch_status();
                 }
-                if (forked3) launch_hub(q, hp_long, vec, w, src_scale != nullptr, long_st);
                 launch_hub(q, hp, vec, w, src_scale != nullptr, hub_st);
                 r = launch_status();
             }
             if (!r) {
                 const bool sparse_rows =
                     sparse_rows_enabled() && A->n_rows > 0 && A->nnz < kSparseRowDeg * (int64_t)A->n_rows;
-                if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, row_st, sparse_rows);
-                else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, row_st);
-                else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, row_st);
+                if (vec == 4) r = launch_vec<4>(q, sp, L, w, samp, src_scale != nullptr, hs, sparse_rows);
+                else if (vec == 2) r = launch_vec<2>(q, sp, L, w, samp, src_scale != nullptr, hs);
+                else r = launch_vec<1>(q, sp, L, w, samp, src_scale != nullptr, hs);
                 if (!r) r = launch_status();
             }
             // join (also after a failed launch, so a fork never stays open -- an unjoined fork
             // would invalidate a hipGraph capture on the caller's stream): the caller's stream
-            // waits for the hub rows (and the long chains and the row kernel)
+            // waits for the hub rows
             if (forked) {
-                const hipStream_t from[3] = {hub_st, long_st, row_st};
-                const hipEvent_t ev[3] = {(hipEvent_t)plan->aux_events[1],
-                                          forked3 ? (hipEvent_t)plan->join_events[0] : nullptr,
-                                          forked3 ? (hipEvent_t)plan->join_events[1] : nullptr};
-                for (int k = 0; k < (forked3 ? 3 : 1); ++k) {
-                    if (hipEventRecord(ev[k], from[k]) != hipSuccess || hipStreamWaitEvent(hs, ev[k], 0) != hipSuccess) {
-                        const int j = launch_status();
-                        if (!r) r = j ? j : GALA_ERR_HIP;
-                    }
+                if (hipEventRecord((hipEvent_t)plan->aux_events[1], hub_st) != hipSuccess ||
+                    hipStreamWaitEvent(hs, (hipEvent_t)plan->aux_events[1], 0) != hipSuccess) {
+                    const int j = launch_status();
+                    if (!r) r = j ? j : GALA_ERR_HIP;
                 }
             }
             if (r) return r;

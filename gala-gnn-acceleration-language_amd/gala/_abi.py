@@ -47,10 +47,6 @@ class gala_split_plan_t(ctypes.Structure):
         ("row_order", ctypes.c_void_p),
         ("aux_stream", ctypes.c_void_p),
         ("aux_events", ctypes.c_void_p * 2),
-        ("n_long", ctypes.c_int64),
-        ("long_stream", ctypes.c_void_p),
-        ("row_stream", ctypes.c_void_p),
-        ("join_events", ctypes.c_void_p * 2),
     ]
 
 
@@ -179,7 +175,7 @@ _lib = None
 
 
 GALA_GAT_IN_RELU = 1
-ABI_VERSION = 6  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
+ABI_VERSION = 5  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
 
 
 def lib() -> ctypes.CDLL:

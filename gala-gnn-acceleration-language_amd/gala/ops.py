@@ -8,7 +8,6 @@ wrappers and autograd Functions of codegen/gala.cu) lives in host/gala_torch.cpp
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -27,58 +26,6 @@ def _dp(t):
     if not t.is_cuda:
         raise ValueError("gala ops take device tensors (no CPU fallback)")
     return t.data_ptr()
-
-
-def long_chain_edges() -> int:
-    """Hub rows of at least this many edges run their REF-order chain on compute units of
-    their own (gala_split_plan_t.n_long): 131072, a chain of ~0.6 ms on MI355X, about the
-    R-MAT row kernel's time; GALA_HUB_LONG overrides it (0: no long launch)."""
-    v = int(os.environ.get("GALA_HUB_LONG", "131072"))
-    return v if v > 0 else 1 << 62
-
-
-MAX_LONG = 8            # long chains in their own launch: the longest, at most one per XCD
-_MASKED: dict = {}      # device index -> (long, hub, row) hipStream_t, created once per process
-
-
-def masked_streams(dev: torch.device):
-    """Three HIP streams with complementary CU masks (hipExtStreamCreateWithCUMask), or None:
-    `long` on one CU of every XCD (CU 0 of each: mask bit i is CU i % 32 of XCD i // 32 on
-    MI355X, profiles/r06_cu_mask_probe.txt), `hub` and `row` on the other CUs -- so the longest
-    serial chains start at once and share their CUs with nothing.  Shared by every plan of
-    the device and never destroyed (a plan may outlive the HIP runtime at exit), like the
-    mirror's."""
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    if idx in _MASKED:
-        return _MASKED[idx]
-    props = torch.cuda.get_device_properties(idx)
-    n_cu, n_xcd = props.multi_processor_count, 8
-    if not str(getattr(props, "gcnArchName", "")).startswith("gfx950") or n_cu % n_xcd or n_cu // n_xcd < 2:
-        _MASKED[idx] = None   # only the measured layout (MI355X: 8 XCDs x 32 CUs)
-        return None
-    words = (n_cu + 31) // 32
-    reserved = [0] * words
-    for x in range(n_xcd):
-        bit = x * (n_cu // n_xcd)
-        reserved[bit // 32] |= 1 << (bit % 32)
-    rest = [(~r) & 0xffffffff for r in reserved]
-    if n_cu % 32:
-        rest[-1] &= (1 << (n_cu % 32)) - 1
-    L = _abi.lib()
-    fn = L.hipExtStreamCreateWithCUMask
-    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
-                                             ctypes.POINTER(ctypes.c_uint32)]
-    out = []
-    with torch.cuda.device(idx):
-        for m in (reserved, rest, rest):
-            h = ctypes.c_void_p()
-            arr = (ctypes.c_uint32 * words)(*m)
-            if fn(ctypes.byref(h), words, arr) != 0:
-                _MASKED[idx] = None
-                return None
-            out.append(h.value)
-    _MASKED[idx] = tuple(out)
-    return _MASKED[idx]
 
 
 class DeviceGraph:
@@ -146,28 +93,15 @@ class DeviceGraph:
         aux = None
         if nr.value > 0 and dev.type == "cuda":
             # the REF-order hub rows run beside the row kernel on a side stream (fork / join
-            # events recorded by the library on the caller's stream)
-            aux = (torch.cuda.Stream(device=dev), torch.cuda.Event(), torch.cuda.Event())
+            # events recorded by the library on the caller's stream); a high-priority one, so
+            # the longest serial chains (the hub launch's first workgroups) are dispatched
+            # before the row kernel fills the CUs (R-MAT: 1.87 -> 1.81 ms,
+            # profiles/r06_hub_clock_swizzle.jsonl)
+            aux = (torch.cuda.Stream(device=dev, priority=-1), torch.cuda.Event(), torch.cuda.Event())
             for ev in aux[1:]:
                 ev.record(aux[0])   # creates the event handles
             plan.aux_stream = aux[0].cuda_stream
             plan.aux_events[0], plan.aux_events[1] = aux[1].cuda_event, aux[2].cuda_event
-            # ABI 6: the longest chains (hub rows of >= long_chain_edges() edges, the order's
-            # first entries) on CUs of their own; the other hub rows and the row kernel on the
-            # remaining CUs
-            n_long = 0
-            if order is not None:
-                deg = np.diff(rp.astype(np.int64))
-                n_long = min(int((deg[order[:nr.value]] >= long_chain_edges()).sum()), MAX_LONG)
-            ms = masked_streams(dev) if n_long > 0 else None
-            if ms is not None:
-                joins = (torch.cuda.Event(), torch.cuda.Event())
-                for ev in joins:
-                    ev.record(aux[0])
-                plan.n_long = n_long
-                plan.long_stream, plan.aux_stream, plan.row_stream = ms
-                plan.join_events[0], plan.join_events[1] = joins[0].cuda_event, joins[1].cuda_event
-                aux = aux + joins
         self._split = {"plan": plan, "arrays": arrays + (order_t,), "ws": None, "aux": aux}
         self._csr = None
 

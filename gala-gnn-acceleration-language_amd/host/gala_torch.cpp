@@ -1,12 +1,7 @@
 // C++/libtorch mirror of GALA's emitted operator API over the C ABI (see gala_torch.h).
 #include "gala_torch.h"
-#include <array>
 #include <climits>
 #include <cstring>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <vector>
 
 #include "gala_cpu.h"
 
@@ -344,52 +339,6 @@ void SplitState::ensure_workspace(int64_t F) {
     plan.ws_cols = F;
 }
 
-// Hub rows of at least this many edges run their REF-order chain on compute units of their
-// own (gala_split_plan_t.n_long; GALA_HUB_LONG overrides, 0 = no long launch) -- the same rule
-// as gala/ops.py's long_chain_edges()
-static int64_t long_chain_edges() {
-    const char *e = std::getenv("GALA_HUB_LONG");
-    const int64_t v = e ? std::atoll(e) : 131072;
-    return v > 0 ? v : INT64_MAX;
-}
-constexpr int64_t kMaxLong = 8;
-
-// Three streams with complementary CU masks per device (long: CU 0 of every XCD; hub, row: the
-// other CUs), created once and never destroyed (gala/ops.py's masked_streams: MI355X only,
-// where the mask layout is measured, profiles/r06_cu_mask_probe.txt); nullptr elsewhere.
-static const std::array<hipStream_t, 3> *masked_streams(int device) {
-    static std::mutex mu;
-    static std::map<int, std::unique_ptr<std::array<hipStream_t, 3>>> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(device);
-    if (it != cache.end()) return it->second.get();
-    hipDeviceProp_t prop{};
-    std::unique_ptr<std::array<hipStream_t, 3>> res;
-    const int n_xcd = 8;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 &&
-        prop.multiProcessorCount % n_xcd == 0 && prop.multiProcessorCount / n_xcd >= 2) {
-        const int n_cu = prop.multiProcessorCount, words = (n_cu + 31) / 32;
-        std::vector<uint32_t> reserved(words, 0), rest(words, 0);
-        for (int x = 0; x < n_xcd; ++x) {
-            const int bit = x * (n_cu / n_xcd);
-            reserved[bit / 32] |= 1u << (bit % 32);
-        }
-        for (int w = 0; w < words; ++w) rest[w] = ~reserved[w];
-        if (n_cu % 32) rest[words - 1] &= (1u << (n_cu % 32)) - 1;
-        int prev = 0;
-        hipGetDevice(&prev);
-        hipSetDevice(device);
-        res = std::make_unique<std::array<hipStream_t, 3>>();
-        const std::vector<uint32_t> *masks[3] = {&reserved, &rest, &rest};
-        for (int k = 0; k < 3 && res; ++k)
-            if (hipExtStreamCreateWithCUMask(&(*res)[k], (uint32_t)words, masks[k]->data()) != hipSuccess) res.reset();
-        hipSetDevice(prev);
-    }
-    auto *p = res.get();
-    cache[device] = std::move(res);
-    return p;
-}
-
 // Hub-row split plan and degree-ordered row schedule of a device graph (gala_split_plan_t),
 // built once per graph on the host: hub rows (deg > max(1024, 8 x mean)) are split into
 // chunks; a skewed graph (max deg > 4 x mean) also gets the descending-degree row order.
@@ -426,33 +375,14 @@ std::shared_ptr<SplitState> make_split_plan(const torch::Tensor &offsets, int se
         st->row_order = order.to(offsets.device());
     }
     if (nr > 0 && offsets.is_cuda()) {
-        // the REF-order hub rows run on a side stream beside the row kernel
-        auto aux = c10::hip::getStreamFromPool(false, offsets.device().index());
+        // the REF-order hub rows run on a side stream beside the row kernel: a high-priority
+        // one, so the longest serial chains are dispatched before the row kernel fills the CUs
+        auto aux = c10::hip::getStreamFromPool(true, offsets.device().index());
         st->plan.aux_stream = (void *)aux.stream();
         for (int i = 0; i < 2; ++i) {
             hipEvent_t ev = nullptr;
             TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
             st->aux_events[i] = st->plan.aux_events[i] = (void *)ev;
-        }
-        // ABI 6: the longest chains (the order's first rows of >= long_chain_edges() edges) on
-        // CUs of their own; the other hub rows and the row kernel on the remaining CUs
-        int64_t n_long = 0;
-        if (skewed) {
-            for (int64_t i = 0; i < n; ++i)   // hub rows (deg > thr) of at least long_chain_edges()
-                n_long += r[i + 1] - r[i] > thr && r[i + 1] - r[i] >= long_chain_edges();
-            n_long = std::min(n_long, kMaxLong);
-        }
-        const auto *ms = n_long > 0 ? masked_streams(offsets.device().index()) : nullptr;
-        if (ms) {
-            for (int i = 0; i < 2; ++i) {
-                hipEvent_t ev = nullptr;
-                TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
-                st->join_events[i] = st->plan.join_events[i] = (void *)ev;
-            }
-            st->plan.n_long = n_long;
-            st->plan.long_stream = (void *)(*ms)[0];
-            st->plan.aux_stream = (void *)(*ms)[1];
-            st->plan.row_stream = (void *)(*ms)[2];
         }
     }
     st->plan.threshold = thr;

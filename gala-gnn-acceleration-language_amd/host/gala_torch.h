@@ -37,7 +37,6 @@ struct SplitState {
     // the side stream (torch's pool) and fork / join events of the REF-order hub rows; the
     // events are never destroyed (a plan may outlive the HIP runtime at process exit)
     void *aux_events[2] = {nullptr, nullptr};
-    void *join_events[2] = {nullptr, nullptr};   // the long-chain / row-stream joins (ABI 6)
     void ensure_workspace(int64_t F);
 };
 // GALA_SPMM_HUB=chunked selects the fast, reordered hub-row mode (GALA_SPMM_HUB_CHUNKED)

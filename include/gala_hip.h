@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GALA_ABI_VERSION 6
+#define GALA_ABI_VERSION 5
 
 typedef enum gala_status {
     GALA_OK = 0,
@@ -100,19 +100,6 @@ typedef struct gala_split_plan {
                                   graph from two host threads / streams must be ordered by
                                   the caller (or use a plan each), else one call's join can
                                   wait on the other's fork.                               */
-    /* ABI 6: the longest serial chains on compute units of their own.  A REF-order hub row's
-       chain is serial (the reference's row loop), so the longest one bounds the SpMM; it must
-       start at once and share its CU with nothing.  With n_long > 0 and long_stream,
-       row_stream and join_events set (and aux_stream / aux_events), gala_spmm_ex_f32 forks the
-       caller's stream three ways: the first n_long rows of row_order in a launch of their own
-       on long_stream, the other hub rows on aux_stream, and the row kernel on row_stream; the
-       caller's stream then waits on all three.  The library only orders the launches; the
-       host gives the streams their compute units (hipExtStreamCreateWithCUMask: long_stream
-       on a few CUs reserved for it, aux_stream and row_stream on the rest).               */
-    int64_t n_long;            /* <= n_rows_split: leading hub rows in the long launch     */
-    void *long_stream;         /* hipStream_t or NULL                                     */
-    void *row_stream;          /* hipStream_t or NULL                                     */
-    void *join_events[2];      /* hipEvent_t: long_stream's and row_stream's joins        */
 } gala_split_plan_t;
 
 typedef struct gala_csr {

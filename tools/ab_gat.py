@@ -29,8 +29,7 @@ def load(path):
     for name, (res, args) in _abi.SIGNATURES.items():
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
-    # an earlier ABI's build reads the prefix of the structs it knows (A/B against it)
-    assert L.gala_abi_version() in (_abi.ABI_VERSION, _abi.ABI_VERSION - 1), path
+    assert L.gala_abi_version() == _abi.ABI_VERSION, path
     return L
 
 

@@ -1,4 +1,5 @@
 #!/usr/bin/env python3
+# Needs commit f2516f9's tree (the GALA_HUB_TRACE build of spmm.hip and the ABI 6 plan fields, since reverted).
 """In-process A/B of the REF-order R-MAT SpMM (Products shape, F = 32) with and without the
 ABI 6 long-chain launch: "long" -- the plan as gala.ops builds it (the longest chains on CU 0 of
 every XCD, the other hub rows and the row kernel on the other CUs) -- against "one" -- one hub

@@ -1,4 +1,5 @@
 #!/usr/bin/env python3
+# Needs commit f2516f9's tree (the GALA_HUB_TRACE build of spmm.hip and the ABI 6 plan fields, since reverted).
 """Timeline of one REF-order R-MAT SpMM (F = 32, Products shape) from a trace build of
 libgala_hip.so (-DGALA_HUB_TRACE: wall-clock stamps written by the kernels themselves):
 the row kernel's first start / last end, the hub kernel's, the 8 longest hub rows' workgroups
