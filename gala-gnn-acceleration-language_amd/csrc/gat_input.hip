@@ -281,8 +281,19 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
 // N = D) with W_ext,h fragments held in registers.
 // one workgroup of 8 waves per CU (2 per SIMD: ~210 VGPRs, no spills; 4 per SIMD spilled
 // and ran 1.5x slower, tools/gat_input_bench.py)
+// The forward's stash of the eight rows' aggregate tiles, in float4 units: tile t, k-quad kq,
+// row slot s, variant v at ((t * 4 + kq) * 8 + s) * 16 + ((v + s) & 15).  The rotation by s
+// puts a phase's stores (wave s: v = 0..15) and the projection's reads (wave h: the 16 (s, v)
+// of head h) each on 16 distinct 16-B bank slots -- also across the k-quads that one
+// ds_read_b128 lane group mixes (lanes {0-3, 12-15} of one quad, {4-11} of the next) -- where
+// [slot][variant][tile][16] put the projection's 16 lanes on one bank (SQ_LDS_BANK_CONFLICT:
+// 71 % of the kernel's LDS cycles, profiles/r06_lds_conflicts.txt).
+__device__ __forceinline__ int fwd_stash(int t, int kq, int s, int v) {
+    return ((t * 4 + kq) * kInWaves + s) * 16 + ((v + s) & 15);
+}
+
 __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
-    __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // [slot][variant][tile][16 floats]
+    __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // fwd_stash
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
     // B fragments of the projection: W_ext,h[j = 16 nt + n16][feature(t, 4 kq + q4)]
@@ -341,14 +352,14 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
                         acc);
         }
 #pragma unroll
-        for (int t = 0; t < kInTiles; ++t) stash[((wave * 16 + n16) * kInTiles + t) * 4 + kq] = acc[t];
+        for (int t = 0; t < kInTiles; ++t) stash[fwd_stash(t, kq, wave, n16)] = acc[t];
         __syncthreads();
         if (h < p.H) {
             f4v y[2] = {f4v{0.0f, 0.0f, 0.0f, 0.0f}, f4v{0.0f, 0.0f, 0.0f, 0.0f}};
             const int s_a = n16 >> 1, v_a = h + 8 * (n16 & 1);
 #pragma unroll
             for (int t = 0; t < kInTiles; ++t) {
-                const f4v a4 = stash[((s_a * 16 + v_a) * kInTiles + t) * 4 + kq];
+                const f4v a4 = stash[fwd_stash(t, kq, s_a, v_a)];
 #pragma unroll
                 for (int q4 = 0; q4 < 4; ++q4) {
                     y[0] = mfma4(a4[q4], wf[t][q4][0], y[0]);
@@ -361,8 +372,9 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
                 const int s = 2 * kq + hs;
                 const int64_t row = prow[hs];
                 if (row < 0) continue;
-                const float S = stf[((s * 16 + h) * kInTiles + 4) * 16 + 12];
-                const float Sm = stf[((s * 16 + h + 8) * kInTiles + 4) * 16 + 12];
+                // sum p / sum m p: tile 4, float 12 (k-quad 3, component 0) of variants h, h + 8
+                const float S = stf[fwd_stash(4, 3, s, h) * 4];
+                const float Sm = stf[fwd_stash(4, 3, s, h + 8) * 4];
                 const float qv = 1.0f / __fadd_rn(S, 1e-12f);   // REF: 1 / (1e-12 + sum p)
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt) {
@@ -405,10 +417,18 @@ __device__ __forceinline__ float head_dot_sum(float v) { return group_sum<DW>(v)
 // Xin_ext[r] (alpha rebuilt from aL[r], q[r] in r's extended row and aR[c]) and c's d_aL from
 // the forward's row statistics; then wave h adds dY_h[c]^T T_h[c] of the eight columns into
 // its register accumulators M_h[D x 112] (K = the columns).  Partials per workgroup.
+// The backward's stash, in floats: slot s, head h, tile t, element i at s * kBwdSlot + h * kBwdHead
+// + t * 16 + i -- the 4-float pads put a phase's float4 stores (wave s, lanes h = 0..7 of one
+// k-quad) and the M phase's reads (lanes of two k-quads: slots s, s + 1) on distinct banks; the
+// columns' dY at slot * kDyLd floats likewise (unpadded: 2-way conflicts on every read).
+constexpr int kBwdHead = kInTiles * 16 + 4;             // 116 floats
+constexpr int kBwdSlot = kInMaxHeads * kBwdHead + 16;   // 944 floats: slots s, s + 1 16 banks apart
+constexpr int kDyLd = 4 * (kWave + 4);                  // 272 floats of dY per slot
+
 template <int DW>
 __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
-    __shared__ f4v stash[kInWaves * kInMaxHeads * kInTiles * 4];   // [slot][head][tile][16]
-    __shared__ f4v dstash[kInWaves * kWave];                        // [slot][256]: the columns' dY (masked)
+    __shared__ f4v stash[kInWaves * kBwdSlot / 4];   // see kBwdSlot
+    __shared__ f4v dstash[kInWaves * kDyLd / 4];     // [slot][kDyLd]: the columns' dY (masked)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
     const int h = wave;
     const float *stf = reinterpret_cast<const float *>(stash);
@@ -481,10 +501,10 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 p.daL[c * p.H + hh] = (sym - accv * p.sma[c * p.H + hh]) + 1e-12f;   // common.h:662-667
             }
         }
-        dstash[wave * kWave + lane] = dy;   // the M phase's A operand, from LDS after the barrier
+        dstash[wave * (kDyLd / 4) + lane] = dy;   // the M phase's A operand, from LDS after the barrier
         if (n16 < kInMaxHeads) {
 #pragma unroll
-            for (int t = 0; t < kInTiles; ++t) stash[((wave * kInMaxHeads + n16) * kInTiles + t) * 4 + kq] = acc[t];
+            for (int t = 0; t < kInTiles; ++t) stash[(wave * kBwdSlot + n16 * kBwdHead + t * 16) / 4 + kq] = acc[t];
         }
         __syncthreads();
         if (h < p.H) {
@@ -493,7 +513,7 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 const int s = 4 * ks + kq;
                 const int64_t si = blk * kInWaves + s;
                 const bool ok = si < p.n_rows;
-                const float *dsf = reinterpret_cast<const float *>(dstash) + s * 4 * kWave;
+                const float *dsf = reinterpret_cast<const float *>(dstash) + s * kDyLd;
                 float a[2];
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
@@ -502,7 +522,7 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 }
 #pragma unroll
                 for (int t = 0; t < kInTiles; ++t) {
-                    const float bv = ok ? stf[((s * kInMaxHeads + h) * kInTiles + t) * 16 + n16] : 0.0f;
+                    const float bv = ok ? stf[s * kBwdSlot + h * kBwdHead + t * 16 + n16] : 0.0f;
                     M[0][t] = mfma4(a[0], bv, M[0][t]);
                     M[1][t] = mfma4(a[1], bv, M[1][t]);
                 }
