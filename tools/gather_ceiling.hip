@@ -74,19 +74,23 @@ __global__ __launch_bounds__(256) void k_gather(const int32_t *__restrict__ idx,
     *reinterpret_cast<f4 *>(out + grp * (G * 4) + gl * 4) = acc;
 }
 
+// lds: dynamic LDS per 256-thread workgroup (caps the workgroups per CU: the waves per CU the
+// gather gets, e.g. 80 KiB -> 2 workgroups = 8 waves, the input-space GAT kernel's occupancy)
 template <int G, int U, int CHUNK, bool NT>
-static float run(const int32_t *idx, const float *X, int64_t E, float *out, const char *name) {
+static float run(const int32_t *idx, const float *X, int64_t E, float *out, const char *name, size_t lds = 0) {
     const int64_t groups = (E + CHUNK - 1) / CHUNK;
     const int64_t blocks = (groups * G + 255) / 256;
+    if (lds > 65536) CK(hipFuncSetAttribute((const void *)k_gather<G, U, CHUNK, NT>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((k_gather<G, U, CHUNK, NT>), dim3(blocks), dim3(256), 0, 0, idx, X, E, out);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((k_gather<G, U, CHUNK, NT>), dim3(blocks), dim3(256), lds, 0, idx, X, E, out);
     CK(hipDeviceSynchronize());
     std::vector<float> ts;
     for (int r = 0; r < 10; ++r) {
         CK(hipEventRecord(a));
-        hipLaunchKernelGGL((k_gather<G, U, CHUNK, NT>), dim3(blocks), dim3(256), 0, 0, idx, X, E, out);
+        hipLaunchKernelGGL((k_gather<G, U, CHUNK, NT>), dim3(blocks), dim3(256), lds, 0, idx, X, E, out);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms;
@@ -96,8 +100,8 @@ static float run(const int32_t *idx, const float *X, int64_t E, float *out, cons
     std::sort(ts.begin(), ts.end());
     const float ms = ts[ts.size() / 2];
     const double row_b = G * 16.0;
-    printf("{\"kernel\": \"%s\", \"row_bytes\": %.0f, \"E\": %lld, \"ms\": %.4f, \"rows_per_s\": %.4e, \"row_GBps\": %.1f}\n",
-           name, row_b, (long long)E, ms, E / (ms * 1e-3), E * row_b / (ms * 1e-3) / 1e9);
+    printf("{\"kernel\": \"%s\", \"lds_per_wg\": %zu, \"row_bytes\": %.0f, \"E\": %lld, \"ms\": %.4f, \"rows_per_s\": %.4e, \"row_GBps\": %.1f}\n",
+           name, lds, row_b, (long long)E, ms, E / (ms * 1e-3), E * row_b / (ms * 1e-3) / 1e9);
     fflush(stdout);
     return ms;
 }
@@ -146,6 +150,11 @@ int main(int argc, char **argv) {
     } else if (F == 128) {
         run<32, 8, 64, false>(idx, X, E, out, "G32_U8_C64");
         run<32, 16, 64, false>(idx, X, E, out, "G32_U16_C64");
+        // the same gather held to fewer waves per CU (LDS per workgroup of 4 waves)
+        for (size_t lds : {20480, 40960, 81920, 160 * 1024}) {
+            run<32, 8, 64, false>(idx, X, E, out, "G32_U8_C64_ldscap", lds);
+            run<32, 4, 64, false>(idx, X, E, out, "G32_U4_C64_ldscap", lds);
+        }
     }
     return 0;
 }
