@@ -196,3 +196,35 @@ def test_bench_matrix_market_graph(tmp_path):
     assert d["config"]["n_vertices"] == n and d["config"]["edges"] == g.nnz
     assert "Matrix Market" in d["data"]
 
+
+
+def test_traffic_is_withheld_when_the_kernel_sources_changed(tmp_path, monkeypatch):
+    """bench.py reports a kernel's PMC bytes (profiles/traffic.json) only while the sources its
+    pass ran on are unchanged: a digest mismatch or a missing digest withholds the number and
+    lists the kernel under traffic_withheld_stale."""
+    sys.path.insert(0, ROOT)
+    import bench
+    committed = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    key = next(k for k in committed["kernels"] if k.startswith("void gala::k_spmm_rowgroup<4, 8, 1, 4"))
+    entry = committed["kernels"][key]
+    assert entry.get("sources_sha256"), "the committed PMC summary records its source digests"
+    # the committed summary against this tree: fresh
+    monkeypatch.setattr(bench, "TRAFFIC_STALE", [])
+    assert bench.load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>") == \
+        float(entry["hbm_bytes_per_launch"])
+    assert bench.TRAFFIC_STALE == []
+    # one source digest off, and none at all: withheld
+    fake_root = tmp_path / "root"
+    (fake_root / "profiles").mkdir(parents=True)
+    os.symlink(os.path.join(ROOT, "gala-gnn-acceleration-language_amd"), fake_root / "gala-gnn-acceleration-language_amd")
+    for digests in ({**entry["sources_sha256"], "gala-gnn-acceleration-language_amd/csrc/spmm.hip": "0" * 64}, None):
+        e = dict(entry)
+        if digests is None:
+            e.pop("sources_sha256")
+        else:
+            e["sources_sha256"] = digests
+        json.dump({"kernels": {key: e}}, open(fake_root / "profiles" / "traffic.json", "w"))
+        monkeypatch.setattr(bench, "ROOT", str(fake_root))
+        monkeypatch.setattr(bench, "TRAFFIC_STALE", [])
+        assert bench.load_traffic("k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>") is None
+        assert bench.TRAFFIC_STALE == ["k_spmm_rowgroup<4, 8, 1, 4, false, false, false, false>"]
