@@ -47,7 +47,8 @@ def check_against_ref(got, ref):
         grad_close(got[k], ref[k], k)
 
 
-@pytest.mark.parametrize("fin,heads,D", [(100, 8, 32), (37, 4, 16), (20, 2, 32), (100, 1, 32), (64, 8, 8)])
+@pytest.mark.parametrize("fin,heads,D", [(100, 8, 32), (37, 4, 16), (20, 2, 32), (100, 1, 32), (64, 8, 8),
+                                         (48, 8, 4), (100, 3, 4)])
 def test_input_space_kernels_against_the_reference_chain(fin, heads, D):
     g = layout.gen_graph("uniform", 3000, 40000, seed=7)
     X, W, b, wL, bL, wR, bR, dY = layer_inputs(g.n_rows, fin, heads, D, seed=fin + heads)
