@@ -919,10 +919,15 @@ def gat_layer(args, dg, hg, dev, timer, sync):
                   exp(LeakyReLU(aL[r] + aR[c])) and the 512-B extended row of c into the
                   per-head input-space aggregates (matrix cores), projected per row by the
                   Linear into Y and Ym, with q = 1/(1e-12 + sum p) and sum m*alpha
-        backward  gala_gat_in_bwd_f32 over the transposed pattern (the symmetric graph itself):
-                  T_h[c] = sum alpha X_ext[r], M_h += dY_h[c]^T T_h[c], d_aL from <dY, Y>,
-                  <dY, Ym>; then G = d_aL^T X (gala_dense_grad_f32) and the parameter
-                  gradients of W, b and both attention Linears
+                  -- in T mode (gala_gat_in_fwd_t_f32, the mirror's default on a symmetric
+                  graph): a pass summing q for every row first, then the same walk also forms
+                  the backward's per-column aggregates T_h[c] = sum alpha X_ext[r] (r in N(c))
+                  from the rows it gathers anyway
+        backward  gala_gat_in_bwd_t_f32: M_h += dY_h[c]^T T_h[c], d_aL from <dY, Y>, <dY, Ym>
+                  (no walk over the graph); then G = d_aL^T X (gala_dense_grad_f32) and the
+                  parameter gradients of W, b and both attention Linears.  `walk` times the
+                  previous backward beside it: gala_gat_in_bwd_f32 gathering the extended rows
+                  again over the transposed pattern
     (the reference's FFN_OP + attention Linears + the edge chains of cuda.h:505-562,679-845 and
     common.h:622-894, fused and regrouped in input space; tests/test_gpu_gat_input.py checks it
     against the oracle's pass-by-pass chain at this size).  `gathering_linear_output` times the
@@ -945,11 +950,12 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     st = {}
 
     def fwd():
-        st["f"] = ops.gat_input_layer(dg, Xin, W, b, wL, bL, wR, bR, H, order=order, relu=True)
+        st["f"] = ops.gat_input_layer(dg, Xin, W, b, wL, bL, wR, bR, H, order=order, relu=True, tmode=True)
 
     def bwd():
         f = st["f"]
-        daL, M = ops.gat_in_bwd(dg, f["xext"], dY, f["Y"], f["Ym"], f["sma"], H, FIN, order=order, relu=True)
+        daL, M = ops.gat_in_bwd(dg, f["xext"], dY, f["Y"], f["Ym"], f["sma"], H, FIN, order=order, relu=True,
+                                T=f["T"])
         Gw, Gb = ops.dense_grad(Xin, daL)
         sLR = (wL + wR).reshape(H, D)
         dW = M[:, :, :FIN] + sLR.unsqueeze(2) * Gw.unsqueeze(1)
@@ -963,32 +969,50 @@ def gat_layer(args, dg, hg, dev, timer, sync):
     steps = max(args.steps // 2, 2)
     t_step = timed_steps(step, steps, 2, sync, lambda: None, lambda x: x)
     f0 = st["f"]
-    xext, Y0, Ym0, sma0 = f0["xext"], f0["Y"], f0["Ym"], f0["sma"]
+    xext, Y0, Ym0, sma0, T0 = f0["xext"], f0["Y"], f0["Ym"], f0["sma"], f0["T"]
 
-    def k_fwd():   # the aggregation kernel alone (its extended rows prepared)
-        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order, relu=True)
+    def k_fwd():   # the aggregation call alone (its extended rows prepared): q pass + T-mode walk
+        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order, relu=True, T=T0)
 
     def k_bwd():
+        ops.gat_in_bwd(dg, xext, dY, Y0, Ym0, sma0, H, FIN, order=order, relu=True, T=T0)
+
+    def k_fwd_walk():   # the walk formulation: forward without T, backward gathering again
+        ops.gat_in_fwd(dg, xext, W, b, H, FIN, order=order, relu=True)
+
+    def k_bwd_walk():
         ops.gat_in_bwd(dg, xext, dY, Y0, Ym0, sma0, H, FIN, order=order, relu=True)
-    # the layer, its two kernels and the same-process gather probe of the 512-B extended rows,
-    # interleaved over three rounds (medians: all move by up to 10 % with the GPU's load state,
-    # DESIGN §4.4)
-    rounds = {"fwd": [], "bwd": [], "k_fwd": [], "k_bwd": [], "ceil": []}
+    # the layer, its kernels (both formulations) and the same-process gather probe of the
+    # 512-B extended rows, interleaved over three rounds (medians: all move by up to 10 % with
+    # the GPU's load state).  The walk's forward writes q into the extended rows
+    # as the T-mode q pass does (the same values), so the two share the rows.
+    rounds = {"fwd": [], "bwd": [], "k_fwd": [], "k_bwd": [], "k_fwd_walk": [], "k_bwd_walk": [], "ceil": []}
     for _ in range(3):
         rounds["fwd"].append(timer(fwd, 5))
         rounds["bwd"].append(timer(bwd, 5))
         rounds["k_fwd"].append(timer(k_fwd, 5))
         rounds["k_bwd"].append(timer(k_bwd, 5))
+        rounds["k_fwd_walk"].append(timer(k_fwd_walk, 5))
+        rounds["k_bwd_walk"].append(timer(k_bwd_walk, 5))
+        k_fwd()   # the T tiles and q of the T-mode forward back in place for the next round
         t_c = gather_ceiling(dg.col, xext, timer, reps=5)
         if t_c:
             rounds["ceil"].append(t_c)
     med = lambda xs: sorted(xs)[len(xs) // 2] if xs else None  # noqa: E731
     t_fwd, t_bwd, t_kf, t_kb = (med(rounds[k]) for k in ("fwd", "bwd", "k_fwd", "k_bwd"))
-    # algorithmic bytes per launch, SURVEY §8(d)'s model (every operand once, no per-edge
-    # outputs): forward rowptr + col + the extended rows + Y, Ym + q, sma (+ q into the rows)
-    # + W; backward rowptr + col + the extended rows + dY, Y, Ym + sma + d_aL
-    alg = 4 * (N + 1) + 4 * E + 512 * N + 2 * 4 * N * F + 3 * 4 * N * H + 4 * F * (FIN + 1)
-    alg_b = 4 * (N + 1) + 4 * E + 512 * N + 3 * 4 * N * F + 2 * 4 * N * H
+    # algorithmic bytes per call, SURVEY §8(d)'s model (every operand once, no per-edge
+    # outputs): the q pass rowptr + col + aR (copied to a compact table: read + write + read),
+    # aL, q into the rows; the forward rowptr + col + the extended rows + Y, Ym + q, sma + W +
+    # the T tiles written (896 floats per row); the backward the T tiles + dY, Y, Ym + sma +
+    # d_aL
+    T_ROW = 896 * 4
+    alg_q = 4 * (N + 1) + 4 * E + 3 * 4 * N * 8 + 2 * 4 * N * H
+    alg = alg_q + 4 * (N + 1) + 4 * E + 512 * N + 2 * 4 * N * F + 2 * 4 * N * H + 4 * F * (FIN + 1) + T_ROW * N
+    alg_b = T_ROW * N + 3 * 4 * N * F + 2 * 4 * N * H
+    # the walk pair's own (the previous round's) byte model, for the kernels timed beside
+    alg_w = 4 * (N + 1) + 4 * E + 512 * N + 2 * 4 * N * F + 3 * 4 * N * H + 4 * F * (FIN + 1)
+    alg_wb = 4 * (N + 1) + 4 * E + 512 * N + 3 * 4 * N * F + 2 * 4 * N * H
+    traffic_f = [load_traffic(k) for k in ("k_gat_in_fwd<true>", "k_gat_in_q", "k_gat_in_ar")]
     out = {"value": 2 * E / t_step, "unit": "edges/s", "ms_per_step": t_step * 1e3, "steps": steps,
            "layer": (f"GAT layer 1 of config 3: {FIN} input features -> {H} heads x {D} (F={F}), Linear + both "
                      f"attention Linears + REF softmax aggregation + the program's ReLU, input space; forward + "
@@ -996,24 +1020,34 @@ def gat_layer(args, dg, hg, dev, timer, sync):
            "fwd_ms": t_fwd * 1e3, "bwd_ms": t_bwd * 1e3,
            "roofline": {"bound": "hbm", "achieved": alg / t_kf / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                         "frac": alg / t_kf / HBM_PEAK, "kernel_ms": t_kf * 1e3, "alg_bytes_per_launch": alg,
-                        "traffic": load_traffic("k_gat_in_fwd"),
-                        "kernel": "gala::k_gat_in_fwd (gala_gat_in_fwd_f32, 8 heads x 32 from 100 inputs)",
-                        "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch (profiles/traffic.json): 126 M "
-                                        "gathered 512-B extended input rows"}}
+                        "traffic": sum(traffic_f) if all(t is not None for t in traffic_f) else None,
+                        "kernel": "gala_gat_in_fwd_t_f32: gala::k_gat_in_ar + k_gat_in_q + k_gat_in_fwd<true> "
+                                  "(8 heads x 32 from 100 inputs)",
+                        "traffic_note": "PMC FETCH_SIZE*2+WRITE_SIZE per launch summed over the call's three "
+                                        "kernels (profiles/traffic.json): 126 M gathered 512-B extended input rows, "
+                                        "the 3.5-KB T tiles per row written"}}
     out["bwd_roofline"] = {"bound": "hbm", "achieved": alg_b / t_kb / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                            "frac": alg_b / t_kb / HBM_PEAK, "kernel_ms": t_kb * 1e3, "alg_bytes_per_launch": alg_b,
-                           "traffic": load_traffic("k_gat_in_bwd<8>"),
-                           "kernel": "gala::k_gat_in_bwd<8> (gala_gat_in_bwd_f32, 8 heads x 32 from 100 inputs)"}
+                           "traffic": load_traffic("k_gat_in_bwd<8, true>"),
+                           "kernel": "gala::k_gat_in_bwd<8, true> (gala_gat_in_bwd_t_f32: the T tiles, no walk)"}
+    t_kfw, t_kbw = med(rounds["k_fwd_walk"]), med(rounds["k_bwd_walk"])
+    out["walk"] = {"note": "the previous formulation timed beside: gala_gat_in_fwd_f32 (no T) and "
+                           "gala_gat_in_bwd_f32 gathering the extended rows again over the transposed pattern",
+                   "fwd_kernel_ms": t_kfw * 1e3, "bwd_kernel_ms": t_kbw * 1e3,
+                   "fwd_frac": alg_w / t_kfw / HBM_PEAK, "bwd_frac": alg_wb / t_kbw / HBM_PEAK,
+                   "pair_ms_vs_tmode_pair_ms": [(t_kfw + t_kbw) * 1e3, (t_kf + t_kb) * 1e3]}
     with_traffic_rate(out["roofline"])
     with_traffic_rate(out["bwd_roofline"])
     t_ceil = med(rounds["ceil"])
     if t_ceil:
         out["roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
         out["roofline"]["frac_of_gather_ceiling"] = med([c / f for c, f in zip(rounds["ceil"], rounds["k_fwd"])])
-        out["bwd_roofline"]["gather_ceiling_ms"] = t_ceil * 1e3
-        out["bwd_roofline"]["frac_of_gather_ceiling"] = med([c / b for c, b in zip(rounds["ceil"], rounds["k_bwd"])])
+        # (the T-mode backward gathers nothing: the ceiling applies to the walk's)
+        out["walk"]["gather_ceiling_ms"] = t_ceil * 1e3
+        out["walk"]["fwd_frac_of_gather_ceiling"] = med([c / f for c, f in zip(rounds["ceil"], rounds["k_fwd_walk"])])
+        out["walk"]["bwd_frac_of_gather_ceiling"] = med([c / b for c, b in zip(rounds["ceil"], rounds["k_bwd_walk"])])
     out["interleaved_ms"] = {k: [round(v * 1e3, 3) for v in vs] for k, vs in rounds.items()}
-    del st, f0, xext, Y0, Ym0, sma0
+    del st, f0, xext, Y0, Ym0, sma0, T0
     torch.cuda.empty_cache()
     # the previous formulation on the same layer: the Linear's output (1-KB rows) gathered by
     # the row-statistics pair, timed from that output (kernels only)

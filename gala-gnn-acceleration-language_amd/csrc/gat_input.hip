@@ -156,6 +156,7 @@ struct InFwdParams {
     float *Y, *Ym, *q, *sma;
     int64_t ldy;
     int32_t relu;   // GALA_GAT_IN_RELU: Y = relu(the aggregation) (the layer's NON_LNR_OP_RELU)
+    float *T;       // T mode: the backward's per-column aggregates (see k_gat_in_fwd), else null
 };
 
 // the gathered extended row of edge (4s + kq) of a 16-edge batch: column from the row's
@@ -207,29 +208,34 @@ struct RowCursor {
     int64_t e0 = 0;
     int32_t deg = 0, win = 0;
     float side = 0.0f;     // xext[row * 128 + side_slot]: aL (forward) / aR (backward) of the lane's head
+    float side2 = 0.0f;    // xext[row * 128 + side_slot2] (side_slot2 >= 0): the forward's aR for T
     f4v xa[4], xb[4];      // the row's first batch (requested)
 };
 
 __device__ __forceinline__ void cursor_start(RowCursor &c, const int32_t *rowptr, const int32_t *col,
-                                             const float *xext, int64_t row, int side_slot, bool side_ok, int lane) {
+                                             const float *xext, int64_t row, int side_slot, int side_slot2, bool side_ok,
+                                             int lane) {
     const int n16 = lane & 15, kq = lane >> 4;
     c.e0 = 0;
     c.deg = 0;
     c.side = 0.0f;
+    c.side2 = 0.0f;
     if (row < 0) return;
     c.e0 = uniform(rowptr[row]);
     c.deg = uniform(rowptr[row + 1]) - (int32_t)c.e0;
     c.side = side_ok ? xext[row * kInLd + side_slot] : 0.0f;
+    if (side_slot2 >= 0) c.side2 = side_ok ? xext[row * kInLd + side_slot2] : 0.0f;
     if (c.deg > 0) {
         c.win = col[c.e0 + (lane < c.deg ? lane : c.deg - 1)];
         load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
     }
 }
 
-template <typename BFn>
+// body(xa, xb, j0, deg): the MFMA work of one loaded 16-edge batch
+template <typename Body>
 __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr, const int32_t *col,
-                                            const float *xext, int64_t next, int side_slot, bool side_ok, int lane,
-                                            BFn &&bfn, f4v (&acc)[kInTiles]) {
+                                            const float *xext, int64_t next, int side_slot, int side_slot2,
+                                            bool side_ok, int lane, Body &&body) {
     const int n16 = lane & 15, kq = lane >> 4;
     // the next row's bounds: scalar loads (their own counter), waited for only below
     int64_t ne0 = 0;
@@ -240,7 +246,7 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
         nend = rowptr[nx + 1];
     }
     int32_t nwin = 0;
-    float nside = 0.0f;
+    float nside = 0.0f, nside2 = 0.0f;
     bool next_issued = false;
     auto issue_next = [&]() {
         if (next < 0 || next_issued) return;
@@ -248,6 +254,7 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
         const int32_t nd = nend - (int32_t)ne0;
         if (nd > 0) nwin = col[ne0 + (lane < nd ? lane : nd - 1)];
         nside = side_ok ? xext[next * kInLd + side_slot] : 0.0f;
+        if (side_slot2 >= 0) nside2 = side_ok ? xext[next * kInLd + side_slot2] : 0.0f;
     };
     for (int32_t j0 = 0; j0 < c.deg; j0 += 16) {
         const int32_t j1 = j0 + 16;
@@ -258,7 +265,7 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
             load_batch(xext, c.win, j1, kq, n16, ya, yb);
         }
         if (j0 == 0) issue_next();
-        mfma_batch(c.xa, c.xb, j0, c.deg, kq, n16, bfn, acc);
+        body(c.xa, c.xb, j0, c.deg);
         if (more) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
@@ -272,6 +279,7 @@ __device__ __forceinline__ void cursor_walk(RowCursor &c, const int32_t *rowptr,
     c.deg = next >= 0 ? uniform(nend - (int32_t)ne0) : 0;
     c.win = nwin;
     c.side = nside;
+    c.side2 = nside2;
     if (c.deg > 0) load_batch(xext, c.win, 0, kq, n16, c.xa, c.xb);
 }
 
@@ -292,6 +300,12 @@ __device__ __forceinline__ int fwd_stash(int t, int kq, int s, int v) {
     return ((t * 4 + kq) * kInWaves + s) * 16 + ((v + s) & 15);
 }
 
+// T mode (TM, symmetric pattern): the same walk also forms the backward's per-column
+// aggregates T_h[c] = sum_{r in N(c)} alpha_{r->c},h Xin_ext[r], alpha = p(aL[r] + aR[c]) q[r]
+// (the gathered row carries aL[r] and q[r], the latter from k_gat_in_q), so the backward reads
+// T instead of gathering the extended rows a second time.  Row c's T tiles go to
+// T[((c * 7 + t) * 4 + kq) * 8 + head] (float4s: 896 floats per row).
+template <bool TM>
 __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
     __shared__ f4v stash[kInWaves * 16 * kInTiles * 4];   // fwd_stash
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, n16 = lane & 15, kq = lane >> 4;
@@ -321,12 +335,17 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
         return p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[ri]) : ri;
     };
     const bool side_ok = n16 < p.H;
+    const int side2 = TM ? aR_slot(n16 & 7) : -1;
+    // T mode: q[h] of a gathered row from lane 13 + h / 3 of its edge's 16 lanes, component h % 3
+    const int hq = n16 & 7;
+    const int qsrc = (16 * kq + 13 + hq / 3) * 4, qc = hq % 3;
     RowCursor cur;
-    cursor_start(cur, p.rowptr, p.col, p.xext, row_of(blockIdx.x), aL_slot(n16 & 7), side_ok, lane);
+    cursor_start(cur, p.rowptr, p.col, p.xext, row_of(blockIdx.x), aL_slot(n16 & 7), side2, side_ok, lane);
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        f4v acc[kInTiles];
+        f4v acc[kInTiles], accT[kInTiles];
 #pragma unroll
-        for (int t = 0; t < kInTiles; ++t) acc[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = 0; t < kInTiles; ++t) acc[t] = accT[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        const int64_t myrow = TM ? row_of(blk) : -1;
         // the rows this lane's projection outputs will go to (slots 2 kq, 2 kq + 1), requested
         // before the walk so the stores after the barrier wait on nothing
         int64_t prow[2];
@@ -336,20 +355,40 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
             prow[hs] = si < p.n_rows ? (p.order ? (int64_t)p.order[si] : si) : -1;
         }
         {
-            const float al = cur.side;
+            const float al = cur.side, ar = cur.side2;
             const int H = p.H;
             const float slope = p.slope;
-            cursor_walk(cur, p.rowptr, p.col, p.xext, row_of(blk + gridDim.x), aL_slot(n16 & 7), side_ok, lane,
-                        [&](const f4v &xb, bool ok) {
-                            const float t = __fadd_rn(al, xb[3]);   // lanes v < 8: aR[col][v]
-                            const bool pos = t > 0.0f;
-                            float pv = ref_exp(pos ? t : __fmul_rn(t, slope));
-                            if (!(ok && n16 < H)) pv = 0.0f;
-                            const float mp = pos ? pv : __fmul_rn(pv, slope);
-                            const float mpo = ror8(mp);
-                            return n16 < 8 ? pv : mpo;
-                        },
-                        acc);
+            auto bfn = [&](const f4v &xb, bool ok) {
+                const float t = __fadd_rn(al, xb[3]);   // lanes v < 8: aR[col][v]
+                const bool pos = t > 0.0f;
+                float pv = ref_exp(pos ? t : __fmul_rn(t, slope));
+                if (!(ok && n16 < H)) pv = 0.0f;
+                const float mp = pos ? pv : __fmul_rn(pv, slope);
+                const float mpo = ror8(mp);
+                return n16 < 8 ? pv : mpo;
+            };
+            // the backward's alpha of edge (col -> row): gala_gat_in_bwd's formula
+            auto bfnT = [&](const f4v &xb, bool ok) {
+                const float alr = ror8(xb[3]);            // aL[col][v] from lane v + 8
+                const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
+                const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
+                const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
+                const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
+                const float t = __fadd_rn(alr, ar);
+                const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
+                const float a = __fmul_rn(pv, qr);
+                return (ok && n16 < H) ? a : 0.0f;
+            };
+            cursor_walk(cur, p.rowptr, p.col, p.xext, row_of(blk + gridDim.x), aL_slot(n16 & 7), side2, side_ok, lane,
+                        [&](const f4v (&xa)[4], const f4v (&xb)[4], int32_t j0, int32_t deg) {
+                            mfma_batch(xa, xb, j0, deg, kq, n16, bfn, acc);
+                            if (TM) mfma_batch(xa, xb, j0, deg, kq, n16, bfnT, accT);
+                        });
+        }
+        if (TM && myrow >= 0 && n16 < kInMaxHeads) {
+            f4v *tr = reinterpret_cast<f4v *>(p.T) + myrow * (kInTiles * 4 * kInMaxHeads);
+#pragma unroll
+            for (int t = 0; t < kInTiles; ++t) tr[(t * 4 + kq) * kInMaxHeads + n16] = accT[t];
         }
 #pragma unroll
         for (int t = 0; t < kInTiles; ++t) stash[fwd_stash(t, kq, wave, n16)] = acc[t];
@@ -375,7 +414,8 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
                 // sum p / sum m p: tile 4, float 12 (k-quad 3, component 0) of variants h, h + 8
                 const float S = stf[fwd_stash(4, 3, s, h) * 4];
                 const float Sm = stf[fwd_stash(4, 3, s, h + 8) * 4];
-                const float qv = 1.0f / __fadd_rn(S, 1e-12f);   // REF: 1 / (1e-12 + sum p)
+                // REF: 1 / (1e-12 + sum p); T mode: k_gat_in_q's (the sequential row sum)
+                const float qv = TM ? p.xext[row * kInLd + q_slot(h)] : 1.0f / __fadd_rn(S, 1e-12f);
 #pragma unroll
                 for (int nt = 0; nt < 2; ++nt) {
                     const int j = 16 * nt + n16;
@@ -389,7 +429,7 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_fwd(InFwdParams p) {
                 if (n16 == 0) {
                     p.q[row * p.H + h] = qv;
                     p.sma[row * p.H + h] = __fmul_rn(qv, Sm);
-                    p.xext[row * kInLd + q_slot(h)] = qv;
+                    if (!TM) p.xext[row * kInLd + q_slot(h)] = qv;
                 }
             }
         }
@@ -407,6 +447,7 @@ struct InBwdParams {
     float *daL;
     float *part;
     int32_t relu;   // Y holds relu(the aggregation): dY is masked by Y > 0 (torch's threshold_backward)    // [gridDim][H][2][kInTiles][64][4]
+    const float *T; // T mode: the forward's per-column aggregates (no walk over the pattern)
 };
 
 template <int DW>   // lanes per head in the row-local d_aL dots: D / 4
@@ -425,7 +466,7 @@ constexpr int kBwdHead = kInTiles * 16 + 4;             // 116 floats
 constexpr int kBwdSlot = kInMaxHeads * kBwdHead + 16;   // 944 floats: slots s, s + 1 16 banks apart
 constexpr int kDyLd = 4 * (kWave + 4);                  // 272 floats of dY per slot
 
-template <int DW>
+template <int DW, bool TM>
 __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
     __shared__ f4v stash[kInWaves * kBwdSlot / 4];   // see kBwdSlot
     __shared__ f4v dstash[kInWaves * kDyLd / 4];     // [slot][kDyLd]: the columns' dY (masked)
@@ -449,7 +490,7 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
     };
     const bool side_ok = n16 < p.H;
     RowCursor cur;
-    cursor_start(cur, p.rowptr, p.col, p.xext, col_of(blockIdx.x), aR_slot(n16 & 7), side_ok, lane);
+    if (!TM) cursor_start(cur, p.rowptr, p.col, p.xext, col_of(blockIdx.x), aR_slot(n16 & 7), -1, side_ok, lane);
     for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         f4v acc[kInTiles];
 #pragma unroll
@@ -468,23 +509,31 @@ __global__ __launch_bounds__(kInBlock, 2) void k_gat_in_bwd(InBwdParams p) {
                 for (int i = 0; i < 4; ++i) dy[i] = yy[i] > 0.0f ? dy[i] : 0.0f;
             }
         }
-        {
+        if (TM) {   // the forward's T tiles of column c (k_gat_in_fwd<true>)
+            if (c >= 0 && n16 < kInMaxHeads) {
+                const f4v *tr = reinterpret_cast<const f4v *>(p.T) + c * (kInTiles * 4 * kInMaxHeads);
+#pragma unroll
+                for (int t = 0; t < kInTiles; ++t) acc[t] = tr[(t * 4 + kq) * kInMaxHeads + n16];
+            }
+        } else {
             const float ar = cur.side;
             const int H = p.H;
             const float slope = p.slope;
-            cursor_walk(cur, p.rowptr, p.col, p.xext, col_of(blk + gridDim.x), aR_slot(n16 & 7), side_ok, lane,
-                        [&](const f4v &xb, bool ok) {
-                            const float alr = ror8(xb[3]);            // aL[r][v] from lane v + 8
-                            const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
-                            const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
-                            const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
-                            const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
-                            const float t = __fadd_rn(alr, ar);
-                            const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
-                            const float a = __fmul_rn(pv, qr);       // K8: alpha = p * q[row]
-                            return (ok && n16 < H) ? a : 0.0f;
-                        },
-                        acc);
+            auto bfn = [&](const f4v &xb, bool ok) {
+                const float alr = ror8(xb[3]);            // aL[r][v] from lane v + 8
+                const float q0 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[0])));
+                const float q1 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[1])));
+                const float q2 = __int_as_float(__builtin_amdgcn_ds_bpermute(qsrc, __float_as_int(xb[2])));
+                const float qr = qc == 0 ? q0 : (qc == 1 ? q1 : q2);
+                const float t = __fadd_rn(alr, ar);
+                const float pv = ref_exp(t > 0.0f ? t : __fmul_rn(t, slope));
+                const float a = __fmul_rn(pv, qr);       // K8: alpha = p * q[row]
+                return (ok && n16 < H) ? a : 0.0f;
+            };
+            cursor_walk(cur, p.rowptr, p.col, p.xext, col_of(blk + gridDim.x), aR_slot(n16 & 7), -1, side_ok, lane,
+                        [&](const f4v (&xa)[4], const f4v (&xb)[4], int32_t j0, int32_t deg) {
+                            mfma_batch(xa, xb, j0, deg, kq, n16, bfn, acc);
+                        });
         }
         if (c >= 0) {   // d_aL[c] from the forward's row statistics (gala_gat_bwd_stats_f32's formula)
             float syy = 0.0f, sym = 0.0f;
@@ -557,6 +606,49 @@ __global__ __launch_bounds__(kBlock) void k_gat_in_reduce(const float *part, int
     M[((int64_t)h * D + j) * (fin + 1) + (f == -2 ? fin : f)] = s;
 }
 
+// T mode's row sums before the forward: q_h[r] = 1 / (1e-12 + sum_e p(aL[r] + aR[c_e])) for every
+// row (the forward's T tiles read q of the rows they gather), 8 lanes per row (lane = head),
+// each summing its head's p over the row's edges in CSR order -- the reference's sequential
+// row sum (K7) -- into the row's q slots of the extended table.
+// the rows' aR in a compact [n][8] table (78 MB at the Products shape: the q pass's gathers
+// hit the MALL instead of fetching a 128-B line of the 1.25 GB extended table per edge)
+__global__ __launch_bounds__(kBlock) void k_gat_in_ar(const float *xext, int64_t n_rows, float *ar) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n_rows * 8) ar[i] = xext[(i >> 3) * kInLd + aR_slot((int)(i & 7))];
+}
+
+__global__ __launch_bounds__(kBlock) void k_gat_in_q(const int32_t *rowptr, const int32_t *col, int64_t n_rows,
+                                                     int32_t H, float slope, const float *art, float *xext) {
+    const int h = threadIdx.x & 7;
+    const int64_t g0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 3, gstep = ((int64_t)gridDim.x * kBlock) >> 3;
+    for (int64_t r = g0; r < n_rows; r += gstep) {
+        if (h >= H) continue;
+        const int64_t e0 = rowptr[r], e1 = rowptr[r + 1];
+        const float al = xext[r * kInLd + aL_slot(h)];
+        float S = 0.0f;
+        // 8 edges per step, the next step's column indices requested before this step's sums
+        constexpr int U = 8;
+        int32_t cn[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) cn[k] = e0 + k < e1 ? col[e0 + k] : 0;
+        for (int64_t e = e0; e < e1; e += U) {
+            float ar[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) ar[k] = art[(int64_t)cn[k] * 8 + h];
+#pragma unroll
+            for (int k = 0; k < U; ++k) cn[k] = e + U + k < e1 ? col[e + U + k] : 0;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                if (e + k < e1) {
+                    const float t = __fadd_rn(al, ar[k]);
+                    S = __fadd_rn(S, ref_exp(t > 0.0f ? t : __fmul_rn(t, slope)));
+                }
+            }
+        }
+        xext[r * kInLd + q_slot(h)] = 1.0f / __fadd_rn(S, 1e-12f);
+    }
+}
+
 int grid_for(int64_t n_rows) {
     const int64_t nblk = (n_rows + kInWaves - 1) / kInWaves;
     return (int)std::min<int64_t>(std::max<int64_t>(nblk, 1), kInGrid);
@@ -590,20 +682,50 @@ extern "C" int gala_gat_in_prep_f32(int64_t n, int32_t fin, const float *Xin, in
     return launch_status();
 }
 
-extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
-                                   float slope,
-                                   float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
-                                   int64_t ldy, float *q, float *sma, int32_t flags, void *stream) {
+namespace {
+int fwd_launch(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D, float slope,
+               float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym, int64_t ldy, float *q,
+               float *sma, int32_t flags, float *T, void *stream) {
     int st = check_in_graph(A, fin, heads, D);
     if (st) return st;
     if (ldw < fin || ldy < (int64_t)heads * D || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (A->n_rows == 0) return GALA_OK;
-    if (!Xext || !W || !Y || !Ym || !q || !sma || ((uintptr_t)Xext & 15)) return GALA_ERR_INVALID_ARG;
+    if (!Xext || !W || !Y || !Ym || !q || !sma || ((uintptr_t)Xext & 15) || ((uintptr_t)T & 15))
+        return GALA_ERR_INVALID_ARG;
     InFwdParams p{A->rowptr, A->col, order ? order : (A->split ? A->split->row_order : nullptr), A->n_rows, Xext, W,
                   b, ldw,
-                  fin, heads, D, slope, Y, Ym, q, sma, ldy, (flags & GALA_GAT_IN_RELU) ? 1 : 0};
-    hipLaunchKernelGGL(k_gat_in_fwd, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, (hipStream_t)stream, p);
+                  fin, heads, D, slope, Y, Ym, q, sma, ldy, (flags & GALA_GAT_IN_RELU) ? 1 : 0, T};
+    hipStream_t hs = (hipStream_t)stream;
+    if (T) {
+        // T's first 8 n floats hold the compact aR table until the forward writes T
+        hipLaunchKernelGGL(k_gat_in_ar, dim3((unsigned)((A->n_rows * 8 + kBlock - 1) / kBlock)), dim3(kBlock), 0, hs,
+                           Xext, A->n_rows, T);
+        if ((st = launch_status())) return st;
+        const int64_t groups = (A->n_rows + kBlock / 8 - 1) / (kBlock / 8);
+        hipLaunchKernelGGL(k_gat_in_q, dim3((unsigned)std::min<int64_t>(groups, 8192)), dim3(kBlock), 0, hs,
+                           A->rowptr, A->col, A->n_rows, heads, slope, T, Xext);
+        if ((st = launch_status())) return st;
+        hipLaunchKernelGGL(k_gat_in_fwd<true>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, hs, p);
+    } else {
+        hipLaunchKernelGGL(k_gat_in_fwd<false>, dim3(grid_for(A->n_rows)), dim3(kInBlock), 0, hs, p);
+    }
     return launch_status();
+}
+}  // namespace
+
+extern "C" int gala_gat_in_fwd_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                   float slope,
+                                   float *Xext, const float *W, int64_t ldw, const float *b, float *Y, float *Ym,
+                                   int64_t ldy, float *q, float *sma, int32_t flags, void *stream) {
+    return fwd_launch(A, order, fin, heads, D, slope, Xext, W, ldw, b, Y, Ym, ldy, q, sma, flags, nullptr, stream);
+}
+
+extern "C" int gala_gat_in_fwd_t_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                     float slope, float *Xext, const float *W, int64_t ldw, const float *b, float *Y,
+                                     float *Ym, int64_t ldy, float *q, float *sma, int32_t flags, float *T,
+                                     void *stream) {
+    if (!T) return GALA_ERR_INVALID_ARG;
+    return fwd_launch(A, order, fin, heads, D, slope, Xext, W, ldw, b, Y, Ym, ldy, q, sma, flags, T, stream);
 }
 
 extern "C" int64_t gala_gat_in_bwd_workspace(int32_t heads) {
@@ -611,42 +733,75 @@ extern "C" int64_t gala_gat_in_bwd_workspace(int32_t heads) {
     return (int64_t)kInGrid * heads * 2 * kInTiles * 64 * 4 * (int64_t)sizeof(float);
 }
 
-extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
-                                   float slope,
-                                   const float *Xext, const float *dY, const float *Y, const float *Ym,
-                                   int64_t ldy, const float *sma, float *daL, float *M, void *ws_,
-                                   int64_t ws_bytes, int32_t flags, void *stream) {
+namespace {
+// AT: the transposed pattern (walked), or null with T: the forward's T tiles of n_rows columns
+int bwd_launch(const gala_csr_t *AT, int64_t n_rows, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+               float slope, const float *Xext, const float *T, const float *dY, const float *Y, const float *Ym,
+               int64_t ldy, const float *sma, float *daL, float *M, void *ws_, int64_t ws_bytes, int32_t flags,
+               void *stream) {
     float *ws = (float *)ws_;
-    int st = check_in_graph(AT, fin, heads, D);
-    if (st) return st;
+    int st;
+    if (AT) {
+        if ((st = check_in_graph(AT, fin, heads, D))) return st;
+        n_rows = AT->n_rows;
+    } else {
+        if (n_rows < 0 || fin < 1 || heads < 1 || D < 1) return GALA_ERR_INVALID_ARG;
+        if (fin > kInMaxFin || heads > kInMaxHeads || !(D == 4 || D == 8 || D == 16 || D == 32))
+            return GALA_ERR_UNSUPPORTED;
+    }
     if (ldy < (int64_t)heads * D || (ldy & 3) || (flags & ~GALA_GAT_IN_RELU)) return GALA_ERR_INVALID_ARG;
     if (!M) return GALA_ERR_INVALID_ARG;
     hipStream_t hs = (hipStream_t)stream;
     const int64_t outn = (int64_t)heads * D * (fin + 1);
-    if (AT->n_rows == 0) {
+    if (n_rows == 0) {
         return hipMemsetAsync(M, 0, outn * sizeof(float), hs) == hipSuccess ? GALA_OK : GALA_ERR_HIP;
     }
-    if (!Xext || !dY || !Y || !Ym || !sma || !daL || !ws || ((uintptr_t)Xext & 15) || ((uintptr_t)dY & 15) ||
-        ((uintptr_t)Y & 15) || ((uintptr_t)Ym & 15))
+    if ((AT ? (!Xext || ((uintptr_t)Xext & 15)) : (!T || ((uintptr_t)T & 15))) || !dY || !Y || !Ym || !sma || !daL ||
+        !ws || ((uintptr_t)dY & 15) || ((uintptr_t)Y & 15) || ((uintptr_t)Ym & 15))
         return GALA_ERR_INVALID_ARG;
     if (ws_bytes < gala_gat_in_bwd_workspace(heads)) return GALA_ERR_INVALID_ARG;
-    const int grid = grid_for(AT->n_rows);
-    InBwdParams p{AT->rowptr, AT->col, order ? order : (AT->split ? AT->split->row_order : nullptr), AT->n_rows, Xext,
-                  dY, Y, Ym,
-                  sma, ldy, fin, heads, D, slope, daL, ws, (flags & GALA_GAT_IN_RELU) ? 1 : 0};
+    const int grid = grid_for(n_rows);
+    const int32_t *ord = order ? order : (AT && AT->split ? AT->split->row_order : nullptr);
+    InBwdParams p{AT ? AT->rowptr : nullptr, AT ? AT->col : nullptr, ord, n_rows, Xext, dY, Y, Ym,
+                  sma, ldy, fin, heads, D, slope, daL, ws, (flags & GALA_GAT_IN_RELU) ? 1 : 0, T};
     if (hipMemsetAsync(M, 0, outn * sizeof(float), hs) != hipSuccess) return GALA_ERR_HIP;
+#define GALA_IN_BWD(DW)                                                                           \
+    do {                                                                                          \
+        if (AT) hipLaunchKernelGGL((k_gat_in_bwd<DW, false>), dim3(grid), dim3(kInBlock), 0, hs, p); \
+        else hipLaunchKernelGGL((k_gat_in_bwd<DW, true>), dim3(grid), dim3(kInBlock), 0, hs, p);     \
+    } while (0)
     switch (D / 4) {
-    case 1: hipLaunchKernelGGL(k_gat_in_bwd<1>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 2: hipLaunchKernelGGL(k_gat_in_bwd<2>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    case 4: hipLaunchKernelGGL(k_gat_in_bwd<4>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
-    default: hipLaunchKernelGGL(k_gat_in_bwd<8>, dim3(grid), dim3(kInBlock), 0, hs, p); break;
+    case 1: GALA_IN_BWD(1); break;
+    case 2: GALA_IN_BWD(2); break;
+    case 4: GALA_IN_BWD(4); break;
+    default: GALA_IN_BWD(8); break;
     }
+#undef GALA_IN_BWD
     st = launch_status();
     if (st) return st;
     const int64_t per = (int64_t)heads * 2 * kInTiles * 64 * 4;
     hipLaunchKernelGGL(k_gat_in_reduce, dim3((unsigned)((per + kBlock - 1) / kBlock)), dim3(kBlock), 0, hs,
                        (const float *)ws, grid, heads, D, fin, M);
     return launch_status();
+}
+}  // namespace
+
+extern "C" int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                   float slope,
+                                   const float *Xext, const float *dY, const float *Y, const float *Ym,
+                                   int64_t ldy, const float *sma, float *daL, float *M, void *ws_,
+                                   int64_t ws_bytes, int32_t flags, void *stream) {
+    if (!AT) return GALA_ERR_INVALID_ARG;
+    return bwd_launch(AT, 0, order, fin, heads, D, slope, Xext, nullptr, dY, Y, Ym, ldy, sma, daL, M, ws_, ws_bytes,
+                      flags, stream);
+}
+
+extern "C" int gala_gat_in_bwd_t_f32(int64_t n_rows, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                                     const float *T, const float *dY, const float *Y, const float *Ym, int64_t ldy,
+                                     const float *sma, float *daL, float *M, void *ws_, int64_t ws_bytes,
+                                     int32_t flags, void *stream) {
+    return bwd_launch(nullptr, n_rows, order, fin, heads, D, 0.0f, nullptr, T, dY, Y, Ym, ldy, sma, daL, M, ws_,
+                      ws_bytes, flags, stream);
 }
 
 }  // namespace gala

@@ -157,6 +157,10 @@ SIGNATURES = {
     "gala_gat_in_bwd_workspace": (ctypes.c_int64, [_I32]),
     "gala_gat_in_bwd_f32": (ctypes.c_int, [_CSR, _P, _I32, _I32, _I32, _F, _P, _P, _P, _P, _I64, _P, _P, _P, _P,
                                            _I64, _I32, _P]),
+    "gala_gat_in_fwd_t_f32": (ctypes.c_int, [_CSR, _P, _I32, _I32, _I32, _F, _P, _P, _I64, _P, _P, _P, _I64, _P,
+                                             _P, _I32, _P, _P]),
+    "gala_gat_in_bwd_t_f32": (ctypes.c_int, [_I64, _P, _I32, _I32, _I32, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _I64,
+                                             _I32, _P]),
 }
 
 
@@ -175,7 +179,7 @@ _lib = None
 
 
 GALA_GAT_IN_RELU = 1
-ABI_VERSION = 5  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
+ABI_VERSION = 6  # GALA_ABI_VERSION of include/gala_hip.h these bindings mirror
 
 
 def lib() -> ctypes.CDLL:

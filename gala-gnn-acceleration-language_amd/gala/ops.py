@@ -572,29 +572,43 @@ def gat_in_prep(X, u, c, heads, xext=None):
     return xext
 
 
-def gat_in_fwd(g: DeviceGraph, xext, W, b, heads, fin, slope=0.2, order=None, relu=False):
-    """gala_gat_in_fwd_f32: (Y, Ym, q, sma); writes q into xext.  order: int32 row order."""
+def gat_in_fwd(g: DeviceGraph, xext, W, b, heads, fin, slope=0.2, order=None, relu=False, T=None):
+    """gala_gat_in_fwd_f32: (Y, Ym, q, sma); writes q into xext.  order: int32 row order.
+    T ([N, 896], symmetric g only): gala_gat_in_fwd_t_f32, which also forms the backward's
+    per-column aggregates there."""
     F = W.shape[0]
     D = F // heads
     Y = torch.empty(g.n_rows, F, device=W.device, dtype=torch.float32)
     Ym = torch.empty_like(Y)
     q = torch.empty(g.n_rows, heads, device=W.device, dtype=torch.float32)
     sma = torch.empty_like(q)
-    _abi.call("gala_gat_in_fwd_f32", g.csr(0), _dp(order), fin, heads, D, slope, _dp(xext), _dp(W), W.stride(0), _dp(b),
-              _dp(Y), _dp(Ym), F, _dp(q), _dp(sma), _abi.GALA_GAT_IN_RELU if relu else 0, _stream())
+    flags = _abi.GALA_GAT_IN_RELU if relu else 0
+    if T is None:
+        _abi.call("gala_gat_in_fwd_f32", g.csr(0), _dp(order), fin, heads, D, slope, _dp(xext), _dp(W), W.stride(0),
+                  _dp(b), _dp(Y), _dp(Ym), F, _dp(q), _dp(sma), flags, _stream())
+    else:
+        _abi.call("gala_gat_in_fwd_t_f32", g.csr(0), _dp(order), fin, heads, D, slope, _dp(xext), _dp(W),
+                  W.stride(0), _dp(b), _dp(Y), _dp(Ym), F, _dp(q), _dp(sma), flags, _dp(T), _stream())
     return Y, Ym, q, sma
 
 
-def gat_in_bwd(gT: DeviceGraph, xext, dY, Y, Ym, sma, heads, fin, slope=0.2, order=None, relu=False):
-    """gala_gat_in_bwd_f32 over the transposed pattern gT: (d_aL [N, H], M [H, D, fin + 1])."""
+def gat_in_bwd(gT: DeviceGraph, xext, dY, Y, Ym, sma, heads, fin, slope=0.2, order=None, relu=False, T=None):
+    """gala_gat_in_bwd_f32 over the transposed pattern gT: (d_aL [N, H], M [H, D, fin + 1]);
+    with T (the T-mode forward's), gala_gat_in_bwd_t_f32 (no walk over the pattern)."""
     F = dY.shape[1]
     D = F // heads
-    daL = torch.empty(gT.n_rows, heads, device=dY.device, dtype=torch.float32)
+    n = dY.shape[0]
+    daL = torch.empty(n, heads, device=dY.device, dtype=torch.float32)
     M = torch.empty(heads, D, fin + 1, device=dY.device, dtype=torch.float32)
     wsb = _abi.lib().gala_gat_in_bwd_workspace(heads)
     ws = torch.empty(max(wsb // 4, 1), device=dY.device, dtype=torch.float32)
-    _abi.call("gala_gat_in_bwd_f32", gT.csr(0), _dp(order), fin, heads, D, slope, _dp(xext), _dp(dY), _dp(Y), _dp(Ym), F,
-              _dp(sma), _dp(daL), _dp(M), _dp(ws), wsb, _abi.GALA_GAT_IN_RELU if relu else 0, _stream())
+    flags = _abi.GALA_GAT_IN_RELU if relu else 0
+    if T is None:
+        _abi.call("gala_gat_in_bwd_f32", gT.csr(0), _dp(order), fin, heads, D, slope, _dp(xext), _dp(dY), _dp(Y),
+                  _dp(Ym), F, _dp(sma), _dp(daL), _dp(M), _dp(ws), wsb, flags, _stream())
+    else:
+        _abi.call("gala_gat_in_bwd_t_f32", n, _dp(order), fin, heads, D, _dp(T), _dp(dY), _dp(Y), _dp(Ym), F,
+                  _dp(sma), _dp(daL), _dp(M), _dp(ws), wsb, flags, _stream())
     return daL, M
 
 
@@ -607,7 +621,7 @@ def degree_order(rowptr):
 
 
 def gat_input_layer(g: DeviceGraph, X, W, b, wL, bL, wR, bR, heads, slope=0.2, dY=None, gT=None, order=None,
-                    order_t=None, relu=False):
+                    order_t=None, relu=False, tmode=False):
     """Config 3's layer 1 in input space through the C ABI, the composition of the mirror's
     GatInputLayer: forward (Y, q, sma, xext) and, with dY, the gradients
     {W, b, wL, bL, wR, bR} (REF: d aR = d aL) and d_aL.  gT: the transposed pattern (default g,
@@ -616,12 +630,15 @@ def gat_input_layer(g: DeviceGraph, X, W, b, wL, bL, wR, bR, heads, slope=0.2, d
     H, D = heads, F // heads
     u, c = gat_in_compose(W, b, wL, bL, wR, bR, heads)
     xext = gat_in_prep(X, u, c, heads)
-    Y, Ym, q, sma = gat_in_fwd(g, xext, W, b, heads, fin, slope, order=order, relu=relu)
-    out = {"Y": Y, "Ym": Ym, "q": q, "sma": sma, "xext": xext}
+    # T mode (tmode, the symmetric g of an undirected program: gT None): the forward also forms
+    # the backward's per-column aggregates
+    T = torch.empty(g.n_rows, 896, device=X.device, dtype=torch.float32) if tmode and gT is None else None
+    Y, Ym, q, sma = gat_in_fwd(g, xext, W, b, heads, fin, slope, order=order, relu=relu, T=T)
+    out = {"Y": Y, "Ym": Ym, "q": q, "sma": sma, "xext": xext, "T": T}
     if dY is None:
         return out
     daL, M = gat_in_bwd(g if gT is None else gT, xext, dY, Y, Ym, sma, heads, fin, slope,
-                        order=order if gT is None else order_t, relu=relu)
+                        order=order if gT is None else order_t, relu=relu, T=T)
     Gw, Gb = dense_grad(X, daL)
     sLR = wL.reshape(H, D) + wR.reshape(H, D)
     bb = b.reshape(H, D) if b is not None else torch.zeros(H, D, device=W.device)

@@ -51,6 +51,8 @@ struct Backend {
     decltype(&gala_gat_in_fwd_f32) gat_in_fwd;
     decltype(&gala_gat_in_bwd_workspace) gat_in_ws;
     decltype(&gala_gat_in_bwd_f32) gat_in_bwd;
+    decltype(&gala_gat_in_fwd_t_f32) gat_in_fwd_t;   // T mode: GPU only (null on the host backend)
+    decltype(&gala_gat_in_bwd_t_f32) gat_in_bwd_t;
 };
 const Backend kHip{gala_spmm_ex_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_row_scale_relu_f32, gala_relu_scale_backward_f32, gala_ffn_fwd_f32,
@@ -62,7 +64,8 @@ const Backend kHip{gala_spmm_ex_f32, gala_degree_f32, gala_row_broadcast_f32,
                    gala_gat_fwd_stats_f32, gala_gat_bwd_stats_f32, gala_gat_bwd_stats_linear_f32,
                    gala_head_attn_f32, gala_head_attn_bwd_f32,
                    gala_edge_permute_f32, gala_dense_grad_workspace, gala_dense_grad_f32,
-                   gala_gat_in_prep_f32, gala_gat_in_fwd_f32, gala_gat_in_bwd_workspace, gala_gat_in_bwd_f32};
+                   gala_gat_in_prep_f32, gala_gat_in_fwd_f32, gala_gat_in_bwd_workspace, gala_gat_in_bwd_f32,
+                   gala_gat_in_fwd_t_f32, gala_gat_in_bwd_t_f32};
 const Backend kCpu{gala_cpu_spmm_ex_f32, gala_cpu_degree_f32, gala_cpu_row_broadcast_f32,
                    gala_cpu_row_scale_relu_f32, gala_cpu_relu_scale_backward_f32, gala_cpu_ffn_fwd_f32,
                    gala_cpu_sddvv_f32, gala_cpu_row_sum_f32, gala_cpu_row_scale_f32,
@@ -74,7 +77,7 @@ const Backend kCpu{gala_cpu_spmm_ex_f32, gala_cpu_degree_f32, gala_cpu_row_broad
                    gala_cpu_head_attn_f32, gala_cpu_head_attn_bwd_f32,
                    gala_cpu_edge_permute_f32, gala_cpu_dense_grad_workspace,
                    gala_cpu_dense_grad_f32, gala_cpu_gat_in_prep_f32, gala_cpu_gat_in_fwd_f32,
-                   gala_cpu_gat_in_bwd_workspace, gala_cpu_gat_in_bwd_f32};
+                   gala_cpu_gat_in_bwd_workspace, gala_cpu_gat_in_bwd_f32, nullptr, nullptr};
 
 const Backend &be(const torch::Tensor &t) {
     TORCH_CHECK(t.is_cuda() || t.is_cpu(), "gala: unsupported device ", t.device());
@@ -1488,6 +1491,7 @@ torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, tor
 // GatAggregateFfn), regrouped.  X itself gets no gradient (the layer's input is the
 // dataset's features); the apply wrapper keeps the three-op chain whenever X needs one.
 const PatternT &transposed_pattern(int64_t idx);
+bool gat_in_tmode_enabled();
 
 struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor W, torch::Tensor b,
@@ -1519,22 +1523,36 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         auto q = torch::empty({N, H}, fopts(x)), sma = torch::empty({N, H}, fopts(x));
         torch::Tensor bc = has_b ? b.contiguous() : torch::Tensor();
         const PatternT &pt = transposed_pattern(2 * li);
-        check(B.gat_in_fwd(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
-                           w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr, Y.data_ptr<float>(),
-                           Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(),
-                           relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
-              "gala_gat_in_fwd_f32");
+        // T mode (GPU, symmetric pattern, gradients wanted): the forward also forms the
+        // backward's per-column aggregates, so the backward does not walk the graph again
+        const bool grad = ctx->needs_input_grad(1) || ctx->needs_input_grad(2) || ctx->needs_input_grad(3) ||
+                          ctx->needs_input_grad(4) || ctx->needs_input_grad(5) || ctx->needs_input_grad(6);
+        const bool tmode = grad && B.gat_in_fwd_t && pt.symmetric && gat_in_tmode_enabled();
+        torch::Tensor T = tmode ? torch::empty({N, 896}, fopts(x)) : torch::empty({0}, fopts(x));
+        if (tmode)
+            check(B.gat_in_fwd_t(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope,
+                                 xext.data_ptr<float>(), w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr,
+                                 Y.data_ptr<float>(), Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(),
+                                 relu ? GALA_GAT_IN_RELU : 0, T.data_ptr<float>(), stream_of(x)),
+                  "gala_gat_in_fwd_t_f32");
+        else
+            check(B.gat_in_fwd(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+                               w.data_ptr<float>(), fin, has_b ? bc.data_ptr<float>() : nullptr, Y.data_ptr<float>(),
+                               Ym.data_ptr<float>(), F, q.data_ptr<float>(), sma.data_ptr<float>(),
+                               relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
+                  "gala_gat_in_fwd_f32");
         ctx->saved_data["li"] = li;
         ctx->saved_data["slope"] = slope;
         ctx->saved_data["heads"] = heads;
         ctx->saved_data["has_b"] = has_b;
         ctx->saved_data["relu"] = relu;
-        ctx->save_for_backward({x, w, has_b ? bc : torch::empty({0}, fopts(x)), wL, wR, xext, Y, Ym, sma});
+        ctx->save_for_backward({x, w, has_b ? bc : torch::empty({0}, fopts(x)), wL, wR, xext, Y, Ym, sma, T});
         return Y;
     }
     static tensor_list backward(AutogradContext *ctx, tensor_list grad_outputs) {
         auto sv = ctx->get_saved_variables();
-        auto x = sv[0], w = sv[1], b = sv[2], wL = sv[3], wR = sv[4], xext = sv[5], Y = sv[6], Ym = sv[7], sma = sv[8];
+        auto x = sv[0], w = sv[1], b = sv[2], wL = sv[3], wR = sv[4], xext = sv[5], Y = sv[6], Ym = sv[7], sma = sv[8],
+             T = sv[9];
         const int64_t li = ctx->saved_data["li"].toInt(), H = ctx->saved_data["heads"].toInt();
         const double slope = ctx->saved_data["slope"].toDouble();
         const bool has_b = ctx->saved_data["has_b"].toBool(), relu = ctx->saved_data["relu"].toBool();
@@ -1552,11 +1570,18 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         const int64_t wsb = B.gat_in_ws((int32_t)H);
         TORCH_CHECK(wsb > 0, "gala: gala_gat_in_bwd_workspace failed");
         auto ws = torch::empty({wsb / 4}, fopts(x));
-        check(B.gat_in_bwd(&cv.c, pt.order_t.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
-                           dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F, sma.data_ptr<float>(),
-                           daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb,
-                           relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
-              "gala_gat_in_bwd_f32");
+        if (T.numel() > 0)   // T mode: the forward's per-column aggregates
+            check(B.gat_in_bwd_t(N, pt.order_t.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D,
+                                 T.data_ptr<float>(), dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F,
+                                 sma.data_ptr<float>(), daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(),
+                                 wsb, relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
+                  "gala_gat_in_bwd_t_f32");
+        else
+            check(B.gat_in_bwd(&cv.c, pt.order_t.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope, xext.data_ptr<float>(),
+                               dY.data_ptr<float>(), Y.data_ptr<float>(), Ym.data_ptr<float>(), F, sma.data_ptr<float>(),
+                               daL.data_ptr<float>(), M.data_ptr<float>(), ws.data_ptr<float>(), wsb,
+                               relu ? GALA_GAT_IN_RELU : 0, stream_of(x)),
+                  "gala_gat_in_bwd_f32");
         // G = d_aL^T X (and its column sums): the attention Linears' terms
         auto Gw = torch::empty({H, fin}, fopts(x)), Gb = torch::empty({H}, fopts(x));
         const int64_t gws = B.dense_ws(N, (int32_t)fin, (int32_t)H);
@@ -1614,6 +1639,15 @@ const PatternT &transposed_pattern(int64_t idx) {
     }
     pt = p;
     return *pt;
+}
+
+// GALA_GAT_IN_T=0 keeps the backward's own walk over the pattern (A/B runs)
+bool gat_in_tmode_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("GALA_GAT_IN_T");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // GALA_GAT_INPUT=0 keeps the three-op chain (A/B runs, the tests' reference spelling)

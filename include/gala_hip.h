@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GALA_ABI_VERSION 5
+#define GALA_ABI_VERSION 6
 
 typedef enum gala_status {
     GALA_OK = 0,
@@ -594,6 +594,19 @@ int gala_gat_in_bwd_f32(const gala_csr_t *AT, const int32_t *order, int32_t fin,
                         const float *Xext, const float *dY, const float *Y, const float *Ym,
                         int64_t ldy, const float *sma, float *daL, float *M, void *ws,
                         int64_t ws_bytes, int32_t flags, void *stream);
+/* T mode (round 6; symmetric A only -- A equal to its transpose, which the caller checks):
+ *   gala_gat_in_fwd_t_f32: gala_gat_in_fwd_f32 that first sums q for every row (a pass over the
+ *     aR of each row's columns, in CSR order) and then, in the same walk as Y, forms the
+ *     backward's per-column aggregates T [n][896] (16-B aligned; 3.5 KB per row) -- so
+ *     gala_gat_in_bwd_t_f32 reads T and dY instead of gathering the extended rows again.
+ *   gala_gat_in_bwd_t_f32: gala_gat_in_bwd_f32's outputs (d_aL, M) from T; no graph. */
+int gala_gat_in_fwd_t_f32(const gala_csr_t *A, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                          float slope, float *Xext, const float *W, int64_t ldw, const float *b, float *Y,
+                          float *Ym, int64_t ldy, float *q, float *sma, int32_t flags, float *T, void *stream);
+int gala_gat_in_bwd_t_f32(int64_t n_rows, const int32_t *order, int32_t fin, int32_t heads, int32_t D,
+                          const float *T, const float *dY, const float *Y, const float *Ym, int64_t ldy,
+                          const float *sma, float *daL, float *M, void *ws, int64_t ws_bytes, int32_t flags,
+                          void *stream);
 
 /* dst[i*heads + h] = src[perm[i]*heads + h]  (edge-value permutation for transposed graphs) */
 int gala_edge_permute_f32(const int32_t *perm, const float *src, int64_t n, int32_t heads,

@@ -45,7 +45,7 @@ def test_version_and_status_strings():
     L = _abi.lib()
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "gala_hip.h")).read()
     declared = int(re.search(r"#define GALA_ABI_VERSION (\d+)", hdr).group(1))
-    assert L.gala_abi_version() == declared == _abi.ABI_VERSION == 5
+    assert L.gala_abi_version() == declared == _abi.ABI_VERSION == 6
     assert L.gala_status_string(0) == b"GALA_OK"
     assert L.gala_status_string(-4) == b"GALA_ERR_GRAPH"
 

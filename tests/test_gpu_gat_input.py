@@ -29,14 +29,14 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, gT=None, relu=False, order=None):
+def gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, gT=None, relu=False, order=None, tmode=False):
     dg = ops.DeviceGraph.from_host(g, split=False)
     dgT = None if gT is None else ops.DeviceGraph.from_host(gT, split=False)
     od = None if order is None else dev(order)
     out = ops.gat_input_layer(dg, dev(X), dev(W), dev(b), dev(wL), dev(bL), dev(wR), dev(bR), heads,
-                              dY=dev(dY), gT=dgT, relu=relu, order=od, order_t=od)
+                              dY=dev(dY), gT=dgT, relu=relu, order=od, order_t=od, tmode=tmode)
     torch.cuda.synchronize()
-    return {k: v.cpu().numpy() for k, v in out.items()}
+    return {k: v.cpu().numpy() for k, v in out.items() if v is not None and k != "T"}
 
 
 def check_against_ref(got, ref):
@@ -59,6 +59,10 @@ def test_input_space_kernels_against_the_reference_chain(fin, heads, D):
     gr = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, relu=True, order=ops.degree_order(g.rowptr))
     rr = ref_on_own_logits(g, gr, X, W, b, wL, bL, wR, bR, dY, heads, relu=True)
     check_against_ref(gr, rr)
+    # T mode (gala_gat_in_{fwd,bwd}_t_f32: the backward's aggregates formed by the forward)
+    gt = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads, relu=True, order=ops.degree_order(g.rowptr), tmode=True)
+    rt = ref_on_own_logits(g, gt, X, W, b, wL, bL, wR, bR, dY, heads, relu=True)
+    check_against_ref(gt, rt)
     # the host twins run the same sums in the same order (exp aside)
     host = cpu_layer(g, X, W, b, wL, bL, wR, bR, dY, heads)
     np.testing.assert_allclose(got["Y"], host["Y"], atol=2e-6, rtol=2e-6)
@@ -75,6 +79,15 @@ def test_input_space_kernels_non_symmetric_and_empty_rows():
     check_against_ref(got, ref)
     deg = np.diff(g.rowptr)
     assert (deg == 0).any() and np.all(got["Y"][deg == 0] == 0) and np.all(got["q"][deg == 0] == np.float32(1e12))
+    # T mode on the symmetrised graph (its empty rows and heavy row kept)
+    src = np.repeat(np.arange(g.n_rows, dtype=np.int32), np.diff(g.rowptr))
+    n2 = g.n_rows + 50   # 50 isolated rows: empty in T mode's q pass and walk
+    gs = layout.csr_build(n2, n2, np.concatenate([src, g.col]), np.concatenate([g.col, src]))
+    X2, W2, b2, wL2, bL2, wR2, bR2, dY2 = layer_inputs(gs.n_rows, 100, 8, 32, seed=6)
+    gt = gpu_layer(gs, X2, W2, b2, wL2, bL2, wR2, bR2, dY2, 8, tmode=True)
+    rt = ref_on_own_logits(gs, gt, X2, W2, b2, wL2, bL2, wR2, bR2, dY2, 8)
+    check_against_ref(gt, rt)
+    assert np.all(gt["Y"][g.n_rows:] == 0) and np.all(gt["q"][g.n_rows:] == np.float32(1e12))
 
 
 def test_input_space_refused_shapes():
@@ -98,11 +111,17 @@ def E():
     return gala.torch_ext()
 
 
-def test_mirror_op_equals_the_three_op_chain(E):
+@pytest.mark.parametrize("symmetric", [False, True])
+def test_mirror_op_equals_the_three_op_chain(E, symmetric):
     """gat_input_layer_apply (the one autograd op galac / HIPGenerator emit for config 3's layer
     1) against ffn_apply -> head_attn_apply -> gat_aggregate_ffn_apply on the same slot: Y and
-    every parameter gradient within 1e-4; the input gets no gradient (the dataset's features)."""
+    every parameter gradient within 1e-4; the input gets no gradient (the dataset's features).
+    On a symmetric pattern (an undirected program's graph) the op runs in T mode
+    (gala_gat_in_{fwd,bwd}_t_f32), else the backward walks the transposed pattern."""
     g = layout.gen_graph("uniform", 4000, 50000, seed=3)
+    if symmetric:
+        src = np.repeat(np.arange(g.n_rows, dtype=np.int32), np.diff(g.rowptr))
+        g = layout.csr_build(g.n_rows, g.n_rows, np.concatenate([src, g.col]), np.concatenate([g.col, src]))
     E.slots_clear()
     off, cols = dev(g.rowptr), dev(g.col)
     vals = torch.ones(g.nnz, device="cuda")
@@ -149,6 +168,6 @@ def test_config3_products_input_layer_against_the_reference_chain():
     fin, H, D = 100, 8, 32
     X, W, b, wL, bL, wR, bR, dY = layer_inputs(g.n_rows, fin, H, D, seed=2024)
     # as the program runs it: the ReLU fused, rows in descending-degree order
-    got = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, H, relu=True, order=ops.degree_order(g.rowptr))
+    got = gpu_layer(g, X, W, b, wL, bL, wR, bR, dY, H, relu=True, order=ops.degree_order(g.rowptr), tmode=True)
     ref = ref_on_own_logits(g, got, X, W, b, wL, bL, wR, bR, dY, H, relu=True)
     check_against_ref(got, ref)
