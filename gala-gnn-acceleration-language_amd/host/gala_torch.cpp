@@ -1492,6 +1492,7 @@ torch::Tensor gat_aggregate_ffn_apply(torch::Tensor attn_l, torch::Tensor X, tor
 // dataset's features); the apply wrapper keeps the three-op chain whenever X needs one.
 const PatternT &transposed_pattern(int64_t idx);
 bool gat_in_tmode_enabled();
+int64_t gat_in_tmode_max_bytes();
 
 struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
     static torch::Tensor forward(AutogradContext *ctx, torch::Tensor X, torch::Tensor W, torch::Tensor b,
@@ -1527,7 +1528,10 @@ struct GatInputLayer : public torch::autograd::Function<GatInputLayer> {
         // backward's per-column aggregates, so the backward does not walk the graph again
         const bool grad = ctx->needs_input_grad(1) || ctx->needs_input_grad(2) || ctx->needs_input_grad(3) ||
                           ctx->needs_input_grad(4) || ctx->needs_input_grad(5) || ctx->needs_input_grad(6);
-        const bool tmode = grad && B.gat_in_fwd_t && pt.symmetric && gat_in_tmode_enabled();
+        // T holds 3.5 KB per row until the backward: within gat_in_tmode_max_bytes() (the walk
+        // otherwise: e.g. papers100M's 111 M rows would need 389 GB)
+        const bool tmode = grad && B.gat_in_fwd_t && pt.symmetric && gat_in_tmode_enabled() &&
+                           N * 896 * (int64_t)sizeof(float) <= gat_in_tmode_max_bytes();
         torch::Tensor T = tmode ? torch::empty({N, 896}, fopts(x)) : torch::empty({0}, fopts(x));
         if (tmode)
             check(B.gat_in_fwd_t(&cv.c, pt.order.data_ptr<int32_t>(), (int32_t)fin, (int32_t)H, (int32_t)D, (float)slope,
@@ -1648,6 +1652,17 @@ bool gat_in_tmode_enabled() {
         return !(e && e[0] == '0');
     }();
     return on;
+}
+
+// GALA_GAT_IN_T_MAX_GB (default 64): the largest T buffer T mode may hold between the forward
+// and the backward
+int64_t gat_in_tmode_max_bytes() {
+    static const int64_t cap = [] {
+        const char *e = std::getenv("GALA_GAT_IN_T_MAX_GB");
+        const double gb = e ? std::atof(e) : 64.0;
+        return (int64_t)(gb * 1073741824.0);
+    }();
+    return cap;
 }
 
 // GALA_GAT_INPUT=0 keeps the three-op chain (A/B runs, the tests' reference spelling)
